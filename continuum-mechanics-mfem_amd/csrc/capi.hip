@@ -1,0 +1,619 @@
+// capi.hip — the C-ABI of libcdfem.so (include/cdfem.h): context, mesh/space upload, partial
+// assembly, FormLinearSystem, Krylov solves, profiling.  Host-side orchestration only; all
+// arithmetic on the hot path runs in the HIP kernels of pa_kernels.hip / vec_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "cdfem_internal.hpp"
+
+using namespace cdfem;
+
+namespace {
+
+struct HipError : std::runtime_error {
+    explicit HipError(const std::string &m) : std::runtime_error(m) {}
+};
+struct ArgError : std::runtime_error {
+    explicit ArgError(const std::string &m) : std::runtime_error(m) {}
+};
+struct StateError : std::runtime_error {
+    explicit StateError(const std::string &m) : std::runtime_error(m) {}
+};
+struct UnsupportedError : std::runtime_error {
+    explicit UnsupportedError(const std::string &m) : std::runtime_error(m) {}
+};
+
+inline void hip_check(hipError_t e, const char *what)
+{
+    if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIPCHK(x) hip_check((x), #x)
+
+template <typename F>
+int guarded(cdfem_ctx *c, F &&f)
+{
+    if (!c) return CDFEM_ERR_ARG;
+    try {
+        c->err.clear();
+        return f();
+    } catch (const ArgError &e) {
+        c->err = e.what();
+        return CDFEM_ERR_ARG;
+    } catch (const StateError &e) {
+        c->err = e.what();
+        return CDFEM_ERR_STATE;
+    } catch (const UnsupportedError &e) {
+        c->err = e.what();
+        return CDFEM_ERR_UNSUPPORTED;
+    } catch (const HipError &e) {
+        c->err = e.what();
+        return CDFEM_ERR_HIP;
+    } catch (const std::bad_alloc &) {
+        c->err = "host allocation failed";
+        return CDFEM_ERR_HIP;
+    } catch (const std::exception &e) {
+        c->err = e.what();
+        return CDFEM_ERR_ARG;
+    }
+}
+
+template <typename T>
+void dfree(T *&p)
+{
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+template <typename T>
+T *dalloc(size_t n)
+{
+    void *p = nullptr;
+    if (n == 0) n = 1;
+    HIPCHK(hipMalloc(&p, n * sizeof(T)));
+    return static_cast<T *>(p);
+}
+
+int nq_of(const cdfem_ctx *c, const Rule1D &r) { return c->dim == 3 ? r.q1 * r.q1 * r.q1 : r.q1 * r.q1; }
+
+void free_mesh(cdfem_ctx *c)
+{
+    dfree(c->d_verts); dfree(c->d_map); dfree(c->d_e2l_off); dfree(c->d_e2l_pos);
+    dfree(c->d_ess); dfree(c->d_ess_list); dfree(c->d_qd); dfree(c->d_Ye); dfree(c->d_dinv);
+    for (auto &w : c->d_w) dfree(w);
+    dfree(c->d_part); dfree(c->d_gm); dfree(c->d_gm_small);
+    c->gm_cap = 0;
+    c->mesh_ready = c->pa_ready = c->dinv_ready = false;
+}
+
+// ---- profiling helpers ---------------------------------------------------------------------------
+void prof_mark(cdfem_ctx *c, int k, bool begin)
+{
+    if (!c->profile) return;
+    ProfileSlot &s = c->prof[k];
+    const size_t need = (size_t)(s.used + 1) * 2;
+    while (s.ev.size() < need) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        s.ev.push_back(e);
+    }
+    if (begin) {
+        HIPCHK(hipEventRecord(s.ev[2 * s.used], c->stream));
+    } else {
+        HIPCHK(hipEventRecord(s.ev[2 * s.used + 1], c->stream));
+        s.used++;
+    }
+}
+
+void prof_collect(cdfem_ctx *c)
+{
+    if (!c->profile) return;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (auto &s : c->prof) {
+        for (int i = 0; i < s.used; ++i) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, s.ev[2 * i], s.ev[2 * i + 1]));
+            s.total_ms += ms;
+            s.count++;
+        }
+        s.used = 0;
+    }
+}
+
+void require_mesh(cdfem_ctx *c)
+{
+    if (!c->mesh_ready) throw StateError("cdfem_mesh_upload has not been called");
+}
+void require_pa(cdfem_ctx *c)
+{
+    require_mesh(c);
+    if (!c->pa_ready) throw StateError("cdfem_pa_setup has not been called");
+}
+
+// operator apply into y (device pointers): Ye = A_e x, y = E->L(Ye) [+ constraint]
+void op_apply(cdfem_ctx *c, const double *x, double *y, bool constrained)
+{
+    prof_mark(c, CDFEM_K_APPLY, true);
+    HIPCHK(launch_apply(c, x, c->d_Ye, constrained));
+    prof_mark(c, CDFEM_K_APPLY, false);
+    prof_mark(c, CDFEM_K_E2L, true);
+    HIPCHK(launch_e2l(c, c->d_Ye, x, y, constrained, 0));
+    prof_mark(c, CDFEM_K_E2L, false);
+}
+
+// copy-in helper: returns a device pointer holding n doubles of src (staging when on host)
+const double *dev_in(cdfem_ctx *c, const double *src, int where, double *staging, size_t n)
+{
+    if (where == CDFEM_DEVICE) return src;
+    HIPCHK(hipMemcpyAsync(staging, src, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return staging;
+}
+
+void dev_out(cdfem_ctx *c, double *dst, int where, const double *dsrc, size_t n)
+{
+    if (where == CDFEM_DEVICE) {
+        if (dst != dsrc)
+            HIPCHK(hipMemcpyAsync(dst, dsrc, n * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        return;
+    }
+    HIPCHK(hipMemcpyAsync(dst, dsrc, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+}
+
+void ensure_dinv(cdfem_ctx *c)
+{
+    if (c->dinv_ready) return;
+    double *diag = c->d_w[7];
+    HIPCHK(launch_diag_elem(c, c->d_Ye));
+    HIPCHK(launch_e2l(c, c->d_Ye, nullptr, diag, false, 0));
+    HIPCHK(launch_dinv(c, diag, c->d_dinv));
+    c->dinv_ready = true;
+}
+
+// MFEM CGSolver on the constrained operator, device-resident
+void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, double *dX,
+              cdfem_solver_result &res)
+{
+    double *x = c->d_w[2], *r = c->d_w[3], *z = c->d_w[4], *d = c->d_w[5];
+    const double *dinv = nullptr;
+    if (p.pc == CDFEM_PC_JACOBI) {
+        ensure_dinv(c);
+        dinv = c->d_dinv;
+    }
+    const int check = p.check_every > 0 ? p.check_every : 16;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(launch_cg_init(c, dB, x, r, z, d, dinv, p.rel_tol, p.abs_tol, p.max_iter));
+    // z = A d ; den
+    prof_mark(c, CDFEM_K_APPLY, true);
+    HIPCHK(launch_apply_st(c, d, c->d_Ye, true, c->d_state));
+    prof_mark(c, CDFEM_K_APPLY, false);
+    prof_mark(c, CDFEM_K_E2L, true);
+    HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 1));
+    prof_mark(c, CDFEM_K_E2L, false);
+    int launched = 0;
+    for (;;) {
+        for (int k = 0; k < check && launched < p.max_iter; ++k, ++launched) {
+            prof_mark(c, CDFEM_K_UPDATE, true);
+            HIPCHK(launch_cg_update(c, x, r, z, d, dinv));
+            prof_mark(c, CDFEM_K_UPDATE, false);
+            prof_mark(c, CDFEM_K_DIRECTION, true);
+            HIPCHK(launch_cg_direction(c, z, d));
+            prof_mark(c, CDFEM_K_DIRECTION, false);
+            prof_mark(c, CDFEM_K_APPLY, true);
+            HIPCHK(launch_apply_st(c, d, c->d_Ye, true, c->d_state));
+            prof_mark(c, CDFEM_K_APPLY, false);
+            prof_mark(c, CDFEM_K_E2L, true);
+            HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 1));
+            prof_mark(c, CDFEM_K_E2L, false);
+        }
+        HIPCHK(hipMemcpyAsync(c->h_state, c->d_state, sizeof(KrylovState), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->h_state->done || launched >= p.max_iter) break;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    prof_collect(c);
+    const KrylovState &s = *c->h_state;
+    res.converged = s.converged;
+    res.iterations = s.final_iter;
+    res.initial_norm = std::sqrt(std::fabs(s.nom0));
+    res.final_norm = (s.final_iter == 0) ? std::sqrt(std::fabs(s.nom0)) : std::sqrt(std::fabs(s.betanom));
+    res.seconds = std::chrono::duration<double>(t1 - t0).count();
+    HIPCHK(hipMemcpyAsync(dX, x, c->nl * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+}
+
+}  // namespace
+
+// ================================================================================================
+extern "C" {
+
+int cdfem_abi_version(void) { return CDFEM_ABI_VERSION; }
+
+int cdfem_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int cdfem_create(int device, cdfem_ctx **out)
+{
+    if (!out) return CDFEM_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CDFEM_ERR_HIP;
+    if (device < 0 || device >= n) return CDFEM_ERR_ARG;
+    cdfem_ctx *c = new (std::nothrow) cdfem_ctx();
+    if (!c) return CDFEM_ERR_HIP;
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_state, sizeof(KrylovState)) != hipSuccess ||
+        hipMemset(c->d_state, 0, sizeof(KrylovState)) != hipSuccess ||
+        hipHostMalloc(&c->h_state, sizeof(KrylovState), hipHostMallocDefault) != hipSuccess) {
+        cdfem_destroy(c);
+        return CDFEM_ERR_HIP;
+    }
+    *out = c;
+    return CDFEM_OK;
+}
+
+void cdfem_destroy(cdfem_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_mesh(c);
+    if (c->d_state) (void)hipFree(c->d_state);
+    if (c->h_state) (void)hipHostFree(c->h_state);
+    for (auto &s : c->prof)
+        for (auto e : s.ev) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *cdfem_last_error(const cdfem_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int cdfem_synchronize(cdfem_ctx *c)
+{
+    return guarded(c, [&] {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_alloc(cdfem_ctx *c, size_t bytes, void **dptr)
+{
+    return guarded(c, [&] {
+        if (!dptr) throw ArgError("dptr is null");
+        HIPCHK(hipMalloc(dptr, bytes ? bytes : 1));
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_free(cdfem_ctx *c, void *dptr)
+{
+    return guarded(c, [&] {
+        HIPCHK(hipFree(dptr));
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_memcpy(cdfem_ctx *c, void *dst, int dw, const void *src, int sw, size_t bytes)
+{
+    return guarded(c, [&] {
+        hipMemcpyKind k = dw == CDFEM_DEVICE ? (sw == CDFEM_DEVICE ? hipMemcpyDeviceToDevice
+                                                                   : hipMemcpyHostToDevice)
+                                             : (sw == CDFEM_DEVICE ? hipMemcpyDeviceToHost
+                                                                   : hipMemcpyHostToHost);
+        HIPCHK(hipMemcpyAsync(dst, src, bytes, k, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_mesh_upload(cdfem_ctx *c, int dim, int order, int ne, const double *elem_verts,
+                      int64_t nldofs, const int32_t *elem_dofs, int n_ess, const int32_t *ess_dofs)
+{
+    return guarded(c, [&] {
+        if (dim != 2 && dim != 3) throw ArgError("dim must be 2 or 3");
+        if (order < 1 || order > kMaxD1 - 1) throw ArgError("order out of range");
+        if (ne <= 0 || nldofs <= 0 || !elem_verts || !elem_dofs) throw ArgError("empty mesh");
+        if (nldofs >= (int64_t)1 << 31) throw ArgError("nldofs exceeds int32 indexing");
+        if (n_ess < 0 || (n_ess > 0 && !ess_dofs)) throw ArgError("bad essential list");
+        HIPCHK(hipSetDevice(c->device));
+        free_mesh(c);
+        c->dim = dim;
+        c->p = order;
+        c->d1 = order + 1;
+        c->nd = dim == 3 ? c->d1 * c->d1 * c->d1 : c->d1 * c->d1;
+        c->nv = 1 << dim;
+        c->ne = ne;
+        c->nl = nldofs;
+        c->nblk = (ne + kLanes - 1) / kLanes;
+        if ((int64_t)ne * c->nd >= (int64_t)1 << 31) throw ArgError("E-vector exceeds int32 indexing");
+        c->rule_op = make_rule(order, rule_points_1d(0, dim, order));
+        c->rule_lf = make_rule(order, rule_points_1d(1, dim, order));
+        c->rule_err = make_rule(order, rule_points_1d(2, dim, order));
+
+        const int nd = c->nd;
+        std::vector<uint8_t> ess(nldofs, 0);
+        for (int i = 0; i < n_ess; ++i) {
+            if (ess_dofs[i] < 0 || ess_dofs[i] >= nldofs) throw ArgError("essential dof out of range");
+            ess[ess_dofs[i]] = 1;
+        }
+        // element map [nblk][nd][64], essential encoded negative; padding -> dof 0 (qdata 0)
+        std::vector<int32_t> map((size_t)c->nblk * nd * kLanes, 0);
+        std::vector<int32_t> cnt(nldofs + 1, 0);
+        for (int e = 0; e < ne; ++e)
+            for (int l = 0; l < nd; ++l) {
+                const int32_t g = elem_dofs[(size_t)e * nd + l];
+                if (g < 0 || g >= nldofs) throw ArgError("element dof out of range");
+                map[((size_t)(e / kLanes) * nd + l) * kLanes + (e % kLanes)] = ess[g] ? -(g + 1) : g;
+                cnt[g + 1]++;
+            }
+        // E->L transpose (positions into the E-vector), ascending element order
+        for (int64_t i = 0; i < nldofs; ++i) cnt[i + 1] += cnt[i];
+        std::vector<int32_t> pos((size_t)ne * nd), fill(cnt.begin(), cnt.end() - 1);
+        for (int e = 0; e < ne; ++e)
+            for (int l = 0; l < nd; ++l) {
+                const int32_t g = elem_dofs[(size_t)e * nd + l];
+                pos[fill[g]++] = (int32_t)(((size_t)(e / kLanes) * nd + l) * kLanes + (e % kLanes));
+            }
+        std::vector<int32_t> ess_list;
+        ess_list.reserve(n_ess);
+        for (int64_t i = 0; i < nldofs; ++i)
+            if (ess[i]) ess_list.push_back((int32_t)i);
+        c->n_ess = (int)ess_list.size();
+
+        c->d_verts = dalloc<double>((size_t)ne * c->nv * dim);
+        c->d_map = dalloc<int32_t>(map.size());
+        c->d_e2l_off = dalloc<int32_t>(nldofs + 1);
+        c->d_e2l_pos = dalloc<int32_t>(pos.size());
+        c->d_ess = dalloc<uint8_t>(nldofs);
+        c->d_ess_list = dalloc<int32_t>(ess_list.size());
+        c->d_Ye = dalloc<double>((size_t)c->nblk * nd * kLanes);
+        c->d_dinv = dalloc<double>(nldofs);
+        for (auto &w : c->d_w) w = dalloc<double>(nldofs);
+        c->d_part = dalloc<double>(c->red_blocks);
+        HIPCHK(hipMemcpyAsync(c->d_verts, elem_verts, (size_t)ne * c->nv * dim * sizeof(double),
+                              hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_e2l_off, cnt.data(), (nldofs + 1) * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_e2l_pos, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_ess, ess.data(), nldofs, hipMemcpyHostToDevice, c->stream));
+        if (!ess_list.empty())
+            HIPCHK(hipMemcpyAsync(c->d_ess_list, ess_list.data(), ess_list.size() * 4,
+                                  hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemsetAsync(c->d_Ye, 0, (size_t)c->nblk * nd * kLanes * sizeof(double), c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));  // host vectors go out of scope
+        c->mesh_ready = true;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_rule_size(cdfem_ctx *c, int rule, int *nq)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        if (!nq) throw ArgError("nq is null");
+        const Rule1D &r = rule == CDFEM_RULE_OPERATOR ? c->rule_op
+                        : rule == CDFEM_RULE_LINEARFORM ? c->rule_lf : c->rule_err;
+        *nq = nq_of(c, r);
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_quadrature_points(cdfem_ctx *c, int rule, double *xyz, int where)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        if (!xyz) throw ArgError("xyz is null");
+        const Rule1D &r = rule == CDFEM_RULE_OPERATOR ? c->rule_op
+                        : rule == CDFEM_RULE_LINEARFORM ? c->rule_lf : c->rule_err;
+        const size_t n = (size_t)c->ne * nq_of(c, r) * c->dim;
+        double *d = where == CDFEM_DEVICE ? xyz : dalloc<double>(n);
+        HIPCHK(launch_quad_points(c, r, d));
+        if (where != CDFEM_DEVICE) {
+            HIPCHK(hipMemcpyAsync(xyz, d, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            dfree(d);
+        }
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_pa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kappa_q, double alpha,
+                   const double *conv, const double *conv_q, double mass, const double *mass_q)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        if (kinds == 0 || kinds > 7) throw ArgError("kinds must be a non-empty DIFFUSION|CONVECTION|MASS mask");
+        if ((kinds & CDFEM_CONVECTION) && !conv && !conv_q) throw ArgError("convection needs a velocity");
+        if (!apply_supported(c->dim, c->p))
+            throw UnsupportedError("no PA apply kernel built for dim=" + std::to_string(c->dim) +
+                                   " order=" + std::to_string(c->p));
+        dfree(c->d_qd);
+        c->kinds = kinds;
+        c->ncomp = ((kinds & CDFEM_DIFFUSION) ? c->dim * (c->dim + 1) / 2 : 0) +
+                   ((kinds & CDFEM_CONVECTION) ? c->dim : 0) + ((kinds & CDFEM_MASS) ? 1 : 0);
+        const int nq = nq_of(c, c->rule_op);
+        c->d_qd = dalloc<double>((size_t)c->nblk * nq * c->ncomp * kLanes);
+        const size_t neq = (size_t)c->ne * nq;
+        double *dk = nullptr, *dc = nullptr, *dm = nullptr;
+        if (kappa_q) {
+            dk = dalloc<double>(neq);
+            HIPCHK(hipMemcpyAsync(dk, kappa_q, neq * 8, hipMemcpyHostToDevice, c->stream));
+        }
+        if (conv_q) {
+            dc = dalloc<double>(neq * c->dim);
+            HIPCHK(hipMemcpyAsync(dc, conv_q, neq * c->dim * 8, hipMemcpyHostToDevice, c->stream));
+        }
+        if (mass_q) {
+            dm = dalloc<double>(neq);
+            HIPCHK(hipMemcpyAsync(dm, mass_q, neq * 8, hipMemcpyHostToDevice, c->stream));
+        }
+        HIPCHK(launch_setup_qdata(c, dk, kappa, alpha, conv, dc, dm, mass));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        dfree(dk); dfree(dc); dfree(dm);
+        c->pa_ready = true;
+        c->dinv_ready = false;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_pa_mult(cdfem_ctx *c, const double *x, double *y, int constrained, int where)
+{
+    return guarded(c, [&] {
+        require_pa(c);
+        if (!x || !y) throw ArgError("null vector");
+        const double *dx = dev_in(c, x, where, c->d_w[0], c->nl);
+        double *dy = where == CDFEM_DEVICE ? y : c->d_w[1];
+        op_apply(c, dx, dy, constrained != 0);
+        dev_out(c, y, where, dy, c->nl);
+        prof_collect(c);
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_pa_diagonal(cdfem_ctx *c, double *diag, int where)
+{
+    return guarded(c, [&] {
+        require_pa(c);
+        if (!diag) throw ArgError("null vector");
+        double *dd = where == CDFEM_DEVICE ? diag : c->d_w[1];
+        HIPCHK(launch_diag_elem(c, c->d_Ye));
+        HIPCHK(launch_e2l(c, c->d_Ye, nullptr, dd, false, 0));
+        dev_out(c, diag, where, dd, c->nl);
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_lf_assemble(cdfem_ctx *c, const double *f_q, double *b, int where)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        if (!f_q || !b) throw ArgError("null vector");
+        const size_t n = (size_t)c->ne * nq_of(c, c->rule_lf);
+        double *dfq = dalloc<double>(n);
+        HIPCHK(hipMemcpyAsync(dfq, f_q, n * 8, where == CDFEM_DEVICE ? hipMemcpyDeviceToDevice
+                                                                     : hipMemcpyHostToDevice, c->stream));
+        double *db = where == CDFEM_DEVICE ? b : c->d_w[1];
+        HIPCHK(launch_lf_elem(c, dfq, c->d_Ye));
+        HIPCHK(launch_e2l(c, c->d_Ye, nullptr, db, false, 0));
+        dev_out(c, b, where, db, c->nl);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        dfree(dfq);
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_form_linear_system(cdfem_ctx *c, const double *x, const double *b, double *X, double *B,
+                             int where)
+{
+    return guarded(c, [&] {
+        require_pa(c);
+        if (!x || !b || !X || !B) throw ArgError("null vector");
+        const double *dx = dev_in(c, x, where, c->d_w[0], c->nl);
+        const double *db = dev_in(c, b, where, c->d_w[1], c->nl);
+        double *xe = c->d_w[2], *z = c->d_w[3];
+        double *dB = where == CDFEM_DEVICE ? B : c->d_w[4];
+        HIPCHK(launch_mask_ess(c, dx, xe));                 // x_e: essential part of x
+        op_apply(c, xe, z, false);                          // z = A x_e
+        if (dB != db) HIPCHK(hipMemcpyAsync(dB, db, c->nl * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(launch_axpby(c, -1.0, z, 1.0, dB));          // B = b - A x_e
+        HIPCHK(launch_set_ess(c, dB, dx));                  // B[ess] = x[ess]
+        dev_out(c, B, where, dB, c->nl);
+        dev_out(c, X, where, dx, c->nl);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        prof_collect(c);
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, double *X, int where,
+                cdfem_solver_result *res)
+{
+    return guarded(c, [&] {
+        require_pa(c);
+        if (!p || !B || !X || !res) throw ArgError("null argument");
+        if (p->max_iter < 0) throw ArgError("max_iter < 0");
+        if (p->pc != CDFEM_PC_NONE && p->pc != CDFEM_PC_JACOBI) throw ArgError("unknown preconditioner");
+        *res = cdfem_solver_result{};
+        const double *dB = dev_in(c, B, where, c->d_w[6], c->nl);
+        double *dX = where == CDFEM_DEVICE ? X : c->d_w[1];
+        if (p->method == CDFEM_CG) {
+            solve_cg(c, *p, dB, dX, *res);
+        } else {
+            throw UnsupportedError("GMRES is not available in this build");
+        }
+        dev_out(c, X, where, dX, c->nl);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return res->converged ? CDFEM_OK : CDFEM_ERR_NOT_CONVERGED;
+    });
+}
+
+int cdfem_profile_enable(cdfem_ctx *c, int on)
+{
+    return guarded(c, [&] {
+        c->profile = on != 0;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_profile_reset(cdfem_ctx *c)
+{
+    return guarded(c, [&] {
+        for (auto &s : c->prof) {
+            s.used = 0;
+            s.total_ms = 0.0;
+            s.count = 0;
+        }
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_profile_read(cdfem_ctx *c, int k, double *total_ms, int64_t *count)
+{
+    return guarded(c, [&] {
+        if (k < 0 || k >= CDFEM_K_COUNT) throw ArgError("bad kernel id");
+        if (total_ms) *total_ms = c->prof[k].total_ms;
+        if (count) *count = c->prof[k].count;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
+{
+    return guarded(c, [&] {
+        require_pa(c);
+        if (!bytes) throw ArgError("bytes is null");
+        const double nl = (double)c->nl, ne = (double)c->ne, nd = c->nd;
+        const double nq = nq_of(c, c->rule_op);
+        switch (k) {
+        case CDFEM_K_APPLY:
+            // x gather (each L-dof once) + qdata stream + element map + E-vector write
+            *bytes = 8.0 * nl + 8.0 * c->ncomp * nq * ne + 4.0 * nd * ne + 8.0 * nd * ne;
+            break;
+        case CDFEM_K_E2L:
+            // E-vector read + positions + offsets + y write + x read (constraint / dot)
+            *bytes = 8.0 * nd * ne + 4.0 * nd * ne + 4.0 * nl + 8.0 * nl + 8.0 * nl;
+            break;
+        case CDFEM_K_UPDATE: *bytes = 8.0 * nl * 8; break;     // x,d,r,z,dinv read; x,r,z write
+        case CDFEM_K_DIRECTION: *bytes = 8.0 * nl * 3; break;  // z,d read; d write
+        default: throw ArgError("bad kernel id");
+        }
+        return CDFEM_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,137 @@
+// cdfem_internal.hpp — context layout and kernel-launch declarations shared by the HIP sources.
+//
+// Device data layout (HBM), chosen for the thread-per-element PA kernels:
+//   elements are grouped in blocks of 64 (one wavefront, lane = element within the block);
+//   elem map   : int32 [nblk][nd][64]      L-dof of local dof l of element 64*b+lane; essential
+//                                           dofs stored as -(gid+1) so the constrained gather
+//                                           reads 0 without a second array
+//   qdata      : f64   [nblk][nq][nc][64]  per quadrature point: D (sym, dim(dim+1)/2), C (dim),
+//                                           M (1), only the kinds present (nc = 7 for K+M, 10 all)
+//   E-vector Y : f64   [nblk][nd][64]      element outputs before the E->L sum
+//   E->L map   : CSR over L-dofs, entries = positions in Y, element order ascending (deterministic)
+// Every wave reads 512 contiguous bytes per qdata component, so the dominant stream is fully
+// coalesced; the x gather is served by L2/MALL (x is 17 MB at 64^3 p=2).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/cdfem.h"
+
+namespace cdfem {
+
+constexpr int kLanes = 64;        // elements per element-block (= wavefront width)
+constexpr int kMaxD1 = 6;
+constexpr int kMaxQ1 = 8;
+
+// 1D tables for one quadrature rule: B[q][d] = phi_d(xi_q), G[q][d] = phi_d'(xi_q), points, weights
+struct Rule1D {
+    int d1 = 0, q1 = 0;
+    double B[kMaxQ1][kMaxD1] = {};
+    double G[kMaxQ1][kMaxD1] = {};
+    double pts[kMaxQ1] = {};
+    double wts[kMaxQ1] = {};
+};
+
+// Product implementation of the 1D rules (independent of the oracle): basis.cpp
+void gll_nodes(int p, double *x);
+void gauss_legendre(int n, double *x, double *w);
+Rule1D make_rule(int p, int q1);
+// MFEM default rule sizes on multilinear tensor elements (which: 0 operator, 1 LF, 2 L2 error)
+int rule_points_1d(int which, int dim, int p);
+
+// Device-side Krylov state (one per context), updated only by kernels.
+struct KrylovState {
+    double nom, nom0, den, alpha, beta, betanom, r0;
+    int iter, done, converged, final_iter, max_iter, first_den;
+    unsigned cnt[4];  // last-block arrival counters (reset by the last arriver)
+};
+
+struct ProfileSlot {
+    std::vector<hipEvent_t> ev;  // pairs
+    int used = 0;
+    double total_ms = 0.0;
+    int64_t count = 0;
+};
+
+}  // namespace cdfem
+
+struct cdfem_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // mesh / space
+    int dim = 0, p = 0, d1 = 0, nd = 0, ne = 0, nblk = 0, nv = 0;
+    int64_t nl = 0;
+    int n_ess = 0;
+    bool mesh_ready = false;
+    double *d_verts = nullptr;          // [ne][nv][dim]
+    int32_t *d_map = nullptr;           // [nblk][nd][64], ess negative
+    int32_t *d_e2l_off = nullptr;       // [nl+1]
+    int32_t *d_e2l_pos = nullptr;       // [ne*nd]
+    uint8_t *d_ess = nullptr;           // [nl]
+    int32_t *d_ess_list = nullptr;      // [n_ess]
+
+    // rules
+    cdfem::Rule1D rule_op, rule_lf, rule_err;
+
+    // partial assembly
+    unsigned kinds = 0;
+    int ncomp = 0;
+    bool pa_ready = false;
+    double *d_qd = nullptr;             // [nblk][nq][nc][64]
+    double *d_Ye = nullptr;             // [nblk][nd][64]
+    double *d_dinv = nullptr;           // Jacobi (constrained: ess -> 1)
+    bool dinv_ready = false;
+
+    // work vectors (L-size)
+    double *d_w[8] = {};                // staging + Krylov vectors
+    double *d_part = nullptr;           // reduction partials
+    int red_blocks = 1024;
+    cdfem::KrylovState *d_state = nullptr;
+    cdfem::KrylovState *h_state = nullptr;  // pinned
+    double *d_gm = nullptr;             // GMRES basis (restart+1) * nl
+    int gm_cap = 0;
+    double *d_gm_small = nullptr;       // GMRES Hessenberg / Givens workspace
+
+    // profiling
+    bool profile = false;
+    cdfem::ProfileSlot prof[CDFEM_K_COUNT];
+};
+
+namespace cdfem {
+
+// ---- kernel launchers (pa_kernels.hip) -------------------------------------------------------
+hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, double kappa, double alpha,
+                              const double *conv, const double *d_conv_q, const double *d_mass_q,
+                              double mass);
+hipError_t launch_apply(cdfem_ctx *c, const double *x, double *Ye, bool constrained);
+hipError_t launch_apply_st(cdfem_ctx *c, const double *x, double *Ye, bool constrained,
+                           const KrylovState *st);
+hipError_t launch_diag_elem(cdfem_ctx *c, double *Ye);
+hipError_t launch_lf_elem(cdfem_ctx *c, const double *d_fq, double *Ye);
+hipError_t launch_quad_points(cdfem_ctx *c, const Rule1D &r, double *xyz);
+bool apply_supported(int dim, int p);
+
+// ---- vector kernels (vec_kernels.hip) --------------------------------------------------------
+// y = E->L sum of Ye; constrained: y[ess] = x[ess]; if dot_part != nullptr also reduces
+// partial sums of y.x into dot_part[blockIdx] and the last block writes state->den and alpha.
+hipError_t launch_e2l(cdfem_ctx *c, const double *Ye, const double *x, double *y, bool constrained,
+                      int cg_mode);
+hipError_t launch_set_ess(cdfem_ctx *c, double *y, const double *x);          // y[ess] = x[ess]
+hipError_t launch_mask_ess(cdfem_ctx *c, const double *x, double *y);        // y = x, y[ess] = 0
+hipError_t launch_axpby(cdfem_ctx *c, double a, const double *x, double b, double *y);  // y = a x + b y
+hipError_t launch_dinv(cdfem_ctx *c, const double *diag, double *dinv);      // 1/diag, ess -> 1
+// CG pieces (MFEM CGSolver semantics)
+hipError_t launch_cg_init(cdfem_ctx *c, const double *B, double *x, double *r, double *z, double *d,
+                          const double *dinv, double rel_tol, double abs_tol, int max_iter);
+hipError_t launch_cg_update(cdfem_ctx *c, double *x, double *r, double *z, const double *d,
+                            const double *dinv);
+hipError_t launch_cg_direction(cdfem_ctx *c, const double *z, double *d);
+// generic deterministic dot into host-visible scalar via state (used by GMRES / tests)
+hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out);
+
+}  // namespace cdfem

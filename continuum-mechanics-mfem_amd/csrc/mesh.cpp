@@ -1,0 +1,165 @@
+// mesh.cpp — structured quad/hex box meshes and z-slab partitions (host side of the product).
+//
+// The reference reads gmsh meshes (Mesh/unit_square.msh) and refines them; BASELINE configs 2, 3
+// and 5 are synthetic structured hex meshes that ship nowhere, so the product generates them:
+// [0,1]^dim split into nx*ny(*nz) elements, boundary attributes as Mesh/unit_square.geo:18-21
+// (all marked essential by the hot path: linear_convection_diffusion_2D.cpp:319-322).
+//
+// Multi-GPU element partition: rank r owns the elements with (last-axis) index in [z0, z1) — a
+// slab — and numbers the dofs of its slab lexicographically (local L-vector).  Interface dofs
+// (the planes at z0 > 0 and z1 < nz) are shared with the neighbouring rank; they are NOT
+// essential.  This is the ParMesh / ParFiniteElementSpace element partition of the reference
+// (linear_convection_diffusion_2D.cpp:300) with a slab partitioner instead of METIS.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+#include "cdfem_internal.hpp"
+
+namespace {
+
+// deterministic jitter in [-1, 1)
+double jitter(uint64_t a)
+{
+    a += 0x9e3779b97f4a7c15ULL;
+    a = (a ^ (a >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    a = (a ^ (a >> 27)) * 0x94d049bb133111ebULL;
+    a ^= a >> 31;
+    return (double)(a >> 11) / 4503599627370496.0 - 1.0;
+}
+
+struct Box {
+    int dim, nx, ny, nz, p, z0, z1;
+    int64_t Lx, Ly, Lz;       // local lattice sizes
+    int ne;
+};
+
+bool make_box(int dim, int nx, int ny, int nz, int p, int z0, int z1, Box &b)
+{
+    if (dim != 2 && dim != 3) return false;
+    if (nx < 1 || ny < 1 || p < 1) return false;
+    if (dim == 2) nz = 1;
+    if (nz < 1) return false;
+    const int nlast = dim == 3 ? nz : ny;
+    if (z1 <= 0 || z1 > nlast) z1 = nlast;
+    if (z0 < 0 || z0 >= z1) return false;
+    b = Box{dim, nx, ny, nz, p, z0, z1, 0, 0, 0, 0};
+    b.Lx = (int64_t)p * nx + 1;
+    if (dim == 3) {
+        b.Ly = (int64_t)p * ny + 1;
+        b.Lz = (int64_t)p * (z1 - z0) + 1;
+        b.ne = nx * ny * (z1 - z0);
+    } else {
+        b.Ly = (int64_t)p * (z1 - z0) + 1;
+        b.Lz = 1;
+        b.ne = nx * (z1 - z0);
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cdfem_box_sizes(int dim, int nx, int ny, int nz, int order, int z0, int z1, int *ne,
+                    int64_t *nldofs, int *n_ess)
+{
+    Box b;
+    if (!make_box(dim, nx, ny, nz, order, z0, z1, b)) return CDFEM_ERR_ARG;
+    const int nlast = dim == 3 ? b.nz : b.ny;
+    int64_t ness = 0;
+    const int64_t nl = b.Lx * b.Ly * b.Lz;
+    for (int64_t i = 0; i < nl; ++i) {
+        const int64_t gx = i % b.Lx, gy = (i / b.Lx) % b.Ly, gz = i / (b.Lx * b.Ly);
+        const int64_t glast = (dim == 3 ? gz : gy) + (int64_t)order * b.z0;  // global last-axis index
+        bool on = gx == 0 || gx == b.Lx - 1 || glast == 0 || glast == (int64_t)order * nlast;
+        if (dim == 3) on = on || gy == 0 || gy == b.Ly - 1;
+        ness += on;
+    }
+    if (ne) *ne = b.ne;
+    if (nldofs) *nldofs = nl;
+    if (n_ess) *n_ess = (int)ness;
+    return CDFEM_OK;
+}
+
+int cdfem_box_mesh(int dim, int nx, int ny, int nz, int order, int z0, int z1, double perturb,
+                   double *elem_verts, int32_t *elem_dofs, int32_t *ess_dofs, double *dof_xyz)
+{
+    Box b;
+    if (!make_box(dim, nx, ny, nz, order, z0, z1, b)) return CDFEM_ERR_ARG;
+    const int p = order, d1 = p + 1;
+    const int nd = dim == 3 ? d1 * d1 * d1 : d1 * d1;
+    const int nv = 1 << dim;
+    const int nlast = dim == 3 ? b.nz : b.ny;
+    const double h[3] = {1.0 / b.nx, 1.0 / b.ny, 1.0 / b.nz};
+    const int64_t gvx = b.nx + 1, gvy = b.ny + 1;
+
+    auto vertex = [&](int gx, int gy, int gz, double X[3]) {
+        const int g[3] = {gx, gy, gz};
+        const int n[3] = {b.nx, b.ny, b.nz};
+        bool interior = true;
+        for (int k = 0; k < dim; ++k) {
+            X[k] = g[k] * h[k];
+            interior = interior && g[k] > 0 && g[k] < n[k];
+        }
+        if (perturb > 0.0 && interior) {
+            const uint64_t id = (uint64_t)gx + (uint64_t)gvx * ((uint64_t)gy + (uint64_t)gvy * gz);
+            for (int k = 0; k < dim; ++k) X[k] += perturb * h[k] * jitter(3 * id + k);
+        }
+    };
+
+    double nodes[cdfem::kMaxD1];
+    cdfem::gll_nodes(p, nodes);
+    for (int e = 0; e < b.ne; ++e) {
+        int ix, iy, iz;
+        if (dim == 3) {
+            ix = e % b.nx; iy = (e / b.nx) % b.ny; iz = e / (b.nx * b.ny) + b.z0;
+        } else {
+            ix = e % b.nx; iy = e / b.nx + b.z0; iz = 0;
+        }
+        double V[8][3] = {};
+        for (int v = 0; v < nv; ++v) {
+            vertex(ix + (v & 1), iy + ((v >> 1) & 1), iz + ((v >> 2) & 1), V[v]);
+            if (elem_verts)
+                for (int k = 0; k < dim; ++k) elem_verts[((size_t)e * nv + v) * dim + k] = V[v][k];
+        }
+        for (int l = 0; l < nd; ++l) {
+            const int dx = l % d1, dy = (l / d1) % d1, dz = l / (d1 * d1);
+            int64_t lx = (int64_t)p * ix + dx, ly, lz;
+            if (dim == 3) {
+                ly = (int64_t)p * iy + dy;
+                lz = (int64_t)p * (iz - b.z0) + dz;
+            } else {
+                ly = (int64_t)p * (iy - b.z0) + dy;
+                lz = 0;
+            }
+            const int64_t gid = lx + b.Lx * (ly + b.Ly * lz);
+            if (elem_dofs) elem_dofs[(size_t)e * nd + l] = (int32_t)gid;
+            if (dof_xyz) {
+                // multilinear image of the GLL node
+                const double xi[3] = {nodes[dx], nodes[dy], dim == 3 ? nodes[dz] : 0.0};
+                double X[3] = {0, 0, 0};
+                for (int v = 0; v < nv; ++v) {
+                    double N = 1.0;
+                    for (int k = 0; k < dim; ++k) N *= ((v >> k) & 1) ? xi[k] : 1.0 - xi[k];
+                    for (int k = 0; k < dim; ++k) X[k] += N * V[v][k];
+                }
+                for (int k = 0; k < dim; ++k) dof_xyz[gid * dim + k] = X[k];
+            }
+        }
+    }
+    if (ess_dofs) {
+        const int64_t nl = b.Lx * b.Ly * b.Lz;
+        int64_t m = 0;
+        for (int64_t i = 0; i < nl; ++i) {
+            const int64_t gx = i % b.Lx, gy = (i / b.Lx) % b.Ly, gz = i / (b.Lx * b.Ly);
+            const int64_t glast = (dim == 3 ? gz : gy) + (int64_t)p * b.z0;
+            bool on = gx == 0 || gx == b.Lx - 1 || glast == 0 || glast == (int64_t)p * nlast;
+            if (dim == 3) on = on || gy == 0 || gy == b.Ly - 1;
+            if (on) ess_dofs[m++] = (int32_t)i;
+        }
+    }
+    return CDFEM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,666 @@
+// pa_kernels.hip — partial-assembly kernels for H1 tensor elements on gfx950.
+//
+// Replaces MFEM's DiffusionIntegrator / ConvectionIntegrator / MassIntegrator AssemblePA +
+// AddMultPA (called from a.Assemble() and Operator::Mult in linear_convection_diffusion_2D.cpp:
+// 335-339, 364-370) with ONE fused operator: per quadrature point
+//     v     = M u + C . grad_ref(u)            (mass + convection, test with phi)
+//     vgrad = D grad_ref(u)                    (diffusion, test with grad phi)
+// where D = W kappa adj(J)adj(J)^T/detJ, C = W alpha adj(J) c, M = W s detJ (qdata, HBM-resident).
+//
+// Apply kernel mapping (MI355X-first): one THREAD per element, one wavefront per
+// 64-element block.  The 1D contractions (sum factorization, x/y/z) run in registers with
+// compile-time-unrolled loops, so there is no LDS traffic, no barrier, and every qdata load of a
+// wavefront is 512 contiguous bytes.  The element loop is a pure stream over qdata (10 doubles
+// per quadrature point at p=2 = 94% of the bytes), which is what bounds the kernel (HBM roofline).
+#include <hip/hip_runtime.h>
+
+#include "cdfem_internal.hpp"
+
+namespace cdfem {
+
+template <int D1, int Q1>
+struct Tab {
+    double B[Q1][D1];
+    double G[Q1][D1];
+};
+
+template <int D1, int Q1>
+static Tab<D1, Q1> make_tab(const Rule1D &r)
+{
+    Tab<D1, Q1> t;
+    for (int q = 0; q < Q1; ++q)
+        for (int d = 0; d < D1; ++d) {
+            t.B[q][d] = r.B[q][d];
+            t.G[q][d] = r.G[q][d];
+        }
+    return t;
+}
+
+// qdata component layout for a kinds mask: [D (sym) | C (dim) | M]
+template <unsigned K, int DIM>
+struct QLayout {
+    static constexpr bool kD = (K & CDFEM_DIFFUSION) != 0;
+    static constexpr bool kC = (K & CDFEM_CONVECTION) != 0;
+    static constexpr bool kM = (K & CDFEM_MASS) != 0;
+    static constexpr int nD = kD ? DIM * (DIM + 1) / 2 : 0;
+    static constexpr int oC = nD;
+    static constexpr int oM = oC + (kC ? DIM : 0);
+    static constexpr int nc = oM + (kM ? 1 : 0);
+};
+
+// ------------------------------------------------------------------------------------------------
+// 3D apply: Ye = A_e x_e for every element (thread per element)
+// ------------------------------------------------------------------------------------------------
+template <int D1, int Q1, unsigned K, bool CON>
+__global__ void __launch_bounds__(256)
+k_apply3d(const int32_t *__restrict__ map, const double *__restrict__ x,
+          const double *__restrict__ qd, double *__restrict__ Ye, const Tab<D1, Q1> T,
+          const int nblk, const KrylovState *__restrict__ st)
+{
+    if (st != nullptr && st->done) return;
+    using L = QLayout<K, 3>;
+    constexpr int ND = D1 * D1 * D1;
+    constexpr int NQ = Q1 * Q1 * Q1;
+    constexpr int NC = L::nc;
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b >= nblk) return;
+
+    // L->E gather (fused): 64 lanes read 256 contiguous bytes of map per local dof
+    const int32_t *mp = map + (size_t)b * ND * kLanes + lane;
+    double X[D1][D1][D1];
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                const int g = mp[(dx + D1 * (dy + D1 * dz)) * kLanes];
+                if constexpr (CON) {
+                    const double v = x[g < 0 ? 0 : g];
+                    X[dz][dy][dx] = g < 0 ? 0.0 : v;
+                } else {
+                    X[dz][dy][dx] = x[g < 0 ? -g - 1 : g];
+                }
+            }
+
+    double Y[D1][D1][D1];
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) Y[dz][dy][dx] = 0.0;
+
+    const double *q0 = qd + (size_t)b * NQ * NC * kLanes + lane;
+
+#pragma unroll
+    for (int qz = 0; qz < Q1; ++qz) {
+        // contract z
+        double T0[D1][D1], Tz[D1][D1];
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+                for (int dz = 0; dz < D1; ++dz) {
+                    s0 += T.B[qz][dz] * X[dz][dy][dx];
+                    s1 += T.G[qz][dz] * X[dz][dy][dx];
+                }
+                T0[dy][dx] = s0;
+                Tz[dy][dx] = s1;
+            }
+        double RT[D1][D1], RTz[D1][D1];
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) { RT[dy][dx] = 0.0; RTz[dy][dx] = 0.0; }
+
+#pragma unroll
+        for (int qy = 0; qy < Q1; ++qy) {
+            // contract y
+            double a[D1], ay[D1], az[D1];
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+                for (int dy = 0; dy < D1; ++dy) {
+                    s0 += T.B[qy][dy] * T0[dy][dx];
+                    s1 += T.G[qy][dy] * T0[dy][dx];
+                    s2 += T.B[qy][dy] * Tz[dy][dx];
+                }
+                a[dx] = s0; ay[dx] = s1; az[dx] = s2;
+            }
+            double Rv[D1], Ry[D1], Rz[D1];
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) { Rv[dx] = 0.0; Ry[dx] = 0.0; Rz[dx] = 0.0; }
+
+#pragma unroll
+            for (int qx = 0; qx < Q1; ++qx) {
+                // contract x -> value and reference gradient at the point
+                double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+                for (int dx = 0; dx < D1; ++dx) {
+                    u += T.B[qx][dx] * a[dx];
+                    ux += T.G[qx][dx] * a[dx];
+                    uy += T.B[qx][dx] * ay[dx];
+                    uz += T.B[qx][dx] * az[dx];
+                }
+                const int q = qx + Q1 * (qy + Q1 * qz);
+                const double *qq = q0 + (size_t)q * NC * kLanes;
+                double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
+                if constexpr (L::kD) {
+                    const double d00 = qq[0 * kLanes], d01 = qq[1 * kLanes], d02 = qq[2 * kLanes];
+                    const double d11 = qq[3 * kLanes], d12 = qq[4 * kLanes], d22 = qq[5 * kLanes];
+                    gx = d00 * ux + d01 * uy + d02 * uz;
+                    gy = d01 * ux + d11 * uy + d12 * uz;
+                    gz = d02 * ux + d12 * uy + d22 * uz;
+                }
+                if constexpr (L::kC) {
+                    vv = qq[(L::oC + 0) * kLanes] * ux + qq[(L::oC + 1) * kLanes] * uy +
+                         qq[(L::oC + 2) * kLanes] * uz;
+                }
+                if constexpr (L::kM) vv += qq[L::oM * kLanes] * u;
+                // transposed contraction in x
+#pragma unroll
+                for (int dx = 0; dx < D1; ++dx) {
+                    if constexpr (L::kD) {
+                        Rv[dx] += T.B[qx][dx] * vv + T.G[qx][dx] * gx;
+                        Ry[dx] += T.B[qx][dx] * gy;
+                        Rz[dx] += T.B[qx][dx] * gz;
+                    } else {
+                        Rv[dx] += T.B[qx][dx] * vv;
+                    }
+                }
+            }
+            // transposed contraction in y
+#pragma unroll
+            for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < D1; ++dx) {
+                    if constexpr (L::kD) {
+                        RT[dy][dx] += T.B[qy][dy] * Rv[dx] + T.G[qy][dy] * Ry[dx];
+                        RTz[dy][dx] += T.B[qy][dy] * Rz[dx];
+                    } else {
+                        RT[dy][dx] += T.B[qy][dy] * Rv[dx];
+                    }
+                }
+        }
+        // transposed contraction in z
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+            for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < D1; ++dx) {
+                    if constexpr (L::kD)
+                        Y[dz][dy][dx] += T.B[qz][dz] * RT[dy][dx] + T.G[qz][dz] * RTz[dy][dx];
+                    else
+                        Y[dz][dy][dx] += T.B[qz][dz] * RT[dy][dx];
+                }
+    }
+
+    double *yp = Ye + (size_t)b * ND * kLanes + lane;
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) yp[(dx + D1 * (dy + D1 * dz)) * kLanes] = Y[dz][dy][dx];
+}
+
+// ------------------------------------------------------------------------------------------------
+// 2D apply (quads), same mapping
+// ------------------------------------------------------------------------------------------------
+template <int D1, int Q1, unsigned K, bool CON>
+__global__ void __launch_bounds__(256)
+k_apply2d(const int32_t *__restrict__ map, const double *__restrict__ x,
+          const double *__restrict__ qd, double *__restrict__ Ye, const Tab<D1, Q1> T,
+          const int nblk, const KrylovState *__restrict__ st)
+{
+    if (st != nullptr && st->done) return;
+    using L = QLayout<K, 2>;
+    constexpr int ND = D1 * D1;
+    constexpr int NQ = Q1 * Q1;
+    constexpr int NC = L::nc;
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b >= nblk) return;
+
+    const int32_t *mp = map + (size_t)b * ND * kLanes + lane;
+    double X[D1][D1];
+#pragma unroll
+    for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) {
+            const int g = mp[(dx + D1 * dy) * kLanes];
+            if constexpr (CON) {
+                const double v = x[g < 0 ? 0 : g];
+                X[dy][dx] = g < 0 ? 0.0 : v;
+            } else {
+                X[dy][dx] = x[g < 0 ? -g - 1 : g];
+            }
+        }
+    double Y[D1][D1];
+#pragma unroll
+    for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) Y[dy][dx] = 0.0;
+
+    const double *q0 = qd + (size_t)b * NQ * NC * kLanes + lane;
+#pragma unroll
+    for (int qy = 0; qy < Q1; ++qy) {
+        double a[D1], ay[D1];
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) {
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int dy = 0; dy < D1; ++dy) {
+                s0 += T.B[qy][dy] * X[dy][dx];
+                s1 += T.G[qy][dy] * X[dy][dx];
+            }
+            a[dx] = s0; ay[dx] = s1;
+        }
+        double Rv[D1], Ry[D1];
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) { Rv[dx] = 0.0; Ry[dx] = 0.0; }
+#pragma unroll
+        for (int qx = 0; qx < Q1; ++qx) {
+            double u = 0.0, ux = 0.0, uy = 0.0;
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                u += T.B[qx][dx] * a[dx];
+                ux += T.G[qx][dx] * a[dx];
+                uy += T.B[qx][dx] * ay[dx];
+            }
+            const int q = qx + Q1 * qy;
+            const double *qq = q0 + (size_t)q * NC * kLanes;
+            double vv = 0.0, gx = 0.0, gy = 0.0;
+            if constexpr (L::kD) {
+                const double d00 = qq[0], d01 = qq[kLanes], d11 = qq[2 * kLanes];
+                gx = d00 * ux + d01 * uy;
+                gy = d01 * ux + d11 * uy;
+            }
+            if constexpr (L::kC) vv = qq[L::oC * kLanes] * ux + qq[(L::oC + 1) * kLanes] * uy;
+            if constexpr (L::kM) vv += qq[L::oM * kLanes] * u;
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                if constexpr (L::kD) {
+                    Rv[dx] += T.B[qx][dx] * vv + T.G[qx][dx] * gx;
+                    Ry[dx] += T.B[qx][dx] * gy;
+                } else {
+                    Rv[dx] += T.B[qx][dx] * vv;
+                }
+            }
+        }
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                if constexpr (L::kD)
+                    Y[dy][dx] += T.B[qy][dy] * Rv[dx] + T.G[qy][dy] * Ry[dx];
+                else
+                    Y[dy][dx] += T.B[qy][dy] * Rv[dx];
+            }
+    }
+    double *yp = Ye + (size_t)b * ND * kLanes + lane;
+#pragma unroll
+    for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) yp[(dx + D1 * dy) * kLanes] = Y[dy][dx];
+}
+
+// ------------------------------------------------------------------------------------------------
+// geometry helpers (multilinear map, lexicographic vertices)
+// ------------------------------------------------------------------------------------------------
+template <int DIM>
+__device__ inline void q1_map(const double *__restrict__ V, const double xi[3], double x[3],
+                              double J[3][3])
+{
+    constexpr int NV = 1 << DIM;
+    for (int i = 0; i < DIM; ++i) {
+        x[i] = 0.0;
+        for (int k = 0; k < DIM; ++k) J[i][k] = 0.0;
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        double f[3], df[3];
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) {
+            const int bit = (v >> k) & 1;
+            f[k] = bit ? xi[k] : 1.0 - xi[k];
+            df[k] = bit ? 1.0 : -1.0;
+        }
+        double N = 1.0;
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) N *= f[k];
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) {
+            double dN = df[k];
+#pragma unroll
+            for (int m = 0; m < DIM; ++m)
+                if (m != k) dN *= f[m];
+#pragma unroll
+            for (int i = 0; i < DIM; ++i) J[i][k] += V[v * DIM + i] * dN;
+        }
+#pragma unroll
+        for (int i = 0; i < DIM; ++i) x[i] += V[v * DIM + i] * N;
+    }
+}
+
+template <int DIM>
+__device__ inline double adjugate(const double J[3][3], double A[3][3])
+{
+    if constexpr (DIM == 2) {
+        A[0][0] = J[1][1]; A[0][1] = -J[0][1];
+        A[1][0] = -J[1][0]; A[1][1] = J[0][0];
+        return J[0][0] * J[1][1] - J[0][1] * J[1][0];
+    } else {
+        A[0][0] = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+        A[0][1] = J[0][2] * J[2][1] - J[0][1] * J[2][2];
+        A[0][2] = J[0][1] * J[1][2] - J[0][2] * J[1][1];
+        A[1][0] = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+        A[1][1] = J[0][0] * J[2][2] - J[0][2] * J[2][0];
+        A[1][2] = J[0][2] * J[1][0] - J[0][0] * J[1][2];
+        A[2][0] = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+        A[2][1] = J[0][1] * J[2][0] - J[0][0] * J[2][1];
+        A[2][2] = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+        return J[0][0] * A[0][0] + J[0][1] * A[1][0] + J[0][2] * A[2][0];
+    }
+}
+
+__device__ inline void qpoint(int q, int q1, int dim, const Rule1D &r, double xi[3], double &W)
+{
+    const int qx = q % q1, qy = (q / q1) % q1, qz = q / (q1 * q1);
+    xi[0] = r.pts[qx];
+    xi[1] = r.pts[qy];
+    xi[2] = dim == 3 ? r.pts[qz] : 0.0;
+    W = r.wts[qx] * r.wts[qy] * (dim == 3 ? r.wts[qz] : 1.0);
+}
+
+// qdata setup: thread per (element-block, q, lane); coalesced writes of the [b][q][c][lane] layout
+template <int DIM>
+__global__ void __launch_bounds__(256)
+k_setup_qdata(const double *__restrict__ verts, int ne, int nblk, const Rule1D r, unsigned kinds,
+              int nc, double kappa, const double *__restrict__ kappa_q, double alpha, double c0,
+              double c1, double c2, const double *__restrict__ conv_q, double mass,
+              const double *__restrict__ mass_q, double *__restrict__ qd)
+{
+    const int q1 = r.q1;
+    const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)nblk * nq * kLanes) return;
+    const int lane = (int)(t % kLanes);
+    const int q = (int)((t / kLanes) % nq);
+    const int b = (int)(t / ((int64_t)kLanes * nq));
+    const int e = b * kLanes + lane;
+    double *out = qd + ((size_t)b * nq + q) * nc * kLanes + lane;
+    if (e >= ne) {
+        for (int k = 0; k < nc; ++k) out[k * kLanes] = 0.0;
+        return;
+    }
+    double xi[3], W;
+    qpoint(q, q1, DIM, r, xi, W);
+    double x[3], J[3][3], A[3][3];
+    q1_map<DIM>(verts + (size_t)e * (1 << DIM) * DIM, xi, x, J);
+    const double det = adjugate<DIM>(J, A);
+    const size_t eq = (size_t)e * nq + q;
+    int o = 0;
+    if (kinds & CDFEM_DIFFUSION) {
+        const double kap = kappa_q ? kappa_q[eq] : kappa;
+        const double s = W * kap / det;
+        for (int i = 0; i < DIM; ++i)
+            for (int j = i; j < DIM; ++j) {
+                double acc = 0.0;
+                for (int k = 0; k < DIM; ++k) acc += A[i][k] * A[j][k];
+                out[(o++) * kLanes] = s * acc;
+            }
+    }
+    if (kinds & CDFEM_CONVECTION) {
+        double cv[3] = {c0, c1, c2};
+        if (conv_q)
+            for (int k = 0; k < DIM; ++k) cv[k] = conv_q[eq * DIM + k];
+        for (int i = 0; i < DIM; ++i) {
+            double acc = 0.0;
+            for (int k = 0; k < DIM; ++k) acc += A[i][k] * cv[k];
+            out[(o++) * kLanes] = W * alpha * acc;
+        }
+    }
+    if (kinds & CDFEM_MASS) {
+        const double s = mass_q ? mass_q[eq] : mass;
+        out[(o++) * kLanes] = W * s * det;
+    }
+}
+
+// physical coordinates of rule points: xyz[(e*nq + q)*dim + k]
+template <int DIM>
+__global__ void k_quad_points(const double *__restrict__ verts, int ne, const Rule1D r,
+                              double *__restrict__ xyz)
+{
+    const int q1 = r.q1;
+    const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)ne * nq) return;
+    const int e = (int)(t / nq), q = (int)(t % nq);
+    double xi[3], W, x[3], J[3][3];
+    qpoint(q, q1, DIM, r, xi, W);
+    q1_map<DIM>(verts + (size_t)e * (1 << DIM) * DIM, xi, x, J);
+    for (int k = 0; k < DIM; ++k) xyz[t * DIM + k] = x[k];
+}
+
+// phi_l and reference gradient of local dof l at point q
+__device__ inline void basis_at(int l, int q, int dim, const Rule1D &r, double &phi, double g[3])
+{
+    const int d1 = r.d1, q1 = r.q1;
+    const int lx = l % d1, ly = (l / d1) % d1, lz = l / (d1 * d1);
+    const int qx = q % q1, qy = (q / q1) % q1, qz = q / (q1 * q1);
+    const double bx = r.B[qx][lx], gx = r.G[qx][lx], by = r.B[qy][ly], gy = r.G[qy][ly];
+    if (dim == 2) {
+        phi = bx * by; g[0] = gx * by; g[1] = bx * gy; g[2] = 0.0;
+    } else {
+        const double bz = r.B[qz][lz], gz = r.G[qz][lz];
+        phi = bx * by * bz; g[0] = gx * by * bz; g[1] = bx * gy * bz; g[2] = bx * by * gz;
+    }
+}
+
+// PA diagonal, element part: thread per (block, l, lane); Ye layout [b][l][lane]
+template <int DIM>
+__global__ void __launch_bounds__(256)
+k_diag_elem(const double *__restrict__ qd, int nblk, int nd, const Rule1D r, unsigned kinds, int nc,
+            double *__restrict__ Ye)
+{
+    const int q1 = r.q1;
+    const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)nblk * nd * kLanes) return;
+    const int lane = (int)(t % kLanes);
+    const int l = (int)((t / kLanes) % nd);
+    const int b = (int)(t / ((int64_t)kLanes * nd));
+    const int oC = (kinds & CDFEM_DIFFUSION) ? DIM * (DIM + 1) / 2 : 0;
+    const int oM = oC + ((kinds & CDFEM_CONVECTION) ? DIM : 0);
+    double acc = 0.0;
+    for (int q = 0; q < nq; ++q) {
+        const double *qq = qd + ((size_t)b * nq + q) * nc * kLanes + lane;
+        double phi, g[3];
+        basis_at(l, q, DIM, r, phi, g);
+        if (kinds & CDFEM_DIFFUSION) {
+            if (DIM == 3) {
+                const double d00 = qq[0], d01 = qq[kLanes], d02 = qq[2 * kLanes];
+                const double d11 = qq[3 * kLanes], d12 = qq[4 * kLanes], d22 = qq[5 * kLanes];
+                acc += g[0] * (d00 * g[0] + d01 * g[1] + d02 * g[2]) +
+                       g[1] * (d01 * g[0] + d11 * g[1] + d12 * g[2]) +
+                       g[2] * (d02 * g[0] + d12 * g[1] + d22 * g[2]);
+            } else {
+                const double d00 = qq[0], d01 = qq[kLanes], d11 = qq[2 * kLanes];
+                acc += g[0] * (d00 * g[0] + d01 * g[1]) + g[1] * (d01 * g[0] + d11 * g[1]);
+            }
+        }
+        if (kinds & CDFEM_CONVECTION) {
+            double cg = 0.0;
+            for (int k = 0; k < DIM; ++k) cg += qq[(oC + k) * kLanes] * g[k];
+            acc += phi * cg;
+        }
+        if (kinds & CDFEM_MASS) acc += qq[oM * kLanes] * phi * phi;
+    }
+    Ye[t] = acc;  // t == (b*nd + l)*64 + lane
+}
+
+// linear form, element part: be_l = sum_q W detJ f_q phi_l; thread per (block, l, lane)
+template <int DIM>
+__global__ void __launch_bounds__(256)
+k_lf_elem(const double *__restrict__ verts, int ne, int nblk, int nd, const Rule1D r,
+          const double *__restrict__ fq, double *__restrict__ Ye)
+{
+    const int q1 = r.q1;
+    const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)nblk * nd * kLanes) return;
+    const int lane = (int)(t % kLanes);
+    const int l = (int)((t / kLanes) % nd);
+    const int b = (int)(t / ((int64_t)kLanes * nd));
+    const int e = b * kLanes + lane;
+    double acc = 0.0;
+    if (e < ne) {
+        for (int q = 0; q < nq; ++q) {
+            double xi[3], W, x[3], J[3][3], A[3][3], phi, g[3];
+            qpoint(q, q1, DIM, r, xi, W);
+            q1_map<DIM>(verts + (size_t)e * (1 << DIM) * DIM, xi, x, J);
+            const double det = adjugate<DIM>(J, A);
+            basis_at(l, q, DIM, r, phi, g);
+            acc += W * det * fq[(size_t)e * nq + q] * phi;
+        }
+    }
+    Ye[t] = acc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+static inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, double kappa, double alpha,
+                              const double *conv, const double *d_conv_q, const double *d_mass_q,
+                              double mass)
+{
+    const int q1 = c->rule_op.q1;
+    const int nq = c->dim == 3 ? q1 * q1 * q1 : q1 * q1;
+    const int64_t n = (int64_t)c->nblk * nq * kLanes;
+    const double c0 = conv ? conv[0] : 0.0, c1 = conv ? conv[1] : 0.0;
+    const double c2 = (conv && c->dim == 3) ? conv[2] : 0.0;
+    if (c->dim == 3)
+        hipLaunchKernelGGL(k_setup_qdata<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
+                           c->d_verts, c->ne, c->nblk, c->rule_op, c->kinds, c->ncomp, kappa,
+                           d_kappa_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
+    else
+        hipLaunchKernelGGL(k_setup_qdata<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
+                           c->d_verts, c->ne, c->nblk, c->rule_op, c->kinds, c->ncomp, kappa,
+                           d_kappa_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
+    return hipGetLastError();
+}
+
+hipError_t launch_quad_points(cdfem_ctx *c, const Rule1D &r, double *xyz)
+{
+    const int nq = c->dim == 3 ? r.q1 * r.q1 * r.q1 : r.q1 * r.q1;
+    const int64_t n = (int64_t)c->ne * nq;
+    if (c->dim == 3)
+        hipLaunchKernelGGL(k_quad_points<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
+                           c->d_verts, c->ne, r, xyz);
+    else
+        hipLaunchKernelGGL(k_quad_points<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
+                           c->d_verts, c->ne, r, xyz);
+    return hipGetLastError();
+}
+
+hipError_t launch_diag_elem(cdfem_ctx *c, double *Ye)
+{
+    const int64_t n = (int64_t)c->nblk * c->nd * kLanes;
+    if (c->dim == 3)
+        hipLaunchKernelGGL(k_diag_elem<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
+                           c->d_qd, c->nblk, c->nd, c->rule_op, c->kinds, c->ncomp, Ye);
+    else
+        hipLaunchKernelGGL(k_diag_elem<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
+                           c->d_qd, c->nblk, c->nd, c->rule_op, c->kinds, c->ncomp, Ye);
+    return hipGetLastError();
+}
+
+hipError_t launch_lf_elem(cdfem_ctx *c, const double *d_fq, double *Ye)
+{
+    const int64_t n = (int64_t)c->nblk * c->nd * kLanes;
+    if (c->dim == 3)
+        hipLaunchKernelGGL(k_lf_elem<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
+                           c->d_verts, c->ne, c->nblk, c->nd, c->rule_lf, d_fq, Ye);
+    else
+        hipLaunchKernelGGL(k_lf_elem<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
+                           c->d_verts, c->ne, c->nblk, c->nd, c->rule_lf, d_fq, Ye);
+    return hipGetLastError();
+}
+
+template <int DIM, int D1, int Q1, unsigned K>
+static hipError_t apply_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con,
+                              const KrylovState *st)
+{
+    const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
+    const dim3 grid(grid_for(c->nblk, 4)), block(256);
+    if constexpr (DIM == 3) {
+        if (con)
+            hipLaunchKernelGGL((k_apply3d<D1, Q1, K, true>), grid, block, 0, c->stream, c->d_map, x,
+                               c->d_qd, Ye, T, c->nblk, st);
+        else
+            hipLaunchKernelGGL((k_apply3d<D1, Q1, K, false>), grid, block, 0, c->stream, c->d_map,
+                               x, c->d_qd, Ye, T, c->nblk, st);
+    } else {
+        if (con)
+            hipLaunchKernelGGL((k_apply2d<D1, Q1, K, true>), grid, block, 0, c->stream, c->d_map, x,
+                               c->d_qd, Ye, T, c->nblk, st);
+        else
+            hipLaunchKernelGGL((k_apply2d<D1, Q1, K, false>), grid, block, 0, c->stream, c->d_map,
+                               x, c->d_qd, Ye, T, c->nblk, st);
+    }
+    return hipGetLastError();
+}
+
+template <int DIM, int D1, int Q1>
+static hipError_t apply_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
+{
+    switch (c->kinds) {
+    case 1: return apply_kinds<DIM, D1, Q1, 1>(c, x, Ye, con, st);
+    case 2: return apply_kinds<DIM, D1, Q1, 2>(c, x, Ye, con, st);
+    case 3: return apply_kinds<DIM, D1, Q1, 3>(c, x, Ye, con, st);
+    case 4: return apply_kinds<DIM, D1, Q1, 4>(c, x, Ye, con, st);
+    case 5: return apply_kinds<DIM, D1, Q1, 5>(c, x, Ye, con, st);
+    case 6: return apply_kinds<DIM, D1, Q1, 6>(c, x, Ye, con, st);
+    case 7: return apply_kinds<DIM, D1, Q1, 7>(c, x, Ye, con, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+bool apply_supported(int dim, int p)
+{
+    if (dim == 3) return p == 1 || p == 2;
+    if (dim == 2) return p >= 1 && p <= 4;
+    return false;
+}
+
+// the kernel-side CG loop passes its state so a finished solve turns queued launches into no-ops
+hipError_t launch_apply_st(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
+{
+    const int q1 = c->rule_op.q1;
+    if (c->dim == 3) {
+        if (c->p == 1 && q1 == 3) return apply_dq<3, 2, 3>(c, x, Ye, con, st);
+        if (c->p == 2 && q1 == 4) return apply_dq<3, 3, 4>(c, x, Ye, con, st);
+    } else {
+        if (c->p == 1 && q1 == 2) return apply_dq<2, 2, 2>(c, x, Ye, con, st);
+        if (c->p == 2 && q1 == 3) return apply_dq<2, 3, 3>(c, x, Ye, con, st);
+        if (c->p == 3 && q1 == 4) return apply_dq<2, 4, 4>(c, x, Ye, con, st);
+        if (c->p == 4 && q1 == 5) return apply_dq<2, 5, 5>(c, x, Ye, con, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_apply(cdfem_ctx *c, const double *x, double *Ye, bool constrained)
+{
+    return launch_apply_st(c, x, Ye, constrained, nullptr);
+}
+
+}  // namespace cdfem

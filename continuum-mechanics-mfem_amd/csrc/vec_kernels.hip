@@ -1,0 +1,355 @@
+// vec_kernels.hip — E->L summation, Krylov vector kernels and deterministic reductions.
+//
+// The CG loop (MFEM CGSolver::Mult semantics, as the reference pins them by use at
+// mesh_recession_handler.cpp:270-276) runs entirely stream-ordered on the device: scalars live in
+// a KrylovState in HBM, every reduction is a fixed-grid block reduction whose LAST arriving block
+// (agent-scope release/acquire, MI355X_MICROARCH.md "Valid forms") sums the partials in index
+// order, so results are bitwise reproducible run to run and independent of dispatch/XCD placement.
+// Kernels queued after convergence see state->done and exit at entry, so the host polls the state
+// only every `check_every` iterations.
+#include <hip/hip_runtime.h>
+
+#include "cdfem_internal.hpp"
+
+namespace cdfem {
+
+constexpr int kRedThreads = 256;
+
+__device__ inline double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// block sum, result valid in thread 0
+__device__ inline double block_sum(double v, double *sh)
+{
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        v = (threadIdx.x < (blockDim.x >> 6)) ? sh[threadIdx.x] : 0.0;
+        v = wave_sum(v);
+    }
+    return v;
+}
+
+// Publish this block's partial and find out whether it is the last arriver.  Producer side: plain
+// store, every wave drains vmcnt, barrier, lane-0 agent release, asm drain, relaxed agent ticket.
+// The last arriver then acquires (agent) before reading other blocks' partials.
+__device__ inline bool publish_partial(double v, double *part, unsigned *cnt, int *sh_last)
+{
+    if (threadIdx.x == 0) part[blockIdx.x] = v;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = (prev == gridDim.x - 1);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *sh_last = last ? 1 : 0;
+    }
+    __syncthreads();
+    return *sh_last != 0;
+}
+
+// deterministic sum of part[0..n) by one block (fixed order), result in thread 0
+__device__ inline double sum_partials(const double *part, int n, double *sh)
+{
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) v += part[i];
+    return block_sum(v, sh);
+}
+
+// ------------------------------------------------------------------------------------------------
+// E->L: y[i] = sum of Ye over the (element, local dof) pairs of dof i (ascending element order).
+// constrained: y[ess] = x[ess] (ConstrainedOperator, DIAG_ONE).  cg_mode: also den = (x, y),
+// last block: MFEM CG "den" step (alpha = betanom / den, nom = betanom).
+// ------------------------------------------------------------------------------------------------
+template <bool CON, bool CG>
+__global__ void __launch_bounds__(kRedThreads)
+k_e2l(const int32_t *__restrict__ off, const int32_t *__restrict__ pos,
+      const uint8_t *__restrict__ ess, const double *__restrict__ Ye, const double *__restrict__ x,
+      double *__restrict__ y, int64_t nl, double *__restrict__ part, KrylovState *__restrict__ st)
+{
+    __shared__ double sh[kRedThreads / 64];
+    __shared__ int sh_last;
+    if (CG && st->done) return;
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
+        double v;
+        if (CON && ess[i]) {
+            v = x[i];
+        } else {
+            v = 0.0;
+            const int k1 = off[i + 1];
+            for (int k = off[i]; k < k1; ++k) v += Ye[pos[k]];
+        }
+        y[i] = v;
+        if (CG) acc += v * x[i];
+    }
+    if (!CG) return;
+    const double bs = block_sum(acc, sh);
+    if (!publish_partial(bs, part, &st->cnt[0], &sh_last)) return;
+    const double den = sum_partials(part, gridDim.x, sh);
+    if (threadIdx.x == 0) {
+        st->cnt[0] = 0;
+        st->den = den;
+        const int first = (st->first_den != 0);
+        st->first_den = 0;
+        if (den == 0.0) {               // CGSolver: den == 0 -> stop, not converged
+            st->done = 1;
+            st->converged = 0;
+            st->final_iter = first ? 0 : st->iter;
+        } else {
+            st->nom = st->betanom;      // (initial den: betanom == nom0)
+            st->alpha = st->nom / den;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// CG init: r = B, x = 0, z = M^{-1} r, d = z, nom = (d, r)
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kRedThreads)
+k_cg_init(const double *__restrict__ B, double *__restrict__ x, double *__restrict__ r,
+          double *__restrict__ z, double *__restrict__ d, const double *__restrict__ dinv, int64_t n,
+          double rel_tol, double abs_tol, int max_iter, double *__restrict__ part,
+          KrylovState *__restrict__ st)
+{
+    __shared__ double sh[kRedThreads / 64];
+    __shared__ int sh_last;
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double ri = B[i];
+        const double zi = dinv ? dinv[i] * ri : ri;
+        r[i] = ri;
+        x[i] = 0.0;
+        z[i] = zi;
+        d[i] = zi;
+        acc += zi * ri;
+    }
+    const double bs = block_sum(acc, sh);
+    if (!publish_partial(bs, part, &st->cnt[2], &sh_last)) return;
+    const double nom = sum_partials(part, gridDim.x, sh);
+    if (threadIdx.x == 0) {
+        st->cnt[2] = 0;
+        st->nom = st->nom0 = st->betanom = nom;
+        const double r0 = fmax(nom * rel_tol * rel_tol, abs_tol * abs_tol);
+        st->r0 = r0;
+        st->iter = 1;
+        st->max_iter = max_iter;
+        st->final_iter = max_iter;
+        st->converged = 0;
+        st->done = 0;
+        st->first_den = 1;  // next den is the initial one
+        if (nom < 0.0) {             // preconditioner not positive definite
+            st->done = 1;
+            st->final_iter = 0;
+        } else if (nom <= r0) {
+            st->done = 1;
+            st->converged = 1;
+            st->final_iter = 0;
+        }
+    }
+}
+
+// x += alpha d, r -= alpha z, z = M^{-1} r, betanom = (r, z); last block: convergence test
+__global__ void __launch_bounds__(kRedThreads)
+k_cg_update(double *__restrict__ x, double *__restrict__ r, double *__restrict__ z,
+            const double *__restrict__ d, const double *__restrict__ dinv, int64_t n,
+            double *__restrict__ part, KrylovState *__restrict__ st)
+{
+    __shared__ double sh[kRedThreads / 64];
+    __shared__ int sh_last;
+    if (st->done) return;
+    const double alpha = st->alpha;
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        x[i] += alpha * d[i];
+        const double ri = r[i] - alpha * z[i];
+        r[i] = ri;
+        const double zi = dinv ? dinv[i] * ri : ri;
+        z[i] = zi;
+        acc += ri * zi;
+    }
+    const double bs = block_sum(acc, sh);
+    if (!publish_partial(bs, part, &st->cnt[1], &sh_last)) return;
+    const double betanom = sum_partials(part, gridDim.x, sh);
+    if (threadIdx.x == 0) {
+        st->cnt[1] = 0;
+        st->betanom = betanom;
+        const int i = st->iter;
+        if (betanom < 0.0) {
+            st->done = 1; st->converged = 0; st->final_iter = i;
+        } else if (betanom <= st->r0) {
+            st->done = 1; st->converged = 1; st->final_iter = i;
+        } else if (i + 1 > st->max_iter) {
+            st->done = 1; st->converged = 0; st->final_iter = st->max_iter;
+        } else {
+            st->beta = betanom / st->nom;
+            st->iter = i + 1;
+        }
+    }
+}
+
+// d = z + beta d
+__global__ void __launch_bounds__(kRedThreads)
+k_cg_direction(const double *__restrict__ z, double *__restrict__ d, int64_t n,
+               const KrylovState *__restrict__ st)
+{
+    if (st->done) return;
+    const double beta = st->beta;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        d[i] = z[i] + beta * d[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// small helpers
+// ------------------------------------------------------------------------------------------------
+__global__ void k_set_ess(const int32_t *__restrict__ list, int n, double *__restrict__ y,
+                          const double *__restrict__ x)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[list[i]] = x[list[i]];
+}
+
+__global__ void k_ess_only(const uint8_t *__restrict__ ess, const double *__restrict__ x,
+                           double *__restrict__ y, int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        y[i] = ess[i] ? x[i] : 0.0;
+}
+
+__global__ void k_axpby(double a, const double *__restrict__ x, double b, double *__restrict__ y,
+                        int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        y[i] = a * x[i] + b * y[i];
+}
+
+__global__ void k_dinv(const uint8_t *__restrict__ ess, const double *__restrict__ diag,
+                       double *__restrict__ dinv, int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        dinv[i] = ess[i] ? 1.0 : 1.0 / diag[i];
+}
+
+// deterministic dot into *out (two-level: partials then last block)
+__global__ void __launch_bounds__(kRedThreads)
+k_dot(const double *__restrict__ a, const double *__restrict__ b, int64_t n,
+      double *__restrict__ part, unsigned *__restrict__ cnt, double *__restrict__ out)
+{
+    __shared__ double sh[kRedThreads / 64];
+    __shared__ int sh_last;
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        acc += a[i] * b[i];
+    const double bs = block_sum(acc, sh);
+    if (!publish_partial(bs, part, cnt, &sh_last)) return;
+    const double s = sum_partials(part, gridDim.x, sh);
+    if (threadIdx.x == 0) {
+        *cnt = 0;
+        *out = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+static inline unsigned red_grid(cdfem_ctx *c, int64_t n)
+{
+    const int64_t need = (n + kRedThreads - 1) / kRedThreads;
+    return (unsigned)(need < c->red_blocks ? (need < 1 ? 1 : need) : c->red_blocks);
+}
+
+hipError_t launch_e2l(cdfem_ctx *c, const double *Ye, const double *x, double *y, bool con,
+                      int cg_mode)
+{
+    const dim3 g(red_grid(c, c->nl)), b(kRedThreads);
+    if (cg_mode)
+        hipLaunchKernelGGL((k_e2l<true, true>), g, b, 0, c->stream, c->d_e2l_off, c->d_e2l_pos,
+                           c->d_ess, Ye, x, y, c->nl, c->d_part, c->d_state);
+    else if (con)
+        hipLaunchKernelGGL((k_e2l<true, false>), g, b, 0, c->stream, c->d_e2l_off, c->d_e2l_pos,
+                           c->d_ess, Ye, x, y, c->nl, c->d_part, c->d_state);
+    else
+        hipLaunchKernelGGL((k_e2l<false, false>), g, b, 0, c->stream, c->d_e2l_off, c->d_e2l_pos,
+                           c->d_ess, Ye, x, y, c->nl, c->d_part, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_ess(cdfem_ctx *c, double *y, const double *x)
+{
+    if (c->n_ess == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_set_ess, dim3((c->n_ess + 255) / 256), dim3(256), 0, c->stream,
+                       c->d_ess_list, c->n_ess, y, x);
+    return hipGetLastError();
+}
+
+hipError_t launch_mask_ess(cdfem_ctx *c, const double *x, double *y)
+{
+    hipLaunchKernelGGL(k_ess_only, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream,
+                       c->d_ess, x, y, c->nl);
+    return hipGetLastError();
+}
+
+hipError_t launch_axpby(cdfem_ctx *c, double a, const double *x, double b, double *y)
+{
+    hipLaunchKernelGGL(k_axpby, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, a, x, b,
+                       y, c->nl);
+    return hipGetLastError();
+}
+
+hipError_t launch_dinv(cdfem_ctx *c, const double *diag, double *dinv)
+{
+    hipLaunchKernelGGL(k_dinv, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, c->d_ess,
+                       diag, dinv, c->nl);
+    return hipGetLastError();
+}
+
+hipError_t launch_cg_init(cdfem_ctx *c, const double *B, double *x, double *r, double *z, double *d,
+                          const double *dinv, double rel_tol, double abs_tol, int max_iter)
+{
+    hipLaunchKernelGGL(k_cg_init, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, B, x, r,
+                       z, d, dinv, c->nl, rel_tol, abs_tol, max_iter, c->d_part, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_cg_update(cdfem_ctx *c, double *x, double *r, double *z, const double *d,
+                            const double *dinv)
+{
+    hipLaunchKernelGGL(k_cg_update, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, x, r,
+                       z, d, dinv, c->nl, c->d_part, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_cg_direction(cdfem_ctx *c, const double *z, double *d)
+{
+    hipLaunchKernelGGL(k_cg_direction, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, z,
+                       d, c->nl, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out)
+{
+    hipLaunchKernelGGL(k_dot, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, a, b, c->nl,
+                       c->d_part, &c->d_state->cnt[3], d_out);
+    return hipGetLastError();
+}
+
+}  // namespace cdfem

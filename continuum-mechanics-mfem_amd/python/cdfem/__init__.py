@@ -1,0 +1,318 @@
+"""Python binding of libcdfem.so (the C-ABI in include/cdfem.h) via ctypes.
+
+This is plumbing for tests, the benchmark and Python callers: every numerical operation runs in
+the HIP kernels of the library.  There is NO CPU fallback — if the shared library or a GPU is
+missing, the calls raise (``CdfemError``), they never compute on the host.
+
+The classes mirror the reference's operator interface on the hot path
+(linear_convection_diffusion_2D.cpp:335-377):
+
+    ParBilinearForm-like  -> Context.pa_setup(...)   (Diffusion/Convection/Mass integrators + Assemble)
+    Operator::Mult        -> Context.mult(x)          (constrained=True: the FormLinearSystem operator)
+    FormLinearSystem      -> Context.form_linear_system(x, b)
+    Krylov Mult(B, X)     -> Context.solve(B, method="cg"|"gmres", ...)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_PKG_ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libcdfem.so")
+HEADER_PATH = os.path.abspath(os.path.join(_PKG_ROOT, "..", "include", "cdfem.h"))
+
+DIFFUSION, CONVECTION, MASS = 1, 2, 4
+HOST, DEVICE = 0, 1
+CG, GMRES = 0, 1
+PC_NONE, PC_JACOBI = 0, 1
+RULE_OPERATOR, RULE_LINEARFORM, RULE_ERROR = 0, 1, 2
+K_APPLY, K_E2L, K_UPDATE, K_DIRECTION = 0, 1, 2, 3
+
+OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_UNSUPPORTED, ERR_NOT_CONVERGED, ERR_COMM = range(7)
+
+
+class CdfemError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"cdfem error {code}: {msg}")
+        self.code = code
+
+
+class SolverParams(C.Structure):
+    _fields_ = [("method", C.c_int), ("pc", C.c_int), ("max_iter", C.c_int), ("restart", C.c_int),
+                ("rel_tol", C.c_double), ("abs_tol", C.c_double), ("check_every", C.c_int),
+                ("print_level", C.c_int)]
+
+
+class SolverResult(C.Structure):
+    _fields_ = [("converged", C.c_int), ("iterations", C.c_int), ("final_norm", C.c_double),
+                ("initial_norm", C.c_double), ("seconds", C.c_double)]
+
+
+_lib = None
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+def _declare(L):
+    vp, i64 = C.c_void_p, C.c_int64
+    sig = {
+        "cdfem_abi_version": (C.c_int, []),
+        "cdfem_device_count": (C.c_int, []),
+        "cdfem_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "cdfem_destroy": (None, [vp]),
+        "cdfem_last_error": (C.c_char_p, [vp]),
+        "cdfem_synchronize": (C.c_int, [vp]),
+        "cdfem_alloc": (C.c_int, [vp, C.c_size_t, C.POINTER(vp)]),
+        "cdfem_free": (C.c_int, [vp, vp]),
+        "cdfem_memcpy": (C.c_int, [vp, vp, C.c_int, vp, C.c_int, C.c_size_t]),
+        "cdfem_mesh_upload": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, _dp, i64, _ip, C.c_int, _ip]),
+        "cdfem_rule_size": (C.c_int, [vp, C.c_int, C.POINTER(C.c_int)]),
+        "cdfem_quadrature_points": (C.c_int, [vp, C.c_int, _dp, C.c_int]),
+        "cdfem_pa_setup": (C.c_int, [vp, C.c_uint, C.c_double, _dp, C.c_double, _dp, _dp, C.c_double, _dp]),
+        "cdfem_pa_mult": (C.c_int, [vp, vp, vp, C.c_int, C.c_int]),
+        "cdfem_pa_diagonal": (C.c_int, [vp, vp, C.c_int]),
+        "cdfem_lf_assemble": (C.c_int, [vp, vp, vp, C.c_int]),
+        "cdfem_form_linear_system": (C.c_int, [vp, vp, vp, vp, vp, C.c_int]),
+        "cdfem_solve": (C.c_int, [vp, C.POINTER(SolverParams), vp, vp, C.c_int, C.POINTER(SolverResult)]),
+        "cdfem_profile_enable": (C.c_int, [vp, C.c_int]),
+        "cdfem_profile_reset": (C.c_int, [vp]),
+        "cdfem_profile_read": (C.c_int, [vp, C.c_int, _dp, C.POINTER(i64)]),
+        "cdfem_kernel_bytes": (C.c_int, [vp, C.c_int, _dp]),
+        "cdfem_box_sizes": (C.c_int, [C.c_int] * 7 + [C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int)]),
+        "cdfem_box_mesh": (C.c_int, [C.c_int] * 7 + [C.c_double, _dp, _ip, _ip, _dp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+def lib():
+    """Load libcdfem.so; raises if it has not been built (no fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise CdfemError(ERR_STATE, f"{LIB_PATH} not built: run __graft_entry__.build() or make")
+        _lib = _declare(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def exported_symbols_from_header(path=HEADER_PATH):
+    """Function names declared in include/cdfem.h (used by the ABI export test)."""
+    import re
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(cdfem_[a-z0-9_]+)\s*\(", txt)))
+
+
+def device_count():
+    return lib().cdfem_device_count()
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+@dataclass
+class Mesh:
+    dim: int
+    order: int
+    verts: np.ndarray      # (ne, 2^dim, dim)
+    dofmap: np.ndarray     # (ne, (p+1)^dim) int32
+    nl: int
+    ess: np.ndarray        # int32
+    dof_xyz: np.ndarray | None = None
+
+    @property
+    def ne(self):
+        return self.dofmap.shape[0]
+
+
+def box_mesh(dim, n, order, z_range=None, perturb=0.0, with_coords=True) -> Mesh:
+    """Structured [0,1]^dim mesh (or a z-slab [z0,z1) of it) generated by the library."""
+    nx, ny, nz = (n, n, n) if np.isscalar(n) else (tuple(n) + (1,))[:3]
+    z0, z1 = z_range if z_range is not None else (0, 0)
+    L = lib()
+    ne, nl, ness = C.c_int(), C.c_int64(), C.c_int()
+    rc = L.cdfem_box_sizes(dim, nx, ny, nz, order, z0, z1, C.byref(ne), C.byref(nl), C.byref(ness))
+    if rc:
+        raise CdfemError(rc, "bad box mesh arguments")
+    nv, nd = 2 ** dim, (order + 1) ** dim
+    verts = np.zeros((ne.value, nv, dim))
+    dofmap = np.zeros((ne.value, nd), dtype=np.int32)
+    ess = np.zeros(ness.value, dtype=np.int32)
+    xyz = np.zeros((nl.value, dim)) if with_coords else None
+    rc = L.cdfem_box_mesh(dim, nx, ny, nz, order, z0, z1, float(perturb), _p(verts),
+                          dofmap.ctypes.data_as(_ip), ess.ctypes.data_as(_ip), _p(xyz))
+    if rc:
+        raise CdfemError(rc, "box mesh generation failed")
+    return Mesh(dim, order, verts, dofmap, nl.value, ess, xyz)
+
+
+class Context:
+    """One GPU context (cdfem_ctx): mesh + H1 space + fused PA operator + Krylov solvers."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = C.c_void_p()
+        rc = L.cdfem_create(int(device), C.byref(h))
+        if rc:
+            raise CdfemError(rc, f"cdfem_create(device={device}) failed "
+                                 f"({L.cdfem_device_count()} HIP devices visible)")
+        self.h = h
+        self.L = L
+        self.mesh = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.cdfem_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, rc, allow=()):
+        if rc and rc not in allow:
+            raise CdfemError(rc, self.L.cdfem_last_error(self.h).decode())
+        return rc
+
+    # -- space ---------------------------------------------------------------------------------
+    def upload_mesh(self, mesh: Mesh):
+        verts = _f64(mesh.verts)
+        dofmap = _i32(mesh.dofmap)
+        ess = _i32(mesh.ess)
+        self._chk(self.L.cdfem_mesh_upload(self.h, mesh.dim, mesh.order, dofmap.shape[0], _p(verts),
+                                           int(mesh.nl), dofmap.ctypes.data_as(_ip), len(ess),
+                                           ess.ctypes.data_as(_ip)))
+        self.mesh = mesh
+        self.nl = int(mesh.nl)
+        return self
+
+    def rule_size(self, rule):
+        n = C.c_int()
+        self._chk(self.L.cdfem_rule_size(self.h, rule, C.byref(n)))
+        return n.value
+
+    def quadrature_points(self, rule):
+        nq = self.rule_size(rule)
+        xyz = np.zeros((self.mesh.ne, nq, self.mesh.dim))
+        self._chk(self.L.cdfem_quadrature_points(self.h, rule, _p(xyz), HOST))
+        return xyz
+
+    # -- operator ------------------------------------------------------------------------------
+    def pa_setup(self, kinds=DIFFUSION | CONVECTION | MASS, kappa=1.0, alpha=1.0, conv=None, mass=1.0,
+                 kappa_q=None, conv_q=None, mass_q=None):
+        cv = None
+        if conv is not None:
+            cv = np.zeros(3)
+            cv[: len(conv)] = conv
+        keep = [_f64(a) if a is not None else None for a in (kappa_q, conv_q, mass_q)]
+        self._chk(self.L.cdfem_pa_setup(self.h, kinds, float(kappa), _p(keep[0]), float(alpha), _p(cv),
+                                        _p(keep[1]), float(mass), _p(keep[2])))
+        return self
+
+    def mult(self, x, constrained=False):
+        x = _f64(x)
+        y = np.zeros(self.nl)
+        self._chk(self.L.cdfem_pa_mult(self.h, x.ctypes.data, y.ctypes.data, int(constrained), HOST))
+        return y
+
+    def diagonal(self):
+        d = np.zeros(self.nl)
+        self._chk(self.L.cdfem_pa_diagonal(self.h, d.ctypes.data, HOST))
+        return d
+
+    def lf_assemble(self, f_q):
+        f_q = _f64(f_q)
+        b = np.zeros(self.nl)
+        self._chk(self.L.cdfem_lf_assemble(self.h, f_q.ctypes.data, b.ctypes.data, HOST))
+        return b
+
+    def form_linear_system(self, x, b):
+        x, b = _f64(x), _f64(b)
+        X, B = np.zeros(self.nl), np.zeros(self.nl)
+        self._chk(self.L.cdfem_form_linear_system(self.h, x.ctypes.data, b.ctypes.data, X.ctypes.data,
+                                                  B.ctypes.data, HOST))
+        return X, B
+
+    def solve(self, B, method="cg", pc="jacobi", rel_tol=1e-12, abs_tol=0.0, max_iter=500, restart=30,
+              check_every=16, raise_on_fail=False):
+        prm = SolverParams(CG if method == "cg" else GMRES, PC_JACOBI if pc == "jacobi" else PC_NONE,
+                           int(max_iter), int(restart), float(rel_tol), float(abs_tol), int(check_every), 0)
+        res = SolverResult()
+        B = _f64(B)
+        X = np.zeros(self.nl)
+        rc = self.L.cdfem_solve(self.h, C.byref(prm), B.ctypes.data, X.ctypes.data, HOST, C.byref(res))
+        self._chk(rc, allow=() if raise_on_fail else (ERR_NOT_CONVERGED,))
+        return X, dict(converged=bool(res.converged), iterations=res.iterations,
+                       final_norm=res.final_norm, initial_norm=res.initial_norm, seconds=res.seconds)
+
+    # -- device-resident variants (benchmarks) ------------------------------------------------------
+    def alloc(self, nbytes):
+        p = C.c_void_p()
+        self._chk(self.L.cdfem_alloc(self.h, int(nbytes), C.byref(p)))
+        return p.value
+
+    def free(self, ptr):
+        self._chk(self.L.cdfem_free(self.h, C.c_void_p(ptr)))
+
+    def to_device(self, a):
+        a = _f64(a)
+        p = self.alloc(a.nbytes)
+        self._chk(self.L.cdfem_memcpy(self.h, C.c_void_p(p), DEVICE, a.ctypes.data, HOST, a.nbytes))
+        return p
+
+    def from_device(self, ptr, n):
+        out = np.zeros(n)
+        self._chk(self.L.cdfem_memcpy(self.h, out.ctypes.data, HOST, C.c_void_p(ptr), DEVICE, out.nbytes))
+        return out
+
+    def solve_device(self, dB, dX, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=100,
+                     restart=30, check_every=0):
+        prm = SolverParams(CG if method == "cg" else GMRES, PC_JACOBI if pc == "jacobi" else PC_NONE,
+                           int(max_iter), int(restart), float(rel_tol), float(abs_tol),
+                           int(check_every if check_every else max_iter), 0)
+        res = SolverResult()
+        rc = self.L.cdfem_solve(self.h, C.byref(prm), C.c_void_p(dB), C.c_void_p(dX), DEVICE, C.byref(res))
+        self._chk(rc, allow=(ERR_NOT_CONVERGED,))
+        return dict(converged=bool(res.converged), iterations=res.iterations, final_norm=res.final_norm,
+                    initial_norm=res.initial_norm, seconds=res.seconds)
+
+    def mult_device(self, dx, dy, constrained=False):
+        self._chk(self.L.cdfem_pa_mult(self.h, C.c_void_p(dx), C.c_void_p(dy), int(constrained), DEVICE))
+
+    def synchronize(self):
+        self._chk(self.L.cdfem_synchronize(self.h))
+
+    # -- profiling -----------------------------------------------------------------------------------
+    def profile(self, on=True):
+        self._chk(self.L.cdfem_profile_enable(self.h, int(on)))
+        self._chk(self.L.cdfem_profile_reset(self.h))
+
+    def profile_read(self, kernel):
+        ms, n = C.c_double(), C.c_int64()
+        self._chk(self.L.cdfem_profile_read(self.h, kernel, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def kernel_bytes(self, kernel):
+        b = C.c_double()
+        self._chk(self.L.cdfem_kernel_bytes(self.h, kernel, C.byref(b)))
+        return b.value

@@ -1,0 +1,170 @@
+/*
+ * cdfem.h — C-ABI of the MI355X-native convection-diffusion FE hot path (libcdfem.so).
+ *
+ * One opaque context per GPU (per process / rank).  All entry points return CDFEM_OK (0) or an
+ * error code; the message is in cdfem_last_error(ctx).  No C++ exception crosses this boundary;
+ * the C++ mfem-compatible layer (include/cdfem/mfem_compat.hpp) turns a non-zero status into
+ * std::runtime_error, which the reference drivers already map to exit code 3
+ * (linear_convection_diffusion_2D.cpp:435-442).
+ *
+ * Each entry point names the reference interface it replaces.  The reference calls MFEM, hypre
+ * and PETSc (not vendored: SURVEY.md §8b/c), so the "replaces" lines cite the reference CALL SITE.
+ *
+ * Ownership: the caller owns every host array; the context owns every device buffer it allocates;
+ * no caller pointer is retained after a call returns.  Pointers tagged `where` are host memory
+ * when where == CDFEM_HOST and device memory (hipMalloc / cdfem_alloc) when where == CDFEM_DEVICE.
+ * A context is not thread-safe.  Calls with where == CDFEM_HOST are synchronous on return.
+ *
+ * Vector spaces.  L-vector = all dofs of the rank's elements (for one rank this is also MFEM's
+ * T-vector: P = I on a conforming mesh).  DoF numbering and element-dof maps are supplied by the
+ * caller; element dofs are LEXICOGRAPHIC on the tensor element (l = dx + (p+1)(dy + (p+1)dz)),
+ * element vertices lexicographic (v = a + 2b + 4c), reference element [0,1]^dim.
+ */
+#ifndef CDFEM_H
+#define CDFEM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CDFEM_ABI_VERSION 1
+
+typedef struct cdfem_ctx cdfem_ctx;
+
+enum cdfem_status {
+    CDFEM_OK = 0,
+    CDFEM_ERR_ARG = 1,          /* bad argument / shape mismatch                          */
+    CDFEM_ERR_HIP = 2,          /* HIP runtime error (no device, OOM, launch failure)     */
+    CDFEM_ERR_STATE = 3,        /* call order violated (e.g. mult before setup)          */
+    CDFEM_ERR_UNSUPPORTED = 4,  /* dim/order/kernel combination not built                 */
+    CDFEM_ERR_NOT_CONVERGED = 5,/* Krylov solve hit max_iter (result still returned)      */
+    CDFEM_ERR_COMM = 6          /* RCCL error                                             */
+};
+
+/* integrator kinds (bit mask) */
+enum { CDFEM_DIFFUSION = 1, CDFEM_CONVECTION = 2, CDFEM_MASS = 4 };
+/* pointer locations */
+enum { CDFEM_HOST = 0, CDFEM_DEVICE = 1 };
+/* Krylov methods and preconditioners */
+enum { CDFEM_CG = 0, CDFEM_GMRES = 1 };
+enum { CDFEM_PC_NONE = 0, CDFEM_PC_JACOBI = 1 };
+/* quadrature rules whose points the host may need for coefficient evaluation */
+enum { CDFEM_RULE_OPERATOR = 0, CDFEM_RULE_LINEARFORM = 1, CDFEM_RULE_ERROR = 2 };
+/* kernel ids for cdfem_profile_read */
+enum { CDFEM_K_APPLY = 0, CDFEM_K_E2L = 1, CDFEM_K_UPDATE = 2, CDFEM_K_DIRECTION = 3, CDFEM_K_COUNT = 8 };
+
+int cdfem_abi_version(void);
+
+/* ---- context ------------------------------------------------------------------------------- */
+/* replaces: Device device("cpu") (linear_convection_diffusion_2D.cpp:287) — here: one MI355X.  */
+int cdfem_create(int device, cdfem_ctx **out);
+void cdfem_destroy(cdfem_ctx *ctx);
+const char *cdfem_last_error(const cdfem_ctx *ctx);
+int cdfem_synchronize(cdfem_ctx *ctx);
+/* number of visible HIP devices (0 on a CPU-only host; never fails) */
+int cdfem_device_count(void);
+
+/* ---- device memory helpers (for where == CDFEM_DEVICE callers and benchmarks) ---------------- */
+int cdfem_alloc(cdfem_ctx *ctx, size_t bytes, void **dptr);
+int cdfem_free(cdfem_ctx *ctx, void *dptr);
+int cdfem_memcpy(cdfem_ctx *ctx, void *dst, int dst_where, const void *src, int src_where, size_t bytes);
+
+/* ---- mesh + H1 space -------------------------------------------------------------------------
+ * replaces: ParMesh + H1_FECollection(order, dim) + ParFiniteElementSpace + GetEssentialTrueDofs
+ *           (linear_convection_diffusion_2D.cpp:300-322; diffusion_mms.cpp:275-285).
+ * elem_verts: ne * 2^dim * dim doubles (multilinear geometry), elem_dofs: ne * (order+1)^dim
+ * L-dof indices in [0, nldofs), ess_dofs: essential L-dofs (Dirichlet on the marked boundary).  */
+int cdfem_mesh_upload(cdfem_ctx *ctx, int dim, int order, int ne, const double *elem_verts,
+                      int64_t nldofs, const int32_t *elem_dofs, int n_ess, const int32_t *ess_dofs);
+
+/* Physical coordinates of the quadrature points of a rule (CDFEM_RULE_*), ne * nq * dim doubles,
+ * element-major, q lexicographic (qx fastest): where a host Coefficient::Eval is sampled
+ * (linear_convection_diffusion_2D.cpp:165-215).  cdfem_rule_size returns nq per element.       */
+int cdfem_rule_size(cdfem_ctx *ctx, int rule, int *nq_per_elem);
+int cdfem_quadrature_points(cdfem_ctx *ctx, int rule, double *xyz, int where);
+
+/* ---- partial assembly (the hot operator) -----------------------------------------------------
+ * replaces: a.AddDomainIntegrator(new DiffusionIntegrator(kappa))          :336
+ *           a.AddDomainIntegrator(new ConvectionIntegrator(c, alpha))      :337
+ *           a.AddDomainIntegrator(new MassIntegrator(s))                   :338
+ *           a.Assemble()                                                   :339
+ * with MFEM partial-assembly semantics: per-quadrature-point data
+ *   D = W kappa adj(J) adj(J)^T / det J,  C = W alpha adj(J) c,  M = W s det J.
+ * *_q arrays (ne*nq of the OPERATOR rule; conv_q ne*nq*dim) override the constants when
+ * non-NULL (host pointers): a variable Coefficient / VectorCoefficient sampled on the host.     */
+int cdfem_pa_setup(cdfem_ctx *ctx, unsigned kinds, double kappa, const double *kappa_q,
+                   double alpha, const double *conv, const double *conv_q, double mass,
+                   const double *mass_q);
+
+/* replaces: Operator::Mult / BilinearForm::Mult (diffusion_mms.cpp:430) when constrained == 0,
+ * and the ConstrainedOperator built by FormLinearSystem (:349-351) when constrained != 0
+ * (input essential entries treated as 0, output y[ess] = x[ess]).                              */
+int cdfem_pa_mult(cdfem_ctx *ctx, const double *x, double *y, int constrained, int where);
+
+/* replaces: BilinearForm::AssembleDiagonal (PA) — unconstrained operator diagonal.             */
+int cdfem_pa_diagonal(cdfem_ctx *ctx, double *diag, int where);
+
+/* ---- linear form -----------------------------------------------------------------------------
+ * replaces: b.AddDomainIntegrator(new DomainLFIntegrator(f)); b.Assemble()  (:341-343).
+ * f_q: values of f at the CDFEM_RULE_LINEARFORM points (ne * nq, host), output b is an L-vector. */
+int cdfem_lf_assemble(cdfem_ctx *ctx, const double *f_q, double *b, int where);
+
+/* ---- constrained linear system -----------------------------------------------------------------
+ * replaces: a.FormLinearSystem(ess_tdof_list, x, b, A, X, B)  (:349-351), PA/ConstrainedOperator
+ * semantics: X = x,  B = b - A x_e (x_e = x on ess dofs, 0 elsewhere),  B[ess] = x[ess].        */
+int cdfem_form_linear_system(cdfem_ctx *ctx, const double *x, const double *b, double *X,
+                             double *B, int where);
+
+/* ---- Krylov solve ------------------------------------------------------------------------------
+ * replaces: PetscLinearSolver(A).Mult(B, X) (:364-375; Input/petsc.opts: gmres, rtol 1e-10,
+ * atol 1e-12, max_it 500, pc jacobi) and CGSolver (mesh_recession_handler.cpp:270-276).
+ * CG follows MFEM CGSolver (convergence (r,z) <= max(nom0 rel^2, abs^2)); GMRES follows PETSc
+ * KSPGMRES (left PC, classical Gram-Schmidt, restart, ||M^{-1} r|| <= max(rtol ||M^{-1}b||, atol)).
+ * X on input is ignored (zero initial guess, iterative_mode = false), on output the solution.
+ * Returns CDFEM_ERR_NOT_CONVERGED (result filled) when max_iter is reached.                     */
+typedef struct {
+    int method;        /* CDFEM_CG / CDFEM_GMRES */
+    int pc;            /* CDFEM_PC_NONE / CDFEM_PC_JACOBI */
+    int max_iter;
+    int restart;       /* GMRES restart (PETSc default 30) */
+    double rel_tol;
+    double abs_tol;
+    int check_every;   /* host convergence poll interval in iterations (0: default 16) */
+    int print_level;
+} cdfem_solver_params;
+
+typedef struct {
+    int converged;
+    int iterations;
+    double final_norm;
+    double initial_norm;
+    double seconds;    /* wall time of the Krylov loop (device-synchronised) */
+} cdfem_solver_result;
+
+int cdfem_solve(cdfem_ctx *ctx, const cdfem_solver_params *prm, const double *B, double *X,
+                int where, cdfem_solver_result *res);
+
+/* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */
+int cdfem_profile_enable(cdfem_ctx *ctx, int on);
+int cdfem_profile_reset(cdfem_ctx *ctx);
+/* total milliseconds and launch count of kernel id (CDFEM_K_*) since the last reset */
+int cdfem_profile_read(cdfem_ctx *ctx, int kernel, double *total_ms, int64_t *count);
+/* algorithmic bytes moved by one launch of kernel id (see DESIGN.md for the per-unit figures) */
+int cdfem_kernel_bytes(cdfem_ctx *ctx, int kernel, double *bytes);
+
+/* ---- structured mesh helper (host only, no device needed) ---------------------------------------
+ * Box [0,1]^dim into nx*ny(*nz) quads/hexes with the conventions above; rank-slab variant for
+ * the element-partitioned multi-GPU path: elements with iz in [z0, z1) only, dofs renumbered
+ * locally (L-vector of the slab).  Sizes: see cdfem_box_sizes.                                 */
+int cdfem_box_sizes(int dim, int nx, int ny, int nz, int order, int z0, int z1, int *ne,
+                    int64_t *nldofs, int *n_ess);
+int cdfem_box_mesh(int dim, int nx, int ny, int nz, int order, int z0, int z1, double perturb,
+                   double *elem_verts, int32_t *elem_dofs, int32_t *ess_dofs, double *dof_xyz);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CDFEM_H */

@@ -1,0 +1,915 @@
+/*
+ * cdfem_oracle.c — CPU ORACLE (TEST INFRASTRUCTURE ONLY).
+ *
+ * This file is the checker, never the product.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it.  The product path (continuum-mechanics-mfem_amd/)
+ * never links, loads or calls it.
+ *
+ * What it restates: the reference's hot path, i.e. what the convection-diffusion drivers do
+ * through MFEM's *legacy full assembly* on the CPU (Device("cpu"), no SetAssemblyLevel):
+ *
+ *   a.AddDomainIntegrator(new DiffusionIntegrator(kappa));        linear_convection_diffusion_2D.cpp:336
+ *   a.AddDomainIntegrator(new ConvectionIntegrator(c, alpha));     :337  (alpha: linear_convection_diffusion_1D.cpp:396)
+ *   a.AddDomainIntegrator(new MassIntegrator(s));                  :338
+ *   a.Assemble();                                                  :339  -> element matrices -> CSR
+ *   b.AddDomainIntegrator(new DomainLFIntegrator(f)); b.Assemble() :341-343
+ *   u.ProjectBdrCoefficient(exact, ess_bdr)                        :345-347 (nodal interpolation)
+ *   a.FormLinearSystem(ess, u, b, A, X, B)                         :349-351 (row+col elimination, diag 1)
+ *   PetscLinearSolver (KSPGMRES + PCJACOBI, restart 30, left PC)   :364-375, Input/petsc.opts:2-6
+ *   CGSolver semantics (MFEM)                                      mesh_recession_handler.cpp:270-276
+ *   u.ComputeL2Error(exact, irs), order max(2, 2p+3)               :383-390
+ *
+ * MFEM, hypre and PETSc are not vendored in /root/reference and not installed,
+ * so the library-internal semantics below are restated from their documented public behaviour
+ * and marked [MFEM-ext] / [PETSc-ext]:
+ *   - H1_FECollection(p): Gauss-Lobatto nodal Lagrange basis on [0,1]^d, tensor product.     [MFEM-ext]
+ *   - default rules (affine/multilinear tensor elements, Gauss-Legendre, n = order/2 + 1):
+ *       Diffusion  order = 2p + dim - 1                                                     [MFEM-ext]
+ *       Convection order = OrderGrad + p + OrderW = (dim-1) + (p-1) + p + (dim-1)           [MFEM-ext]
+ *         (older MFEM uses Trans.Order() = 1 instead of OrderW: the same n for p=1 2D, p=2,4 3D)
+ *       Mass       order = 2p + OrderW = 2p + dim - 1                                       [MFEM-ext]
+ *       DomainLF   order = 2p                                                               [MFEM-ext]
+ *     -> Diffusion/Convection/Mass share n = p + 1 ... p + 2 points: p=1 quad n=2, p=2 hex n=4,
+ *        p=4 hex n=6 (computed, not assumed, by orc_rule_npts()).
+ *   - element matrix convention elmat(i,j) = a(phi_j, phi_i): row = test function.           [MFEM-ext]
+ *
+ * PARITY PINNING.  The reference holds no golden vectors, no recorded outputs and no tests for this
+ * path, and MFEM cannot be built here.  This oracle is therefore pinned by the
+ * reference's own verification method — manufactured solutions (linear_convection_diffusion_2D.cpp:159-215,
+ * diffusion_mms.cpp:136-178) — turned into asserted known answers in tests/test_oracle.py:
+ * exact reproduction of polynomial solutions in the FE space, O(h^{p+1}) L2 convergence, and
+ * algebraic identities (mass = volume, K*1 = 0, C*1 = 0, symmetry).  Bit-level parity with an
+ * actual MFEM run is UNPINNED (no MFEM in this image).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_API __attribute__((visibility("default")))
+#define ORC_PI 3.14159265358979323846
+
+/* ------------------------------------------------------------------------------------------ */
+/* 1D rules and basis                                                                          */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Legendre P_n(t) and P_n'(t) on [-1,1] by the three-term recurrence. */
+static void legendre(int n, double t, double *P, double *dP)
+{
+    double p0 = 1.0, p1 = t;
+    if (n == 0) { *P = 1.0; *dP = 0.0; return; }
+    for (int k = 2; k <= n; k++) {
+        double pk = ((2.0 * k - 1.0) * t * p1 - (k - 1.0) * p0) / k;
+        p0 = p1; p1 = pk;
+    }
+    *P = p1;
+    *dP = (fabs(1.0 - t * t) > 0.0) ? n * (p0 - t * p1) / (1.0 - t * t) : 0.0;
+}
+
+/* n-point Gauss-Legendre rule on [0,1], nodes ascending, weights sum to 1. */
+ORC_API void orc_gauss_legendre(int n, double *x, double *w)
+{
+    for (int i = 0; i < n; i++) {
+        double t = cos(ORC_PI * (i + 0.75) / (n + 0.5)); /* descending guess */
+        for (int it = 0; it < 100; it++) {
+            double P, dP;
+            legendre(n, t, &P, &dP);
+            double dt = P / dP;
+            t -= dt;
+            if (fabs(dt) < 1e-17) break;
+        }
+        double P, dP;
+        legendre(n, t, &P, &dP);
+        /* map t in [-1,1] (descending in i) to ascending [0,1] */
+        x[i] = 0.5 * (1.0 - t);
+        w[i] = 1.0 / ((1.0 - t * t) * dP * dP);
+    }
+}
+
+/* p+1 Gauss-Lobatto nodes on [0,1]: endpoints and the roots of P_p'. [MFEM-ext BasisType::GaussLobatto] */
+ORC_API void orc_gll_nodes(int p, double *x)
+{
+    x[0] = 0.0;
+    x[p] = 1.0;
+    for (int i = 1; i < p; i++) {
+        double t = -cos(ORC_PI * i / p); /* Chebyshev-Gauss-Lobatto guess, ascending */
+        for (int it = 0; it < 100; it++) {
+            /* f = P_p'(t), f' = P_p''(t) = (2t P_p' - p(p+1) P_p) / (1 - t^2) */
+            double P, dP;
+            legendre(p, t, &P, &dP);
+            double d2P = (2.0 * t * dP - p * (p + 1.0) * P) / (1.0 - t * t);
+            double dt = dP / d2P;
+            t -= dt;
+            if (fabs(dt) < 1e-17) break;
+        }
+        x[i] = 0.5 * (t + 1.0);
+    }
+    /* enforce exact symmetry, as the nodal set is symmetric about 1/2 */
+    for (int i = 0; i <= p / 2; i++) {
+        double a = 0.5 * (x[i] + (1.0 - x[p - i]));
+        x[i] = a;
+        x[p - i] = 1.0 - a;
+    }
+}
+
+/* Lagrange basis through nodes[0..p] and its derivative at xi. */
+ORC_API void orc_lagrange(int p, const double *nodes, double xi, double *phi, double *dphi)
+{
+    for (int j = 0; j <= p; j++) {
+        double v = 1.0, d = 0.0;
+        for (int k = 0; k <= p; k++) {
+            if (k == j) continue;
+            double den = nodes[j] - nodes[k];
+            double f = (xi - nodes[k]) / den;
+            d = d * f + v / den;
+            v *= f;
+        }
+        phi[j] = v;
+        if (dphi) dphi[j] = d;
+    }
+}
+
+/* Number of 1D Gauss-Legendre points of MFEM's default rule for each integrator on a tensor
+ * (quad/hex) element with a multilinear (Q1) geometry.  which: 0 diffusion, 1 convection,
+ * 2 mass, 3 domain LF, 4 L2 error (driver's max(2,2p+3): linear_convection_diffusion_2D.cpp:383). */
+ORC_API int orc_rule_npts(int which, int dim, int p)
+{
+    int order_w = dim - 1;          /* Q1: OrderW = k*dim - 1, k=1          [MFEM-ext] */
+    int order;
+    switch (which) {
+    case 0: order = p + p + dim - 1; break;                 /* DiffusionIntegrator::GetRule  */
+    case 1: order = ((dim - 1) + (p - 1)) + p + order_w; break; /* ConvectionIntegrator::GetRule */
+    case 2: order = p + p + order_w; break;                 /* MassIntegrator::GetRule       */
+    case 3: order = 2 * p; break;                           /* DomainLFIntegrator oa=2, ob=0 */
+    case 4: order = (2 * p + 3 > 2) ? 2 * p + 3 : 2; break; /* driver's error rule           */
+    default: return -1;
+    }
+    return order / 2 + 1;           /* IntRules.Get(Geometry::SQUARE/CUBE, order): GL n=order/2+1 */
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Structured meshes                                                                           */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Deterministic hash in [-1,1) used to perturb interior vertices (non-affine test meshes). */
+static double hash_unit(uint64_t a)
+{
+    a ^= a >> 33; a *= 0xff51afd7ed558ccdULL; a ^= a >> 33; a *= 0xc4ceb9fe1a85ec53ULL; a ^= a >> 33;
+    return (double)(a >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
+/*
+ * Box [0,1]^dim split into nx*ny(*nz) quads/hexes, element e = ix + nx*(iy + ny*iz).
+ * Element vertices in lexicographic local order v = a + 2b (+ 4c), a along x.
+ * H1 order p dofs numbered globally lexicographic on the (p*nx+1) x (p*ny+1) (x (p*nz+1)) lattice
+ * of *reference* GLL positions; local element dof l = dx + (p+1)(dy + (p+1) dz).
+ * perturb > 0 moves interior vertices by perturb*h*hash (a non-affine multilinear mesh).
+ * Boundary attribute convention follows Mesh/unit_square.geo:18-21 (1 bottom, 2 right, 3 top,
+ * 4 left); the hot path marks all boundaries essential (linear_convection_diffusion_2D.cpp:319-322).
+ * Outputs (caller-allocated): verts[NE*nv*dim], dofmap[NE*(p+1)^dim], bdr[NL] (1 on boundary).
+ */
+ORC_API void orc_mesh_box(int dim, int nx, int ny, int nz, int p, double perturb,
+                          double *verts, int *dofmap, int *bdr)
+{
+    if (dim == 2) nz = 1;
+    const int vx = nx + 1, vy = ny + 1;
+    const int nv = (dim == 3) ? 8 : 4;
+    const int d1 = p + 1;
+    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
+    const int Lx = p * nx + 1, Ly = p * ny + 1, Lz = (dim == 3) ? p * nz + 1 : 1;
+    const double hx = 1.0 / nx, hy = 1.0 / ny, hz = 1.0 / nz;
+    const int ne = nx * ny * nz;
+    for (int e = 0; e < ne; e++) {
+        int ix = e % nx, iy = (e / nx) % ny, iz = e / (nx * ny);
+        for (int v = 0; v < nv; v++) {
+            int a = v & 1, b = (v >> 1) & 1, c = (v >> 2) & 1;
+            int gx = ix + a, gy = iy + b, gz = iz + c;
+            double X[3] = {gx * hx, gy * hy, gz * hz};
+            int interior = gx > 0 && gx < nx && gy > 0 && gy < ny && (dim == 2 || (gz > 0 && gz < nz));
+            if (perturb > 0.0 && interior) {
+                uint64_t id = (uint64_t)gx + (uint64_t)vx * ((uint64_t)gy + (uint64_t)vy * gz);
+                X[0] += perturb * hx * hash_unit(3 * id + 0);
+                X[1] += perturb * hy * hash_unit(3 * id + 1);
+                if (dim == 3) X[2] += perturb * hz * hash_unit(3 * id + 2);
+            }
+            for (int k = 0; k < dim; k++) verts[((size_t)e * nv + v) * dim + k] = X[k];
+        }
+        for (int l = 0; l < nd; l++) {
+            int dx = l % d1, dy = (l / d1) % d1, dz = l / (d1 * d1);
+            int gx = p * ix + dx, gy = p * iy + dy, gz = p * iz + dz;
+            dofmap[(size_t)e * nd + l] = gx + Lx * (gy + Ly * gz);
+        }
+    }
+    const int64_t nl = (int64_t)Lx * Ly * Lz;
+    for (int64_t i = 0; i < nl; i++) {
+        int gx = (int)(i % Lx), gy = (int)((i / Lx) % Ly), gz = (int)(i / ((int64_t)Lx * Ly));
+        int on = gx == 0 || gx == Lx - 1 || gy == 0 || gy == Ly - 1;
+        if (dim == 3) on = on || gz == 0 || gz == Lz - 1;
+        bdr[i] = on;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Geometry: multilinear map from the element vertices                                          */
+/* ------------------------------------------------------------------------------------------ */
+
+/* x(xi) and J = dx/dxi at reference point xi for a Q1 element. */
+static void q1_map(int dim, const double *V, const double *xi, double *x, double J[3][3])
+{
+    const int nv = (dim == 3) ? 8 : 4;
+    for (int i = 0; i < dim; i++) {
+        x[i] = 0.0;
+        for (int k = 0; k < dim; k++) J[i][k] = 0.0;
+    }
+    for (int v = 0; v < nv; v++) {
+        int bit[3] = {v & 1, (v >> 1) & 1, (v >> 2) & 1};
+        double f[3], df[3];
+        for (int k = 0; k < dim; k++) {
+            f[k] = bit[k] ? xi[k] : 1.0 - xi[k];
+            df[k] = bit[k] ? 1.0 : -1.0;
+        }
+        double N = 1.0;
+        for (int k = 0; k < dim; k++) N *= f[k];
+        for (int k = 0; k < dim; k++) {
+            double dN = df[k];
+            for (int m = 0; m < dim; m++) if (m != k) dN *= f[m];
+            for (int i = 0; i < dim; i++) J[i][k] += V[v * dim + i] * dN;
+        }
+        for (int i = 0; i < dim; i++) x[i] += V[v * dim + i] * N;
+    }
+}
+
+/* det(J) and adj(J) = det(J) J^{-1}. */
+static double adjugate(int dim, double J[3][3], double A[3][3])
+{
+    if (dim == 2) {
+        A[0][0] = J[1][1]; A[0][1] = -J[0][1];
+        A[1][0] = -J[1][0]; A[1][1] = J[0][0];
+        return J[0][0] * J[1][1] - J[0][1] * J[1][0];
+    }
+    A[0][0] = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+    A[0][1] = J[0][2] * J[2][1] - J[0][1] * J[2][2];
+    A[0][2] = J[0][1] * J[1][2] - J[0][2] * J[1][1];
+    A[1][0] = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+    A[1][1] = J[0][0] * J[2][2] - J[0][2] * J[2][0];
+    A[1][2] = J[0][2] * J[1][0] - J[0][0] * J[1][2];
+    A[2][0] = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+    A[2][1] = J[0][1] * J[2][0] - J[0][0] * J[2][1];
+    A[2][2] = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+    return J[0][0] * A[0][0] + J[0][1] * A[1][0] + J[0][2] * A[2][0];
+}
+
+/* Tensor tables for order p at n Gauss points: B[q*(p+1)+d], G[...], pts, wts. */
+static void tables(int p, int n, double *B, double *G, double *pts, double *wts)
+{
+    double nodes[16];
+    orc_gll_nodes(p, nodes);
+    orc_gauss_legendre(n, pts, wts);
+    for (int q = 0; q < n; q++) orc_lagrange(p, nodes, pts[q], B + q * (p + 1), G + q * (p + 1));
+}
+
+/* Basis values and reference gradients of the nd tensor functions at tensor point (qx,qy,qz). */
+static void tensor_basis(int dim, int p, const double *B, const double *G, const int *qi,
+                         double *phi, double (*gphi)[3])
+{
+    const int d1 = p + 1;
+    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
+    for (int l = 0; l < nd; l++) {
+        int ix = l % d1, iy = (l / d1) % d1, iz = l / (d1 * d1);
+        double bx = B[qi[0] * d1 + ix], gx = G[qi[0] * d1 + ix];
+        double by = B[qi[1] * d1 + iy], gy = G[qi[1] * d1 + iy];
+        if (dim == 2) {
+            phi[l] = bx * by;
+            gphi[l][0] = gx * by; gphi[l][1] = bx * gy; gphi[l][2] = 0.0;
+        } else {
+            double bz = B[qi[2] * d1 + iz], gz = G[qi[2] * d1 + iz];
+            phi[l] = bx * by * bz;
+            gphi[l][0] = gx * by * bz; gphi[l][1] = bx * gy * bz; gphi[l][2] = bx * by * gz;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Full assembly (the reference's legacy FA path)                                              */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct {
+    int64_t n;        /* rows */
+    int64_t nnz;
+    int64_t *rp;      /* row pointer n+1 */
+    int32_t *col;     /* sorted within row */
+    double *val;
+} orc_csr;
+
+/* Coefficients of a(u,v) = kappa (grad u, grad v) + alpha (c . grad u, v) + s (u, v). */
+typedef struct {
+    double kappa, alpha, s, c[3];
+    int use_diff, use_conv, use_mass;
+} orc_coef;
+
+/* Element matrix (row = test, col = trial), nd x nd, for element with vertices V. */
+static void element_matrix(int dim, int p, const double *V, const orc_coef *cf, int nq,
+                           const double *B, const double *G, const double *pts, const double *wts,
+                           double *Ae)
+{
+    const int d1 = p + 1;
+    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
+    double phi[125], gphi[125][3];
+    memset(Ae, 0, sizeof(double) * nd * nd);
+    const int nqz = (dim == 3) ? nq : 1;
+    for (int qz = 0; qz < nqz; qz++)
+    for (int qy = 0; qy < nq; qy++)
+    for (int qx = 0; qx < nq; qx++) {
+        int qi[3] = {qx, qy, qz};
+        double xi[3] = {pts[qx], pts[qy], (dim == 3) ? pts[qz] : 0.0};
+        double W = wts[qx] * wts[qy] * ((dim == 3) ? wts[qz] : 1.0);
+        double x[3], J[3][3], A[3][3];
+        q1_map(dim, V, xi, x, J);
+        double detJ = adjugate(dim, J, A);
+        /* D = W kappa adj adj^T / detJ ; Cv = W alpha adj c ; M = W s detJ   [MFEM-ext PA qdata] */
+        double D[3][3] = {{0}}, Cv[3] = {0}, M = 0.0;
+        if (cf->use_diff)
+            for (int i = 0; i < dim; i++)
+                for (int j = 0; j < dim; j++) {
+                    double acc = 0.0;
+                    for (int k = 0; k < dim; k++) acc += A[i][k] * A[j][k];
+                    D[i][j] = W * cf->kappa * acc / detJ;
+                }
+        if (cf->use_conv)
+            for (int i = 0; i < dim; i++) {
+                double acc = 0.0;
+                for (int k = 0; k < dim; k++) acc += A[i][k] * cf->c[k];
+                Cv[i] = W * cf->alpha * acc;
+            }
+        if (cf->use_mass) M = W * cf->s * detJ;
+        tensor_basis(dim, p, B, G, qi, phi, gphi);
+        for (int j = 0; j < nd; j++) {
+            double Dg[3] = {0, 0, 0};
+            for (int a = 0; a < dim; a++)
+                for (int b = 0; b < dim; b++) Dg[a] += D[a][b] * gphi[j][b];
+            double cg = 0.0;
+            for (int a = 0; a < dim; a++) cg += Cv[a] * gphi[j][a];
+            double rest = cg + M * phi[j];
+            for (int i = 0; i < nd; i++) {
+                double v = phi[i] * rest;
+                for (int a = 0; a < dim; a++) v += gphi[i][a] * Dg[a];
+                Ae[i * nd + j] += v;
+            }
+        }
+    }
+}
+
+/* Build the CSR matrix sum_e A_e (ParBilinearForm::Assemble + Finalize, SpMat form). */
+ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, const int *dofmap,
+                                 int64_t nl, double kappa, double alpha, double s, const double *c,
+                                 int kinds)
+{
+    const int d1 = p + 1;
+    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
+    const int nv = (dim == 3) ? 8 : 4;
+    orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
+                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0};
+    /* one shared rule: Diffusion/Convection/Mass coincide on Q1 tensor elements (checked) */
+    int nq = orc_rule_npts(0, dim, p);
+    if (orc_rule_npts(1, dim, p) != nq || orc_rule_npts(2, dim, p) != nq) return NULL;
+    double B[64], G[64], pts[8], wts[8];
+    tables(p, nq, B, G, pts, wts);
+
+    double *Ae = (double *)malloc(sizeof(double) * (size_t)ne * nd * nd);
+    #pragma omp parallel for schedule(static)
+    for (int e = 0; e < ne; e++)
+        element_matrix(dim, p, verts + (size_t)e * nv * dim, &cf, nq, B, G, pts, wts,
+                       Ae + (size_t)e * nd * nd);
+
+    /* dof -> (element, local) transpose, element order ascending (deterministic accumulation) */
+    int64_t *cnt = (int64_t *)calloc(nl + 1, sizeof(int64_t));
+    for (int64_t k = 0; k < (int64_t)ne * nd; k++) cnt[dofmap[k] + 1]++;
+    for (int64_t i = 0; i < nl; i++) cnt[i + 1] += cnt[i];
+    int64_t *fill = (int64_t *)malloc(sizeof(int64_t) * nl);
+    memcpy(fill, cnt, sizeof(int64_t) * nl);
+    int64_t *el = (int64_t *)malloc(sizeof(int64_t) * (size_t)ne * nd);
+    for (int64_t k = 0; k < (int64_t)ne * nd; k++) el[fill[dofmap[k]]++] = k; /* k = e*nd + l */
+    free(fill);
+
+    orc_csr *A = (orc_csr *)calloc(1, sizeof(orc_csr));
+    A->n = nl;
+    A->rp = (int64_t *)calloc(nl + 1, sizeof(int64_t));
+    const int maxc = (1 << dim) * nd;
+    /* pass 1: row lengths */
+    #pragma omp parallel
+    {
+        int *buf = (int *)malloc(sizeof(int) * maxc * 2);
+        #pragma omp for schedule(dynamic, 256)
+        for (int64_t i = 0; i < nl; i++) {
+            int m = 0;
+            for (int64_t k = cnt[i]; k < cnt[i + 1]; k++) {
+                int64_t e = el[k] / nd;
+                for (int l = 0; l < nd; l++) buf[m++] = dofmap[e * nd + l];
+            }
+            /* insertion sort + unique (m <= 8*125) */
+            for (int a = 1; a < m; a++) {
+                int v = buf[a], b = a - 1;
+                while (b >= 0 && buf[b] > v) { buf[b + 1] = buf[b]; b--; }
+                buf[b + 1] = v;
+            }
+            int u = 0;
+            for (int a = 0; a < m; a++) if (a == 0 || buf[a] != buf[a - 1]) u++;
+            A->rp[i + 1] = u;
+        }
+        free(buf);
+    }
+    for (int64_t i = 0; i < nl; i++) A->rp[i + 1] += A->rp[i];
+    A->nnz = A->rp[nl];
+    A->col = (int32_t *)malloc(sizeof(int32_t) * A->nnz);
+    A->val = (double *)calloc(A->nnz, sizeof(double));
+    /* pass 2: columns and values */
+    #pragma omp parallel
+    {
+        int *buf = (int *)malloc(sizeof(int) * maxc * 2);
+        #pragma omp for schedule(dynamic, 256)
+        for (int64_t i = 0; i < nl; i++) {
+            int m = 0;
+            for (int64_t k = cnt[i]; k < cnt[i + 1]; k++) {
+                int64_t e = el[k] / nd;
+                for (int l = 0; l < nd; l++) buf[m++] = dofmap[e * nd + l];
+            }
+            for (int a = 1; a < m; a++) {
+                int v = buf[a], b = a - 1;
+                while (b >= 0 && buf[b] > v) { buf[b + 1] = buf[b]; b--; }
+                buf[b + 1] = v;
+            }
+            int64_t base = A->rp[i], u = 0;
+            for (int a = 0; a < m; a++) if (a == 0 || buf[a] != buf[a - 1]) A->col[base + u++] = buf[a];
+            for (int64_t k = cnt[i]; k < cnt[i + 1]; k++) {
+                int64_t e = el[k] / nd;
+                int li = (int)(el[k] % nd);
+                const double *row = Ae + (size_t)e * nd * nd + (size_t)li * nd;
+                for (int l = 0; l < nd; l++) {
+                    int cj = dofmap[e * nd + l];
+                    int64_t lo = base, hi = base + u - 1;
+                    while (lo < hi) {
+                        int64_t mid = (lo + hi) >> 1;
+                        if (A->col[mid] < cj) lo = mid + 1; else hi = mid;
+                    }
+                    A->val[lo] += row[l];
+                }
+            }
+        }
+        free(buf);
+    }
+    free(cnt); free(el); free(Ae);
+    return A;
+}
+
+ORC_API void orc_csr_free(orc_csr *A)
+{
+    if (!A) return;
+    free(A->rp); free(A->col); free(A->val); free(A);
+}
+ORC_API int64_t orc_csr_n(const orc_csr *A) { return A->n; }
+ORC_API int64_t orc_csr_nnz(const orc_csr *A) { return A->nnz; }
+ORC_API void orc_csr_export(const orc_csr *A, int64_t *rp, int32_t *col, double *val)
+{
+    memcpy(rp, A->rp, sizeof(int64_t) * (A->n + 1));
+    memcpy(col, A->col, sizeof(int32_t) * A->nnz);
+    memcpy(val, A->val, sizeof(double) * A->nnz);
+}
+
+ORC_API void orc_csr_spmv(const orc_csr *A, const double *x, double *y)
+{
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < A->n; i++) {
+        double acc = 0.0;
+        for (int64_t k = A->rp[i]; k < A->rp[i + 1]; k++) acc += A->val[k] * x[A->col[k]];
+        y[i] = acc;
+    }
+}
+
+/*
+ * FormLinearSystem (FA, single rank so P = I):  eliminate essential rows AND columns, diagonal 1,
+ *   B = b - A_e X,  B[ess] = X[ess]                                 [MFEM-ext, DIAG_ONE policy]
+ * Returns a new matrix; A is not modified.  ess_marker[i] != 0 marks essential dof i.
+ */
+ORC_API orc_csr *orc_form_linear_system(const orc_csr *A, const int *ess_marker, const double *X,
+                                        const double *b, double *B)
+{
+    orc_csr *Ac = (orc_csr *)calloc(1, sizeof(orc_csr));
+    Ac->n = A->n; Ac->nnz = A->nnz;
+    Ac->rp = (int64_t *)malloc(sizeof(int64_t) * (A->n + 1));
+    Ac->col = (int32_t *)malloc(sizeof(int32_t) * A->nnz);
+    Ac->val = (double *)malloc(sizeof(double) * A->nnz);
+    memcpy(Ac->rp, A->rp, sizeof(int64_t) * (A->n + 1));
+    memcpy(Ac->col, A->col, sizeof(int32_t) * A->nnz);
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < A->n; i++) {
+        if (ess_marker[i]) {
+            for (int64_t k = A->rp[i]; k < A->rp[i + 1]; k++)
+                Ac->val[k] = (A->col[k] == i) ? 1.0 : 0.0;
+            B[i] = X[i];
+        } else {
+            double bi = b[i];
+            for (int64_t k = A->rp[i]; k < A->rp[i + 1]; k++) {
+                int j = A->col[k];
+                if (ess_marker[j]) { bi -= A->val[k] * X[j]; Ac->val[k] = 0.0; }
+                else Ac->val[k] = A->val[k];
+            }
+            B[i] = bi;
+        }
+    }
+    return Ac;
+}
+
+ORC_API void orc_csr_diag(const orc_csr *A, double *d)
+{
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < A->n; i++) {
+        d[i] = 0.0;
+        for (int64_t k = A->rp[i]; k < A->rp[i + 1]; k++) if (A->col[k] == i) d[i] = A->val[k];
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Krylov solvers                                                                              */
+/* ------------------------------------------------------------------------------------------ */
+
+static double dot(int64_t n, const double *a, const double *b)
+{
+    double s = 0.0;
+    #pragma omp parallel for reduction(+ : s) schedule(static)
+    for (int64_t i = 0; i < n; i++) s += a[i] * b[i];
+    return s;
+}
+
+/*
+ * MFEM CGSolver::Mult semantics (iterative_mode = false), optional Jacobi preconditioner
+ * z = dinv .* r (OperatorJacobiSmoother / HypreDiagScale).  Convergence when
+ * (r, z) <= max(nom0 * rel_tol^2, abs_tol^2).  Pinned by use: mesh_recession_handler.cpp:270-276.
+ * Returns 1 if converged; *iters = final_iter, *final_norm = sqrt(betanom).
+ */
+ORC_API int orc_cg(const orc_csr *A, const double *dinv, const double *b, double *x, double rel_tol,
+                   double abs_tol, int max_iter, int *iters, double *final_norm)
+{
+    const int64_t n = A->n;
+    double *r = (double *)malloc(sizeof(double) * n), *d = (double *)malloc(sizeof(double) * n);
+    double *z = (double *)malloc(sizeof(double) * n);
+    memcpy(r, b, sizeof(double) * n);
+    memset(x, 0, sizeof(double) * n);
+    if (dinv) { for (int64_t i = 0; i < n; i++) z[i] = dinv[i] * r[i]; memcpy(d, z, sizeof(double) * n); }
+    else memcpy(d, r, sizeof(double) * n);
+    double nom = dot(n, d, r);
+    const double r0 = fmax(nom * rel_tol * rel_tol, abs_tol * abs_tol);
+    int converged = 0;
+    double betanom = nom;
+    *iters = 0;
+    if (nom <= r0) { *final_norm = sqrt(nom); free(r); free(d); free(z); return 1; }
+    orc_csr_spmv(A, d, z);
+    double den = dot(n, z, d);
+    if (den == 0.0) { *final_norm = sqrt(nom); free(r); free(d); free(z); return 0; }
+    int final_iter = max_iter;
+    for (int i = 1;;) {
+        double alpha = nom / den;
+        #pragma omp parallel for schedule(static)
+        for (int64_t k = 0; k < n; k++) { x[k] += alpha * d[k]; r[k] -= alpha * z[k]; }
+        if (dinv) {
+            #pragma omp parallel for schedule(static)
+            for (int64_t k = 0; k < n; k++) z[k] = dinv[k] * r[k];
+            betanom = dot(n, r, z);
+        } else betanom = dot(n, r, r);
+        if (betanom <= r0) { converged = 1; final_iter = i; break; }
+        if (++i > max_iter) break;
+        double beta = betanom / nom;
+        const double *src = dinv ? z : r;
+        #pragma omp parallel for schedule(static)
+        for (int64_t k = 0; k < n; k++) d[k] = src[k] + beta * d[k];
+        orc_csr_spmv(A, d, z);
+        den = dot(n, d, z);
+        if (den == 0.0) { final_iter = i; break; }
+        nom = betanom;
+    }
+    *iters = final_iter;
+    *final_norm = sqrt(fabs(betanom));
+    free(r); free(d); free(z);
+    return converged;
+}
+
+/*
+ * PETSc KSPGMRES semantics [PETSc-ext]: restarted GMRES(m), LEFT preconditioning (Jacobi when
+ * dinv != NULL), classical Gram-Schmidt without refinement, Givens-rotation residual estimate,
+ * zero initial guess, KSPConvergedDefault on the preconditioned residual norm:
+ * converged when rnorm <= max(rtol * rnorm0, atol).  Input/petsc.opts:2-6.
+ */
+ORC_API int orc_gmres(const orc_csr *A, const double *dinv, const double *b, double *x, int m,
+                      double rtol, double atol, int max_it, int *iters, double *final_norm)
+{
+    const int64_t n = A->n;
+    double *V = (double *)malloc(sizeof(double) * n * (m + 1));
+    double *w = (double *)malloc(sizeof(double) * n);
+    double *H = (double *)calloc((size_t)(m + 1) * m, sizeof(double));
+    double *cs = (double *)malloc(sizeof(double) * m), *sn = (double *)malloc(sizeof(double) * m);
+    double *g = (double *)malloc(sizeof(double) * (m + 1)), *y = (double *)malloc(sizeof(double) * m);
+    memset(x, 0, sizeof(double) * n);
+    int its = 0, converged = 0, first = 1;
+    double ttol = 0.0, res = 0.0;
+    for (;;) {
+        /* preconditioned initial residual of this cycle: V0 = M^{-1}(b - A x) */
+        orc_csr_spmv(A, x, w);
+        for (int64_t i = 0; i < n; i++) {
+            double r = b[i] - w[i];
+            V[i] = dinv ? dinv[i] * r : r;
+        }
+        double beta = sqrt(dot(n, V, V));
+        res = beta;
+        if (first) { ttol = fmax(rtol * beta, atol); first = 0; }
+        if (beta <= ttol || beta == 0.0) { converged = 1; break; }
+        if (its >= max_it) break;
+        for (int64_t i = 0; i < n; i++) V[i] /= beta;
+        for (int i = 0; i <= m; i++) g[i] = 0.0;
+        g[0] = beta;
+        int j, kk = 0;
+        for (j = 0; j < m && its < max_it; j++) {
+            its++;
+            double *vj = V + (size_t)j * n, *vn = V + (size_t)(j + 1) * n;
+            orc_csr_spmv(A, vj, w);
+            if (dinv) for (int64_t i = 0; i < n; i++) w[i] *= dinv[i];
+            /* classical Gram-Schmidt: all projections from the same w */
+            for (int i = 0; i <= j; i++) H[i * m + j] = dot(n, w, V + (size_t)i * n);
+            for (int i = 0; i <= j; i++) {
+                const double h = H[i * m + j], *vi = V + (size_t)i * n;
+                for (int64_t k = 0; k < n; k++) w[k] -= h * vi[k];
+            }
+            double hn = sqrt(dot(n, w, w));
+            H[(j + 1) * m + j] = hn;
+            for (int i = 0; i < j; i++) {
+                double a = H[i * m + j], c2 = H[(i + 1) * m + j];
+                H[i * m + j] = cs[i] * a + sn[i] * c2;
+                H[(i + 1) * m + j] = -sn[i] * a + cs[i] * c2;
+            }
+            double a = H[j * m + j], c2 = H[(j + 1) * m + j];
+            double rr = sqrt(a * a + c2 * c2);
+            cs[j] = (rr == 0.0) ? 1.0 : a / rr;
+            sn[j] = (rr == 0.0) ? 0.0 : c2 / rr;
+            H[j * m + j] = rr;
+            H[(j + 1) * m + j] = 0.0;
+            g[j + 1] = -sn[j] * g[j];
+            g[j] = cs[j] * g[j];
+            res = fabs(g[j + 1]);
+            kk = j + 1;
+            if (hn == 0.0) break;                      /* happy breakdown */
+            for (int64_t k = 0; k < n; k++) vn[k] = w[k] / hn;
+            if (res <= ttol) break;
+        }
+        /* x += V_k y_k with H_k y_k = g_k (upper triangular) */
+        for (int i = kk - 1; i >= 0; i--) {
+            double acc = g[i];
+            for (int l = i + 1; l < kk; l++) acc -= H[i * m + l] * y[l];
+            y[i] = acc / H[i * m + i];
+        }
+        for (int i = 0; i < kk; i++) {
+            const double *vi = V + (size_t)i * n;
+            for (int64_t k = 0; k < n; k++) x[k] += y[i] * vi[k];
+        }
+        if (res <= ttol) { converged = 1; break; }
+        if (its >= max_it) break;
+    }
+    *iters = its;
+    *final_norm = res;
+    free(V); free(w); free(H); free(cs); free(sn); free(g); free(y);
+    return converged;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Manufactured solutions, RHS assembly, projection, L2 error                                  */
+/* ------------------------------------------------------------------------------------------ */
+
+/*
+ * prm[0] = kind:
+ *   1: u = sin(n pi x) sin(m pi y) [sin(l pi z)]; f = -kappa Lap u + alpha c.grad u + s u
+ *      (linear_convection_diffusion_2D.cpp:159-215; z factor is the 3D extension)
+ *   2: u = prod_d g(x_d), g(t) = sum_k a_k t^k, degree p: in the FE space -> exact Galerkin
+ *   3: u = sin(t) cos(2(x-.5)^2 + 2(y-.5)^2), f = u_t - alpha Lap u   (diffusion_mms.cpp:136-178)
+ * prm: [kind, kappa, s, alpha, c0, c1, c2, n, m, l, t, p, dim]
+ */
+static void poly1d(int p, double t, double *g, double *dg, double *d2g)
+{
+    /* fixed, non-symmetric coefficients: a_k = (k + 1) / (k + 2) * (-1)^k + 0.25 */
+    *g = 0; *dg = 0; *d2g = 0;
+    for (int k = 0; k <= p; k++) {
+        double a = (k + 1.0) / (k + 2.0) * ((k & 1) ? -1.0 : 1.0) + 0.25;
+        *g += a * pow(t, k);
+        if (k >= 1) *dg += a * k * pow(t, k - 1);
+        if (k >= 2) *d2g += a * k * (k - 1) * pow(t, k - 2);
+    }
+}
+
+ORC_API double orc_mms_u(const double *prm, const double *x)
+{
+    int kind = (int)prm[0], dim = (int)prm[12];
+    if (kind == 1) {
+        double u = sin(prm[7] * ORC_PI * x[0]) * sin(prm[8] * ORC_PI * x[1]);
+        if (dim == 3) u *= sin(prm[9] * ORC_PI * x[2]);
+        return u;
+    }
+    if (kind == 2) {
+        double u = 1.0, g, dg, d2g;
+        for (int d = 0; d < dim; d++) { poly1d((int)prm[11], x[d], &g, &dg, &d2g); u *= g; }
+        return u;
+    }
+    if (kind == 3) {
+        double dx = x[0] - 0.5, dy = x[1] - 0.5;
+        return sin(prm[10]) * cos(2.0 * dx * dx + 2.0 * dy * dy);
+    }
+    return 0.0;
+}
+
+ORC_API double orc_mms_f(const double *prm, const double *x)
+{
+    int kind = (int)prm[0], dim = (int)prm[12];
+    double kappa = prm[1], s = prm[2], alpha = prm[3];
+    const double *c = prm + 4;
+    if (kind == 1) {
+        double k[3] = {prm[7] * ORC_PI, prm[8] * ORC_PI, prm[9] * ORC_PI};
+        double sv[3], cv[3];
+        for (int d = 0; d < 3; d++) { sv[d] = sin(k[d] * x[d]); cv[d] = cos(k[d] * x[d]); }
+        if (dim == 2) {
+            /* linear_convection_diffusion_2D.cpp:198-205 (alpha = 1 there) */
+            double diff = kappa * (k[0] * k[0] + k[1] * k[1]) * sv[0] * sv[1];
+            double conv = c[0] * k[0] * cv[0] * sv[1] + c[1] * k[1] * sv[0] * cv[1];
+            return diff + alpha * conv + s * sv[0] * sv[1];
+        }
+        double u = sv[0] * sv[1] * sv[2];
+        double diff = kappa * (k[0] * k[0] + k[1] * k[1] + k[2] * k[2]) * u;
+        double conv = c[0] * k[0] * cv[0] * sv[1] * sv[2] + c[1] * k[1] * sv[0] * cv[1] * sv[2]
+                    + c[2] * k[2] * sv[0] * sv[1] * cv[2];
+        return diff + alpha * conv + s * u;
+    }
+    if (kind == 2) {
+        double g[3], dg[3], d2g[3];
+        for (int d = 0; d < dim; d++) poly1d((int)prm[11], x[d], &g[d], &dg[d], &d2g[d]);
+        double u = 1, lap = 0, cg = 0;
+        for (int d = 0; d < dim; d++) u *= g[d];
+        for (int d = 0; d < dim; d++) {
+            double t2 = d2g[d], t1 = dg[d];
+            for (int e = 0; e < dim; e++) if (e != d) { t2 *= g[e]; t1 *= g[e]; }
+            lap += t2; cg += c[d] * t1;
+        }
+        return -kappa * lap + alpha * cg + s * u;
+    }
+    if (kind == 3) {
+        double t = prm[10], dx = x[0] - 0.5, dy = x[1] - 0.5;
+        double r2 = dx * dx + dy * dy, q = 2.0 * r2;
+        double ut = cos(t) * cos(q);
+        double lap = sin(t) * (-16.0 * r2 * cos(q) - 8.0 * sin(q));
+        return ut - alpha * lap;
+    }
+    return 0.0;
+}
+
+/* b_i = sum_e sum_q W detJ f(x_q) phi_i(xi_q), DomainLFIntegrator default order 2p. */
+ORC_API void orc_lf_assemble(int dim, int p, int ne, const double *verts, const int *dofmap,
+                             int64_t nl, const double *prm, double *b)
+{
+    const int d1 = p + 1;
+    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
+    const int nv = (dim == 3) ? 8 : 4;
+    const int nq = orc_rule_npts(3, dim, p);
+    double B[64], G[64], pts[8], wts[8];
+    tables(p, nq, B, G, pts, wts);
+    double *be = (double *)malloc(sizeof(double) * (size_t)ne * nd);
+    #pragma omp parallel for schedule(static)
+    for (int e = 0; e < ne; e++) {
+        double phi[125], gphi[125][3];
+        double *out = be + (size_t)e * nd;
+        for (int l = 0; l < nd; l++) out[l] = 0.0;
+        const int nqz = (dim == 3) ? nq : 1;
+        for (int qz = 0; qz < nqz; qz++)
+        for (int qy = 0; qy < nq; qy++)
+        for (int qx = 0; qx < nq; qx++) {
+            int qi[3] = {qx, qy, qz};
+            double xi[3] = {pts[qx], pts[qy], (dim == 3) ? pts[qz] : 0.0};
+            double W = wts[qx] * wts[qy] * ((dim == 3) ? wts[qz] : 1.0);
+            double x[3], J[3][3], A[3][3];
+            q1_map(dim, verts + (size_t)e * nv * dim, xi, x, J);
+            double detJ = adjugate(dim, J, A);
+            double fw = W * detJ * orc_mms_f(prm, x);
+            tensor_basis(dim, p, B, G, qi, phi, gphi);
+            for (int l = 0; l < nd; l++) out[l] += fw * phi[l];
+        }
+    }
+    memset(b, 0, sizeof(double) * nl);
+    for (int64_t k = 0; k < (int64_t)ne * nd; k++) b[dofmap[k]] += be[k];
+    free(be);
+}
+
+/* Physical coordinates of every L-dof (GLL node images); used for nodal projection. */
+ORC_API void orc_dof_coords(int dim, int p, int ne, const double *verts, const int *dofmap,
+                            double *xyz)
+{
+    const int d1 = p + 1;
+    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
+    const int nv = (dim == 3) ? 8 : 4;
+    double nodes[16];
+    orc_gll_nodes(p, nodes);
+    #pragma omp parallel for schedule(static)
+    for (int e = 0; e < ne; e++)
+        for (int l = 0; l < nd; l++) {
+            double xi[3] = {nodes[l % d1], nodes[(l / d1) % d1], (dim == 3) ? nodes[l / (d1 * d1)] : 0};
+            double x[3], J[3][3];
+            q1_map(dim, verts + (size_t)e * nv * dim, xi, x, J);
+            for (int k = 0; k < dim; k++) xyz[(size_t)dofmap[(size_t)e * nd + l] * dim + k] = x[k];
+        }
+}
+
+/* ||u_h - u||_{L2} with the driver's rule order max(2, 2p+3)  (linear_convection_diffusion_2D.cpp:383-390). */
+ORC_API double orc_l2_error(int dim, int p, int ne, const double *verts, const int *dofmap,
+                            const double *u, const double *prm, int exact_zero)
+{
+    const int d1 = p + 1;
+    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
+    const int nv = (dim == 3) ? 8 : 4;
+    const int nq = orc_rule_npts(4, dim, p);
+    double B[64], G[64], pts[8], wts[8];
+    tables(p, nq, B, G, pts, wts);
+    double err = 0.0;
+    #pragma omp parallel for reduction(+ : err) schedule(static)
+    for (int e = 0; e < ne; e++) {
+        double phi[125], gphi[125][3];
+        const int nqz = (dim == 3) ? nq : 1;
+        for (int qz = 0; qz < nqz; qz++)
+        for (int qy = 0; qy < nq; qy++)
+        for (int qx = 0; qx < nq; qx++) {
+            int qi[3] = {qx, qy, qz};
+            double xi[3] = {pts[qx], pts[qy], (dim == 3) ? pts[qz] : 0.0};
+            double W = wts[qx] * wts[qy] * ((dim == 3) ? wts[qz] : 1.0);
+            double x[3], J[3][3], A[3][3];
+            q1_map(dim, verts + (size_t)e * nv * dim, xi, x, J);
+            double detJ = adjugate(dim, J, A);
+            tensor_basis(dim, p, B, G, qi, phi, gphi);
+            double uh = 0.0;
+            for (int l = 0; l < nd; l++) uh += u[dofmap[(size_t)e * nd + l]] * phi[l];
+            double ex = exact_zero ? 0.0 : orc_mms_u(prm, x);
+            err += W * detJ * (uh - ex) * (uh - ex);
+        }
+    }
+    return sqrt(err);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* CPU element-by-element apply (matrix-free, no CSR; independent of the GPU algorithm)          */
+/* ------------------------------------------------------------------------------------------ */
+
+/*
+ * qdata per quadrature point (element-major, q lexicographic qx fastest), 10 (3D) / 6 (2D) comps:
+ *   D (sym, row-major upper: 00 01 02 11 12 22 | 2D: 00 01 11), Cv (dim), M (1)
+ *   D = W kappa adj(J) adj(J)^T / detJ, Cv = W alpha adj(J) c, M = W s detJ     [MFEM-ext PA]
+ * y = A x computed element by element with the full tensor basis (no sum factorization:
+ * the CPU check must not share the GPU kernel's algorithm).
+ */
+ORC_API void orc_ebe_mult(int dim, int p, int ne, const double *verts, const int *dofmap,
+                         int64_t nl, double kappa, double alpha, double s, const double *c,
+                         int kinds, const double *x, double *y)
+{
+    const int d1 = p + 1;
+    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
+    const int nv = (dim == 3) ? 8 : 4;
+    const int nq = orc_rule_npts(0, dim, p);
+    orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
+                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0};
+    double B[64], G[64], pts[8], wts[8];
+    tables(p, nq, B, G, pts, wts);
+    double *ye = (double *)malloc(sizeof(double) * (size_t)ne * nd);
+    #pragma omp parallel for schedule(static)
+    for (int e = 0; e < ne; e++) {
+        double Ae[125 * 125];
+        double *out = ye + (size_t)e * nd;
+        element_matrix(dim, p, verts + (size_t)e * nv * dim, &cf, nq, B, G, pts, wts, Ae);
+        for (int i = 0; i < nd; i++) {
+            double acc = 0.0;
+            for (int j = 0; j < nd; j++) acc += Ae[i * nd + j] * x[dofmap[(size_t)e * nd + j]];
+            out[i] = acc;
+        }
+    }
+    memset(y, 0, sizeof(double) * nl);
+    for (int64_t k = 0; k < (int64_t)ne * nd; k++) y[dofmap[k]] += ye[k];
+    free(ye);
+}
+
+ORC_API int orc_num_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+ORC_API void orc_set_num_threads(int n)
+{
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}

@@ -1,0 +1,287 @@
+"""CPU oracle bindings — TEST INFRASTRUCTURE ONLY.
+
+Thin ctypes/numpy wrapper over ``oracle/_build/liborc.so`` (built from ``oracle/cdfem_oracle.c``).
+Only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of ``bench.py`` import this
+module, and only as the checker.  The product (``continuum-mechanics-mfem_amd/``) never imports it.
+
+See the header of ``cdfem_oracle.c`` for what is restated from the reference and how the oracle is
+pinned (manufactured-solution known answers; bit parity with an MFEM run is unpinned).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liborc.so")
+
+DIFFUSION, CONVECTION, MASS = 1, 2, 4
+RULE_DIFFUSION, RULE_CONVECTION, RULE_MASS, RULE_LF, RULE_L2 = 0, 1, 2, 3, 4
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH) or (
+        os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "cdfem_oracle.c"))
+    ):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB_PATH)
+        dp, ip, lp = C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int64)
+        L.orc_gauss_legendre.argtypes = [C.c_int, dp, dp]
+        L.orc_gll_nodes.argtypes = [C.c_int, dp]
+        L.orc_lagrange.argtypes = [C.c_int, dp, C.c_double, dp, dp]
+        L.orc_rule_npts.argtypes = [C.c_int, C.c_int, C.c_int]
+        L.orc_mesh_box.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, dp, ip, ip]
+        L.orc_fa_assemble.restype = C.c_void_p
+        L.orc_fa_assemble.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, C.c_int64, C.c_double,
+                                      C.c_double, C.c_double, dp, C.c_int]
+        L.orc_csr_free.argtypes = [C.c_void_p]
+        L.orc_csr_n.argtypes = [C.c_void_p]
+        L.orc_csr_n.restype = C.c_int64
+        L.orc_csr_nnz.argtypes = [C.c_void_p]
+        L.orc_csr_nnz.restype = C.c_int64
+        L.orc_csr_export.argtypes = [C.c_void_p, lp, C.POINTER(C.c_int32), dp]
+        L.orc_csr_spmv.argtypes = [C.c_void_p, dp, dp]
+        L.orc_form_linear_system.restype = C.c_void_p
+        L.orc_form_linear_system.argtypes = [C.c_void_p, ip, dp, dp, dp]
+        L.orc_csr_diag.argtypes = [C.c_void_p, dp]
+        L.orc_cg.argtypes = [C.c_void_p, dp, dp, dp, C.c_double, C.c_double, C.c_int, ip, dp]
+        L.orc_gmres.argtypes = [C.c_void_p, dp, dp, dp, C.c_int, C.c_double, C.c_double, C.c_int, ip, dp]
+        L.orc_mms_u.argtypes = [dp, dp]
+        L.orc_mms_u.restype = C.c_double
+        L.orc_mms_f.argtypes = [dp, dp]
+        L.orc_mms_f.restype = C.c_double
+        L.orc_lf_assemble.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, C.c_int64, dp, dp]
+        L.orc_dof_coords.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, dp]
+        L.orc_l2_error.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, dp, dp, C.c_int]
+        L.orc_l2_error.restype = C.c_double
+        L.orc_ebe_mult.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, C.c_int64, C.c_double,
+                                   C.c_double, C.c_double, dp, C.c_int, dp, dp]
+        L.orc_num_threads.restype = C.c_int
+        L.orc_set_num_threads.argtypes = [C.c_int]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _i(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+def gauss_legendre(n):
+    x, w = np.zeros(n), np.zeros(n)
+    lib().orc_gauss_legendre(n, _d(x), _d(w))
+    return x, w
+
+
+def gll_nodes(p):
+    x = np.zeros(p + 1)
+    lib().orc_gll_nodes(p, _d(x))
+    return x
+
+
+def basis_tables(p, n):
+    """B[q, d] = phi_d(xi_q), G[q, d] = phi_d'(xi_q) at n Gauss points on [0,1]."""
+    nodes = gll_nodes(p)
+    pts, _ = gauss_legendre(n)
+    B, G = np.zeros((n, p + 1)), np.zeros((n, p + 1))
+    for q in range(n):
+        phi, dphi = np.zeros(p + 1), np.zeros(p + 1)
+        lib().orc_lagrange(p, _d(nodes), float(pts[q]), _d(phi), _d(dphi))
+        B[q], G[q] = phi, dphi
+    return B, G
+
+
+def rule_npts(which, dim, p):
+    return lib().orc_rule_npts(which, dim, p)
+
+
+class BoxMesh:
+    """Structured [0,1]^dim box mesh (see orc_mesh_box for numbering conventions)."""
+
+    def __init__(self, dim, n, p, perturb=0.0):
+        nx, ny, nz = (n, n, n) if np.isscalar(n) else tuple(n) + ((1,) if len(n) == 2 else ())
+        if dim == 2:
+            nz = 1
+        self.dim, self.p, self.n = dim, p, (nx, ny, nz)
+        self.ne = nx * ny * nz
+        self.nv = 8 if dim == 3 else 4
+        self.nd = (p + 1) ** dim
+        self.nl = (p * nx + 1) * (p * ny + 1) * ((p * nz + 1) if dim == 3 else 1)
+        self.verts = np.zeros((self.ne, self.nv, dim))
+        self.dofmap = np.zeros((self.ne, self.nd), dtype=np.int32)
+        self.bdr = np.zeros(self.nl, dtype=np.int32)
+        lib().orc_mesh_box(dim, nx, ny, nz, p, float(perturb), _d(self.verts), _i(self.dofmap),
+                           _i(self.bdr))
+        self.ess = np.nonzero(self.bdr)[0].astype(np.int32)
+
+    def dof_coords(self):
+        xyz = np.zeros((self.nl, self.dim))
+        lib().orc_dof_coords(self.dim, self.p, self.ne, _d(self.verts), _i(self.dofmap), _d(xyz))
+        return xyz
+
+
+class CSR:
+    def __init__(self, handle):
+        self.h = handle
+        L = lib()
+        self.n, self.nnz = L.orc_csr_n(handle), L.orc_csr_nnz(handle)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_csr_free(self.h)
+            self.h = None
+
+    def export(self):
+        rp = np.zeros(self.n + 1, dtype=np.int64)
+        col = np.zeros(self.nnz, dtype=np.int32)
+        val = np.zeros(self.nnz)
+        lib().orc_csr_export(self.h, rp.ctypes.data_as(C.POINTER(C.c_int64)),
+                             col.ctypes.data_as(C.POINTER(C.c_int32)), _d(val))
+        return rp, col, val
+
+    def to_scipy(self):
+        import scipy.sparse as sp
+        rp, col, val = self.export()
+        return sp.csr_matrix((val, col, rp), shape=(self.n, self.n))
+
+    def mult(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros(self.n)
+        lib().orc_csr_spmv(self.h, _d(x), _d(y))
+        return y
+
+    def diag(self):
+        d = np.zeros(self.n)
+        lib().orc_csr_diag(self.h, _d(d))
+        return d
+
+
+def _conv(c, dim):
+    cc = np.zeros(3)
+    if c is not None:
+        cc[: len(c)] = c
+    return cc
+
+
+def fa_assemble(mesh: BoxMesh, kappa=1.0, alpha=1.0, s=1.0, c=None, kinds=DIFFUSION | CONVECTION | MASS):
+    cc = _conv(c, mesh.dim)
+    h = lib().orc_fa_assemble(mesh.dim, mesh.p, mesh.ne, _d(mesh.verts), _i(mesh.dofmap), mesh.nl,
+                              kappa, alpha, s, _d(cc), kinds)
+    if not h:
+        raise RuntimeError("orc_fa_assemble: integrator rules do not coincide")
+    return CSR(h)
+
+
+def ebe_mult(mesh: BoxMesh, x, kappa=1.0, alpha=1.0, s=1.0, c=None, kinds=DIFFUSION | CONVECTION | MASS):
+    cc = _conv(c, mesh.dim)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.zeros(mesh.nl)
+    lib().orc_ebe_mult(mesh.dim, mesh.p, mesh.ne, _d(mesh.verts), _i(mesh.dofmap), mesh.nl, kappa,
+                       alpha, s, _d(cc), kinds, _d(x), _d(y))
+    return y
+
+
+def form_linear_system(A: CSR, ess_marker, X, b):
+    B = np.zeros(A.n)
+    ess_marker = np.ascontiguousarray(ess_marker, dtype=np.int32)
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    h = lib().orc_form_linear_system(A.h, _i(ess_marker), _d(X), _d(b), _d(B))
+    return CSR(h), B
+
+
+def cg(A: CSR, b, dinv=None, rel_tol=1e-12, abs_tol=0.0, max_iter=500):
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(A.n)
+    it, fn = C.c_int(0), C.c_double(0)
+    di = None if dinv is None else _d(np.ascontiguousarray(dinv, dtype=np.float64))
+    conv = lib().orc_cg(A.h, di, _d(b), _d(x), rel_tol, abs_tol, max_iter, C.byref(it), C.byref(fn))
+    return x, dict(converged=bool(conv), iterations=it.value, final_norm=fn.value)
+
+
+def gmres(A: CSR, b, dinv=None, restart=30, rtol=1e-10, atol=1e-12, max_it=500):
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(A.n)
+    it, fn = C.c_int(0), C.c_double(0)
+    di = None if dinv is None else _d(np.ascontiguousarray(dinv, dtype=np.float64))
+    conv = lib().orc_gmres(A.h, di, _d(b), _d(x), restart, rtol, atol, max_it, C.byref(it), C.byref(fn))
+    return x, dict(converged=bool(conv), iterations=it.value, final_norm=fn.value)
+
+
+MMS_SIN, MMS_POLY, MMS_DIFFUSION_T = 1, 2, 3
+
+
+def mms_params(kind, dim, kappa=0.1, s=1.0, alpha=1.0, c=(1.0, -2.0, 0.5), modes=(3, 3, 3), t=0.0, p=1):
+    cc = _conv(c, dim)
+    return np.array([kind, kappa, s, alpha, cc[0], cc[1], cc[2], modes[0], modes[1], modes[2], t, p, dim],
+                    dtype=np.float64)
+
+
+def mms_u(prm, xyz):
+    xyz = np.atleast_2d(xyz)
+    out = np.zeros(len(xyz))
+    L = lib()
+    for i, x in enumerate(xyz):
+        xx = np.zeros(3)
+        xx[: len(x)] = x
+        out[i] = L.orc_mms_u(_d(prm), _d(xx))
+    return out
+
+
+def lf_assemble(mesh: BoxMesh, prm):
+    b = np.zeros(mesh.nl)
+    lib().orc_lf_assemble(mesh.dim, mesh.p, mesh.ne, _d(mesh.verts), _i(mesh.dofmap), mesh.nl,
+                          _d(np.ascontiguousarray(prm)), _d(b))
+    return b
+
+
+def l2_error(mesh: BoxMesh, u, prm=None):
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    if prm is None:
+        return lib().orc_l2_error(mesh.dim, mesh.p, mesh.ne, _d(mesh.verts), _i(mesh.dofmap), _d(u),
+                                  _d(np.zeros(13)), 1)
+    return lib().orc_l2_error(mesh.dim, mesh.p, mesh.ne, _d(mesh.verts), _i(mesh.dofmap), _d(u),
+                              _d(np.ascontiguousarray(prm)), 0)
+
+
+def solve_mms(mesh: BoxMesh, prm, kappa, s, c, alpha=1.0, solver="gmres", tol=1e-10, atol=1e-12,
+              max_it=500):
+    """The driver sequence of linear_convection_diffusion_2D.cpp:319-377 on the CPU oracle.
+
+    Returns (u, info, l2_error).
+    """
+    A = fa_assemble(mesh, kappa=kappa, alpha=alpha, s=s, c=c)
+    b = lf_assemble(mesh, prm)
+    u = np.zeros(mesh.nl)
+    xyz = mesh.dof_coords()
+    u[mesh.ess] = mms_u(prm, xyz[mesh.ess])                # ProjectBdrCoefficient
+    Ac, B = form_linear_system(A, mesh.bdr, u, b)           # FormLinearSystem
+    dinv = 1.0 / Ac.diag()
+    if solver == "gmres":
+        X, info = gmres(Ac, B, dinv=dinv, rtol=tol, atol=atol, max_it=max_it)
+    else:
+        X, info = cg(Ac, B, dinv=dinv, rel_tol=tol, abs_tol=0.0, max_iter=max_it)
+    return X, info, l2_error(mesh, X, prm)                  # RecoverFEMSolution (P = I) + L2 error
+
+
+def set_threads(n):
+    lib().orc_set_num_threads(int(n))
+
+
+def num_threads():
+    return lib().orc_num_threads()

@@ -1,0 +1,78 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every entry point that
+include/cdfem.h declares, and its host-side mesh generator agrees with the oracle's."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import cdfem
+from oracle import oracle as O
+
+
+def test_library_exports_every_declared_symbol():
+    L = cdfem.lib()
+    names = cdfem.exported_symbols_from_header()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert L.cdfem_abi_version() == 1
+
+
+def test_no_fallback_without_device():
+    """On a host without a HIP device the context refuses to exist (never a CPU fallback)."""
+    if cdfem.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    with pytest.raises(cdfem.CdfemError):
+        cdfem.Context(0)
+
+
+@pytest.mark.parametrize("dim,n,p", [(2, 5, 1), (2, 4, 3), (3, 3, 2), (3, 2, 4)])
+def test_box_mesh_matches_oracle(dim, n, p):
+    m = cdfem.box_mesh(dim, n, p)
+    o = O.BoxMesh(dim, n, p)
+    np.testing.assert_array_equal(m.dofmap, o.dofmap)
+    np.testing.assert_array_equal(m.verts, o.verts)
+    assert m.nl == o.nl
+    np.testing.assert_array_equal(np.sort(m.ess), o.ess)
+    np.testing.assert_allclose(m.dof_xyz, o.dof_coords(), rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_slab_partition_covers_mesh(dim):
+    """z-slabs [z0,z1) reassemble the global mesh; interface planes are shared, not essential."""
+    n, p = 4, 2
+    full = cdfem.box_mesh(dim, n, p)
+    cuts = [(0, 1), (1, 3), (3, 4)]
+    seen = np.zeros(full.ne, dtype=int)
+    for z0, z1 in cuts:
+        s = cdfem.box_mesh(dim, n, p, z_range=(z0, z1))
+        per_layer = n ** (dim - 1)
+        e0 = z0 * per_layer
+        np.testing.assert_array_equal(s.verts, full.verts[e0:e0 + s.ne])
+        seen[e0:e0 + s.ne] += 1
+        # local->global: slab lattice offset by p*z0 planes along the last axis
+        plane = (p * n + 1) ** (dim - 1)
+        np.testing.assert_array_equal(s.dofmap + p * z0 * plane, full.dofmap[e0:e0 + s.ne])
+        ess_global = set((s.ess + p * z0 * plane).tolist())
+        assert ess_global <= set(full.ess.tolist())
+        # interface plane dofs (z0 > 0) must be non-essential unless on the lateral boundary
+        if z0 > 0:
+            iface = np.arange(plane) + p * z0 * plane
+            lateral = set(full.ess.tolist())
+            for g in iface:
+                assert (g in ess_global) == (g in lateral)
+    assert (seen == 1).all()
+
+
+def test_box_mesh_rejects_bad_arguments():
+    L = cdfem.lib()
+    ne, nl, ness = C.c_int(), C.c_int64(), C.c_int()
+    assert L.cdfem_box_sizes(4, 2, 2, 2, 1, 0, 0, C.byref(ne), C.byref(nl), C.byref(ness)) == cdfem.ERR_ARG
+    assert L.cdfem_box_sizes(3, 2, 2, 2, 0, 0, 0, C.byref(ne), C.byref(nl), C.byref(ness)) == cdfem.ERR_ARG
+    assert L.cdfem_box_sizes(3, 2, 2, 2, 1, 2, 1, C.byref(ne), C.byref(nl), C.byref(ness)) == cdfem.ERR_ARG
+
+
+def test_null_context_is_rejected():
+    L = cdfem.lib()
+    assert L.cdfem_synchronize(None) == cdfem.ERR_ARG
+    assert L.cdfem_last_error(None) == b"null context"
