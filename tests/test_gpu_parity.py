@@ -214,7 +214,7 @@ def test_mms_solution_error_matches_oracle(gpu_ctx):
     xo, io = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=1e-12, max_iter=2000)
     eo = O.l2_error(om, xo, prm)
     assert abs(eg - eo) <= 1e-6 * eo
-    assert eo < 5e-3
+    assert eo < 1e-2                     # 8^3 p=2: O(h^3) error of sin(3 pi x)...
 
 
 def test_variable_coefficients(gpu_ctx):
