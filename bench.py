@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes of the apply kernel from a rocprofv3 --pmc pass")
     ap.add_argument("--no-profile-events", action="store_true")
+    ap.add_argument("--path", choices=["brick", "generic"], default="brick",
+                    help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
     return ap.parse_args()
 
 
@@ -118,6 +120,8 @@ def main():
         pass
     ctx = cdfem.Context(local)
     ctx.upload_mesh(mesh)
+    if args.path == "brick":
+        ctx.set_structured(n, n, n)
     c = (1.0, -2.0, 0.5)
     ctx.pa_setup(kinds=args.kinds, kappa=0.1, alpha=1.0, conv=c, mass=1.0)
 
@@ -171,7 +175,8 @@ def main():
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "k_apply3d (fused L->E gather + D/C/M PA apply)",
+                    "kernel": ("k_brick3d (patch gather + D/C/M PA apply + in-LDS E->L)" if args.path == "brick"
+                               else "k_apply3d (fused L->E gather + D/C/M PA apply)"),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
                     "launches": cnt,
                     "other_kernels_avg_us": {
@@ -198,7 +203,7 @@ def main():
             "config": {"workload": f"{n}x{n}x{nz} hex, H1 p={p}, PA D+C+M (kinds={args.kinds}), "
                                    f"Jacobi-CG {args.cg_iters} it/step",
                        "dofs": total_dofs, "elements": n * n * nz, "cg_iters_per_step": args.cg_iters,
-                       "parallelism": f"slab{world}" if world > 1 else "single"},
+                       "parallelism": f"slab{world}" if world > 1 else "single", "path": args.path},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

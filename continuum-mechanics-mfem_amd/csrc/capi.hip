@@ -90,8 +90,10 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_ess); dfree(c->d_ess_list); dfree(c->d_qd); dfree(c->d_Ye); dfree(c->d_dinv);
     for (auto &w : c->d_w) dfree(w);
     dfree(c->d_part); dfree(c->d_gm); dfree(c->d_gm_small);
+    dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones);
     c->gm_cap = 0;
     c->mesh_ready = c->pa_ready = c->dinv_ready = false;
+    c->structured = false;
 }
 
 // ---- profiling helpers ---------------------------------------------------------------------------
@@ -128,6 +130,63 @@ void prof_collect(cdfem_ctx *c)
     }
 }
 
+// (Re)build the element-block layout for a permutation perm[blk*64 + lane] = element (-1 pad):
+// element map [blk][l][lane] (ess negative), E->L positions, and the device permutation.
+void build_layout(cdfem_ctx *c, const std::vector<int32_t> &perm)
+{
+    const int nd = c->nd;
+    const int64_t nl = c->nl;
+    std::vector<int32_t> map((size_t)c->nblk * nd * kLanes, 0);
+    std::vector<int32_t> where(c->ne, -1);
+    for (size_t k = 0; k < perm.size(); ++k)
+        if (perm[k] >= 0) where[perm[k]] = (int32_t)k;
+    std::vector<int32_t> cnt(nl + 1, 0);
+    for (int e = 0; e < c->ne; ++e) {
+        const int blk = where[e] / kLanes, lane = where[e] % kLanes;
+        for (int l = 0; l < nd; ++l) {
+            const int32_t g = c->h_dofs[(size_t)e * nd + l];
+            map[((size_t)blk * nd + l) * kLanes + lane] = c->h_ess[g] ? -(g + 1) : g;
+            cnt[g + 1]++;
+        }
+    }
+    for (int64_t i = 0; i < nl; ++i) cnt[i + 1] += cnt[i];
+    std::vector<int32_t> pos((size_t)c->ne * nd), fill(cnt.begin(), cnt.end() - 1);
+    for (int e = 0; e < c->ne; ++e) {
+        const int blk = where[e] / kLanes, lane = where[e] % kLanes;
+        for (int l = 0; l < nd; ++l) {
+            const int32_t g = c->h_dofs[(size_t)e * nd + l];
+            pos[fill[g]++] = (int32_t)(((size_t)blk * nd + l) * kLanes + lane);
+        }
+    }
+    dfree(c->d_map); dfree(c->d_e2l_off); dfree(c->d_e2l_pos); dfree(c->d_perm); dfree(c->d_Ye);
+    dfree(c->d_part);
+    c->d_map = dalloc<int32_t>(map.size());
+    c->d_e2l_off = dalloc<int32_t>(nl + 1);
+    c->d_e2l_pos = dalloc<int32_t>(pos.size());
+    c->d_perm = dalloc<int32_t>(perm.size());
+    c->d_Ye = dalloc<double>((size_t)c->nblk * nd * kLanes);
+    c->d_part = dalloc<double>((size_t)c->red_blocks + c->nblk);
+    HIPCHK(hipMemcpyAsync(c->d_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_e2l_off, cnt.data(), (nl + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_e2l_pos, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_perm, perm.data(), perm.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_Ye, 0, (size_t)c->nblk * nd * kLanes * sizeof(double), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+}
+
+bool use_brick(const cdfem_ctx *c) { return c->structured && brick_supported(c->dim, c->p); }
+
+const double *ones_vector(cdfem_ctx *c)
+{
+    if (!c->d_ones) {
+        c->d_ones = dalloc<double>(c->nl);
+        std::vector<double> one(c->nl, 1.0);
+        HIPCHK(hipMemcpyAsync(c->d_ones, one.data(), c->nl * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return c->d_ones;
+}
+
 void require_mesh(cdfem_ctx *c)
 {
     if (!c->mesh_ready) throw StateError("cdfem_mesh_upload has not been called");
@@ -141,6 +200,15 @@ void require_pa(cdfem_ctx *c)
 // operator apply into y (device pointers): Ye = A_e x, y = E->L(Ye) [+ constraint]
 void op_apply(cdfem_ctx *c, const double *x, double *y, bool constrained)
 {
+    if (use_brick(c)) {
+        prof_mark(c, CDFEM_K_APPLY, true);
+        HIPCHK(launch_brick_mult(c, x, y, constrained, 1));
+        prof_mark(c, CDFEM_K_APPLY, false);
+        prof_mark(c, CDFEM_K_E2L, true);
+        HIPCHK(launch_brick_mult(c, x, y, constrained, 2));
+        prof_mark(c, CDFEM_K_E2L, false);
+        return;
+    }
     prof_mark(c, CDFEM_K_APPLY, true);
     HIPCHK(launch_apply(c, x, c->d_Ye, constrained));
     prof_mark(c, CDFEM_K_APPLY, false);
@@ -176,6 +244,56 @@ void ensure_dinv(cdfem_ctx *c)
     HIPCHK(launch_e2l(c, c->d_Ye, nullptr, diag, false, 0));
     HIPCHK(launch_dinv(c, diag, c->d_dinv));
     c->dinv_ready = true;
+}
+
+// brick-path CG: 3 kernels per iteration (brick apply with fused direction update, face sum with
+// den/alpha, update with betanom/beta); identical MFEM CGSolver arithmetic
+void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, double *dX,
+                    cdfem_solver_result &res)
+{
+    double *x = c->d_w[2], *r = c->d_w[3], *q = c->d_w[4], *d = c->d_w[5];
+    const double *dinv;
+    if (p.pc == CDFEM_PC_JACOBI) {
+        ensure_dinv(c);
+        dinv = c->d_dinv;
+    } else {
+        dinv = ones_vector(c);
+    }
+    const int check = p.check_every > 0 ? p.check_every : 16;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(launch_cg_init(c, dB, x, r, q, d, dinv, p.rel_tol, p.abs_tol, p.max_iter));
+    auto apply = [&] {
+        prof_mark(c, CDFEM_K_APPLY, true);
+        HIPCHK(launch_brick_cg(c, r, dinv, d, q, 1));
+        prof_mark(c, CDFEM_K_APPLY, false);
+        prof_mark(c, CDFEM_K_E2L, true);
+        HIPCHK(launch_brick_cg(c, r, dinv, d, q, 2));
+        prof_mark(c, CDFEM_K_E2L, false);
+    };
+    apply();
+    int launched = 0;
+    for (;;) {
+        for (int k = 0; k < check && launched < p.max_iter; ++k, ++launched) {
+            prof_mark(c, CDFEM_K_UPDATE, true);
+            HIPCHK(launch_cg_update_noz(c, x, r, q, d, dinv));
+            prof_mark(c, CDFEM_K_UPDATE, false);
+            apply();
+        }
+        HIPCHK(hipMemcpyAsync(c->h_state, c->d_state, sizeof(KrylovState), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->h_state->done || launched >= p.max_iter) break;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    prof_collect(c);
+    const KrylovState &s = *c->h_state;
+    res.converged = s.converged;
+    res.iterations = s.final_iter;
+    res.initial_norm = std::sqrt(std::fabs(s.nom0));
+    res.final_norm = (s.final_iter == 0) ? std::sqrt(std::fabs(s.nom0)) : std::sqrt(std::fabs(s.betanom));
+    res.seconds = std::chrono::duration<double>(t1 - t0).count();
+    HIPCHK(hipMemcpyAsync(dX, x, c->nl * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
 }
 
 // MFEM CGSolver on the constrained operator, device-resident
@@ -346,57 +464,84 @@ int cdfem_mesh_upload(cdfem_ctx *c, int dim, int order, int ne, const double *el
         c->rule_err = make_rule(order, rule_points_1d(2, dim, order));
 
         const int nd = c->nd;
-        std::vector<uint8_t> ess(nldofs, 0);
+        c->h_ess.assign(nldofs, 0);
         for (int i = 0; i < n_ess; ++i) {
             if (ess_dofs[i] < 0 || ess_dofs[i] >= nldofs) throw ArgError("essential dof out of range");
-            ess[ess_dofs[i]] = 1;
+            c->h_ess[ess_dofs[i]] = 1;
         }
-        // element map [nblk][nd][64], essential encoded negative; padding -> dof 0 (qdata 0)
-        std::vector<int32_t> map((size_t)c->nblk * nd * kLanes, 0);
-        std::vector<int32_t> cnt(nldofs + 1, 0);
-        for (int e = 0; e < ne; ++e)
-            for (int l = 0; l < nd; ++l) {
-                const int32_t g = elem_dofs[(size_t)e * nd + l];
-                if (g < 0 || g >= nldofs) throw ArgError("element dof out of range");
-                map[((size_t)(e / kLanes) * nd + l) * kLanes + (e % kLanes)] = ess[g] ? -(g + 1) : g;
-                cnt[g + 1]++;
-            }
-        // E->L transpose (positions into the E-vector), ascending element order
-        for (int64_t i = 0; i < nldofs; ++i) cnt[i + 1] += cnt[i];
-        std::vector<int32_t> pos((size_t)ne * nd), fill(cnt.begin(), cnt.end() - 1);
-        for (int e = 0; e < ne; ++e)
-            for (int l = 0; l < nd; ++l) {
-                const int32_t g = elem_dofs[(size_t)e * nd + l];
-                pos[fill[g]++] = (int32_t)(((size_t)(e / kLanes) * nd + l) * kLanes + (e % kLanes));
-            }
+        c->h_dofs.assign(elem_dofs, elem_dofs + (size_t)ne * nd);
+        for (int32_t g : c->h_dofs)
+            if (g < 0 || g >= nldofs) throw ArgError("element dof out of range");
         std::vector<int32_t> ess_list;
-        ess_list.reserve(n_ess);
         for (int64_t i = 0; i < nldofs; ++i)
-            if (ess[i]) ess_list.push_back((int32_t)i);
+            if (c->h_ess[i]) ess_list.push_back((int32_t)i);
         c->n_ess = (int)ess_list.size();
 
         c->d_verts = dalloc<double>((size_t)ne * c->nv * dim);
-        c->d_map = dalloc<int32_t>(map.size());
-        c->d_e2l_off = dalloc<int32_t>(nldofs + 1);
-        c->d_e2l_pos = dalloc<int32_t>(pos.size());
         c->d_ess = dalloc<uint8_t>(nldofs);
         c->d_ess_list = dalloc<int32_t>(ess_list.size());
-        c->d_Ye = dalloc<double>((size_t)c->nblk * nd * kLanes);
         c->d_dinv = dalloc<double>(nldofs);
         for (auto &w : c->d_w) w = dalloc<double>(nldofs);
-        c->d_part = dalloc<double>(c->red_blocks);
         HIPCHK(hipMemcpyAsync(c->d_verts, elem_verts, (size_t)ne * c->nv * dim * sizeof(double),
                               hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(c->d_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(c->d_e2l_off, cnt.data(), (nldofs + 1) * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(c->d_e2l_pos, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(c->d_ess, ess.data(), nldofs, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_ess, c->h_ess.data(), nldofs, hipMemcpyHostToDevice, c->stream));
         if (!ess_list.empty())
             HIPCHK(hipMemcpyAsync(c->d_ess_list, ess_list.data(), ess_list.size() * 4,
                                   hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemsetAsync(c->d_Ye, 0, (size_t)c->nblk * nd * kLanes * sizeof(double), c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));  // host vectors go out of scope
+        // element blocks of 64 in input order (identity permutation, padded)
+        std::vector<int32_t> perm((size_t)c->nblk * kLanes, -1);
+        for (int e = 0; e < ne; ++e) perm[e] = e;
+        build_layout(c, perm);
         c->mesh_ready = true;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        if (c->dim != 3) throw UnsupportedError("structured fast path is 3D only");
+        if (nx < 1 || ny < 1 || nz < 1 || (int64_t)nx * ny * nz != c->ne)
+            throw ArgError("nx*ny*nz must equal the number of elements");
+        const int p = c->p, d1 = c->d1, nd = c->nd;
+        const int64_t Lx = (int64_t)p * nx + 1, Ly = (int64_t)p * ny + 1, Lz = (int64_t)p * nz + 1;
+        if (Lx * Ly * Lz != c->nl) throw ArgError("dof count does not match the structured lattice");
+        // the element dof map must be the lexicographic lattice numbering (cdfem_box_mesh)
+        for (int e = 0; e < c->ne; ++e) {
+            const int ix = e % nx, iy = (e / nx) % ny, iz = e / (nx * ny);
+            for (int l = 0; l < nd; ++l) {
+                const int dx = l % d1, dy = (l / d1) % d1, dz = l / (d1 * d1);
+                const int64_t g = (p * ix + dx) + Lx * ((p * iy + dy) + Ly * (int64_t)(p * iz + dz));
+                if (c->h_dofs[(size_t)e * nd + l] != g)
+                    throw ArgError("element dof map is not the lexicographic structured numbering");
+            }
+        }
+        c->sx = nx; c->sy = ny; c->sz = nz;
+        c->Lx = Lx; c->Ly = Ly; c->Lz = Lz;
+        c->nbx = (nx + kBrick - 1) / kBrick;
+        c->nby = (ny + kBrick - 1) / kBrick;
+        c->nbz = (nz + kBrick - 1) / kBrick;
+        c->nblk = c->nbx * c->nby * c->nbz;
+        // brick permutation: block = brick (lexicographic), lane = ex + 4 (ey + 4 ez)
+        std::vector<int32_t> perm((size_t)c->nblk * kLanes, -1);
+        for (int b = 0; b < c->nblk; ++b) {
+            const int bx = b % c->nbx, by = (b / c->nbx) % c->nby, bz = b / (c->nbx * c->nby);
+            for (int t = 0; t < kLanes; ++t) {
+                const int ix = kBrick * bx + (t & 3), iy = kBrick * by + ((t >> 2) & 3),
+                          iz = kBrick * bz + (t >> 4);
+                if (ix < nx && iy < ny && iz < nz) perm[(size_t)b * kLanes + t] = ix + nx * (iy + ny * iz);
+            }
+        }
+        build_layout(c, perm);
+        const int S = kBrick * p + 1;
+        c->nface = 2 * S * S + (S - 2) * (4 * S - 4);
+        dfree(c->d_face);
+        c->d_face = dalloc<double>((size_t)c->nblk * c->nface);
+        dfree(c->d_qd);
+        c->structured = true;
+        c->pa_ready = false;
+        c->dinv_ready = false;
         return CDFEM_OK;
     });
 }
@@ -552,7 +697,10 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
         const double *dB = dev_in(c, B, where, c->d_w[6], c->nl);
         double *dX = where == CDFEM_DEVICE ? X : c->d_w[1];
         if (p->method == CDFEM_CG) {
-            solve_cg(c, *p, dB, dX, *res);
+            if (use_brick(c))
+                solve_cg_brick(c, *p, dB, dX, *res);
+            else
+                solve_cg(c, *p, dB, dX, *res);
         } else {
             throw UnsupportedError("GMRES is not available in this build");
         }
@@ -599,6 +747,30 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
         if (!bytes) throw ArgError("bytes is null");
         const double nl = (double)c->nl, ne = (double)c->ne, nd = c->nd;
         const double nq = nq_of(c, c->rule_op);
+        if (use_brick(c)) {
+            // CG-mode brick kernels (what the Krylov loop launches); see DESIGN.md section 4
+            const int64_t s1 = (int64_t)kBrick * c->p;
+            int64_t nface_dofs = 0;
+            for (int64_t z = 0; z < c->Lz; ++z)
+                for (int64_t y = 0; y < c->Ly; ++y) {
+                    if (z % s1 == 0 || y % s1 == 0) { nface_dofs += c->Lx; continue; }
+                    nface_dofs += (c->Lx - 1) / s1 + 1;
+                }
+            const double nf = (double)nface_dofs, nown = nl - nf;
+            const double partials = 8.0 * c->nface * (double)c->nblk;
+            switch (k) {
+            case CDFEM_K_APPLY:   // qdata + gathered r, M^-1, d + ess flags + owned d, q + face partials
+                *bytes = 8.0 * c->ncomp * nq * ne + 24.0 * nl + 1.0 * nl + 16.0 * nown + partials;
+                return CDFEM_OK;
+            case CDFEM_K_E2L:     // face partials + r, M^-1, d, ess of face dofs + d, q of face dofs
+                *bytes = partials + 25.0 * nf + 16.0 * nf;
+                return CDFEM_OK;
+            case CDFEM_K_UPDATE:  // x, d, r, q, M^-1 read; x, r write
+                *bytes = 56.0 * nl;
+                return CDFEM_OK;
+            default: throw ArgError("kernel not launched on the brick path");
+            }
+        }
         switch (k) {
         case CDFEM_K_APPLY:
             // x gather (each L-dof once) + qdata stream + element map + E-vector write

@@ -74,6 +74,18 @@ struct cdfem_ctx {
     int32_t *d_e2l_pos = nullptr;       // [ne*nd]
     uint8_t *d_ess = nullptr;           // [nl]
     int32_t *d_ess_list = nullptr;      // [n_ess]
+    int32_t *d_perm = nullptr;          // [nblk*64] element at (block, lane), -1 = padding
+    std::vector<int32_t> h_dofs;        // host copy of the element dof map (ne*nd)
+    std::vector<uint8_t> h_ess;         // host essential marker (nl)
+
+    // structured-box fast path (cdfem_mesh_set_structured): 4x4x4-element bricks
+    bool structured = false;
+    int sx = 0, sy = 0, sz = 0;         // elements per axis of the local box
+    int nbx = 0, nby = 0, nbz = 0;      // bricks per axis
+    int64_t Lx = 0, Ly = 0, Lz = 0;     // dof lattice per axis
+    double *d_face = nullptr;           // [nblk][F] brick-face partial sums
+    double *d_ones = nullptr;           // all-ones vector (unpreconditioned brick CG)
+    int nface = 0;                      // F
 
     // rules
     cdfem::Rule1D rule_op, rule_lf, rule_err;
@@ -89,7 +101,7 @@ struct cdfem_ctx {
 
     // work vectors (L-size)
     double *d_w[8] = {};                // staging + Krylov vectors
-    double *d_part = nullptr;           // reduction partials
+    double *d_part = nullptr;           // reduction partials [red_blocks + nblk]
     int red_blocks = 1024;
     cdfem::KrylovState *d_state = nullptr;
     cdfem::KrylovState *h_state = nullptr;  // pinned
@@ -116,6 +128,15 @@ hipError_t launch_lf_elem(cdfem_ctx *c, const double *d_fq, double *Ye);
 hipError_t launch_quad_points(cdfem_ctx *c, const Rule1D &r, double *xyz);
 bool apply_supported(int dim, int p);
 
+// ---- structured brick kernels (brick_kernels.hip) --------------------------------------------
+constexpr int kBrick = 4;               // elements per brick edge (4^3 = 64 = one wavefront)
+bool brick_supported(int dim, int p);
+// y = A x (constrained: ess in -> 0, y[ess] = x[ess]); fused E->L through LDS + face partials
+hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool constrained, int which);
+// CG-fused: d = M^{-1} r + beta d (in place), q = A_c d, den = (d, q) -> state (alpha, nom)
+hipError_t launch_brick_cg(cdfem_ctx *c, const double *r, const double *dinv, double *d, double *q,
+                           int which);  // which: 1 brick kernel, 2 face kernel, 3 both
+
 // ---- vector kernels (vec_kernels.hip) --------------------------------------------------------
 // y = E->L sum of Ye; constrained: y[ess] = x[ess]; if dot_part != nullptr also reduces
 // partial sums of y.x into dot_part[blockIdx] and the last block writes state->den and alpha.
@@ -131,6 +152,10 @@ hipError_t launch_cg_init(cdfem_ctx *c, const double *B, double *x, double *r, d
 hipError_t launch_cg_update(cdfem_ctx *c, double *x, double *r, double *z, const double *d,
                             const double *dinv);
 hipError_t launch_cg_direction(cdfem_ctx *c, const double *z, double *d);
+// x += alpha d, r -= alpha q, betanom = (r, M^{-1} r); z is not stored (brick path recomputes it)
+hipError_t launch_cg_update_noz(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
+                                const double *dinv);
+hipError_t launch_zero(cdfem_ctx *c, double *y);
 // generic deterministic dot into host-visible scalar via state (used by GMRES / tests)
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out);
 

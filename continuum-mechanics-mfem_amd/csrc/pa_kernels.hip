@@ -15,38 +15,9 @@
 #include <hip/hip_runtime.h>
 
 #include "cdfem_internal.hpp"
+#include "pa_core.hpp"
 
 namespace cdfem {
-
-template <int D1, int Q1>
-struct Tab {
-    double B[Q1][D1];
-    double G[Q1][D1];
-};
-
-template <int D1, int Q1>
-static Tab<D1, Q1> make_tab(const Rule1D &r)
-{
-    Tab<D1, Q1> t;
-    for (int q = 0; q < Q1; ++q)
-        for (int d = 0; d < D1; ++d) {
-            t.B[q][d] = r.B[q][d];
-            t.G[q][d] = r.G[q][d];
-        }
-    return t;
-}
-
-// qdata component layout for a kinds mask: [D (sym) | C (dim) | M]
-template <unsigned K, int DIM>
-struct QLayout {
-    static constexpr bool kD = (K & CDFEM_DIFFUSION) != 0;
-    static constexpr bool kC = (K & CDFEM_CONVECTION) != 0;
-    static constexpr bool kM = (K & CDFEM_MASS) != 0;
-    static constexpr int nD = kD ? DIM * (DIM + 1) / 2 : 0;
-    static constexpr int oC = nD;
-    static constexpr int oM = oC + (kC ? DIM : 0);
-    static constexpr int nc = oM + (kM ? 1 : 0);
-};
 
 // ------------------------------------------------------------------------------------------------
 // 3D apply: Ye = A_e x_e for every element (thread per element)
@@ -85,121 +56,8 @@ k_apply3d(const int32_t *__restrict__ map, const double *__restrict__ x,
             }
 
     double Y[D1][D1][D1];
-#pragma unroll
-    for (int dz = 0; dz < D1; ++dz)
-#pragma unroll
-        for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) Y[dz][dy][dx] = 0.0;
-
     const double *q0 = qd + (size_t)b * NQ * NC * kLanes + lane;
-
-#pragma unroll
-    for (int qz = 0; qz < Q1; ++qz) {
-        // contract z
-        double T0[D1][D1], Tz[D1][D1];
-#pragma unroll
-        for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) {
-                double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-                for (int dz = 0; dz < D1; ++dz) {
-                    s0 += T.B[qz][dz] * X[dz][dy][dx];
-                    s1 += T.G[qz][dz] * X[dz][dy][dx];
-                }
-                T0[dy][dx] = s0;
-                Tz[dy][dx] = s1;
-            }
-        double RT[D1][D1], RTz[D1][D1];
-#pragma unroll
-        for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) { RT[dy][dx] = 0.0; RTz[dy][dx] = 0.0; }
-
-#pragma unroll
-        for (int qy = 0; qy < Q1; ++qy) {
-            // contract y
-            double a[D1], ay[D1], az[D1];
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) {
-                double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-#pragma unroll
-                for (int dy = 0; dy < D1; ++dy) {
-                    s0 += T.B[qy][dy] * T0[dy][dx];
-                    s1 += T.G[qy][dy] * T0[dy][dx];
-                    s2 += T.B[qy][dy] * Tz[dy][dx];
-                }
-                a[dx] = s0; ay[dx] = s1; az[dx] = s2;
-            }
-            double Rv[D1], Ry[D1], Rz[D1];
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) { Rv[dx] = 0.0; Ry[dx] = 0.0; Rz[dx] = 0.0; }
-
-#pragma unroll
-            for (int qx = 0; qx < Q1; ++qx) {
-                // contract x -> value and reference gradient at the point
-                double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
-#pragma unroll
-                for (int dx = 0; dx < D1; ++dx) {
-                    u += T.B[qx][dx] * a[dx];
-                    ux += T.G[qx][dx] * a[dx];
-                    uy += T.B[qx][dx] * ay[dx];
-                    uz += T.B[qx][dx] * az[dx];
-                }
-                const int q = qx + Q1 * (qy + Q1 * qz);
-                const double *qq = q0 + (size_t)q * NC * kLanes;
-                double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
-                if constexpr (L::kD) {
-                    const double d00 = qq[0 * kLanes], d01 = qq[1 * kLanes], d02 = qq[2 * kLanes];
-                    const double d11 = qq[3 * kLanes], d12 = qq[4 * kLanes], d22 = qq[5 * kLanes];
-                    gx = d00 * ux + d01 * uy + d02 * uz;
-                    gy = d01 * ux + d11 * uy + d12 * uz;
-                    gz = d02 * ux + d12 * uy + d22 * uz;
-                }
-                if constexpr (L::kC) {
-                    vv = qq[(L::oC + 0) * kLanes] * ux + qq[(L::oC + 1) * kLanes] * uy +
-                         qq[(L::oC + 2) * kLanes] * uz;
-                }
-                if constexpr (L::kM) vv += qq[L::oM * kLanes] * u;
-                // transposed contraction in x
-#pragma unroll
-                for (int dx = 0; dx < D1; ++dx) {
-                    if constexpr (L::kD) {
-                        Rv[dx] += T.B[qx][dx] * vv + T.G[qx][dx] * gx;
-                        Ry[dx] += T.B[qx][dx] * gy;
-                        Rz[dx] += T.B[qx][dx] * gz;
-                    } else {
-                        Rv[dx] += T.B[qx][dx] * vv;
-                    }
-                }
-            }
-            // transposed contraction in y
-#pragma unroll
-            for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-                for (int dx = 0; dx < D1; ++dx) {
-                    if constexpr (L::kD) {
-                        RT[dy][dx] += T.B[qy][dy] * Rv[dx] + T.G[qy][dy] * Ry[dx];
-                        RTz[dy][dx] += T.B[qy][dy] * Rz[dx];
-                    } else {
-                        RT[dy][dx] += T.B[qy][dy] * Rv[dx];
-                    }
-                }
-        }
-        // transposed contraction in z
-#pragma unroll
-        for (int dz = 0; dz < D1; ++dz)
-#pragma unroll
-            for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-                for (int dx = 0; dx < D1; ++dx) {
-                    if constexpr (L::kD)
-                        Y[dz][dy][dx] += T.B[qz][dz] * RT[dy][dx] + T.G[qz][dz] * RTz[dy][dx];
-                    else
-                        Y[dz][dy][dx] += T.B[qz][dz] * RT[dy][dx];
-                }
-    }
+    elem_apply3d<D1, Q1, K>(X, q0, T, Y);
 
     double *yp = Ye + (size_t)b * ND * kLanes + lane;
 #pragma unroll
@@ -382,7 +240,8 @@ __device__ inline void qpoint(int q, int q1, int dim, const Rule1D &r, double xi
 // qdata setup: thread per (element-block, q, lane); coalesced writes of the [b][q][c][lane] layout
 template <int DIM>
 __global__ void __launch_bounds__(256)
-k_setup_qdata(const double *__restrict__ verts, int ne, int nblk, const Rule1D r, unsigned kinds,
+k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm, int ne, int nblk,
+              const Rule1D r, unsigned kinds,
               int nc, double kappa, const double *__restrict__ kappa_q, double alpha, double c0,
               double c1, double c2, const double *__restrict__ conv_q, double mass,
               const double *__restrict__ mass_q, double *__restrict__ qd)
@@ -394,9 +253,9 @@ k_setup_qdata(const double *__restrict__ verts, int ne, int nblk, const Rule1D r
     const int lane = (int)(t % kLanes);
     const int q = (int)((t / kLanes) % nq);
     const int b = (int)(t / ((int64_t)kLanes * nq));
-    const int e = b * kLanes + lane;
+    const int e = perm[(size_t)b * kLanes + lane];
     double *out = qd + ((size_t)b * nq + q) * nc * kLanes + lane;
-    if (e >= ne) {
+    if (e < 0 || e >= ne) {
         for (int k = 0; k < nc; ++k) out[k * kLanes] = 0.0;
         return;
     }
@@ -509,7 +368,8 @@ k_diag_elem(const double *__restrict__ qd, int nblk, int nd, const Rule1D r, uns
 // linear form, element part: be_l = sum_q W detJ f_q phi_l; thread per (block, l, lane)
 template <int DIM>
 __global__ void __launch_bounds__(256)
-k_lf_elem(const double *__restrict__ verts, int ne, int nblk, int nd, const Rule1D r,
+k_lf_elem(const double *__restrict__ verts, const int32_t *__restrict__ perm, int ne, int nblk, int nd,
+          const Rule1D r,
           const double *__restrict__ fq, double *__restrict__ Ye)
 {
     const int q1 = r.q1;
@@ -519,9 +379,9 @@ k_lf_elem(const double *__restrict__ verts, int ne, int nblk, int nd, const Rule
     const int lane = (int)(t % kLanes);
     const int l = (int)((t / kLanes) % nd);
     const int b = (int)(t / ((int64_t)kLanes * nd));
-    const int e = b * kLanes + lane;
+    const int e = perm[(size_t)b * kLanes + lane];
     double acc = 0.0;
-    if (e < ne) {
+    if (e >= 0 && e < ne) {
         for (int q = 0; q < nq; ++q) {
             double xi[3], W, x[3], J[3][3], A[3][3], phi, g[3];
             qpoint(q, q1, DIM, r, xi, W);
@@ -550,11 +410,11 @@ hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, double kapp
     const double c2 = (conv && c->dim == 3) ? conv[2] : 0.0;
     if (c->dim == 3)
         hipLaunchKernelGGL(k_setup_qdata<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->ne, c->nblk, c->rule_op, c->kinds, c->ncomp, kappa,
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->rule_op, c->kinds, c->ncomp, kappa,
                            d_kappa_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
     else
         hipLaunchKernelGGL(k_setup_qdata<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->ne, c->nblk, c->rule_op, c->kinds, c->ncomp, kappa,
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->rule_op, c->kinds, c->ncomp, kappa,
                            d_kappa_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
     return hipGetLastError();
 }
@@ -589,10 +449,10 @@ hipError_t launch_lf_elem(cdfem_ctx *c, const double *d_fq, double *Ye)
     const int64_t n = (int64_t)c->nblk * c->nd * kLanes;
     if (c->dim == 3)
         hipLaunchKernelGGL(k_lf_elem<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->ne, c->nblk, c->nd, c->rule_lf, d_fq, Ye);
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->rule_lf, d_fq, Ye);
     else
         hipLaunchKernelGGL(k_lf_elem<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->ne, c->nblk, c->nd, c->rule_lf, d_fq, Ye);
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->rule_lf, d_fq, Ye);
     return hipGetLastError();
 }
 

@@ -10,62 +10,9 @@
 #include <hip/hip_runtime.h>
 
 #include "cdfem_internal.hpp"
+#include "reduce.hpp"
 
 namespace cdfem {
-
-constexpr int kRedThreads = 256;
-
-__device__ inline double wave_sum(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// block sum, result valid in thread 0
-__device__ inline double block_sum(double v, double *sh)
-{
-    v = wave_sum(v);
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) sh[w] = v;
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        v = (threadIdx.x < (blockDim.x >> 6)) ? sh[threadIdx.x] : 0.0;
-        v = wave_sum(v);
-    }
-    return v;
-}
-
-// Publish this block's partial and find out whether it is the last arriver.  Producer side: plain
-// store, every wave drains vmcnt, barrier, lane-0 agent release, asm drain, relaxed agent ticket.
-// The last arriver then acquires (agent) before reading other blocks' partials.
-__device__ inline bool publish_partial(double v, double *part, unsigned *cnt, int *sh_last)
-{
-    if (threadIdx.x == 0) part[blockIdx.x] = v;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = (prev == gridDim.x - 1);
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *sh_last = last ? 1 : 0;
-    }
-    __syncthreads();
-    return *sh_last != 0;
-}
-
-// deterministic sum of part[0..n) by one block (fixed order), result in thread 0
-__device__ inline double sum_partials(const double *part, int n, double *sh)
-{
-    double v = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) v += part[i];
-    return block_sum(v, sh);
-}
 
 // ------------------------------------------------------------------------------------------------
 // E->L: y[i] = sum of Ye over the (element, local dof) pairs of dof i (ascending element order).
@@ -101,17 +48,7 @@ k_e2l(const int32_t *__restrict__ off, const int32_t *__restrict__ pos,
     const double den = sum_partials(part, gridDim.x, sh);
     if (threadIdx.x == 0) {
         st->cnt[0] = 0;
-        st->den = den;
-        const int first = (st->first_den != 0);
-        st->first_den = 0;
-        if (den == 0.0) {               // CGSolver: den == 0 -> stop, not converged
-            st->done = 1;
-            st->converged = 0;
-            st->final_iter = first ? 0 : st->iter;
-        } else {
-            st->nom = st->betanom;      // (initial den: betanom == nom0)
-            st->alpha = st->nom / den;
-        }
+        cg_den_step(st, den);
     }
 }
 
@@ -151,6 +88,7 @@ k_cg_init(const double *__restrict__ B, double *__restrict__ x, double *__restri
         st->converged = 0;
         st->done = 0;
         st->first_den = 1;  // next den is the initial one
+        st->beta = 0.0;
         if (nom < 0.0) {             // preconditioner not positive definite
             st->done = 1;
             st->final_iter = 0;
@@ -163,6 +101,7 @@ k_cg_init(const double *__restrict__ B, double *__restrict__ x, double *__restri
 }
 
 // x += alpha d, r -= alpha z, z = M^{-1} r, betanom = (r, z); last block: convergence test
+template <bool STORE_Z>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update(double *__restrict__ x, double *__restrict__ r, double *__restrict__ z,
             const double *__restrict__ d, const double *__restrict__ dinv, int64_t n,
@@ -179,7 +118,7 @@ k_cg_update(double *__restrict__ x, double *__restrict__ r, double *__restrict__
         const double ri = r[i] - alpha * z[i];
         r[i] = ri;
         const double zi = dinv ? dinv[i] * ri : ri;
-        z[i] = zi;
+        if (STORE_Z) z[i] = zi;
         acc += ri * zi;
     }
     const double bs = block_sum(acc, sh);
@@ -333,8 +272,29 @@ hipError_t launch_cg_init(cdfem_ctx *c, const double *B, double *x, double *r, d
 hipError_t launch_cg_update(cdfem_ctx *c, double *x, double *r, double *z, const double *d,
                             const double *dinv)
 {
-    hipLaunchKernelGGL(k_cg_update, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, x, r,
-                       z, d, dinv, c->nl, c->d_part, c->d_state);
+    hipLaunchKernelGGL(k_cg_update<true>, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, x,
+                       r, z, d, dinv, c->nl, c->d_part, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_cg_update_noz(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
+                                const double *dinv)
+{
+    // k_cg_update reads "z" as A d: pass q there; the z output is not written
+    hipLaunchKernelGGL(k_cg_update<false>, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, x,
+                       r, const_cast<double *>(q), d, dinv, c->nl, c->d_part, c->d_state);
+    return hipGetLastError();
+}
+
+__global__ void k_zero(double *__restrict__ y, int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = 0.0;
+}
+
+hipError_t launch_zero(cdfem_ctx *c, double *y)
+{
+    hipLaunchKernelGGL(k_zero, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, y, c->nl);
     return hipGetLastError();
 }
 

@@ -69,6 +69,7 @@ def _declare(L):
         "cdfem_free": (C.c_int, [vp, vp]),
         "cdfem_memcpy": (C.c_int, [vp, vp, C.c_int, vp, C.c_int, C.c_size_t]),
         "cdfem_mesh_upload": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, _dp, i64, _ip, C.c_int, _ip]),
+        "cdfem_mesh_set_structured": (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
         "cdfem_rule_size": (C.c_int, [vp, C.c_int, C.POINTER(C.c_int)]),
         "cdfem_quadrature_points": (C.c_int, [vp, C.c_int, _dp, C.c_int]),
         "cdfem_pa_setup": (C.c_int, [vp, C.c_uint, C.c_double, _dp, C.c_double, _dp, _dp, C.c_double, _dp]),
@@ -204,6 +205,11 @@ class Context:
                                            ess.ctypes.data_as(_ip)))
         self.mesh = mesh
         self.nl = int(mesh.nl)
+        return self
+
+    def set_structured(self, nx, ny, nz):
+        """Enable the structured brick fast path (mesh must be the lexicographic box numbering)."""
+        self._chk(self.L.cdfem_mesh_set_structured(self.h, int(nx), int(ny), int(nz)))
         return self
 
     def rule_size(self, rule):

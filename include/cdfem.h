@@ -80,6 +80,13 @@ int cdfem_memcpy(cdfem_ctx *ctx, void *dst, int dst_where, const void *src, int 
 int cdfem_mesh_upload(cdfem_ctx *ctx, int dim, int order, int ne, const double *elem_verts,
                       int64_t nldofs, const int32_t *elem_dofs, int n_ess, const int32_t *ess_dofs);
 
+/* Declare the uploaded mesh a structured nx*ny*nz box with the lexicographic numbering of
+ * cdfem_box_mesh (validated; element vertices may be perturbed).  Enables the brick fast path:
+ * 4x4x4-element bricks per wavefront, E->L sum fused into the apply through LDS, CG direction
+ * update fused into the operator gather.  Same results as the generic path to rounding.
+ * Call before cdfem_pa_setup.  (Specialisation of ParFiniteElementSpace for Cartesian meshes.)  */
+int cdfem_mesh_set_structured(cdfem_ctx *ctx, int nx, int ny, int nz);
+
 /* Physical coordinates of the quadrature points of a rule (CDFEM_RULE_*), ne * nq * dim doubles,
  * element-major, q lexicographic (qx fastest): where a host Coefficient::Eval is sampled
  * (linear_convection_diffusion_2D.cpp:165-215).  cdfem_rule_size returns nq per element.       */

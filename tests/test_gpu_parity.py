@@ -279,3 +279,96 @@ def test_full_size_cg_residual(gpu_ctx, full_size):
     d[gm.ess] = 1.0
     rz = r @ (r / d)
     assert np.sqrt(rz) <= 2e-8 * info["initial_norm"]
+
+
+# ---------------------------------------------------------------------------------------------
+# structured brick fast path (cdfem_mesh_set_structured): same parity bar as the generic path
+# ---------------------------------------------------------------------------------------------
+def _brick_pair(n, p, perturb, kinds):
+    om = O.BoxMesh(3, n, p, perturb=perturb)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    return om, gm
+
+
+@pytest.mark.parametrize("n,p,pert", [(4, 2, 0.0), (5, 2, 0.2), (3, 2, 0.1), (8, 2, 0.15), (6, 1, 0.2),
+                                      (9, 1, 0.0)])
+@pytest.mark.parametrize("kinds", [7, 5, 3])
+def test_brick_mult_parity(gpu_ctx, n, p, pert, kinds):
+    om, gm = _brick_pair(n, p, pert, kinds)
+    gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+    gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_to_oracle(kinds))
+    x = np.random.default_rng(13).uniform(-1, 1, om.nl)
+    assert _relmax(gpu_ctx.mult(x), A.mult(x)) <= MULT_TOL
+    xz = x.copy()
+    xz[om.ess] = 0.0
+    yco = A.mult(xz)
+    yco[om.ess] = x[om.ess]
+    assert _relmax(gpu_ctx.mult(x, constrained=True), yco) <= MULT_TOL
+    assert _relmax(gpu_ctx.diagonal(), A.diag()) <= MULT_TOL
+
+
+def test_brick_anisotropic_box(gpu_ctx):
+    """nx != ny != nz, none a multiple of the brick size."""
+    nx, ny, nz, p = 6, 5, 7, 2
+    om = O.BoxMesh(3, (nx, ny, nz), p, perturb=0.1)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    gpu_ctx.upload_mesh(gm).set_structured(nx, ny, nz)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3)
+    x = np.random.default_rng(17).uniform(-1, 1, om.nl)
+    assert _relmax(gpu_ctx.mult(x), A.mult(x)) <= MULT_TOL
+
+
+def test_brick_rejects_non_lexicographic(gpu_ctx):
+    om = O.BoxMesh(3, 4, 2)
+    dm = om.dofmap.copy()
+    dm[[0, 1]] = dm[[1, 0]]                           # swap two elements
+    gm = cdfem.Mesh(3, 2, om.verts, dm, om.nl, om.ess)
+    gpu_ctx.upload_mesh(gm)
+    with pytest.raises(cdfem.CdfemError) as ei:
+        gpu_ctx.set_structured(4, 4, 4)
+    assert ei.value.code == cdfem.ERR_ARG
+
+
+def test_brick_cg_parity(gpu_ctx):
+    n, p = 8, 2
+    om = O.BoxMesh(3, n, p, perturb=0.15)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+    gpu_ctx.pa_setup(kinds=5, kappa=0.1, mass=1.0)
+    A = O.fa_assemble(om, kappa=0.1, s=1.0, kinds=O.DIFFUSION | O.MASS)
+    rng = np.random.default_rng(9)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    assert _relmax(B, Bo) <= MULT_TOL
+    dinv = 1.0 / Ac.diag()
+    xo, io = O.cg(Ac, Bo, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=50)
+    xg, ig = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=50, check_every=9)
+    assert ig["iterations"] == 50
+    assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
+    xo, io = O.cg(Ac, Bo, dinv=dinv, rel_tol=1e-13, max_iter=2000)
+    xg, ig = gpu_ctx.solve(B, method="cg", rel_tol=1e-13, max_iter=2000)
+    assert ig["converged"] and abs(ig["iterations"] - io["iterations"]) <= 2
+    assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
+    xg2, _ = gpu_ctx.solve(B, method="cg", rel_tol=1e-13, max_iter=2000)
+    np.testing.assert_array_equal(xg, xg2)
+    xn, inn = gpu_ctx.solve(B, method="cg", pc="none", rel_tol=1e-12, max_iter=2000)
+    xon, ion = O.cg(Ac, Bo, dinv=None, rel_tol=1e-12, max_iter=2000)
+    assert inn["converged"] and np.linalg.norm(xn - xon) <= 1e-10 * np.linalg.norm(xon)
+
+
+def test_brick_full_size_matches_generic(gpu_ctx):
+    """64^3 p=2: brick and generic paths agree (different E->L summation order only)."""
+    gm = cdfem.box_mesh(3, 64, 2, with_coords=False)
+    x = np.random.default_rng(21).uniform(-1, 1, gm.nl)
+    gpu_ctx.upload_mesh(gm)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, conv=C3, mass=1.0)
+    y_gen = gpu_ctx.mult(x, constrained=True)
+    gpu_ctx.set_structured(64, 64, 64)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, conv=C3, mass=1.0)
+    y_brk = gpu_ctx.mult(x, constrained=True)
+    assert _relmax(y_brk, y_gen) <= 1e-14
