@@ -17,6 +17,8 @@
 // elements, and removes the element map and E->L index arrays from the stream entirely.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "cdfem_internal.hpp"
 #include "pa_core.hpp"
 #include "reduce.hpp"
@@ -45,8 +47,10 @@ template <int S>
 constexpr int face_count() { return 2 * S * S + (S - 2) * (4 * S - 4); }
 
 // MODE 0: y = A x;  MODE 1: y = A_c x (ConstrainedOperator);  MODE 2: CG-fused (x := r)
-template <int D1, int Q1, unsigned K, int MODE>
-__global__ void __launch_bounds__(64)
+// W: minimum waves per SIMD requested from the register allocator (1: unconstrained, 2: <= 256
+// VGPR+AGPR so two bricks share a SIMD; selected at run time, CDFEM_BRICK_WAVES, default 2)
+template <int D1, int Q1, unsigned K, int MODE, int W>
+__global__ void __launch_bounds__(64, W)
 k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double *__restrict__ d,
           double *__restrict__ y, double *__restrict__ face, const double *__restrict__ qd,
           const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g,
@@ -71,8 +75,12 @@ k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double 
     const int bx = b % g.nbx, by = (b / g.nbx) % g.nby, bz = b / (g.nbx * g.nby);
     const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
 
-    // 1. gather the input patch (zero outside the lattice and, when constrained, on ess dofs)
-    for (int i = t; i < S3; i += 64) {
+    // 1. gather the input patch (zero outside the lattice and, when constrained, on ess dofs);
+    //    fully unrolled so all of a thread's loads are in flight together
+#pragma unroll
+    for (int k = 0; k < (S3 + 63) / 64; ++k) {
+        const int i = t + 64 * k;
+        if (i >= S3) break;
         const int px = i % S, py = (i / S) % S, pz = i / S2;
         const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
         double v = 0.0;
@@ -96,14 +104,9 @@ k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double 
     // 2. element apply
     const int ex = t & 3, ey = (t >> 2) & 3, ez = t >> 4;
     const int o0 = P * ez * S2 + P * ey * S + P * ex;
-    double X[D1][D1][D1], Y[D1][D1][D1];
-#pragma unroll
-    for (int dz = 0; dz < D1; ++dz)
-#pragma unroll
-        for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) X[dz][dy][dx] = s_in[o0 + dz * S2 + dy * S + dx];
-    elem_apply3d<D1, Q1, K>(X, qd + (size_t)b * NQ * NC * kLanes + t, T, Y);
+    double Y[D1][D1][D1];
+    elem_apply3d<D1, Q1, K>([&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; },
+                            qd + (size_t)b * NQ * NC * kLanes, t, T, Y);
 
     // 3. deterministic E->L inside the brick: one local dof per step, all lanes distinct targets
 #pragma unroll
@@ -119,7 +122,10 @@ k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double 
 
     // 4. owned dofs -> y, face dofs -> partial buffer
     double acc = 0.0;
-    for (int i = t; i < S3; i += 64) {
+#pragma unroll
+    for (int k = 0; k < (S3 + 63) / 64; ++k) {
+        const int i = t + 64 * k;
+        if (i >= S3) break;
         const int px = i % S, py = (i / S) % S, pz = i / S2;
         const double v = s_out[i];
         const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
@@ -148,43 +154,60 @@ k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double 
     }
 }
 
-// sum the brick-face partials of every dof lying on a brick face
+// Sum the brick-face partials of every dof lying on a brick face: one thread per face dof.
+// Grid (x, z-plane): a plane gz = multiple of 4p is all face dofs; any other plane holds full
+// lines (gy = multiple of 4p) and, on the remaining lines, the dofs gx = 0, 4p, 8p, ...
+// CG mode also forms d = M^{-1} r + beta d for these dofs and the partial (d, A d).
 template <int S, int MODE>
 __global__ void __launch_bounds__(kRedThreads)
 k_brick_faces(const double *__restrict__ x, const double *__restrict__ dinv, double *__restrict__ d,
               double *__restrict__ y, const double *__restrict__ face, const uint8_t *__restrict__ ess,
-              const BrickGeom g, double *__restrict__ part, int n_apply_parts,
-              KrylovState *__restrict__ st)
+              const BrickGeom g, double *__restrict__ part, const KrylovState *__restrict__ st)
 {
     constexpr int F = face_count<S>();
     constexpr int s1 = S - 1;
     __shared__ double sh[kRedThreads / 64];
-    __shared__ int sh_last;
     double beta = 0.0;
     if constexpr (MODE == 2) {
         if (st->done) return;
         beta = st->beta;
     }
-    const int64_t n = (int64_t)g.Lx * g.Ly * g.Lz;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int gz = blockIdx.y;
+    const bool fz = gz % s1 == 0;
+    const int Lx = g.Lx, Ly = g.Ly;
+    const int nfx = (Lx - 1) / s1 + 1, nfy = (Ly - 1) / s1 + 1;
+    const int per = Lx + (s1 - 1) * nfx;                     // dofs per s1-line period (sparse plane)
+    const int count = fz ? Lx * Ly : nfy * Lx + (Ly - nfy) * nfx;
+    int bzs[2], pzs[2], nzc = 0;
+    {
+        const int qz = gz / s1;
+        if (fz) {
+            if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
+            if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
+        } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
+    }
     double acc = 0.0;
-    for (int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += stride) {
-        const int gx = (int)(gid % g.Lx), gy = (int)((gid / g.Lx) % g.Ly), gz = (int)(gid / ((int64_t)g.Lx * g.Ly));
-        const bool fx = gx % s1 == 0, fy = gy % s1 == 0, fz = gz % s1 == 0;
-        if (!(fx || fy || fz)) continue;
-        int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
-        auto cand = [](int gc, bool f, int nb, int *bs, int *ps, int &nc) {
-            const int q = gc / s1;
-            if (f) {
-                if (q - 1 >= 0 && q - 1 < nb) { bs[nc] = q - 1; ps[nc] = s1; ++nc; }
-                if (q < nb) { bs[nc] = q; ps[nc] = 0; ++nc; }
-            } else {
-                bs[0] = q; ps[0] = gc - q * s1; nc = 1;
-            }
-        };
-        cand(gx, fx, g.nbx, bxs, pxs, nxc);
-        cand(gy, fy, g.nby, bys, pys, nyc);
-        cand(gz, fz, g.nbz, bzs, pzs, nzc);
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < count; k += gridDim.x * blockDim.x) {
+        int gx, gy;
+        if (fz) {
+            gy = k / Lx; gx = k - gy * Lx;
+        } else {
+            const int pi = k / per, rem = k - pi * per;
+            if (rem < Lx) { gy = s1 * pi; gx = rem; }
+            else { const int j = rem - Lx, jl = j / nfx; gy = s1 * pi + 1 + jl; gx = (j - jl * nfx) * s1; }
+        }
+        int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0;
+        {
+            const int qx = gx / s1, qy = gy / s1;
+            if (gx - qx * s1 == 0) {
+                if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
+                if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
+            } else { bxs[0] = qx; pxs[0] = gx - qx * s1; nxc = 1; }
+            if (gy - qy * s1 == 0) {
+                if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
+                if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
+            } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
+        }
         double sum = 0.0;
         for (int kz = 0; kz < nzc; ++kz)
             for (int ky = 0; ky < nyc; ++ky)
@@ -192,6 +215,7 @@ k_brick_faces(const double *__restrict__ x, const double *__restrict__ dinv, dou
                     const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
                     sum += face[(size_t)bb * F + face_index<S>(pxs[kx], pys[ky], pzs[kz])];
                 }
+        const int64_t gid = gx + (int64_t)Lx * (gy + (int64_t)Ly * gz);
         if constexpr (MODE == 0) {
             y[gid] = sum;
         } else if constexpr (MODE == 1) {
@@ -206,15 +230,7 @@ k_brick_faces(const double *__restrict__ x, const double *__restrict__ dinv, dou
     }
     if constexpr (MODE == 2) {
         const double bs = block_sum(acc, sh);
-        if (!publish_partial(bs, part + n_apply_parts, &st->cnt[0], &sh_last)) return;
-        // den = sum over the apply kernel's per-brick partials, then this kernel's, fixed order
-        double v = 0.0;
-        for (int i = threadIdx.x; i < n_apply_parts + (int)gridDim.x; i += blockDim.x) v += part[i];
-        const double den = block_sum(v, sh);
-        if (threadIdx.x == 0) {
-            st->cnt[0] = 0;
-            cg_den_step(st, den);
-        }
+        if (threadIdx.x == 0) part[blockIdx.x + gridDim.x * blockIdx.y] = bs;
     }
 }
 
@@ -226,10 +242,12 @@ static BrickGeom geom_of(const cdfem_ctx *c)
     return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz};
 }
 
-static unsigned faces_grid(const cdfem_ctx *c)
+static dim3 faces_grid(const cdfem_ctx *c)
 {
-    const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
-    return (unsigned)(need < c->red_blocks ? (need < 1 ? 1 : need) : c->red_blocks);
+    const int64_t plane = c->Lx * c->Ly;
+    int64_t bx = (plane + kRedThreads - 1) / kRedThreads;
+    if (bx > 64) bx = 64;  // grid-stride beyond 64 blocks per plane (keeps the partial count small)
+    return dim3((unsigned)bx, (unsigned)c->Lz);
 }
 
 template <int D1, int Q1, unsigned K, int MODE>
@@ -240,15 +258,23 @@ static hipError_t brick_launch(cdfem_ctx *c, const double *x, const double *dinv
     const BrickGeom g = geom_of(c);
     if (which & 1) {
         const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
-        hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv,
-                           d, y, c->d_face, c->d_qd, c->d_ess, T, g, c->d_part, c->d_state);
+        if (c->brick_waves == 1)
+            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 1>), dim3(c->nblk), dim3(64), 0, c->stream, x,
+                               dinv, d, y, c->d_face, c->d_qd, c->d_ess, T, g, c->d_part, c->d_state);
+        else
+            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 2>), dim3(c->nblk), dim3(64), 0, c->stream, x,
+                               dinv, d, y, c->d_face, c->d_qd, c->d_ess, T, g, c->d_part, c->d_state);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    if (which & 2)
-        hipLaunchKernelGGL((k_brick_faces<S, MODE>), dim3(faces_grid(c)), dim3(kRedThreads), 0,
-                           c->stream, x, dinv, d, y, c->d_face, c->d_ess, g, c->d_part, c->nblk,
-                           c->d_state);
+    if (which & 2) {
+        const dim3 fg = faces_grid(c);
+        hipLaunchKernelGGL((k_brick_faces<S, MODE>), fg, dim3(kRedThreads), 0, c->stream, x, dinv, d, y,
+                           c->d_face, c->d_ess, g, c->d_part + c->nblk, c->d_state);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+
+    }
     return hipGetLastError();
 }
 
@@ -284,10 +310,242 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
                        : brick_dispatch<0>(c, x, nullptr, nullptr, y, which);
 }
 
-hipError_t launch_brick_cg(cdfem_ctx *c, const double *r, const double *dinv, double *d, double *q,
-                           int which)
+
+
+
+
+// ================================================================================================
+// Brick CG, version 2 (the Krylov hot loop on structured boxes): 2 streaming kernels + 2 one-block
+// finalizers per iteration.
+//   k_brick_cg:         d_new = M^{-1} r + beta d_old for the whole patch (recomputed by every brick
+//                       containing a dof: same inputs, bitwise-identical values), written once by its
+//                       writer brick into the OTHER d buffer (double-buffered: no brick ever reads a
+//                       d entry another brick writes in the same launch); element apply; den
+//                       contribution computed ELEMENT-WISE, den = sum_e d0_e . A_e d0_e + sum_ess d^2
+//                       (= (d, A_c d) exactly in exact arithmetic); in-LDS E->L; interior q and face
+//                       partials out.
+//   k_cg_update_faces:  q = interior q | sum of face partials | d (ess), then the CG update
+//                       x += alpha d, r -= alpha q, betanom = (r, M^{-1} r).  Face dofs are never
+//                       touched by a strided pass of their own.
+// Multi-rank slabs: zlo_shared = 1 when the local gz = 0 plane is the interface with the rank
+// below, which owns it for the dot products (remote_lo / remote_hi carry the neighbours' partial
+// sums of the interface planes; nullptr on a single GPU).
+// ================================================================================================
+// VAR 0: elem_apply3d fully unrolled; 1: elem_apply3d, plane loop; 2: low-register core
+template <int D1, int Q1, unsigned K, int VAR>
+__global__ void __launch_bounds__(64)
+k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
+           const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
+           double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
+           const Tab<D1, Q1> T, const BrickGeom g, int zlo_shared, double *__restrict__ part,
+           const KrylovState *__restrict__ st)
 {
-    return brick_dispatch<2>(c, r, dinv, d, q, which);
+    constexpr int P = D1 - 1;
+    constexpr int S = kBrick * P + 1;
+    constexpr int S2 = S * S, S3 = S * S * S;
+    constexpr int F = face_count<S>();
+    constexpr int NC = QLayout<K, 3>::nc;
+    constexpr int NQ = Q1 * Q1 * Q1;
+    __shared__ double s_in[S3];
+    __shared__ double s_out[S3];
+    if (st->done) return;
+    const double beta = st->beta;
+    const int t = threadIdx.x;
+    const int b = blockIdx.x;
+    const int bx = b % g.nbx, by = (b / g.nbx) % g.nby, bz = b / (g.nbx * g.nby);
+    const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
+    const bool lastx = bx == g.nbx - 1, lasty = by == g.nby - 1, lastz = bz == g.nbz - 1;
+
+    double den = 0.0;
+#pragma unroll
+    for (int k = 0; k < (S3 + 63) / 64; ++k) {
+        const int i = t + 64 * k;
+        if (i >= S3) break;
+        const int px = i % S, py = (i / S) % S, pz = i / S2;
+        const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
+        double v = 0.0;
+        if (gx < g.Lx && gy < g.Ly && gz < g.Lz) {
+            const int64_t gid = gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz);
+            const double dn = dinv[gid] * r[gid] + beta * d_old[gid];
+            const bool e = ess[gid] != 0;
+            const bool writer = (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
+            if (writer) {
+                d_new[gid] = dn;
+                if (e && !(zlo_shared && gz == 0)) den += dn * dn;  // (A_c d)_i = d_i on ess dofs
+            }
+            v = e ? 0.0 : dn;
+        }
+        s_in[i] = v;
+        s_out[i] = 0.0;
+    }
+    __syncthreads();
+
+    const int ex = t & 3, ey = (t >> 2) & 3, ez = t >> 4;
+    const int o0 = P * ez * S2 + P * ey * S + P * ex;
+    auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
+    const double *q0 = qd + (size_t)b * NQ * NC * kLanes;
+    double Y[D1][D1][D1];
+    if constexpr (VAR == 2)
+        elem_apply3d_lr<D1, Q1, K, decltype(xl), 1>(xl, q0, t, T, Y);
+    else if constexpr (VAR == 1)
+        elem_apply3d<D1, Q1, K, decltype(xl), 1>(xl, q0, t, T, Y);
+    else
+        elem_apply3d<D1, Q1, K, decltype(xl), Q1>(xl, q0, t, T, Y);
+
+    // element-wise den contribution d0_e . (A_e d0_e) and deterministic in-LDS E->L
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                const int o = o0 + dz * S2 + dy * S + dx;
+                den += s_in[o] * Y[dz][dy][dx];
+                s_out[o] += Y[dz][dy][dx];
+                __syncthreads();
+            }
+
+#pragma unroll
+    for (int k = 0; k < (S3 + 63) / 64; ++k) {
+        const int i = t + 64 * k;
+        if (i >= S3) break;
+        const int px = i % S, py = (i / S) % S, pz = i / S2;
+        const double v = s_out[i];
+        if (px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1) {
+            face[(size_t)b * F + face_index<S>(px, py, pz)] = v;
+            continue;
+        }
+        const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
+        if (gx >= g.Lx || gy >= g.Ly || gz >= g.Lz) continue;
+        q[gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz)] = v;  // ess rows: replaced by d in the update
+    }
+    den = wave_sum(den);
+    if (t == 0) part[b] = den;
+}
+
+template <int S>
+__global__ void __launch_bounds__(kRedThreads)
+k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ q,
+                  const double *__restrict__ d, const double *__restrict__ dinv,
+                  const double *__restrict__ face, const uint8_t *__restrict__ ess, const BrickGeom g,
+                  const FastDiv fdx, const FastDiv fdxy, int zlo_shared,
+                  const double *__restrict__ remote_lo, const double *__restrict__ remote_hi,
+                  double *__restrict__ part, const KrylovState *__restrict__ st)
+{
+    constexpr int F = face_count<S>();
+    constexpr int s1 = S - 1;
+    __shared__ double sh[kRedThreads / 64];
+    if (st->done) return;
+    const double alpha = st->alpha;
+    const int n = g.Lx * g.Ly * g.Lz;
+    const int plane = g.Lx * g.Ly;
+    double acc = 0.0;
+    for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += gridDim.x * blockDim.x) {
+        const int gz = (int)fdiv((uint32_t)gid, fdxy);
+        const int rem = gid - gz * plane;
+        const int gy = (int)fdiv((uint32_t)rem, fdx);
+        const int gx = rem - gy * g.Lx;
+        const double di = d[gid];
+        double qi;
+        if (ess[gid]) {
+            qi = di;
+        } else if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
+            int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
+            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
+            if (gx - qx * s1 == 0) {
+                if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
+                if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
+            } else { bxs[0] = qx; pxs[0] = gx - qx * s1; nxc = 1; }
+            if (gy - qy * s1 == 0) {
+                if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
+                if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
+            } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
+            if (gz - qz * s1 == 0) {
+                if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
+                if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
+            } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
+            qi = 0.0;
+            for (int kz = 0; kz < nzc; ++kz)
+                for (int ky = 0; ky < nyc; ++ky)
+                    for (int kx = 0; kx < nxc; ++kx) {
+                        const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
+                        qi += face[(size_t)bb * F + face_index<S>(pxs[kx], pys[ky], pzs[kz])];
+                    }
+        } else {
+            qi = q[gid];
+        }
+        if (!ess[gid]) {  // interface planes: add the neighbour rank's partial sums
+            if (remote_lo && gz == 0) qi += remote_lo[rem];
+            if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
+        }
+        x[gid] += alpha * di;
+        const double ri = r[gid] - alpha * qi;
+        r[gid] = ri;
+        if (!(zlo_shared && gz == 0)) acc += ri * (dinv[gid] * ri);
+    }
+    const double bs = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = bs;
+}
+
+template <int D1, int Q1, unsigned K>
+static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *dinv,
+                                   const double *d_old, double *d_new, double *q)
+{
+    const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
+    const BrickGeom g = geom_of(c);
+#define CDFEM_L(V)                                                                                  \
+    hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, V>), dim3(c->nblk), dim3(64), 0, c->stream, r, dinv, d_old, \
+                       d_new, q, c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state)
+    if (c->brick_variant == 2) CDFEM_L(2);
+    else if (c->brick_variant == 1) CDFEM_L(1);
+    else CDFEM_L(0);
+#undef CDFEM_L
+    return hipGetLastError();
+}
+
+hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
+                            double *d_new, double *q)
+{
+    const int q1 = c->rule_op.q1;
+#define CDFEM_K(D1_, Q1_)                                                                           \
+    switch (c->kinds) {                                                                             \
+    case 1: return brick_cg2_launch<D1_, Q1_, 1>(c, r, dinv, d_old, d_new, q);                      \
+    case 2: return brick_cg2_launch<D1_, Q1_, 2>(c, r, dinv, d_old, d_new, q);                      \
+    case 3: return brick_cg2_launch<D1_, Q1_, 3>(c, r, dinv, d_old, d_new, q);                      \
+    case 4: return brick_cg2_launch<D1_, Q1_, 4>(c, r, dinv, d_old, d_new, q);                      \
+    case 5: return brick_cg2_launch<D1_, Q1_, 5>(c, r, dinv, d_old, d_new, q);                      \
+    case 6: return brick_cg2_launch<D1_, Q1_, 6>(c, r, dinv, d_old, d_new, q);                      \
+    case 7: return brick_cg2_launch<D1_, Q1_, 7>(c, r, dinv, d_old, d_new, q);                      \
+    default: return hipErrorInvalidValue;                                                           \
+    }
+    if (c->p == 1 && q1 == 3) { CDFEM_K(2, 3) }
+    if (c->p == 2 && q1 == 4) { CDFEM_K(3, 4) }
+#undef CDFEM_K
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
+                                  const double *dinv, const double *remote_lo, const double *remote_hi)
+{
+    const BrickGeom g = geom_of(c);
+    const FastDiv fdx = make_fastdiv((uint32_t)c->Lx), fdxy = make_fastdiv((uint32_t)(c->Lx * c->Ly));
+    // one dof per thread (no grid-stride up to 16384 blocks): the face gathers are dependent
+    // loads, so every dof's chain must be in flight at once
+    const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
+    const unsigned grid = (unsigned)(need < 16384 ? need : 16384);
+    if (c->p == 1)
+        hipLaunchKernelGGL(k_cg_update_faces<kBrick * 1 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
+                           x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
+                           remote_hi, c->d_part, c->d_state);
+    else if (c->p == 2)
+        hipLaunchKernelGGL(k_cg_update_faces<kBrick * 2 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
+                           x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
+                           remote_hi, c->d_part, c->d_state);
+    else
+        return hipErrorInvalidValue;
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_update_fin(c, (int)grid);
 }
 
 }  // namespace cdfem

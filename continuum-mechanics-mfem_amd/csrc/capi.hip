@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <stdexcept>
@@ -90,7 +91,7 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_ess); dfree(c->d_ess_list); dfree(c->d_qd); dfree(c->d_Ye); dfree(c->d_dinv);
     for (auto &w : c->d_w) dfree(w);
     dfree(c->d_part); dfree(c->d_gm); dfree(c->d_gm_small);
-    dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones);
+    dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones); dfree(c->d_dalt);
     c->gm_cap = 0;
     c->mesh_ready = c->pa_ready = c->dinv_ready = false;
     c->structured = false;
@@ -165,7 +166,7 @@ void build_layout(cdfem_ctx *c, const std::vector<int32_t> &perm)
     c->d_e2l_pos = dalloc<int32_t>(pos.size());
     c->d_perm = dalloc<int32_t>(perm.size());
     c->d_Ye = dalloc<double>((size_t)c->nblk * nd * kLanes);
-    c->d_part = dalloc<double>((size_t)c->red_blocks + c->nblk);
+    c->d_part = dalloc<double>((size_t)c->red_blocks + c->nblk + 64 * 8192 + 16384);
     HIPCHK(hipMemcpyAsync(c->d_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_e2l_off, cnt.data(), (nl + 1) * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_e2l_pos, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, c->stream));
@@ -246,12 +247,15 @@ void ensure_dinv(cdfem_ctx *c)
     c->dinv_ready = true;
 }
 
-// brick-path CG: 3 kernels per iteration (brick apply with fused direction update, face sum with
-// den/alpha, update with betanom/beta); identical MFEM CGSolver arithmetic
+// brick-path CG (MFEM CGSolver arithmetic): per iteration k_brick_cg (direction + apply + den
+// partials) -> den finalizer -> k_cg_update_faces (q assembly + x, r update + betanom partials) ->
+// betanom finalizer.  The search direction alternates between two buffers.
 void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, double *dX,
                     cdfem_solver_result &res)
 {
-    double *x = c->d_w[2], *r = c->d_w[3], *q = c->d_w[4], *d = c->d_w[5];
+    double *x = c->d_w[2], *r = c->d_w[3], *q = c->d_w[4];
+    if (!c->d_dalt) c->d_dalt = dalloc<double>(c->nl);
+    double *dprev = c->d_w[5], *dcur = c->d_dalt;
     const double *dinv;
     if (p.pc == CDFEM_PC_JACOBI) {
         ensure_dinv(c);
@@ -262,13 +266,13 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     const int check = p.check_every > 0 ? p.check_every : 16;
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
-    HIPCHK(launch_cg_init(c, dB, x, r, q, d, dinv, p.rel_tol, p.abs_tol, p.max_iter));
+    HIPCHK(launch_cg_init(c, dB, x, r, q, dprev, dinv, p.rel_tol, p.abs_tol, p.max_iter));
     auto apply = [&] {
         prof_mark(c, CDFEM_K_APPLY, true);
-        HIPCHK(launch_brick_cg(c, r, dinv, d, q, 1));
+        HIPCHK(launch_brick_cg2(c, r, dinv, dprev, dcur, q));
         prof_mark(c, CDFEM_K_APPLY, false);
         prof_mark(c, CDFEM_K_E2L, true);
-        HIPCHK(launch_brick_cg(c, r, dinv, d, q, 2));
+        HIPCHK(launch_den_fin(c, c->nblk));
         prof_mark(c, CDFEM_K_E2L, false);
     };
     apply();
@@ -276,8 +280,9 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     for (;;) {
         for (int k = 0; k < check && launched < p.max_iter; ++k, ++launched) {
             prof_mark(c, CDFEM_K_UPDATE, true);
-            HIPCHK(launch_cg_update_noz(c, x, r, q, d, dinv));
+            HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv, nullptr, nullptr));
             prof_mark(c, CDFEM_K_UPDATE, false);
+            std::swap(dprev, dcur);
             apply();
         }
         HIPCHK(hipMemcpyAsync(c->h_state, c->d_state, sizeof(KrylovState), hipMemcpyDeviceToHost,
@@ -373,6 +378,7 @@ int cdfem_create(int device, cdfem_ctx **out)
     cdfem_ctx *c = new (std::nothrow) cdfem_ctx();
     if (!c) return CDFEM_ERR_HIP;
     c->device = device;
+    if (const char *w = std::getenv("CDFEM_BRICK_WAVES")) c->brick_waves = std::atoi(w) == 1 ? 1 : 2;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_state, sizeof(KrylovState)) != hipSuccess ||
@@ -707,6 +713,52 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
         dev_out(c, X, where, dX, c->nl);
         HIPCHK(hipStreamSynchronize(c->stream));
         return res->converged ? CDFEM_OK : CDFEM_ERR_NOT_CONVERGED;
+    });
+}
+
+int cdfem_stream_bench(cdfem_ctx *c, int mode, size_t bytes, int reps, double *gbps)
+{
+    return guarded(c, [&] {
+        if (!gbps || reps < 1 || mode < 0 || mode > 2) throw ArgError("bad stream bench arguments");
+        const int64_t n = (int64_t)(bytes / 16) * 2;
+        double *a = dalloc<double>(n), *b = dalloc<double>(n);
+        HIPCHK(hipMemsetAsync(a, 0, n * 8, c->stream));
+        HIPCHK(hipMemsetAsync(b, 0, n * 8, c->stream));
+        HIPCHK(launch_stream(c, mode, a, b, n));  // warm-up
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipEventRecord(e0, c->stream));
+        for (int i = 0; i < reps; ++i) HIPCHK(launch_stream(c, mode, a, b, n));
+        HIPCHK(hipEventRecord(e1, c->stream));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        dfree(a);
+        dfree(b);
+        const double moved = (mode == 2 ? 2.0 : 1.0) * 8.0 * (double)n * reps;
+        *gbps = moved / (ms * 1e-3) / 1e9;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
+{
+    return guarded(c, [&] {
+        if (!key) throw ArgError("key is null");
+        const std::string k(key);
+        if (k == "brick_variant") {
+            if (value < 0 || value > 2) throw ArgError("brick_variant must be 0, 1 or 2");
+            c->brick_variant = value;
+        } else if (k == "brick_waves") {
+            if (value != 1 && value != 2) throw ArgError("brick_waves must be 1 or 2");
+            c->brick_waves = value;
+        } else {
+            throw ArgError("unknown option " + k);
+        }
+        return CDFEM_OK;
     });
 }
 

@@ -46,7 +46,7 @@ int rule_points_1d(int which, int dim, int p);
 struct KrylovState {
     double nom, nom0, den, alpha, beta, betanom, r0;
     int iter, done, converged, final_iter, max_iter, first_den;
-    unsigned cnt[4];  // last-block arrival counters (reset by the last arriver)
+    unsigned reserved[4];
 };
 
 struct ProfileSlot {
@@ -55,6 +55,9 @@ struct ProfileSlot {
     double total_ms = 0.0;
     int64_t count = 0;
 };
+
+// ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
+hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 
 }  // namespace cdfem
 
@@ -85,7 +88,11 @@ struct cdfem_ctx {
     int64_t Lx = 0, Ly = 0, Lz = 0;     // dof lattice per axis
     double *d_face = nullptr;           // [nblk][F] brick-face partial sums
     double *d_ones = nullptr;           // all-ones vector (unpreconditioned brick CG)
+    double *d_dalt = nullptr;           // second search-direction buffer (brick CG)
     int nface = 0;                      // F
+    int brick_waves = 2;                // register budget of k_brick3d (CDFEM_BRICK_WAVES)
+    int brick_variant = 0;              // element core of k_brick_cg (0 unrolled, 1 plane loop, 2 low-reg)
+    int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)
 
     // rules
     cdfem::Rule1D rule_op, rule_lf, rule_err;
@@ -133,9 +140,7 @@ constexpr int kBrick = 4;               // elements per brick edge (4^3 = 64 = o
 bool brick_supported(int dim, int p);
 // y = A x (constrained: ess in -> 0, y[ess] = x[ess]); fused E->L through LDS + face partials
 hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool constrained, int which);
-// CG-fused: d = M^{-1} r + beta d (in place), q = A_c d, den = (d, q) -> state (alpha, nom)
-hipError_t launch_brick_cg(cdfem_ctx *c, const double *r, const double *dinv, double *d, double *q,
-                           int which);  // which: 1 brick kernel, 2 face kernel, 3 both
+
 
 // ---- vector kernels (vec_kernels.hip) --------------------------------------------------------
 // y = E->L sum of Ye; constrained: y[ess] = x[ess]; if dot_part != nullptr also reduces
@@ -156,7 +161,19 @@ hipError_t launch_cg_direction(cdfem_ctx *c, const double *z, double *d);
 hipError_t launch_cg_update_noz(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
                                 const double *dinv);
 hipError_t launch_zero(cdfem_ctx *c, double *y);
+// one-block finalizers: den = sum(d_part[0..nparts)) (MFEM CG den step); betanom (update step)
+hipError_t launch_den_fin(cdfem_ctx *c, int nparts);
+hipError_t launch_update_fin(cdfem_ctx *c, int nparts);
+// brick CG v2 (brick_kernels.hip): d_new = M^{-1} r + beta d_old, q/face partials, den partials
+hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
+                            double *d_new, double *q);
+// q from interior/face partials (+ remote interface sums), x += alpha d, r -= alpha q, betanom
+hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
+                                  const double *dinv, const double *remote_lo, const double *remote_hi);
 // generic deterministic dot into host-visible scalar via state (used by GMRES / tests)
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out);
+
+// ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
+hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 
 }  // namespace cdfem

@@ -38,10 +38,35 @@ struct QLayout {
     static constexpr int nc = oM + (kM ? 1 : 0);
 };
 
+// qdata layout inside one quadrature point's block of NC*64 doubles: components 2p, 2p+1 are
+// interleaved per lane ([pair][lane][2]) so a wave reads them with ONE 16-byte load per lane
+// (dwordx4: 6.45 TB/s on MI355X vs 5.90 TB/s for 8-byte loads); an odd last component follows as
+// [lane].  qd_offset() is the single definition used by setup, apply and diagonal kernels.
+__host__ __device__ constexpr int qd_offset(int c, int lane, int nc)
+{
+    return (c < (nc & ~1)) ? ((c >> 1) * kLanes + lane) * 2 + (c & 1) : (nc & ~1) * kLanes + lane;
+}
+
+template <int NC>
+__device__ __forceinline__ void load_qp(const double *__restrict__ qp, int lane, double (&v)[NC])
+{
+#pragma unroll
+    for (int p = 0; p < NC / 2; ++p) {
+        const double2 w = reinterpret_cast<const double2 *>(qp + p * 2 * kLanes)[lane];
+        v[2 * p] = w.x;
+        v[2 * p + 1] = w.y;
+    }
+    if constexpr (NC & 1) v[NC - 1] = qp[(NC - 1) * kLanes + lane];
+}
+
 // Y = A_e X for one element: X, Y lexicographic [dz][dy][dx]; q0 points at this element's
-// qdata for q = 0 (component stride kLanes, point stride NC * kLanes).
-template <int D1, int Q1, unsigned K>
-__device__ __forceinline__ void elem_apply3d(const double (&X)[D1][D1][D1], const double *__restrict__ q0,
+// block's qdata (q = 0, lane 0; point stride NC * kLanes), lane = element.  X is read through the
+// loader xl(dz, dy, dx) once per quadrature plane, so a caller holding X in LDS keeps only one
+// plane's worth of it live in registers.  QZU = unroll factor of the quadrature-plane loop
+// (Q1: straight-line code, the compiler hoists qdata loads across planes; 1: one plane's loads
+// in flight, ~250 VGPRs at p = 2, two waves per SIMD).
+template <int D1, int Q1, unsigned K, typename XL, int QZU = Q1>
+__device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restrict__ q0, int lane,
                                              const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
 {
     using L = QLayout<K, 3>;
@@ -53,7 +78,7 @@ __device__ __forceinline__ void elem_apply3d(const double (&X)[D1][D1][D1], cons
 #pragma unroll
             for (int dx = 0; dx < D1; ++dx) Y[dz][dy][dx] = 0.0;
 
-#pragma unroll
+#pragma unroll QZU
     for (int qz = 0; qz < Q1; ++qz) {
         // contract z
         double T0[D1][D1], Tz[D1][D1];
@@ -64,8 +89,9 @@ __device__ __forceinline__ void elem_apply3d(const double (&X)[D1][D1][D1], cons
                 double s0 = 0.0, s1 = 0.0;
 #pragma unroll
                 for (int dz = 0; dz < D1; ++dz) {
-                    s0 += T.B[qz][dz] * X[dz][dy][dx];
-                    s1 += T.G[qz][dz] * X[dz][dy][dx];
+                    const double xv = xl(dz, dy, dx);
+                    s0 += T.B[qz][dz] * xv;
+                    s1 += T.G[qz][dz] * xv;
                 }
                 T0[dy][dx] = s0;
                 Tz[dy][dx] = s1;
@@ -107,20 +133,16 @@ __device__ __forceinline__ void elem_apply3d(const double (&X)[D1][D1][D1], cons
                     uz += T.B[qx][dx] * az[dx];
                 }
                 const int q = qx + Q1 * (qy + Q1 * qz);
-                const double *qq = q0 + (size_t)q * NC * kLanes;
+                double qv[NC];
+                load_qp<NC>(q0 + (size_t)q * NC * kLanes, lane, qv);
                 double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
                 if constexpr (L::kD) {
-                    const double d00 = qq[0 * kLanes], d01 = qq[1 * kLanes], d02 = qq[2 * kLanes];
-                    const double d11 = qq[3 * kLanes], d12 = qq[4 * kLanes], d22 = qq[5 * kLanes];
-                    gx = d00 * ux + d01 * uy + d02 * uz;
-                    gy = d01 * ux + d11 * uy + d12 * uz;
-                    gz = d02 * ux + d12 * uy + d22 * uz;
+                    gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;
+                    gy = qv[1] * ux + qv[3] * uy + qv[4] * uz;
+                    gz = qv[2] * ux + qv[4] * uy + qv[5] * uz;
                 }
-                if constexpr (L::kC) {
-                    vv = qq[(L::oC + 0) * kLanes] * ux + qq[(L::oC + 1) * kLanes] * uy +
-                         qq[(L::oC + 2) * kLanes] * uz;
-                }
-                if constexpr (L::kM) vv += qq[L::oM * kLanes] * u;
+                if constexpr (L::kC) vv = qv[L::oC] * ux + qv[L::oC + 1] * uy + qv[L::oC + 2] * uz;
+                if constexpr (L::kM) vv += qv[L::oM] * u;
                 // transposed contraction in x
 #pragma unroll
                 for (int dx = 0; dx < D1; ++dx) {
@@ -160,6 +182,120 @@ __device__ __forceinline__ void elem_apply3d(const double (&X)[D1][D1][D1], cons
                 }
     }
 
+}
+
+}  // namespace cdfem
+
+namespace cdfem {
+
+// Low-register variant of elem_apply3d: no per-plane intermediates (T0/Tz, RT/RTz).  For every
+// (qz, qy) pair the y/z-contracted input a[dx] = sum_{dz,dy} Bz By X is formed straight from the
+// loader (LDS) and the transposed result is folded straight into Y.  ~35% more FMAs, ~70 fewer
+// VGPRs; the loader is called 16x per element instead of 4x.
+template <int D1, int Q1, unsigned K, typename XL, int QZU = 1>
+__device__ __forceinline__ void elem_apply3d_lr(const XL &xl, const double *__restrict__ q0, int lane,
+                                                const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
+{
+    using L = QLayout<K, 3>;
+    constexpr int NC = L::nc;
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) Y[dz][dy][dx] = 0.0;
+#pragma unroll QZU
+    for (int qz = 0; qz < Q1; ++qz) {
+#pragma unroll
+        for (int qy = 0; qy < Q1; ++qy) {
+            double a[D1], ay[D1], az[D1];
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) { a[dx] = 0.0; ay[dx] = 0.0; az[dx] = 0.0; }
+#pragma unroll
+            for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+                for (int dy = 0; dy < D1; ++dy) {
+                    const double bb = T.B[qz][dz] * T.B[qy][dy];
+                    const double bg = T.B[qz][dz] * T.G[qy][dy];
+                    const double gb = T.G[qz][dz] * T.B[qy][dy];
+#pragma unroll
+                    for (int dx = 0; dx < D1; ++dx) {
+                        const double xv = xl(dz, dy, dx);
+                        a[dx] += bb * xv;
+                        ay[dx] += bg * xv;
+                        az[dx] += gb * xv;
+                    }
+                }
+            double Rv[D1], Ry[D1], Rz[D1];
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) { Rv[dx] = 0.0; Ry[dx] = 0.0; Rz[dx] = 0.0; }
+#pragma unroll
+            for (int qx = 0; qx < Q1; ++qx) {
+                double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+                for (int dx = 0; dx < D1; ++dx) {
+                    u += T.B[qx][dx] * a[dx];
+                    ux += T.G[qx][dx] * a[dx];
+                    uy += T.B[qx][dx] * ay[dx];
+                    uz += T.B[qx][dx] * az[dx];
+                }
+                const int q = qx + Q1 * (qy + Q1 * qz);
+                double qv[NC];
+                load_qp<NC>(q0 + (size_t)q * NC * kLanes, lane, qv);
+                double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
+                if constexpr (L::kD) {
+                    gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;
+                    gy = qv[1] * ux + qv[3] * uy + qv[4] * uz;
+                    gz = qv[2] * ux + qv[4] * uy + qv[5] * uz;
+                }
+                if constexpr (L::kC) vv = qv[L::oC] * ux + qv[L::oC + 1] * uy + qv[L::oC + 2] * uz;
+                if constexpr (L::kM) vv += qv[L::oM] * u;
+#pragma unroll
+                for (int dx = 0; dx < D1; ++dx) {
+                    if constexpr (L::kD) {
+                        Rv[dx] += T.B[qx][dx] * vv + T.G[qx][dx] * gx;
+                        Ry[dx] += T.B[qx][dx] * gy;
+                        Rz[dx] += T.B[qx][dx] * gz;
+                    } else {
+                        Rv[dx] += T.B[qx][dx] * vv;
+                    }
+                }
+            }
+#pragma unroll
+            for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+                for (int dy = 0; dy < D1; ++dy) {
+                    const double bb = T.B[qz][dz] * T.B[qy][dy];
+                    const double bg = T.B[qz][dz] * T.G[qy][dy];
+                    const double gb = T.G[qz][dz] * T.B[qy][dy];
+#pragma unroll
+                    for (int dx = 0; dx < D1; ++dx) {
+                        if constexpr (L::kD)
+                            Y[dz][dy][dx] += bb * Rv[dx] + bg * Ry[dx] + gb * Rz[dx];
+                        else
+                            Y[dz][dy][dx] += bb * Rv[dx];
+                    }
+                }
+        }
+    }
+}
+
+// exact unsigned division by a run-time divisor: n / d == (n * m) >> k for n < 2^31
+struct FastDiv {
+    uint64_t m;
+    uint32_t k, d;
+};
+inline FastDiv make_fastdiv(uint32_t d)
+{
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    const uint32_t k = 32 + l;
+    const uint64_t m = ((1ull << k) + d - 1) / d;
+    return FastDiv{m, k, d};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f)
+{
+    return (uint32_t)(((uint64_t)n * f.m) >> f.k);
 }
 
 }  // namespace cdfem

@@ -56,8 +56,8 @@ k_apply3d(const int32_t *__restrict__ map, const double *__restrict__ x,
             }
 
     double Y[D1][D1][D1];
-    const double *q0 = qd + (size_t)b * NQ * NC * kLanes + lane;
-    elem_apply3d<D1, Q1, K>(X, q0, T, Y);
+    const double *q0 = qd + (size_t)b * NQ * NC * kLanes;
+    elem_apply3d<D1, Q1, K>([&](int dz, int dy, int dx) { return X[dz][dy][dx]; }, q0, lane, T, Y);
 
     double *yp = Ye + (size_t)b * ND * kLanes + lane;
 #pragma unroll
@@ -106,7 +106,7 @@ k_apply2d(const int32_t *__restrict__ map, const double *__restrict__ x,
 #pragma unroll
         for (int dx = 0; dx < D1; ++dx) Y[dy][dx] = 0.0;
 
-    const double *q0 = qd + (size_t)b * NQ * NC * kLanes + lane;
+    const double *q0 = qd + (size_t)b * NQ * NC * kLanes;
 #pragma unroll
     for (int qy = 0; qy < Q1; ++qy) {
         double a[D1], ay[D1];
@@ -133,15 +133,15 @@ k_apply2d(const int32_t *__restrict__ map, const double *__restrict__ x,
                 uy += T.B[qx][dx] * ay[dx];
             }
             const int q = qx + Q1 * qy;
-            const double *qq = q0 + (size_t)q * NC * kLanes;
+            double qv[NC];
+            load_qp<NC>(q0 + (size_t)q * NC * kLanes, lane, qv);
             double vv = 0.0, gx = 0.0, gy = 0.0;
             if constexpr (L::kD) {
-                const double d00 = qq[0], d01 = qq[kLanes], d11 = qq[2 * kLanes];
-                gx = d00 * ux + d01 * uy;
-                gy = d01 * ux + d11 * uy;
+                gx = qv[0] * ux + qv[1] * uy;
+                gy = qv[1] * ux + qv[2] * uy;
             }
-            if constexpr (L::kC) vv = qq[L::oC * kLanes] * ux + qq[(L::oC + 1) * kLanes] * uy;
-            if constexpr (L::kM) vv += qq[L::oM * kLanes] * u;
+            if constexpr (L::kC) vv = qv[L::oC] * ux + qv[L::oC + 1] * uy;
+            if constexpr (L::kM) vv += qv[L::oM] * u;
 #pragma unroll
             for (int dx = 0; dx < D1; ++dx) {
                 if constexpr (L::kD) {
@@ -254,9 +254,9 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
     const int q = (int)((t / kLanes) % nq);
     const int b = (int)(t / ((int64_t)kLanes * nq));
     const int e = perm[(size_t)b * kLanes + lane];
-    double *out = qd + ((size_t)b * nq + q) * nc * kLanes + lane;
+    double *out = qd + ((size_t)b * nq + q) * nc * kLanes;
     if (e < 0 || e >= ne) {
-        for (int k = 0; k < nc; ++k) out[k * kLanes] = 0.0;
+        for (int k = 0; k < nc; ++k) out[qd_offset(k, lane, nc)] = 0.0;
         return;
     }
     double xi[3], W;
@@ -273,7 +273,7 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
             for (int j = i; j < DIM; ++j) {
                 double acc = 0.0;
                 for (int k = 0; k < DIM; ++k) acc += A[i][k] * A[j][k];
-                out[(o++) * kLanes] = s * acc;
+                out[qd_offset(o++, lane, nc)] = s * acc;
             }
     }
     if (kinds & CDFEM_CONVECTION) {
@@ -283,12 +283,12 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
         for (int i = 0; i < DIM; ++i) {
             double acc = 0.0;
             for (int k = 0; k < DIM; ++k) acc += A[i][k] * cv[k];
-            out[(o++) * kLanes] = W * alpha * acc;
+            out[qd_offset(o++, lane, nc)] = W * alpha * acc;
         }
     }
     if (kinds & CDFEM_MASS) {
         const double s = mass_q ? mass_q[eq] : mass;
-        out[(o++) * kLanes] = W * s * det;
+        out[qd_offset(o++, lane, nc)] = W * s * det;
     }
 }
 
@@ -340,27 +340,28 @@ k_diag_elem(const double *__restrict__ qd, int nblk, int nd, const Rule1D r, uns
     const int oM = oC + ((kinds & CDFEM_CONVECTION) ? DIM : 0);
     double acc = 0.0;
     for (int q = 0; q < nq; ++q) {
-        const double *qq = qd + ((size_t)b * nq + q) * nc * kLanes + lane;
+        const double *qb = qd + ((size_t)b * nq + q) * nc * kLanes;
+        auto qq = [&](int k) { return qb[qd_offset(k, lane, nc)]; };
         double phi, g[3];
         basis_at(l, q, DIM, r, phi, g);
         if (kinds & CDFEM_DIFFUSION) {
             if (DIM == 3) {
-                const double d00 = qq[0], d01 = qq[kLanes], d02 = qq[2 * kLanes];
-                const double d11 = qq[3 * kLanes], d12 = qq[4 * kLanes], d22 = qq[5 * kLanes];
+                const double d00 = qq(0), d01 = qq(1), d02 = qq(2);
+                const double d11 = qq(3), d12 = qq(4), d22 = qq(5);
                 acc += g[0] * (d00 * g[0] + d01 * g[1] + d02 * g[2]) +
                        g[1] * (d01 * g[0] + d11 * g[1] + d12 * g[2]) +
                        g[2] * (d02 * g[0] + d12 * g[1] + d22 * g[2]);
             } else {
-                const double d00 = qq[0], d01 = qq[kLanes], d11 = qq[2 * kLanes];
+                const double d00 = qq(0), d01 = qq(1), d11 = qq(2);
                 acc += g[0] * (d00 * g[0] + d01 * g[1]) + g[1] * (d01 * g[0] + d11 * g[1]);
             }
         }
         if (kinds & CDFEM_CONVECTION) {
             double cg = 0.0;
-            for (int k = 0; k < DIM; ++k) cg += qq[(oC + k) * kLanes] * g[k];
+            for (int k = 0; k < DIM; ++k) cg += qq(oC + k) * g[k];
             acc += phi * cg;
         }
-        if (kinds & CDFEM_MASS) acc += qq[oM * kLanes] * phi * phi;
+        if (kinds & CDFEM_MASS) acc += qq(oM) * phi * phi;
     }
     Ye[t] = acc;  // t == (b*nd + l)*64 + lane
 }

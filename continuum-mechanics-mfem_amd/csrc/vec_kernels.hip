@@ -26,7 +26,6 @@ k_e2l(const int32_t *__restrict__ off, const int32_t *__restrict__ pos,
       double *__restrict__ y, int64_t nl, double *__restrict__ part, KrylovState *__restrict__ st)
 {
     __shared__ double sh[kRedThreads / 64];
-    __shared__ int sh_last;
     if (CG && st->done) return;
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -43,13 +42,7 @@ k_e2l(const int32_t *__restrict__ off, const int32_t *__restrict__ pos,
         if (CG) acc += v * x[i];
     }
     if (!CG) return;
-    const double bs = block_sum(acc, sh);
-    if (!publish_partial(bs, part, &st->cnt[0], &sh_last)) return;
-    const double den = sum_partials(part, gridDim.x, sh);
-    if (threadIdx.x == 0) {
-        st->cnt[0] = 0;
-        cg_den_step(st, den);
-    }
+    store_partial(block_sum(acc, sh), part);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -58,11 +51,9 @@ k_e2l(const int32_t *__restrict__ off, const int32_t *__restrict__ pos,
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_init(const double *__restrict__ B, double *__restrict__ x, double *__restrict__ r,
           double *__restrict__ z, double *__restrict__ d, const double *__restrict__ dinv, int64_t n,
-          double rel_tol, double abs_tol, int max_iter, double *__restrict__ part,
-          KrylovState *__restrict__ st)
+          double *__restrict__ part)
 {
     __shared__ double sh[kRedThreads / 64];
-    __shared__ int sh_last;
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -74,11 +65,17 @@ k_cg_init(const double *__restrict__ B, double *__restrict__ x, double *__restri
         d[i] = zi;
         acc += zi * ri;
     }
-    const double bs = block_sum(acc, sh);
-    if (!publish_partial(bs, part, &st->cnt[2], &sh_last)) return;
-    const double nom = sum_partials(part, gridDim.x, sh);
+    store_partial(block_sum(acc, sh), part);
+}
+
+// one block: nom = sum of the init partials; MFEM CGSolver initial convergence test
+__global__ void __launch_bounds__(1024)
+k_cg_init_fin(const double *__restrict__ part, int n, double rel_tol, double abs_tol, int max_iter,
+              KrylovState *__restrict__ st)
+{
+    __shared__ double sh[1024 / 64];
+    const double nom = sum_partials(part, n, sh);
     if (threadIdx.x == 0) {
-        st->cnt[2] = 0;
         st->nom = st->nom0 = st->betanom = nom;
         const double r0 = fmax(nom * rel_tol * rel_tol, abs_tol * abs_tol);
         st->r0 = r0;
@@ -100,6 +97,16 @@ k_cg_init(const double *__restrict__ B, double *__restrict__ x, double *__restri
     }
 }
 
+// one block: den = sum of the partials (Mult kernels), MFEM CG den step
+__global__ void __launch_bounds__(1024)
+k_cg_den_fin(const double *__restrict__ part, int n, KrylovState *__restrict__ st)
+{
+    __shared__ double sh[1024 / 64];
+    if (st->done) return;
+    const double den = sum_partials(part, n, sh);
+    if (threadIdx.x == 0) cg_den_step(st, den);
+}
+
 // x += alpha d, r -= alpha z, z = M^{-1} r, betanom = (r, z); last block: convergence test
 template <bool STORE_Z>
 __global__ void __launch_bounds__(kRedThreads)
@@ -108,12 +115,30 @@ k_cg_update(double *__restrict__ x, double *__restrict__ r, double *__restrict__
             double *__restrict__ part, KrylovState *__restrict__ st)
 {
     __shared__ double sh[kRedThreads / 64];
-    __shared__ int sh_last;
     if (st->done) return;
     const double alpha = st->alpha;
     double acc = 0.0;
+    // 16-byte accesses: pairs (2i, 2i+1); the odd tail element is taken by thread 0 of block 0
+    const int64_t n2 = n >> 1;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+        double2 xv = reinterpret_cast<const double2 *>(x)[i];
+        const double2 dv = reinterpret_cast<const double2 *>(d)[i];
+        double2 rv = reinterpret_cast<const double2 *>(r)[i];
+        const double2 qv = reinterpret_cast<const double2 *>(z)[i];
+        double2 mv = make_double2(1.0, 1.0);
+        if (dinv) mv = reinterpret_cast<const double2 *>(dinv)[i];
+        xv.x += alpha * dv.x; xv.y += alpha * dv.y;
+        rv.x -= alpha * qv.x; rv.y -= alpha * qv.y;
+        const double z0 = dinv ? mv.x * rv.x : rv.x, z1 = dinv ? mv.y * rv.y : rv.y;
+        reinterpret_cast<double2 *>(x)[i] = xv;
+        reinterpret_cast<double2 *>(r)[i] = rv;
+        if (STORE_Z) reinterpret_cast<double2 *>(z)[i] = make_double2(z0, z1);
+        acc += rv.x * z0;
+        acc += rv.y * z1;
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        const int64_t i = n - 1;
         x[i] += alpha * d[i];
         const double ri = r[i] - alpha * z[i];
         r[i] = ri;
@@ -121,11 +146,17 @@ k_cg_update(double *__restrict__ x, double *__restrict__ r, double *__restrict__
         if (STORE_Z) z[i] = zi;
         acc += ri * zi;
     }
-    const double bs = block_sum(acc, sh);
-    if (!publish_partial(bs, part, &st->cnt[1], &sh_last)) return;
-    const double betanom = sum_partials(part, gridDim.x, sh);
+    store_partial(block_sum(acc, sh), part);
+}
+
+// one block: betanom = sum of the update partials; MFEM CGSolver convergence test and beta
+__global__ void __launch_bounds__(1024)
+k_cg_update_fin(const double *__restrict__ part, int n, KrylovState *__restrict__ st)
+{
+    __shared__ double sh[1024 / 64];
+    if (st->done) return;
+    const double betanom = sum_partials(part, n, sh);
     if (threadIdx.x == 0) {
-        st->cnt[1] = 0;
         st->betanom = betanom;
         const int i = st->iter;
         if (betanom < 0.0) {
@@ -187,24 +218,24 @@ __global__ void k_dinv(const uint8_t *__restrict__ ess, const double *__restrict
         dinv[i] = ess[i] ? 1.0 : 1.0 / diag[i];
 }
 
-// deterministic dot into *out (two-level: partials then last block)
+// deterministic dot: partials, then k_dot_fin
 __global__ void __launch_bounds__(kRedThreads)
-k_dot(const double *__restrict__ a, const double *__restrict__ b, int64_t n,
-      double *__restrict__ part, unsigned *__restrict__ cnt, double *__restrict__ out)
+k_dot(const double *__restrict__ a, const double *__restrict__ b, int64_t n, double *__restrict__ part)
 {
     __shared__ double sh[kRedThreads / 64];
-    __shared__ int sh_last;
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         acc += a[i] * b[i];
-    const double bs = block_sum(acc, sh);
-    if (!publish_partial(bs, part, cnt, &sh_last)) return;
-    const double s = sum_partials(part, gridDim.x, sh);
-    if (threadIdx.x == 0) {
-        *cnt = 0;
-        *out = s;
-    }
+    store_partial(block_sum(acc, sh), part);
+}
+
+__global__ void __launch_bounds__(1024)
+k_dot_fin(const double *__restrict__ part, int n, double *__restrict__ out)
+{
+    __shared__ double sh[1024 / 64];
+    const double s = sum_partials(part, n, sh);
+    if (threadIdx.x == 0) *out = s;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -216,13 +247,29 @@ static inline unsigned red_grid(cdfem_ctx *c, int64_t n)
     return (unsigned)(need < c->red_blocks ? (need < 1 ? 1 : need) : c->red_blocks);
 }
 
+hipError_t launch_den_fin(cdfem_ctx *c, int nparts)
+{
+    hipLaunchKernelGGL(k_cg_den_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, nparts, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_update_fin(cdfem_ctx *c, int nparts)
+{
+    hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, nparts, c->d_state);
+    return hipGetLastError();
+}
+
 hipError_t launch_e2l(cdfem_ctx *c, const double *Ye, const double *x, double *y, bool con,
                       int cg_mode)
 {
     const dim3 g(red_grid(c, c->nl)), b(kRedThreads);
-    if (cg_mode)
+    if (cg_mode) {
         hipLaunchKernelGGL((k_e2l<true, true>), g, b, 0, c->stream, c->d_e2l_off, c->d_e2l_pos,
                            c->d_ess, Ye, x, y, c->nl, c->d_part, c->d_state);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return launch_den_fin(c, (int)g.x);
+    }
     else if (con)
         hipLaunchKernelGGL((k_e2l<true, false>), g, b, 0, c->stream, c->d_e2l_off, c->d_e2l_pos,
                            c->d_ess, Ye, x, y, c->nl, c->d_part, c->d_state);
@@ -264,16 +311,21 @@ hipError_t launch_dinv(cdfem_ctx *c, const double *diag, double *dinv)
 hipError_t launch_cg_init(cdfem_ctx *c, const double *B, double *x, double *r, double *z, double *d,
                           const double *dinv, double rel_tol, double abs_tol, int max_iter)
 {
-    hipLaunchKernelGGL(k_cg_init, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, B, x, r,
-                       z, d, dinv, c->nl, rel_tol, abs_tol, max_iter, c->d_part, c->d_state);
+    const unsigned g = red_grid(c, c->nl);
+    hipLaunchKernelGGL(k_cg_init, dim3(g), dim3(kRedThreads), 0, c->stream, B, x, r, z, d, dinv, c->nl,
+                       c->d_part);
+    hipLaunchKernelGGL(k_cg_init_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g, rel_tol,
+                       abs_tol, max_iter, c->d_state);
     return hipGetLastError();
 }
 
 hipError_t launch_cg_update(cdfem_ctx *c, double *x, double *r, double *z, const double *d,
                             const double *dinv)
 {
-    hipLaunchKernelGGL(k_cg_update<true>, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, x,
-                       r, z, d, dinv, c->nl, c->d_part, c->d_state);
+    const unsigned g = red_grid(c, c->nl);
+    hipLaunchKernelGGL(k_cg_update<true>, dim3(g), dim3(kRedThreads), 0, c->stream, x, r, z, d, dinv,
+                       c->nl, c->d_part, c->d_state);
+    hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g, c->d_state);
     return hipGetLastError();
 }
 
@@ -281,8 +333,10 @@ hipError_t launch_cg_update_noz(cdfem_ctx *c, double *x, double *r, const double
                                 const double *dinv)
 {
     // k_cg_update reads "z" as A d: pass q there; the z output is not written
-    hipLaunchKernelGGL(k_cg_update<false>, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, x,
-                       r, const_cast<double *>(q), d, dinv, c->nl, c->d_part, c->d_state);
+    const unsigned g = red_grid(c, c->nl);
+    hipLaunchKernelGGL(k_cg_update<false>, dim3(g), dim3(kRedThreads), 0, c->stream, x, r,
+                       const_cast<double *>(q), d, dinv, c->nl, c->d_part, c->d_state);
+    hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g, c->d_state);
     return hipGetLastError();
 }
 
@@ -307,8 +361,9 @@ hipError_t launch_cg_direction(cdfem_ctx *c, const double *z, double *d)
 
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out)
 {
-    hipLaunchKernelGGL(k_dot, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, a, b, c->nl,
-                       c->d_part, &c->d_state->cnt[3], d_out);
+    const unsigned g = red_grid(c, c->nl);
+    hipLaunchKernelGGL(k_dot, dim3(g), dim3(kRedThreads), 0, c->stream, a, b, c->nl, c->d_part);
+    hipLaunchKernelGGL(k_dot_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g, d_out);
     return hipGetLastError();
 }
 

@@ -78,6 +78,8 @@ def _declare(L):
         "cdfem_lf_assemble": (C.c_int, [vp, vp, vp, C.c_int]),
         "cdfem_form_linear_system": (C.c_int, [vp, vp, vp, vp, vp, C.c_int]),
         "cdfem_solve": (C.c_int, [vp, C.POINTER(SolverParams), vp, vp, C.c_int, C.POINTER(SolverResult)]),
+        "cdfem_set_option": (C.c_int, [vp, C.c_char_p, C.c_int]),
+        "cdfem_stream_bench": (C.c_int, [vp, C.c_int, C.c_size_t, C.c_int, _dp]),
         "cdfem_profile_enable": (C.c_int, [vp, C.c_int]),
         "cdfem_profile_reset": (C.c_int, [vp]),
         "cdfem_profile_read": (C.c_int, [vp, C.c_int, _dp, C.POINTER(i64)]),
@@ -307,6 +309,15 @@ class Context:
 
     def synchronize(self):
         self._chk(self.L.cdfem_synchronize(self.h))
+
+    def stream_bench(self, mode=0, nbytes=2 << 30, reps=10):
+        """Measured HBM bandwidth (GB/s): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy."""
+        g = C.c_double()
+        self._chk(self.L.cdfem_stream_bench(self.h, int(mode), int(nbytes), int(reps), C.byref(g)))
+        return g.value
+
+    def set_option(self, key, value):
+        self._chk(self.L.cdfem_set_option(self.h, key.encode(), int(value)))
 
     # -- profiling -----------------------------------------------------------------------------------
     def profile(self, on=True):

@@ -154,6 +154,16 @@ typedef struct {
 int cdfem_solve(cdfem_ctx *ctx, const cdfem_solver_params *prm, const double *B, double *X,
                 int where, cdfem_solver_result *res);
 
+/* ---- HBM bandwidth probe: mode 0 read (16 B/lane), 1 read (8 B/lane), 2 copy (16 B/lane) of a
+ * `bytes`-sized buffer, `reps` launches; returns achieved GB/s (bytes moved / time).            */
+int cdfem_stream_bench(cdfem_ctx *ctx, int mode, size_t bytes, int reps, double *gbps);
+
+/* ---- tuning knobs (performance only; results identical to rounding) --------------------------
+ * "brick_waves": 1 or 2 — register budget of the structured Mult kernel (waves per SIMD).
+ * "brick_variant": 0, 1, 2 — element core of the structured CG kernel (unrolled / plane loop /
+ *                  low-register).                                                               */
+int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
+
 /* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */
 int cdfem_profile_enable(cdfem_ctx *ctx, int on);
 int cdfem_profile_reset(cdfem_ctx *ctx);

@@ -359,6 +359,13 @@ def test_brick_cg_parity(gpu_ctx):
     xn, inn = gpu_ctx.solve(B, method="cg", pc="none", rel_tol=1e-12, max_iter=2000)
     xon, ion = O.cg(Ac, Bo, dinv=None, rel_tol=1e-12, max_iter=2000)
     assert inn["converged"] and np.linalg.norm(xn - xon) <= 1e-10 * np.linalg.norm(xon)
+    # every element-core variant of the CG kernel gives the same iterates (to rounding)
+    x50, _ = O.cg(Ac, Bo, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=50)
+    for v in (0, 1, 2):
+        gpu_ctx.set_option("brick_variant", v)
+        xv, iv = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=50)
+        assert np.linalg.norm(xv - x50) <= 1e-11 * np.linalg.norm(x50), v
+    gpu_ctx.set_option("brick_variant", 0)
 
 
 def test_brick_full_size_matches_generic(gpu_ctx):

@@ -1,0 +1,67 @@
+"""Interleaved in-process A/B of kernel variants on the 64^3 p=2 CG workload (GPU box only).
+
+Usage: python tools/ab.py [--rounds R] [--iters K] [--n N] [--kinds K]
+Prints per-variant median per-kernel launch times (HIP events) and iteration time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "continuum-mechanics-mfem_amd", "python"))
+import cdfem  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--iters", type=int, default=100)
+ap.add_argument("--n", type=int, default=64)
+ap.add_argument("--p", type=int, default=2)
+ap.add_argument("--kinds", type=int, default=7)
+ap.add_argument("--variants", default="brick_waves=1,brick_waves=2")
+args = ap.parse_args()
+
+n = args.n
+mesh = cdfem.box_mesh(3, n, args.p, with_coords=False)
+ctx = cdfem.Context(0)
+ctx.upload_mesh(mesh).set_structured(n, n, n)
+ctx.pa_setup(kinds=args.kinds, kappa=0.1, conv=(1.0, -2.0, 0.5), mass=1.0)
+b = np.random.default_rng(1).uniform(-1, 1, mesh.nl)
+_, B = ctx.form_linear_system(np.zeros(mesh.nl), b)
+dB, dX = ctx.to_device(B), ctx.alloc(8 * mesh.nl)
+variants = [v.split("=") for v in args.variants.split(",")]
+res = {f"{k}={v}": {"iter_us": [], "apply": [], "faces": [], "update": []} for k, v in variants}
+ref = None
+for rnd in range(args.rounds + 1):
+    for k, v in variants:
+        ctx.set_option(k, int(v))
+        ctx.profile(True)
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        info = ctx.solve_device(dB, dX, max_iter=args.iters)
+        dt = time.perf_counter() - t0
+        a = ctx.profile_read(cdfem.K_APPLY)
+        f = ctx.profile_read(cdfem.K_E2L)
+        u = ctx.profile_read(cdfem.K_UPDATE)
+        ctx.profile(False)
+        x = ctx.from_device(dX, mesh.nl)
+        if ref is None:
+            ref = x
+        assert np.array_equal(x, ref) or np.abs(x - ref).max() <= 1e-12 * np.abs(ref).max()
+        if rnd == 0:
+            continue  # warm-up round
+        r = res[f"{k}={v}"]
+        r["iter_us"].append(dt / info["iterations"] * 1e6)
+        r["apply"].append(a[0] / a[1] * 1e3)
+        r["faces"].append(f[0] / f[1] * 1e3)
+        r["update"].append(u[0] / max(u[1], 1) * 1e3)
+bytes_apply = ctx.kernel_bytes(cdfem.K_APPLY)
+out = {"stream_GBs": {m: ctx.stream_bench(i, 2 << 30, 10) for i, m in enumerate(("read16", "read8", "copy16"))}}
+for name, r in res.items():
+    med = {k: float(np.median(v)) for k, v in r.items()}
+    med["apply_GBs"] = bytes_apply / (med["apply"] * 1e-6) / 1e9
+    out[name] = med
+print(json.dumps(out, indent=1))
