@@ -114,14 +114,18 @@ def main():
     # weak scaling: rank r owns elements iz in [r n, (r+1) n) of an n x n x (world n) mesh
     nz = n * world
     mesh = cdfem.box_mesh(3, (n, n, nz), p, z_range=(rank * n, (rank + 1) * n), with_coords=False)
-    if world > 1 and not getattr(cdfem, "HAS_PARTITIONED_SOLVER", False):
-        # replicas: each rank solves its own slab with the interface treated as Dirichlet-free
-        # local boundary (no exchange yet) -- labelled in the output
-        pass
     ctx = cdfem.Context(local)
     ctx.upload_mesh(mesh)
     if args.path == "brick":
         ctx.set_structured(n, n, n)
+    if world > 1:
+        if args.path != "brick":
+            raise SystemExit("multi-GPU runs use the structured brick path")
+        # RCCL communicator over xGMI; the id travels over the gloo control group
+        obj = [cdfem.comm_unique_id() if rank == 0 else None]
+        pg.broadcast_object_list(obj, src=0)
+        ctx.comm_init_rccl(rank, world, obj[0])
+        ctx.set_slab(rank > 0, rank < world - 1)
     c = (1.0, -2.0, 0.5)
     ctx.pa_setup(kinds=args.kinds, kappa=0.1, alpha=1.0, conv=c, mass=1.0)
 

@@ -545,7 +545,71 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
         return hipErrorInvalidValue;
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (multi_rank(c)) return launch_fin_sum(c, (int)grid, 1);
     return launch_update_fin(c, (int)grid);
+}
+
+// local partial sums of q = A d on the shared interface planes (what the neighbour must add)
+template <int S>
+__global__ void __launch_bounds__(256)
+k_pack_qplanes(const double *__restrict__ q, const double *__restrict__ face, const BrickGeom g,
+               int lo, int hi, double *__restrict__ out_lo, double *__restrict__ out_hi,
+               const KrylovState *__restrict__ st)
+{
+    constexpr int F = face_count<S>();
+    constexpr int s1 = S - 1;
+    if (st->done) return;
+    const int n = g.Lx * g.Ly;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int gy = k / g.Lx, gx = k - gy * g.Lx;
+    for (int side = 0; side < 2; ++side) {
+        if (side == 0 ? !lo : !hi) continue;
+        const int gz = side == 0 ? 0 : g.Lz - 1;
+        double v;
+        if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
+            int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
+            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
+            if (gx - qx * s1 == 0) {
+                if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
+                if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
+            } else { bxs[0] = qx; pxs[0] = gx - qx * s1; nxc = 1; }
+            if (gy - qy * s1 == 0) {
+                if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
+                if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
+            } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
+            if (gz - qz * s1 == 0) {
+                if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
+                if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
+            } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
+            v = 0.0;
+            for (int kz = 0; kz < nzc; ++kz)
+                for (int ky = 0; ky < nyc; ++ky)
+                    for (int kx = 0; kx < nxc; ++kx) {
+                        const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
+                        v += face[(size_t)bb * F + face_index<S>(pxs[kx], pys[ky], pzs[kz])];
+                    }
+        } else {
+            v = q[gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz)];
+        }
+        (side == 0 ? out_lo : out_hi)[k] = v;
+    }
+}
+
+hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q)
+{
+    const BrickGeom g = geom_of(c);
+    const int n = (int)(c->Lx * c->Ly);
+    const dim3 grid((n + 255) / 256), block(256);
+    if (c->p == 1)
+        hipLaunchKernelGGL(k_pack_qplanes<kBrick * 1 + 1>, grid, block, 0, c->stream, q, c->d_face, g,
+                           c->zlo_shared, c->zhi_shared, c->d_if[0], c->d_if[2], c->d_state);
+    else if (c->p == 2)
+        hipLaunchKernelGGL(k_pack_qplanes<kBrick * 2 + 1>, grid, block, 0, c->stream, q, c->d_face, g,
+                           c->zlo_shared, c->zhi_shared, c->d_if[0], c->d_if[2], c->d_state);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
 }
 
 }  // namespace cdfem

@@ -92,6 +92,8 @@ void free_mesh(cdfem_ctx *c)
     for (auto &w : c->d_w) dfree(w);
     dfree(c->d_part); dfree(c->d_gm); dfree(c->d_gm_small);
     dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones); dfree(c->d_dalt);
+    for (auto &b : c->d_if) dfree(b);
+    c->zlo_shared = c->zhi_shared = 0;
     c->gm_cap = 0;
     c->mesh_ready = c->pa_ready = c->dinv_ready = false;
     c->structured = false;
@@ -243,6 +245,7 @@ void ensure_dinv(cdfem_ctx *c)
     double *diag = c->d_w[7];
     HIPCHK(launch_diag_elem(c, c->d_Ye));
     HIPCHK(launch_e2l(c, c->d_Ye, nullptr, diag, false, 0));
+    interface_sum(c, diag);  // shared planes: the full diagonal (both ranks' elements)
     HIPCHK(launch_dinv(c, diag, c->d_dinv));
     c->dinv_ready = true;
 }
@@ -264,15 +267,32 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
         dinv = ones_vector(c);
     }
     const int check = p.check_every > 0 ? p.check_every : 16;
+    const bool mr = multi_rank(c);
+    double *red = c->d_state->red;  // device scalars awaiting the all-reduce
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
-    HIPCHK(launch_cg_init(c, dB, x, r, q, dprev, dinv, p.rel_tol, p.abs_tol, p.max_iter));
+    if (mr) {
+        HIPCHK(launch_cg_init_nofin(c, dB, x, r, q, dprev, dinv));
+        comm_allreduce(c, red + 2, 1);
+        HIPCHK(launch_init_step(c, p.rel_tol, p.abs_tol, p.max_iter));
+    } else {
+        HIPCHK(launch_cg_init(c, dB, x, r, q, dprev, dinv, p.rel_tol, p.abs_tol, p.max_iter));
+    }
     auto apply = [&] {
         prof_mark(c, CDFEM_K_APPLY, true);
         HIPCHK(launch_brick_cg2(c, r, dinv, dprev, dcur, q));
         prof_mark(c, CDFEM_K_APPLY, false);
         prof_mark(c, CDFEM_K_E2L, true);
-        HIPCHK(launch_den_fin(c, c->nblk));
+        if (mr) {
+            // neighbours' partial sums of q on the shared planes (added by the update kernel)
+            HIPCHK(launch_pack_qplanes(c, q));
+            comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], c->Lx * c->Ly);
+            HIPCHK(launch_fin_sum(c, c->nblk, 0));
+            comm_allreduce(c, red + 0, 1);
+            HIPCHK(launch_den_step(c));
+        } else {
+            HIPCHK(launch_den_fin(c, c->nblk));
+        }
         prof_mark(c, CDFEM_K_E2L, false);
     };
     apply();
@@ -280,7 +300,13 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     for (;;) {
         for (int k = 0; k < check && launched < p.max_iter; ++k, ++launched) {
             prof_mark(c, CDFEM_K_UPDATE, true);
-            HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv, nullptr, nullptr));
+            HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv,
+                                          mr && c->zlo_shared ? c->d_if[1] : nullptr,
+                                          mr && c->zhi_shared ? c->d_if[3] : nullptr));
+            if (mr) {
+                comm_allreduce(c, red + 1, 1);
+                HIPCHK(launch_update_step(c));
+            }
             prof_mark(c, CDFEM_K_UPDATE, false);
             std::swap(dprev, dcur);
             apply();
@@ -397,6 +423,7 @@ void cdfem_destroy(cdfem_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_mesh(c);
+    comm_destroy(c);
     if (c->d_state) (void)hipFree(c->d_state);
     if (c->h_state) (void)hipHostFree(c->h_state);
     for (auto &s : c->prof)
@@ -552,6 +579,24 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
     });
 }
 
+int cdfem_set_slab(cdfem_ctx *c, int zlo_shared, int zhi_shared)
+{
+    return guarded(c, [&] {
+        if (!c->structured) throw StateError("cdfem_mesh_set_structured must precede cdfem_set_slab");
+        if ((zlo_shared || zhi_shared) && !c->comm) throw StateError("attach a communicator first");
+        c->zlo_shared = zlo_shared != 0;
+        c->zhi_shared = zhi_shared != 0;
+        const int64_t n = c->Lx * c->Ly;
+        for (auto &b : c->d_if) {
+            dfree(b);
+            b = dalloc<double>(n);
+            HIPCHK(hipMemsetAsync(b, 0, n * 8, c->stream));
+        }
+        c->dinv_ready = false;
+        return CDFEM_OK;
+    });
+}
+
 int cdfem_rule_size(cdfem_ctx *c, int rule, int *nq)
 {
     return guarded(c, [&] {
@@ -629,7 +674,10 @@ int cdfem_pa_mult(cdfem_ctx *c, const double *x, double *y, int constrained, int
         if (!x || !y) throw ArgError("null vector");
         const double *dx = dev_in(c, x, where, c->d_w[0], c->nl);
         double *dy = where == CDFEM_DEVICE ? y : c->d_w[1];
+        if (multi_rank(c) && constrained)
+            throw UnsupportedError("constrained Mult across ranks: use cdfem_solve");
         op_apply(c, dx, dy, constrained != 0);
+        interface_sum(c, dy);  // shared planes: add the neighbour's partial sums
         dev_out(c, y, where, dy, c->nl);
         prof_collect(c);
         return CDFEM_OK;
@@ -682,6 +730,7 @@ int cdfem_form_linear_system(cdfem_ctx *c, const double *x, const double *b, dou
         op_apply(c, xe, z, false);                          // z = A x_e
         if (dB != db) HIPCHK(hipMemcpyAsync(dB, db, c->nl * 8, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(launch_axpby(c, -1.0, z, 1.0, dB));          // B = b - A x_e
+        interface_sum(c, dB);                               // P^T on the shared planes
         HIPCHK(launch_set_ess(c, dB, dx));                  // B[ess] = x[ess]
         dev_out(c, B, where, dB, c->nl);
         dev_out(c, X, where, dx, c->nl);

@@ -45,9 +45,12 @@ int rule_points_1d(int which, int dim, int p);
 // Device-side Krylov state (one per context), updated only by kernels.
 struct KrylovState {
     double nom, nom0, den, alpha, beta, betanom, r0;
+    double red[4];  // rank-local reductions awaiting the all-reduce (0 den, 1 betanom, 2 nom)
     int iter, done, converged, final_iter, max_iter, first_den;
     unsigned reserved[4];
 };
+
+struct Comm;  // comm.hip
 
 struct ProfileSlot {
     std::vector<hipEvent_t> ev;  // pairs
@@ -55,9 +58,6 @@ struct ProfileSlot {
     double total_ms = 0.0;
     int64_t count = 0;
 };
-
-// ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
-hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 
 }  // namespace cdfem
 
@@ -93,6 +93,10 @@ struct cdfem_ctx {
     int brick_waves = 2;                // register budget of k_brick3d (CDFEM_BRICK_WAVES)
     int brick_variant = 0;              // element core of k_brick_cg (0 unrolled, 1 plane loop, 2 low-reg)
     int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)
+    int zhi_shared = 0;                 // local gz=Lz-1 plane shared with the rank above
+    cdfem::Comm *comm = nullptr;        // rank communicator (comm.hip), nullptr on one GPU
+    int rank = 0, nranks = 1;
+    double *d_if[4] = {};               // interface planes: send_lo, recv_lo, send_hi, recv_hi
 
     // rules
     cdfem::Rule1D rule_op, rule_lf, rule_err;
@@ -172,6 +176,23 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
                                   const double *dinv, const double *remote_lo, const double *remote_hi);
 // generic deterministic dot into host-visible scalar via state (used by GMRES / tests)
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out);
+
+// ---- communication (comm.hip) -----------------------------------------------------------------
+void comm_destroy(cdfem_ctx *c);
+void comm_allreduce(cdfem_ctx *c, double *dbuf, int n);
+void comm_exchange(cdfem_ctx *c, const double *send_lo, double *recv_lo, const double *send_hi,
+                   double *recv_hi, int64_t n);
+void interface_sum(cdfem_ctx *c, double *v);  // L-vector interface planes summed over ranks
+inline bool multi_rank(const cdfem_ctx *c) { return c->nranks > 1; }
+// split CG finalizers for the multi-rank path: local sum -> all-reduce -> step
+hipError_t launch_fin_sum(cdfem_ctx *c, int nparts, int slot);
+hipError_t launch_den_step(cdfem_ctx *c);
+hipError_t launch_update_step(cdfem_ctx *c);
+hipError_t launch_init_step(cdfem_ctx *c, double rel_tol, double abs_tol, int max_iter);
+hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double *r, double *z, double *d,
+                                const double *dinv);
+// pack the local partial sums of q on the shared interface planes into d_if[0] / d_if[2]
+hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q);
 
 // ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);

@@ -1,0 +1,205 @@
+// comm.hip — rank communication for the element-partitioned (slab) multi-GPU path.
+//
+// Replaces the reference's MPI layer on the hot path (SURVEY.md §5 "Distributed comm backend"):
+// ParMesh(MPI_COMM_WORLD) element partition (linear_convection_diffusion_2D.cpp:300), hypre/PETSc
+// halo exchange inside MatMult and the MPI_Allreduce of the Krylov dot products.
+//
+// Each rank owns a z-slab of the structured box.  Its local L-vector holds the dofs of its
+// elements; the interface planes (local gz = 0 / gz = Lz-1) are shared with the rank below / above
+// and are OWNED by the lower rank for dot products.  Per Krylov iteration:
+//   * the two interface planes' LOCAL partial sums of q = A d are exchanged with the neighbours
+//     (RCCL send/recv, 8*(p nx + 1)*(p ny + 1) bytes per plane) and added by the update kernel;
+//   * the three Krylov scalars (nom, den, betanom) are summed with an 8-byte all-reduce.
+// Two backends: RCCL (stream-ordered, no host sync: the production path over xGMI) and host
+// callbacks (device->host staging + user functions, e.g. torch.distributed/gloo or MPI; used to
+// test the distributed kernels with several processes on ONE GPU, which RCCL refuses).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "cdfem_internal.hpp"
+
+namespace cdfem {
+
+struct Comm {
+    int rank = 0, nranks = 1;
+    ncclComm_t nccl = nullptr;
+    cdfem_allreduce_fn h_allreduce = nullptr;
+    cdfem_exchange_fn h_exchange = nullptr;
+    void *user = nullptr;
+    double *h_buf = nullptr;  // pinned staging for the host backend
+    size_t h_cap = 0;
+};
+
+static void nccl_check(ncclResult_t r, const char *what)
+{
+    if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+void comm_destroy(cdfem_ctx *c)
+{
+    if (!c->comm) return;
+    if (c->comm->nccl) (void)ncclCommDestroy(c->comm->nccl);
+    if (c->comm->h_buf) (void)hipHostFree(c->comm->h_buf);
+    delete c->comm;
+    c->comm = nullptr;
+    c->rank = 0;
+    c->nranks = 1;
+}
+
+static double *host_staging(Comm *m, size_t n)
+{
+    if (m->h_cap < n) {
+        if (m->h_buf) (void)hipHostFree(m->h_buf);
+        if (hipHostMalloc(&m->h_buf, n * sizeof(double), hipHostMallocDefault) != hipSuccess)
+            throw std::runtime_error("pinned staging allocation failed");
+        m->h_cap = n;
+    }
+    return m->h_buf;
+}
+
+// in-place sum over ranks of n doubles in device memory (stream-ordered)
+void comm_allreduce(cdfem_ctx *c, double *dbuf, int n)
+{
+    Comm *m = c->comm;
+    if (!m || m->nranks == 1) return;
+    if (m->nccl) {
+        nccl_check(ncclAllReduce(dbuf, dbuf, n, ncclDouble, ncclSum, m->nccl, c->stream), "ncclAllReduce");
+        return;
+    }
+    double *h = host_staging(m, n);
+    if (hipMemcpyAsync(h, dbuf, n * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        throw std::runtime_error("allreduce staging failed");
+    if (m->h_allreduce(h, n, m->user) != 0) throw std::runtime_error("host allreduce callback failed");
+    if (hipMemcpyAsync(dbuf, h, n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        throw std::runtime_error("allreduce staging failed");
+}
+
+// exchange interface planes with the neighbours: send_lo -> rank-1 (recv into its recv_hi) and
+// send_hi -> rank+1; n doubles per plane
+void comm_exchange(cdfem_ctx *c, const double *send_lo, double *recv_lo, const double *send_hi,
+                   double *recv_hi, int64_t n)
+{
+    Comm *m = c->comm;
+    if (!m || m->nranks == 1) return;
+    const bool lo = m->rank > 0, hi = m->rank < m->nranks - 1;
+    if (m->nccl) {
+        nccl_check(ncclGroupStart(), "ncclGroupStart");
+        if (lo) {
+            nccl_check(ncclSend(send_lo, n, ncclDouble, m->rank - 1, m->nccl, c->stream), "ncclSend");
+            nccl_check(ncclRecv(recv_lo, n, ncclDouble, m->rank - 1, m->nccl, c->stream), "ncclRecv");
+        }
+        if (hi) {
+            nccl_check(ncclSend(send_hi, n, ncclDouble, m->rank + 1, m->nccl, c->stream), "ncclSend");
+            nccl_check(ncclRecv(recv_hi, n, ncclDouble, m->rank + 1, m->nccl, c->stream), "ncclRecv");
+        }
+        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+        return;
+    }
+    double *h = host_staging(m, 4 * (size_t)n);
+    double *hs_lo = h, *hr_lo = h + n, *hs_hi = h + 2 * n, *hr_hi = h + 3 * n;
+    if ((lo && hipMemcpyAsync(hs_lo, send_lo, n * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) ||
+        (hi && hipMemcpyAsync(hs_hi, send_hi, n * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        throw std::runtime_error("exchange staging failed");
+    if (m->h_exchange(lo ? hs_lo : nullptr, lo ? hr_lo : nullptr, hi ? hs_hi : nullptr,
+                      hi ? hr_hi : nullptr, n, m->user) != 0)
+        throw std::runtime_error("host exchange callback failed");
+    if ((lo && hipMemcpyAsync(recv_lo, hr_lo, n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
+        (hi && hipMemcpyAsync(recv_hi, hr_hi, n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess))
+        throw std::runtime_error("exchange staging failed");
+    // the staging buffer is reused by the next call: complete the uploads first
+    if (hipStreamSynchronize(c->stream) != hipSuccess) throw std::runtime_error("exchange staging failed");
+}
+
+// ---- plane kernels ----------------------------------------------------------------------------
+__global__ void k_get_plane(const double *__restrict__ v, int64_t plane_off, int64_t n,
+                            double *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = v[plane_off + i];
+}
+
+__global__ void k_add_plane(double *__restrict__ v, int64_t plane_off, int64_t n,
+                            const double *__restrict__ in)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[plane_off + i] += in[i];
+}
+
+// sum of the interface planes of an L-vector over the ranks sharing them (MFEM P^T then P)
+void interface_sum(cdfem_ctx *c, double *v)
+{
+    if (!c->comm || c->comm->nranks == 1) return;
+    const int64_t n = c->Lx * c->Ly, off_hi = (c->Lz - 1) * n;
+    const dim3 g((unsigned)((n + 255) / 256)), b(256);
+    if (c->zlo_shared) hipLaunchKernelGGL(k_get_plane, g, b, 0, c->stream, v, (int64_t)0, n, c->d_if[0]);
+    if (c->zhi_shared) hipLaunchKernelGGL(k_get_plane, g, b, 0, c->stream, v, off_hi, n, c->d_if[2]);
+    comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], n);
+    if (c->zlo_shared) hipLaunchKernelGGL(k_add_plane, g, b, 0, c->stream, v, (int64_t)0, n, c->d_if[1]);
+    if (c->zhi_shared) hipLaunchKernelGGL(k_add_plane, g, b, 0, c->stream, v, off_hi, n, c->d_if[3]);
+}
+
+}  // namespace cdfem
+
+using namespace cdfem;
+
+extern "C" {
+
+int cdfem_comm_unique_id(unsigned char *id)
+{
+    if (!id) return CDFEM_ERR_ARG;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return CDFEM_ERR_COMM;
+    for (int i = 0; i < NCCL_UNIQUE_ID_BYTES; ++i) id[i] = (unsigned char)u.internal[i];
+    return CDFEM_OK;
+}
+
+int cdfem_comm_init_rccl(cdfem_ctx *c, int rank, int nranks, const unsigned char *id)
+{
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return CDFEM_ERR_ARG;
+    comm_destroy(c);
+    Comm *m = new Comm();
+    m->rank = rank;
+    m->nranks = nranks;
+    if (nranks > 1) {
+        ncclUniqueId u;
+        for (int i = 0; i < NCCL_UNIQUE_ID_BYTES; ++i) u.internal[i] = (char)id[i];
+        if (hipSetDevice(c->device) != hipSuccess) {
+            delete m;
+            return CDFEM_ERR_HIP;
+        }
+        const ncclResult_t r = ncclCommInitRank(&m->nccl, nranks, u, rank);
+        if (r != ncclSuccess) {
+            c->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+            delete m;
+            return CDFEM_ERR_COMM;
+        }
+    }
+    c->comm = m;
+    c->rank = rank;
+    c->nranks = nranks;
+    return CDFEM_OK;
+}
+
+int cdfem_comm_init_host(cdfem_ctx *c, int rank, int nranks, cdfem_allreduce_fn allreduce,
+                         cdfem_exchange_fn exchange, void *user)
+{
+    if (!c || !allreduce || !exchange || nranks < 1 || rank < 0 || rank >= nranks) return CDFEM_ERR_ARG;
+    comm_destroy(c);
+    Comm *m = new Comm();
+    m->rank = rank;
+    m->nranks = nranks;
+    m->h_allreduce = allreduce;
+    m->h_exchange = exchange;
+    m->user = user;
+    c->comm = m;
+    c->rank = rank;
+    c->nranks = nranks;
+    return CDFEM_OK;
+}
+
+}  // extern "C"

@@ -51,7 +51,7 @@ k_e2l(const int32_t *__restrict__ off, const int32_t *__restrict__ pos,
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_init(const double *__restrict__ B, double *__restrict__ x, double *__restrict__ r,
           double *__restrict__ z, double *__restrict__ d, const double *__restrict__ dinv, int64_t n,
-          double *__restrict__ part)
+          int64_t skip_lo, double *__restrict__ part)
 {
     __shared__ double sh[kRedThreads / 64];
     double acc = 0.0;
@@ -63,9 +63,50 @@ k_cg_init(const double *__restrict__ B, double *__restrict__ x, double *__restri
         x[i] = 0.0;
         z[i] = zi;
         d[i] = zi;
-        acc += zi * ri;
+        if (i >= skip_lo) acc += zi * ri;  // shared plane owned by the rank below
     }
     store_partial(block_sum(acc, sh), part);
+}
+
+// MFEM CGSolver initial convergence test on nom = (z, r)
+__device__ inline void cg_init_logic(KrylovState *st, double nom, double rel_tol, double abs_tol,
+                                     int max_iter)
+{
+    st->nom = st->nom0 = st->betanom = nom;
+    const double r0 = fmax(nom * rel_tol * rel_tol, abs_tol * abs_tol);
+    st->r0 = r0;
+    st->iter = 1;
+    st->max_iter = max_iter;
+    st->final_iter = max_iter;
+    st->converged = 0;
+    st->done = 0;
+    st->first_den = 1;  // next den is the initial one
+    st->beta = 0.0;
+    if (nom < 0.0) {             // preconditioner not positive definite
+        st->done = 1;
+        st->final_iter = 0;
+    } else if (nom <= r0) {
+        st->done = 1;
+        st->converged = 1;
+        st->final_iter = 0;
+    }
+}
+
+// MFEM CGSolver after betanom = (r, z): convergence test, iteration bound, beta
+__device__ inline void cg_update_logic(KrylovState *st, double betanom)
+{
+    st->betanom = betanom;
+    const int i = st->iter;
+    if (betanom < 0.0) {
+        st->done = 1; st->converged = 0; st->final_iter = i;
+    } else if (betanom <= st->r0) {
+        st->done = 1; st->converged = 1; st->final_iter = i;
+    } else if (i + 1 > st->max_iter) {
+        st->done = 1; st->converged = 0; st->final_iter = st->max_iter;
+    } else {
+        st->beta = betanom / st->nom;
+        st->iter = i + 1;
+    }
 }
 
 // one block: nom = sum of the init partials; MFEM CGSolver initial convergence test
@@ -75,26 +116,32 @@ k_cg_init_fin(const double *__restrict__ part, int n, double rel_tol, double abs
 {
     __shared__ double sh[1024 / 64];
     const double nom = sum_partials(part, n, sh);
-    if (threadIdx.x == 0) {
-        st->nom = st->nom0 = st->betanom = nom;
-        const double r0 = fmax(nom * rel_tol * rel_tol, abs_tol * abs_tol);
-        st->r0 = r0;
-        st->iter = 1;
-        st->max_iter = max_iter;
-        st->final_iter = max_iter;
-        st->converged = 0;
-        st->done = 0;
-        st->first_den = 1;  // next den is the initial one
-        st->beta = 0.0;
-        if (nom < 0.0) {             // preconditioner not positive definite
-            st->done = 1;
-            st->final_iter = 0;
-        } else if (nom <= r0) {
-            st->done = 1;
-            st->converged = 1;
-            st->final_iter = 0;
-        }
-    }
+    if (threadIdx.x == 0) cg_init_logic(st, nom, rel_tol, abs_tol, max_iter);
+}
+
+// multi-rank split: rank-local sum into st->red[slot] (then all-reduce, then a *_step kernel)
+__global__ void __launch_bounds__(1024)
+k_fin_sum(const double *__restrict__ part, int n, int slot, KrylovState *__restrict__ st)
+{
+    __shared__ double sh[1024 / 64];
+    if (slot != 2 && st->done) return;
+    const double v = sum_partials(part, n, sh);
+    if (threadIdx.x == 0) st->red[slot] = v;
+}
+
+__global__ void k_init_step(double rel_tol, double abs_tol, int max_iter, KrylovState *__restrict__ st)
+{
+    cg_init_logic(st, st->red[2], rel_tol, abs_tol, max_iter);
+}
+
+__global__ void k_den_step(KrylovState *__restrict__ st)
+{
+    if (!st->done) cg_den_step(st, st->red[0]);
+}
+
+__global__ void k_update_step(KrylovState *__restrict__ st)
+{
+    if (!st->done) cg_update_logic(st, st->red[1]);
 }
 
 // one block: den = sum of the partials (Mult kernels), MFEM CG den step
@@ -156,20 +203,7 @@ k_cg_update_fin(const double *__restrict__ part, int n, KrylovState *__restrict_
     __shared__ double sh[1024 / 64];
     if (st->done) return;
     const double betanom = sum_partials(part, n, sh);
-    if (threadIdx.x == 0) {
-        st->betanom = betanom;
-        const int i = st->iter;
-        if (betanom < 0.0) {
-            st->done = 1; st->converged = 0; st->final_iter = i;
-        } else if (betanom <= st->r0) {
-            st->done = 1; st->converged = 1; st->final_iter = i;
-        } else if (i + 1 > st->max_iter) {
-            st->done = 1; st->converged = 0; st->final_iter = st->max_iter;
-        } else {
-            st->beta = betanom / st->nom;
-            st->iter = i + 1;
-        }
-    }
+    if (threadIdx.x == 0) cg_update_logic(st, betanom);
 }
 
 // d = z + beta d
@@ -313,9 +347,43 @@ hipError_t launch_cg_init(cdfem_ctx *c, const double *B, double *x, double *r, d
 {
     const unsigned g = red_grid(c, c->nl);
     hipLaunchKernelGGL(k_cg_init, dim3(g), dim3(kRedThreads), 0, c->stream, B, x, r, z, d, dinv, c->nl,
-                       c->d_part);
+                       (int64_t)0, c->d_part);
     hipLaunchKernelGGL(k_cg_init_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g, rel_tol,
                        abs_tol, max_iter, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double *r, double *z, double *d,
+                                const double *dinv)
+{
+    const unsigned g = red_grid(c, c->nl);
+    const int64_t skip = c->zlo_shared ? c->Lx * c->Ly : 0;
+    hipLaunchKernelGGL(k_cg_init, dim3(g), dim3(kRedThreads), 0, c->stream, B, x, r, z, d, dinv, c->nl,
+                       skip, c->d_part);
+    return launch_fin_sum(c, (int)g, 2);
+}
+
+hipError_t launch_fin_sum(cdfem_ctx *c, int nparts, int slot)
+{
+    hipLaunchKernelGGL(k_fin_sum, dim3(1), dim3(1024), 0, c->stream, c->d_part, nparts, slot, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_init_step(cdfem_ctx *c, double rel_tol, double abs_tol, int max_iter)
+{
+    hipLaunchKernelGGL(k_init_step, dim3(1), dim3(1), 0, c->stream, rel_tol, abs_tol, max_iter, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_den_step(cdfem_ctx *c)
+{
+    hipLaunchKernelGGL(k_den_step, dim3(1), dim3(1), 0, c->stream, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_update_step(cdfem_ctx *c)
+{
+    hipLaunchKernelGGL(k_update_step, dim3(1), dim3(1), 0, c->stream, c->d_state);
     return hipGetLastError();
 }
 

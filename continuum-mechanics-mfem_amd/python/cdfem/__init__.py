@@ -51,6 +51,10 @@ class SolverResult(C.Structure):
                 ("initial_norm", C.c_double), ("seconds", C.c_double)]
 
 
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                          C.POINTER(C.c_double), C.c_int64, C.c_void_p)
+
 _lib = None
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
@@ -84,6 +88,10 @@ def _declare(L):
         "cdfem_profile_reset": (C.c_int, [vp]),
         "cdfem_profile_read": (C.c_int, [vp, C.c_int, _dp, C.POINTER(i64)]),
         "cdfem_kernel_bytes": (C.c_int, [vp, C.c_int, _dp]),
+        "cdfem_comm_unique_id": (C.c_int, [C.c_char_p]),
+        "cdfem_comm_init_rccl": (C.c_int, [vp, C.c_int, C.c_int, C.c_char_p]),
+        "cdfem_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, ALLREDUCE_FN, EXCHANGE_FN, vp]),
+        "cdfem_set_slab": (C.c_int, [vp, C.c_int, C.c_int]),
         "cdfem_box_sizes": (C.c_int, [C.c_int] * 7 + [C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int)]),
         "cdfem_box_mesh": (C.c_int, [C.c_int] * 7 + [C.c_double, _dp, _ip, _ip, _dp]),
     }
@@ -114,6 +122,15 @@ def exported_symbols_from_header(path=HEADER_PATH):
 
 def device_count():
     return lib().cdfem_device_count()
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (128 bytes) created on rank 0 and broadcast to the other ranks."""
+    buf = C.create_string_buffer(128)
+    rc = lib().cdfem_comm_unique_id(buf)
+    if rc:
+        raise CdfemError(rc, "ncclGetUniqueId failed")
+    return buf.raw
 
 
 def _f64(a):
@@ -272,6 +289,56 @@ class Context:
         self._chk(rc, allow=() if raise_on_fail else (ERR_NOT_CONVERGED,))
         return X, dict(converged=bool(res.converged), iterations=res.iterations,
                        final_norm=res.final_norm, initial_norm=res.initial_norm, seconds=res.seconds)
+
+    # -- multi-GPU (z-slab element partition) ----------------------------------------------------
+    def comm_init_rccl(self, rank, nranks, uid: bytes):
+        """RCCL communicator from a 128-byte unique id (rank 0: comm_unique_id(), broadcast it)."""
+        self._chk(self.L.cdfem_comm_init_rccl(self.h, int(rank), int(nranks), uid))
+
+    def comm_init_torch(self, group=None):
+        """Host-callback communicator over torch.distributed (any backend, e.g. gloo)."""
+        import torch
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+
+        def allreduce(buf, n, _user):
+            try:
+                a = np.ctypeslib.as_array(buf, shape=(n,))
+                t = torch.from_numpy(a.copy())
+                dist.all_reduce(t, group=group)
+                a[:] = t.numpy()
+                return 0
+            except Exception:  # errors must not unwind through C
+                return 1
+
+        def exchange(send_lo, recv_lo, send_hi, recv_hi, n, _user):
+            try:
+                reqs, outs = [], []
+                if bool(send_lo):
+                    reqs.append(dist.isend(torch.from_numpy(np.ctypeslib.as_array(send_lo, (n,)).copy()),
+                                           rank - 1, group=group))
+                    t = torch.empty(n, dtype=torch.float64)
+                    reqs.append(dist.irecv(t, rank - 1, group=group))
+                    outs.append((recv_lo, t))
+                if bool(send_hi):
+                    reqs.append(dist.isend(torch.from_numpy(np.ctypeslib.as_array(send_hi, (n,)).copy()),
+                                           rank + 1, group=group))
+                    t = torch.empty(n, dtype=torch.float64)
+                    reqs.append(dist.irecv(t, rank + 1, group=group))
+                    outs.append((recv_hi, t))
+                for r in reqs:
+                    r.wait()
+                for ptr, t in outs:
+                    np.ctypeslib.as_array(ptr, (n,))[:] = t.numpy()
+                return 0
+            except Exception:
+                return 1
+
+        self._cb = (ALLREDUCE_FN(allreduce), EXCHANGE_FN(exchange))  # keep alive
+        self._chk(self.L.cdfem_comm_init_host(self.h, rank, world, self._cb[0], self._cb[1], None))
+
+    def set_slab(self, zlo_shared, zhi_shared):
+        self._chk(self.L.cdfem_set_slab(self.h, int(bool(zlo_shared)), int(bool(zhi_shared))))
 
     # -- device-resident variants (benchmarks) ------------------------------------------------------
     def alloc(self, nbytes):

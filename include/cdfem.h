@@ -172,6 +172,22 @@ int cdfem_profile_read(cdfem_ctx *ctx, int kernel, double *total_ms, int64_t *co
 /* algorithmic bytes moved by one launch of kernel id (see DESIGN.md for the per-unit figures) */
 int cdfem_kernel_bytes(cdfem_ctx *ctx, int kernel, double *bytes);
 
+/* ---- multi-GPU (element-partitioned z-slabs, one context per GPU / rank) ----------------------
+ * replaces: MPI_COMM_WORLD + ParMesh partition (linear_convection_diffusion_2D.cpp:300) and the MPI
+ * traffic inside hypre/PETSc (halo sums, Krylov all-reduces).  Each rank uploads its slab
+ * (cdfem_box_mesh with [z0,z1)), declares it structured, then attaches a communicator and marks
+ * which of its z-end planes are shared with a neighbour (the lower rank owns a shared plane).
+ * Backends: RCCL (stream-ordered, over xGMI) or host callbacks (any transport: gloo, MPI).      */
+typedef int (*cdfem_allreduce_fn)(double *buf, int n, void *user);  /* in-place sum over ranks */
+/* send_lo -> rank-1, recv_lo <- rank-1, send_hi -> rank+1, recv_hi <- rank+1 (NULL if absent) */
+typedef int (*cdfem_exchange_fn)(const double *send_lo, double *recv_lo, const double *send_hi,
+                                 double *recv_hi, int64_t n, void *user);
+int cdfem_comm_unique_id(unsigned char *id /* 128 bytes */);
+int cdfem_comm_init_rccl(cdfem_ctx *ctx, int rank, int nranks, const unsigned char *id);
+int cdfem_comm_init_host(cdfem_ctx *ctx, int rank, int nranks, cdfem_allreduce_fn allreduce,
+                         cdfem_exchange_fn exchange, void *user);
+int cdfem_set_slab(cdfem_ctx *ctx, int zlo_shared, int zhi_shared);
+
 /* ---- structured mesh helper (host only, no device needed) ---------------------------------------
  * Box [0,1]^dim into nx*ny(*nz) quads/hexes with the conventions above; rank-slab variant for
  * the element-partitioned multi-GPU path: elements with iz in [z0, z1) only, dofs renumbered

@@ -1,0 +1,197 @@
+"""Multi-rank (z-slab element partition) path, world_size 2 over torch.distributed.
+
+CPU (gloo): the distributed algorithm the GPU path implements, restated with the oracle's slab
+operators: slab meshes from the PRODUCT's partitioner (cdfem_box_mesh with [z0, z1)), local
+assembly, interface-plane sums with the neighbour (send/recv), dot products owned by the lower
+rank on shared planes, all-reduced Krylov scalars.  The gathered solution must equal the
+single-domain oracle solve (partition invariance).
+
+GPU (marked gpu): the same with the HIP kernels — 2 processes on ONE device, communicator = host
+callbacks over gloo (RCCL refuses two ranks per GPU) — against a single-context solve.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+N, P, NZ = 4, 2, 8          # 4 x 4 x 8 elements, p = 2, split in z between 2 ranks
+KAPPA, S = 0.1, 1.0
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _slab(rank, world):
+    import cdfem
+    per = NZ // world
+    return cdfem.box_mesh(3, (N, N, NZ), P, z_range=(rank * per, (rank + 1) * per))
+
+
+def _interface_sum(dist, rank, world, v, plane):
+    """Add the neighbours' partial sums on the shared z-end planes (MFEM P^T / P)."""
+    import torch
+    reqs, bufs = [], []
+    if rank > 0:
+        reqs.append(dist.isend(torch.from_numpy(v[:plane].copy()), rank - 1))
+        t = torch.empty(plane, dtype=torch.float64)
+        reqs.append(dist.irecv(t, rank - 1))
+        bufs.append((slice(0, plane), t))
+    if rank < world - 1:
+        reqs.append(dist.isend(torch.from_numpy(v[-plane:].copy()), rank + 1))
+        t = torch.empty(plane, dtype=torch.float64)
+        reqs.append(dist.irecv(t, rank + 1))
+        bufs.append((slice(len(v) - plane, len(v)), t))
+    for r in reqs:
+        r.wait()
+    out = v.copy()
+    for sl, t in bufs:
+        out[sl] += t.numpy()
+    return out
+
+
+def _allsum(dist, x):
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def _cpu_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    from oracle import oracle as O
+    dist = _init(rank, world, port)
+    m = _slab(rank, world)
+    plane = (P * N + 1) ** 2
+    om = O.BoxMesh(3, 1, P)                      # container for the slab arrays
+    om.verts, om.dofmap, om.ne, om.nl = m.verts, m.dofmap, m.ne, m.nl
+    A = O.fa_assemble(om, kappa=KAPPA, s=S, kinds=O.DIFFUSION | O.MASS)
+    prm = O.mms_params(O.MMS_SIN, 3, kappa=KAPPA, s=S, c=(0.0, 0.0, 0.0), p=P)
+    b_loc = O.lf_assemble(om, prm)
+    ess = np.zeros(m.nl, dtype=bool)
+    ess[m.ess] = True
+    # constrained operator on the local L-vector: zero ess input, local apply, interface sum,
+    # ess rows = identity (ConstrainedOperator, DIAG_ONE)
+    def amult(x):
+        xz = np.where(ess, 0.0, x)
+        y = _interface_sum(dist, rank, world, A.mult(xz), plane)
+        return np.where(ess, x, y)
+    B = _interface_sum(dist, rank, world, b_loc, plane)
+    B[ess] = 0.0                                  # homogeneous Dirichlet (u = 0 on the boundary)
+    diag = _interface_sum(dist, rank, world, A.diag(), plane)
+    dinv = np.where(ess, 1.0, 1.0 / diag)
+    w = np.ones(m.nl)
+    if rank > 0:
+        w[:plane] = 0.0                           # shared plane owned by the rank below
+    dot = lambda a, b: _allsum(dist, float(np.sum(w * a * b)))
+    # MFEM CGSolver
+    x = np.zeros(m.nl)
+    r = B.copy()
+    z = dinv * r
+    d = z.copy()
+    nom = nom0 = dot(d, r)
+    r0 = max(nom * 1e-24, 0.0)
+    q = amult(d)
+    den = dot(d, q)
+    it = 0
+    for it in range(1, 500):
+        alpha = nom / den
+        x += alpha * d
+        r -= alpha * q
+        z = dinv * r
+        betanom = dot(r, z)
+        if betanom <= r0:
+            break
+        d = z + (betanom / nom) * d
+        q = amult(d)
+        den = dot(d, q)
+        nom = betanom
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), x)
+    np.save(os.path.join(out_dir, f"its{rank}.npy"), np.array([it]))
+    dist.destroy_process_group()
+
+
+def test_slab_cg_matches_single_domain(tmp_path):
+    from oracle import oracle as O
+    world = 2
+    mp.start_processes(_cpu_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    full = O.BoxMesh(3, (N, N, NZ), P)
+    A = O.fa_assemble(full, kappa=KAPPA, s=S, kinds=O.DIFFUSION | O.MASS)
+    prm = O.mms_params(O.MMS_SIN, 3, kappa=KAPPA, s=S, c=(0.0, 0.0, 0.0), p=P)
+    Ac, Bo = O.form_linear_system(A, full.bdr, np.zeros(full.nl), O.lf_assemble(full, prm))
+    xo, io = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=1e-12, max_iter=500)
+    plane = (P * N + 1) ** 2
+    x0, x1 = np.load(tmp_path / "x0.npy"), np.load(tmp_path / "x1.npy")
+    per_rank = plane * (P * NZ // world)
+    xg = np.concatenate([x0, x1[plane:]])         # rank 1's first plane duplicates rank 0's last
+    assert len(xg) == full.nl
+    np.testing.assert_allclose(x1[:plane], x0[-plane:], rtol=0, atol=1e-14)   # consistent copies
+    assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
+    its = int(np.load(tmp_path / "its0.npy")[0])
+    assert abs(its - io["iterations"]) <= 1
+    assert per_rank + plane == len(x0)
+
+
+# ---------------------------------------------------------------------------------------------
+def _gpu_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    import cdfem
+    dist = _init(rank, world, port)
+    m = _slab(rank, world)
+    per = NZ // world
+    ctx = cdfem.Context(0)
+    ctx.upload_mesh(m).set_structured(N, N, per)
+    ctx.comm_init_torch()
+    ctx.set_slab(rank > 0, rank < world - 1)
+    ctx.pa_setup(kinds=cdfem.DIFFUSION | cdfem.MASS, kappa=KAPPA, mass=S)
+    b = np.random.default_rng(100 + rank).uniform(-1, 1, m.nl)
+    np.save(os.path.join(out_dir, f"b{rank}.npy"), b)
+    _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+    X, info = ctx.solve(B, method="cg", rel_tol=1e-12, max_iter=1000, check_every=5)
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), X)
+    np.save(os.path.join(out_dir, f"its{rank}.npy"), np.array([info["iterations"], info["converged"]]))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_two_ranks_one_device(tmp_path):
+    import cdfem
+    world = 2
+    mp.start_processes(_gpu_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    plane = (P * N + 1) ** 2
+    b0, b1 = np.load(tmp_path / "b0.npy"), np.load(tmp_path / "b1.npy")
+    # the single-domain right-hand side = sum of the rank-local (partial) L-vectors
+    bfull = np.concatenate([b0, np.zeros(len(b1) - plane)])
+    bfull[len(b0) - plane:] += b1
+    m = cdfem.box_mesh(3, (N, N, NZ), P)
+    with cdfem.Context(0) as ctx:
+        ctx.upload_mesh(m).set_structured(N, N, NZ)
+        ctx.pa_setup(kinds=cdfem.DIFFUSION | cdfem.MASS, kappa=KAPPA, mass=S)
+        _, B = ctx.form_linear_system(np.zeros(m.nl), bfull)
+        xs, info = ctx.solve(B, method="cg", rel_tol=1e-12, max_iter=1000)
+    x0, x1 = np.load(tmp_path / "x0.npy"), np.load(tmp_path / "x1.npy")
+    its = np.load(tmp_path / "its0.npy")
+    assert its[1] and abs(int(its[0]) - info["iterations"]) <= 1
+    np.testing.assert_allclose(x1[:plane], x0[-plane:], rtol=0, atol=1e-13 * np.abs(x0).max())
+    xg = np.concatenate([x0, x1[plane:]])
+    assert np.linalg.norm(xg - xs) <= 1e-10 * np.linalg.norm(xs)
