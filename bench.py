@@ -43,13 +43,17 @@ def parse():
     ap.add_argument("--cg-iters", type=int, default=100)
     ap.add_argument("--kinds", type=int, default=7, help="1 diffusion | 2 convection | 4 mass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=30)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="target length of the timed CPU-baseline sample (iterations scaled to it)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes of the apply kernel from a rocprofv3 --pmc pass")
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--path", choices=["brick", "generic"], default="brick",
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
+    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
+                    help="N>1 data-path communicator: rccl (production, one GPU per rank) or host "
+                         "(gloo callbacks; rehearses the N>1 flow with several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -96,8 +100,13 @@ def cpu_baseline(args, n, p, kinds):
     del A
     dinv = 1.0 / Ac.diag()
     t_asm = time.perf_counter() - t0
+    # calibrate on 10 iterations, then time a sample of about --cpu-seconds
     t0 = time.perf_counter()
-    _, info = O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=args.cpu_iters)
+    O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=10)
+    per_it = (time.perf_counter() - t0) / 10
+    n_it = int(min(20000, max(10, args.cpu_seconds / per_it)))
+    t0 = time.perf_counter()
+    _, info = O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=n_it)
     dt = time.perf_counter() - t0
     its = info["iterations"]
     return {"value": m.nl * its / dt, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
@@ -114,17 +123,21 @@ def main():
     # weak scaling: rank r owns elements iz in [r n, (r+1) n) of an n x n x (world n) mesh
     nz = n * world
     mesh = cdfem.box_mesh(3, (n, n, nz), p, z_range=(rank * n, (rank + 1) * n), with_coords=False)
-    ctx = cdfem.Context(local)
+    ndev = cdfem.device_count()
+    ctx = cdfem.Context(local % ndev if args.comm == "host" else local)
     ctx.upload_mesh(mesh)
     if args.path == "brick":
         ctx.set_structured(n, n, n)
     if world > 1:
         if args.path != "brick":
             raise SystemExit("multi-GPU runs use the structured brick path")
-        # RCCL communicator over xGMI; the id travels over the gloo control group
-        obj = [cdfem.comm_unique_id() if rank == 0 else None]
-        pg.broadcast_object_list(obj, src=0)
-        ctx.comm_init_rccl(rank, world, obj[0])
+        if args.comm == "rccl":
+            # RCCL communicator over xGMI; the id travels over the gloo control group
+            obj = [cdfem.comm_unique_id() if rank == 0 else None]
+            pg.broadcast_object_list(obj, src=0)
+            ctx.comm_init_rccl(rank, world, obj[0])
+        else:
+            ctx.comm_init_torch()
         ctx.set_slab(rank > 0, rank < world - 1)
     c = (1.0, -2.0, 0.5)
     ctx.pa_setup(kinds=args.kinds, kappa=0.1, alpha=1.0, conv=c, mass=1.0)
@@ -179,7 +192,7 @@ def main():
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": ("k_brick3d (patch gather + D/C/M PA apply + in-LDS E->L)" if args.path == "brick"
+                    "kernel": ("k_brick_cg (brick patch gather + D/C/M PA apply + in-LDS E->L + d.Ad)" if args.path == "brick"
                                else "k_apply3d (fused L->E gather + D/C/M PA apply)"),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
                     "launches": cnt,
@@ -187,6 +200,14 @@ def main():
                         "e2l": round(e_ms / max(e_cnt, 1) * 1e3, 2),
                         "cg_update": round(u_ms / max(u_cnt, 1) * 1e3, 2),
                         "cg_direction": round(d_ms / max(d_cnt, 1) * 1e3, 2)}}
+
+    # host-boundary (PCIe-inclusive) rate: one solve with B and X in host memory (not `value`)
+    host_rate = None
+    if world == 1:
+        t0 = time.perf_counter()
+        _, hinfo = ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0,
+                             max_iter=args.cg_iters, check_every=args.cg_iters)
+        host_rate = mesh.nl * hinfo["iterations"] / (time.perf_counter() - t0)
 
     ntrue = mesh.nl  # per rank (slab L-vector); interface planes counted once below
     total_dofs = (p * n + 1) ** 2 * (p * nz + 1) if world > 1 else ntrue
@@ -207,9 +228,13 @@ def main():
             "config": {"workload": f"{n}x{n}x{nz} hex, H1 p={p}, PA D+C+M (kinds={args.kinds}), "
                                    f"Jacobi-CG {args.cg_iters} it/step",
                        "dofs": total_dofs, "elements": n * n * nz, "cg_iters_per_step": args.cg_iters,
-                       "parallelism": f"slab{world}" if world > 1 else "single", "path": args.path},
+                       "parallelism": f"slab{world}" if world > 1 else "single", "path": args.path,
+                       **({"comm": args.comm} if world > 1 else {})},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if host_rate is not None:
+            out["host_boundary_rate"] = {"value": host_rate, "unit": "DoF-iter/s",
+                                         "note": "one solve with B/X in host memory (PCIe copies included)"}
         print(json.dumps(out), flush=True)
     ctx.free(dB)
     ctx.free(dX)

@@ -21,6 +21,10 @@ fi
 if [ "$STEP" = all ] || [ "$STEP" = prof ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_brick -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_brick.log 2>&1 || exit $?
 fi
+if [ "$STEP" = dist ]; then
+  # N>1 bench flow rehearsal: 2 ranks on the box's single GPU, host-callback communicator
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --comm host --cg-iters 20 > gpurun_out/bench_dist.log 2>&1 || exit $?
+fi
 if [ "$STEP" = cpu ]; then
   timeout -k 10 900 python bench.py --steps 3 --warmup 1 > gpurun_out/bench_full.log 2>&1 || exit $?
 fi

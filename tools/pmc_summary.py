@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Turn a tools/profile_round.sh output directory into the committed profile artifacts.
+
+  python tools/pmc_summary.py gpurun_out/prof_r01 r01
+
+writes profiles/<tag>_kernel_stats.csv   (rocprofv3 --kernel-trace --stats of the bench command)
+       profiles/<tag>_bench.json         (the bench line of the same round)
+       profiles/<tag>_pmc.json           (per-kernel HBM bytes per launch, corrected)
+       profiles/pmc_traffic.json         (the apply kernel's entry, read by bench.py -> roofline.traffic)
+
+Correction (MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE reports 1/2 of the bytes actually read.  The factor is not assumed but
+re-derived from the stream-probe calibration pass (k_stream_read over a known 1 GiB buffer) and
+the write factor from k_stream_copy (writes a known 1 GiB).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+GIB_KB = 1 << 20
+
+
+def per_kernel(path):
+    rows = list(csv.DictReader(open(path)))
+    agg = collections.defaultdict(float)
+    name = {}
+    for r in rows:
+        agg[r["Dispatch_Id"]] += float(r["Counter_Value"])
+        name[r["Dispatch_Id"]] = r["Kernel_Name"].split("(")[0]
+    out = collections.defaultdict(list)
+    for d, v in agg.items():
+        out[name[d]].append(v)
+    return {k: (sum(v) / len(v), len(v)) for k, v in out.items()}
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    json.dump(bench, open(os.path.join(prof, f"{tag}_bench.json"), "w"), indent=1)
+
+    cf = per_kernel(os.path.join(src, "calib_FETCH_SIZE", "run_counter_collection.csv"))
+    cw = per_kernel(os.path.join(src, "calib_WRITE_SIZE", "run_counter_collection.csv"))
+    f_corr = GIB_KB / cf["k_stream_read"][0]          # ~2.0 on gfx950
+    w_corr = GIB_KB / cw["k_stream_copy"][0]          # ~1.0
+    fetch = per_kernel(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"))
+    write = per_kernel(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"))
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        fb = fetch.get(k, (0.0, 0))[0] * 1024 * f_corr
+        wb = write.get(k, (0.0, 0))[0] * 1024 * w_corr
+        kernels[k] = {"launches": fetch.get(k, (0, 0))[1], "read_bytes": round(fb), "write_bytes": round(wb),
+                      "hbm_bytes_per_launch": round(fb + wb)}
+    cfg = bench["config"]
+    alg = bench["roofline"]["algorithmic_bytes_per_launch"]
+    apply = kernels["k_brick_cg"] if cfg.get("path") == "brick" else kernels["k_apply3d"]
+    pmc = {"tag": tag, "fetch_correction": f_corr, "write_correction": w_corr,
+           "calibration": "k_stream_read (1 GiB read) / k_stream_copy (1 GiB write)",
+           "workload": cfg["workload"], "kernels": kernels,
+           "apply_kernel": {"hbm_bytes_per_launch": apply["hbm_bytes_per_launch"],
+                            "algorithmic_bytes_per_launch": alg,
+                            "traffic_over_algorithmic": apply["hbm_bytes_per_launch"] / alg}}
+    json.dump(pmc, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
+    p = os.path.join(prof, "pmc_traffic.json")
+    tj = json.load(open(p)) if os.path.exists(p) else {}
+    n = int(cfg["workload"].split("x")[0])
+    order = int(cfg["workload"].split("p=")[1].split(",")[0])
+    kinds = int(cfg["workload"].split("kinds=")[1].split(")")[0])
+    tj[f"n{n}_p{order}_k{kinds}"] = {"hbm_bytes_per_launch": apply["hbm_bytes_per_launch"], "round": tag,
+                                     "path": cfg.get("path"), "source": f"profiles/{tag}_pmc.json"}
+    json.dump(tj, open(p, "w"), indent=1)
+    print(json.dumps(pmc["apply_kernel"]), f_corr, w_corr)
+
+
+if __name__ == "__main__":
+    main()
