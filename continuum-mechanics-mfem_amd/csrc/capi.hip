@@ -90,7 +90,7 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_verts); dfree(c->d_map); dfree(c->d_e2l_off); dfree(c->d_e2l_pos);
     dfree(c->d_ess); dfree(c->d_ess_list); dfree(c->d_qd); dfree(c->d_Ye); dfree(c->d_dinv);
     for (auto &w : c->d_w) dfree(w);
-    dfree(c->d_part); dfree(c->d_gm); dfree(c->d_gm_small);
+    dfree(c->d_part); dfree(c->d_gm); dfree(c->d_gm_part);
     dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones); dfree(c->d_dalt);
     for (auto &b : c->d_if) dfree(b);
     c->zlo_shared = c->zhi_shared = 0;
@@ -102,7 +102,7 @@ void free_mesh(cdfem_ctx *c)
 // ---- profiling helpers ---------------------------------------------------------------------------
 void prof_mark(cdfem_ctx *c, int k, bool begin)
 {
-    if (!c->profile) return;
+    if (!c->profile || !((c->prof_mask >> k) & 1u)) return;
     ProfileSlot &s = c->prof[k];
     const size_t need = (size_t)(s.used + 1) * 2;
     while (s.ev.size() < need) {
@@ -380,6 +380,81 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     HIPCHK(hipMemcpyAsync(dX, x, c->nl * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
 }
 
+// PETSc KSPGMRES(m) + left Jacobi on the constrained operator (gmres.hip).  One host sync per
+// restart cycle plus a lag-one poll inside the cycle: step j + 1 is queued before the host waits
+// for step j's flags, so the GPU never idles on the host; a step queued past the end of a cycle
+// costs one wasted operator apply (its GMRES kernels exit at entry).
+void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, double *dX,
+                 cdfem_solver_result &res)
+{
+    if (multi_rank(c)) throw UnsupportedError("GMRES on a multi-rank partition is not available yet");
+    const int m = p.restart > 0 ? p.restart : 30;
+    if (m > kGmMaxRestart) throw ArgError("restart > 64");
+    const int64_t n = c->nl;
+    const int nb = gmres_blocks(n);
+    if (c->gm_cap < m) {
+        dfree(c->d_gm);
+        dfree(c->d_gm_part);
+        c->d_gm = dalloc<double>((size_t)(m + 1) * n);
+        c->d_gm_part = dalloc<double>((size_t)(m + 1) * nb);
+        c->gm_cap = m;
+    }
+    if (!c->d_gmst) {
+        HIPCHK(hipMalloc(&c->d_gmst, sizeof(GmresState)));
+        HIPCHK(hipHostMalloc(&c->h_gmpoll, 2 * sizeof(GmresState), hipHostMallocDefault));
+        for (auto &e : c->gm_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    const double *dinv = nullptr;
+    if (p.pc == CDFEM_PC_JACOBI) {
+        ensure_dinv(c);
+        dinv = c->d_dinv;
+    }
+    double *x = c->d_w[2], *w = c->d_w[4], *V = c->d_gm, *part = c->d_gm_part;
+    GmresState *st = c->d_gmst, *poll = c->h_gmpoll;
+    auto post = [&](int slot) {
+        HIPCHK(hipMemcpyAsync(&poll[slot], st, kGmPollBytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipEventRecord(c->gm_ev[slot], c->stream));
+    };
+    auto wait = [&](int slot) -> const GmresState & {
+        HIPCHK(hipEventSynchronize(c->gm_ev[slot]));
+        return poll[slot];
+    };
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(hipMemsetAsync(x, 0, n * sizeof(double), c->stream));
+    HIPCHK(launch_gm_init(c, st, m, p.max_iter));
+    for (bool first = true;; first = false) {
+        // v0 = M^{-1}(b - A x); x = 0 on the first cycle, so A x is skipped there
+        if (!first) op_apply(c, x, w, true);
+        HIPCHK(launch_gm_residual(c, dB, first ? nullptr : w, dinv, V, part, st, first, p.rel_tol, p.abs_tol));
+        post(0);
+        if (wait(0).done) break;
+        for (int j = 0; j < m; ++j) {
+            op_apply(c, V + (int64_t)j * n, w, true);
+            prof_mark(c, CDFEM_K_ORTH, true);
+            HIPCHK(launch_gm_orth(c, w, dinv, V, n, part, st));
+            prof_mark(c, CDFEM_K_ORTH, false);
+            post(j & 1);
+            if (j > 0 && wait((j - 1) & 1).cycle_done) break;
+        }
+        prof_mark(c, CDFEM_K_UPDATE, true);
+        HIPCHK(launch_gm_update(c, x, V, n, st));
+        prof_mark(c, CDFEM_K_UPDATE, false);
+        post(0);
+        if (wait(0).done) break;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    prof_collect(c);
+    GmresState fin{};
+    HIPCHK(hipMemcpy(&fin, st, sizeof(GmresState), hipMemcpyDeviceToHost));
+    res.converged = fin.converged;
+    res.iterations = fin.its;
+    res.initial_norm = fin.res0;
+    res.final_norm = fin.res;
+    res.seconds = std::chrono::duration<double>(t1 - t0).count();
+    HIPCHK(hipMemcpyAsync(dX, x, n * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -426,6 +501,10 @@ void cdfem_destroy(cdfem_ctx *c)
     comm_destroy(c);
     if (c->d_state) (void)hipFree(c->d_state);
     if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->d_gmst) (void)hipFree(c->d_gmst);
+    if (c->h_gmpoll) (void)hipHostFree(c->h_gmpoll);
+    for (auto e : c->gm_ev)
+        if (e) (void)hipEventDestroy(e);
     for (auto &s : c->prof)
         for (auto e : s.ev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -756,8 +835,10 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
                 solve_cg_brick(c, *p, dB, dX, *res);
             else
                 solve_cg(c, *p, dB, dX, *res);
+        } else if (p->method == CDFEM_GMRES) {
+            solve_gmres(c, *p, dB, dX, *res);
         } else {
-            throw UnsupportedError("GMRES is not available in this build");
+            throw ArgError("unknown method");
         }
         dev_out(c, X, where, dX, c->nl);
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -801,6 +882,8 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         if (k == "brick_variant") {
             if (value < 0 || value > 2) throw ArgError("brick_variant must be 0, 1 or 2");
             c->brick_variant = value;
+        } else if (k == "profile_mask") {
+            c->prof_mask = (unsigned)value;
         } else if (k == "brick_waves") {
             if (value != 1 && value != 2) throw ArgError("brick_waves must be 1 or 2");
             c->brick_waves = value;

@@ -50,6 +50,21 @@ struct KrylovState {
     unsigned reserved[4];
 };
 
+// Device-side GMRES(m) state (gmres.hip).  The first 32 bytes are what the host polls.
+constexpr int kGmMaxRestart = 64;
+struct GmresState {
+    int cycle_done, done, converged, its;
+    double res;
+    int j, kk;
+    // ----
+    int max_it, m;
+    double ttol, res0;
+    double s[kGmMaxRestart + 1];   // basis scales: v_i = s_i * V_i
+    double g[kGmMaxRestart + 1], cs[kGmMaxRestart], sn[kGmMaxRestart];
+    double H[(kGmMaxRestart + 1) * kGmMaxRestart];  // row-major, leading dimension kGmMaxRestart
+};
+constexpr size_t kGmPollBytes = 32;
+
 struct Comm;  // comm.hip
 
 struct ProfileSlot {
@@ -118,11 +133,15 @@ struct cdfem_ctx {
     cdfem::KrylovState *h_state = nullptr;  // pinned
     double *d_gm = nullptr;             // GMRES basis (restart+1) * nl
     int gm_cap = 0;
-    double *d_gm_small = nullptr;       // GMRES Hessenberg / Givens workspace
+    double *d_gm_part = nullptr;        // GMRES partials [(restart+1) * blocks]
+    cdfem::GmresState *d_gmst = nullptr;   // device GMRES state
+    cdfem::GmresState *h_gmpoll = nullptr; // pinned, 2 poll slots of kGmPollBytes
+    hipEvent_t gm_ev[2] = {};
 
     // profiling
     bool profile = false;
     cdfem::ProfileSlot prof[CDFEM_K_COUNT];
+    unsigned prof_mask = ~0u;  // kernels that get HIP events while profiling (set_option profile_mask)
 };
 
 namespace cdfem {
@@ -195,6 +214,14 @@ hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double
 hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q);
 
 // ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
+// GMRES(m) (gmres.hip)
+int gmres_blocks(int64_t n);
+hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it);
+hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
+                              double *part, GmresState *st, bool first, double rtol, double atol);
+hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
+                          GmresState *st);
+hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st);
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 
 }  // namespace cdfem

@@ -1,0 +1,300 @@
+// gmres.hip — restarted GMRES(m) with left Jacobi preconditioning, device-resident.
+//
+// Semantics: PETSc KSPGMRES as the reference configures it (Input/petsc.opts:2-6 "-ksp_type gmres
+// -pc_type jacobi -ksp_rtol 1e-10 -ksp_atol 1e-12", solver built at
+// linear_convection_diffusion_2D.cpp:364-374): restart m (PETSc default 30), LEFT preconditioning,
+// classical Gram-Schmidt without refinement, Givens rotations, convergence on the preconditioned
+// residual norm  res <= max(rtol * res0, atol)  (KSPConvergedDefault), zero initial guess.
+// The CPU restatement is oracle/cdfem_oracle.c:orc_gmres.
+//
+// MI355X layout: the Krylov basis V is (m + 1) L-vectors contiguous in HBM.  Basis vectors are
+// stored UNNORMALISED with a device scalar s_i (v_i = s_i * V_i), which removes the separate
+// normalisation pass.  Per inner step j (besides the operator apply):
+//   pass 1  w = s_j M^{-1} (A V_j), h_i = s_i (w, V_i) for all i <= j   (reads w once, V_0..j once)
+//   fin     h_i summed over blocks in fixed order -> H[:, j]
+//   pass 2  V_{j+1} = w - sum_i h_i s_i V_i and the partials of |V_{j+1}|^2
+//   fin     h_{j+1,j}, Givens rotation, residual estimate, cycle control flags
+// Bytes per step = 8 N (2 j + 7) + apply.  All reductions: fixed grid, fixed order (bitwise
+// reproducible).  Every kernel checks the cycle_done flag, so steps the host queued beyond the end
+// of a cycle exit at entry.
+#include <hip/hip_runtime.h>
+
+#include "cdfem_internal.hpp"
+#include "reduce.hpp"
+
+namespace cdfem {
+
+constexpr int kGmEPT = 8;                         // L-vector entries per thread in the pass kernels
+constexpr int kGmChunk = kRedThreads * kGmEPT;    // entries per block
+
+int gmres_blocks(int64_t n) { return (int)((n + kGmChunk - 1) / kGmChunk); }
+
+// ---- v0 = M^{-1} (b - A x) and partials of |v0|^2 ------------------------------------------------
+__global__ void __launch_bounds__(kRedThreads)
+k_gm_residual(const double *__restrict__ b, const double *__restrict__ Ax, const double *__restrict__ dinv,
+              double *__restrict__ v0, int64_t n, double *__restrict__ part, const GmresState *__restrict__ st)
+{
+    __shared__ double sh[kRedThreads / 64];
+    if (st->done) return;
+    const int64_t base = (int64_t)blockIdx.x * kGmChunk + threadIdx.x;
+    double acc = 0.0;
+#pragma unroll
+    for (int e = 0; e < kGmEPT; ++e) {
+        const int64_t k = base + (int64_t)e * kRedThreads;
+        if (k < n) {
+            double r = Ax ? b[k] - Ax[k] : b[k];
+            if (dinv) r *= dinv[k];
+            v0[k] = r;
+            acc += r * r;
+        }
+    }
+    store_partial(block_sum(acc, sh), part);
+}
+
+// ---- start of a cycle: beta = |v0|, first-cycle tolerance, convergence / max_it test ------------
+__global__ void __launch_bounds__(1024)
+k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st, int first, double rtol,
+           double atol)
+{
+    __shared__ double sh[1024 / 64];
+    const double sum = sum_partials(part, nb, sh);
+    if (threadIdx.x != 0 || st->done) return;
+    const double beta = sqrt(sum);
+    st->res = beta;
+    if (first) {
+        st->ttol = fmax(rtol * beta, atol);
+        st->res0 = beta;
+    }
+    st->cycle_done = 1;
+    if (beta <= st->ttol || beta == 0.0) {
+        st->converged = 1;
+        st->done = 1;
+        return;
+    }
+    if (st->its >= st->max_it) {
+        st->done = 1;
+        return;
+    }
+    st->s[0] = 1.0 / beta;
+    for (int i = 0; i <= st->m; ++i) st->g[i] = 0.0;
+    st->g[0] = beta;
+    st->j = 0;
+    st->kk = 0;
+    st->cycle_done = 0;
+}
+
+// ---- pass 1: w = s_j M^{-1} A V_j (in place over the apply output), partial (w, V_i), i <= j ----
+__global__ void __launch_bounds__(kRedThreads)
+k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double *__restrict__ V, int64_t n,
+           int64_t ldv, double *__restrict__ part, int nb, const GmresState *__restrict__ st)
+{
+    __shared__ double sh[kRedThreads / 64];
+    if (st->cycle_done) return;
+    const int j = st->j;
+    const double sj = st->s[j];
+    const int64_t base = (int64_t)blockIdx.x * kGmChunk + threadIdx.x;
+    double wv[kGmEPT];
+#pragma unroll
+    for (int e = 0; e < kGmEPT; ++e) {
+        const int64_t k = base + (int64_t)e * kRedThreads;
+        double v = 0.0;
+        if (k < n) {
+            v = sj * w[k];
+            if (dinv) v *= dinv[k];
+            w[k] = v;
+        }
+        wv[e] = v;
+    }
+    for (int i = 0; i <= j; ++i) {
+        const double *vi = V + (int64_t)i * ldv;
+        double acc = 0.0;
+#pragma unroll
+        for (int e = 0; e < kGmEPT; ++e) {
+            const int64_t k = base + (int64_t)e * kRedThreads;
+            if (k < n) acc += wv[e] * vi[k];
+        }
+        const double t = block_sum(acc, sh);
+        if (threadIdx.x == 0) part[(int64_t)i * nb + blockIdx.x] = t;
+        __syncthreads();  // sh is reused by the next block_sum
+    }
+}
+
+// ---- H[i][j] = s_i * sum_b part[i][b], one wave per i (fixed order) ------------------------------
+__global__ void __launch_bounds__(1024)
+k_gm_dots_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ st)
+{
+    if (st->cycle_done) return;
+    const int j = st->j;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = wv; i <= j; i += 16) {
+        double v = 0.0;
+        for (int b = lane; b < nb; b += 64) v += part[(int64_t)i * nb + b];
+        v = wave_sum(v);
+        if (lane == 0) st->H[i * kGmMaxRestart + j] = st->s[i] * v;
+    }
+}
+
+// ---- pass 2: V_{j+1} = w - sum_i H[i][j] s_i V_i, partials of |V_{j+1}|^2 ------------------------
+__global__ void __launch_bounds__(kRedThreads)
+k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int64_t ldv,
+           double *__restrict__ part, const GmresState *__restrict__ st)
+{
+    __shared__ double sh[kRedThreads / 64];
+    if (st->cycle_done) return;
+    const int j = st->j;
+    const int64_t base = (int64_t)blockIdx.x * kGmChunk + threadIdx.x;
+    double acc[kGmEPT];
+#pragma unroll
+    for (int e = 0; e < kGmEPT; ++e) {
+        const int64_t k = base + (int64_t)e * kRedThreads;
+        acc[e] = k < n ? w[k] : 0.0;
+    }
+    for (int i = 0; i <= j; ++i) {
+        const double coef = st->H[i * kGmMaxRestart + j] * st->s[i];
+        const double *vi = V + (int64_t)i * ldv;
+#pragma unroll
+        for (int e = 0; e < kGmEPT; ++e) {
+            const int64_t k = base + (int64_t)e * kRedThreads;
+            if (k < n) acc[e] -= coef * vi[k];
+        }
+    }
+    double *vn = V + (int64_t)(j + 1) * ldv;
+    double nrm = 0.0;
+#pragma unroll
+    for (int e = 0; e < kGmEPT; ++e) {
+        const int64_t k = base + (int64_t)e * kRedThreads;
+        if (k < n) {
+            vn[k] = acc[e];
+            nrm += acc[e] * acc[e];
+        }
+    }
+    store_partial(block_sum(nrm, sh), part);
+}
+
+// ---- h_{j+1,j}, Givens rotations, residual estimate, cycle control ------------------------------
+__global__ void __launch_bounds__(1024)
+k_gm_norm_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ st)
+{
+    __shared__ double sh[1024 / 64];
+    if (st->cycle_done) return;  // uniform: every thread reads the same flag before the reduction
+    const double sum = sum_partials(part, nb, sh);
+    if (threadIdx.x != 0) return;
+    constexpr int LD = kGmMaxRestart;
+    const int j = st->j;
+    double *H = st->H;
+    const double hn = sqrt(sum);
+    H[(j + 1) * LD + j] = hn;
+    for (int i = 0; i < j; ++i) {
+        const double a = H[i * LD + j], c2 = H[(i + 1) * LD + j];
+        H[i * LD + j] = st->cs[i] * a + st->sn[i] * c2;
+        H[(i + 1) * LD + j] = -st->sn[i] * a + st->cs[i] * c2;
+    }
+    const double a = H[j * LD + j], c2 = H[(j + 1) * LD + j];
+    const double rr = sqrt(a * a + c2 * c2);
+    st->cs[j] = (rr == 0.0) ? 1.0 : a / rr;
+    st->sn[j] = (rr == 0.0) ? 0.0 : c2 / rr;
+    H[j * LD + j] = rr;
+    H[(j + 1) * LD + j] = 0.0;
+    st->g[j + 1] = -st->sn[j] * st->g[j];
+    st->g[j] = st->cs[j] * st->g[j];
+    st->res = fabs(st->g[j + 1]);
+    st->kk = j + 1;
+    st->its += 1;
+    st->s[j + 1] = (hn != 0.0) ? 1.0 / hn : 0.0;
+    st->j = j + 1;
+    if (hn == 0.0 || st->res <= st->ttol || j + 1 == st->m || st->its >= st->max_it) st->cycle_done = 1;
+}
+
+// ---- end of cycle: y = H_k^{-1} g_k (every block, redundantly: k <= 64), x += sum_i y_i s_i V_i --
+__global__ void __launch_bounds__(kRedThreads)
+k_gm_update(double *__restrict__ x, const double *__restrict__ V, int64_t n, int64_t ldv,
+            const GmresState *__restrict__ st)
+{
+    __shared__ double y[kGmMaxRestart];
+    if (st->done) return;
+    const int kk = st->kk;
+    if (threadIdx.x == 0) {
+        constexpr int LD = kGmMaxRestart;
+        for (int i = kk - 1; i >= 0; --i) {
+            double acc = st->g[i];
+            for (int l = i + 1; l < kk; ++l) acc -= st->H[i * LD + l] * y[l];
+            y[i] = acc / st->H[i * LD + i];
+        }
+        for (int i = 0; i < kk; ++i) y[i] *= st->s[i];
+    }
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kGmChunk + threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < kGmEPT; ++e) {
+        const int64_t k = base + (int64_t)e * kRedThreads;
+        if (k >= n) continue;
+        double v = x[k];
+        for (int i = 0; i < kk; ++i) v += y[i] * V[(int64_t)i * ldv + k];
+        x[k] = v;
+    }
+}
+
+__global__ void k_gm_cycle_end(GmresState *__restrict__ st)
+{
+    if (st->done) return;
+    if (st->res <= st->ttol) {
+        st->converged = 1;
+        st->done = 1;
+    } else if (st->its >= st->max_it) {
+        st->done = 1;
+    }
+}
+
+__global__ void k_gm_init(GmresState *__restrict__ st, int m, int max_it)
+{
+    st->cycle_done = 1;
+    st->done = 0;
+    st->converged = 0;
+    st->its = 0;
+    st->j = 0;
+    st->kk = 0;
+    st->max_it = max_it;
+    st->m = m;
+    st->res = 0.0;
+    st->ttol = 0.0;
+    st->res0 = 0.0;
+}
+
+// ---- launchers ---------------------------------------------------------------------------------
+hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it)
+{
+    hipLaunchKernelGGL(k_gm_init, dim3(1), dim3(1), 0, c->stream, st, m, max_it);
+    return hipGetLastError();
+}
+
+hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
+                              double *part, GmresState *st, bool first, double rtol, double atol)
+{
+    const int nb = gmres_blocks(c->nl);
+    hipLaunchKernelGGL(k_gm_residual, dim3(nb), dim3(kRedThreads), 0, c->stream, b, Ax, dinv, v0,
+                       (int64_t)c->nl, part, st);
+    hipLaunchKernelGGL(k_gm_start, dim3(1), dim3(1024), 0, c->stream, part, nb, st, first ? 1 : 0, rtol, atol);
+    return hipGetLastError();
+}
+
+hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
+                          GmresState *st)
+{
+    const int nb = gmres_blocks(c->nl);
+    const int64_t n = c->nl;
+    hipLaunchKernelGGL(k_gm_pass1, dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv, part, nb, st);
+    hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st);
+    hipLaunchKernelGGL(k_gm_pass2, dim3(nb), dim3(kRedThreads), 0, c->stream, w, V, n, ldv, part, st);
+    hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st)
+{
+    const int nb = gmres_blocks(c->nl);
+    hipLaunchKernelGGL(k_gm_update, dim3(nb), dim3(kRedThreads), 0, c->stream, x, V, (int64_t)c->nl, ldv, st);
+    hipLaunchKernelGGL(k_gm_cycle_end, dim3(1), dim3(1), 0, c->stream, st);
+    return hipGetLastError();
+}
+
+}  // namespace cdfem

@@ -29,7 +29,7 @@ HOST, DEVICE = 0, 1
 CG, GMRES = 0, 1
 PC_NONE, PC_JACOBI = 0, 1
 RULE_OPERATOR, RULE_LINEARFORM, RULE_ERROR = 0, 1, 2
-K_APPLY, K_E2L, K_UPDATE, K_DIRECTION = 0, 1, 2, 3
+K_APPLY, K_E2L, K_UPDATE, K_DIRECTION, K_ORTH = 0, 1, 2, 3, 4
 
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_UNSUPPORTED, ERR_NOT_CONVERGED, ERR_COMM = range(7)
 

@@ -54,7 +54,8 @@ enum { CDFEM_PC_NONE = 0, CDFEM_PC_JACOBI = 1 };
 /* quadrature rules whose points the host may need for coefficient evaluation */
 enum { CDFEM_RULE_OPERATOR = 0, CDFEM_RULE_LINEARFORM = 1, CDFEM_RULE_ERROR = 2 };
 /* kernel ids for cdfem_profile_read */
-enum { CDFEM_K_APPLY = 0, CDFEM_K_E2L = 1, CDFEM_K_UPDATE = 2, CDFEM_K_DIRECTION = 3, CDFEM_K_COUNT = 8 };
+enum { CDFEM_K_APPLY = 0, CDFEM_K_E2L = 1, CDFEM_K_UPDATE = 2, CDFEM_K_DIRECTION = 3, CDFEM_K_ORTH = 4,
+       CDFEM_K_COUNT = 8 };
 
 int cdfem_abi_version(void);
 
@@ -131,6 +132,8 @@ int cdfem_form_linear_system(cdfem_ctx *ctx, const double *x, const double *b, d
  * CG follows MFEM CGSolver (convergence (r,z) <= max(nom0 rel^2, abs^2)); GMRES follows PETSc
  * KSPGMRES (left PC, classical Gram-Schmidt, restart, ||M^{-1} r|| <= max(rtol ||M^{-1}b||, atol)).
  * X on input is ignored (zero initial guess, iterative_mode = false), on output the solution.
+ * GMRES: restart 1..64; iterations = inner steps; final_norm = last preconditioned residual
+ * estimate (PETSc rnorm); single rank only in this version (CDFEM_ERR_UNSUPPORTED otherwise).
  * Returns CDFEM_ERR_NOT_CONVERGED (result filled) when max_iter is reached.                     */
 typedef struct {
     int method;        /* CDFEM_CG / CDFEM_GMRES */
@@ -160,6 +163,8 @@ int cdfem_stream_bench(cdfem_ctx *ctx, int mode, size_t bytes, int reps, double 
 
 /* ---- tuning knobs (performance only; results identical to rounding) --------------------------
  * "brick_waves": 1 or 2 — register budget of the structured Mult kernel (waves per SIMD).
+ * "profile_mask": bit k set = kernel slot k (CDFEM_K_*) gets HIP events while profiling is on
+ *                 (default all; events around every kernel cost ~1 us each on the stream).
  * "brick_variant": 0, 1, 2 — element core of the structured CG kernel (unrolled / plane loop /
  *                  low-register).                                                               */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
