@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cg-iters", type=int, default=100)
     ap.add_argument("--kinds", type=int, default=7, help="1 diffusion | 2 convection | 4 mass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gmres-iters", type=int, default=60,
+                    help="informational GMRES(30)+Jacobi line (the reference's solver); 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target length of the timed CPU-baseline sample (iterations scaled to it)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -217,6 +219,33 @@ def main():
                              max_iter=args.cg_iters, check_every=args.cg_iters)
         host_rate = mesh.nl * hinfo["iterations"] / (time.perf_counter() - t0)
 
+    # informational: GMRES(30) + Jacobi (Input/petsc.opts) on the same operator, fixed inner steps
+    gm = None
+    if world == 1 and args.gmres_iters > 0:
+        def gstep():
+            return ctx.solve_device(dB, dX, method="gmres", pc="jacobi", rel_tol=0.0, abs_tol=0.0,
+                                    max_iter=args.gmres_iters, restart=30)
+        gstep()
+        ctx.synchronize()
+        ctx.set_option("profile_mask", -1)
+        ctx.profile(True)
+        t0 = time.perf_counter()
+        ginfo = gstep()
+        ctx.synchronize()
+        gdt = time.perf_counter() - t0
+        o_ms, o_cnt = ctx.profile_read(cdfem.K_ORTH)
+        a_ms, a_cnt = ctx.profile_read(cdfem.K_APPLY)
+        ctx.profile(False)
+        its = ginfo["iterations"]
+        # CGS passes at inner step j move 8 N (2 j + 7) bytes (gmres.hip header)
+        js = [k % 30 for k in range(its)]
+        orth_bytes = sum(8.0 * mesh.nl * (2 * j + 7) for j in js) / max(len(js), 1)
+        gm = {"value": mesh.nl * its / gdt, "unit": "DoF-iter/s", "iterations": its, "restart": 30,
+              "ms_per_iter": gdt / max(its, 1) * 1e3,
+              "apply_avg_us": round(a_ms / max(a_cnt, 1) * 1e3, 2),
+              "orth_avg_us": round(o_ms / max(o_cnt, 1) * 1e3, 2),
+              "orth_achieved_gbs": round(orth_bytes / (o_ms / max(o_cnt, 1) * 1e-3) / 1e9, 1) if o_cnt else None}
+
     ntrue = mesh.nl  # per rank (slab L-vector); interface planes counted once below
     total_dofs = (p * n + 1) ** 2 * (p * nz + 1) if world > 1 else ntrue
     value = total_dofs * iters / dt_max
@@ -240,6 +269,8 @@ def main():
                        **({"comm": args.comm} if world > 1 else {})},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if gm is not None:
+            out["gmres"] = gm
         if host_rate is not None:
             out["host_boundary_rate"] = {"value": host_rate, "unit": "DoF-iter/s",
                                          "note": "one solve with B/X in host memory (PCIe copies included)"}
