@@ -8,6 +8,7 @@
 // L2-error rule max(2, 2p+3) (:383).
 #include <cmath>
 #include <stdexcept>
+#include <vector>
 
 #include "cdfem_internal.hpp"
 
@@ -119,6 +120,70 @@ int rule_points_1d(int which, int dim, int p)
     default: throw std::runtime_error("bad rule id");
     }
     return order / 2 + 1;
+}
+
+// ---- simplices (P1/P2 Lagrange on triangles / tetrahedra, BASELINE config C4) ----------------
+// Collapsed tensor Gauss-Legendre rule on the reference simplex (0, e_1, .., e_dim), n points per
+// direction: xi_1 = u, xi_2 = (1-u) v, xi_3 = (1-u)(1-v) w, weight w_u w_v w_w (1-u)^(dim-1) (1-v)
+// (3D).  Exact to degree 2n - dim; n = p + 2 integrates the mass form of P2 exactly in 3D.
+int simplex_rule(int dim, int n, std::vector<double> &xi, std::vector<double> &w)
+{
+    std::vector<double> x(n), wx(n);
+    gauss_legendre(n, x.data(), wx.data());
+    const int nq = dim == 3 ? n * n * n : n * n;
+    xi.assign((size_t)nq * dim, 0.0);
+    w.assign(nq, 0.0);
+    int q = 0;
+    for (int iu = 0; iu < n; ++iu)
+        for (int iv = 0; iv < n; ++iv) {
+            const double u = x[iu], v = x[iv];
+            if (dim == 2) {
+                xi[q * 2] = u;
+                xi[q * 2 + 1] = (1.0 - u) * v;
+                w[q] = wx[iu] * wx[iv] * (1.0 - u);
+                ++q;
+                continue;
+            }
+            for (int iw = 0; iw < n; ++iw, ++q) {
+                xi[q * 3] = u;
+                xi[q * 3 + 1] = (1.0 - u) * v;
+                xi[q * 3 + 2] = (1.0 - u) * (1.0 - v) * x[iw];
+                w[q] = wx[iu] * wx[iv] * wx[iw] * (1.0 - u) * (1.0 - u) * (1.0 - v);
+            }
+        }
+    return nq;
+}
+
+int simplex_ndofs(int dim, int p) { return p == 1 ? dim + 1 : (dim + 1) * (dim + 2) / 2; }
+
+// Local order: vertices, then edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3) [2D (0,1),(0,2),(1,2)].
+const int kSimplexEdge[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
+const int kTriEdge[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+
+void simplex_basis(int dim, int p, const double *xi, double *phi, double *dphi)
+{
+    double lam[4], dl[4][3] = {};
+    lam[0] = 1.0;
+    for (int k = 0; k < dim; ++k) {
+        lam[0] -= xi[k];
+        dl[0][k] = -1.0;
+        lam[k + 1] = xi[k];
+        dl[k + 1][k] = 1.0;
+    }
+    for (int a = 0; a <= dim; ++a) {
+        phi[a] = p == 1 ? lam[a] : lam[a] * (2.0 * lam[a] - 1.0);
+        const double f = p == 1 ? 1.0 : 4.0 * lam[a] - 1.0;
+        for (int k = 0; k < dim; ++k) dphi[a * dim + k] = f * dl[a][k];
+    }
+    if (p == 1) return;
+    const int nedge = dim == 3 ? 6 : 3;
+    for (int e = 0; e < nedge; ++e) {
+        const int a = dim == 3 ? kSimplexEdge[e][0] : kTriEdge[e][0];
+        const int b = dim == 3 ? kSimplexEdge[e][1] : kTriEdge[e][1];
+        const int l = dim + 1 + e;
+        phi[l] = 4.0 * lam[a] * lam[b];
+        for (int k = 0; k < dim; ++k) dphi[l * dim + k] = 4.0 * (lam[a] * dl[b][k] + lam[b] * dl[a][k]);
+    }
 }
 
 }  // namespace cdfem

@@ -38,6 +38,12 @@ struct Rule1D {
 // Product implementation of the 1D rules (independent of the oracle): basis.cpp
 void gll_nodes(int p, double *x);
 void gauss_legendre(int n, double *x, double *w);
+// simplices (basis.cpp)
+int simplex_rule(int dim, int n, std::vector<double> &xi, std::vector<double> &w);
+int simplex_ndofs(int dim, int p);
+void simplex_basis(int dim, int p, const double *xi, double *phi, double *dphi);
+extern const int kSimplexEdge[6][2];
+extern const int kTriEdge[3][2];
 Rule1D make_rule(int p, int q1);
 // MFEM default rule sizes on multilinear tensor elements (which: 0 operator, 1 LF, 2 L2 error)
 int rule_points_1d(int which, int dim, int p);
@@ -115,6 +121,22 @@ struct cdfem_ctx {
 
     // rules
     cdfem::Rule1D rule_op, rule_lf, rule_err;
+
+    // geometry family: 0 tensor (quad/hex: PA), 1 simplex (tri/tet: FA, cdfem_mesh_upload_simplex)
+    int geom = 0;
+    int nq_simplex = 0;                 // points of the simplex operator rule
+    double *d_stab = nullptr;           // simplex rule tables: phi [nq][nd], dphi [nq][nd][dim], w [nq]
+    std::vector<double> h_verts;        // simplex host geometry (quadrature points for coefficients)
+    std::vector<double> h_sxi;          // simplex rule points (reference coordinates)
+    // full assembly (cdfem_fa_setup): CSR with sorted columns + deterministic contribution lists
+    bool fa_ready = false;
+    int64_t nnz = 0;
+    int fa_lpr = 8;                     // lanes per CSR row in the SpMV
+    int32_t *d_rowptr = nullptr, *d_cols = nullptr, *d_diagpos = nullptr;
+    int32_t *d_coff = nullptr, *d_cpos = nullptr;  // per-nonzero contribution lists into d_Ee
+    double *d_vals = nullptr;           // A
+    double *d_vals_c = nullptr;         // eliminated A (FormLinearSystem, DIAG_ONE)
+    double *d_Ee = nullptr;             // element matrices [blk][nd*nd][64]
 
     // partial assembly
     unsigned kinds = 0;
@@ -214,6 +236,20 @@ hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double
 hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q);
 
 // ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
+// full assembly on simplices (fa_kernels.hip)
+constexpr int kSpmvMaxBlocks = 8192;
+struct FaPattern {
+    int64_t nnz = 0;
+    std::vector<int32_t> rowptr, cols, diagpos, coff, cpos;
+};
+FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl);
+hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, double kappa, double alpha, const double *conv,
+                               const double *cq, const double *mq, double mass);
+hipError_t launch_fa_assemble(cdfem_ctx *c);
+hipError_t launch_csr_diag(cdfem_ctx *c, double *d);
+hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y);
+hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q);
+
 // GMRES(m) (gmres.hip)
 int gmres_blocks(int64_t n);
 hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it);

@@ -1,0 +1,365 @@
+// fa_kernels.hip — full assembly (FA) on simplex meshes: element matrices, deterministic CSR
+// assembly and the CSR SpMV that the Krylov solvers run on (BASELINE config C4: unstructured
+// tetrahedra, FA CSR SpMV + GMRES(30)/Jacobi — the reference's own solver path,
+// linear_convection_diffusion_2D.cpp:339 (Assemble, FA), :349-351 (FormLinearSystem ->
+// HypreParMatrix), :364-375 (PETSc MATAIJ + KSPGMRES)).
+//
+// Pipeline (once per operator, cdfem_fa_setup):
+//   host    CSR pattern (sorted columns per row) + for every nonzero the list of element-matrix
+//           entries that sum into it, in ascending element order (built once per mesh);
+//   k_simplex_elem   one thread per element: affine Jacobian, rule loop, nd x nd element matrix
+//                    written element-block-major [blk][i*nd+j][lane] (coalesced stores);
+//   k_fa_gather      one thread per nonzero: fixed-order sum of its contributions (bitwise
+//                    reproducible, no atomics);
+//   k_fa_eliminate   the FormLinearSystem matrix: ess rows/cols zeroed, unit diagonal (DIAG_ONE).
+// Hot loop: k_spmv<LPR> — LPR lanes per row (8 for P2 tets, ~27 nnz/row), column/value loads
+// coalesced within a row group, x gathered (lexicographic numbering keeps it L2-local).
+// Algorithmic bytes per SpMV = 12 nnz + 4 (n + 1) + 16 n.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <thread>
+#include <vector>
+
+#include "cdfem_internal.hpp"
+#include "reduce.hpp"
+
+namespace cdfem {
+
+// ---- host: CSR pattern and contribution lists --------------------------------------------------
+template <class F>
+static void parallel_rows(int64_t n, F &&f)
+{
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int64_t chunk = (n + hw - 1) / hw;
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < hw; ++t) {
+        const int64_t lo = t * chunk, hi = std::min(n, lo + chunk);
+        if (lo >= hi) break;
+        th.emplace_back([&, lo, hi] { f(lo, hi); });
+    }
+    for (auto &x : th) x.join();
+}
+
+static inline int64_t ee_index(int e, int i, int j, int nd)
+{
+    return ((int64_t)(e / kLanes) * nd * nd + (int64_t)i * nd + j) * kLanes + e % kLanes;
+}
+
+FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int64_t nl)
+{
+    // dof -> incidences (e * nd + l), ascending
+    std::vector<int64_t> cnt(nl + 1, 0);
+    for (int64_t k = 0; k < (int64_t)ne * nd; ++k) cnt[dof[k] + 1]++;
+    for (int64_t i = 0; i < nl; ++i) cnt[i + 1] += cnt[i];
+    std::vector<int64_t> inc((size_t)ne * nd);
+    {
+        std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
+        for (int64_t k = 0; k < (int64_t)ne * nd; ++k) inc[fill[dof[k]]++] = k;
+    }
+    if ((int64_t)ne * nd * nd >= ((int64_t)1 << 31)) throw std::runtime_error("FA contributions exceed int32");
+    auto row_cols = [&](int64_t i, std::vector<int32_t> &buf) {
+        buf.clear();
+        for (int64_t k = cnt[i]; k < cnt[i + 1]; ++k) {
+            const int64_t e = inc[k] / nd;
+            for (int l = 0; l < nd; ++l) buf.push_back(dof[e * nd + l]);
+        }
+        std::sort(buf.begin(), buf.end());
+        buf.erase(std::unique(buf.begin(), buf.end()), buf.end());
+    };
+    // pass 1: row lengths
+    std::vector<int32_t> rowptr(nl + 1, 0);
+    parallel_rows(nl, [&](int64_t lo, int64_t hi) {
+        std::vector<int32_t> buf;
+        for (int64_t i = lo; i < hi; ++i) {
+            row_cols(i, buf);
+            rowptr[i + 1] = (int32_t)buf.size();
+        }
+    });
+    int64_t nnz = 0;
+    for (int64_t i = 0; i < nl; ++i) {
+        nnz += rowptr[i + 1];
+        if (nnz >= ((int64_t)1 << 31)) throw std::runtime_error("nnz exceeds int32 indexing");
+        rowptr[i + 1] = (int32_t)nnz;
+    }
+    // pass 2: columns, diagonal positions, contribution lists.  Row i owns the contribution
+    // slots [nd * cnt[i], nd * cnt[i+1]) (every incidence of dof i contributes nd entries).
+    FaPattern P;
+    P.nnz = nnz;
+    std::vector<int32_t> &cols = P.cols, &diagpos = P.diagpos, &coff = P.coff, &cpos = P.cpos;
+    cols.resize(nnz);
+    diagpos.resize(nl);
+    coff.resize(nnz + 1);
+    cpos.resize((size_t)ne * nd * nd);
+    coff[nnz] = (int32_t)((int64_t)ne * nd * nd);
+    parallel_rows(nl, [&](int64_t lo, int64_t hi) {
+        std::vector<int32_t> buf, hits, slot;
+        for (int64_t i = lo; i < hi; ++i) {
+            row_cols(i, buf);
+            const int32_t base = rowptr[i];
+            const int len = (int)buf.size();
+            std::copy(buf.begin(), buf.end(), cols.begin() + base);
+            diagpos[i] = base + (int32_t)(std::lower_bound(buf.begin(), buf.end(), (int32_t)i) - buf.begin());
+            hits.assign(len, 0);
+            slot.clear();
+            for (int64_t k = cnt[i]; k < cnt[i + 1]; ++k) {  // ascending element
+                const int64_t e = inc[k] / nd;
+                for (int l = 0; l < nd; ++l) {
+                    const int t = (int)(std::lower_bound(buf.begin(), buf.end(), dof[e * nd + l]) - buf.begin());
+                    hits[t]++;
+                    slot.push_back(t);
+                }
+            }
+            int64_t run = (int64_t)nd * cnt[i];
+            for (int t = 0; t < len; ++t) {
+                coff[base + t] = (int32_t)run;
+                run += hits[t];
+            }
+            std::fill(hits.begin(), hits.end(), 0);
+            size_t s = 0;
+            for (int64_t k = cnt[i]; k < cnt[i + 1]; ++k) {
+                const int64_t e = inc[k] / nd;
+                const int li = (int)(inc[k] % nd);
+                for (int l = 0; l < nd; ++l, ++s) {
+                    const int t = slot[s];
+                    cpos[(size_t)coff[base + t] + hits[t]++] = (int32_t)ee_index((int)e, li, l, nd);
+                }
+            }
+        }
+    });
+    P.rowptr = std::move(rowptr);
+    return P;
+}
+
+
+// ---- element matrices on affine simplices ----------------------------------------------------------
+template <int DIM, int P>
+__global__ void __launch_bounds__(64)
+k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *__restrict__ stab, unsigned kinds,
+               double kappa, const double *__restrict__ kq, double alpha, double c0, double c1, double c2,
+               const double *__restrict__ cq, double mass, const double *__restrict__ mq, double *__restrict__ Ee)
+{
+    constexpr int ND = P == 1 ? DIM + 1 : (DIM + 1) * (DIM + 2) / 2;
+    const int e = blockIdx.x * 64 + threadIdx.x;
+    if (e >= ne) return;
+    const double *V = verts + (size_t)e * (DIM + 1) * DIM;
+    double J[DIM][DIM], A[DIM][DIM];
+#pragma unroll
+    for (int k = 0; k < DIM; ++k)
+#pragma unroll
+        for (int m = 0; m < DIM; ++m) J[k][m] = V[(m + 1) * DIM + k] - V[k];
+    double det;
+    if constexpr (DIM == 3) {
+        A[0][0] = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+        A[0][1] = J[0][2] * J[2][1] - J[0][1] * J[2][2];
+        A[0][2] = J[0][1] * J[1][2] - J[0][2] * J[1][1];
+        A[1][0] = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+        A[1][1] = J[0][0] * J[2][2] - J[0][2] * J[2][0];
+        A[1][2] = J[0][2] * J[1][0] - J[0][0] * J[1][2];
+        A[2][0] = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+        A[2][1] = J[0][1] * J[2][0] - J[0][0] * J[2][1];
+        A[2][2] = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+        det = J[0][0] * A[0][0] + J[0][1] * A[1][0] + J[0][2] * A[2][0];
+    } else {
+        A[0][0] = J[1][1];
+        A[0][1] = -J[0][1];
+        A[1][0] = -J[1][0];
+        A[1][1] = J[0][0];
+        det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+    }
+    double M[ND][ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i)
+#pragma unroll
+        for (int j = 0; j < ND; ++j) M[i][j] = 0.0;
+    const double *phi_t = stab, *dphi_t = stab + (size_t)nq * ND, *w_t = stab + (size_t)nq * ND * (DIM + 1);
+    const double cc[3] = {c0, c1, c2};
+    for (int q = 0; q < nq; ++q) {
+        const double W = w_t[q];
+        double D[DIM][DIM] = {}, Cv[DIM] = {}, Ms = 0.0;
+        if (kinds & CDFEM_DIFFUSION) {
+            const double f = W * (kq ? kq[(size_t)e * nq + q] : kappa) / det;
+#pragma unroll
+            for (int a = 0; a < DIM; ++a)
+#pragma unroll
+                for (int b = 0; b < DIM; ++b) {
+                    double s = 0.0;
+#pragma unroll
+                    for (int k = 0; k < DIM; ++k) s += A[a][k] * A[b][k];
+                    D[a][b] = f * s;
+                }
+        }
+        if (kinds & CDFEM_CONVECTION) {
+#pragma unroll
+            for (int a = 0; a < DIM; ++a) {
+                double s = 0.0;
+#pragma unroll
+                for (int k = 0; k < DIM; ++k)
+                    s += A[a][k] * (cq ? cq[((size_t)e * nq + q) * DIM + k] : cc[k]);
+                Cv[a] = W * alpha * s;
+            }
+        }
+        if (kinds & CDFEM_MASS) Ms = W * (mq ? mq[(size_t)e * nq + q] : mass) * det;
+        double ph[ND], dph[ND][DIM];
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+            ph[i] = phi_t[q * ND + i];
+#pragma unroll
+            for (int k = 0; k < DIM; ++k) dph[i][k] = dphi_t[(q * ND + i) * DIM + k];
+        }
+#pragma unroll
+        for (int j = 0; j < ND; ++j) {
+            double Dg[DIM], rest = Ms * ph[j];
+#pragma unroll
+            for (int a = 0; a < DIM; ++a) {
+                Dg[a] = 0.0;
+#pragma unroll
+                for (int b = 0; b < DIM; ++b) Dg[a] += D[a][b] * dph[j][b];
+                rest += Cv[a] * dph[j][a];
+            }
+#pragma unroll
+            for (int i = 0; i < ND; ++i) {
+                double v = ph[i] * rest;
+#pragma unroll
+                for (int a = 0; a < DIM; ++a) v += dph[i][a] * Dg[a];
+                M[i][j] += v;
+            }
+        }
+    }
+    const int64_t base = (int64_t)(e / kLanes) * ND * ND * kLanes + e % kLanes;
+#pragma unroll
+    for (int i = 0; i < ND; ++i)
+#pragma unroll
+        for (int j = 0; j < ND; ++j) Ee[base + (int64_t)(i * ND + j) * kLanes] = M[i][j];
+}
+
+__global__ void __launch_bounds__(256)
+k_fa_gather(const int32_t *__restrict__ coff, const int32_t *__restrict__ cpos, const double *__restrict__ Ee,
+            double *__restrict__ vals, int64_t nnz)
+{
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nnz) return;
+    double v = 0.0;
+    for (int32_t t = coff[k]; t < coff[k + 1]; ++t) v += Ee[cpos[t]];
+    vals[k] = v;
+}
+
+// FormLinearSystem matrix (MFEM EliminateRowsCols, DIAG_ONE): ess rows and columns zeroed, 1 on
+// the diagonal of ess rows
+__global__ void __launch_bounds__(256)
+k_fa_eliminate(const int32_t *__restrict__ rowptr, const int32_t *__restrict__ cols, const double *__restrict__ vals,
+               const uint8_t *__restrict__ ess, double *__restrict__ vals_c, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool ei = ess[i] != 0;
+    for (int32_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        const int32_t j = cols[k];
+        vals_c[k] = (ei || ess[j]) ? (j == i ? 1.0 : 0.0) : vals[k];
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_csr_diag(const double *__restrict__ vals, const int32_t *__restrict__ diagpos, double *__restrict__ d, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) d[i] = vals[diagpos[i]];
+}
+
+// y = A x, LPR lanes per row (grid-stride over row groups).  CG mode also accumulates the
+// partials of (x, y) (den = (d, A d)) and exits at entry once the Krylov state is done.
+template <int LPR, bool CG>
+__global__ void __launch_bounds__(256)
+k_spmv(const int32_t *__restrict__ rowptr, const int32_t *__restrict__ cols, const double *__restrict__ vals,
+       const double *__restrict__ x, double *__restrict__ y, int64_t n, double *__restrict__ part,
+       const KrylovState *__restrict__ st)
+{
+    __shared__ double sh[256 / 64];
+    if (CG && st->done) return;
+    const int sub = threadIdx.x % LPR;
+    const int64_t groups = (int64_t)gridDim.x * (256 / LPR);
+    double dd = 0.0;
+    for (int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR; row < n; row += groups) {
+        double acc = 0.0;
+        const int32_t k1 = rowptr[row + 1];
+        for (int32_t k = rowptr[row] + sub; k < k1; k += LPR) acc += vals[k] * x[cols[k]];
+#pragma unroll
+        for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, LPR);
+        if (sub == 0) {
+            y[row] = acc;
+            if (CG) dd += acc * x[row];
+        }
+    }
+    if (CG) store_partial(block_sum(dd, sh), part);
+}
+
+// ---- launchers ---------------------------------------------------------------------------------
+hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, double kappa, double alpha, const double *conv,
+                               const double *cq, const double *mq, double mass)
+{
+    const dim3 g((c->ne + 63) / 64), b(64);
+    const double c0 = conv ? conv[0] : 0.0, c1 = conv ? conv[1] : 0.0, c2 = (conv && c->dim == 3) ? conv[2] : 0.0;
+#define CDFEM_SIMPLEX(D, P)                                                                              \
+    hipLaunchKernelGGL((k_simplex_elem<D, P>), g, b, 0, c->stream, c->d_verts, c->ne, c->nq_simplex,     \
+                       c->d_stab, c->kinds, kappa, kq, alpha, c0, c1, c2, cq, mass, mq, c->d_Ee)
+    if (c->dim == 3 && c->p == 1) CDFEM_SIMPLEX(3, 1);
+    else if (c->dim == 3 && c->p == 2) CDFEM_SIMPLEX(3, 2);
+    else if (c->dim == 2 && c->p == 1) CDFEM_SIMPLEX(2, 1);
+    else if (c->dim == 2 && c->p == 2) CDFEM_SIMPLEX(2, 2);
+    else return hipErrorInvalidValue;
+#undef CDFEM_SIMPLEX
+    return hipGetLastError();
+}
+
+hipError_t launch_fa_assemble(cdfem_ctx *c)
+{
+    hipLaunchKernelGGL(k_fa_gather, dim3((unsigned)((c->nnz + 255) / 256)), dim3(256), 0, c->stream, c->d_coff,
+                       c->d_cpos, c->d_Ee, c->d_vals, c->nnz);
+    hipLaunchKernelGGL(k_fa_eliminate, dim3((unsigned)((c->nl + 255) / 256)), dim3(256), 0, c->stream,
+                       c->d_rowptr, c->d_cols, c->d_vals, c->d_ess, c->d_vals_c, (int64_t)c->nl);
+    return hipGetLastError();
+}
+
+hipError_t launch_csr_diag(cdfem_ctx *c, double *d)
+{
+    hipLaunchKernelGGL(k_csr_diag, dim3((unsigned)((c->nl + 255) / 256)), dim3(256), 0, c->stream, c->d_vals,
+                       c->d_diagpos, d, (int64_t)c->nl);
+    return hipGetLastError();
+}
+
+static unsigned spmv_grid(cdfem_ctx *c)
+{
+    const int64_t need = (c->nl * c->fa_lpr + 255) / 256;
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, kSpmvMaxBlocks));
+}
+
+hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y)
+{
+    const double *v = constrained ? c->d_vals_c : c->d_vals;
+    const dim3 g(spmv_grid(c)), b(256);
+    if (c->fa_lpr == 8)
+        hipLaunchKernelGGL((k_spmv<8, false>), g, b, 0, c->stream, c->d_rowptr, c->d_cols, v, x, y, (int64_t)c->nl,
+                           nullptr, nullptr);
+    else
+        hipLaunchKernelGGL((k_spmv<4, false>), g, b, 0, c->stream, c->d_rowptr, c->d_cols, v, x, y, (int64_t)c->nl,
+                           nullptr, nullptr);
+    return hipGetLastError();
+}
+
+// q = A_c d and the den partials, then the MFEM CG den step (one-block finalizer)
+hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q)
+{
+    const dim3 g(spmv_grid(c)), b(256);
+    if (c->fa_lpr == 8)
+        hipLaunchKernelGGL((k_spmv<8, true>), g, b, 0, c->stream, c->d_rowptr, c->d_cols, c->d_vals_c, d, q,
+                           (int64_t)c->nl, c->d_part, c->d_state);
+    else
+        hipLaunchKernelGGL((k_spmv<4, true>), g, b, 0, c->stream, c->d_rowptr, c->d_cols, c->d_vals_c, d, q,
+                           (int64_t)c->nl, c->d_part, c->d_state);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_den_fin(c, (int)g.x);
+}
+
+}  // namespace cdfem

@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <utility>
 
 #include "cdfem_internal.hpp"
 
@@ -160,6 +161,104 @@ int cdfem_box_mesh(int dim, int nx, int ny, int nz, int order, int z0, int z1, d
         }
     }
     return CDFEM_OK;
+}
+
+// ---- Kuhn simplex meshes (BASELINE config C4: "unstructured tet mesh ~1M elements") ----------
+// [0,1]^dim cut into n^dim cubes, each split into dim! simplices along the axis permutations
+// (v_{k+1} = v_k + e_pi(k)); odd permutations swap the last two vertices so det J > 0.  Element
+// order: cube-major, permutations lexicographic.  H1 P1/P2 dofs = the (p n + 1)^dim lattice
+// (a P2 edge midpoint is the unique odd lattice point of its edge), lexicographic.  The solver
+// path treats the result as an unstructured mesh (explicit element -> dof map, CSR).
+int cdfem_kuhn_sizes(int dim, int n, int order, int *ne, int64_t *nldofs, int *n_ess)
+{
+    if ((dim != 2 && dim != 3) || n < 1 || order < 1 || order > 2) return CDFEM_ERR_ARG;
+    const int64_t L = (int64_t)order * n + 1;
+    const int64_t nl = dim == 3 ? L * L * L : L * L;
+    const int64_t inner = dim == 3 ? (L - 2) * (L - 2) * (L - 2) : (L - 2) * (L - 2);
+    if (ne) *ne = dim == 3 ? 6 * n * n * n : 2 * n * n;
+    if (nldofs) *nldofs = nl;
+    if (n_ess) *n_ess = (int)(nl - inner);
+    return CDFEM_OK;
+}
+
+int cdfem_kuhn_mesh(int dim, int n, int order, double perturb, double *elem_verts, int32_t *elem_dofs,
+                    int32_t *ess_dofs, double *dof_xyz)
+{
+    static const int perm3[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
+    static const int odd3[6] = {0, 1, 1, 0, 0, 1};
+    static const int perm2[2][2] = {{0, 1}, {1, 0}};
+    int ne;
+    int64_t nl;
+    if (cdfem_kuhn_sizes(dim, n, order, &ne, &nl, nullptr) != CDFEM_OK) return CDFEM_ERR_ARG;
+    const int p = order, nsub = dim == 3 ? 6 : 2, nv = dim + 1, nd = cdfem::simplex_ndofs(dim, p);
+    const int64_t L = (int64_t)p * n + 1;
+    const int ncube = dim == 3 ? n * n * n : n * n;
+    const double h = 1.0 / n;
+    bool inverted = false;
+    for (int ci = 0; ci < ncube; ++ci) {
+        const int c[3] = {ci % n, (ci / n) % n, dim == 3 ? ci / (n * n) : 0};
+        for (int s = 0; s < nsub; ++s) {
+            const int e = ci * nsub + s;
+            int V[4][3] = {};
+            for (int k = 0; k < 3; ++k) V[0][k] = c[k];
+            for (int k = 0; k < dim; ++k) {
+                const int ax = dim == 3 ? perm3[s][k] : perm2[s][k];
+                for (int m = 0; m < 3; ++m) V[k + 1][m] = V[k][m] + (m == ax ? 1 : 0);
+            }
+            if (dim == 3 ? odd3[s] : s == 1)
+                for (int m = 0; m < 3; ++m) std::swap(V[dim][m], V[dim - 1][m]);
+            double X[4][3] = {};
+            for (int v = 0; v < nv; ++v) {
+                bool interior = true;
+                for (int k = 0; k < dim; ++k) {
+                    X[v][k] = V[v][k] * h;
+                    interior = interior && V[v][k] > 0 && V[v][k] < n;
+                }
+                if (perturb > 0.0 && interior) {
+                    const uint64_t id = (uint64_t)V[v][0] + (uint64_t)(n + 1) * ((uint64_t)V[v][1] + (uint64_t)(n + 1) * V[v][2]);
+                    for (int k = 0; k < dim; ++k) X[v][k] += perturb * h * jitter(3 * id + k);
+                }
+                if (elem_verts)
+                    for (int k = 0; k < dim; ++k) elem_verts[((size_t)e * nv + v) * dim + k] = X[v][k];
+            }
+            double J[3][3] = {};
+            for (int k = 0; k < dim; ++k)
+                for (int m = 0; m < dim; ++m) J[k][m] = X[m + 1][k] - X[0][k];
+            const double det = dim == 3 ? J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) -
+                                              J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                                              J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0])
+                                        : J[0][0] * J[1][1] - J[0][1] * J[1][0];
+            if (!(det > 0.0)) inverted = true;
+            for (int l = 0; l < nd; ++l) {
+                int G[3] = {0, 0, 0};
+                double Xl[3] = {0, 0, 0};
+                if (l < nv) {
+                    for (int m = 0; m < 3; ++m) G[m] = p * V[l][m];
+                    for (int k = 0; k < dim; ++k) Xl[k] = X[l][k];
+                } else {
+                    const int ed = l - nv;
+                    const int a = dim == 3 ? cdfem::kSimplexEdge[ed][0] : cdfem::kTriEdge[ed][0];
+                    const int b = dim == 3 ? cdfem::kSimplexEdge[ed][1] : cdfem::kTriEdge[ed][1];
+                    for (int m = 0; m < 3; ++m) G[m] = V[a][m] + V[b][m];
+                    for (int k = 0; k < dim; ++k) Xl[k] = 0.5 * (X[a][k] + X[b][k]);
+                }
+                const int64_t gid = G[0] + L * (G[1] + L * G[2]);
+                if (elem_dofs) elem_dofs[(size_t)e * nd + l] = (int32_t)gid;
+                if (dof_xyz)
+                    for (int k = 0; k < dim; ++k) dof_xyz[gid * dim + k] = Xl[k];
+            }
+        }
+    }
+    if (ess_dofs) {
+        int64_t m = 0;
+        for (int64_t i = 0; i < nl; ++i) {
+            const int64_t gx = i % L, gy = (i / L) % L, gz = i / (L * L);
+            bool on = gx == 0 || gx == L - 1 || gy == 0 || gy == L - 1;
+            if (dim == 3) on = on || gz == 0 || gz == L - 1;
+            if (on) ess_dofs[m++] = (int32_t)i;
+        }
+    }
+    return inverted ? CDFEM_ERR_ARG : CDFEM_OK;
 }
 
 }  // extern "C"

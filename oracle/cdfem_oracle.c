@@ -362,32 +362,19 @@ static void element_matrix(int dim, int p, const double *V, const orc_coef *cf, 
     }
 }
 
-/* Build the CSR matrix sum_e A_e (ParBilinearForm::Assemble + Finalize, SpMat form). */
-ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, const int *dofmap,
-                                 int64_t nl, double kappa, double alpha, double s, const double *c,
-                                 int kinds)
+/* CSR of sum_e A_e from element matrices Ae[e][i][j] (row = test dof, col = trial dof) and the
+ * element dof map (ParBilinearForm::Assemble + Finalize, SpMat form).  Columns sorted per row;
+ * each entry accumulates its contributions in ascending (element, local row, local col) order. */
+static orc_csr *csr_from_elements(int nd, int ne, const int *dofmap, int64_t nl, const double *Ae)
 {
-    const int d1 = p + 1;
-    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
-    const int nv = (dim == 3) ? 8 : 4;
-    orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
-                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0};
-    /* one shared rule: Diffusion/Convection/Mass coincide on Q1 tensor elements (checked) */
-    int nq = orc_rule_npts(0, dim, p);
-    if (orc_rule_npts(1, dim, p) != nq || orc_rule_npts(2, dim, p) != nq) return NULL;
-    double B[64], G[64], pts[8], wts[8];
-    tables(p, nq, B, G, pts, wts);
-
-    double *Ae = (double *)malloc(sizeof(double) * (size_t)ne * nd * nd);
-    #pragma omp parallel for schedule(static)
-    for (int e = 0; e < ne; e++)
-        element_matrix(dim, p, verts + (size_t)e * nv * dim, &cf, nq, B, G, pts, wts,
-                       Ae + (size_t)e * nd * nd);
-
     /* dof -> (element, local) transpose, element order ascending (deterministic accumulation) */
     int64_t *cnt = (int64_t *)calloc(nl + 1, sizeof(int64_t));
     for (int64_t k = 0; k < (int64_t)ne * nd; k++) cnt[dofmap[k] + 1]++;
-    for (int64_t i = 0; i < nl; i++) cnt[i + 1] += cnt[i];
+    int64_t maxcnt = 0;
+    for (int64_t i = 0; i < nl; i++) {
+        if (cnt[i + 1] > maxcnt) maxcnt = cnt[i + 1];
+        cnt[i + 1] += cnt[i];
+    }
     int64_t *fill = (int64_t *)malloc(sizeof(int64_t) * nl);
     memcpy(fill, cnt, sizeof(int64_t) * nl);
     int64_t *el = (int64_t *)malloc(sizeof(int64_t) * (size_t)ne * nd);
@@ -397,11 +384,11 @@ ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, co
     orc_csr *A = (orc_csr *)calloc(1, sizeof(orc_csr));
     A->n = nl;
     A->rp = (int64_t *)calloc(nl + 1, sizeof(int64_t));
-    const int maxc = (1 << dim) * nd;
+    const int64_t maxc = maxcnt * nd;
     /* pass 1: row lengths */
     #pragma omp parallel
     {
-        int *buf = (int *)malloc(sizeof(int) * maxc * 2);
+        int *buf = (int *)malloc(sizeof(int) * (maxc + 1));
         #pragma omp for schedule(dynamic, 256)
         for (int64_t i = 0; i < nl; i++) {
             int m = 0;
@@ -409,8 +396,7 @@ ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, co
                 int64_t e = el[k] / nd;
                 for (int l = 0; l < nd; l++) buf[m++] = dofmap[e * nd + l];
             }
-            /* insertion sort + unique (m <= 8*125) */
-            for (int a = 1; a < m; a++) {
+            for (int a = 1; a < m; a++) {  /* insertion sort + unique */
                 int v = buf[a], b = a - 1;
                 while (b >= 0 && buf[b] > v) { buf[b + 1] = buf[b]; b--; }
                 buf[b + 1] = v;
@@ -428,7 +414,7 @@ ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, co
     /* pass 2: columns and values */
     #pragma omp parallel
     {
-        int *buf = (int *)malloc(sizeof(int) * maxc * 2);
+        int *buf = (int *)malloc(sizeof(int) * (maxc + 1));
         #pragma omp for schedule(dynamic, 256)
         for (int64_t i = 0; i < nl; i++) {
             int m = 0;
@@ -460,7 +446,33 @@ ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, co
         }
         free(buf);
     }
-    free(cnt); free(el); free(Ae);
+    free(cnt); free(el);
+    return A;
+}
+
+/* Build the CSR matrix sum_e A_e for tensor (quad/hex) elements. */
+ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, const int *dofmap,
+                                 int64_t nl, double kappa, double alpha, double s, const double *c,
+                                 int kinds)
+{
+    const int d1 = p + 1;
+    const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
+    const int nv = (dim == 3) ? 8 : 4;
+    orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
+                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0};
+    /* one shared rule: Diffusion/Convection/Mass coincide on Q1 tensor elements (checked) */
+    int nq = orc_rule_npts(0, dim, p);
+    if (orc_rule_npts(1, dim, p) != nq || orc_rule_npts(2, dim, p) != nq) return NULL;
+    double B[64], G[64], pts[8], wts[8];
+    tables(p, nq, B, G, pts, wts);
+
+    double *Ae = (double *)malloc(sizeof(double) * (size_t)ne * nd * nd);
+    #pragma omp parallel for schedule(static)
+    for (int e = 0; e < ne; e++)
+        element_matrix(dim, p, verts + (size_t)e * nv * dim, &cf, nq, B, G, pts, wts,
+                       Ae + (size_t)e * nd * nd);
+    orc_csr *A = csr_from_elements(nd, ne, dofmap, nl, Ae);
+    free(Ae);
     return A;
 }
 
@@ -912,4 +924,233 @@ ORC_API void orc_set_num_threads(int n)
 #else
     (void)n;
 #endif
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Simplex elements: BASELINE config C4 (unstructured tetrahedra, FA CSR + GMRES(30)/Jacobi,     */
+/* the reference's own solver path: linear_convection_diffusion_2D.cpp:339,364-375,              */
+/* Input/petsc.opts:2-6).  H1 P1/P2 Lagrange (MFEM H1_FECollection on simplices: nodal, vertices  */
+/* then edge midpoints), affine geometry.                                                       */
+/* ------------------------------------------------------------------------------------------ */
+
+ORC_API int orc_simplex_nd(int dim, int p)
+{
+    if (p == 1) return dim + 1;
+    if (p == 2) return (dim + 1) * (dim + 2) / 2;
+    return -1;
+}
+
+/* Collapsed (Duffy) tensor Gauss-Legendre rule on the reference simplex (vertices 0, e_1 .. e_d),
+ * n points per direction, exact for polynomial degree 2n - dim:
+ *   xi_1 = u, xi_2 = (1-u) v [, xi_3 = (1-u)(1-v) w],  W = w_u w_v [w_w] (1-u)^(d-1) [(1-v)].
+ * Point q = (iu * n + iv) [* n + iw]. Parity is unpinned vs MFEM's simplex rules:
+ * for constant coefficients on affine elements any rule exact to degree 2p gives the same
+ * matrix, and this one is exact to degree 2p + 1 with n = p + 2 in 3D. */
+ORC_API int orc_simplex_rule(int dim, int n, double *xi, double *w)
+{
+    double x[16], wx[16];
+    if (n < 1 || n > 16) return -1;
+    orc_gauss_legendre(n, x, wx);
+    const int nq = (dim == 3) ? n * n * n : n * n;
+    for (int q = 0; q < nq; q++) {
+        int iu, iv, iw = 0;
+        if (dim == 3) { iu = q / (n * n); iv = (q / n) % n; iw = q % n; }
+        else { iu = q / n; iv = q % n; }
+        const double u = x[iu], v = x[iv];
+        if (dim == 3) {
+            const double t = x[iw];
+            xi[q * 3 + 0] = u;
+            xi[q * 3 + 1] = (1.0 - u) * v;
+            xi[q * 3 + 2] = (1.0 - u) * (1.0 - v) * t;
+            w[q] = wx[iu] * wx[iv] * wx[iw] * (1.0 - u) * (1.0 - u) * (1.0 - v);
+        } else {
+            xi[q * 2 + 0] = u;
+            xi[q * 2 + 1] = (1.0 - u) * v;
+            w[q] = wx[iu] * wx[iv] * (1.0 - u);
+        }
+    }
+    return nq;
+}
+
+/* Reference basis at xi: phi[nd], dphi[nd][dim] (d/dxi_k), barycentric lambda_0 = 1 - sum xi.
+ * Local order: vertices 0..dim, then (P2) edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3) [2D: (0,1),
+ * (0,2),(1,2)]. */
+static const int kEdge3[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
+static const int kEdge2[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+
+static void simplex_basis(int dim, int p, const double *xi, double *phi, double *dphi)
+{
+    double lam[4], dlam[4][3];  /* d lambda_a / d xi_k */
+    lam[0] = 1.0;
+    for (int k = 0; k < dim; k++) lam[0] -= xi[k];
+    for (int k = 0; k < dim; k++) dlam[0][k] = -1.0;
+    for (int a = 1; a <= dim; a++) {
+        lam[a] = xi[a - 1];
+        for (int k = 0; k < dim; k++) dlam[a][k] = (k == a - 1) ? 1.0 : 0.0;
+    }
+    if (p == 1) {
+        for (int a = 0; a <= dim; a++) {
+            phi[a] = lam[a];
+            for (int k = 0; k < dim; k++) dphi[a * dim + k] = dlam[a][k];
+        }
+        return;
+    }
+    for (int a = 0; a <= dim; a++) {
+        phi[a] = lam[a] * (2.0 * lam[a] - 1.0);
+        for (int k = 0; k < dim; k++) dphi[a * dim + k] = (4.0 * lam[a] - 1.0) * dlam[a][k];
+    }
+    const int ne = dim == 3 ? 6 : 3;
+    for (int e = 0; e < ne; e++) {
+        const int a = dim == 3 ? kEdge3[e][0] : kEdge2[e][0], b = dim == 3 ? kEdge3[e][1] : kEdge2[e][1];
+        const int l = dim + 1 + e;
+        phi[l] = 4.0 * lam[a] * lam[b];
+        for (int k = 0; k < dim; k++) dphi[l * dim + k] = 4.0 * (lam[a] * dlam[b][k] + lam[b] * dlam[a][k]);
+    }
+}
+
+/* Kuhn (Freudenthal) subdivision of the n^dim cube grid of [0,1]^dim: every cube (square) splits
+ * into dim! simplices v0 = corner, v_{k+1} = v_k + e_{pi(k)} for each axis permutation pi;
+ * odd permutations swap the last two vertices so every element has det J > 0.  Element order:
+ * cube-major (lexicographic), then permutation in lexicographic order.  Dofs: the lattice
+ * (p n + 1)^dim numbered lexicographically (P2 edge midpoints are the odd lattice points, each on
+ * exactly one Kuhn edge).  perturb moves interior vertices as orc_mesh_box does.
+ * Returns 0, or -1 if a perturbed element is inverted. */
+static const int kPerm3[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
+static const int kPerm3Odd[6] = {0, 1, 1, 0, 0, 1};
+static const int kPerm2[2][2] = {{0, 1}, {1, 0}};
+
+ORC_API void orc_mesh_kuhn_sizes(int dim, int n, int p, int *ne, int64_t *nl)
+{
+    const int64_t L = (int64_t)p * n + 1;
+    *ne = (dim == 3) ? 6 * n * n * n : 2 * n * n;
+    *nl = (dim == 3) ? L * L * L : L * L;
+}
+
+ORC_API int orc_mesh_kuhn(int dim, int n, int p, double perturb, double *verts, int *dofmap, int *bdr)
+{
+    const int nsub = dim == 3 ? 6 : 2, nv = dim + 1, nd = orc_simplex_nd(dim, p);
+    const int64_t L = (int64_t)p * n + 1;
+    const int ncube = dim == 3 ? n * n * n : n * n;
+    const double h = 1.0 / n;
+    int bad = 0;
+    for (int cidx = 0; cidx < ncube; cidx++) {
+        const int c[3] = {cidx % n, (cidx / n) % n, dim == 3 ? cidx / (n * n) : 0};
+        for (int s = 0; s < nsub; s++) {
+            const int e = cidx * nsub + s;
+            int V[4][3] = {{0}};
+            for (int k = 0; k < 3; k++) V[0][k] = c[k];
+            for (int k = 0; k < dim; k++) {
+                const int ax = dim == 3 ? kPerm3[s][k] : kPerm2[s][k];
+                for (int m = 0; m < 3; m++) V[k + 1][m] = V[k][m] + (m == ax);
+            }
+            const int odd = dim == 3 ? kPerm3Odd[s] : (s == 1);
+            if (odd)
+                for (int m = 0; m < 3; m++) { int t = V[dim][m]; V[dim][m] = V[dim - 1][m]; V[dim - 1][m] = t; }
+            double X[4][3] = {{0}};
+            for (int v = 0; v < nv; v++) {
+                int interior = 1;
+                for (int k = 0; k < dim; k++) {
+                    X[v][k] = V[v][k] * h;
+                    interior = interior && V[v][k] > 0 && V[v][k] < n;
+                }
+                if (perturb > 0.0 && interior) {
+                    uint64_t id = (uint64_t)V[v][0] + (uint64_t)(n + 1) * ((uint64_t)V[v][1] + (uint64_t)(n + 1) * V[v][2]);
+                    for (int k = 0; k < dim; k++) X[v][k] += perturb * h * hash_unit(3 * id + k);
+                }
+                for (int k = 0; k < dim; k++) verts[((size_t)e * nv + v) * dim + k] = X[v][k];
+            }
+            double J[3][3] = {{0}};
+            for (int k = 0; k < dim; k++)
+                for (int m = 0; m < dim; m++) J[k][m] = X[m + 1][k] - X[0][k];
+            double A[3][3];
+            if (adjugate(dim, J, A) <= 0.0) bad = 1;
+            for (int l = 0; l < nd; l++) {
+                int G[3] = {0, 0, 0};
+                if (l < nv) {
+                    for (int m = 0; m < 3; m++) G[m] = p * V[l][m];
+                } else {
+                    const int ed = l - nv;
+                    const int a = dim == 3 ? kEdge3[ed][0] : kEdge2[ed][0], b = dim == 3 ? kEdge3[ed][1] : kEdge2[ed][1];
+                    for (int m = 0; m < 3; m++) G[m] = V[a][m] + V[b][m];  /* p = 2: midpoint */
+                }
+                dofmap[(size_t)e * nd + l] = (int)(G[0] + L * (G[1] + L * G[2]));
+            }
+        }
+    }
+    const int64_t nl = dim == 3 ? L * L * L : L * L;
+    for (int64_t i = 0; i < nl; i++) {
+        const int64_t gx = i % L, gy = (i / L) % L, gz = i / (L * L);
+        int on = gx == 0 || gx == L - 1 || gy == 0 || gy == L - 1;
+        if (dim == 3) on = on || gz == 0 || gz == L - 1;
+        bdr[i] = on;
+    }
+    return bad ? -1 : 0;
+}
+
+/* Element matrix of an affine simplex (same integrand as element_matrix: D = W kappa adj adj^T /
+ * det J, C = W alpha adj c, M = W s det J on reference gradients). */
+static void simplex_element_matrix(int dim, int p, const double *V, const orc_coef *cf, int nq,
+                                   const double *xi, const double *wq, double *Ae)
+{
+    const int nd = orc_simplex_nd(dim, p);
+    double J[3][3] = {{0}}, A[3][3];
+    for (int k = 0; k < dim; k++)
+        for (int m = 0; m < dim; m++) J[k][m] = V[(m + 1) * dim + k] - V[k];
+    const double detJ = adjugate(dim, J, A);
+    memset(Ae, 0, sizeof(double) * nd * nd);
+    double phi[10], dphi[30];
+    for (int q = 0; q < nq; q++) {
+        const double W = wq[q];
+        double D[3][3] = {{0}}, Cv[3] = {0}, M = 0.0;
+        if (cf->use_diff)
+            for (int i = 0; i < dim; i++)
+                for (int j = 0; j < dim; j++) {
+                    double acc = 0.0;
+                    for (int k = 0; k < dim; k++) acc += A[i][k] * A[j][k];
+                    D[i][j] = W * cf->kappa * acc / detJ;
+                }
+        if (cf->use_conv)
+            for (int i = 0; i < dim; i++) {
+                double acc = 0.0;
+                for (int k = 0; k < dim; k++) acc += A[i][k] * cf->c[k];
+                Cv[i] = W * cf->alpha * acc;
+            }
+        if (cf->use_mass) M = W * cf->s * detJ;
+        simplex_basis(dim, p, xi + (size_t)q * dim, phi, dphi);
+        for (int j = 0; j < nd; j++) {
+            double Dg[3] = {0, 0, 0}, cg = 0.0;
+            for (int a = 0; a < dim; a++) {
+                for (int b = 0; b < dim; b++) Dg[a] += D[a][b] * dphi[j * dim + b];
+                cg += Cv[a] * dphi[j * dim + a];
+            }
+            const double rest = cg + M * phi[j];
+            for (int i = 0; i < nd; i++) {
+                double v = phi[i] * rest;
+                for (int a = 0; a < dim; a++) v += dphi[i * dim + a] * Dg[a];
+                Ae[i * nd + j] += v;
+            }
+        }
+    }
+}
+
+/* FA CSR of the convection-diffusion-reaction form on P1/P2 simplices (rule: n = p + 2). */
+ORC_API orc_csr *orc_fa_assemble_simplex(int dim, int p, int ne, const double *verts, const int *dofmap,
+                                         int64_t nl, double kappa, double alpha, double s, const double *c,
+                                         int kinds)
+{
+    const int nd = orc_simplex_nd(dim, p);
+    if (nd < 0 || (dim != 2 && dim != 3)) return NULL;
+    orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
+                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0};
+    const int n1 = p + 2;
+    double xi[16 * 16 * 16 * 3 / 16], wq[16 * 16 * 16 / 16];  /* n1 <= 4: 64 points */
+    const int nq = orc_simplex_rule(dim, n1, xi, wq);
+    double *Ae = (double *)malloc(sizeof(double) * (size_t)ne * nd * nd);
+    #pragma omp parallel for schedule(static)
+    for (int e = 0; e < ne; e++)
+        simplex_element_matrix(dim, p, verts + (size_t)e * (dim + 1) * dim, &cf, nq, xi, wq,
+                               Ae + (size_t)e * nd * nd);
+    orc_csr *A = csr_from_elements(nd, ne, dofmap, nl, Ae);
+    free(Ae);
+    return A;
 }
