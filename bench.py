@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--path", choices=["brick", "generic"], default="brick",
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
+    ap.add_argument("--config", choices=["c2", "c4"], default="c2",
+                    help="c2: 64^3 hex p=2 PA + CG (BASELINE metric config); c4: Kuhn 55^3 x 6 tets P2, "
+                         "FA CSR + GMRES(30)/Jacobi (BASELINE configs[3])")
+    ap.add_argument("--tet-n", type=int, default=55, help="c4: cubes per direction (6 tets each)")
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N>1 data-path communicator: rccl (production, one GPU per rank) or host "
                          "(gloo callbacks; rehearses the N>1 flow with several ranks on one GPU)")
@@ -116,8 +120,110 @@ def cpu_baseline(args, n, p, kinds):
                       f"{its} iterations timed ({dt:.2f} s); assembly+FormLinearSystem {t_asm:.1f} s untimed"}
 
 
+def cpu_baseline_c4(args, n, p):
+    """Oracle FA-CSR GMRES(30)/Jacobi on the same Kuhn mesh (bounded sample)."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    O.set_threads(threads)
+    m = O.KuhnMesh(3, n, p)
+    t0 = time.perf_counter()
+    A = O.fa_assemble_simplex(m, kappa=0.1, alpha=1.0, s=1.0, c=(1.0, -2.0, 0.5))
+    b = np.random.default_rng(20261015).uniform(-1, 1, m.nl)
+    Ac, B = O.form_linear_system(A, m.bdr, np.zeros(m.nl), b)
+    del A
+    dinv = 1.0 / Ac.diag()
+    t_asm = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=5)
+    per_it = (time.perf_counter() - t0) / 5
+    n_it = int(min(3000, max(10, args.cpu_seconds / per_it)))
+    t0 = time.perf_counter()
+    _, info = O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=n_it)
+    dt = time.perf_counter() - t0
+    its = info["iterations"]
+    return {"value": m.nl * its / dt, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
+            "sample": f"oracle FA-CSR GMRES(30)/Jacobi, Kuhn {n}^3x6 tets P{p} ({m.nl} DoFs, nnz={Ac.nnz}), "
+                      f"{its} iterations timed ({dt:.2f} s); assembly+FormLinearSystem {t_asm:.1f} s untimed"}
+
+
+def main_c4(args):
+    """BASELINE configs[3]: unstructured-path tets, FA CSR SpMV + GMRES(30)/Jacobi on 1 GPU."""
+    import cdfem
+    n, p = args.tet_n, 2
+    mesh = cdfem.kuhn_mesh(3, n, p, with_coords=False)
+    ctx = cdfem.Context(0)
+    ctx.upload_mesh(mesh)
+    t0 = time.perf_counter()
+    ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=(1.0, -2.0, 0.5), mass=1.0)
+    t_setup = time.perf_counter() - t0
+    b = np.random.default_rng(20261015).uniform(-1, 1, mesh.nl)
+    _, B = ctx.form_linear_system(np.zeros(mesh.nl), b)
+    dB, dX = ctx.to_device(B), ctx.alloc(8 * mesh.nl)
+    iters_per_step = args.gmres_iters or 60
+
+    def step():
+        return ctx.solve_device(dB, dX, method="gmres", pc="jacobi", rel_tol=0.0, abs_tol=0.0,
+                                max_iter=iters_per_step, restart=30)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    if not args.no_profile_events:
+        ctx.set_option("profile_mask", (1 << cdfem.K_APPLY) | (1 << cdfem.K_ORTH))
+        ctx.profile(True)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(args.steps):
+        iters += step()["iterations"]
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    roof = None
+    if not args.no_profile_events:
+        ms, cnt = ctx.profile_read(cdfem.K_APPLY)
+        o_ms, o_cnt = ctx.profile_read(cdfem.K_ORTH)
+        ctx.profile(False)
+        if cnt:
+            per = ms / cnt * 1e-3
+            bytes_ = ctx.kernel_bytes(cdfem.K_APPLY)
+            traffic = None
+            if os.path.exists(args.traffic_json):
+                try:
+                    traffic = json.load(open(args.traffic_json)).get(f"c4_n{n}_p{p}", {}).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roof = {"bound": "hbm", "achieved": round(bytes_ / per / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(bytes_ / per / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "k_spmv (CSR SpMV on the eliminated FA matrix)",
+                    "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2), "launches": cnt,
+                    "other_kernels_avg_us": {"gmres_orth": round(o_ms / max(o_cnt, 1) * 1e3, 2)}}
+    rp, _, _ = ctx.fa_csr()
+    nnz = int(rp[-1])
+    cpu = None
+    if not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline_c4(args, n, p)
+        except Exception as e:
+            cpu = {"error": repr(e)}
+    out = {"metric": "DoF-iter/s (CG, 3D p=2 hex convection-diffusion) + achieved HBM GB/s",
+           "value": mesh.nl * iters / dt, "unit": "DoF-iter/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": f"C4: Kuhn {n}^3x6 tets P2, FA CSR (GPU-assembled) + GMRES(30)/Jacobi "
+                                  f"{iters_per_step} it/step", "dofs": mesh.nl, "elements": mesh.ne, "nnz": nnz,
+                      "fa_setup_s": round(t_setup, 3), "parallelism": "single"},
+           "roofline": roof, "cpu_baseline": cpu}
+    print(json.dumps(out), flush=True)
+    ctx.free(dB)
+    ctx.free(dX)
+    ctx.close()
+
+
 def main():
     args = parse()
+    if args.config == "c4":
+        return main_c4(args)
     world, rank, local, pg = dist_setup(args)
     import cdfem
 

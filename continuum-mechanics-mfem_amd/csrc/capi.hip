@@ -93,6 +93,13 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_part); dfree(c->d_gm); dfree(c->d_gm_part);
     dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones); dfree(c->d_dalt);
     for (auto &b : c->d_if) dfree(b);
+    dfree(c->d_stab); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);
+    dfree(c->d_cpos); dfree(c->d_vals); dfree(c->d_vals_c); dfree(c->d_Ee);
+    c->geom = 0;
+    c->fa_ready = false;
+    c->nnz = 0;
+    c->h_verts.clear();
+    c->h_sxi.clear();
     c->zlo_shared = c->zhi_shared = 0;
     c->gm_cap = 0;
     c->mesh_ready = c->pa_ready = c->dinv_ready = false;
@@ -197,12 +204,18 @@ void require_mesh(cdfem_ctx *c)
 void require_pa(cdfem_ctx *c)
 {
     require_mesh(c);
-    if (!c->pa_ready) throw StateError("cdfem_pa_setup has not been called");
+    if (!c->pa_ready && !c->fa_ready) throw StateError("no operator: call cdfem_pa_setup or cdfem_fa_setup");
 }
 
 // operator apply into y (device pointers): Ye = A_e x, y = E->L(Ye) [+ constraint]
 void op_apply(cdfem_ctx *c, const double *x, double *y, bool constrained)
 {
+    if (c->fa_ready) {  // assembled CSR: A, or the eliminated matrix for the constrained operator
+        prof_mark(c, CDFEM_K_APPLY, true);
+        HIPCHK(launch_spmv(c, constrained, x, y));
+        prof_mark(c, CDFEM_K_APPLY, false);
+        return;
+    }
     if (use_brick(c)) {
         prof_mark(c, CDFEM_K_APPLY, true);
         HIPCHK(launch_brick_mult(c, x, y, constrained, 1));
@@ -243,8 +256,12 @@ void ensure_dinv(cdfem_ctx *c)
 {
     if (c->dinv_ready) return;
     double *diag = c->d_w[7];
-    HIPCHK(launch_diag_elem(c, c->d_Ye));
-    HIPCHK(launch_e2l(c, c->d_Ye, nullptr, diag, false, 0));
+    if (c->fa_ready) {
+        HIPCHK(launch_csr_diag(c, diag));
+    } else {
+        HIPCHK(launch_diag_elem(c, c->d_Ye));
+        HIPCHK(launch_e2l(c, c->d_Ye, nullptr, diag, false, 0));
+    }
     interface_sum(c, diag);  // shared planes: the full diagonal (both ranks' elements)
     HIPCHK(launch_dinv(c, diag, c->d_dinv));
     c->dinv_ready = true;
@@ -341,13 +358,21 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(launch_cg_init(c, dB, x, r, z, d, dinv, p.rel_tol, p.abs_tol, p.max_iter));
-    // z = A d ; den
-    prof_mark(c, CDFEM_K_APPLY, true);
-    HIPCHK(launch_apply_st(c, d, c->d_Ye, true, c->d_state));
-    prof_mark(c, CDFEM_K_APPLY, false);
-    prof_mark(c, CDFEM_K_E2L, true);
-    HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 1));
-    prof_mark(c, CDFEM_K_E2L, false);
+    // z = A d ; den = (d, z) and the MFEM den step
+    auto apply = [&] {
+        prof_mark(c, CDFEM_K_APPLY, true);
+        if (c->fa_ready) {
+            HIPCHK(launch_spmv_cg(c, d, z));
+            prof_mark(c, CDFEM_K_APPLY, false);
+            return;
+        }
+        HIPCHK(launch_apply_st(c, d, c->d_Ye, true, c->d_state));
+        prof_mark(c, CDFEM_K_APPLY, false);
+        prof_mark(c, CDFEM_K_E2L, true);
+        HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 1));
+        prof_mark(c, CDFEM_K_E2L, false);
+    };
+    apply();
     int launched = 0;
     for (;;) {
         for (int k = 0; k < check && launched < p.max_iter; ++k, ++launched) {
@@ -357,12 +382,7 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
             prof_mark(c, CDFEM_K_DIRECTION, true);
             HIPCHK(launch_cg_direction(c, z, d));
             prof_mark(c, CDFEM_K_DIRECTION, false);
-            prof_mark(c, CDFEM_K_APPLY, true);
-            HIPCHK(launch_apply_st(c, d, c->d_Ye, true, c->d_state));
-            prof_mark(c, CDFEM_K_APPLY, false);
-            prof_mark(c, CDFEM_K_E2L, true);
-            HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 1));
-            prof_mark(c, CDFEM_K_E2L, false);
+            apply();
         }
         HIPCHK(hipMemcpyAsync(c->h_state, c->d_state, sizeof(KrylovState), hipMemcpyDeviceToHost,
                               c->stream));
@@ -612,6 +632,7 @@ int cdfem_mesh_upload(cdfem_ctx *c, int dim, int order, int ne, const double *el
 int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
 {
     return guarded(c, [&] {
+        if (c->mesh_ready && c->geom != 0) throw ArgError("structured bricks need a hexahedral mesh");
         require_mesh(c);
         if (c->dim != 3) throw UnsupportedError("structured fast path is 3D only");
         if (nx < 1 || ny < 1 || nz < 1 || (int64_t)nx * ny * nz != c->ne)
@@ -681,6 +702,11 @@ int cdfem_rule_size(cdfem_ctx *c, int rule, int *nq)
     return guarded(c, [&] {
         require_mesh(c);
         if (!nq) throw ArgError("nq is null");
+        if (c->geom != 0) {
+            if (rule != CDFEM_RULE_OPERATOR) throw UnsupportedError("simplex meshes: operator rule only");
+            *nq = c->nq_simplex;
+            return CDFEM_OK;
+        }
         const Rule1D &r = rule == CDFEM_RULE_OPERATOR ? c->rule_op
                         : rule == CDFEM_RULE_LINEARFORM ? c->rule_lf : c->rule_err;
         *nq = nq_of(c, r);
@@ -693,6 +719,27 @@ int cdfem_quadrature_points(cdfem_ctx *c, int rule, double *xyz, int where)
     return guarded(c, [&] {
         require_mesh(c);
         if (!xyz) throw ArgError("xyz is null");
+        if (c->geom != 0) {  // affine simplices: x = v0 + J xi, evaluated on the host
+            if (rule != CDFEM_RULE_OPERATOR) throw UnsupportedError("simplex meshes: operator rule only");
+            const int dim = c->dim, nv = dim + 1, nq = c->nq_simplex;
+            std::vector<double> out((size_t)c->ne * nq * dim);
+            for (int e = 0; e < c->ne; ++e) {
+                const double *V = &c->h_verts[(size_t)e * nv * dim];
+                for (int q = 0; q < nq; ++q)
+                    for (int k = 0; k < dim; ++k) {
+                        double x = V[k];
+                        for (int m = 0; m < dim; ++m) x += (V[(m + 1) * dim + k] - V[k]) * c->h_sxi[(size_t)q * dim + m];
+                        out[((size_t)e * nq + q) * dim + k] = x;
+                    }
+            }
+            if (where == CDFEM_DEVICE) {
+                HIPCHK(hipMemcpyAsync(xyz, out.data(), out.size() * 8, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(hipStreamSynchronize(c->stream));
+            } else {
+                std::copy(out.begin(), out.end(), xyz);
+            }
+            return CDFEM_OK;
+        }
         const Rule1D &r = rule == CDFEM_RULE_OPERATOR ? c->rule_op
                         : rule == CDFEM_RULE_LINEARFORM ? c->rule_lf : c->rule_err;
         const size_t n = (size_t)c->ne * nq_of(c, r) * c->dim;
@@ -714,6 +761,7 @@ int cdfem_pa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kap
         require_mesh(c);
         if (kinds == 0 || kinds > 7) throw ArgError("kinds must be a non-empty DIFFUSION|CONVECTION|MASS mask");
         if ((kinds & CDFEM_CONVECTION) && !conv && !conv_q) throw ArgError("convection needs a velocity");
+        if (c->geom != 0) throw UnsupportedError("simplex meshes use full assembly: cdfem_fa_setup");
         if (!apply_supported(c->dim, c->p))
             throw UnsupportedError("no PA apply kernel built for dim=" + std::to_string(c->dim) +
                                    " order=" + std::to_string(c->p));
@@ -741,7 +789,143 @@ int cdfem_pa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kap
         HIPCHK(hipStreamSynchronize(c->stream));
         dfree(dk); dfree(dc); dfree(dm);
         c->pa_ready = true;
+        c->fa_ready = false;
         c->dinv_ready = false;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_mesh_upload_simplex(cdfem_ctx *c, int dim, int order, int ne, const double *elem_verts,
+                              int64_t nldofs, const int32_t *elem_dofs, int n_ess, const int32_t *ess_dofs)
+{
+    return guarded(c, [&] {
+        if (dim != 2 && dim != 3) throw ArgError("dim must be 2 or 3");
+        if (order < 1 || order > 2) throw ArgError("simplex order must be 1 or 2");
+        if (ne <= 0 || nldofs <= 0 || !elem_verts || !elem_dofs) throw ArgError("empty mesh");
+        if (nldofs >= (int64_t)1 << 31) throw ArgError("nldofs exceeds int32 indexing");
+        if (n_ess < 0 || (n_ess > 0 && !ess_dofs)) throw ArgError("bad essential list");
+        HIPCHK(hipSetDevice(c->device));
+        free_mesh(c);
+        c->geom = 1;
+        c->dim = dim;
+        c->p = order;
+        c->d1 = order + 1;
+        c->nd = simplex_ndofs(dim, order);
+        c->nv = dim + 1;
+        c->ne = ne;
+        c->nl = nldofs;
+        c->nblk = (ne + kLanes - 1) / kLanes;
+        const int nd = c->nd;
+        c->h_ess.assign(nldofs, 0);
+        for (int i = 0; i < n_ess; ++i) {
+            if (ess_dofs[i] < 0 || ess_dofs[i] >= nldofs) throw ArgError("essential dof out of range");
+            c->h_ess[ess_dofs[i]] = 1;
+        }
+        c->h_dofs.assign(elem_dofs, elem_dofs + (size_t)ne * nd);
+        for (int32_t g : c->h_dofs)
+            if (g < 0 || g >= nldofs) throw ArgError("element dof out of range");
+        c->h_verts.assign(elem_verts, elem_verts + (size_t)ne * c->nv * dim);
+        std::vector<int32_t> ess_list;
+        for (int64_t i = 0; i < nldofs; ++i)
+            if (c->h_ess[i]) ess_list.push_back((int32_t)i);
+        c->n_ess = (int)ess_list.size();
+        // operator rule (collapsed Gauss, n = p + 2) and its basis tables
+        std::vector<double> w;
+        c->nq_simplex = simplex_rule(dim, order + 2, c->h_sxi, w);
+        const int nq = c->nq_simplex;
+        std::vector<double> tab((size_t)nq * nd * (dim + 1) + nq);
+        for (int q = 0; q < nq; ++q) {
+            double phi[10], dphi[30];
+            simplex_basis(dim, order, &c->h_sxi[(size_t)q * dim], phi, dphi);
+            for (int i = 0; i < nd; ++i) {
+                tab[(size_t)q * nd + i] = phi[i];
+                for (int k = 0; k < dim; ++k) tab[(size_t)nq * nd + ((size_t)q * nd + i) * dim + k] = dphi[i * dim + k];
+            }
+            tab[(size_t)nq * nd * (dim + 1) + q] = w[q];
+        }
+        c->d_stab = dalloc<double>(tab.size());
+        c->d_verts = dalloc<double>(c->h_verts.size());
+        c->d_ess = dalloc<uint8_t>(nldofs);
+        c->d_ess_list = dalloc<int32_t>(ess_list.size());
+        c->d_dinv = dalloc<double>(nldofs);
+        for (auto &v : c->d_w) v = dalloc<double>(nldofs);
+        c->d_part = dalloc<double>((size_t)c->red_blocks + kSpmvMaxBlocks + 16384);
+        HIPCHK(hipMemcpyAsync(c->d_stab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_verts, c->h_verts.data(), c->h_verts.size() * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_ess, c->h_ess.data(), nldofs, hipMemcpyHostToDevice, c->stream));
+        if (!ess_list.empty())
+            HIPCHK(hipMemcpyAsync(c->d_ess_list, ess_list.data(), ess_list.size() * 4, hipMemcpyHostToDevice,
+                                  c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->mesh_ready = true;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_fa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kappa_q, double alpha,
+                   const double *conv, const double *conv_q, double mass, const double *mass_q)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        if (kinds == 0 || kinds > 7) throw ArgError("kinds must be a non-empty DIFFUSION|CONVECTION|MASS mask");
+        if ((kinds & CDFEM_CONVECTION) && !conv && !conv_q) throw ArgError("convection needs a velocity");
+        if (c->geom != 1) throw UnsupportedError("full assembly is implemented for simplex meshes");
+        if (!c->d_rowptr) {  // CSR pattern + contribution lists: once per mesh
+            FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl);
+            c->nnz = P.nnz;
+            c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
+            c->d_cols = dalloc<int32_t>(P.cols.size());
+            c->d_diagpos = dalloc<int32_t>(P.diagpos.size());
+            c->d_coff = dalloc<int32_t>(P.coff.size());
+            c->d_cpos = dalloc<int32_t>(P.cpos.size());
+            c->d_vals = dalloc<double>(c->nnz);
+            c->d_vals_c = dalloc<double>(c->nnz);
+            c->d_Ee = dalloc<double>((size_t)c->nblk * c->nd * c->nd * kLanes);
+            HIPCHK(hipMemcpyAsync(c->d_rowptr, P.rowptr.data(), P.rowptr.size() * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->d_diagpos, P.diagpos.data(), P.diagpos.size() * 4, hipMemcpyHostToDevice,
+                                  c->stream));
+            HIPCHK(hipMemcpyAsync(c->d_coff, P.coff.data(), P.coff.size() * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->d_cpos, P.cpos.data(), P.cpos.size() * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));  // P's host buffers die at scope exit
+            c->fa_lpr = c->nnz > 12 * c->nl ? 8 : 4;
+        }
+        const size_t neq = (size_t)c->ne * c->nq_simplex;
+        double *dk = nullptr, *dc = nullptr, *dm = nullptr;
+        if (kappa_q) {
+            dk = dalloc<double>(neq);
+            HIPCHK(hipMemcpyAsync(dk, kappa_q, neq * 8, hipMemcpyHostToDevice, c->stream));
+        }
+        if (conv_q) {
+            dc = dalloc<double>(neq * c->dim);
+            HIPCHK(hipMemcpyAsync(dc, conv_q, neq * c->dim * 8, hipMemcpyHostToDevice, c->stream));
+        }
+        if (mass_q) {
+            dm = dalloc<double>(neq);
+            HIPCHK(hipMemcpyAsync(dm, mass_q, neq * 8, hipMemcpyHostToDevice, c->stream));
+        }
+        c->kinds = kinds;
+        HIPCHK(launch_simplex_elem(c, dk, kappa, alpha, conv, dc, dm, mass));
+        HIPCHK(launch_fa_assemble(c));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        dfree(dk); dfree(dc); dfree(dm);
+        c->fa_ready = true;
+        c->pa_ready = false;
+        c->dinv_ready = false;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_fa_csr(cdfem_ctx *c, int constrained, int64_t *nnz, int32_t *rowptr, int32_t *cols, double *vals)
+{
+    return guarded(c, [&] {
+        if (!c->fa_ready) throw StateError("cdfem_fa_setup has not been called");
+        if (!nnz) throw ArgError("nnz is null");
+        *nnz = c->nnz;
+        if (rowptr) HIPCHK(hipMemcpy(rowptr, c->d_rowptr, (c->nl + 1) * 4, hipMemcpyDeviceToHost));
+        if (cols) HIPCHK(hipMemcpy(cols, c->d_cols, c->nnz * 4, hipMemcpyDeviceToHost));
+        if (vals)
+            HIPCHK(hipMemcpy(vals, constrained ? c->d_vals_c : c->d_vals, c->nnz * 8, hipMemcpyDeviceToHost));
         return CDFEM_OK;
     });
 }
@@ -769,8 +953,12 @@ int cdfem_pa_diagonal(cdfem_ctx *c, double *diag, int where)
         require_pa(c);
         if (!diag) throw ArgError("null vector");
         double *dd = where == CDFEM_DEVICE ? diag : c->d_w[1];
-        HIPCHK(launch_diag_elem(c, c->d_Ye));
-        HIPCHK(launch_e2l(c, c->d_Ye, nullptr, dd, false, 0));
+        if (c->fa_ready) {
+            HIPCHK(launch_csr_diag(c, dd));
+        } else {
+            HIPCHK(launch_diag_elem(c, c->d_Ye));
+            HIPCHK(launch_e2l(c, c->d_Ye, nullptr, dd, false, 0));
+        }
         dev_out(c, diag, where, dd, c->nl);
         return CDFEM_OK;
     });
@@ -781,6 +969,7 @@ int cdfem_lf_assemble(cdfem_ctx *c, const double *f_q, double *b, int where)
     return guarded(c, [&] {
         require_mesh(c);
         if (!f_q || !b) throw ArgError("null vector");
+        if (c->geom != 0) throw UnsupportedError("linear forms on simplex meshes are not available yet");
         const size_t n = (size_t)c->ne * nq_of(c, c->rule_lf);
         double *dfq = dalloc<double>(n);
         HIPCHK(hipMemcpyAsync(dfq, f_q, n * 8, where == CDFEM_DEVICE ? hipMemcpyDeviceToDevice
@@ -930,6 +1119,11 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
         require_pa(c);
         if (!bytes) throw ArgError("bytes is null");
         const double nl = (double)c->nl, ne = (double)c->ne, nd = c->nd;
+        if (c->fa_ready) {  // CSR SpMV: values + columns + row pointers + x + y
+            if (k != CDFEM_K_APPLY) throw ArgError("FA operators report the SpMV (CDFEM_K_APPLY) only");
+            *bytes = 12.0 * (double)c->nnz + 4.0 * (nl + 1) + 16.0 * nl;
+            return CDFEM_OK;
+        }
         const double nq = nq_of(c, c->rule_op);
         if (use_brick(c)) {
             // CG-mode brick kernels (what the Krylov loop launches); see DESIGN.md section 4

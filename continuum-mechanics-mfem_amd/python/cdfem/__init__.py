@@ -94,6 +94,11 @@ def _declare(L):
         "cdfem_set_slab": (C.c_int, [vp, C.c_int, C.c_int]),
         "cdfem_box_sizes": (C.c_int, [C.c_int] * 7 + [C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int)]),
         "cdfem_box_mesh": (C.c_int, [C.c_int] * 7 + [C.c_double, _dp, _ip, _ip, _dp]),
+        "cdfem_mesh_upload_simplex": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, _dp, i64, _ip, C.c_int, _ip]),
+        "cdfem_fa_setup": (C.c_int, [vp, C.c_uint, C.c_double, _dp, C.c_double, _dp, _dp, C.c_double, _dp]),
+        "cdfem_fa_csr": (C.c_int, [vp, C.c_int, C.POINTER(i64), _ip, _ip, _dp]),
+        "cdfem_kuhn_sizes": (C.c_int, [C.c_int] * 3 + [C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int)]),
+        "cdfem_kuhn_mesh": (C.c_int, [C.c_int] * 3 + [C.c_double, _dp, _ip, _ip, _dp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -149,11 +154,12 @@ def _p(a):
 class Mesh:
     dim: int
     order: int
-    verts: np.ndarray      # (ne, 2^dim, dim)
-    dofmap: np.ndarray     # (ne, (p+1)^dim) int32
+    verts: np.ndarray      # (ne, 2^dim, dim) tensor / (ne, dim+1, dim) simplex
+    dofmap: np.ndarray     # (ne, nd) int32
     nl: int
     ess: np.ndarray        # int32
     dof_xyz: np.ndarray | None = None
+    simplex: bool = False
 
     @property
     def ne(self):
@@ -179,6 +185,25 @@ def box_mesh(dim, n, order, z_range=None, perturb=0.0, with_coords=True) -> Mesh
     if rc:
         raise CdfemError(rc, "box mesh generation failed")
     return Mesh(dim, order, verts, dofmap, nl.value, ess, xyz)
+
+
+def kuhn_mesh(dim, n, order, perturb=0.0, with_coords=True) -> Mesh:
+    """Kuhn simplex mesh of [0,1]^dim (n^dim cubes x dim! simplices, P1/P2; config C4)."""
+    L = lib()
+    ne, nl, ness = C.c_int(), C.c_int64(), C.c_int()
+    rc = L.cdfem_kuhn_sizes(dim, n, order, C.byref(ne), C.byref(nl), C.byref(ness))
+    if rc:
+        raise CdfemError(rc, "bad Kuhn mesh arguments")
+    nd = dim + 1 if order == 1 else (dim + 1) * (dim + 2) // 2
+    verts = np.zeros((ne.value, dim + 1, dim))
+    dofmap = np.zeros((ne.value, nd), dtype=np.int32)
+    ess = np.zeros(ness.value, dtype=np.int32)
+    xyz = np.zeros((nl.value, dim)) if with_coords else None
+    rc = L.cdfem_kuhn_mesh(dim, n, order, float(perturb), _p(verts), dofmap.ctypes.data_as(_ip),
+                           ess.ctypes.data_as(_ip), _p(xyz))
+    if rc:
+        raise CdfemError(rc, "Kuhn mesh generation failed (inverted element?)")
+    return Mesh(dim, order, verts, dofmap, nl.value, ess, xyz, simplex=True)
 
 
 class Context:
@@ -219,9 +244,9 @@ class Context:
         verts = _f64(mesh.verts)
         dofmap = _i32(mesh.dofmap)
         ess = _i32(mesh.ess)
-        self._chk(self.L.cdfem_mesh_upload(self.h, mesh.dim, mesh.order, dofmap.shape[0], _p(verts),
-                                           int(mesh.nl), dofmap.ctypes.data_as(_ip), len(ess),
-                                           ess.ctypes.data_as(_ip)))
+        up = self.L.cdfem_mesh_upload_simplex if mesh.simplex else self.L.cdfem_mesh_upload
+        self._chk(up(self.h, mesh.dim, mesh.order, dofmap.shape[0], _p(verts), int(mesh.nl),
+                     dofmap.ctypes.data_as(_ip), len(ess), ess.ctypes.data_as(_ip)))
         self.mesh = mesh
         self.nl = int(mesh.nl)
         return self
@@ -253,6 +278,29 @@ class Context:
         self._chk(self.L.cdfem_pa_setup(self.h, kinds, float(kappa), _p(keep[0]), float(alpha), _p(cv),
                                         _p(keep[1]), float(mass), _p(keep[2])))
         return self
+
+    def fa_setup(self, kinds=DIFFUSION | CONVECTION | MASS, kappa=1.0, alpha=1.0, conv=None, mass=1.0,
+                 kappa_q=None, conv_q=None, mass_q=None):
+        """Full assembly (CSR on the GPU) of the same form; simplex meshes."""
+        cv = None
+        if conv is not None:
+            cv = np.zeros(3)
+            cv[: len(conv)] = conv
+        keep = [_f64(a) if a is not None else None for a in (kappa_q, conv_q, mass_q)]
+        self._chk(self.L.cdfem_fa_setup(self.h, kinds, float(kappa), _p(keep[0]), float(alpha), _p(cv),
+                                        _p(keep[1]), float(mass), _p(keep[2])))
+        return self
+
+    def fa_csr(self, constrained=False):
+        """(rowptr, cols, vals) of the assembled matrix (constrained: the FormLinearSystem one)."""
+        nnz = C.c_int64()
+        self._chk(self.L.cdfem_fa_csr(self.h, int(constrained), C.byref(nnz), None, None, None))
+        rp = np.zeros(self.nl + 1, dtype=np.int32)
+        cols = np.zeros(nnz.value, dtype=np.int32)
+        vals = np.zeros(nnz.value)
+        self._chk(self.L.cdfem_fa_csr(self.h, int(constrained), C.byref(nnz), rp.ctypes.data_as(_ip),
+                                      cols.ctypes.data_as(_ip), _p(vals)))
+        return rp, cols, vals
 
     def mult(self, x, constrained=False):
         x = _f64(x)

@@ -107,6 +107,24 @@ int cdfem_pa_setup(cdfem_ctx *ctx, unsigned kinds, double kappa, const double *k
                    double alpha, const double *conv, const double *conv_q, double mass,
                    const double *mass_q);
 
+/* ---- full assembly on simplex meshes (BASELINE config C4: unstructured tetrahedra) -------------
+ * replaces: the same ParMesh / H1_FECollection(p, dim) / ParFiniteElementSpace calls on a triangle
+ * or tetrahedral mesh (gmsh input, Input/input_2d.yaml:1), and ParBilinearForm::Assemble +
+ * FormLinearSystem -> HypreParMatrix (linear_convection_diffusion_2D.cpp:339,349-351) whose CSR
+ * PETSc's KSPGMRES then multiplies (MATAIJ, :364-375).
+ * cdfem_mesh_upload_simplex: P1/P2 Lagrange (order 1, 2) on affine simplices; elem_verts ne*(dim+1)
+ * *dim, elem_dofs ne*nd with nd = dim+1 (P1) / (dim+1)(dim+2)/2 (P2), local order: vertices, then
+ * edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3) [2D: (0,1),(0,2),(1,2)]; det J > 0 required.
+ * cdfem_fa_setup: same coefficients as cdfem_pa_setup (per-point arrays on the OPERATOR rule);
+ * assembles A (CSR, columns sorted) and the eliminated matrix of FormLinearSystem on the GPU.
+ * Afterwards cdfem_pa_mult / cdfem_pa_diagonal / cdfem_form_linear_system / cdfem_solve run on the
+ * CSR operator.  cdfem_fa_csr exports it (rowptr n+1, cols/vals nnz; pass NULLs to query nnz).   */
+int cdfem_mesh_upload_simplex(cdfem_ctx *ctx, int dim, int order, int ne, const double *elem_verts,
+                              int64_t nldofs, const int32_t *elem_dofs, int n_ess, const int32_t *ess_dofs);
+int cdfem_fa_setup(cdfem_ctx *ctx, unsigned kinds, double kappa, const double *kappa_q, double alpha,
+                   const double *conv, const double *conv_q, double mass, const double *mass_q);
+int cdfem_fa_csr(cdfem_ctx *ctx, int constrained, int64_t *nnz, int32_t *rowptr, int32_t *cols, double *vals);
+
 /* replaces: Operator::Mult / BilinearForm::Mult (diffusion_mms.cpp:430) when constrained == 0,
  * and the ConstrainedOperator built by FormLinearSystem (:349-351) when constrained != 0
  * (input essential entries treated as 0, output y[ess] = x[ess]).                              */
@@ -201,6 +219,13 @@ int cdfem_box_sizes(int dim, int nx, int ny, int nz, int order, int z0, int z1, 
                     int64_t *nldofs, int *n_ess);
 int cdfem_box_mesh(int dim, int nx, int ny, int nz, int order, int z0, int z1, double perturb,
                    double *elem_verts, int32_t *elem_dofs, int32_t *ess_dofs, double *dof_xyz);
+
+/* Kuhn simplex mesh of [0,1]^dim (config C4): n^dim cubes, dim! simplices each, P1/P2 dofs on the
+ * (order n + 1)^dim lattice; perturb moves interior vertices (returns CDFEM_ERR_ARG if that inverts
+ * an element).  Host only.                                                                      */
+int cdfem_kuhn_sizes(int dim, int n, int order, int *ne, int64_t *nldofs, int *n_ess);
+int cdfem_kuhn_mesh(int dim, int n, int order, double perturb, double *elem_verts, int32_t *elem_dofs,
+                    int32_t *ess_dofs, double *dof_xyz);
 
 #ifdef __cplusplus
 }

@@ -1154,3 +1154,85 @@ ORC_API orc_csr *orc_fa_assemble_simplex(int dim, int p, int ne, const double *v
     free(Ae);
     return A;
 }
+
+/* DomainLF b_i = int f phi_i and ||u_h - u||_L2 on affine simplices with the MMS data of
+ * orc_mms_f / orc_mms_u; rules: collapsed Gauss with n = p + 3 (exact to degree 2p + 6 - dim). */
+static void simplex_point(int dim, const double *V, const double *xi, double *x, double *det)
+{
+    double J[3][3] = {{0}}, A[3][3];
+    for (int k = 0; k < dim; k++) {
+        x[k] = V[k];
+        for (int m = 0; m < dim; m++) {
+            J[k][m] = V[(m + 1) * dim + k] - V[k];
+            x[k] += J[k][m] * xi[m];
+        }
+    }
+    if (dim == 2) x[2] = 0.0;
+    *det = adjugate(dim, J, A);
+}
+
+ORC_API void orc_lf_assemble_simplex(int dim, int p, int ne, const double *verts, const int *dofmap,
+                                     int64_t nl, const double *prm, double *b)
+{
+    const int nd = orc_simplex_nd(dim, p), n1 = p + 3;
+    double xi[7 * 7 * 7 * 3], wq[7 * 7 * 7];
+    const int nq = orc_simplex_rule(dim, n1, xi, wq);
+    double *be = (double *)malloc(sizeof(double) * (size_t)ne * nd);
+    #pragma omp parallel for schedule(static)
+    for (int e = 0; e < ne; e++) {
+        double phi[10], dphi[30], x[3], det;
+        double *out = be + (size_t)e * nd;
+        for (int l = 0; l < nd; l++) out[l] = 0.0;
+        for (int q = 0; q < nq; q++) {
+            simplex_point(dim, verts + (size_t)e * (dim + 1) * dim, xi + (size_t)q * dim, x, &det);
+            simplex_basis(dim, p, xi + (size_t)q * dim, phi, dphi);
+            const double fw = wq[q] * det * orc_mms_f(prm, x);
+            for (int l = 0; l < nd; l++) out[l] += fw * phi[l];
+        }
+    }
+    memset(b, 0, sizeof(double) * nl);
+    for (int64_t k = 0; k < (int64_t)ne * nd; k++) b[dofmap[k]] += be[k];
+    free(be);
+}
+
+ORC_API double orc_l2_error_simplex(int dim, int p, int ne, const double *verts, const int *dofmap,
+                                    const double *u, const double *prm)
+{
+    const int nd = orc_simplex_nd(dim, p), n1 = p + 3;
+    double xi[7 * 7 * 7 * 3], wq[7 * 7 * 7];
+    const int nq = orc_simplex_rule(dim, n1, xi, wq);
+    double err = 0.0;
+    #pragma omp parallel for reduction(+ : err) schedule(static)
+    for (int e = 0; e < ne; e++) {
+        double phi[10], dphi[30], x[3], det;
+        for (int q = 0; q < nq; q++) {
+            simplex_point(dim, verts + (size_t)e * (dim + 1) * dim, xi + (size_t)q * dim, x, &det);
+            simplex_basis(dim, p, xi + (size_t)q * dim, phi, dphi);
+            double uh = 0.0;
+            for (int l = 0; l < nd; l++) uh += u[dofmap[(size_t)e * nd + l]] * phi[l];
+            const double d = uh - orc_mms_u(prm, x);
+            err += wq[q] * det * d * d;
+        }
+    }
+    return sqrt(err);
+}
+
+/* Physical coordinates of the simplex dofs (vertices, edge midpoints). */
+ORC_API void orc_dof_coords_simplex(int dim, int p, int ne, const double *verts, const int *dofmap, double *xyz)
+{
+    const int nd = orc_simplex_nd(dim, p), nv = dim + 1;
+    for (int e = 0; e < ne; e++) {
+        const double *V = verts + (size_t)e * nv * dim;
+        for (int l = 0; l < nd; l++) {
+            double X[3] = {0, 0, 0};
+            if (l < nv) {
+                for (int k = 0; k < dim; k++) X[k] = V[l * dim + k];
+            } else {
+                const int ed = l - nv;
+                const int a = dim == 3 ? kEdge3[ed][0] : kEdge2[ed][0], b = dim == 3 ? kEdge3[ed][1] : kEdge2[ed][1];
+                for (int k = 0; k < dim; k++) X[k] = 0.5 * (V[a * dim + k] + V[b * dim + k]);
+            }
+            for (int k = 0; k < dim; k++) xyz[(size_t)dofmap[(size_t)e * nd + l] * dim + k] = X[k];
+        }
+    }
+}

@@ -68,6 +68,17 @@ def lib():
         L.orc_l2_error.restype = C.c_double
         L.orc_ebe_mult.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, C.c_int64, C.c_double,
                                    C.c_double, C.c_double, dp, C.c_int, dp, dp]
+        L.orc_simplex_nd.argtypes = [C.c_int, C.c_int]
+        L.orc_simplex_rule.argtypes = [C.c_int, C.c_int, dp, dp]
+        L.orc_mesh_kuhn_sizes.argtypes = [C.c_int, C.c_int, C.c_int, ip, lp]
+        L.orc_mesh_kuhn.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, dp, ip, ip]
+        L.orc_fa_assemble_simplex.restype = C.c_void_p
+        L.orc_fa_assemble_simplex.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, C.c_int64, C.c_double,
+                                              C.c_double, C.c_double, dp, C.c_int]
+        L.orc_lf_assemble_simplex.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, C.c_int64, dp, dp]
+        L.orc_l2_error_simplex.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, dp, dp]
+        L.orc_l2_error_simplex.restype = C.c_double
+        L.orc_dof_coords_simplex.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, dp]
         L.orc_num_threads.restype = C.c_int
         L.orc_set_num_threads.argtypes = [C.c_int]
         _lib = L
@@ -135,6 +146,67 @@ class BoxMesh:
         return xyz
 
 
+class KuhnMesh:
+    """Kuhn simplex mesh of [0,1]^dim, P1/P2 (see orc_mesh_kuhn for the conventions; config C4)."""
+
+    def __init__(self, dim, n, p, perturb=0.0):
+        L = lib()
+        ne, nl = C.c_int(), C.c_int64()
+        L.orc_mesh_kuhn_sizes(dim, n, p, C.byref(ne), C.byref(nl))
+        self.dim, self.p, self.n = dim, p, n
+        self.ne, self.nl = ne.value, nl.value
+        self.nv = dim + 1
+        self.nd = L.orc_simplex_nd(dim, p)
+        self.verts = np.zeros((self.ne, self.nv, dim))
+        self.dofmap = np.zeros((self.ne, self.nd), dtype=np.int32)
+        self.bdr = np.zeros(self.nl, dtype=np.int32)
+        if L.orc_mesh_kuhn(dim, n, p, float(perturb), _d(self.verts), _i(self.dofmap), _i(self.bdr)):
+            raise RuntimeError("orc_mesh_kuhn: inverted element")
+        self.ess = np.nonzero(self.bdr)[0].astype(np.int32)
+
+
+def _simplex_arrays(mesh):
+    return (np.ascontiguousarray(mesh.verts, dtype=np.float64), np.ascontiguousarray(mesh.dofmap, dtype=np.int32))
+
+
+def lf_assemble_simplex(mesh, prm):
+    v, d = _simplex_arrays(mesh)
+    b = np.zeros(mesh.nl)
+    lib().orc_lf_assemble_simplex(mesh.dim, mesh.p, mesh.ne, _d(v), _i(d), mesh.nl, _d(prm), _d(b))
+    return b
+
+
+def l2_error_simplex(mesh, u, prm):
+    v, d = _simplex_arrays(mesh)
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    return lib().orc_l2_error_simplex(mesh.dim, mesh.p, mesh.ne, _d(v), _i(d), _d(u), _d(prm))
+
+
+def dof_coords_simplex(mesh):
+    v, d = _simplex_arrays(mesh)
+    xyz = np.zeros((mesh.nl, mesh.dim))
+    lib().orc_dof_coords_simplex(mesh.dim, mesh.p, mesh.ne, _d(v), _i(d), _d(xyz))
+    return xyz
+
+
+def solve_mms_simplex(mesh, prm, kappa, s, c, alpha=1.0, tol=1e-10, atol=1e-12, max_it=500):
+    """C4 driver sequence on the oracle: FA CSR, FormLinearSystem, GMRES(30) + Jacobi, L2 error."""
+    A = fa_assemble_simplex(mesh, kappa=kappa, alpha=alpha, s=s, c=c)
+    b = lf_assemble_simplex(mesh, prm)
+    u = np.zeros(mesh.nl)
+    xyz = dof_coords_simplex(mesh)
+    u[mesh.ess] = mms_u(prm, xyz[mesh.ess])
+    Ac, B = form_linear_system(A, mesh.bdr, u, b)
+    X, info = gmres(Ac, B, dinv=1.0 / Ac.diag(), rtol=tol, atol=atol, max_it=max_it)
+    return X, info, l2_error_simplex(mesh, X, prm)
+
+
+def simplex_rule(dim, n):
+    xi, w = np.zeros(n ** dim * dim), np.zeros(n ** dim)
+    nq = lib().orc_simplex_rule(dim, n, _d(xi), _d(w))
+    return xi.reshape(nq, dim), w
+
+
 class CSR:
     def __init__(self, handle):
         self.h = handle
@@ -184,6 +256,18 @@ def fa_assemble(mesh: BoxMesh, kappa=1.0, alpha=1.0, s=1.0, c=None, kinds=DIFFUS
                               kappa, alpha, s, _d(cc), kinds)
     if not h:
         raise RuntimeError("orc_fa_assemble: integrator rules do not coincide")
+    return CSR(h)
+
+
+def fa_assemble_simplex(mesh, kappa=1.0, alpha=1.0, s=1.0, c=None, kinds=DIFFUSION | CONVECTION | MASS):
+    """FA CSR on P1/P2 simplices (mesh: KuhnMesh or any object with dim/p/ne/verts/dofmap/nl)."""
+    cc = _conv(c, mesh.dim)
+    verts = np.ascontiguousarray(mesh.verts, dtype=np.float64)
+    dofmap = np.ascontiguousarray(mesh.dofmap, dtype=np.int32)
+    h = lib().orc_fa_assemble_simplex(mesh.dim, mesh.p, mesh.ne, _d(verts), _i(dofmap), mesh.nl,
+                                      kappa, alpha, s, _d(cc), kinds)
+    if not h:
+        raise RuntimeError("orc_fa_assemble_simplex: unsupported order")
     return CSR(h)
 
 
