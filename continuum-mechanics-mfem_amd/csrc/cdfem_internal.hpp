@@ -131,12 +131,14 @@ struct cdfem_ctx {
     // full assembly (cdfem_fa_setup): CSR with sorted columns + deterministic contribution lists
     bool fa_ready = false;
     int64_t nnz = 0;
-    int fa_lpr = 8;                     // lanes per CSR row in the SpMV
     int32_t *d_rowptr = nullptr, *d_cols = nullptr, *d_diagpos = nullptr;
     int32_t *d_coff = nullptr, *d_cpos = nullptr;  // per-nonzero contribution lists into d_Ee
     double *d_vals = nullptr;           // A
     double *d_vals_c = nullptr;         // eliminated A (FormLinearSystem, DIAG_ONE)
     double *d_Ee = nullptr;             // element matrices [blk][nd*nd][64]
+    int64_t nslices = 0, nstored = 0;   // SELL-64 copy (the SpMV layout)
+    int32_t *d_sptr = nullptr, *d_srows = nullptr, *d_scols = nullptr, *d_smap = nullptr;
+    double *d_svals = nullptr, *d_svals_c = nullptr;
 
     // partial assembly
     unsigned kinds = 0;
@@ -237,15 +239,21 @@ hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q);
 
 // ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
 // full assembly on simplices (fa_kernels.hip)
-constexpr int kSpmvMaxBlocks = 8192;
+constexpr int kSpmvMaxBlocks = 65536;  // partial slots reserved for the SpMV-CG den
 struct FaPattern {
     int64_t nnz = 0;
     std::vector<int32_t> rowptr, cols, diagpos, coff, cpos;
+    // SELL-64 (sigma = global sort by row length) copy of the pattern for the SpMV
+    std::vector<int32_t> sptr;   // [nslices + 1] first stored entry of each 64-row slice
+    std::vector<int32_t> srows;  // [nslices * 64] original row of (slice, lane), -1 = padding
+    std::vector<int32_t> scols;  // [stored] column, slice-major then entry-major then lane
+    std::vector<int32_t> smap;   // [stored] CSR index of the stored entry, -1 = padding
 };
 FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl);
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, double kappa, double alpha, const double *conv,
                                const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);
+hipError_t launch_sell_fill(cdfem_ctx *c);
 hipError_t launch_csr_diag(cdfem_ctx *c, double *d);
 hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y);
 hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q);

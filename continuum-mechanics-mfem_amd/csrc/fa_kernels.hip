@@ -12,8 +12,9 @@
 //   k_fa_gather      one thread per nonzero: fixed-order sum of its contributions (bitwise
 //                    reproducible, no atomics);
 //   k_fa_eliminate   the FormLinearSystem matrix: ess rows/cols zeroed, unit diagonal (DIAG_ONE).
-// Hot loop: k_spmv<LPR> — LPR lanes per row (8 for P2 tets, ~27 nnz/row), column/value loads
-// coalesced within a row group, x gathered (lexicographic numbering keeps it L2-local).
+// Hot loop: k_sell_spmv on a SELL-64 copy of the matrix (rows sorted by length, 64-row slices
+// stored column-major: one lane per row, each value/column load one coalesced wave access; < 1 %
+// padding for Kuhn P2), x gathered (lexicographic numbering keeps it L2-local).
 // Algorithmic bytes per SpMV = 12 nnz + 4 (n + 1) + 16 n.
 #include <hip/hip_runtime.h>
 
@@ -128,6 +129,45 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
             }
         }
     });
+    // SELL-64 with a global stable sort by row length (descending): Kuhn P2 rows take a handful
+    // of distinct lengths, so the padding is < 1 %.  Within a row the entries keep CSR order.
+    std::vector<int32_t> order(nl);
+    for (int64_t i = 0; i < nl; ++i) order[i] = (int32_t)i;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+        return rowptr[a + 1] - rowptr[a] > rowptr[b + 1] - rowptr[b];
+    });
+    const int64_t ns = (nl + kLanes - 1) / kLanes;
+    P.sptr.assign(ns + 1, 0);
+    P.srows.assign(ns * kLanes, -1);
+    int64_t stored = 0;
+    for (int64_t sl = 0; sl < ns; ++sl) {
+        int len = 0;
+        for (int l = 0; l < kLanes && sl * kLanes + l < nl; ++l) {
+            const int32_t r = order[sl * kLanes + l];
+            P.srows[sl * kLanes + l] = r;
+            len = std::max(len, rowptr[r + 1] - rowptr[r]);
+        }
+        stored += (int64_t)len * kLanes;
+        if (stored >= ((int64_t)1 << 31)) throw std::runtime_error("SELL storage exceeds int32 indexing");
+        P.sptr[sl + 1] = (int32_t)stored;
+    }
+    P.scols.assign(stored, 0);
+    P.smap.assign(stored, -1);
+    for (int64_t sl = 0; sl < ns; ++sl) {
+        const int len = (P.sptr[sl + 1] - P.sptr[sl]) / kLanes;
+        for (int l = 0; l < kLanes; ++l) {
+            const int32_t r = P.srows[sl * kLanes + l];
+            for (int j = 0; j < len; ++j) {
+                const int64_t t = P.sptr[sl] + (int64_t)j * kLanes + l;
+                if (r >= 0 && j < rowptr[r + 1] - rowptr[r]) {
+                    P.scols[t] = cols[rowptr[r] + j];
+                    P.smap[t] = rowptr[r] + j;
+                } else {
+                    P.scols[t] = r >= 0 ? r : 0;  // padding: a valid column, value 0
+                }
+            }
+        }
+    }
     P.rowptr = std::move(rowptr);
     return P;
 }
@@ -267,28 +307,53 @@ k_csr_diag(const double *__restrict__ vals, const int32_t *__restrict__ diagpos,
     if (i < n) d[i] = vals[diagpos[i]];
 }
 
-// y = A x, LPR lanes per row (grid-stride over row groups).  CG mode also accumulates the
-// partials of (x, y) (den = (d, A d)) and exits at entry once the Krylov state is done.
-template <int LPR, bool CG>
+// SELL copies of A and of the eliminated A (after every assembly)
 __global__ void __launch_bounds__(256)
-k_spmv(const int32_t *__restrict__ rowptr, const int32_t *__restrict__ cols, const double *__restrict__ vals,
-       const double *__restrict__ x, double *__restrict__ y, int64_t n, double *__restrict__ part,
-       const KrylovState *__restrict__ st)
+k_sell_fill(const int32_t *__restrict__ smap, const double *__restrict__ vals, const double *__restrict__ vals_c,
+            double *__restrict__ svals, double *__restrict__ svals_c, int64_t stored)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= stored) return;
+    const int32_t k = smap[t];
+    svals[t] = k >= 0 ? vals[k] : 0.0;
+    svals_c[t] = k >= 0 ? vals_c[k] : 0.0;
+}
+
+// y = A x on the SELL-64 layout: one wave per 64-row slice, one lane per row, entries of a row
+// summed in CSR order; every value/column load is one coalesced 512/256-byte wave access.
+// CG mode: partials of (x, y) and early exit once the Krylov state is done.
+template <bool CG>
+__global__ void __launch_bounds__(256)
+k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows, const int32_t *__restrict__ scols,
+            const double *__restrict__ svals, const double *__restrict__ x, double *__restrict__ y, int64_t nslices,
+            double *__restrict__ part, const KrylovState *__restrict__ st)
 {
     __shared__ double sh[256 / 64];
     if (CG && st->done) return;
-    const int sub = threadIdx.x % LPR;
-    const int64_t groups = (int64_t)gridDim.x * (256 / LPR);
+    const int lane = threadIdx.x & 63;
+    const int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     double dd = 0.0;
-    for (int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR; row < n; row += groups) {
-        double acc = 0.0;
-        const int32_t k1 = rowptr[row + 1];
-        for (int32_t k = rowptr[row] + sub; k < k1; k += LPR) acc += vals[k] * x[cols[k]];
-#pragma unroll
-        for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, LPR);
-        if (sub == 0) {
+    if (sl < nslices) {
+        const int32_t b = sptr[sl], len = (sptr[sl + 1] - b) >> 6;
+        const int32_t row = srows[sl * 64 + lane];
+        const double *v = svals + b + lane;
+        const int32_t *cidx = scols + b + lane;
+        double a0 = 0.0;
+        int j = 0;
+        for (; j + 4 <= len; j += 4) {  // 4 independent loads in flight per lane
+            const double v0 = v[(j + 0) * 64], v1 = v[(j + 1) * 64], v2 = v[(j + 2) * 64], v3 = v[(j + 3) * 64];
+            const int32_t c0 = cidx[(j + 0) * 64], c1 = cidx[(j + 1) * 64], c2 = cidx[(j + 2) * 64],
+                          c3 = cidx[(j + 3) * 64];
+            a0 = fma(v0, x[c0], a0);
+            a0 = fma(v1, x[c1], a0);
+            a0 = fma(v2, x[c2], a0);
+            a0 = fma(v3, x[c3], a0);
+        }
+        for (; j < len; ++j) a0 = fma(v[j * 64], x[cidx[j * 64]], a0);
+        const double acc = a0;
+        if (row >= 0) {
             y[row] = acc;
-            if (CG) dd += acc * x[row];
+            if (CG) dd = acc * x[row];
         }
     }
     if (CG) store_partial(block_sum(dd, sh), part);
@@ -328,38 +393,30 @@ hipError_t launch_csr_diag(cdfem_ctx *c, double *d)
     return hipGetLastError();
 }
 
-static unsigned spmv_grid(cdfem_ctx *c)
+hipError_t launch_sell_fill(cdfem_ctx *c)
 {
-    const int64_t need = (c->nl * c->fa_lpr + 255) / 256;
-    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, kSpmvMaxBlocks));
+    hipLaunchKernelGGL(k_sell_fill, dim3((unsigned)((c->nstored + 255) / 256)), dim3(256), 0, c->stream, c->d_smap,
+                       c->d_vals, c->d_vals_c, c->d_svals, c->d_svals_c, c->nstored);
+    return hipGetLastError();
 }
+
+unsigned sell_grid(const cdfem_ctx *c) { return (unsigned)((c->nslices + 3) / 4); }
 
 hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y)
 {
-    const double *v = constrained ? c->d_vals_c : c->d_vals;
-    const dim3 g(spmv_grid(c)), b(256);
-    if (c->fa_lpr == 8)
-        hipLaunchKernelGGL((k_spmv<8, false>), g, b, 0, c->stream, c->d_rowptr, c->d_cols, v, x, y, (int64_t)c->nl,
-                           nullptr, nullptr);
-    else
-        hipLaunchKernelGGL((k_spmv<4, false>), g, b, 0, c->stream, c->d_rowptr, c->d_cols, v, x, y, (int64_t)c->nl,
-                           nullptr, nullptr);
+    hipLaunchKernelGGL((k_sell_spmv<false>), dim3(sell_grid(c)), dim3(256), 0, c->stream, c->d_sptr, c->d_srows,
+                       c->d_scols, constrained ? c->d_svals_c : c->d_svals, x, y, c->nslices, nullptr, nullptr);
     return hipGetLastError();
 }
 
 // q = A_c d and the den partials, then the MFEM CG den step (one-block finalizer)
 hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q)
 {
-    const dim3 g(spmv_grid(c)), b(256);
-    if (c->fa_lpr == 8)
-        hipLaunchKernelGGL((k_spmv<8, true>), g, b, 0, c->stream, c->d_rowptr, c->d_cols, c->d_vals_c, d, q,
-                           (int64_t)c->nl, c->d_part, c->d_state);
-    else
-        hipLaunchKernelGGL((k_spmv<4, true>), g, b, 0, c->stream, c->d_rowptr, c->d_cols, c->d_vals_c, d, q,
-                           (int64_t)c->nl, c->d_part, c->d_state);
+    hipLaunchKernelGGL((k_sell_spmv<true>), dim3(sell_grid(c)), dim3(256), 0, c->stream, c->d_sptr, c->d_srows,
+                       c->d_scols, c->d_svals_c, d, q, c->nslices, c->d_part, c->d_state);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_den_fin(c, (int)g.x);
+    return launch_den_fin(c, (int)sell_grid(c));
 }
 
 }  // namespace cdfem

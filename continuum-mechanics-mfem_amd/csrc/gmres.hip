@@ -24,7 +24,8 @@
 
 namespace cdfem {
 
-constexpr int kGmEPT = 8;                         // L-vector entries per thread in the pass kernels
+constexpr int kGmEPT = 4;                         // L-vector entries per thread in the pass kernels
+constexpr int kGmBatch = 8;                       // projections reduced together in pass 1
 constexpr int kGmChunk = kRedThreads * kGmEPT;    // entries per block
 
 int gmres_blocks(int64_t n) { return (int)((n + kGmChunk - 1) / kGmChunk); }
@@ -84,15 +85,18 @@ k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st,
 }
 
 // ---- pass 1: w = s_j M^{-1} A V_j (in place over the apply output), partial (w, V_i), i <= j ----
+// The projections are formed kGmBatch at a time: kGmBatch * kGmEPT independent loads per lane in
+// flight, one LDS exchange + barrier per batch (not per basis vector).
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double *__restrict__ V, int64_t n,
            int64_t ldv, double *__restrict__ part, int nb, const GmresState *__restrict__ st)
 {
-    __shared__ double sh[kRedThreads / 64];
+    __shared__ double sh[kGmBatch][kRedThreads / 64];
     if (st->cycle_done) return;
     const int j = st->j;
     const double sj = st->s[j];
     const int64_t base = (int64_t)blockIdx.x * kGmChunk + threadIdx.x;
+    const int lane = threadIdx.x & 63, wv_id = threadIdx.x >> 6;
     double wv[kGmEPT];
 #pragma unroll
     for (int e = 0; e < kGmEPT; ++e) {
@@ -105,17 +109,33 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
         }
         wv[e] = v;
     }
-    for (int i = 0; i <= j; ++i) {
-        const double *vi = V + (int64_t)i * ldv;
-        double acc = 0.0;
+    for (int i0 = 0; i0 <= j; i0 += kGmBatch) {
+        double acc[kGmBatch];
 #pragma unroll
-        for (int e = 0; e < kGmEPT; ++e) {
-            const int64_t k = base + (int64_t)e * kRedThreads;
-            if (k < n) acc += wv[e] * vi[k];
+        for (int b = 0; b < kGmBatch; ++b) {
+            acc[b] = 0.0;
+            if (i0 + b <= j) {
+                const double *vi = V + (int64_t)(i0 + b) * ldv;
+#pragma unroll
+                for (int e = 0; e < kGmEPT; ++e) {
+                    const int64_t k = base + (int64_t)e * kRedThreads;
+                    if (k < n) acc[b] += wv[e] * vi[k];
+                }
+            }
         }
-        const double t = block_sum(acc, sh);
-        if (threadIdx.x == 0) part[(int64_t)i * nb + blockIdx.x] = t;
-        __syncthreads();  // sh is reused by the next block_sum
+#pragma unroll
+        for (int b = 0; b < kGmBatch; ++b) {
+            const double t = wave_sum(acc[b]);
+            if (lane == 0) sh[b][wv_id] = t;
+        }
+        __syncthreads();
+        if (threadIdx.x < kGmBatch && i0 + (int)threadIdx.x <= j) {
+            double t = 0.0;
+#pragma unroll
+            for (int q = 0; q < kRedThreads / 64; ++q) t += sh[threadIdx.x][q];
+            part[(int64_t)(i0 + threadIdx.x) * nb + blockIdx.x] = t;
+        }
+        __syncthreads();
     }
 }
 
@@ -149,6 +169,7 @@ k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int6
         const int64_t k = base + (int64_t)e * kRedThreads;
         acc[e] = k < n ? w[k] : 0.0;
     }
+#pragma unroll 4
     for (int i = 0; i <= j; ++i) {
         const double coef = st->H[i * kGmMaxRestart + j] * st->s[i];
         const double *vi = V + (int64_t)i * ldv;
