@@ -153,22 +153,26 @@ void build_layout(cdfem_ctx *c, const std::vector<int32_t> &perm)
     std::vector<int32_t> where(c->ne, -1);
     for (size_t k = 0; k < perm.size(); ++k)
         if (perm[k] >= 0) where[perm[k]] = (int32_t)k;
+    // E-vector / map index of (element, local dof): blocks of 64 lanes, or element-major
+    auto eidx = [&](int e, int l) -> size_t {
+        if (c->qlay == 1) return (size_t)e * nd + l;
+        const int blk = where[e] / kLanes, lane = where[e] % kLanes;
+        return ((size_t)blk * nd + l) * kLanes + lane;
+    };
     std::vector<int32_t> cnt(nl + 1, 0);
     for (int e = 0; e < c->ne; ++e) {
-        const int blk = where[e] / kLanes, lane = where[e] % kLanes;
         for (int l = 0; l < nd; ++l) {
             const int32_t g = c->h_dofs[(size_t)e * nd + l];
-            map[((size_t)blk * nd + l) * kLanes + lane] = c->h_ess[g] ? -(g + 1) : g;
+            map[eidx(e, l)] = c->h_ess[g] ? -(g + 1) : g;
             cnt[g + 1]++;
         }
     }
     for (int64_t i = 0; i < nl; ++i) cnt[i + 1] += cnt[i];
     std::vector<int32_t> pos((size_t)c->ne * nd), fill(cnt.begin(), cnt.end() - 1);
     for (int e = 0; e < c->ne; ++e) {
-        const int blk = where[e] / kLanes, lane = where[e] % kLanes;
         for (int l = 0; l < nd; ++l) {
             const int32_t g = c->h_dofs[(size_t)e * nd + l];
-            pos[fill[g]++] = (int32_t)(((size_t)blk * nd + l) * kLanes + lane);
+            pos[fill[g]++] = (int32_t)eidx(e, l);
         }
     }
     dfree(c->d_map); dfree(c->d_e2l_off); dfree(c->d_e2l_pos); dfree(c->d_perm); dfree(c->d_Ye);
@@ -593,7 +597,8 @@ int cdfem_mesh_upload(cdfem_ctx *c, int dim, int order, int ne, const double *el
         c->ne = ne;
         c->nl = nldofs;
         c->nblk = (ne + kLanes - 1) / kLanes;
-        if ((int64_t)ne * c->nd >= (int64_t)1 << 31) throw ArgError("E-vector exceeds int32 indexing");
+        c->qlay = (dim == 3 && order >= 3) ? 1 : 0;
+        if ((int64_t)c->nblk * kLanes * c->nd >= (int64_t)1 << 31) throw ArgError("E-vector exceeds int32 indexing");
         c->rule_op = make_rule(order, rule_points_1d(0, dim, order));
         c->rule_lf = make_rule(order, rule_points_1d(1, dim, order));
         c->rule_err = make_rule(order, rule_points_1d(2, dim, order));
@@ -636,6 +641,7 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
 {
     return guarded(c, [&] {
         if (c->mesh_ready && c->geom != 0) throw ArgError("structured bricks need a hexahedral mesh");
+        if (c->mesh_ready && c->qlay != 0) throw UnsupportedError("structured bricks are built for p <= 2");
         require_mesh(c);
         if (c->dim != 3) throw UnsupportedError("structured fast path is 3D only");
         if (nx < 1 || ny < 1 || nz < 1 || (int64_t)nx * ny * nz != c->ne)

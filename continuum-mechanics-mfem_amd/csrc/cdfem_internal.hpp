@@ -89,6 +89,8 @@ struct cdfem_ctx {
 
     // mesh / space
     int dim = 0, p = 0, d1 = 0, nd = 0, ne = 0, nblk = 0, nv = 0;
+    int qlay = 0;                       // 0: element blocks of 64 (thread per element), 1: element-major
+                                        //    map / E-vector / qdata (wave per element, 3D p >= 3)
     int64_t nl = 0;
     int n_ess = 0;
     bool mesh_ready = false;
@@ -175,6 +177,7 @@ hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, double kapp
                               const double *conv, const double *d_conv_q, const double *d_mass_q,
                               double mass);
 hipError_t launch_apply(cdfem_ctx *c, const double *x, double *Ye, bool constrained);
+hipError_t launch_apply_wpe(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st);
 hipError_t launch_apply_st(cdfem_ctx *c, const double *x, double *Ye, bool constrained,
                            const KrylovState *st);
 hipError_t launch_diag_elem(cdfem_ctx *c, double *Ye);

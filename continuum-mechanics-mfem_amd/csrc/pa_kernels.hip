@@ -240,7 +240,7 @@ __device__ inline void qpoint(int q, int q1, int dim, const Rule1D &r, double xi
 // qdata setup: thread per (element-block, q, lane); coalesced writes of the [b][q][c][lane] layout
 template <int DIM>
 __global__ void __launch_bounds__(256)
-k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm, int ne, int nblk,
+k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm, int ne, int nblk, int qlay,
               const Rule1D r, unsigned kinds,
               int nc, double kappa, const double *__restrict__ kappa_q, double alpha, double c0,
               double c1, double c2, const double *__restrict__ conv_q, double mass,
@@ -255,8 +255,14 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
     const int b = (int)(t / ((int64_t)kLanes * nq));
     const int e = perm[(size_t)b * kLanes + lane];
     double *out = qd + ((size_t)b * nq + q) * nc * kLanes;
+    // component k of this point: block layout (qd_offset) or element-major [e][k][q]
+    auto put = [&](int k, double v) {
+        if (qlay == 1) qd[((size_t)e * nc + k) * nq + q] = v;
+        else out[qd_offset(k, lane, nc)] = v;
+    };
     if (e < 0 || e >= ne) {
-        for (int k = 0; k < nc; ++k) out[qd_offset(k, lane, nc)] = 0.0;
+        if (qlay == 0)
+            for (int k = 0; k < nc; ++k) out[qd_offset(k, lane, nc)] = 0.0;
         return;
     }
     double xi[3], W;
@@ -273,7 +279,7 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
             for (int j = i; j < DIM; ++j) {
                 double acc = 0.0;
                 for (int k = 0; k < DIM; ++k) acc += A[i][k] * A[j][k];
-                out[qd_offset(o++, lane, nc)] = s * acc;
+                put(o++, s * acc);
             }
     }
     if (kinds & CDFEM_CONVECTION) {
@@ -283,12 +289,12 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
         for (int i = 0; i < DIM; ++i) {
             double acc = 0.0;
             for (int k = 0; k < DIM; ++k) acc += A[i][k] * cv[k];
-            out[qd_offset(o++, lane, nc)] = W * alpha * acc;
+            put(o++, W * alpha * acc);
         }
     }
     if (kinds & CDFEM_MASS) {
         const double s = mass_q ? mass_q[eq] : mass;
-        out[qd_offset(o++, lane, nc)] = W * s * det;
+        put(o++, W * s * det);
     }
 }
 
@@ -326,8 +332,8 @@ __device__ inline void basis_at(int l, int q, int dim, const Rule1D &r, double &
 // PA diagonal, element part: thread per (block, l, lane); Ye layout [b][l][lane]
 template <int DIM>
 __global__ void __launch_bounds__(256)
-k_diag_elem(const double *__restrict__ qd, int nblk, int nd, const Rule1D r, unsigned kinds, int nc,
-            double *__restrict__ Ye)
+k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int ne, int nblk, int nd, int qlay,
+            const Rule1D r, unsigned kinds, int nc, double *__restrict__ Ye)
 {
     const int q1 = r.q1;
     const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
@@ -338,10 +344,14 @@ k_diag_elem(const double *__restrict__ qd, int nblk, int nd, const Rule1D r, uns
     const int b = (int)(t / ((int64_t)kLanes * nd));
     const int oC = (kinds & CDFEM_DIFFUSION) ? DIM * (DIM + 1) / 2 : 0;
     const int oM = oC + ((kinds & CDFEM_CONVECTION) ? DIM : 0);
+    const int e = perm[(size_t)b * kLanes + lane];
+    if (qlay == 1 && (e < 0 || e >= ne)) return;
     double acc = 0.0;
     for (int q = 0; q < nq; ++q) {
         const double *qb = qd + ((size_t)b * nq + q) * nc * kLanes;
-        auto qq = [&](int k) { return qb[qd_offset(k, lane, nc)]; };
+        auto qq = [&](int k) {
+            return qlay == 1 ? qd[((size_t)e * nc + k) * nq + q] : qb[qd_offset(k, lane, nc)];
+        };
         double phi, g[3];
         basis_at(l, q, DIM, r, phi, g);
         if (kinds & CDFEM_DIFFUSION) {
@@ -363,13 +373,14 @@ k_diag_elem(const double *__restrict__ qd, int nblk, int nd, const Rule1D r, uns
         }
         if (kinds & CDFEM_MASS) acc += qq(oM) * phi * phi;
     }
-    Ye[t] = acc;  // t == (b*nd + l)*64 + lane
+    if (qlay == 1) Ye[(size_t)e * nd + l] = acc;
+    else Ye[t] = acc;  // t == (b*nd + l)*64 + lane
 }
 
 // linear form, element part: be_l = sum_q W detJ f_q phi_l; thread per (block, l, lane)
 template <int DIM>
 __global__ void __launch_bounds__(256)
-k_lf_elem(const double *__restrict__ verts, const int32_t *__restrict__ perm, int ne, int nblk, int nd,
+k_lf_elem(const double *__restrict__ verts, const int32_t *__restrict__ perm, int ne, int nblk, int nd, int qlay,
           const Rule1D r,
           const double *__restrict__ fq, double *__restrict__ Ye)
 {
@@ -392,7 +403,11 @@ k_lf_elem(const double *__restrict__ verts, const int32_t *__restrict__ perm, in
             acc += W * det * fq[(size_t)e * nq + q] * phi;
         }
     }
-    Ye[t] = acc;
+    if (qlay == 1) {
+        if (e >= 0 && e < ne) Ye[(size_t)e * nd + l] = acc;
+    } else {
+        Ye[t] = acc;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -411,11 +426,11 @@ hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, double kapp
     const double c2 = (conv && c->dim == 3) ? conv[2] : 0.0;
     if (c->dim == 3)
         hipLaunchKernelGGL(k_setup_qdata<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->d_perm, c->ne, c->nblk, c->rule_op, c->kinds, c->ncomp, kappa,
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->qlay, c->rule_op, c->kinds, c->ncomp, kappa,
                            d_kappa_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
     else
         hipLaunchKernelGGL(k_setup_qdata<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->d_perm, c->ne, c->nblk, c->rule_op, c->kinds, c->ncomp, kappa,
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->qlay, c->rule_op, c->kinds, c->ncomp, kappa,
                            d_kappa_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
     return hipGetLastError();
 }
@@ -438,10 +453,10 @@ hipError_t launch_diag_elem(cdfem_ctx *c, double *Ye)
     const int64_t n = (int64_t)c->nblk * c->nd * kLanes;
     if (c->dim == 3)
         hipLaunchKernelGGL(k_diag_elem<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_qd, c->nblk, c->nd, c->rule_op, c->kinds, c->ncomp, Ye);
+                           c->d_qd, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, c->rule_op, c->kinds, c->ncomp, Ye);
     else
         hipLaunchKernelGGL(k_diag_elem<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_qd, c->nblk, c->nd, c->rule_op, c->kinds, c->ncomp, Ye);
+                           c->d_qd, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, c->rule_op, c->kinds, c->ncomp, Ye);
     return hipGetLastError();
 }
 
@@ -450,10 +465,10 @@ hipError_t launch_lf_elem(cdfem_ctx *c, const double *d_fq, double *Ye)
     const int64_t n = (int64_t)c->nblk * c->nd * kLanes;
     if (c->dim == 3)
         hipLaunchKernelGGL(k_lf_elem<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->rule_lf, d_fq, Ye);
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, c->rule_lf, d_fq, Ye);
     else
         hipLaunchKernelGGL(k_lf_elem<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->rule_lf, d_fq, Ye);
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, c->rule_lf, d_fq, Ye);
     return hipGetLastError();
 }
 
@@ -498,7 +513,7 @@ static hipError_t apply_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, 
 
 bool apply_supported(int dim, int p)
 {
-    if (dim == 3) return p == 1 || p == 2;
+    if (dim == 3) return p >= 1 && p <= 4;  // p = 3, 4: wave per element (ho_kernels.hip)
     if (dim == 2) return p >= 1 && p <= 4;
     return false;
 }
@@ -510,6 +525,7 @@ hipError_t launch_apply_st(cdfem_ctx *c, const double *x, double *Ye, bool con, 
     if (c->dim == 3) {
         if (c->p == 1 && q1 == 3) return apply_dq<3, 2, 3>(c, x, Ye, con, st);
         if (c->p == 2 && q1 == 4) return apply_dq<3, 3, 4>(c, x, Ye, con, st);
+        if (c->p >= 3) return launch_apply_wpe(c, x, Ye, con, st);
     } else {
         if (c->p == 1 && q1 == 2) return apply_dq<2, 2, 2>(c, x, Ye, con, st);
         if (c->p == 2 && q1 == 3) return apply_dq<2, 3, 3>(c, x, Ye, con, st);

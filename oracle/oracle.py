@@ -327,6 +327,19 @@ def mms_u(prm, xyz):
     return out
 
 
+def mms_f(prm, xyz):
+    """Forcing of the manufactured solution at points (orc_mms_f), shape (..., dim) -> (...)."""
+    xyz = np.asarray(xyz, dtype=np.float64)
+    pts = xyz.reshape(-1, xyz.shape[-1])
+    out = np.zeros(len(pts))
+    L = lib()
+    for i, x in enumerate(pts):
+        xx = np.zeros(3)
+        xx[: len(x)] = x
+        out[i] = L.orc_mms_f(_d(prm), _d(xx))
+    return out.reshape(xyz.shape[:-1])
+
+
 def lf_assemble(mesh: BoxMesh, prm):
     b = np.zeros(mesh.nl)
     lib().orc_lf_assemble(mesh.dim, mesh.p, mesh.ne, _d(mesh.verts), _i(mesh.dofmap), mesh.nl,

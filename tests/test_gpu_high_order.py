@@ -1,0 +1,111 @@
+"""GPU high-order hex path (3D p = 3, 4: wave-per-element kernel, element-major layout; BASELINE
+config C3 is 128^3 at p = 4) against the oracle, same parity ladder as tests/test_gpu_parity.py:
+Mult / diagonal / linear form to 1e-13, fixed CG iterates to 1e-11, MMS error to 1e-6 relative.
+At a full-size-class mesh (32^3, p = 4: 2.1 M DoFs) size-independent properties are checked.
+"""
+import numpy as np
+import pytest
+
+import cdfem
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+C3 = (1.0, -2.0, 0.5)
+
+
+def _kinds_o(k):
+    return (O.DIFFUSION if k & 1 else 0) | (O.CONVECTION if k & 2 else 0) | (O.MASS if k & 4 else 0)
+
+
+def _pair(gpu_ctx, n, p, pert, kinds):
+    om = O.BoxMesh(3, n, p, perturb=pert)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    gpu_ctx.upload_mesh(gm)
+    gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(kinds))
+    return om, A
+
+
+@pytest.mark.parametrize("n,p,pert", [(2, 3, 0.1), (3, 3, 0.0), (2, 4, 0.15), (3, 4, 0.1), (5, 4, 0.0)])
+@pytest.mark.parametrize("kinds", [7, 5, 1, 2, 4])
+def test_ho_mult_parity(gpu_ctx, n, p, pert, kinds):
+    om, A = _pair(gpu_ctx, n, p, pert, kinds)
+    x = np.random.default_rng(13).uniform(-1, 1, om.nl)
+    yo = A.mult(x)
+    assert np.abs(gpu_ctx.mult(x) - yo).max() <= 1e-13 * np.abs(yo).max()
+    xz = x.copy()
+    xz[om.ess] = 0.0
+    yc = A.mult(xz)
+    yc[om.ess] = x[om.ess]
+    assert np.abs(gpu_ctx.mult(x, constrained=True) - yc).max() <= 1e-13 * np.abs(yc).max()
+
+
+@pytest.mark.parametrize("n,p", [(2, 3), (3, 4)])
+def test_ho_diagonal_and_lf(gpu_ctx, n, p):
+    om, A = _pair(gpu_ctx, n, p, 0.1, 7)
+    d = gpu_ctx.diagonal()
+    assert np.abs(d - A.diag()).max() <= 1e-13 * np.abs(A.diag()).max()
+    prm = O.mms_params(O.MMS_SIN, 3, kappa=0.1, s=1.0, c=C3, p=p)
+    xyz = gpu_ctx.quadrature_points(cdfem.RULE_LINEARFORM)
+    b = gpu_ctx.lf_assemble(O.mms_f(prm, xyz).reshape(-1))
+    bo = O.lf_assemble(om, prm)
+    assert np.abs(b - bo).max() <= 1e-12 * np.abs(bo).max()
+
+
+def test_ho_cg_parity(gpu_ctx):
+    om, A = _pair(gpu_ctx, 3, 4, 0.1, 5)
+    rng = np.random.default_rng(2)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    assert np.abs(B - Bo).max() <= 1e-13 * np.abs(Bo).max()
+    xo, io = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=50)
+    xg, ig = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=50, check_every=11)
+    assert io["iterations"] == ig["iterations"] == 50
+    assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
+    xo, io = O.gmres(Ac, Bo, dinv=1.0 / Ac.diag(), restart=30, rtol=1e-10, atol=1e-12, max_it=500)
+    om2, A2 = _pair(gpu_ctx, 3, 4, 0.1, 5)
+    _, B2 = gpu_ctx.form_linear_system(u, b)
+    xg, ig = gpu_ctx.solve(B2, method="gmres", restart=30, rel_tol=1e-10, abs_tol=1e-12, max_iter=500)
+    assert io["converged"] and ig["converged"] and abs(io["iterations"] - ig["iterations"]) <= 1
+    assert np.linalg.norm(xg - xo) <= 1e-8 * np.linalg.norm(xo)
+
+
+def test_ho_mms_error_matches_oracle(gpu_ctx):
+    n, p = 3, 4
+    om = O.BoxMesh(3, n, p)
+    prm = O.mms_params(O.MMS_SIN, 3, kappa=0.1, s=1.0, c=C3, modes=(1, 1, 1), p=p)
+    Xo, io, eo = O.solve_mms(om, prm, kappa=0.1, s=1.0, c=C3, solver="gmres", tol=1e-12, atol=1e-14)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    gpu_ctx.upload_mesh(gm)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    xyz = gpu_ctx.quadrature_points(cdfem.RULE_LINEARFORM)
+    b = gpu_ctx.lf_assemble(O.mms_f(prm, xyz).reshape(-1))
+    u = np.zeros(om.nl)
+    u[om.ess] = O.mms_u(prm, om.dof_coords()[om.ess])
+    _, B = gpu_ctx.form_linear_system(u, b)
+    X, ig = gpu_ctx.solve(B, method="gmres", restart=30, rel_tol=1e-12, abs_tol=1e-14, max_iter=2000)
+    assert ig["converged"]
+    eg = O.l2_error(om, X, prm)
+    assert abs(eg - eo) <= 1e-6 * eo
+
+
+def test_ho_full_size_properties(gpu_ctx):
+    """32^3 hexes at p = 4 (2,146,689 DoFs): constants in the kernel of D + C, mass total = volume,
+    linearity, the diffusion form symmetric, bitwise-reproducible Mult."""
+    m = cdfem.box_mesh(3, 32, 4, perturb=0.1, with_coords=False)
+    gpu_ctx.upload_mesh(m)
+    one = np.ones(m.nl)
+    gpu_ctx.pa_setup(kinds=3, kappa=0.1, alpha=1.0, conv=C3)
+    assert np.abs(gpu_ctx.mult(one)).max() <= 1e-12
+    gpu_ctx.pa_setup(kinds=4, mass=1.0)
+    assert abs(one @ gpu_ctx.mult(one) - 1.0) <= 1e-11
+    gpu_ctx.pa_setup(kinds=1, kappa=1.0)
+    rng = np.random.default_rng(5)
+    x, y = rng.uniform(-1, 1, m.nl), rng.uniform(-1, 1, m.nl)
+    Kx, Ky = gpu_ctx.mult(x), gpu_ctx.mult(y)
+    assert abs(x @ Ky - y @ Kx) <= 1e-11 * abs(x @ Ky)
+    assert np.abs(gpu_ctx.mult(2.0 * x - 3.0 * y) - (2.0 * Kx - 3.0 * Ky)).max() <= 1e-12 * np.abs(Kx).max()
+    np.testing.assert_array_equal(gpu_ctx.mult(x), Kx)
