@@ -38,9 +38,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=64, help="elements per direction (per-rank slab depth)")
-    ap.add_argument("--order", type=int, default=2)
-    ap.add_argument("--cg-iters", type=int, default=100)
+    ap.add_argument("--n", type=int, default=None, help="elements per direction (per-rank slab depth); "
+                    "default 64 (c2) / 128 (c3)")
+    ap.add_argument("--order", type=int, default=None, help="default 2 (c2) / 4 (c3)")
+    ap.add_argument("--cg-iters", type=int, default=None, help="default 100 (c2) / 20 (c3)")
     ap.add_argument("--kinds", type=int, default=7, help="1 diffusion | 2 convection | 4 mass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gmres-iters", type=int, default=60,
@@ -51,16 +52,22 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes of the apply kernel from a rocprofv3 --pmc pass")
     ap.add_argument("--no-profile-events", action="store_true")
-    ap.add_argument("--path", choices=["brick", "generic"], default="brick",
+    ap.add_argument("--path", choices=["brick", "generic"], default=None,
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
-    ap.add_argument("--config", choices=["c2", "c4"], default="c2",
-                    help="c2: 64^3 hex p=2 PA + CG (BASELINE metric config); c4: Kuhn 55^3 x 6 tets P2, "
-                         "FA CSR + GMRES(30)/Jacobi (BASELINE configs[3])")
+    ap.add_argument("--config", choices=["c2", "c3", "c4"], default="c2",
+                    help="c2: 64^3 hex p=2 PA + CG (BASELINE metric config); c3: 128^3 hex p=4 PA + CG "
+                         "(configs[2]); c4: Kuhn 55^3 x 6 tets P2, FA CSR + GMRES(30)/Jacobi (configs[3])")
     ap.add_argument("--tet-n", type=int, default=55, help="c4: cubes per direction (6 tets each)")
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N>1 data-path communicator: rccl (production, one GPU per rank) or host "
                          "(gloo callbacks; rehearses the N>1 flow with several ranks on one GPU)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c3 = a.config == "c3"
+    a.n = a.n or (128 if c3 else 64)
+    a.order = a.order or (4 if c3 else 2)
+    a.cg_iters = a.cg_iters or (20 if c3 else 100)
+    a.path = a.path or ("brick" if a.order <= 2 else "generic")
+    return a
 
 
 def dist_setup(args):
@@ -91,11 +98,15 @@ def allmax(pg, v):
 
 
 def cpu_baseline(args, n, p, kinds):
-    """Oracle (C restatement of the reference's CPU FA path) timed on this host's cores."""
+    """Oracle (C restatement of the reference's CPU FA path) timed on this host's cores.  For p >= 3
+    the FA matrix of the full mesh is out of reach of the CPU (729-wide rows at p = 4), so the
+    sample is a 12^3 mesh of the same order (throughput per DoF-iteration is the reported unit)."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     O.set_threads(threads)
+    if p >= 3:
+        n = min(n, 12)
     m = O.BoxMesh(3, n, p)
     t0 = time.perf_counter()
     ok = (O.DIFFUSION if kinds & 1 else 0) | (O.CONVECTION if kinds & 2 else 0) | (O.MASS if kinds & 4 else 0)
@@ -195,7 +206,7 @@ def main_c4(args):
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(bytes_ / per / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(bytes_ / per / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "k_spmv (CSR SpMV on the eliminated FA matrix)",
+                    "kernel": "k_sell_spmv (SELL-64 SpMV on the eliminated FA matrix)",
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2), "launches": cnt,
                     "other_kernels_avg_us": {"gmres_orth": round(o_ms / max(o_cnt, 1) * 1e3, 2)}}
     rp, _, _ = ctx.fa_csr()
@@ -234,8 +245,8 @@ def main():
     ndev = cdfem.device_count()
     ctx = cdfem.Context(local % ndev if args.comm == "host" else local)
     ctx.upload_mesh(mesh)
-    if args.path == "brick":
-        ctx.set_structured(n, n, n)
+    if args.path == "brick" or p >= 3:
+        ctx.set_structured(n, n, n)  # p >= 3: structured E->L (no position arrays)
     if world > 1:
         if args.path != "brick":
             raise SystemExit("multi-GPU runs use the structured brick path")
@@ -309,6 +320,7 @@ def main():
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": ("k_brick_cg (brick patch gather + D/C/M PA apply + in-LDS E->L + d.Ad)" if args.path == "brick"
+                               else "k_apply3d_wpe (wave per element, LDS sum factorization)" if args.order >= 3
                                else "k_apply3d (fused L->E gather + D/C/M PA apply)"),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
                     "launches": cnt,

@@ -641,7 +641,6 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
 {
     return guarded(c, [&] {
         if (c->mesh_ready && c->geom != 0) throw ArgError("structured bricks need a hexahedral mesh");
-        if (c->mesh_ready && c->qlay != 0) throw UnsupportedError("structured bricks are built for p <= 2");
         require_mesh(c);
         if (c->dim != 3) throw UnsupportedError("structured fast path is 3D only");
         if (nx < 1 || ny < 1 || nz < 1 || (int64_t)nx * ny * nz != c->ne)
@@ -661,6 +660,11 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
         }
         c->sx = nx; c->sy = ny; c->sz = nz;
         c->Lx = Lx; c->Ly = Ly; c->Lz = Lz;
+        if (c->qlay == 1) {
+            // high order: keep the element-major layout; the E->L sum uses the lattice (k_e2l_box)
+            c->structured = true;
+            return CDFEM_OK;
+        }
         c->nbx = (nx + kBrick - 1) / kBrick;
         c->nby = (ny + kBrick - 1) / kBrick;
         c->nbz = (nz + kBrick - 1) / kBrick;
@@ -692,6 +696,7 @@ int cdfem_set_slab(cdfem_ctx *c, int zlo_shared, int zhi_shared)
 {
     return guarded(c, [&] {
         if (!c->structured) throw StateError("cdfem_mesh_set_structured must precede cdfem_set_slab");
+        if (!use_brick(c)) throw UnsupportedError("multi-rank slabs use the structured brick path (3D, p <= 2)");
         if ((zlo_shared || zhi_shared) && !c->comm) throw StateError("attach a communicator first");
         c->zlo_shared = zlo_shared != 0;
         c->zhi_shared = zhi_shared != 0;

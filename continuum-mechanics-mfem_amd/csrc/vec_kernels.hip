@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "cdfem_internal.hpp"
+#include "pa_core.hpp"
 #include "reduce.hpp"
 
 namespace cdfem {
@@ -37,6 +38,77 @@ k_e2l(const int32_t *__restrict__ off, const int32_t *__restrict__ pos,
             v = 0.0;
             const int k1 = off[i + 1];
             for (int k = off[i]; k < k1; ++k) v += Ye[pos[k]];
+        }
+        y[i] = v;
+        if (CG) acc += v * x[i];
+    }
+    if (!CG) return;
+    store_partial(block_sum(acc, sh), part);
+}
+
+// ------------------------------------------------------------------------------------------------
+// E->L on a structured box with the element-major E-vector (3D, p >= 3): the (element, local dof)
+// pairs of a dof follow from its lattice coordinates, so no position arrays are read.  Per axis a
+// lattice coordinate g lies in one element (interior) or two (element boundary); the pairs are
+// visited z-outer / x-inner = ascending element index, the order of the generic k_e2l, so both
+// give bitwise-identical sums.
+// ------------------------------------------------------------------------------------------------
+struct BoxE2L {
+    FastDiv fLx, fLxy;
+    uint32_t Lx, Ly, nx, ny, nz;
+};
+
+template <int P>
+__device__ __forceinline__ int axis_pairs(uint32_t g, uint32_t n, int *el, int *lo)
+{
+    const int e = (int)(g / P), l = (int)(g % P);
+    if (l != 0) {
+        el[0] = e;
+        lo[0] = l;
+        return 1;
+    }
+    int k = 0;
+    if (e > 0) {
+        el[k] = e - 1;
+        lo[k++] = P;
+    }
+    if (e < (int)n) {
+        el[k] = e;
+        lo[k++] = 0;
+    }
+    return k;
+}
+
+template <bool CON, bool CG, int P>
+__global__ void __launch_bounds__(kRedThreads)
+k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__restrict__ Ye,
+          const double *__restrict__ x, double *__restrict__ y, int64_t nl, double *__restrict__ part,
+          KrylovState *__restrict__ st)
+{
+    constexpr int D1 = P + 1, ND = D1 * D1 * D1;
+    __shared__ double sh[kRedThreads / 64];
+    if (CG && st->done) return;
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
+        double v;
+        if (CON && ess[i]) {
+            v = x[i];
+        } else {
+            const uint32_t ii = (uint32_t)i;
+            const uint32_t gz = fdiv(ii, bx.fLxy), rem = ii - gz * bx.Lx * bx.Ly;
+            const uint32_t gy = fdiv(rem, bx.fLx), gx = rem - gy * bx.Lx;
+            int ex[2], lx[2], ey[2], ly[2], ez[2], lz[2];
+            const int nxp = axis_pairs<P>(gx, bx.nx, ex, lx);
+            const int nyp = axis_pairs<P>(gy, bx.ny, ey, ly);
+            const int nzp = axis_pairs<P>(gz, bx.nz, ez, lz);
+            v = 0.0;
+            for (int a = 0; a < nzp; ++a)
+                for (int b = 0; b < nyp; ++b)
+                    for (int c = 0; c < nxp; ++c) {
+                        const int64_t e = ex[c] + (int64_t)bx.nx * (ey[b] + (int64_t)bx.ny * ez[a]);
+                        v += Ye[e * ND + lx[c] + D1 * (ly[b] + D1 * lz[a])];
+                    }
         }
         y[i] = v;
         if (CG) acc += v * x[i];
@@ -293,9 +365,41 @@ hipError_t launch_update_fin(cdfem_ctx *c, int nparts)
     return hipGetLastError();
 }
 
+template <int P>
+static hipError_t launch_e2l_box(cdfem_ctx *c, const double *Ye, const double *x, double *y, bool con, int cg_mode)
+{
+    const dim3 g(red_grid(c, c->nl)), b(kRedThreads);
+    BoxE2L bx;
+    bx.Lx = (uint32_t)c->Lx;
+    bx.Ly = (uint32_t)c->Ly;
+    bx.nx = (uint32_t)c->sx;
+    bx.ny = (uint32_t)c->sy;
+    bx.nz = (uint32_t)c->sz;
+    bx.fLx = make_fastdiv(bx.Lx);
+    bx.fLxy = make_fastdiv(bx.Lx * bx.Ly);
+    if (cg_mode) {
+        hipLaunchKernelGGL((k_e2l_box<true, true, P>), g, b, 0, c->stream, bx, c->d_ess, Ye, x, y, c->nl, c->d_part,
+                           c->d_state);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return launch_den_fin(c, (int)g.x);
+    }
+    if (con)
+        hipLaunchKernelGGL((k_e2l_box<true, false, P>), g, b, 0, c->stream, bx, c->d_ess, Ye, x, y, c->nl, c->d_part,
+                           c->d_state);
+    else
+        hipLaunchKernelGGL((k_e2l_box<false, false, P>), g, b, 0, c->stream, bx, c->d_ess, Ye, x, y, c->nl,
+                           c->d_part, c->d_state);
+    return hipGetLastError();
+}
+
 hipError_t launch_e2l(cdfem_ctx *c, const double *Ye, const double *x, double *y, bool con,
                       int cg_mode)
 {
+    if (c->structured && c->qlay == 1 && c->nl < ((int64_t)1 << 32)) {
+        if (c->p == 3) return launch_e2l_box<3>(c, Ye, x, y, con, cg_mode);
+        if (c->p == 4) return launch_e2l_box<4>(c, Ye, x, y, con, cg_mode);
+    }
     const dim3 g(red_grid(c, c->nl)), b(kRedThreads);
     if (cg_mode) {
         hipLaunchKernelGGL((k_e2l<true, true>), g, b, 0, c->stream, c->d_e2l_off, c->d_e2l_pos,

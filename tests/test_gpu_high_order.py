@@ -52,6 +52,24 @@ def test_ho_diagonal_and_lf(gpu_ctx, n, p):
     assert np.abs(b - bo).max() <= 1e-12 * np.abs(bo).max()
 
 
+@pytest.mark.parametrize("n,p", [(3, 3), (4, 4)])
+def test_ho_structured_e2l_bitwise(gpu_ctx, n, p):
+    """cdfem_mesh_set_structured at p >= 3 switches to the lattice E->L (k_e2l_box): same sums,
+    same order as the generic position-array E->L -> bitwise-identical results."""
+    m = cdfem.box_mesh(3, n, p, perturb=0.1)
+    x = np.random.default_rng(21).uniform(-1, 1, m.nl)
+    gpu_ctx.upload_mesh(m)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    y0, yc0, d0 = gpu_ctx.mult(x), gpu_ctx.mult(x, constrained=True), gpu_ctx.diagonal()
+    gpu_ctx.upload_mesh(m).set_structured(n, n, n)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    np.testing.assert_array_equal(gpu_ctx.mult(x), y0)
+    np.testing.assert_array_equal(gpu_ctx.mult(x, constrained=True), yc0)
+    np.testing.assert_array_equal(gpu_ctx.diagonal(), d0)
+    om = O.BoxMesh(3, n, p, perturb=0.0)
+    assert np.array_equal(om.dofmap, m.dofmap)
+
+
 def test_ho_cg_parity(gpu_ctx):
     om, A = _pair(gpu_ctx, 3, 4, 0.1, 5)
     rng = np.random.default_rng(2)
