@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Turn a tools/profile_round.sh output directory into the committed profile artifacts.
 
-  python tools/pmc_summary.py gpurun_out/prof_r01 r01
+  python tools/pmc_summary.py gpurun_out/prof_r01_c2 r01_c2
 
 writes profiles/<tag>_kernel_stats.csv   (rocprofv3 --kernel-trace --stats of the bench command)
        profiles/<tag>_bench.json         (the bench line of the same round)
        profiles/<tag>_pmc.json           (per-kernel HBM bytes per launch, corrected)
-       profiles/pmc_traffic.json         (the apply kernel's entry, read by bench.py -> roofline.traffic)
+       profiles/pmc_traffic.json         (the roofline kernel's entry, read by bench.py -> roofline.traffic;
+                                          key n{n}_p{p}_k{kinds} for the hex configs, c4_n{n}_p2 for C4)
 
 Correction (MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE reports 1/2 of the bytes actually read.  The factor is not assumed but
@@ -33,7 +34,13 @@ def per_kernel(path):
     out = collections.defaultdict(list)
     for d, v in agg.items():
         out[name[d]].append(v)
-    return {k: (sum(v) / len(v), len(v)) for k, v in out.items()}
+    res = {}
+    for k, v in out.items():
+        # Krylov kernels queued past convergence exit at entry (device done flag): ~0 bytes; they
+        # are not launches of the measured work, so they are left out of the per-launch average
+        big = [x for x in v if x > 0.01 * max(v)] if max(v) > 0 else v
+        res[k] = (sum(big) / len(big), len(big))
+    return res
 
 
 def main():
@@ -59,7 +66,8 @@ def main():
                       "hbm_bytes_per_launch": round(fb + wb)}
     cfg = bench["config"]
     alg = bench["roofline"]["algorithmic_bytes_per_launch"]
-    apply = kernels["k_brick_cg"] if cfg.get("path") == "brick" else kernels["k_apply3d"]
+    kname = bench["roofline"]["kernel"].split()[0]
+    apply = next(v for k, v in kernels.items() if k.split("<")[0] == kname)
     pmc = {"tag": tag, "fetch_correction": f_corr, "write_correction": w_corr,
            "calibration": "k_stream_read (1 GiB read) / k_stream_copy (1 GiB write)",
            "workload": cfg["workload"], "kernels": kernels,
@@ -69,11 +77,16 @@ def main():
     json.dump(pmc, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
     p = os.path.join(prof, "pmc_traffic.json")
     tj = json.load(open(p)) if os.path.exists(p) else {}
-    n = int(cfg["workload"].split("x")[0])
-    order = int(cfg["workload"].split("p=")[1].split(",")[0])
-    kinds = int(cfg["workload"].split("kinds=")[1].split(")")[0])
-    tj[f"n{n}_p{order}_k{kinds}"] = {"hbm_bytes_per_launch": apply["hbm_bytes_per_launch"], "round": tag,
-                                     "path": cfg.get("path"), "source": f"profiles/{tag}_pmc.json"}
+    wl = cfg["workload"]
+    if wl.startswith("C4"):
+        key = f"c4_n{int(wl.split('Kuhn ')[1].split('^')[0])}_p2"
+    else:
+        n = int(wl.split("x")[0])
+        order = int(wl.split("p=")[1].split(",")[0])
+        kinds = int(wl.split("kinds=")[1].split(")")[0])
+        key = f"n{n}_p{order}_k{kinds}"
+    tj[key] = {"hbm_bytes_per_launch": apply["hbm_bytes_per_launch"], "round": tag,
+                                     "kernel": kname, "source": f"profiles/{tag}_pmc.json"}
     json.dump(tj, open(p, "w"), indent=1)
     print(json.dumps(pmc["apply_kernel"]), f_corr, w_corr)
 

@@ -1,17 +1,24 @@
 #!/bin/bash
-# Round profile: bench line (with CPU baseline), rocprofv3 kernel stats of the same bench command,
-# PMC HBM traffic passes (FETCH_SIZE, WRITE_SIZE) with stream-probe calibration.
+# Round profile of one bench configuration:
+#   bench line (with CPU baseline), rocprofv3 kernel stats of the same bench command, and
+#   PMC HBM traffic passes (FETCH_SIZE, WRITE_SIZE) plus the stream-probe calibration pass.
+# usage: bash tools/profile_round.sh TAG [c2|c3|c4]
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=${1:-r01}
-OUT=gpurun_out/prof_$TAG
+CFG=${2:-c2}
+OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p $OUT
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline"
-timeout -k 10 900 python bench.py --steps 5 --warmup 1 > $OUT/bench.json 2> $OUT/bench.err || exit $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/stats -o run --output-format csv -- python3 bench.py $ARGS --no-profile-events > $OUT/stats.log 2>&1 || exit $?
+case $CFG in
+  c2) SHORT="--cg-iters 20";;
+  c3) SHORT="--cg-iters 4 --gmres-iters 0";;
+  c4) SHORT="--gmres-iters 30";;
+esac
+timeout -k 10 900 python bench.py --config $CFG --steps 5 --warmup 1 > $OUT/bench.json 2> $OUT/bench.err || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/stats -o run --output-format csv -- python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-profile-events > $OUT/stats.log 2>&1 || exit $?
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace -T -d $OUT/pmc_$C -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --cg-iters 20 --no-cpu-baseline --no-profile-events > $OUT/pmc_$C.log 2>&1 || exit $?
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace -T -d $OUT/pmc_$C -o run --output-format csv -- python3 bench.py --config $CFG --steps 1 --warmup 0 $SHORT --no-cpu-baseline --no-profile-events > $OUT/pmc_$C.log 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace -T -d $OUT/calib_$C -o run --output-format csv -- python3 tools/calib.py > $OUT/calib_$C.log 2>&1 || exit $?
 done
 exit 0
