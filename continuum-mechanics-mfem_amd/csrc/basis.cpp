@@ -6,6 +6,7 @@
 // tensor elements: Diffusion 2p+dim-1, Convection (dim-1)+(p-1)+p+(dim-1),
 // Mass 2p+dim-1 -> one shared n = order/2+1 for the fused operator; DomainLF 2p; the driver's
 // L2-error rule max(2, 2p+3) (:383).
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <vector>
@@ -154,7 +155,77 @@ int simplex_rule(int dim, int n, std::vector<double> &xi, std::vector<double> &w
     return nq;
 }
 
-int simplex_ndofs(int dim, int p) { return p == 1 ? dim + 1 : (dim + 1) * (dim + 2) / 2; }
+int simplex_ndofs(int dim, int p)
+{
+    if (p == 1) return dim + 1;
+    if (p == 2) return (dim + 1) * (dim + 2) / 2;
+    if (p == 3 && dim == 2) return 10;
+    return -1;
+}
+
+// P3 triangle (H1_FECollection(3, 2), GaussLobatto nodes): vertices, 2 nodes per edge at the
+// interior GLL points t = (1 -+ 1/sqrt(5)) / 2 along a -> b for the edges (0,1), (0,2), (1,2),
+// and the centroid.  Nodal basis = monomials x^i y^j (i + j <= 3) times the inverse Vandermonde
+// matrix, formed once.
+double p3_edge_t(int k) { return k == 0 ? 0.5 * (1.0 - 1.0 / std::sqrt(5.0)) : 0.5 * (1.0 + 1.0 / std::sqrt(5.0)); }
+
+void p3_tri_nodes(double (*X)[2])
+{
+    const double V[3][2] = {{0, 0}, {1, 0}, {0, 1}};
+    for (int v = 0; v < 3; ++v) { X[v][0] = V[v][0]; X[v][1] = V[v][1]; }
+    for (int e = 0; e < 3; ++e)
+        for (int k = 0; k < 2; ++k) {
+            const int a = kTriEdge[e][0], b = kTriEdge[e][1];
+            const double t = p3_edge_t(k);
+            for (int d = 0; d < 2; ++d) X[3 + 2 * e + k][d] = V[a][d] + t * (V[b][d] - V[a][d]);
+        }
+    X[9][0] = X[9][1] = 1.0 / 3.0;
+}
+
+static void p3_monomials(const double *x, double *m, double *mx, double *my)
+{
+    int k = 0;
+    for (int tot = 0; tot <= 3; ++tot)
+        for (int j = 0; j <= tot; ++j, ++k) {
+            const int i = tot - j;  // x^i y^j
+            m[k] = std::pow(x[0], i) * std::pow(x[1], j);
+            mx[k] = i > 0 ? i * std::pow(x[0], i - 1) * std::pow(x[1], j) : 0.0;
+            my[k] = j > 0 ? j * std::pow(x[0], i) * std::pow(x[1], j - 1) : 0.0;
+        }
+}
+
+static const std::vector<double> &p3_coeffs()
+{
+    static const std::vector<double> C = [] {
+        double X[10][2];
+        p3_tri_nodes(X);
+        double A[10][20] = {};
+        for (int r = 0; r < 10; ++r) {  // V[r][c] = m_c(node_r), augmented with I
+            double m[10], mx[10], my[10];
+            p3_monomials(X[r], m, mx, my);
+            for (int c = 0; c < 10; ++c) A[r][c] = m[c];
+            A[r][10 + r] = 1.0;
+        }
+        for (int c = 0; c < 10; ++c) {  // Gauss-Jordan, partial pivoting
+            int piv = c;
+            for (int r = c + 1; r < 10; ++r)
+                if (std::fabs(A[r][c]) > std::fabs(A[piv][c])) piv = r;
+            for (int k = 0; k < 20; ++k) std::swap(A[c][k], A[piv][k]);
+            const double d = A[c][c];
+            for (int k = 0; k < 20; ++k) A[c][k] /= d;
+            for (int r = 0; r < 10; ++r)
+                if (r != c) {
+                    const double f = A[r][c];
+                    for (int k = 0; k < 20; ++k) A[r][k] -= f * A[c][k];
+                }
+        }
+        std::vector<double> out(100);  // out[c * 10 + i] = (V^-1)[c][i]: phi_i = sum_c m_c out[c][i]
+        for (int c = 0; c < 10; ++c)
+            for (int i = 0; i < 10; ++i) out[c * 10 + i] = A[c][10 + i];
+        return out;
+    }();
+    return C;
+}
 
 // Local order: vertices, then edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3) [2D (0,1),(0,2),(1,2)].
 const int kSimplexEdge[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
@@ -162,6 +233,23 @@ const int kTriEdge[3][2] = {{0, 1}, {0, 2}, {1, 2}};
 
 void simplex_basis(int dim, int p, const double *xi, double *phi, double *dphi)
 {
+    if (dim == 2 && p == 3) {
+        const std::vector<double> &C = p3_coeffs();
+        double m[10], mx[10], my[10];
+        p3_monomials(xi, m, mx, my);
+        for (int i = 0; i < 10; ++i) {
+            double v = 0.0, gx = 0.0, gy = 0.0;
+            for (int c = 0; c < 10; ++c) {
+                v += m[c] * C[c * 10 + i];
+                gx += mx[c] * C[c * 10 + i];
+                gy += my[c] * C[c * 10 + i];
+            }
+            phi[i] = v;
+            dphi[i * 2] = gx;
+            dphi[i * 2 + 1] = gy;
+        }
+        return;
+    }
     double lam[4], dl[4][3] = {};
     lam[0] = 1.0;
     for (int k = 0; k < dim; ++k) {

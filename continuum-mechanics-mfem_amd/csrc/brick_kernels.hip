@@ -331,9 +331,10 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // below, which owns it for the dot products (remote_lo / remote_hi carry the neighbours' partial
 // sums of the interface planes; nullptr on a single GPU).
 // ================================================================================================
-// VAR 0: elem_apply3d fully unrolled; 1: elem_apply3d, plane loop; 2: low-register core
+// VAR % 3 = element core: 0 elem_apply3d fully unrolled; 1 elem_apply3d, plane loop; 2 low-register
+// core.  VAR >= 3: the same cores compiled for 2 waves per SIMD (<= 256 registers).
 template <int D1, int Q1, unsigned K, int VAR>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, VAR >= 3 ? 2 : 1)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
@@ -385,9 +386,9 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
     const double *q0 = qd + (size_t)b * NQ * NC * kLanes;
     double Y[D1][D1][D1];
-    if constexpr (VAR == 2)
+    if constexpr (VAR % 3 == 2)
         elem_apply3d_lr<D1, Q1, K, decltype(xl), 1>(xl, q0, t, T, Y);
-    else if constexpr (VAR == 1)
+    else if constexpr (VAR % 3 == 1)
         elem_apply3d<D1, Q1, K, decltype(xl), 1>(xl, q0, t, T, Y);
     else
         elem_apply3d<D1, Q1, K, decltype(xl), Q1>(xl, q0, t, T, Y);
@@ -496,9 +497,14 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
 #define CDFEM_L(V)                                                                                  \
     hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, V>), dim3(c->nblk), dim3(64), 0, c->stream, r, dinv, d_old, \
                        d_new, q, c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state)
-    if (c->brick_variant == 2) CDFEM_L(2);
-    else if (c->brick_variant == 1) CDFEM_L(1);
-    else CDFEM_L(0);
+    switch (c->brick_variant) {
+    case 1: CDFEM_L(1); break;
+    case 2: CDFEM_L(2); break;
+    case 3: CDFEM_L(3); break;
+    case 4: CDFEM_L(4); break;
+    case 5: CDFEM_L(5); break;
+    default: CDFEM_L(0); break;
+    }
 #undef CDFEM_L
     return hipGetLastError();
 }

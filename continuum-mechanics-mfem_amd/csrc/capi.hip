@@ -93,7 +93,7 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_part); dfree(c->d_gm); dfree(c->d_gm_part);
     dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones); dfree(c->d_dalt);
     for (auto &b : c->d_if) dfree(b);
-    dfree(c->d_stab); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);
+    dfree(c->d_stab); dfree(c->d_stab_lf); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);
     dfree(c->d_cpos); dfree(c->d_vals); dfree(c->d_vals_c); dfree(c->d_Ee);
     dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_svals);
     dfree(c->d_svals_c);
@@ -103,6 +103,7 @@ void free_mesh(cdfem_ctx *c)
     c->nnz = 0;
     c->h_verts.clear();
     c->h_sxi.clear();
+    c->h_sxi_lf.clear();
     c->zlo_shared = c->zhi_shared = 0;
     c->gm_cap = 0;
     c->mesh_ready = c->pa_ready = c->dinv_ready = false;
@@ -717,8 +718,8 @@ int cdfem_rule_size(cdfem_ctx *c, int rule, int *nq)
         require_mesh(c);
         if (!nq) throw ArgError("nq is null");
         if (c->geom != 0) {
-            if (rule != CDFEM_RULE_OPERATOR) throw UnsupportedError("simplex meshes: operator rule only");
-            *nq = c->nq_simplex;
+            if (rule == CDFEM_RULE_ERROR) throw UnsupportedError("simplex meshes: operator / linear-form rules");
+            *nq = rule == CDFEM_RULE_OPERATOR ? c->nq_simplex : c->nq_lf;
             return CDFEM_OK;
         }
         const Rule1D &r = rule == CDFEM_RULE_OPERATOR ? c->rule_op
@@ -734,15 +735,16 @@ int cdfem_quadrature_points(cdfem_ctx *c, int rule, double *xyz, int where)
         require_mesh(c);
         if (!xyz) throw ArgError("xyz is null");
         if (c->geom != 0) {  // affine simplices: x = v0 + J xi, evaluated on the host
-            if (rule != CDFEM_RULE_OPERATOR) throw UnsupportedError("simplex meshes: operator rule only");
-            const int dim = c->dim, nv = dim + 1, nq = c->nq_simplex;
+            if (rule == CDFEM_RULE_ERROR) throw UnsupportedError("simplex meshes: operator / linear-form rules");
+            const std::vector<double> &sxi = rule == CDFEM_RULE_OPERATOR ? c->h_sxi : c->h_sxi_lf;
+            const int dim = c->dim, nv = dim + 1, nq = rule == CDFEM_RULE_OPERATOR ? c->nq_simplex : c->nq_lf;
             std::vector<double> out((size_t)c->ne * nq * dim);
             for (int e = 0; e < c->ne; ++e) {
                 const double *V = &c->h_verts[(size_t)e * nv * dim];
                 for (int q = 0; q < nq; ++q)
                     for (int k = 0; k < dim; ++k) {
                         double x = V[k];
-                        for (int m = 0; m < dim; ++m) x += (V[(m + 1) * dim + k] - V[k]) * c->h_sxi[(size_t)q * dim + m];
+                        for (int m = 0; m < dim; ++m) x += (V[(m + 1) * dim + k] - V[k]) * sxi[(size_t)q * dim + m];
                         out[((size_t)e * nq + q) * dim + k] = x;
                     }
             }
@@ -814,7 +816,7 @@ int cdfem_mesh_upload_simplex(cdfem_ctx *c, int dim, int order, int ne, const do
 {
     return guarded(c, [&] {
         if (dim != 2 && dim != 3) throw ArgError("dim must be 2 or 3");
-        if (order < 1 || order > 2) throw ArgError("simplex order must be 1 or 2");
+        if (order < 1 || order > (dim == 2 ? 3 : 2)) throw ArgError("simplex order: 1-3 (triangles), 1-2 (tets)");
         if (ne <= 0 || nldofs <= 0 || !elem_verts || !elem_dofs) throw ArgError("empty mesh");
         if (nldofs >= (int64_t)1 << 31) throw ArgError("nldofs exceeds int32 indexing");
         if (n_ess < 0 || (n_ess > 0 && !ess_dofs)) throw ArgError("bad essential list");
@@ -857,6 +859,31 @@ int cdfem_mesh_upload_simplex(cdfem_ctx *c, int dim, int order, int ne, const do
             }
             tab[(size_t)nq * nd * (dim + 1) + q] = w[q];
         }
+        // linear-form rule (n = p + 3) tables
+        std::vector<double> wl;
+        c->nq_lf = simplex_rule(dim, order + 3, c->h_sxi_lf, wl);
+        std::vector<double> tab_lf((size_t)c->nq_lf * (nd + 1));
+        for (int q = 0; q < c->nq_lf; ++q) {
+            double phi[10], dphi[30];
+            simplex_basis(dim, order, &c->h_sxi_lf[(size_t)q * dim], phi, dphi);
+            for (int i = 0; i < nd; ++i) tab_lf[(size_t)q * nd + i] = phi[i];
+            tab_lf[(size_t)c->nq_lf * nd + q] = wl[q];
+        }
+        // E->L transpose of the element-major E-vector (linear forms)
+        std::vector<int32_t> cnt(nldofs + 1, 0), pos((size_t)ne * nd);
+        for (int32_t g : c->h_dofs) cnt[g + 1]++;
+        for (int64_t i = 0; i < nldofs; ++i) cnt[i + 1] += cnt[i];
+        {
+            std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+            for (int64_t k = 0; k < (int64_t)ne * nd; ++k) pos[fill[c->h_dofs[k]]++] = (int32_t)k;
+        }
+        c->d_e2l_off = dalloc<int32_t>(nldofs + 1);
+        c->d_e2l_pos = dalloc<int32_t>(pos.size());
+        c->d_Ye = dalloc<double>(pos.size());
+        HIPCHK(hipMemcpyAsync(c->d_e2l_off, cnt.data(), (nldofs + 1) * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_e2l_pos, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, c->stream));
+        c->d_stab_lf = dalloc<double>(tab_lf.size());
+        HIPCHK(hipMemcpyAsync(c->d_stab_lf, tab_lf.data(), tab_lf.size() * 8, hipMemcpyHostToDevice, c->stream));
         c->d_stab = dalloc<double>(tab.size());
         c->d_verts = dalloc<double>(c->h_verts.size());
         c->d_ess = dalloc<uint8_t>(nldofs);
@@ -996,13 +1023,13 @@ int cdfem_lf_assemble(cdfem_ctx *c, const double *f_q, double *b, int where)
     return guarded(c, [&] {
         require_mesh(c);
         if (!f_q || !b) throw ArgError("null vector");
-        if (c->geom != 0) throw UnsupportedError("linear forms on simplex meshes are not available yet");
-        const size_t n = (size_t)c->ne * nq_of(c, c->rule_lf);
+        const size_t n = (size_t)c->ne * (c->geom != 0 ? c->nq_lf : nq_of(c, c->rule_lf));
         double *dfq = dalloc<double>(n);
         HIPCHK(hipMemcpyAsync(dfq, f_q, n * 8, where == CDFEM_DEVICE ? hipMemcpyDeviceToDevice
                                                                      : hipMemcpyHostToDevice, c->stream));
         double *db = where == CDFEM_DEVICE ? b : c->d_w[1];
-        HIPCHK(launch_lf_elem(c, dfq, c->d_Ye));
+        if (c->geom != 0) HIPCHK(launch_simplex_lf(c, dfq, c->d_Ye));
+        else HIPCHK(launch_lf_elem(c, dfq, c->d_Ye));
         HIPCHK(launch_e2l(c, c->d_Ye, nullptr, db, false, 0));
         dev_out(c, b, where, db, c->nl);
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -1065,8 +1092,9 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
 int cdfem_stream_bench(cdfem_ctx *c, int mode, size_t bytes, int reps, double *gbps)
 {
     return guarded(c, [&] {
-        if (!gbps || reps < 1 || mode < 0 || mode > 2) throw ArgError("bad stream bench arguments");
-        const int64_t n = (int64_t)(bytes / 16) * 2;
+        if (!gbps || reps < 1 || mode < 0 || mode > 9) throw ArgError("bad stream bench arguments");
+        int64_t n = (int64_t)(bytes / 16) * 2;
+        if (mode >= 3) n = n / 40960 * 40960;  // whole 320 KiB chunks
         double *a = dalloc<double>(n), *b = dalloc<double>(n);
         HIPCHK(hipMemsetAsync(a, 0, n * 8, c->stream));
         HIPCHK(hipMemsetAsync(b, 0, n * 8, c->stream));
@@ -1096,7 +1124,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         if (!key) throw ArgError("key is null");
         const std::string k(key);
         if (k == "brick_variant") {
-            if (value < 0 || value > 2) throw ArgError("brick_variant must be 0, 1 or 2");
+            if (value < 0 || value > 5) throw ArgError("brick_variant must be 0..5");
             c->brick_variant = value;
         } else if (k == "profile_mask") {
             c->prof_mask = (unsigned)value;

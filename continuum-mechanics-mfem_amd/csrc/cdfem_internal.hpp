@@ -43,6 +43,8 @@ int simplex_rule(int dim, int n, std::vector<double> &xi, std::vector<double> &w
 int simplex_ndofs(int dim, int p);
 void simplex_basis(int dim, int p, const double *xi, double *phi, double *dphi);
 extern const int kSimplexEdge[6][2];
+double p3_edge_t(int k);
+void p3_tri_nodes(double (*X)[2]);
 extern const int kTriEdge[3][2];
 Rule1D make_rule(int p, int q1);
 // MFEM default rule sizes on multilinear tensor elements (which: 0 operator, 1 LF, 2 L2 error)
@@ -130,6 +132,9 @@ struct cdfem_ctx {
     double *d_stab = nullptr;           // simplex rule tables: phi [nq][nd], dphi [nq][nd][dim], w [nq]
     std::vector<double> h_verts;        // simplex host geometry (quadrature points for coefficients)
     std::vector<double> h_sxi;          // simplex rule points (reference coordinates)
+    int nq_lf = 0;                      // simplex LINEARFORM rule (collapsed Gauss, n = p + 3)
+    std::vector<double> h_sxi_lf;
+    double *d_stab_lf = nullptr;        // phi [nq_lf][nd], w [nq_lf]
     // full assembly (cdfem_fa_setup): CSR with sorted columns + deterministic contribution lists
     bool fa_ready = false;
     int64_t nnz = 0;
@@ -256,6 +261,7 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, double kappa, double alpha, const double *conv,
                                const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);
+hipError_t launch_simplex_lf(cdfem_ctx *c, const double *fq, double *Ye);
 hipError_t launch_sell_fill(cdfem_ctx *c);
 hipError_t launch_csr_diag(cdfem_ctx *c, double *d);
 hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y);

@@ -180,7 +180,7 @@ k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *_
                double kappa, const double *__restrict__ kq, double alpha, double c0, double c1, double c2,
                const double *__restrict__ cq, double mass, const double *__restrict__ mq, double *__restrict__ Ee)
 {
-    constexpr int ND = P == 1 ? DIM + 1 : (DIM + 1) * (DIM + 2) / 2;
+    constexpr int ND = P == 1 ? DIM + 1 : P == 2 ? (DIM + 1) * (DIM + 2) / 2 : 10;
     const int e = blockIdx.x * 64 + threadIdx.x;
     if (e >= ne) return;
     const double *V = verts + (size_t)e * (DIM + 1) * DIM;
@@ -272,6 +272,38 @@ k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *_
     for (int i = 0; i < ND; ++i)
 #pragma unroll
         for (int j = 0; j < ND; ++j) Ee[base + (int64_t)(i * ND + j) * kLanes] = M[i][j];
+}
+
+// DomainLF on affine simplices: be_l = sum_q w_q det J f_q phi_l(q), element-major E-vector
+// (summed by k_e2l).  Tables: phi [nq][ND], w [nq] of the LINEARFORM rule.
+template <int DIM, int ND>
+__global__ void __launch_bounds__(64)
+k_simplex_lf(const double *__restrict__ verts, int ne, int nq, const double *__restrict__ tab,
+             const double *__restrict__ fq, double *__restrict__ Ye)
+{
+    const int e = blockIdx.x * 64 + threadIdx.x;
+    if (e >= ne) return;
+    const double *V = verts + (size_t)e * (DIM + 1) * DIM;
+    double det;
+    if constexpr (DIM == 3) {
+        double J[3][3];
+        for (int k = 0; k < 3; ++k)
+            for (int m = 0; m < 3; ++m) J[k][m] = V[(m + 1) * 3 + k] - V[k];
+        det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+              J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+    } else {
+        det = (V[2] - V[0]) * (V[5] - V[1]) - (V[4] - V[0]) * (V[3] - V[1]);
+    }
+    double b[ND];
+#pragma unroll
+    for (int l = 0; l < ND; ++l) b[l] = 0.0;
+    for (int q = 0; q < nq; ++q) {
+        const double f = tab[(size_t)nq * ND + q] * det * fq[(size_t)e * nq + q];
+#pragma unroll
+        for (int l = 0; l < ND; ++l) b[l] += f * tab[q * ND + l];
+    }
+#pragma unroll
+    for (int l = 0; l < ND; ++l) Ye[(size_t)e * ND + l] = b[l];
 }
 
 __global__ void __launch_bounds__(256)
@@ -372,8 +404,27 @@ hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, double kappa, dou
     else if (c->dim == 3 && c->p == 2) CDFEM_SIMPLEX(3, 2);
     else if (c->dim == 2 && c->p == 1) CDFEM_SIMPLEX(2, 1);
     else if (c->dim == 2 && c->p == 2) CDFEM_SIMPLEX(2, 2);
+    else if (c->dim == 2 && c->p == 3) CDFEM_SIMPLEX(2, 3);
     else return hipErrorInvalidValue;
 #undef CDFEM_SIMPLEX
+    return hipGetLastError();
+}
+
+hipError_t launch_simplex_lf(cdfem_ctx *c, const double *fq, double *Ye)
+{
+    const dim3 g((c->ne + 63) / 64), b(64);
+    if (c->dim == 3 && c->p == 1)
+        hipLaunchKernelGGL((k_simplex_lf<3, 4>), g, b, 0, c->stream, c->d_verts, c->ne, c->nq_lf, c->d_stab_lf, fq, Ye);
+    else if (c->dim == 3 && c->p == 2)
+        hipLaunchKernelGGL((k_simplex_lf<3, 10>), g, b, 0, c->stream, c->d_verts, c->ne, c->nq_lf, c->d_stab_lf, fq, Ye);
+    else if (c->dim == 2 && c->p == 1)
+        hipLaunchKernelGGL((k_simplex_lf<2, 3>), g, b, 0, c->stream, c->d_verts, c->ne, c->nq_lf, c->d_stab_lf, fq, Ye);
+    else if (c->dim == 2 && c->p == 2)
+        hipLaunchKernelGGL((k_simplex_lf<2, 6>), g, b, 0, c->stream, c->d_verts, c->ne, c->nq_lf, c->d_stab_lf, fq, Ye);
+    else if (c->dim == 2 && c->p == 3)
+        hipLaunchKernelGGL((k_simplex_lf<2, 10>), g, b, 0, c->stream, c->d_verts, c->ne, c->nq_lf, c->d_stab_lf, fq, Ye);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -11,6 +11,13 @@
 // essential.  This is the ParMesh / ParFiniteElementSpace element partition of the reference
 // (linear_convection_diffusion_2D.cpp:300) with a slab partitioner instead of METIS.
 #include <cmath>
+#include <vector>
+#include <string>
+#include <sstream>
+#include <map>
+#include <cstdio>
+#include <array>
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <utility>
@@ -259,6 +266,212 @@ int cdfem_kuhn_mesh(int dim, int n, int order, double perturb, double *elem_vert
         }
     }
     return inverted ? CDFEM_ERR_ARG : CDFEM_OK;
+}
+
+// ---- gmsh v2.2 ASCII meshes (the reference's inputs: Mesh/unit_square.msh, unit_circle.msh) ----
+// replaces: make_unique<Mesh>(params.mesh_file.c_str(), 1, 1) (linear_convection_diffusion_2D.cpp:290)
+// + H1_FECollection(order, dim) + ParFiniteElementSpace (:311-313) for simplex meshes.
+// Domain elements: triangles (2D) or tetrahedra (3D, when present); boundary elements: lines (2D) or
+// triangles (3D), physical tag = boundary attribute.  Numbering: vertex dofs in increasing gmsh node
+// id, then (order - 1) dofs per edge (edges in order of first appearance, dofs along the direction
+// of increasing vertex dof), then P3 triangle interiors.  Elements are re-oriented to det J > 0.
+namespace {
+
+struct Gmsh {
+    int dim = 0, order = 1, nv = 0, nd = 0;
+    std::vector<int32_t> dofs;       // ne * nd
+    std::vector<double> verts;       // ne * (dim + 1) * dim
+    std::vector<double> xyz;         // nl * dim
+    std::vector<int32_t> bmask;      // nl: bit (attr - 1) set on boundary elements of attribute attr
+    int64_t nl = 0;
+    int ne = 0;
+};
+
+bool read_gmsh(const char *path, int order, Gmsh &G, std::string &err)
+{
+    std::FILE *f = std::fopen(path, "r");
+    if (!f) { err = "cannot open mesh file"; return false; }
+    std::map<long, std::array<double, 3>> nodes;
+    struct El { int type, tag; std::vector<long> v; };
+    std::vector<El> els;
+    char line[4096];
+    while (std::fgets(line, sizeof line, f)) {
+        if (!std::strncmp(line, "$MeshFormat", 11)) {
+            double ver = 0; int ft = 0, ds = 0;
+            if (!std::fgets(line, sizeof line, f) || std::sscanf(line, "%lf %d %d", &ver, &ft, &ds) != 3 ||
+                ver < 2.0 || ver >= 3.0 || ft != 0) {
+                err = "only gmsh 2.x ASCII meshes are supported";
+                std::fclose(f);
+                return false;
+            }
+        } else if (!std::strncmp(line, "$Nodes", 6)) {
+            long n = 0;
+            if (!std::fgets(line, sizeof line, f) || std::sscanf(line, "%ld", &n) != 1) break;
+            for (long i = 0; i < n && std::fgets(line, sizeof line, f); ++i) {
+                long id; double x, y, z;
+                if (std::sscanf(line, "%ld %lf %lf %lf", &id, &x, &y, &z) == 4) nodes[id] = {x, y, z};
+            }
+        } else if (!std::strncmp(line, "$Elements", 9)) {
+            long n = 0;
+            if (!std::fgets(line, sizeof line, f) || std::sscanf(line, "%ld", &n) != 1) break;
+            for (long i = 0; i < n && std::fgets(line, sizeof line, f); ++i) {
+                std::istringstream ss(line);
+                long id; int type, ntags;
+                ss >> id >> type >> ntags;
+                std::vector<long> tags(ntags);
+                for (auto &t : tags) ss >> t;
+                const int nn = type == 1 ? 2 : type == 2 ? 3 : type == 4 ? 4 : type == 15 ? 1 : -1;
+                if (nn < 0) { err = "unsupported gmsh element type " + std::to_string(type); std::fclose(f); return false; }
+                El e{type, ntags > 0 ? (int)tags[0] : 1, std::vector<long>(nn)};
+                for (auto &v : e.v) ss >> v;
+                els.push_back(std::move(e));
+            }
+        }
+    }
+    std::fclose(f);
+    const bool has_tet = std::any_of(els.begin(), els.end(), [](const El &e) { return e.type == 4; });
+    const int dim = has_tet ? 3 : 2, dtype = has_tet ? 4 : 2, btype = has_tet ? 2 : 1;
+    if (order < 1 || order > (dim == 2 ? 3 : 2)) { err = "unsupported order for this mesh"; return false; }
+    G.dim = dim; G.order = order; G.nv = dim + 1; G.nd = cdfem::simplex_ndofs(dim, order);
+    // vertex dofs: nodes used by domain elements, increasing node id
+    std::map<long, int32_t> vdof;
+    for (const El &e : els)
+        if (e.type == dtype)
+            for (long v : e.v) vdof[v] = 0;
+    int32_t k = 0;
+    for (auto &kv : vdof) {
+        if (!nodes.count(kv.first)) { err = "element references an unknown node"; return false; }
+        kv.second = k++;
+    }
+    const int64_t nvd = k;
+    const int nedge_loc = dim == 3 ? 6 : 3, ne_dofs = order - 1;
+    std::map<std::pair<int32_t, int32_t>, int32_t> edge;  // (lo, hi) vertex dof -> edge index
+    std::vector<std::array<long, 4>> tv;
+    for (const El &e : els) {
+        if (e.type != dtype) continue;
+        std::array<long, 4> v{};
+        for (int i = 0; i <= dim; ++i) v[i] = e.v[i];
+        // orientation: det J > 0
+        const auto &a = nodes[v[0]], &b = nodes[v[1]], &c = nodes[v[2]];
+        double det;
+        if (dim == 2) {
+            det = (b[0] - a[0]) * (c[1] - a[1]) - (b[1] - a[1]) * (c[0] - a[0]);
+            if (det < 0) std::swap(v[1], v[2]);
+        } else {
+            const auto &d = nodes[v[3]];
+            const double J[3][3] = {{b[0] - a[0], c[0] - a[0], d[0] - a[0]},
+                                    {b[1] - a[1], c[1] - a[1], d[1] - a[1]},
+                                    {b[2] - a[2], c[2] - a[2], d[2] - a[2]}};
+            det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                  J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+            if (det < 0) std::swap(v[2], v[3]);
+        }
+        if (det == 0.0) { err = "degenerate element"; return false; }
+        tv.push_back(v);
+        if (ne_dofs > 0)
+            for (int ed = 0; ed < nedge_loc; ++ed) {
+                const int la = dim == 3 ? cdfem::kSimplexEdge[ed][0] : cdfem::kTriEdge[ed][0];
+                const int lb = dim == 3 ? cdfem::kSimplexEdge[ed][1] : cdfem::kTriEdge[ed][1];
+                int32_t ga = vdof[v[la]], gb = vdof[v[lb]];
+                if (ga > gb) std::swap(ga, gb);
+                edge.emplace(std::make_pair(ga, gb), (int32_t)edge.size());
+            }
+    }
+    G.ne = (int)tv.size();
+    if (G.ne == 0) { err = "mesh has no domain elements"; return false; }
+    // edge indices by first appearance (std::map emplace keeps the first index; renumber in order)
+    const int64_t nedges = (int64_t)edge.size();
+    const int64_t nint = (dim == 2 && order == 3) ? G.ne : 0;
+    G.nl = nvd + nedges * ne_dofs + nint;
+    G.dofs.assign((size_t)G.ne * G.nd, 0);
+    G.verts.assign((size_t)G.ne * G.nv * dim, 0.0);
+    G.xyz.assign((size_t)G.nl * dim, 0.0);
+    G.bmask.assign(G.nl, 0);
+    auto pos = [&](long node, int d) { return nodes[node][d]; };
+    for (auto &kv : vdof)
+        for (int d = 0; d < dim; ++d) G.xyz[(size_t)kv.second * dim + d] = pos(kv.first, d);
+    std::vector<long> dof_node(nvd);
+    for (auto &kv : vdof) dof_node[kv.second] = kv.first;
+    auto edge_t = [&](int kk) { return order == 2 ? 0.5 : cdfem::p3_edge_t(kk); };
+    for (auto &kv : edge) {
+        const int32_t ga = kv.first.first, gb = kv.first.second;
+        for (int kk = 0; kk < ne_dofs; ++kk) {
+            const int64_t g = nvd + (int64_t)kv.second * ne_dofs + kk;
+            const double t = edge_t(kk);
+            for (int d = 0; d < dim; ++d)
+                G.xyz[(size_t)g * dim + d] = pos(dof_node[ga], d) + t * (pos(dof_node[gb], d) - pos(dof_node[ga], d));
+        }
+    }
+    for (int e = 0; e < G.ne; ++e) {
+        const auto &v = tv[e];
+        int32_t *ld = &G.dofs[(size_t)e * G.nd];
+        for (int i = 0; i <= dim; ++i) {
+            ld[i] = vdof[v[i]];
+            for (int d = 0; d < dim; ++d) G.verts[((size_t)e * G.nv + i) * dim + d] = pos(v[i], d);
+        }
+        for (int ed = 0; ed < nedge_loc && ne_dofs > 0; ++ed) {
+            const int la = dim == 3 ? cdfem::kSimplexEdge[ed][0] : cdfem::kTriEdge[ed][0];
+            const int lb = dim == 3 ? cdfem::kSimplexEdge[ed][1] : cdfem::kTriEdge[ed][1];
+            const int32_t ga = vdof[v[la]], gb = vdof[v[lb]];
+            const bool fwd = ga < gb;
+            const int32_t id = edge[{std::min(ga, gb), std::max(ga, gb)}];
+            for (int kk = 0; kk < ne_dofs; ++kk)
+                ld[G.nv + ed * ne_dofs + kk] = (int32_t)(nvd + (int64_t)id * ne_dofs + (fwd ? kk : ne_dofs - 1 - kk));
+        }
+        if (nint) {
+            const int64_t g = nvd + nedges * ne_dofs + e;
+            ld[G.nd - 1] = (int32_t)g;
+            for (int d = 0; d < dim; ++d)
+                G.xyz[(size_t)g * dim + d] = (pos(v[0], d) + pos(v[1], d) + pos(v[2], d)) / 3.0;
+        }
+    }
+    // boundary attributes
+    for (const El &e : els) {
+        if (e.type != btype || e.tag < 1 || e.tag > 31) continue;
+        const int32_t bit = 1 << (e.tag - 1);
+        std::vector<int32_t> bv;
+        for (long n : e.v) {
+            auto it = vdof.find(n);
+            if (it == vdof.end()) continue;
+            bv.push_back(it->second);
+            G.bmask[it->second] |= bit;
+        }
+        for (size_t i = 0; i < bv.size() && ne_dofs > 0; ++i)
+            for (size_t j = i + 1; j < bv.size(); ++j) {
+                auto it = edge.find({std::min(bv[i], bv[j]), std::max(bv[i], bv[j])});
+                if (it == edge.end()) continue;
+                for (int kk = 0; kk < ne_dofs; ++kk) G.bmask[nvd + (int64_t)it->second * ne_dofs + kk] |= bit;
+            }
+    }
+    return true;
+}
+
+}  // namespace
+
+int cdfem_gmsh_sizes(const char *path, int order, int *dim, int *ne, int64_t *nldofs)
+{
+    if (!path) return CDFEM_ERR_ARG;
+    Gmsh G;
+    std::string err;
+    if (!read_gmsh(path, order, G, err)) return CDFEM_ERR_ARG;
+    if (dim) *dim = G.dim;
+    if (ne) *ne = G.ne;
+    if (nldofs) *nldofs = G.nl;
+    return CDFEM_OK;
+}
+
+int cdfem_gmsh_mesh(const char *path, int order, double *elem_verts, int32_t *elem_dofs, int32_t *dof_bdr_mask,
+                    double *dof_xyz)
+{
+    if (!path) return CDFEM_ERR_ARG;
+    Gmsh G;
+    std::string err;
+    if (!read_gmsh(path, order, G, err)) return CDFEM_ERR_ARG;
+    if (elem_verts) std::copy(G.verts.begin(), G.verts.end(), elem_verts);
+    if (elem_dofs) std::copy(G.dofs.begin(), G.dofs.end(), elem_dofs);
+    if (dof_bdr_mask) std::copy(G.bmask.begin(), G.bmask.end(), dof_bdr_mask);
+    if (dof_xyz) std::copy(G.xyz.begin(), G.xyz.end(), dof_xyz);
+    return CDFEM_OK;
 }
 
 }  // extern "C"

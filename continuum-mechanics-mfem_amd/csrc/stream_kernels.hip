@@ -33,10 +33,64 @@ __global__ void __launch_bounds__(256) k_stream_copy(const double *__restrict__ 
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 2; i += stride) b2[i] = a2[i];
 }
 
+// Per-wave private chunks (the brick kernel's qdata pattern): one 64-lane block streams its own
+// contiguous kChunk bytes with 16-byte loads, U loads issued back to back.  PAD reserves 39 KB of
+// LDS per block so that at most one wave runs per SIMD (the brick kernel's occupancy).
+constexpr int64_t kChunkDoubles = 40960;  // 320 KiB
+template <int U, bool PAD>
+__global__ void __launch_bounds__(64) k_stream_chunk(const double *__restrict__ a, int64_t nchunks, double *out)
+{
+    __shared__ double pad[PAD ? 4992 : 1];
+    if (threadIdx.x == 64) pad[0] = 0.0;  // never true: keeps the allocation
+    const int64_t b = blockIdx.x;
+    if (b >= nchunks) return;
+    const double2 *p = reinterpret_cast<const double2 *>(a + b * kChunkDoubles) + threadIdx.x;
+    constexpr int iters = (int)(kChunkDoubles / 128);
+    double s = 0.0;
+    for (int i = 0; i < iters; i += U) {
+        double2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = p[(int64_t)(i + u) * 64];
+#pragma unroll
+        for (int u = 0; u < U; ++u) s += v[u].x + v[u].y;
+    }
+    if (s == 12345.678) out[0] = s + pad[0];
+}
+
+// Same work per wave, INTERLEAVED layout: the i-th 1 KiB piece of wave b lives at (i * nchunks + b),
+// so waves at the same step read adjacent kilobytes (candidate qdata layout [q][brick][...]).
+template <int U>
+__global__ void __launch_bounds__(64) k_stream_ileave(const double *__restrict__ a, int64_t nchunks, double *out)
+{
+    __shared__ double pad[4992];
+    if (threadIdx.x == 64) pad[0] = 0.0;
+    const int64_t b = blockIdx.x;
+    if (b >= nchunks) return;
+    const double2 *p = reinterpret_cast<const double2 *>(a) + b * 64 + threadIdx.x;
+    constexpr int iters = (int)(kChunkDoubles / 128);
+    double s = 0.0;
+    for (int i = 0; i < iters; i += U) {
+        double2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = p[(int64_t)(i + u) * nchunks * 64];
+#pragma unroll
+        for (int u = 0; u < U; ++u) s += v[u].x + v[u].y;
+    }
+    if (s == 12345.678) out[0] = s + pad[0];
+}
+
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n)
 {
     const dim3 grid(256 * 16), block(256);
+    const int64_t nch = n / kChunkDoubles;
     switch (mode) {
+    case 3: hipLaunchKernelGGL((k_stream_chunk<8, true>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
+    case 4: hipLaunchKernelGGL((k_stream_chunk<16, true>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
+    case 5: hipLaunchKernelGGL((k_stream_chunk<8, false>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
+    case 6: hipLaunchKernelGGL((k_stream_chunk<4, true>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
+    case 7: hipLaunchKernelGGL((k_stream_chunk<32, true>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
+    case 8: hipLaunchKernelGGL((k_stream_ileave<8>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
+    case 9: hipLaunchKernelGGL((k_stream_ileave<4>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
     case 0: hipLaunchKernelGGL(k_stream_read<16>, grid, block, 0, c->stream, a, n, b); break;
     case 1: hipLaunchKernelGGL(k_stream_read<8>, grid, block, 0, c->stream, a, n, b); break;
     case 2: hipLaunchKernelGGL(k_stream_copy, grid, block, 0, c->stream, a, b, n); break;

@@ -99,6 +99,8 @@ def _declare(L):
         "cdfem_fa_csr": (C.c_int, [vp, C.c_int, C.POINTER(i64), _ip, _ip, _dp]),
         "cdfem_kuhn_sizes": (C.c_int, [C.c_int] * 3 + [C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int)]),
         "cdfem_kuhn_mesh": (C.c_int, [C.c_int] * 3 + [C.c_double, _dp, _ip, _ip, _dp]),
+        "cdfem_gmsh_sizes": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(i64)]),
+        "cdfem_gmsh_mesh": (C.c_int, [C.c_char_p, C.c_int, _dp, _ip, _ip, _dp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -204,6 +206,30 @@ def kuhn_mesh(dim, n, order, perturb=0.0, with_coords=True) -> Mesh:
     if rc:
         raise CdfemError(rc, "Kuhn mesh generation failed (inverted element?)")
     return Mesh(dim, order, verts, dofmap, nl.value, ess, xyz, simplex=True)
+
+
+def gmsh_mesh(path, order, ess_attrs=None) -> Mesh:
+    """A gmsh v2.2 simplex mesh (e.g. the reference's Mesh/unit_square.msh) with an H1 space of the
+    given order; essential dofs on the boundary attributes ess_attrs (None: all)."""
+    L = lib()
+    dim, ne, nl = C.c_int(), C.c_int(), C.c_int64()
+    bpath = os.fsencode(path)
+    rc = L.cdfem_gmsh_sizes(bpath, order, C.byref(dim), C.byref(ne), C.byref(nl))
+    if rc:
+        raise CdfemError(rc, f"cannot read gmsh mesh {path} at order {order}")
+    d = dim.value
+    nd = d + 1 if order == 1 else (d + 1) * (d + 2) // 2 if order == 2 else 10
+    verts = np.zeros((ne.value, d + 1, d))
+    dofmap = np.zeros((ne.value, nd), dtype=np.int32)
+    mask = np.zeros(nl.value, dtype=np.int32)
+    xyz = np.zeros((nl.value, d))
+    rc = L.cdfem_gmsh_mesh(bpath, order, _p(verts), dofmap.ctypes.data_as(_ip), mask.ctypes.data_as(_ip), _p(xyz))
+    if rc:
+        raise CdfemError(rc, f"cannot read gmsh mesh {path}")
+    sel = mask != 0 if ess_attrs is None else (mask & sum(1 << (a - 1) for a in ess_attrs)) != 0
+    m = Mesh(d, order, verts, dofmap, nl.value, np.nonzero(sel)[0].astype(np.int32), xyz, simplex=True)
+    m.bdr_mask = mask
+    return m
 
 
 class Context:

@@ -112,9 +112,11 @@ int cdfem_pa_setup(cdfem_ctx *ctx, unsigned kinds, double kappa, const double *k
  * or tetrahedral mesh (gmsh input, Input/input_2d.yaml:1), and ParBilinearForm::Assemble +
  * FormLinearSystem -> HypreParMatrix (linear_convection_diffusion_2D.cpp:339,349-351) whose CSR
  * PETSc's KSPGMRES then multiplies (MATAIJ, :364-375).
- * cdfem_mesh_upload_simplex: P1/P2 Lagrange (order 1, 2) on affine simplices; elem_verts ne*(dim+1)
- * *dim, elem_dofs ne*nd with nd = dim+1 (P1) / (dim+1)(dim+2)/2 (P2), local order: vertices, then
- * edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3) [2D: (0,1),(0,2),(1,2)]; det J > 0 required.
+ * cdfem_mesh_upload_simplex: Lagrange P1/P2 (triangles also P3) on affine simplices; elem_verts
+ * ne*(dim+1)*dim, elem_dofs ne*nd with nd = dim+1 (P1) / (dim+1)(dim+2)/2 (P2) / 10 (P3 triangle),
+ * local order: vertices, then edge nodes along a->b for edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3)
+ * [2D: (0,1),(0,2),(1,2)], then the P3 centroid; det J > 0 required.  cdfem_lf_assemble works on
+ * simplex meshes with f sampled at the CDFEM_RULE_LINEARFORM points (collapsed Gauss, n = p + 3).
  * cdfem_fa_setup: same coefficients as cdfem_pa_setup (per-point arrays on the OPERATOR rule);
  * assembles A (CSR, columns sorted) and the eliminated matrix of FormLinearSystem on the GPU.
  * Afterwards cdfem_pa_mult / cdfem_pa_diagonal / cdfem_form_linear_system / cdfem_solve run on the
@@ -176,7 +178,10 @@ int cdfem_solve(cdfem_ctx *ctx, const cdfem_solver_params *prm, const double *B,
                 int where, cdfem_solver_result *res);
 
 /* ---- HBM bandwidth probe: mode 0 read (16 B/lane), 1 read (8 B/lane), 2 copy (16 B/lane) of a
- * `bytes`-sized buffer, `reps` launches; returns achieved GB/s (bytes moved / time).            */
+ * `bytes`-sized buffer, `reps` launches; returns achieved GB/s (bytes moved / time).
+ * Modes 3-7: per-wave private 320 KiB chunks (16 B/lane), 8/16/8/4/32 loads in flight; 3, 4, 6, 7
+ * limited to one wave per SIMD by an LDS reservation, 5 unrestricted.  Modes 8, 9: the same
+ * per-wave work (8 / 4 loads in flight, one wave per SIMD) on an interleaved layout.            */
 int cdfem_stream_bench(cdfem_ctx *ctx, int mode, size_t bytes, int reps, double *gbps);
 
 /* ---- tuning knobs (performance only; results identical to rounding) --------------------------
@@ -226,6 +231,17 @@ int cdfem_box_mesh(int dim, int nx, int ny, int nz, int order, int z0, int z1, d
 int cdfem_kuhn_sizes(int dim, int n, int order, int *ne, int64_t *nldofs, int *n_ess);
 int cdfem_kuhn_mesh(int dim, int n, int order, double perturb, double *elem_verts, int32_t *elem_dofs,
                     int32_t *ess_dofs, double *dof_xyz);
+
+/* gmsh v2.2 ASCII simplex meshes (the reference's inputs, e.g. Mesh/unit_square.msh); replaces
+ * Mesh(mesh_file, 1, 1) + H1_FECollection(order, dim) + ParFiniteElementSpace
+ * (linear_convection_diffusion_2D.cpp:290,311-313).  Triangles (order 1-3) or tetrahedra (1-2),
+ * re-oriented to det J > 0; dofs: vertices (increasing gmsh node id), then (order-1) per edge along
+ * increasing vertex dof, then P3 triangle centroids.  dof_bdr_mask[i] has bit (a-1) set when dof i
+ * lies on a boundary element of physical attribute a (GetEssentialTrueDofs with an ess_bdr marker).
+ * Host only; the element arrays feed cdfem_mesh_upload_simplex.                               */
+int cdfem_gmsh_sizes(const char *path, int order, int *dim, int *ne, int64_t *nldofs);
+int cdfem_gmsh_mesh(const char *path, int order, double *elem_verts, int32_t *elem_dofs, int32_t *dof_bdr_mask,
+                    double *dof_xyz);
 
 #ifdef __cplusplus
 }

@@ -937,7 +937,67 @@ ORC_API int orc_simplex_nd(int dim, int p)
 {
     if (p == 1) return dim + 1;
     if (p == 2) return (dim + 1) * (dim + 2) / 2;
+    if (p == 3 && dim == 2) return 10;
     return -1;
+}
+
+static const int kEdge3[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
+static const int kEdge2[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+
+/* P3 triangle, MFEM H1_FECollection(3, 2) (BasisType::GaussLobatto): nodes = vertices, the two
+ * interior GLL points of each edge (0,1), (0,2), (1,2) along a -> b, the centroid.  The nodal
+ * basis is solved in the space spanned by lambda_1^a lambda_2^b (a + b <= 3). */
+static double p3_coef[10][10];  /* phi_i = sum_k p3_coef[k][i] m_k */
+static int p3_ready = 0;
+
+static void p3_mono(const double *xi, double *m, double *m1, double *m2)
+{
+    /* m_k = l1^a l2^b with l1 = xi_0, l2 = xi_1; derivatives w.r.t. xi_0, xi_1 */
+    int k = 0;
+    for (int a = 0; a <= 3; a++)
+        for (int b = 0; a + b <= 3; b++, k++) {
+            m[k] = pow(xi[0], a) * pow(xi[1], b);
+            m1[k] = a ? a * pow(xi[0], a - 1) * pow(xi[1], b) : 0.0;
+            m2[k] = b ? b * pow(xi[0], a) * pow(xi[1], b - 1) : 0.0;
+        }
+}
+
+static void p3_init(void)
+{
+    if (p3_ready) return;
+    const double g = 0.5 * (1.0 - 1.0 / sqrt(5.0));
+    const double V3[3][2] = {{0, 0}, {1, 0}, {0, 1}};
+    double X[10][2];
+    for (int v = 0; v < 3; v++) { X[v][0] = V3[v][0]; X[v][1] = V3[v][1]; }
+    for (int e = 0; e < 3; e++)
+        for (int k = 0; k < 2; k++) {
+            const double t = k == 0 ? g : 1.0 - g;
+            for (int d = 0; d < 2; d++)
+                X[3 + 2 * e + k][d] = V3[kEdge2[e][0]][d] + t * (V3[kEdge2[e][1]][d] - V3[kEdge2[e][0]][d]);
+        }
+    X[9][0] = X[9][1] = 1.0 / 3.0;
+    /* solve V c_i = e_i for all i: V[r][k] = m_k(X_r) */
+    double M[10][20];
+    for (int r = 0; r < 10; r++) {
+        double m[10], m1[10], m2[10];
+        p3_mono(X[r], m, m1, m2);
+        for (int k = 0; k < 10; k++) M[r][k] = m[k];
+        for (int k = 0; k < 10; k++) M[r][10 + k] = (r == k);
+    }
+    for (int c = 0; c < 10; c++) {
+        int pr = c;
+        for (int r = c + 1; r < 10; r++) if (fabs(M[r][c]) > fabs(M[pr][c])) pr = r;
+        for (int k = 0; k < 20; k++) { double t = M[c][k]; M[c][k] = M[pr][k]; M[pr][k] = t; }
+        const double d = M[c][c];
+        for (int k = 0; k < 20; k++) M[c][k] /= d;
+        for (int r = 0; r < 10; r++) if (r != c) {
+            const double f = M[r][c];
+            for (int k = 0; k < 20; k++) M[r][k] -= f * M[c][k];
+        }
+    }
+    for (int k = 0; k < 10; k++)
+        for (int i = 0; i < 10; i++) p3_coef[k][i] = M[k][10 + i];
+    p3_ready = 1;
 }
 
 /* Collapsed (Duffy) tensor Gauss-Legendre rule on the reference simplex (vertices 0, e_1 .. e_d),
@@ -975,11 +1035,25 @@ ORC_API int orc_simplex_rule(int dim, int n, double *xi, double *w)
 /* Reference basis at xi: phi[nd], dphi[nd][dim] (d/dxi_k), barycentric lambda_0 = 1 - sum xi.
  * Local order: vertices 0..dim, then (P2) edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3) [2D: (0,1),
  * (0,2),(1,2)]. */
-static const int kEdge3[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
-static const int kEdge2[3][2] = {{0, 1}, {0, 2}, {1, 2}};
 
 static void simplex_basis(int dim, int p, const double *xi, double *phi, double *dphi)
 {
+    if (dim == 2 && p == 3) {
+        double m[10], m1[10], m2[10];
+        p3_mono(xi, m, m1, m2);
+        for (int i = 0; i < 10; i++) {
+            double v = 0.0, gx = 0.0, gy = 0.0;
+            for (int k = 0; k < 10; k++) {
+                v += p3_coef[k][i] * m[k];
+                gx += p3_coef[k][i] * m1[k];
+                gy += p3_coef[k][i] * m2[k];
+            }
+            phi[i] = v;
+            dphi[i * 2] = gx;
+            dphi[i * 2 + 1] = gy;
+        }
+        return;
+    }
     double lam[4], dlam[4][3];  /* d lambda_a / d xi_k */
     lam[0] = 1.0;
     for (int k = 0; k < dim; k++) lam[0] -= xi[k];
@@ -1138,6 +1212,7 @@ ORC_API orc_csr *orc_fa_assemble_simplex(int dim, int p, int ne, const double *v
                                          int64_t nl, double kappa, double alpha, double s, const double *c,
                                          int kinds)
 {
+    p3_init();
     const int nd = orc_simplex_nd(dim, p);
     if (nd < 0 || (dim != 2 && dim != 3)) return NULL;
     orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
@@ -1174,6 +1249,7 @@ static void simplex_point(int dim, const double *V, const double *xi, double *x,
 ORC_API void orc_lf_assemble_simplex(int dim, int p, int ne, const double *verts, const int *dofmap,
                                      int64_t nl, const double *prm, double *b)
 {
+    p3_init();
     const int nd = orc_simplex_nd(dim, p), n1 = p + 3;
     double xi[7 * 7 * 7 * 3], wq[7 * 7 * 7];
     const int nq = orc_simplex_rule(dim, n1, xi, wq);
@@ -1198,6 +1274,7 @@ ORC_API void orc_lf_assemble_simplex(int dim, int p, int ne, const double *verts
 ORC_API double orc_l2_error_simplex(int dim, int p, int ne, const double *verts, const int *dofmap,
                                     const double *u, const double *prm)
 {
+    p3_init();
     const int nd = orc_simplex_nd(dim, p), n1 = p + 3;
     double xi[7 * 7 * 7 * 3], wq[7 * 7 * 7];
     const int nq = orc_simplex_rule(dim, n1, xi, wq);
@@ -1221,16 +1298,20 @@ ORC_API double orc_l2_error_simplex(int dim, int p, int ne, const double *verts,
 ORC_API void orc_dof_coords_simplex(int dim, int p, int ne, const double *verts, const int *dofmap, double *xyz)
 {
     const int nd = orc_simplex_nd(dim, p), nv = dim + 1;
+    const double g = 0.5 * (1.0 - 1.0 / sqrt(5.0));
     for (int e = 0; e < ne; e++) {
         const double *V = verts + (size_t)e * nv * dim;
         for (int l = 0; l < nd; l++) {
             double X[3] = {0, 0, 0};
             if (l < nv) {
                 for (int k = 0; k < dim; k++) X[k] = V[l * dim + k];
+            } else if (p == 3 && l == nd - 1) {  /* P3 centroid */
+                for (int k = 0; k < dim; k++) X[k] = (V[k] + V[dim + k] + V[2 * dim + k]) / 3.0;
             } else {
-                const int ed = l - nv;
+                const int ed = (l - nv) / (p - 1), kk = (l - nv) % (p - 1);
                 const int a = dim == 3 ? kEdge3[ed][0] : kEdge2[ed][0], b = dim == 3 ? kEdge3[ed][1] : kEdge2[ed][1];
-                for (int k = 0; k < dim; k++) X[k] = 0.5 * (V[a * dim + k] + V[b * dim + k]);
+                const double t = p == 2 ? 0.5 : (kk == 0 ? g : 1.0 - g);
+                for (int k = 0; k < dim; k++) X[k] = V[a * dim + k] + t * (V[b * dim + k] - V[a * dim + k]);
             }
             for (int k = 0; k < dim; k++) xyz[(size_t)dofmap[(size_t)e * nd + l] * dim + k] = X[k];
         }
