@@ -266,6 +266,22 @@ struct Element {
 // 5 x=0, 6 z=sz.
 class Mesh {
 public:
+    // gmsh v2.2 simplex mesh file, as Mesh(mesh_file, 1, 1) at linear_convection_diffusion_2D.cpp:290
+    explicit Mesh(const char *path, int = 1, int = 1) : dim_(0), n_{0, 0, 0}, s_{1.0, 1.0, 1.0}, path_(path)
+    {
+        int ne = 0;
+        int64_t nl = 0;
+        check(cdfem_gmsh_sizes(path, 1, &dim_, &ne, &nl), nullptr, "cdfem_gmsh_sizes (mesh file)");
+        ne_ = ne;
+        std::vector<int32_t> mask((size_t)nl);
+        check(cdfem_gmsh_mesh(path, 1, nullptr, nullptr, mask.data(), nullptr), nullptr, "cdfem_gmsh_mesh");
+        int32_t all = 0;
+        for (int32_t m : mask) all |= m;
+        for (int a = 1; a <= 31; ++a)
+            if (all & (1 << (a - 1))) bdr_attributes.Append(a);
+    }
+    bool FromFile() const { return !path_.empty(); }
+    const std::string &Path() const { return path_; }
     static Mesh MakeCartesian2D(int nx, int ny, Element::Type, bool = false, double sx = 1.0, double sy = 1.0)
     {
         return Mesh(2, nx, ny, 1, sx, sy, 1.0);
@@ -276,7 +292,7 @@ public:
         return Mesh(3, nx, ny, nz, sx, sy, sz);
     }
     int Dimension() const { return dim_; }
-    int GetNE() const { return dim_ == 3 ? n_[0] * n_[1] * n_[2] : n_[0] * n_[1]; }
+    int GetNE() const { return FromFile() ? ne_ : dim_ == 3 ? n_[0] * n_[1] * n_[2] : n_[0] * n_[1]; }
     int N(int k) const { return n_[k]; }
     double Size(int k) const { return s_[k]; }
     Array<int> bdr_attributes;
@@ -291,6 +307,8 @@ private:
     int dim_;
     int n_[3];
     double s_[3];
+    std::string path_;
+    int ne_ = 0;
 };
 using ParMesh = Mesh;
 
@@ -313,6 +331,22 @@ public:
     {
         if (mesh->Dimension() != fec->GetDim()) throw std::invalid_argument("FiniteElementSpace: dim mismatch");
         const int dim = mesh->Dimension(), p = fec->GetOrder();
+        if (mesh->FromFile()) {  // simplices: numbering and boundary attributes from the reader
+            int d = 0;
+            int64_t nl = 0;
+            check(cdfem_gmsh_sizes(mesh->Path().c_str(), p, &d, &ne_, &nl), nullptr, "cdfem_gmsh_sizes");
+            nl_ = (int)nl;
+            nv_ = dim + 1;
+            nd_ = p == 1 ? dim + 1 : p == 2 ? (dim + 1) * (dim + 2) / 2 : 10;
+            verts_.resize((size_t)ne_ * nv_ * dim);
+            dofs_.resize((size_t)ne_ * nd_);
+            xyz_.resize((size_t)nl_ * dim);
+            bmask_.resize(nl_);
+            check(cdfem_gmsh_mesh(mesh->Path().c_str(), p, verts_.data(), dofs_.data(), bmask_.data(), xyz_.data()),
+                  nullptr, "cdfem_gmsh_mesh");
+            simplex_ = true;
+            return;
+        }
         int64_t nl = 0;
         int ness = 0;
         check(cdfem_box_sizes(dim, mesh->N(0), mesh->N(1), mesh->N(2), p, 0, 0, &ne_, &nl, &ness), nullptr,
@@ -347,6 +381,11 @@ public:
     }
     bool OnMarkedBoundary(int i, const Array<int> &marker, int dim) const
     {
+        if (simplex_) {
+            for (int a = 1; a <= marker.Size() && a <= 31; ++a)
+                if (marker[a - 1] && (bmask_[i] & (1 << (a - 1)))) return true;
+            return false;
+        }
         const double *X = &xyz_[(size_t)i * dim];
         auto at = [&](int attr) { return attr <= marker.Size() && marker[attr - 1] != 0; };
         const double sx = mesh_->Size(0), sy = mesh_->Size(1), sz = mesh_->Size(2);
@@ -358,14 +397,16 @@ public:
     const std::vector<double> &ElementVertices() const { return verts_; }
     const std::vector<int32_t> &ElementDofs() const { return dofs_; }
     const std::vector<double> &DofCoordinates() const { return xyz_; }
-    bool Structured() const { return true; }
+    bool Simplex() const { return simplex_; }
+    int NumElementDofs() const { return nd_; }
 
 private:
     Mesh *mesh_;
     H1_FECollection *fec_;
     int ne_ = 0, nl_ = 0, nv_ = 0, nd_ = 0;
+    bool simplex_ = false;
     std::vector<double> verts_, xyz_;
-    std::vector<int32_t> dofs_;
+    std::vector<int32_t> dofs_, bmask_;
 };
 using ParFiniteElementSpace = FiniteElementSpace;
 
@@ -384,16 +425,26 @@ public:
     void Upload(const FiniteElementSpace &fes, const Array<int> &ess, bool structured)
     {
         Mesh *m = fes.GetMesh();
+        simplex_ = fes.Simplex();
+        if (simplex_) {
+            check(cdfem_mesh_upload_simplex(ctx_, m->Dimension(), fes.GetOrder(), fes.GetNE(),
+                                            fes.ElementVertices().data(), fes.GetVSize(), fes.ElementDofs().data(),
+                                            ess.Size(), ess.GetData()),
+                  ctx_, "cdfem_mesh_upload_simplex");
+            ess_ = ess;
+            return;
+        }
         check(cdfem_mesh_upload(ctx_, m->Dimension(), fes.GetOrder(), fes.GetNE(), fes.ElementVertices().data(),
                                 fes.GetVSize(), fes.ElementDofs().data(), ess.Size(), ess.GetData()),
               ctx_, "cdfem_mesh_upload");
-        // the Cartesian box is lexicographic: the structured (brick) fast path where it exists
-        if (structured && m->Dimension() == 3 && fes.GetOrder() <= 2)
+        // the Cartesian box is lexicographic: the structured fast paths (bricks p <= 2, lattice E->L p >= 3)
+        if (structured && m->Dimension() == 3)
             check(cdfem_mesh_set_structured(ctx_, m->N(0), m->N(1), m->N(2)), ctx_, "cdfem_mesh_set_structured");
         ess_ = ess;
     }
     cdfem_ctx *ctx() const { return ctx_; }
     const Array<int> &Ess() const { return ess_; }
+    bool Simplex() const { return simplex_; }
     // physical coordinates of a rule's points, element-major
     std::vector<double> Points(int rule, int dim, int ne, int &nq) const
     {
@@ -406,6 +457,7 @@ public:
 private:
     cdfem_ctx *ctx_ = nullptr;
     Array<int> ess_;
+    bool simplex_ = false;
 };
 
 // sample a scalar coefficient at the given points (host virtual calls, as in MFEM)
@@ -609,9 +661,11 @@ private:
                 }
             }
         }
-        check(cdfem_pa_setup(ctx(), kinds, kappa, kq.empty() ? nullptr : kq.data(), alpha, conv,
-                             cq.empty() ? nullptr : cq.data(), mass, mq.empty() ? nullptr : mq.data()),
-              ctx(), "cdfem_pa_setup");
+        // hexes / quads: partial assembly; simplices: full assembly (CSR on the GPU)
+        auto setup = dev_->Simplex() ? cdfem_fa_setup : cdfem_pa_setup;
+        check(setup(ctx(), kinds, kappa, kq.empty() ? nullptr : kq.data(), alpha, conv, cq.empty() ? nullptr : cq.data(),
+                    mass, mq.empty() ? nullptr : mq.data()),
+              ctx(), dev_->Simplex() ? "cdfem_fa_setup" : "cdfem_pa_setup");
     }
 
     FiniteElementSpace *fes_;
@@ -766,8 +820,49 @@ private:
             (*this)[i] = q.Eval(T, ip);
         }
     }
+    // simplices: collapsed Gauss with n = p + 3 points per direction (exact to degree 2p + 6 - dim
+    // >= the driver's max(2, 2p + 3) in 2D), the product's nodal basis
+    double L2Simplex(Coefficient *exact, bool exact_only) const
+    {
+        const int dim = fes_->GetMesh()->Dimension(), p = fes_->GetOrder(), nd = fes_->NumElementDofs();
+        const int nq = cdfem_simplex_rule(dim, p + 3, nullptr, nullptr);
+        std::vector<double> xi((size_t)nq * dim), w(nq), phi((size_t)nq * nd);
+        cdfem_simplex_rule(dim, p + 3, xi.data(), w.data());
+        check(cdfem_simplex_basis(dim, p, nq, xi.data(), phi.data(), nullptr), nullptr, "cdfem_simplex_basis");
+        const std::vector<double> &V = fes_->ElementVertices();
+        const std::vector<int32_t> &D = fes_->ElementDofs();
+        ElementTransformation T;
+        IntegrationPoint ip;
+        double err2 = 0.0;
+        for (int e = 0; e < fes_->GetNE(); ++e) {
+            const double *ev = &V[(size_t)e * (dim + 1) * dim];
+            double J[3][3] = {};
+            for (int k = 0; k < dim; ++k)
+                for (int m = 0; m < dim; ++m) J[k][m] = ev[(m + 1) * dim + k] - ev[k];
+            const double det = dim == 3 ? J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) -
+                                              J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                                              J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0])
+                                        : J[0][0] * J[1][1] - J[0][1] * J[1][0];
+            for (int q = 0; q < nq; ++q) {
+                double X[3] = {0, 0, 0};
+                for (int k = 0; k < dim; ++k) {
+                    X[k] = ev[k];
+                    for (int m = 0; m < dim; ++m) X[k] += J[k][m] * xi[(size_t)q * dim + m];
+                }
+                double uh = 0.0;
+                if (!exact_only)
+                    for (int l = 0; l < nd; ++l) uh += phi[(size_t)q * nd + l] * (*this)[D[(size_t)e * nd + l]];
+                T.ElementNo = e;
+                T.SetPoint(dim, X);
+                const double u = exact->Eval(T, ip);
+                err2 += w[q] * std::fabs(det) * (uh - u) * (uh - u);
+            }
+        }
+        return std::sqrt(err2);
+    }
     double L2(Coefficient *exact, const IntegrationRule *irs[], bool exact_only) const
     {
+        if (fes_->Simplex()) return L2Simplex(exact, exact_only);
         const int dim = fes_->GetMesh()->Dimension(), p = fes_->GetOrder(), d1 = p + 1;
         const int geom = dim == 3 ? Geometry::CUBE : Geometry::SQUARE;
         const int order = (irs && irs[geom]) ? irs[geom]->GetOrder() : std::max(2, 2 * p + 3);
@@ -838,7 +933,7 @@ using ParGridFunction = GridFunction;
 inline double ComputeGlobalLpNorm(double p, Coefficient &exact, Mesh &mesh, const IntegrationRule *irs[])
 {
     if (p != 2.0) throw std::invalid_argument("ComputeGlobalLpNorm: only p = 2");
-    H1_FECollection fec(1, mesh.Dimension());
+    H1_FECollection fec(mesh.FromFile() ? 2 : 1, mesh.Dimension());  // simplex rule n = p + 3 >= 5
     FiniteElementSpace fes(&mesh, &fec);
     GridFunction z(&fes);
     return z.ComputeL2Norm(exact, irs);

@@ -9,7 +9,7 @@
 // (:159-170), extended with sin(l pi z) in 3D; the forcing is the reference's (:174-205) plus the
 // z terms.  Configuration comes from the command line instead of YAML (out of scope).
 //
-//   convection_diffusion [-d dim] [-n elems] [-p order] [-k kappa] [-s reaction]
+//   convection_diffusion [-d dim] [-n elems | -mesh file.msh] [-p order] [-k kappa] [-s reaction]
 //                        [-c cx,cy,cz] [-m n,m,l] [-opts petsc.opts] [-pl print_level]
 // Output (stdout, one "key value" per line): dofs, iterations, converged, final_norm, l2_abs,
 // l2_rel, solve_seconds.  Exit code 3 on error (as the reference drivers, :435-442).
@@ -29,7 +29,7 @@ struct Params {
     int dim = 2, n = 16, order = 2, print_level = 0;
     double kappa = 0.1, reaction = 1.0, c[3] = {1.0, -2.0, 0.5};
     int modes[3] = {3, 3, 3};
-    std::string opts;
+    std::string opts, mesh;
 };
 
 class ExactSolution : public Coefficient {
@@ -99,6 +99,7 @@ Params parse(int argc, char **argv)
         else if (k == "-c") parse_triplet(v, p.c);
         else if (k == "-m") std::sscanf(v, "%d,%d,%d", &p.modes[0], &p.modes[1], &p.modes[2]);
         else if (k == "-opts") p.opts = v;
+        else if (k == "-mesh") p.mesh = v;
         else if (k == "-pl") p.print_level = std::atoi(v);
         else throw std::invalid_argument("unknown option " + k);
     }
@@ -114,8 +115,12 @@ int main(int argc, char **argv)
         const Params prm = parse(argc, argv);
         MFEMInitializePetsc(&argc, &argv, prm.opts.empty() ? nullptr : prm.opts.c_str(), nullptr);
 
-        Mesh mesh = prm.dim == 2 ? Mesh::MakeCartesian2D(prm.n, prm.n, Element::QUADRILATERAL)
-                                 : Mesh::MakeCartesian3D(prm.n, prm.n, prm.n, Element::HEXAHEDRON);
+        // -mesh: a gmsh file as in the reference's inputs (Input/input_2d.yaml: mesh_file), else a box
+        Mesh mesh = !prm.mesh.empty() ? Mesh(prm.mesh.c_str(), 1, 1)
+                    : prm.dim == 2   ? Mesh::MakeCartesian2D(prm.n, prm.n, Element::QUADRILATERAL)
+                                     : Mesh::MakeCartesian3D(prm.n, prm.n, prm.n, Element::HEXAHEDRON);
+        if (!prm.mesh.empty() && mesh.Dimension() != prm.dim)
+            throw std::invalid_argument("-d does not match the mesh file's dimension");
         H1_FECollection fec(prm.order, prm.dim);
         ParFiniteElementSpace fespace(&mesh, &fec);
 

@@ -474,4 +474,29 @@ int cdfem_gmsh_mesh(const char *path, int order, double *elem_verts, int32_t *el
     return CDFEM_OK;
 }
 
+// host helpers: the simplex rule and nodal basis the kernels use (for host-side functionals such as
+// ComputeL2Error, linear_convection_diffusion_2D.cpp:383-392)
+int cdfem_simplex_rule(int dim, int n, double *xi, double *w)
+{
+    if ((dim != 2 && dim != 3) || n < 1 || n > 16) return -CDFEM_ERR_ARG;
+    std::vector<double> x, ww;
+    const int nq = cdfem::simplex_rule(dim, n, x, ww);
+    if (xi) std::copy(x.begin(), x.end(), xi);
+    if (w) std::copy(ww.begin(), ww.end(), w);
+    return nq;
+}
+
+int cdfem_simplex_basis(int dim, int order, int npts, const double *xi, double *phi, double *dphi)
+{
+    const int nd = cdfem::simplex_ndofs(dim, order);
+    if ((dim != 2 && dim != 3) || nd < 0 || npts < 0 || !xi || !phi) return CDFEM_ERR_ARG;
+    double p[10], g[30];
+    for (int i = 0; i < npts; ++i) {
+        cdfem::simplex_basis(dim, order, xi + (size_t)i * dim, p, g);
+        std::copy(p, p + nd, phi + (size_t)i * nd);
+        if (dphi) std::copy(g, g + nd * dim, dphi + (size_t)i * nd * dim);
+    }
+    return CDFEM_OK;
+}
+
 }  // extern "C"

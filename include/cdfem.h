@@ -243,6 +243,12 @@ int cdfem_gmsh_sizes(const char *path, int order, int *dim, int *ne, int64_t *nl
 int cdfem_gmsh_mesh(const char *path, int order, double *elem_verts, int32_t *elem_dofs, int32_t *dof_bdr_mask,
                     double *dof_xyz);
 
+/* Host helpers: the collapsed-Gauss simplex rule (returns the point count; xi/w may be NULL to
+ * query it) and the nodal simplex basis phi [npts][nd], dphi [npts][nd][dim] in the local dof
+ * order above — for host-side functionals (ComputeL2Error, :383-392).                         */
+int cdfem_simplex_rule(int dim, int n, double *xi, double *w);
+int cdfem_simplex_basis(int dim, int order, int npts, const double *xi, double *phi, double *dphi);
+
 #ifdef __cplusplus
 }
 #endif

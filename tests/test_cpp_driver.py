@@ -84,3 +84,32 @@ def test_driver_cg_options(exe, tmp_path):
     assert out["converged"] == 1 and abs(out["iterations"] - info["iterations"]) <= 1
     assert abs(out["l2_abs"] - l2) <= 1e-6 * l2
     assert np.isfinite(out["solve_seconds"])
+
+
+@pytest.mark.gpu
+def test_driver_gmsh_p3_reference_configuration(exe, tmp_path):
+    """The reference's default run (Input/input_2d.yaml: gmsh mesh, order 3, kappa 0.1, s 1,
+    c (1,-2), modes 3,3, Input/petsc.opts) through `convection_diffusion -mesh`, on a synthetic
+    gmsh v2.2 square, against the oracle's restatement of the same sequence."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import gmsh_synth
+    import cdfem
+    from oracle import oracle as O
+    msh = str(tmp_path / "square.msh")
+    gmsh_synth.write_square(msh, 10, perturb=0.25, seed=7)
+    rc, out, err = _run(["-d", "2", "-mesh", msh, "-p", "3", "-c", "1,-2,0", "-m", "3,3,3"], PETSC_OPTS, tmp_path)
+    assert rc == 0, err
+    m = cdfem.gmsh_mesh(msh, 3)
+
+    class OM:
+        pass
+    om = OM()
+    om.dim, om.p, om.ne, om.nl, om.verts, om.dofmap, om.ess = 2, 3, m.ne, m.nl, m.verts, m.dofmap, m.ess
+    om.bdr = np.zeros(m.nl, dtype=np.int32)
+    om.bdr[m.ess] = 1
+    prm = O.mms_params(O.MMS_SIN, 2, kappa=0.1, s=1.0, c=(1.0, -2.0), modes=(3, 3, 3), p=3)
+    _, info, l2 = O.solve_mms_simplex(om, prm, 0.1, 1.0, (1.0, -2.0))
+    assert int(out["dofs"]) == m.nl
+    assert out["converged"] == 1 and abs(out["iterations"] - info["iterations"]) <= 1
+    assert abs(out["l2_abs"] - l2) <= 1e-6 * l2
