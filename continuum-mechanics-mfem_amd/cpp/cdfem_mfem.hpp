@@ -325,6 +325,8 @@ private:
     int p_, dim_;
 };
 
+class DeviceSpace;
+
 class FiniteElementSpace {
 public:
     FiniteElementSpace(Mesh *mesh, H1_FECollection *fec) : mesh_(mesh), fec_(fec)
@@ -399,8 +401,12 @@ public:
     const std::vector<double> &DofCoordinates() const { return xyz_; }
     bool Simplex() const { return simplex_; }
     int NumElementDofs() const { return nd_; }
+    // device context for linear forms on this space, created on first use and reused (the
+    // reference builds a new ParLinearForm every time step, diffusion_mms.cpp:434-437)
+    std::shared_ptr<DeviceSpace> &LinearFormDevice() const { return lf_dev_; }
 
 private:
+    mutable std::shared_ptr<DeviceSpace> lf_dev_;
     Mesh *mesh_;
     H1_FECollection *fec_;
     int ne_ = 0, nl_ = 0, nv_ = 0, nd_ = 0;
@@ -698,7 +704,9 @@ public:
     void AddDomainIntegrator(LinearFormIntegrator *lfi) { integs_.emplace_back(lfi); }
     void Assemble()
     {
-        DeviceSpace dev(*fes_, Array<int>(), false);
+        std::shared_ptr<DeviceSpace> &cached = fes_->LinearFormDevice();
+        if (!cached) cached = std::make_shared<DeviceSpace>(*fes_, Array<int>(), false);
+        DeviceSpace &dev = *cached;
         const int dim = fes_->GetMesh()->Dimension();
         int nq = 0;
         const std::vector<double> xyz = dev.Points(CDFEM_RULE_LINEARFORM, dim, fes_->GetNE(), nq);
