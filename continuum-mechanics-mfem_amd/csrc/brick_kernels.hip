@@ -334,7 +334,7 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // VAR % 3 = element core: 0 elem_apply3d fully unrolled; 1 elem_apply3d, plane loop; 2 low-register
 // core.  VAR >= 3: the same cores compiled for 2 waves per SIMD (<= 256 registers).
 template <int D1, int Q1, unsigned K, int VAR>
-__global__ void __launch_bounds__(64, VAR >= 3 ? 2 : 1)
+__global__ void __launch_bounds__(64, (VAR >= 3 && VAR <= 5) ? 2 : 1)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
@@ -386,7 +386,9 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
     const double *q0 = qd + (size_t)b * NQ * NC * kLanes;
     double Y[D1][D1][D1];
-    if constexpr (VAR % 3 == 2)
+    if constexpr (VAR == 6)
+        elem_apply3d<D1, Q1, K, decltype(xl), Q1, false>(xl, q0, t, T, Y);  // temporal qdata loads (A/B)
+    else if constexpr (VAR % 3 == 2)
         elem_apply3d_lr<D1, Q1, K, decltype(xl), 1>(xl, q0, t, T, Y);
     else if constexpr (VAR % 3 == 1)
         elem_apply3d<D1, Q1, K, decltype(xl), 1>(xl, q0, t, T, Y);
@@ -503,6 +505,7 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     case 3: CDFEM_L(3); break;
     case 4: CDFEM_L(4); break;
     case 5: CDFEM_L(5); break;
+    case 6: CDFEM_L(6); break;
     default: CDFEM_L(0); break;
     }
 #undef CDFEM_L

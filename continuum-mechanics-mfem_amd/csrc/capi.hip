@@ -1124,7 +1124,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         if (!key) throw ArgError("key is null");
         const std::string k(key);
         if (k == "brick_variant") {
-            if (value < 0 || value > 5) throw ArgError("brick_variant must be 0..5");
+            if (value < 0 || value > 6) throw ArgError("brick_variant must be 0..6");
             c->brick_variant = value;
         } else if (k == "profile_mask") {
             c->prof_mask = (unsigned)value;

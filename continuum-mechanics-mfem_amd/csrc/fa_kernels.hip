@@ -373,15 +373,20 @@ k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows,
         double a0 = 0.0;
         int j = 0;
         for (; j + 4 <= len; j += 4) {  // 4 independent loads in flight per lane
-            const double v0 = v[(j + 0) * 64], v1 = v[(j + 1) * 64], v2 = v[(j + 2) * 64], v3 = v[(j + 3) * 64];
-            const int32_t c0 = cidx[(j + 0) * 64], c1 = cidx[(j + 1) * 64], c2 = cidx[(j + 2) * 64],
-                          c3 = cidx[(j + 3) * 64];
+            // values and columns are streamed once per SpMV: non-temporal, x stays in L2
+            const double v0 = __builtin_nontemporal_load(v + (j + 0) * 64), v1 = __builtin_nontemporal_load(v + (j + 1) * 64),
+                         v2 = __builtin_nontemporal_load(v + (j + 2) * 64), v3 = __builtin_nontemporal_load(v + (j + 3) * 64);
+            const int32_t c0 = __builtin_nontemporal_load(cidx + (j + 0) * 64),
+                          c1 = __builtin_nontemporal_load(cidx + (j + 1) * 64),
+                          c2 = __builtin_nontemporal_load(cidx + (j + 2) * 64),
+                          c3 = __builtin_nontemporal_load(cidx + (j + 3) * 64);
             a0 = fma(v0, x[c0], a0);
             a0 = fma(v1, x[c1], a0);
             a0 = fma(v2, x[c2], a0);
             a0 = fma(v3, x[c3], a0);
         }
-        for (; j < len; ++j) a0 = fma(v[j * 64], x[cidx[j * 64]], a0);
+        for (; j < len; ++j)
+            a0 = fma(__builtin_nontemporal_load(v + j * 64), x[__builtin_nontemporal_load(cidx + j * 64)], a0);
         const double acc = a0;
         if (row >= 0) {
             y[row] = acc;

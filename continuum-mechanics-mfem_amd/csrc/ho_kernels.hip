@@ -67,7 +67,7 @@ k_apply3d_wpe(const int32_t *__restrict__ map, const double *__restrict__ x, con
         const int q = lane + 64 * i;
 #pragma unroll
         for (int c = 0; c < NC; ++c)
-            qv[i][c] = (valid && q < NQ) ? qd[((size_t)e * NC + c) * NQ + q] : 0.0;
+            qv[i][c] = (valid && q < NQ) ? qd[((size_t)e * NC + c) * NQ + q] : 0.0;  // (non-temporal measured 3 % slower)
     }
     // gather
     if (valid) {

@@ -47,16 +47,31 @@ __host__ __device__ constexpr int qd_offset(int c, int lane, int nc)
     return (c < (nc & ~1)) ? ((c >> 1) * kLanes + lane) * 2 + (c & 1) : (nc & ~1) * kLanes + lane;
 }
 
-template <int NC>
+typedef double v2d_t __attribute__((ext_vector_type(2)));
+
+// NT: non-temporal (streaming) loads — qdata is read once per Mult, so it must not displace the
+// L-vectors that neighbouring elements / bricks re-read from L2.  Measured on k_brick_cg (64^3,
+// p = 2): 283 -> 245 us per launch, and the following CG update 42.7 -> 35.5 us (its vectors
+// are still cached); tools/ab.py brick_variant 0 vs 6 (6 = temporal loads, kept for A/B).
+template <int NC, bool NT = false>
 __device__ __forceinline__ void load_qp(const double *__restrict__ qp, int lane, double (&v)[NC])
 {
 #pragma unroll
     for (int p = 0; p < NC / 2; ++p) {
-        const double2 w = reinterpret_cast<const double2 *>(qp + p * 2 * kLanes)[lane];
-        v[2 * p] = w.x;
-        v[2 * p + 1] = w.y;
+        if constexpr (NT) {
+            const v2d_t w = __builtin_nontemporal_load(reinterpret_cast<const v2d_t *>(qp + p * 2 * kLanes) + lane);
+            v[2 * p] = w.x;
+            v[2 * p + 1] = w.y;
+        } else {
+            const double2 w = reinterpret_cast<const double2 *>(qp + p * 2 * kLanes)[lane];
+            v[2 * p] = w.x;
+            v[2 * p + 1] = w.y;
+        }
     }
-    if constexpr (NC & 1) v[NC - 1] = qp[(NC - 1) * kLanes + lane];
+    if constexpr (NC & 1) {
+        if constexpr (NT) v[NC - 1] = __builtin_nontemporal_load(qp + (NC - 1) * kLanes + lane);
+        else v[NC - 1] = qp[(NC - 1) * kLanes + lane];
+    }
 }
 
 // Y = A_e X for one element: X, Y lexicographic [dz][dy][dx]; q0 points at this element's
@@ -65,7 +80,7 @@ __device__ __forceinline__ void load_qp(const double *__restrict__ qp, int lane,
 // plane's worth of it live in registers.  QZU = unroll factor of the quadrature-plane loop
 // (Q1: straight-line code, the compiler hoists qdata loads across planes; 1: one plane's loads
 // in flight, ~250 VGPRs at p = 2, two waves per SIMD).
-template <int D1, int Q1, unsigned K, typename XL, int QZU = Q1>
+template <int D1, int Q1, unsigned K, typename XL, int QZU = Q1, bool NT = true>
 __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restrict__ q0, int lane,
                                              const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
 {
@@ -134,7 +149,7 @@ __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restr
                 }
                 const int q = qx + Q1 * (qy + Q1 * qz);
                 double qv[NC];
-                load_qp<NC>(q0 + (size_t)q * NC * kLanes, lane, qv);
+                load_qp<NC, NT>(q0 + (size_t)q * NC * kLanes, lane, qv);
                 double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
                 if constexpr (L::kD) {
                     gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;
@@ -241,7 +256,7 @@ __device__ __forceinline__ void elem_apply3d_lr(const XL &xl, const double *__re
                 }
                 const int q = qx + Q1 * (qy + Q1 * qz);
                 double qv[NC];
-                load_qp<NC>(q0 + (size_t)q * NC * kLanes, lane, qv);
+                load_qp<NC, true>(q0 + (size_t)q * NC * kLanes, lane, qv);
                 double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
                 if constexpr (L::kD) {
                     gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;

@@ -134,7 +134,7 @@ k_apply2d(const int32_t *__restrict__ map, const double *__restrict__ x,
             }
             const int q = qx + Q1 * qy;
             double qv[NC];
-            load_qp<NC>(q0 + (size_t)q * NC * kLanes, lane, qv);
+            load_qp<NC, true>(q0 + (size_t)q * NC * kLanes, lane, qv);
             double vv = 0.0, gx = 0.0, gy = 0.0;
             if constexpr (L::kD) {
                 gx = qv[0] * ux + qv[1] * uy;

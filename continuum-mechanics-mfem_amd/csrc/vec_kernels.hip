@@ -107,7 +107,7 @@ k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__rest
                 for (int b = 0; b < nyp; ++b)
                     for (int c = 0; c < nxp; ++c) {
                         const int64_t e = ex[c] + (int64_t)bx.nx * (ey[b] + (int64_t)bx.ny * ez[a]);
-                        v += Ye[e * ND + lx[c] + D1 * (ly[b] + D1 * lz[a])];
+                        v += Ye[e * ND + lx[c] + D1 * (ly[b] + D1 * lz[a])];  // gathers reuse lines: temporal
                     }
         }
         y[i] = v;
