@@ -320,7 +320,7 @@ def main():
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": ("k_brick_cg (brick patch gather + D/C/M PA apply + in-LDS E->L + d.Ad)" if args.path == "brick"
-                               else "k_apply3d_wpe (wave per element, LDS sum factorization)" if args.order >= 3
+                               else "k_apply3d_tile (Q1 x Q1 thread tile per element, z planes in registers)" if args.order >= 3
                                else "k_apply3d (fused L->E gather + D/C/M PA apply)"),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
                     "launches": cnt,

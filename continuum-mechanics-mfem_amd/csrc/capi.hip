@@ -108,6 +108,7 @@ void free_mesh(cdfem_ctx *c)
     c->gm_cap = 0;
     c->mesh_ready = c->pa_ready = c->dinv_ready = false;
     c->structured = false;
+    c->epencil = false;
 }
 
 // ---- profiling helpers ---------------------------------------------------------------------------
@@ -662,8 +663,10 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
         c->sx = nx; c->sy = ny; c->sz = nz;
         c->Lx = Lx; c->Ly = Ly; c->Lz = Lz;
         if (c->qlay == 1) {
-            // high order: keep the element-major layout; the E->L sum uses the lattice (k_e2l_box)
+            // high order: lattice gather in the apply, pencil E-vector layout, lattice E->L
+            // (k_e2l_box); element-major qdata and map are kept
             c->structured = true;
+            c->epencil = c->nl < ((int64_t)1 << 32);
             return CDFEM_OK;
         }
         c->nbx = (nx + kBrick - 1) / kBrick;
@@ -786,7 +789,8 @@ int cdfem_pa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kap
         c->ncomp = ((kinds & CDFEM_DIFFUSION) ? c->dim * (c->dim + 1) / 2 : 0) +
                    ((kinds & CDFEM_CONVECTION) ? c->dim : 0) + ((kinds & CDFEM_MASS) ? 1 : 0);
         const int nq = nq_of(c, c->rule_op);
-        c->d_qd = dalloc<double>((size_t)c->nblk * nq * c->ncomp * kLanes);
+        c->d_qd = c->qlay == 1 ? dalloc<double>((size_t)c->ne * c->rule_op.q1 * qd_ho_plane(c->ncomp, c->rule_op.q1))
+                               : dalloc<double>((size_t)c->nblk * nq * c->ncomp * kLanes);
         const size_t neq = (size_t)c->ne * nq;
         double *dk = nullptr, *dc = nullptr, *dm = nullptr;
         if (kappa_q) {
@@ -1206,12 +1210,16 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
         }
         switch (k) {
         case CDFEM_K_APPLY:
-            // x gather (each L-dof once) + qdata stream + element map + E-vector write
-            *bytes = 8.0 * nl + 8.0 * c->ncomp * nq * ne + 4.0 * nd * ne + 8.0 * nd * ne;
+            if (c->epencil)  // lattice gather: x + ess flags (each L-dof once) + qdata + E-vector write
+                *bytes = 9.0 * nl + 8.0 * c->ncomp * nq * ne + 8.0 * nd * ne;
+            else             // x gather (each L-dof once) + qdata stream + element map + E-vector write
+                *bytes = 8.0 * nl + 8.0 * c->ncomp * nq * ne + 4.0 * nd * ne + 8.0 * nd * ne;
             break;
         case CDFEM_K_E2L:
-            // E-vector read + positions + offsets + y write + x read (constraint / dot)
-            *bytes = 8.0 * nd * ne + 4.0 * nd * ne + 4.0 * nl + 8.0 * nl + 8.0 * nl;
+            if (c->epencil)  // E-vector read + ess flags + y write + x read (constraint / dot)
+                *bytes = 8.0 * nd * ne + 1.0 * nl + 8.0 * nl + 8.0 * nl;
+            else             // E-vector read + positions + offsets + y write + x read (constraint / dot)
+                *bytes = 8.0 * nd * ne + 4.0 * nd * ne + 4.0 * nl + 8.0 * nl + 8.0 * nl;
             break;
         case CDFEM_K_UPDATE: *bytes = 8.0 * nl * 8; break;     // x,d,r,z,dinv read; x,r,z write
         case CDFEM_K_DIRECTION: *bytes = 8.0 * nl * 3; break;  // z,d read; d write

@@ -50,6 +50,17 @@ Rule1D make_rule(int p, int q1);
 // MFEM default rule sizes on multilinear tensor elements (which: 0 operator, 1 LF, 2 L2 error)
 int rule_points_1d(int which, int dim, int p);
 
+// High-order qdata layout (cdfem_ctx::qlay = 1, 3D p >= 3, ho_kernels.hip): per element and
+// quadrature plane qz one block of nc * Q1^2 doubles (padded to an even count so every block is
+// 16-byte aligned), components paired as [pair][qxy][2] with an odd last component as [qxy].
+__host__ __device__ constexpr int qd_ho_plane(int nc, int q1) { return (nc * q1 * q1 + 1) & ~1; }
+__host__ __device__ inline size_t qd_ho_index(int64_t e, int c, int q, int nc, int q1)
+{
+    const int qq = q1 * q1, qz = q / qq, qxy = q - qz * qq;
+    const size_t base = ((size_t)e * q1 + qz) * qd_ho_plane(nc, q1);
+    return base + ((c < (nc & ~1)) ? ((size_t)(c >> 1) * qq + qxy) * 2 + (c & 1) : (size_t)(nc & ~1) * qq + qxy);
+}
+
 // Device-side Krylov state (one per context), updated only by kernels.
 struct KrylovState {
     double nom, nom0, den, alpha, beta, betanom, r0;
@@ -108,6 +119,7 @@ struct cdfem_ctx {
 
     // structured-box fast path (cdfem_mesh_set_structured): 4x4x4-element bricks
     bool structured = false;
+    bool epencil = false;               // qlay 1 on a structured box: pencil E-vector layout (ho_eidx)
     int sx = 0, sy = 0, sz = 0;         // elements per axis of the local box
     int nbx = 0, nby = 0, nbz = 0;      // bricks per axis
     int64_t Lx = 0, Ly = 0, Lz = 0;     // dof lattice per axis

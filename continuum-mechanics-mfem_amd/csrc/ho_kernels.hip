@@ -1,27 +1,35 @@
-// ho_kernels.hip — high-order (3D p = 3, 4) partial-assembly apply: ONE WAVEFRONT PER ELEMENT.
+// ho_kernels.hip — high-order (3D p = 3, 4) partial-assembly apply: one Q1 x Q1 THREAD TILE PER
+// ELEMENT, quadrature planes (z) in registers.
 //
 // BASELINE config C3 (128^3 hex, H1 order 4: D1 = 5 dofs and Q1 = 6 Gauss points per direction,
-// 125 dofs and 216 points per element).  Thread-per-element (pa_kernels.hip) would need ~700 live
-// doubles per thread, so here the 64 lanes of a wave share one element and every sum-factorisation
-// stage spreads its outputs over the lanes, with the intermediates in LDS:
-//   gather     X[dz][dy][dx]                       (125, from the element-major map)
-//   stage x    BX, GX  [dz][dy][qx]                (2 x 150)
-//   stage y    BB, BG, GB [dz][qy][qx]             (3 x 180)
-//   stage z    u, ux, uy, uz at (qz,qy,qx) and, in the same lane, the quadrature-point operator
-//              v0 = C.grad u + M u,  (vx,vy,vz) = D grad u   with the lane's qdata prefetched into
-//              registers at kernel entry (10 x 4 coalesced 512-byte loads per lane in flight while
-//              the gather and the first stages run)
-//   stage z^T  W0, Wx, Wy [dz][qy][qx]             (3 x 180)
-//   stage y^T  ZB, ZG [dz][dy][qx]                 (2 x 150)
-//   stage x^T  Y[dz][dy][dx] -> E-vector (element-major, coalesced), summed by k_e2l.
-// qdata layout (element-major, cdfem_ctx::qlay = 1): qd[(e * NC + c) * NQ + q], so a component of
-// 64 consecutive points is one 512-byte wave load.  LDS: (4 NQ + 3 D1 Q1^2) doubles per wave
-// (11.2 KB at p = 4), 4 waves (elements) per 256-thread block.
+// 125 dofs and 216 points per element).  Thread (tx, ty) of an element's 6 x 6 tile owns the
+// column of points (qx = tx, qy = ty, qz = 0..Q1-1):
+//   gather   X[dz][dy][dx]                    threads (dx, dy), 5 loads each        -> LDS
+//   stage x  BX, GX [dz][dy][qx]              threads (qx, dy)                      -> LDS
+//   stage y  bb, bg, gb [dz]                  threads (qx, qy), kept in registers
+//   stage z, quadrature-point operator and stage z^T, fused per plane qz, all in registers:
+//            u, ux, uy, uz = B_z/G_z contractions of the column;
+//            v0 = C.grad u + M u, (vx, vy, vz) = D grad u with this thread's qdata;
+//            w0[dz] += B[qz][dz] v0 + G[qz][dz] vz, wx[dz] += B vx, wy[dz] += B vy.
+//            The z tables are uniform across the block (kernel arguments, compile-time indices:
+//            scalar registers), so this stage reads no LDS at all.
+//   stage y^T ZB, ZG [dz][dy][qx]             threads (qx, dy)                      -> LDS
+//   stage x^T Y[dz][dy][dx] -> E-vector       threads (dx, dy); element-major (summed by k_e2l) or,
+//            on structured boxes, the pencil layout of ho_eidx (summed by k_e2l_box)
+// Four barriers per element.  The previous wave-per-element kernel kept every intermediate in
+// LDS and read the 1D tables from LDS in every FMA (~270 KB of LDS traffic per element, which
+// bounded it at 9.4 ms / 0.54 of HBM); this tile reads ~55 KB.
+//
+// qdata layout (cdfem_ctx::qlay = 1): qd_ho_index() — per element and plane qz one block of
+// nc x Q1^2 doubles with components paired ([pair][qxy][2]), so every thread reads its point's
+// components with 16-byte loads and an element's tile reads 576 contiguous bytes per pair.  The
+// whole element's qdata (Q1 planes) is issued at kernel entry, in flight behind the gather and the
+// x / y stages.  Streaming (non-temporal) loads keep the L-vector in L2 for the gathers.
 //
 // MFMA is not used: on gfx950 the f64 MFMA rate equals the f64 vector FMA rate
 // (MI355X_MICROARCH.md), and these contractions (6x5 by 5xN) fill at most 6/16 x 5/8 of a
-// 16x16x4 f64 tile, so the VALU path is the faster one; the kernel is bounded by the qdata stream
-// (HBM): 8 * 10 * 216 bytes per element against ~38 kflop.
+// 16x16x4 f64 tile; the kernel is bounded by the qdata stream (8 * 10 * 216 bytes per element
+// against ~20 k FMA).
 #include <hip/hip_runtime.h>
 
 #include "cdfem_internal.hpp"
@@ -29,195 +37,284 @@
 
 namespace cdfem {
 
-template <int D1, int Q1, unsigned K, bool CON>
+// structured-box geometry of the lattice gather / pencil E-vector (LAT = true)
+struct TileGeo {
+    HoLayout ho;
+    uint32_t Lx, Ly;
+    const uint8_t *ess;
+};
+
+template <int D1, int Q1, unsigned K, bool CON, bool LAT>
 __global__ void __launch_bounds__(256)
-k_apply3d_wpe(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qd,
-              double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const KrylovState *__restrict__ st)
+k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qd,
+               double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const TileGeo geo,
+               const KrylovState *__restrict__ st)
 {
     if (st != nullptr && st->done) return;
     using L = QLayout<K, 3>;
-    constexpr int ND = D1 * D1 * D1, NQ = Q1 * Q1 * Q1, NC = L::nc;
-    constexpr int S1 = D1 * D1 * Q1;  // stage x / y^T outputs per field
-    constexpr int S2 = D1 * Q1 * Q1;  // stage y / z^T outputs per field
-    constexpr int NA = 4 * NQ, NB = 3 * S2;
-    static_assert(NB >= ND && NA >= 2 * S1, "LDS buffer sizes");
-    constexpr int QI = (NQ + 63) / 64;
-    __shared__ double sB[Q1 * D1], sG[Q1 * D1];
-    __shared__ double bufA[4][NA];
-    __shared__ double bufB[4][NB];
+    constexpr int NC = L::nc, NP = NC / 2, QQ = Q1 * Q1, ND = D1 * D1 * D1;
+    constexpr int PS = qd_ho_plane(NC, Q1);  // doubles per (element, plane) block
+    constexpr int EPB = 256 / QQ;            // elements per block
+    constexpr int SA = 3 * D1 * QQ;          // X, then W0 / Wx / Wy [dz][qy][qx]
+    constexpr int SB = 2 * D1 * D1 * Q1;     // BX / GX, then ZB / ZG [dz][dy][qx]
+    static_assert(SA >= ND, "LDS buffer sizes");
+    __shared__ double sBt[Q1 * D1], sGt[Q1 * D1];
+    __shared__ double bufA[EPB][SA];
+    __shared__ double bufB[EPB][SB];
 
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int e = blockIdx.x * 4 + w;
-    const bool valid = e < ne;
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int q = 0; q < Q1; ++q)
-#pragma unroll
-            for (int d = 0; d < D1; ++d) {
-                sB[q * D1 + d] = T.B[q][d];
-                sG[q * D1 + d] = T.G[q][d];
-            }
+    const int le = threadIdx.x / QQ, t = threadIdx.x - le * QQ;
+    const int tx = t % Q1, ty = t / Q1;
+    const int e = blockIdx.x * EPB + le;
+    const bool valid = le < EPB && e < ne;
+    if (threadIdx.x < Q1 * D1) {
+        const int q = threadIdx.x / D1, d = threadIdx.x % D1;
+        sBt[threadIdx.x] = T.B[q][d];
+        sGt[threadIdx.x] = T.G[q][d];
     }
-    double *A = bufA[w], *Bf = bufB[w];
+    double *A = bufA[le < EPB ? le : 0], *Bf = bufB[le < EPB ? le : 0];
 
-    // qdata of this lane's points, in flight from here on
-    double qv[QI][NC];
+    // gather X[dz][dy][dx] (threads dx = tx, dy = ty) into registers FIRST: vmcnt retires in
+    // issue order, so loads issued before the qdata stream can be waited for without waiting for
+    // the stream.  All loads are unconditional (clamped indices), so gather, stream and the
+    // first wait share one basic block and the wait covers only the gather.  Structured boxes
+    // (LAT) address x by lattice arithmetic (no map, no dependent load); generic meshes read the
+    // element-major map.
+    const bool gthr = valid && tx < D1 && ty < D1;
+    const int ec = valid ? e : ne - 1;
+    const int gx = tx < D1 ? tx : D1 - 1, gy = ty < D1 ? ty : D1 - 1;
+    uint32_t ex = 0, ey = 0, ez = 0;
+    double xr[D1];
+    int32_t m[D1];  // LAT: ess flag; map path: map entry
+    if constexpr (LAT) {
+        const uint32_t r = fdiv((uint32_t)ec, geo.ho.fnx);
+        ex = (uint32_t)ec - r * geo.ho.nx;
+        ez = fdiv(r, geo.ho.fny);
+        ey = r - ez * geo.ho.ny;
+        constexpr int P = D1 - 1;
+        const size_t g0 = (size_t)(ex * P + gx) + (size_t)geo.Lx * ((ey * P + gy) + (size_t)geo.Ly * (ez * P));
+        const size_t sz = (size_t)geo.Lx * geo.Ly;
 #pragma unroll
-    for (int i = 0; i < QI; ++i) {
-        const int q = lane + 64 * i;
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-            qv[i][c] = (valid && q < NQ) ? qd[((size_t)e * NC + c) * NQ + q] : 0.0;  // (non-temporal measured 3 % slower)
-    }
-    // gather
-    if (valid) {
-        for (int l = lane; l < ND; l += 64) {
-            const int g = map[(size_t)e * ND + l];
-            double v;
-            if constexpr (CON) v = g < 0 ? 0.0 : x[g];
-            else v = x[g < 0 ? -g - 1 : g];
-            Bf[l] = v;
+        for (int dz = 0; dz < D1; ++dz) {
+            xr[dz] = x[g0 + dz * sz];
+            m[dz] = CON ? geo.ess[g0 + dz * sz] : 0;
         }
-    }
-    __syncthreads();
-    // stage x
-    for (int o = lane; o < S1; o += 64) {
-        const int qx = o % Q1, r = o / Q1;
-        double bx = 0.0, gx = 0.0;
+    } else {
+        const int32_t *me = map + (size_t)ec * ND + gy * D1 + gx;
 #pragma unroll
-        for (int dx = 0; dx < D1; ++dx) {
-            const double xv = Bf[r * D1 + dx];
-            bx += sB[qx * D1 + dx] * xv;
-            gx += sG[qx * D1 + dx] * xv;
-        }
-        A[o] = bx;
-        A[S1 + o] = gx;
-    }
-    __syncthreads();
-    // stage y
-    for (int o = lane; o < S2; o += 64) {
-        const int qx = o % Q1, qy = (o / Q1) % Q1, dz = o / (Q1 * Q1);
-        double bb = 0.0, bg = 0.0, gb = 0.0;
+        for (int dz = 0; dz < D1; ++dz) m[dz] = me[dz * D1 * D1];
 #pragma unroll
-        for (int dy = 0; dy < D1; ++dy) {
-            const int i = (dz * D1 + dy) * Q1 + qx;
-            const double bxv = A[i], gxv = A[S1 + i];
-            const double by = sB[qy * D1 + dy], gy = sG[qy * D1 + dy];
-            bb += by * bxv;
-            bg += by * gxv;
-            gb += gy * bxv;
-        }
-        Bf[o] = bb;
-        Bf[S2 + o] = bg;
-        Bf[2 * S2 + o] = gb;
+        for (int dz = 0; dz < D1; ++dz) xr[dz] = x[m[dz] < 0 ? -m[dz] - 1 : m[dz]];
     }
-    __syncthreads();
-    // stage z + quadrature-point operator (lane owns points lane + 64 i, as in the prefetch)
-#pragma unroll
-    for (int i = 0; i < QI; ++i) {
-        const int o = lane + 64 * i;
-        if (o < NQ) {
-            const int qxy = o % (Q1 * Q1), qz = o / (Q1 * Q1);
-            double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
-#pragma unroll
-            for (int dz = 0; dz < D1; ++dz) {
-                const int j = dz * Q1 * Q1 + qxy;
-                const double bz = sB[qz * D1 + dz], gz = sG[qz * D1 + dz];
-                const double bb = Bf[j];
-                u += bz * bb;
-                uz += gz * bb;
-                ux += bz * Bf[S2 + j];
-                uy += bz * Bf[2 * S2 + j];
-            }
-            double v0 = 0.0, vx = 0.0, vy = 0.0, vz = 0.0;
-            if constexpr (L::kD) {
-                const double d00 = qv[i][0], d01 = qv[i][1], d02 = qv[i][2];
-                const double d11 = qv[i][3], d12 = qv[i][4], d22 = qv[i][5];
-                vx = d00 * ux + d01 * uy + d02 * uz;
-                vy = d01 * ux + d11 * uy + d12 * uz;
-                vz = d02 * ux + d12 * uy + d22 * uz;
-            }
-            if constexpr (L::kC) v0 += qv[i][L::oC] * ux + qv[i][L::oC + 1] * uy + qv[i][L::oC + 2] * uz;
-            if constexpr (L::kM) v0 += qv[i][L::oM] * u;
-            A[o] = v0;
-            A[NQ + o] = vx;
-            A[2 * NQ + o] = vy;
-            A[3 * NQ + o] = vz;
-        }
-    }
-    __syncthreads();
-    // stage z^T
-    for (int o = lane; o < S2; o += 64) {
-        const int qxy = o % (Q1 * Q1), dz = o / (Q1 * Q1);
-        double w0 = 0.0, wx = 0.0, wy = 0.0;
+    // this thread's qdata, all planes, in flight from here on (the scheduling barrier keeps the
+    // gather loads ahead of the stream in issue order)
+    __builtin_amdgcn_sched_barrier(0);
+    double qv[Q1][NC];
+    {
+        const double *qe = qd + (size_t)ec * Q1 * PS;
 #pragma unroll
         for (int qz = 0; qz < Q1; ++qz) {
-            const int j = qz * Q1 * Q1 + qxy;
-            const double bz = sB[qz * D1 + dz], gz = sG[qz * D1 + dz];
-            w0 += bz * A[j] + gz * A[3 * NQ + j];
-            wx += bz * A[NQ + j];
-            wy += bz * A[2 * NQ + j];
+            const double *qp = qe + qz * PS;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const v2d_t w = __builtin_nontemporal_load(reinterpret_cast<const v2d_t *>(qp + p * 2 * QQ) + t);
+                qv[qz][2 * p] = w.x;
+                qv[qz][2 * p + 1] = w.y;
+            }
+            if constexpr (NC & 1) qv[qz][NC - 1] = __builtin_nontemporal_load(qp + 2 * NP * QQ + t);
         }
-        Bf[o] = w0;
-        Bf[S2 + o] = wx;
-        Bf[2 * S2 + o] = wy;
+    }
+    // unconditional store (a conditional one lets the compiler sink the gather loads behind the
+    // stream): threads outside the gather write into the unused tail of bufA
+    static_assert(ND + QQ * D1 <= SA, "junk slots");
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz) {
+        const bool zero = CON && (LAT ? m[dz] != 0 : m[dz] < 0);
+        A[gthr ? (dz * D1 + ty) * D1 + tx : ND + t * D1 + dz] = zero ? 0.0 : xr[dz];
     }
     __syncthreads();
-    // stage y^T
-    for (int o = lane; o < S1; o += 64) {
-        const int qx = o % Q1, dy = (o / Q1) % D1, dz = o / (Q1 * D1);
-        double zb = 0.0, zg = 0.0;
+    // stage x: threads (qx = tx, dy = ty)
+    if (valid && ty < D1) {
+        double b[D1], g[D1];
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) {
+            b[dx] = sBt[tx * D1 + dx];
+            g[dx] = sGt[tx * D1 + dx];
+        }
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            double bx = 0.0, gx = 0.0;
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                const double xv = A[(dz * D1 + ty) * D1 + dx];
+                bx += b[dx] * xv;
+                gx += g[dx] * xv;
+            }
+            Bf[(dz * D1 + ty) * Q1 + tx] = bx;
+            Bf[D1 * D1 * Q1 + (dz * D1 + ty) * Q1 + tx] = gx;
+        }
+    }
+    __syncthreads();
+    // stage y: threads (qx = tx, qy = ty), column over dz in registers
+    double bb[D1], bg[D1], gb[D1];
+    {
+        double by[D1], gy[D1];
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy) {
+            by[dy] = sBt[ty * D1 + dy];
+            gy[dy] = sGt[ty * D1 + dy];
+        }
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+            for (int dy = 0; dy < D1; ++dy) {
+                const int i = (dz * D1 + dy) * Q1 + tx;
+                const double bxv = Bf[i], gxv = Bf[D1 * D1 * Q1 + i];
+                s0 += by[dy] * bxv;
+                s1 += by[dy] * gxv;
+                s2 += gy[dy] * bxv;
+            }
+            bb[dz] = s0;
+            bg[dz] = s1;
+            gb[dz] = s2;
+        }
+    }
+    // stage z + quadrature-point operator + stage z^T, plane by plane in registers
+    double w0[D1], wx[D1], wy[D1];
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz) w0[dz] = wx[dz] = wy[dz] = 0.0;
+#pragma unroll
+    for (int qz = 0; qz < Q1; ++qz) {
+        double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            const double bz = T.B[qz][dz], gz = T.G[qz][dz];
+            u += bz * bb[dz];
+            uz += gz * bb[dz];
+            ux += bz * bg[dz];
+            uy += bz * gb[dz];
+        }
+        double v0 = 0.0, vx = 0.0, vy = 0.0, vz = 0.0;
+        if constexpr (L::kD) {
+            const double d00 = qv[qz][0], d01 = qv[qz][1], d02 = qv[qz][2];
+            const double d11 = qv[qz][3], d12 = qv[qz][4], d22 = qv[qz][5];
+            vx = d00 * ux + d01 * uy + d02 * uz;
+            vy = d01 * ux + d11 * uy + d12 * uz;
+            vz = d02 * ux + d12 * uy + d22 * uz;
+        }
+        if constexpr (L::kC) v0 += qv[qz][L::oC] * ux + qv[qz][L::oC + 1] * uy + qv[qz][L::oC + 2] * uz;
+        if constexpr (L::kM) v0 += qv[qz][L::oM] * u;
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            const double bz = T.B[qz][dz], gz = T.G[qz][dz];
+            w0[dz] += bz * v0 + gz * vz;
+            wx[dz] += bz * vx;
+            wy[dz] += bz * vy;
+        }
+    }
+    // X (bufA) was last read in stage x, before the previous barrier
+    if (le < EPB) {
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            A[dz * QQ + t] = w0[dz];
+            A[(D1 + dz) * QQ + t] = wx[dz];
+            A[(2 * D1 + dz) * QQ + t] = wy[dz];
+        }
+    }
+    __syncthreads();
+    // stage y^T: threads (qx = tx, dy = ty); BX / GX (bufB) were last read in stage y
+    if (valid && ty < D1) {
+        double cb[Q1], cg[Q1];
 #pragma unroll
         for (int qy = 0; qy < Q1; ++qy) {
-            const int j = (dz * Q1 + qy) * Q1 + qx;
-            const double by = sB[qy * D1 + dy], gy = sG[qy * D1 + dy];
-            zb += by * Bf[j] + gy * Bf[2 * S2 + j];
-            zg += by * Bf[S2 + j];
+            cb[qy] = sBt[qy * D1 + ty];
+            cg[qy] = sGt[qy * D1 + ty];
         }
-        A[o] = zb;
-        A[S1 + o] = zg;
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            double zb = 0.0, zg = 0.0;
+#pragma unroll
+            for (int qy = 0; qy < Q1; ++qy) {
+                const int j = dz * QQ + qy * Q1 + tx;
+                zb += cb[qy] * A[j] + cg[qy] * A[2 * D1 * QQ + j];
+                zg += cb[qy] * A[D1 * QQ + j];
+            }
+            Bf[(dz * D1 + ty) * Q1 + tx] = zb;
+            Bf[D1 * D1 * Q1 + (dz * D1 + ty) * Q1 + tx] = zg;
+        }
     }
     __syncthreads();
-    // stage x^T -> E-vector
-    if (valid) {
-        for (int o = lane; o < ND; o += 64) {
-            const int dx = o % D1, r = o / D1;
+    // stage x^T -> E-vector: threads (dx = tx, dy = ty)
+    if (valid && tx < D1 && ty < D1) {
+        double cb[Q1], cg[Q1];
+#pragma unroll
+        for (int qx = 0; qx < Q1; ++qx) {
+            cb[qx] = sBt[qx * D1 + tx];
+            cg[qx] = sGt[qx * D1 + tx];
+        }
+        double *ye;
+        size_t zs;  // stride between dz planes
+        if constexpr (LAT) {
+            const size_t row = (size_t)geo.ho.nx * D1;
+            ye = Ye + (((size_t)ez * D1 * geo.ho.ny + ey) * D1 + ty) * row + (size_t)ex * D1 + tx;
+            zs = (size_t)geo.ho.ny * D1 * row;
+        } else {
+            ye = Ye + (size_t)e * ND + ty * D1 + tx;
+            zs = D1 * D1;
+        }
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
             double y = 0.0;
 #pragma unroll
             for (int qx = 0; qx < Q1; ++qx) {
-                const int j = r * Q1 + qx;
-                y += sB[qx * D1 + dx] * A[j] + sG[qx * D1 + dx] * A[S1 + j];
+                const int j = (dz * D1 + ty) * Q1 + qx;
+                y += cb[qx] * Bf[j] + cg[qx] * Bf[D1 * D1 * Q1 + j];
             }
-            Ye[(size_t)e * ND + o] = y;
+            ye[dz * zs] = y;
         }
     }
 }
 
 template <int D1, int Q1, unsigned K>
-static hipError_t wpe_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
+static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
 {
     const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
-    const dim3 grid((unsigned)((c->ne + 3) / 4)), block(256);
-    if (con)
-        hipLaunchKernelGGL((k_apply3d_wpe<D1, Q1, K, true>), grid, block, 0, c->stream, c->d_map, x, c->d_qd, Ye, T,
-                           c->ne, st);
-    else
-        hipLaunchKernelGGL((k_apply3d_wpe<D1, Q1, K, false>), grid, block, 0, c->stream, c->d_map, x, c->d_qd, Ye,
-                           T, c->ne, st);
+    constexpr int EPB = 256 / (Q1 * Q1);
+    const dim3 grid((unsigned)((c->ne + EPB - 1) / EPB)), block(256);
+    TileGeo geo{};
+    geo.ho = ho_layout(c);
+    geo.Lx = (uint32_t)c->Lx;
+    geo.Ly = (uint32_t)c->Ly;
+    geo.ess = c->d_ess;
+    if (c->epencil) {
+        if (con)
+            hipLaunchKernelGGL((k_apply3d_tile<D1, Q1, K, true, true>), grid, block, 0, c->stream, c->d_map, x,
+                               c->d_qd, Ye, T, c->ne, geo, st);
+        else
+            hipLaunchKernelGGL((k_apply3d_tile<D1, Q1, K, false, true>), grid, block, 0, c->stream, c->d_map, x,
+                               c->d_qd, Ye, T, c->ne, geo, st);
+    } else {
+        if (con)
+            hipLaunchKernelGGL((k_apply3d_tile<D1, Q1, K, true, false>), grid, block, 0, c->stream, c->d_map, x,
+                               c->d_qd, Ye, T, c->ne, geo, st);
+        else
+            hipLaunchKernelGGL((k_apply3d_tile<D1, Q1, K, false, false>), grid, block, 0, c->stream, c->d_map, x,
+                               c->d_qd, Ye, T, c->ne, geo, st);
+    }
     return hipGetLastError();
 }
 
 template <int D1, int Q1>
-static hipError_t wpe_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
+static hipError_t tile_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
 {
     switch (c->kinds) {
-    case 1: return wpe_kinds<D1, Q1, 1>(c, x, Ye, con, st);
-    case 2: return wpe_kinds<D1, Q1, 2>(c, x, Ye, con, st);
-    case 3: return wpe_kinds<D1, Q1, 3>(c, x, Ye, con, st);
-    case 4: return wpe_kinds<D1, Q1, 4>(c, x, Ye, con, st);
-    case 5: return wpe_kinds<D1, Q1, 5>(c, x, Ye, con, st);
-    case 6: return wpe_kinds<D1, Q1, 6>(c, x, Ye, con, st);
-    case 7: return wpe_kinds<D1, Q1, 7>(c, x, Ye, con, st);
+    case 1: return tile_kinds<D1, Q1, 1>(c, x, Ye, con, st);
+    case 2: return tile_kinds<D1, Q1, 2>(c, x, Ye, con, st);
+    case 3: return tile_kinds<D1, Q1, 3>(c, x, Ye, con, st);
+    case 4: return tile_kinds<D1, Q1, 4>(c, x, Ye, con, st);
+    case 5: return tile_kinds<D1, Q1, 5>(c, x, Ye, con, st);
+    case 6: return tile_kinds<D1, Q1, 6>(c, x, Ye, con, st);
+    case 7: return tile_kinds<D1, Q1, 7>(c, x, Ye, con, st);
     default: return hipErrorInvalidValue;
     }
 }
@@ -225,8 +322,8 @@ static hipError_t wpe_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, co
 hipError_t launch_apply_wpe(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
 {
     const int q1 = c->rule_op.q1;
-    if (c->p == 3 && q1 == 5) return wpe_dq<4, 5>(c, x, Ye, con, st);
-    if (c->p == 4 && q1 == 6) return wpe_dq<5, 6>(c, x, Ye, con, st);
+    if (c->p == 3 && q1 == 5) return tile_dq<4, 5>(c, x, Ye, con, st);
+    if (c->p == 4 && q1 == 6) return tile_dq<5, 6>(c, x, Ye, con, st);
     return hipErrorInvalidValue;
 }
 

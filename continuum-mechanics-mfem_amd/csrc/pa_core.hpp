@@ -313,4 +313,33 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f)
     return (uint32_t)(((uint64_t)n * f.m) >> f.k);
 }
 
+// E-vector index of (element e, local dof l) on the high-order layout (qlay = 1, 3D p >= 3).
+// Generic meshes: element-major [e][l].  Structured boxes (pencil != 0, cdfem_mesh_set_structured):
+// [ez][dz][ey][dy][ex][dx], so every x-row of the dof lattice is ONE contiguous run of the
+// E-vector (its element-boundary dofs are adjacent pairs) and k_e2l_box reads it coalesced.
+struct HoLayout {
+    uint32_t pencil, nx, ny, d1;
+    FastDiv fnx, fny;
+};
+__device__ __forceinline__ size_t ho_eidx(const HoLayout &h, uint32_t e, int l)
+{
+    const int d1 = (int)h.d1;
+    if (!h.pencil) return (size_t)e * (d1 * d1 * d1) + l;
+    const uint32_t r = fdiv(e, h.fnx), ex = e - r * h.nx;
+    const uint32_t ez = fdiv(r, h.fny), ey = r - ez * h.ny;
+    const int dx = l % d1, dy = (l / d1) % d1, dz = l / (d1 * d1);
+    return ((((size_t)ez * d1 + dz) * h.ny + ey) * d1 + dy) * ((size_t)h.nx * d1) + (size_t)ex * d1 + dx;
+}
+inline HoLayout ho_layout(const cdfem_ctx *c)
+{
+    HoLayout h{};
+    h.pencil = c->epencil ? 1u : 0u;
+    h.d1 = (uint32_t)c->d1;
+    h.nx = (uint32_t)(c->epencil ? c->sx : 1);
+    h.ny = (uint32_t)(c->epencil ? c->sy : 1);
+    h.fnx = make_fastdiv(h.nx);
+    h.fny = make_fastdiv(h.ny);
+    return h;
+}
+
 }  // namespace cdfem

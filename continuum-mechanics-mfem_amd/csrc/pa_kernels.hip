@@ -257,7 +257,7 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
     double *out = qd + ((size_t)b * nq + q) * nc * kLanes;
     // component k of this point: block layout (qd_offset) or element-major [e][k][q]
     auto put = [&](int k, double v) {
-        if (qlay == 1) qd[((size_t)e * nc + k) * nq + q] = v;
+        if (qlay == 1) qd[qd_ho_index(e, k, q, nc, q1)] = v;
         else out[qd_offset(k, lane, nc)] = v;
     };
     if (e < 0 || e >= ne) {
@@ -333,7 +333,7 @@ __device__ inline void basis_at(int l, int q, int dim, const Rule1D &r, double &
 template <int DIM>
 __global__ void __launch_bounds__(256)
 k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int ne, int nblk, int nd, int qlay,
-            const Rule1D r, unsigned kinds, int nc, double *__restrict__ Ye)
+            const HoLayout ho, const Rule1D r, unsigned kinds, int nc, double *__restrict__ Ye)
 {
     const int q1 = r.q1;
     const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
@@ -350,7 +350,7 @@ k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int
     for (int q = 0; q < nq; ++q) {
         const double *qb = qd + ((size_t)b * nq + q) * nc * kLanes;
         auto qq = [&](int k) {
-            return qlay == 1 ? qd[((size_t)e * nc + k) * nq + q] : qb[qd_offset(k, lane, nc)];
+            return qlay == 1 ? qd[qd_ho_index(e, k, q, nc, q1)] : qb[qd_offset(k, lane, nc)];
         };
         double phi, g[3];
         basis_at(l, q, DIM, r, phi, g);
@@ -373,7 +373,7 @@ k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int
         }
         if (kinds & CDFEM_MASS) acc += qq(oM) * phi * phi;
     }
-    if (qlay == 1) Ye[(size_t)e * nd + l] = acc;
+    if (qlay == 1) Ye[ho_eidx(ho, (uint32_t)e, l)] = acc;
     else Ye[t] = acc;  // t == (b*nd + l)*64 + lane
 }
 
@@ -381,7 +381,7 @@ k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int
 template <int DIM>
 __global__ void __launch_bounds__(256)
 k_lf_elem(const double *__restrict__ verts, const int32_t *__restrict__ perm, int ne, int nblk, int nd, int qlay,
-          const Rule1D r,
+          const HoLayout ho, const Rule1D r,
           const double *__restrict__ fq, double *__restrict__ Ye)
 {
     const int q1 = r.q1;
@@ -404,7 +404,7 @@ k_lf_elem(const double *__restrict__ verts, const int32_t *__restrict__ perm, in
         }
     }
     if (qlay == 1) {
-        if (e >= 0 && e < ne) Ye[(size_t)e * nd + l] = acc;
+        if (e >= 0 && e < ne) Ye[ho_eidx(ho, (uint32_t)e, l)] = acc;
     } else {
         Ye[t] = acc;
     }
@@ -453,10 +453,10 @@ hipError_t launch_diag_elem(cdfem_ctx *c, double *Ye)
     const int64_t n = (int64_t)c->nblk * c->nd * kLanes;
     if (c->dim == 3)
         hipLaunchKernelGGL(k_diag_elem<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_qd, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, c->rule_op, c->kinds, c->ncomp, Ye);
+                           c->d_qd, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, ho_layout(c), c->rule_op, c->kinds, c->ncomp, Ye);
     else
         hipLaunchKernelGGL(k_diag_elem<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_qd, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, c->rule_op, c->kinds, c->ncomp, Ye);
+                           c->d_qd, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, ho_layout(c), c->rule_op, c->kinds, c->ncomp, Ye);
     return hipGetLastError();
 }
 
@@ -465,10 +465,10 @@ hipError_t launch_lf_elem(cdfem_ctx *c, const double *d_fq, double *Ye)
     const int64_t n = (int64_t)c->nblk * c->nd * kLanes;
     if (c->dim == 3)
         hipLaunchKernelGGL(k_lf_elem<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, c->rule_lf, d_fq, Ye);
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, ho_layout(c), c->rule_lf, d_fq, Ye);
     else
         hipLaunchKernelGGL(k_lf_elem<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
-                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, c->rule_lf, d_fq, Ye);
+                           c->d_verts, c->d_perm, c->ne, c->nblk, c->nd, c->qlay, ho_layout(c), c->rule_lf, d_fq, Ye);
     return hipGetLastError();
 }
 

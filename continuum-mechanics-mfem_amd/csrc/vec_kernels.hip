@@ -9,6 +9,8 @@
 // only every `check_every` iterations.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "cdfem_internal.hpp"
 #include "pa_core.hpp"
 #include "reduce.hpp"
@@ -47,8 +49,9 @@ k_e2l(const int32_t *__restrict__ off, const int32_t *__restrict__ pos,
 }
 
 // ------------------------------------------------------------------------------------------------
-// E->L on a structured box with the element-major E-vector (3D, p >= 3): the (element, local dof)
-// pairs of a dof follow from its lattice coordinates, so no position arrays are read.  Per axis a
+// E->L on a structured box with the pencil E-vector (3D, p >= 3, ho_eidx): the (element, local
+// dof) pairs of a dof follow from its lattice coordinates, so no position arrays are read, and the
+// contributions to consecutive dofs of an x-row are consecutive E-vector entries (coalesced).  Per axis a
 // lattice coordinate g lies in one element (interior) or two (element boundary); the pairs are
 // visited z-outer / x-inner = ascending element index, the order of the generic k_e2l, so both
 // give bitwise-identical sums.
@@ -85,33 +88,43 @@ k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__rest
           const double *__restrict__ x, double *__restrict__ y, int64_t nl, double *__restrict__ part,
           KrylovState *__restrict__ st)
 {
-    constexpr int D1 = P + 1, ND = D1 * D1 * D1;
+    // one wave per x-row (gy, gz) of the dof lattice (grid-stride over rows): the y / z element
+    // pairs are uniform across the wave, lanes run along x, and the row's contributions are one
+    // contiguous run of the pencil E-vector (entries gx + ex - 1 and gx + ex, ex = gx / P)
+    constexpr int D1 = P + 1;
     __shared__ double sh[kRedThreads / 64];
     if (CG && st->done) return;
     double acc = 0.0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
-        double v;
-        if (CON && ess[i]) {
-            v = x[i];
-        } else {
-            const uint32_t ii = (uint32_t)i;
-            const uint32_t gz = fdiv(ii, bx.fLxy), rem = ii - gz * bx.Lx * bx.Ly;
-            const uint32_t gy = fdiv(rem, bx.fLx), gx = rem - gy * bx.Lx;
-            int ex[2], lx[2], ey[2], ly[2], ez[2], lz[2];
-            const int nxp = axis_pairs<P>(gx, bx.nx, ex, lx);
-            const int nyp = axis_pairs<P>(gy, bx.ny, ey, ly);
-            const int nzp = axis_pairs<P>(gz, bx.nz, ez, lz);
-            v = 0.0;
-            for (int a = 0; a < nzp; ++a)
-                for (int b = 0; b < nyp; ++b)
-                    for (int c = 0; c < nxp; ++c) {
-                        const int64_t e = ex[c] + (int64_t)bx.nx * (ey[b] + (int64_t)bx.ny * ez[a]);
-                        v += Ye[e * ND + lx[c] + D1 * (ly[b] + D1 * lz[a])];  // gathers reuse lines: temporal
-                    }
+    const int lane = threadIdx.x & 63;
+    const uint32_t rows = bx.Ly * (uint32_t)(nl / ((int64_t)bx.Lx * bx.Ly));
+    const uint32_t ew = bx.nx * D1;  // E-vector row length
+    for (uint32_t r = blockIdx.x * (kRedThreads / 64) + (threadIdx.x >> 6); r < rows;
+         r += gridDim.x * (kRedThreads / 64)) {
+        const uint32_t gz = r / bx.Ly, gy = r - gz * bx.Ly;
+        int ey[2], ly[2], ez[2], lz[2];
+        const int nyp = axis_pairs<P>(gy, bx.ny, ey, ly);
+        const int nzp = axis_pairs<P>(gz, bx.nz, ez, lz);
+        int64_t erow[4];
+        int ne_rows = 0;
+        for (int a = 0; a < nzp; ++a)
+            for (int b = 0; b < nyp; ++b)
+                erow[ne_rows++] = (((int64_t)(ez[a] * D1 + lz[a]) * bx.ny + ey[b]) * D1 + ly[b]) * ew;
+        const int64_t lrow = (int64_t)r * bx.Lx;
+#pragma unroll 3
+        for (uint32_t gx = lane; gx < bx.Lx; gx += 64) {
+            const uint32_t ex = gx / P, lx = gx - ex * P;
+            const bool left = lx == 0 && ex > 0, right = lx != 0 || ex < bx.nx;
+            const int64_t i = lrow + gx;
+            double v = 0.0;
+            for (int k = 0; k < ne_rows; ++k) {
+                const double *er = Ye + erow[k] + gx + ex;
+                if (left) v += er[-1];
+                if (right) v += er[0];
+            }
+            if (CON && ess[i]) v = x[i];
+            y[i] = v;
+            if (CG) acc += v * x[i];
         }
-        y[i] = v;
-        if (CG) acc += v * x[i];
     }
     if (!CG) return;
     store_partial(block_sum(acc, sh), part);
@@ -368,7 +381,8 @@ hipError_t launch_update_fin(cdfem_ctx *c, int nparts)
 template <int P>
 static hipError_t launch_e2l_box(cdfem_ctx *c, const double *Ye, const double *x, double *y, bool con, int cg_mode)
 {
-    const dim3 g(red_grid(c, c->nl)), b(kRedThreads);
+    const int64_t rows = c->Ly * c->Lz;
+    const dim3 g((unsigned)std::min<int64_t>((rows + 3) / 4, 65536)), b(kRedThreads);
     BoxE2L bx;
     bx.Lx = (uint32_t)c->Lx;
     bx.Ly = (uint32_t)c->Ly;
