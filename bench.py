@@ -54,16 +54,18 @@ def parse():
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--path", choices=["brick", "generic"], default=None,
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
-    ap.add_argument("--config", choices=["c2", "c3", "c4"], default="c2",
-                    help="c2: 64^3 hex p=2 PA + CG (BASELINE metric config); c3: 128^3 hex p=4 PA + CG "
-                         "(configs[2]); c4: Kuhn 55^3 x 6 tets P2, FA CSR + GMRES(30)/Jacobi (configs[3])")
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2: 64^3 hex p=2 PA + CG (BASELINE metric config; N>1: weak scaling, a 64^3 slab "
+                         "per rank); c3: 128^3 hex p=4 PA + CG (configs[2]); c4: Kuhn 55^3 x 6 tets P2, FA CSR "
+                         "+ GMRES(30)/Jacobi (configs[3]); c5: 256^3 hex p=2 PA + CG split into N z-slabs "
+                         "(configs[4] at N=8: 256 x 256 x 32 per rank)")
     ap.add_argument("--tet-n", type=int, default=55, help="c4: cubes per direction (6 tets each)")
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N>1 data-path communicator: rccl (production, one GPU per rank) or host "
                          "(gloo callbacks; rehearses the N>1 flow with several ranks on one GPU)")
     a = ap.parse_args()
     c3 = a.config == "c3"
-    a.n = a.n or (128 if c3 else 64)
+    a.n = a.n or (128 if c3 else 256 if a.config == "c5" else 64)
     a.order = a.order or (4 if c3 else 2)
     a.cg_iters = a.cg_iters or (20 if c3 else 100)
     a.path = a.path or ("brick" if a.order <= 2 else "generic")
@@ -239,14 +241,20 @@ def main():
     import cdfem
 
     n, p = args.n, args.order
-    # weak scaling: rank r owns elements iz in [r n, (r+1) n) of an n x n x (world n) mesh
-    nz = n * world
-    mesh = cdfem.box_mesh(3, (n, n, nz), p, z_range=(rank * n, (rank + 1) * n), with_coords=False)
+    if args.config == "c5":
+        # configs[4]: one n^3 mesh split into `world` z-slabs (n x n x n/world elements per rank)
+        if n % world:
+            raise SystemExit(f"c5: {n} element layers do not split over {world} ranks")
+        nzr, nz = n // world, n
+    else:
+        # weak scaling: rank r owns elements iz in [r n, (r+1) n) of an n x n x (world n) mesh
+        nzr, nz = n, n * world
+    mesh = cdfem.box_mesh(3, (n, n, nz), p, z_range=(rank * nzr, (rank + 1) * nzr), with_coords=False)
     ndev = cdfem.device_count()
     ctx = cdfem.Context(local % ndev if args.comm == "host" else local)
     ctx.upload_mesh(mesh)
     if args.path == "brick" or p >= 3:
-        ctx.set_structured(n, n, n)  # p >= 3: structured E->L (no position arrays)
+        ctx.set_structured(n, n, nzr)  # p >= 3: structured E->L (no position arrays)
     if world > 1:
         if args.path != "brick":
             raise SystemExit("multi-GPU runs use the structured brick path")
@@ -372,18 +380,22 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(args, n, p, args.kinds)
+                # c5: the 256^3 FA matrix is out of the host's reach; per-DoF rate on the 64^3 mesh
+                cpu = cpu_baseline(args, min(n, 64), p, args.kinds)
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"error": repr(e)}
         out = {
             "metric": "DoF-iter/s (CG, 3D p=2 hex convection-diffusion) + achieved HBM GB/s",
             "value": value, "unit": "DoF-iter/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "scaling": "strong" if args.config == "c5" else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
             "config": {"workload": f"{n}x{n}x{nz} hex, H1 p={p}, PA D+C+M (kinds={args.kinds}), "
                                    f"Jacobi-CG {args.cg_iters} it/step",
                        "dofs": total_dofs, "elements": n * n * nz, "cg_iters_per_step": args.cg_iters,
                        "parallelism": f"slab{world}" if world > 1 else "single", "path": args.path,
+                       "series": "strong: fixed n^3 split into z-slabs" if args.config == "c5"
+                                 else "weak: an n^3 slab per rank",
                        **({"comm": args.comm} if world > 1 else {})},
             "roofline": roof, "cpu_baseline": cpu,
         }

@@ -448,11 +448,12 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         const int rem = gid - gz * plane;
         const int gy = (int)fdiv((uint32_t)rem, fdx);
         const int gx = rem - gy * g.Lx;
-        const double di = d[gid];
+        // every load is issued before any is consumed: which of q / the face partials holds this
+        // dof's row sum depends on its lattice position only, and the essential flag selects last
+        const double di = d[gid], xi = x[gid], rold = r[gid], mi = dinv[gid];
+        const bool is_ess = ess[gid] != 0;
         double qi;
-        if (ess[gid]) {
-            qi = di;
-        } else if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
+        if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
             int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
             const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
             if (gx - qx * s1 == 0) {
@@ -477,14 +478,14 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         } else {
             qi = q[gid];
         }
-        if (!ess[gid]) {  // interface planes: add the neighbour rank's partial sums
-            if (remote_lo && gz == 0) qi += remote_lo[rem];
-            if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
-        }
-        x[gid] += alpha * di;
-        const double ri = r[gid] - alpha * qi;
+        // interface planes: add the neighbour rank's partial sums
+        if (remote_lo && gz == 0) qi += remote_lo[rem];
+        if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
+        if (is_ess) qi = di;
+        x[gid] = xi + alpha * di;
+        const double ri = rold - alpha * qi;
         r[gid] = ri;
-        if (!(zlo_shared && gz == 0)) acc += ri * (dinv[gid] * ri);
+        if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
     }
     const double bs = block_sum(acc, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = bs;

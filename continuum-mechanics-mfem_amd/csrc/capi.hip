@@ -1122,6 +1122,29 @@ int cdfem_stream_bench(cdfem_ctx *c, int mode, size_t bytes, int reps, double *g
     });
 }
 
+int cdfem_fp64_bench(cdfem_ctx *c, int mode, int reps, double *tflops)
+{
+    return guarded(c, [&] {
+        if (!tflops || reps < 1 || mode < 0 || mode > 1) throw ArgError("bad fp64 bench arguments");
+        double *out = dalloc<double>(1), flops = 0.0;
+        HIPCHK(launch_fp64_probe(c, mode, out, &flops));  // warm-up
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipEventRecord(e0, c->stream));
+        for (int i = 0; i < reps; ++i) HIPCHK(launch_fp64_probe(c, mode, out, &flops));
+        HIPCHK(hipEventRecord(e1, c->stream));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        dfree(out);
+        *tflops = flops * reps / (ms * 1e-3) / 1e12;
+        return CDFEM_OK;
+    });
+}
+
 int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
 {
     return guarded(c, [&] {
@@ -1130,6 +1153,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         if (k == "brick_variant") {
             if (value < 0 || value > 6) throw ArgError("brick_variant must be 0..6");
             c->brick_variant = value;
+        } else if (k == "spmv_variant") {
+            if (value < 0 || value > 1) throw ArgError("spmv_variant must be 0..1");
+            c->spmv_variant = value;
         } else if (k == "profile_mask") {
             c->prof_mask = (unsigned)value;
         } else if (k == "brick_waves") {

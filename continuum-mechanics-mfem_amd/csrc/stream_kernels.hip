@@ -79,6 +79,60 @@ __global__ void __launch_bounds__(64) k_stream_ileave(const double *__restrict__
     if (s == 12345.678) out[0] = s + pad[0];
 }
 
+// ---- f64 compute-rate probes (VALU vs MFMA for the high-order contractions) ----
+// VALU: 8 independent v_fma_f64 chains per lane.  MFMA: 4 independent v_mfma_f64_16x16x4_f64
+// accumulators per wave (16 x 16 x 4 x 2 = 2048 flop per instruction).  ITERS loop trips; the
+// results are written under an impossible condition so nothing is dead-code eliminated.
+constexpr int kFp64Iters = 4096;
+__global__ void __launch_bounds__(256) k_fp64_valu(double seed, double *out)
+{
+    double a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = seed + threadIdx.x + k;
+    const double m = 1.0 + 1e-9 * seed, c = 1e-12;
+    for (int i = 0; i < kFp64Iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] = fma(a[k], m, c);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += a[k];
+    if (s == 12345.678) out[0] = s;
+}
+
+typedef double v4d_t __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) k_fp64_mfma(double seed, double *out)
+{
+    const double a = seed + (threadIdx.x & 63), b = 1.0 + 1e-9 * seed;
+    v4d_t acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = v4d_t{0.0, 0.0, 0.0, (double)k};
+    for (int i = 0; i < kFp64Iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+    if (s == 12345.678) out[0] = s;
+}
+
+hipError_t launch_fp64_probe(cdfem_ctx *c, int mode, double *out, double *flops)
+{
+    const dim3 grid(256 * 8), block(256);
+    const double waves = (double)grid.x * (block.x / 64);
+    if (mode == 0) {
+        hipLaunchKernelGGL(k_fp64_valu, grid, block, 0, c->stream, 1.0, out);
+        *flops = waves * 64.0 * 8.0 * 2.0 * kFp64Iters;
+    } else if (mode == 1) {
+        hipLaunchKernelGGL(k_fp64_mfma, grid, block, 0, c->stream, 1.0, out);
+        *flops = waves * 4.0 * 2048.0 * kFp64Iters;
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n)
 {
     const dim3 grid(256 * 16), block(256);

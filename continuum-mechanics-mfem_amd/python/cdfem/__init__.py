@@ -84,6 +84,7 @@ def _declare(L):
         "cdfem_solve": (C.c_int, [vp, C.POINTER(SolverParams), vp, vp, C.c_int, C.POINTER(SolverResult)]),
         "cdfem_set_option": (C.c_int, [vp, C.c_char_p, C.c_int]),
         "cdfem_stream_bench": (C.c_int, [vp, C.c_int, C.c_size_t, C.c_int, _dp]),
+        "cdfem_fp64_bench": (C.c_int, [vp, C.c_int, C.c_int, _dp]),
         "cdfem_profile_enable": (C.c_int, [vp, C.c_int]),
         "cdfem_profile_reset": (C.c_int, [vp]),
         "cdfem_profile_read": (C.c_int, [vp, C.c_int, _dp, C.POINTER(i64)]),
@@ -456,6 +457,12 @@ class Context:
         g = C.c_double()
         self._chk(self.L.cdfem_stream_bench(self.h, int(mode), int(nbytes), int(reps), C.byref(g)))
         return g.value
+
+    def fp64_bench(self, mode=0, reps=10):
+        """Achieved f64 TFLOP/s of a compute probe: mode 0 VALU v_fma_f64, 1 v_mfma_f64_16x16x4_f64."""
+        t = C.c_double()
+        self._chk(self.L.cdfem_fp64_bench(self.h, int(mode), int(reps), C.byref(t)))
+        return t.value
 
     def set_option(self, key, value):
         self._chk(self.L.cdfem_set_option(self.h, key.encode(), int(value)))

@@ -184,6 +184,11 @@ int cdfem_solve(cdfem_ctx *ctx, const cdfem_solver_params *prm, const double *B,
  * per-wave work (8 / 4 loads in flight, one wave per SIMD) on an interleaved layout.            */
 int cdfem_stream_bench(cdfem_ctx *ctx, int mode, size_t bytes, int reps, double *gbps);
 
+/* f64 compute-rate probe (diagnostic; backs DESIGN.md's VALU-vs-MFMA choice for the high-order
+ * contractions): mode 0 = v_fma_f64 (8 independent chains per lane), 1 = v_mfma_f64_16x16x4_f64
+ * (4 independent accumulators per wave); *tflops = achieved f64 TFLOP/s over `reps` launches. */
+int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
+
 /* ---- tuning knobs (performance only; results identical to rounding) --------------------------
  * "brick_waves": 1 or 2 — register budget of the structured Mult kernel (waves per SIMD).
  * "profile_mask": bit k set = kernel slot k (CDFEM_K_*) gets HIP events while profiling is on
