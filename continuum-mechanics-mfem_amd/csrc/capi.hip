@@ -242,6 +242,18 @@ void op_apply(cdfem_ctx *c, const double *x, double *y, bool constrained)
     prof_mark(c, CDFEM_K_E2L, false);
 }
 
+// the operator on the global (all-rank) space, rank-local L-vectors: the local apply, then the
+// shared planes summed with the neighbours (MFEM P^T A P on the true dofs, then P), and for the
+// constrained operator the essential rows reset to the identity (an essential dof on a shared
+// plane was set by both ranks, so the sum doubled it)
+void op_apply_global(cdfem_ctx *c, const double *x, double *y, bool constrained)
+{
+    op_apply(c, x, y, constrained);
+    if (!multi_rank(c)) return;
+    interface_sum(c, y);
+    if (constrained) HIPCHK(launch_set_ess(c, y, x));
+}
+
 // copy-in helper: returns a device pointer holding n doubles of src (staging when on host)
 const double *dev_in(cdfem_ctx *c, const double *src, int where, double *staging, size_t n)
 {
@@ -416,7 +428,6 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
 void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, double *dX,
                  cdfem_solver_result &res)
 {
-    if (multi_rank(c)) throw UnsupportedError("GMRES on a multi-rank partition is not available yet");
     const int m = p.restart > 0 ? p.restart : 30;
     if (m > kGmMaxRestart) throw ArgError("restart > 64");
     const int64_t n = c->nl;
@@ -454,14 +465,14 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     HIPCHK(launch_gm_init(c, st, m, p.max_iter));
     for (bool first = true;; first = false) {
         // v0 = M^{-1}(b - A x); x = 0 on the first cycle, so A x is skipped there
-        if (!first) op_apply(c, x, w, true);
+        if (!first) op_apply_global(c, x, w, true);
         HIPCHK(launch_gm_residual(c, dB, first ? nullptr : w, dinv, V, part, st, first, p.rel_tol, p.abs_tol));
         post(0);
         if (wait(0).done) break;
         for (int j = 0; j < m; ++j) {
-            op_apply(c, V + (int64_t)j * n, w, true);
+            op_apply_global(c, V + (int64_t)j * n, w, true);
             prof_mark(c, CDFEM_K_ORTH, true);
-            HIPCHK(launch_gm_orth(c, w, dinv, V, n, part, st));
+            HIPCHK(launch_gm_orth(c, w, dinv, V, n, part, st, m));
             prof_mark(c, CDFEM_K_ORTH, false);
             post(j & 1);
             if (j > 0 && wait((j - 1) & 1).cycle_done) break;
@@ -995,10 +1006,7 @@ int cdfem_pa_mult(cdfem_ctx *c, const double *x, double *y, int constrained, int
         if (!x || !y) throw ArgError("null vector");
         const double *dx = dev_in(c, x, where, c->d_w[0], c->nl);
         double *dy = where == CDFEM_DEVICE ? y : c->d_w[1];
-        if (multi_rank(c) && constrained)
-            throw UnsupportedError("constrained Mult across ranks: use cdfem_solve");
-        op_apply(c, dx, dy, constrained != 0);
-        interface_sum(c, dy);  // shared planes: add the neighbour's partial sums
+        op_apply_global(c, dx, dy, constrained != 0);  // shared planes: neighbours' partial sums added
         dev_out(c, y, where, dy, c->nl);
         prof_collect(c);
         return CDFEM_OK;
@@ -1153,9 +1161,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         if (k == "brick_variant") {
             if (value < 0 || value > 6) throw ArgError("brick_variant must be 0..6");
             c->brick_variant = value;
-        } else if (k == "spmv_variant") {
-            if (value < 0 || value > 1) throw ArgError("spmv_variant must be 0..1");
-            c->spmv_variant = value;
+
         } else if (k == "profile_mask") {
             c->prof_mask = (unsigned)value;
         } else if (k == "brick_waves") {

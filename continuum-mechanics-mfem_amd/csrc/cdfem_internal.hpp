@@ -61,17 +61,6 @@ __host__ __device__ inline size_t qd_ho_index(int64_t e, int c, int q, int nc, i
     return base + ((c < (nc & ~1)) ? ((size_t)(c >> 1) * qq + qxy) * 2 + (c & 1) : (size_t)(nc & ~1) * qq + qxy);
 }
 
-// XCD-aware workgroup order: the dispatcher sends workgroup b to XCD b % 8, so consecutive
-// workgroups land on different L2s.  xcd_remap() is a bijection on [0, G) that gives every XCD a
-// CONTIGUOUS range of logical workgroups, so data shared by neighbouring workgroups (gathered
-// vector entries of a banded matrix) is fetched into one L2 instead of eight.
-constexpr int kXcds = 8;
-__host__ __device__ inline unsigned xcd_remap(unsigned b, unsigned G)
-{
-    const unsigned x = b % kXcds, k = b / kXcds, q = G / kXcds, r = G % kXcds;
-    return x * q + (x < r ? x : r) + k;
-}
-
 // Device-side Krylov state (one per context), updated only by kernels.
 struct KrylovState {
     double nom, nom0, den, alpha, beta, betanom, r0;
@@ -92,6 +81,7 @@ struct GmresState {
     double s[kGmMaxRestart + 1];   // basis scales: v_i = s_i * V_i
     double g[kGmMaxRestart + 1], cs[kGmMaxRestart], sn[kGmMaxRestart];
     double H[(kGmMaxRestart + 1) * kGmMaxRestart];  // row-major, leading dimension kGmMaxRestart
+    double red[kGmMaxRestart + 1];  // multi-rank: rank-local sums awaiting the all-reduce
 };
 constexpr size_t kGmPollBytes = 32;
 
@@ -139,7 +129,6 @@ struct cdfem_ctx {
     double *d_dalt = nullptr;           // second search-direction buffer (brick CG)
     int nface = 0;                      // F
     int brick_waves = 2;                // register budget of k_brick3d (CDFEM_BRICK_WAVES)
-    int spmv_variant = 1;               // SELL SpMV: 0 dispatch order, 1 XCD-contiguous slices
     int brick_variant = 0;              // element core of k_brick_cg (0 unrolled, 1 plane loop, 2 low-reg)
     int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)
     int zhi_shared = 0;                 // local gz=Lz-1 plane shared with the rank above
@@ -297,7 +286,7 @@ hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it);
 hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
                               double *part, GmresState *st, bool first, double rtol, double atol);
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st);
+                          GmresState *st, int m);
 hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st);
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 // f64 compute-rate probes: mode 0 VALU v_fma_f64, 1 v_mfma_f64_16x16x4_f64; *flops per launch

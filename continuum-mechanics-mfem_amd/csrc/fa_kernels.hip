@@ -354,7 +354,7 @@ k_sell_fill(const int32_t *__restrict__ smap, const double *__restrict__ vals, c
 // y = A x on the SELL-64 layout: one wave per 64-row slice, one lane per row, entries of a row
 // summed in CSR order; every value/column load is one coalesced 512/256-byte wave access.
 // CG mode: partials of (x, y) and early exit once the Krylov state is done.
-template <bool CG, bool XCD>
+template <bool CG>
 __global__ void __launch_bounds__(256)
 k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows, const int32_t *__restrict__ scols,
             const double *__restrict__ svals, const double *__restrict__ x, double *__restrict__ y, int64_t nslices,
@@ -363,8 +363,7 @@ k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows,
     __shared__ double sh[256 / 64];
     if (CG && st->done) return;
     const int lane = threadIdx.x & 63;
-    const unsigned blk = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int64_t sl = (int64_t)blk * 4 + (threadIdx.x >> 6);
+    const int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     double dd = 0.0;
     if (sl < nslices) {
         const int32_t b = sptr[sl], len = (sptr[sl + 1] - b) >> 6;
@@ -461,8 +460,7 @@ unsigned sell_grid(const cdfem_ctx *c) { return (unsigned)((c->nslices + 3) / 4)
 
 hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y)
 {
-    auto k = c->spmv_variant == 1 ? k_sell_spmv<false, true> : k_sell_spmv<false, false>;
-    hipLaunchKernelGGL(k, dim3(sell_grid(c)), dim3(256), 0, c->stream, c->d_sptr, c->d_srows,
+    hipLaunchKernelGGL((k_sell_spmv<false>), dim3(sell_grid(c)), dim3(256), 0, c->stream, c->d_sptr, c->d_srows,
                        c->d_scols, constrained ? c->d_svals_c : c->d_svals, x, y, c->nslices, nullptr, nullptr);
     return hipGetLastError();
 }
@@ -470,8 +468,7 @@ hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *
 // q = A_c d and the den partials, then the MFEM CG den step (one-block finalizer)
 hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q)
 {
-    auto k = c->spmv_variant == 1 ? k_sell_spmv<true, true> : k_sell_spmv<true, false>;
-    hipLaunchKernelGGL(k, dim3(sell_grid(c)), dim3(256), 0, c->stream, c->d_sptr, c->d_srows,
+    hipLaunchKernelGGL((k_sell_spmv<true>), dim3(sell_grid(c)), dim3(256), 0, c->stream, c->d_sptr, c->d_srows,
                        c->d_scols, c->d_svals_c, d, q, c->nslices, c->d_part, c->d_state);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

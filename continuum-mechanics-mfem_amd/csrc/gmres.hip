@@ -33,7 +33,8 @@ int gmres_blocks(int64_t n) { return (int)((n + kGmChunk - 1) / kGmChunk); }
 // ---- v0 = M^{-1} (b - A x) and partials of |v0|^2 ------------------------------------------------
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_residual(const double *__restrict__ b, const double *__restrict__ Ax, const double *__restrict__ dinv,
-              double *__restrict__ v0, int64_t n, double *__restrict__ part, const GmresState *__restrict__ st)
+              double *__restrict__ v0, int64_t n, int64_t skip_lo, double *__restrict__ part,
+              const GmresState *__restrict__ st)
 {
     __shared__ double sh[kRedThreads / 64];
     if (st->done) return;
@@ -46,7 +47,7 @@ k_gm_residual(const double *__restrict__ b, const double *__restrict__ Ax, const
             double r = Ax ? b[k] - Ax[k] : b[k];
             if (dinv) r *= dinv[k];
             v0[k] = r;
-            acc += r * r;
+            if (k >= skip_lo) acc += r * r;  // shared plane owned by the rank below
         }
     }
     store_partial(block_sum(acc, sh), part);
@@ -55,11 +56,16 @@ k_gm_residual(const double *__restrict__ b, const double *__restrict__ Ax, const
 // ---- start of a cycle: beta = |v0|, first-cycle tolerance, convergence / max_it test ------------
 __global__ void __launch_bounds__(1024)
 k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st, int first, double rtol,
-           double atol)
+           double atol, int mode)
 {
     __shared__ double sh[1024 / 64];
-    const double sum = sum_partials(part, nb, sh);
-    if (threadIdx.x != 0 || st->done) return;
+    const double sum = mode == 2 ? st->red[0] : sum_partials(part, nb, sh);
+    if (threadIdx.x != 0) return;
+    if (mode == 1) {  // multi-rank: local sum, all-reduced before the mode-2 launch
+        st->red[0] = sum;
+        return;
+    }
+    if (st->done) return;
     const double beta = sqrt(sum);
     st->res = beta;
     if (first) {
@@ -89,7 +95,7 @@ k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st,
 // flight, one LDS exchange + barrier per batch (not per basis vector).
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double *__restrict__ V, int64_t n,
-           int64_t ldv, double *__restrict__ part, int nb, const GmresState *__restrict__ st)
+           int64_t ldv, int64_t skip_lo, double *__restrict__ part, int nb, const GmresState *__restrict__ st)
 {
     __shared__ double sh[kGmBatch][kRedThreads / 64];
     if (st->cycle_done) return;
@@ -107,7 +113,7 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
             if (dinv) v *= dinv[k];
             w[k] = v;
         }
-        wv[e] = v;
+        wv[e] = k >= skip_lo ? v : 0.0;  // projections: owned entries only
     }
     for (int i0 = 0; i0 <= j; i0 += kGmBatch) {
         double acc[kGmBatch];
@@ -141,22 +147,29 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
 
 // ---- H[i][j] = s_i * sum_b part[i][b], one wave per i (fixed order) ------------------------------
 __global__ void __launch_bounds__(1024)
-k_gm_dots_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ st)
+k_gm_dots_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ st, int mode)
 {
     if (st->cycle_done) return;
     const int j = st->j;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int i = wv; i <= j; i += 16) {
+    if (mode == 2) {  // multi-rank: H[i][j] from the all-reduced sums
+        if (threadIdx.x <= j) st->H[threadIdx.x * kGmMaxRestart + j] = st->s[threadIdx.x] * st->red[threadIdx.x];
+        return;
+    }
+    for (int i = wv; i <= st->m; i += 16) {
         double v = 0.0;
-        for (int b = lane; b < nb; b += 64) v += part[(int64_t)i * nb + b];
+        if (i <= j)
+            for (int b = lane; b < nb; b += 64) v += part[(int64_t)i * nb + b];
         v = wave_sum(v);
-        if (lane == 0) st->H[i * kGmMaxRestart + j] = st->s[i] * v;
+        if (lane != 0) continue;
+        if (mode == 1) st->red[i] = v;  // multi-rank: local sums (zero past j), all-reduced next
+        else if (i <= j) st->H[i * kGmMaxRestart + j] = st->s[i] * v;
     }
 }
 
 // ---- pass 2: V_{j+1} = w - sum_i H[i][j] s_i V_i, partials of |V_{j+1}|^2 ------------------------
 __global__ void __launch_bounds__(kRedThreads)
-k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int64_t ldv,
+k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int64_t ldv, int64_t skip_lo,
            double *__restrict__ part, const GmresState *__restrict__ st)
 {
     __shared__ double sh[kRedThreads / 64];
@@ -186,7 +199,7 @@ k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int6
         const int64_t k = base + (int64_t)e * kRedThreads;
         if (k < n) {
             vn[k] = acc[e];
-            nrm += acc[e] * acc[e];
+            if (k >= skip_lo) nrm += acc[e] * acc[e];
         }
     }
     store_partial(block_sum(nrm, sh), part);
@@ -194,12 +207,16 @@ k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int6
 
 // ---- h_{j+1,j}, Givens rotations, residual estimate, cycle control ------------------------------
 __global__ void __launch_bounds__(1024)
-k_gm_norm_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ st)
+k_gm_norm_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ st, int mode)
 {
     __shared__ double sh[1024 / 64];
     if (st->cycle_done) return;  // uniform: every thread reads the same flag before the reduction
-    const double sum = sum_partials(part, nb, sh);
+    const double sum = mode == 2 ? st->red[0] : sum_partials(part, nb, sh);
     if (threadIdx.x != 0) return;
+    if (mode == 1) {  // multi-rank: local sum, all-reduced before the mode-2 launch
+        st->red[0] = sum;
+        return;
+    }
     constexpr int LD = kGmMaxRestart;
     const int j = st->j;
     double *H = st->H;
@@ -288,25 +305,46 @@ hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it)
     return hipGetLastError();
 }
 
+// multi-rank: partial sums -> local sum (mode 1) -> all-reduce over ranks -> scalar logic (mode 2);
+// every rank then runs the same scalar arithmetic on the same sums and takes the same branches
+static int64_t owned_from(const cdfem_ctx *c) { return c->zlo_shared ? c->Lx * c->Ly : 0; }
+static double *red_of(GmresState *st) { return st->red; }
+
 hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
                               double *part, GmresState *st, bool first, double rtol, double atol)
 {
     const int nb = gmres_blocks(c->nl);
+    const bool mr = multi_rank(c);
     hipLaunchKernelGGL(k_gm_residual, dim3(nb), dim3(kRedThreads), 0, c->stream, b, Ax, dinv, v0,
-                       (int64_t)c->nl, part, st);
-    hipLaunchKernelGGL(k_gm_start, dim3(1), dim3(1024), 0, c->stream, part, nb, st, first ? 1 : 0, rtol, atol);
+                       (int64_t)c->nl, owned_from(c), part, st);
+    hipLaunchKernelGGL(k_gm_start, dim3(1), dim3(1024), 0, c->stream, part, nb, st, first ? 1 : 0, rtol, atol,
+                       mr ? 1 : 0);
+    if (mr) {
+        comm_allreduce(c, red_of(st), 1);
+        hipLaunchKernelGGL(k_gm_start, dim3(1), dim3(1024), 0, c->stream, part, nb, st, first ? 1 : 0, rtol, atol, 2);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st)
+                          GmresState *st, int m)
 {
     const int nb = gmres_blocks(c->nl);
     const int64_t n = c->nl;
-    hipLaunchKernelGGL(k_gm_pass1, dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv, part, nb, st);
-    hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st);
-    hipLaunchKernelGGL(k_gm_pass2, dim3(nb), dim3(kRedThreads), 0, c->stream, w, V, n, ldv, part, st);
-    hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st);
+    const bool mr = multi_rank(c);
+    hipLaunchKernelGGL(k_gm_pass1, dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv, owned_from(c), part,
+                       nb, st);
+    hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, mr ? 1 : 0);
+    if (mr) {
+        comm_allreduce(c, red_of(st), m + 1);
+        hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2);
+    }
+    hipLaunchKernelGGL(k_gm_pass2, dim3(nb), dim3(kRedThreads), 0, c->stream, w, V, n, ldv, owned_from(c), part, st);
+    hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, mr ? 1 : 0);
+    if (mr) {
+        comm_allreduce(c, red_of(st), 1);
+        hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2);
+    }
     return hipGetLastError();
 }
 

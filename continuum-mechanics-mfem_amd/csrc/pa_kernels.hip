@@ -329,7 +329,8 @@ __device__ inline void basis_at(int l, int q, int dim, const Rule1D &r, double &
     }
 }
 
-// PA diagonal, element part: thread per (block, l, lane); Ye layout [b][l][lane]
+// PA diagonal, element part: thread per (block, l, lane), Ye layout [b][l][lane]; element-major
+// (qlay 1): thread per (e, l), Ye at ho_eidx(e, l)
 template <int DIM>
 __global__ void __launch_bounds__(256)
 k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int ne, int nblk, int nd, int qlay,
@@ -339,13 +340,15 @@ k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int
     const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)nblk * nd * kLanes) return;
-    const int lane = (int)(t % kLanes);
-    const int l = (int)((t / kLanes) % nd);
-    const int b = (int)(t / ((int64_t)kLanes * nd));
+    // element blocks: lane = element; element-major (qlay 1): consecutive threads share an
+    // element (l fastest), so every qdata read of a wave is one broadcast address
+    const int lane = qlay == 1 ? 0 : (int)(t % kLanes);
+    const int l = qlay == 1 ? (int)(t % nd) : (int)((t / kLanes) % nd);
+    const int b = qlay == 1 ? 0 : (int)(t / ((int64_t)kLanes * nd));
     const int oC = (kinds & CDFEM_DIFFUSION) ? DIM * (DIM + 1) / 2 : 0;
     const int oM = oC + ((kinds & CDFEM_CONVECTION) ? DIM : 0);
-    const int e = perm[(size_t)b * kLanes + lane];
-    if (qlay == 1 && (e < 0 || e >= ne)) return;
+    const int e = qlay == 1 ? (int)(t / nd) : perm[(size_t)b * kLanes + lane];
+    if (qlay == 1 && e >= ne) return;
     double acc = 0.0;
     for (int q = 0; q < nq; ++q) {
         const double *qb = qd + ((size_t)b * nq + q) * nc * kLanes;
@@ -388,10 +391,11 @@ k_lf_elem(const double *__restrict__ verts, const int32_t *__restrict__ perm, in
     const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)nblk * nd * kLanes) return;
-    const int lane = (int)(t % kLanes);
-    const int l = (int)((t / kLanes) % nd);
-    const int b = (int)(t / ((int64_t)kLanes * nd));
-    const int e = perm[(size_t)b * kLanes + lane];
+    // element-major (qlay 1): thread per (e, l), l fastest (as k_diag_elem)
+    const int lane = qlay == 1 ? 0 : (int)(t % kLanes);
+    const int l = qlay == 1 ? (int)(t % nd) : (int)((t / kLanes) % nd);
+    const int b = qlay == 1 ? 0 : (int)(t / ((int64_t)kLanes * nd));
+    const int e = qlay == 1 ? (int)(t / nd) : perm[(size_t)b * kLanes + lane];
     double acc = 0.0;
     if (e >= 0 && e < ne) {
         for (int q = 0; q < nq; ++q) {
