@@ -451,10 +451,9 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     }
     double *x = c->d_w[2], *w = c->d_w[4], *V = c->d_gm, *part = c->d_gm_part;
     GmresState *st = c->d_gmst, *poll = c->h_gmpoll;
-    auto post = [&](int slot) {
-        HIPCHK(hipMemcpyAsync(&poll[slot], st, kGmPollBytes, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipEventRecord(c->gm_ev[slot], c->stream));
-    };
+    // the step's last scalar kernel has written poll[slot] (post_poll in gmres.hip); the event
+    // marks its completion for the host
+    auto post = [&](int slot) { HIPCHK(hipEventRecord(c->gm_ev[slot], c->stream)); };
     auto wait = [&](int slot) -> const GmresState & {
         HIPCHK(hipEventSynchronize(c->gm_ev[slot]));
         return poll[slot];
@@ -466,19 +465,20 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     for (bool first = true;; first = false) {
         // v0 = M^{-1}(b - A x); x = 0 on the first cycle, so A x is skipped there
         if (!first) op_apply_global(c, x, w, true);
-        HIPCHK(launch_gm_residual(c, dB, first ? nullptr : w, dinv, V, part, st, first, p.rel_tol, p.abs_tol));
+        HIPCHK(launch_gm_residual(c, dB, first ? nullptr : w, dinv, V, part, st, first, p.rel_tol, p.abs_tol,
+                                  &poll[0]));
         post(0);
         if (wait(0).done) break;
         for (int j = 0; j < m; ++j) {
             op_apply_global(c, V + (int64_t)j * n, w, true);
             prof_mark(c, CDFEM_K_ORTH, true);
-            HIPCHK(launch_gm_orth(c, w, dinv, V, n, part, st, m));
+            HIPCHK(launch_gm_orth(c, w, dinv, V, n, part, st, m, &poll[j & 1]));
             prof_mark(c, CDFEM_K_ORTH, false);
             post(j & 1);
             if (j > 0 && wait((j - 1) & 1).cycle_done) break;
         }
         prof_mark(c, CDFEM_K_UPDATE, true);
-        HIPCHK(launch_gm_update(c, x, V, n, st));
+        HIPCHK(launch_gm_update(c, x, V, n, st, &poll[0]));
         prof_mark(c, CDFEM_K_UPDATE, false);
         post(0);
         if (wait(0).done) break;

@@ -283,11 +283,12 @@ hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q);
 // GMRES(m) (gmres.hip)
 int gmres_blocks(int64_t n);
 hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it);
+// poll: pinned host slot the step's last scalar kernel writes the state head into (solve_gmres)
 hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
-                              double *part, GmresState *st, bool first, double rtol, double atol);
+                              double *part, GmresState *st, bool first, double rtol, double atol, GmresState *poll);
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m);
-hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st);
+                          GmresState *st, int m, GmresState *poll);
+hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st, GmresState *poll);
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 // f64 compute-rate probes: mode 0 VALU v_fma_f64, 1 v_mfma_f64_16x16x4_f64; *flops per launch
 hipError_t launch_fp64_probe(cdfem_ctx *c, int mode, double *out, double *flops);

@@ -53,10 +53,27 @@ k_gm_residual(const double *__restrict__ b, const double *__restrict__ Ax, const
     store_partial(block_sum(acc, sh), part);
 }
 
+// host poll without a copy kernel: the last scalar kernel of every polled step writes the head of
+// the state (kGmPollBytes: cycle_done, done, converged, its, res, j, kk) straight into the
+// pinned host slot the host will wait on (hipHostMalloc memory is device-visible).  A D2H
+// hipMemcpyAsync of the same 32 bytes cost a 4 us blit kernel per GMRES step.
+__device__ inline void post_poll(const GmresState *st, GmresState *poll)
+{
+    if (!poll) return;
+    poll->cycle_done = st->cycle_done;
+    poll->done = st->done;
+    poll->converged = st->converged;
+    poll->its = st->its;
+    poll->res = st->res;
+    poll->j = st->j;
+    poll->kk = st->kk;
+    __threadfence_system();
+}
+
 // ---- start of a cycle: beta = |v0|, first-cycle tolerance, convergence / max_it test ------------
 __global__ void __launch_bounds__(1024)
 k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st, int first, double rtol,
-           double atol, int mode)
+           double atol, int mode, GmresState *__restrict__ poll)
 {
     __shared__ double sh[1024 / 64];
     const double sum = mode == 2 ? st->red[0] : sum_partials(part, nb, sh);
@@ -65,29 +82,29 @@ k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st,
         st->red[0] = sum;
         return;
     }
-    if (st->done) return;
-    const double beta = sqrt(sum);
-    st->res = beta;
-    if (first) {
-        st->ttol = fmax(rtol * beta, atol);
-        st->res0 = beta;
+    if (!st->done) {
+        const double beta = sqrt(sum);
+        st->res = beta;
+        if (first) {
+            st->ttol = fmax(rtol * beta, atol);
+            st->res0 = beta;
+        }
+        st->cycle_done = 1;
+        if (beta <= st->ttol || beta == 0.0) {
+            st->converged = 1;
+            st->done = 1;
+        } else if (st->its >= st->max_it) {
+            st->done = 1;
+        } else {
+            st->s[0] = 1.0 / beta;
+            for (int i = 0; i <= st->m; ++i) st->g[i] = 0.0;
+            st->g[0] = beta;
+            st->j = 0;
+            st->kk = 0;
+            st->cycle_done = 0;
+        }
     }
-    st->cycle_done = 1;
-    if (beta <= st->ttol || beta == 0.0) {
-        st->converged = 1;
-        st->done = 1;
-        return;
-    }
-    if (st->its >= st->max_it) {
-        st->done = 1;
-        return;
-    }
-    st->s[0] = 1.0 / beta;
-    for (int i = 0; i <= st->m; ++i) st->g[i] = 0.0;
-    st->g[0] = beta;
-    st->j = 0;
-    st->kk = 0;
-    st->cycle_done = 0;
+    post_poll(st, poll);
 }
 
 // ---- pass 1: w = s_j M^{-1} A V_j (in place over the apply output), partial (w, V_i), i <= j ----
@@ -157,9 +174,18 @@ k_gm_dots_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ 
         return;
     }
     for (int i = wv; i <= st->m; i += 16) {
-        double v = 0.0;
-        if (i <= j)
-            for (int b = lane; b < nb; b += 64) v += part[(int64_t)i * nb + b];
+        // 8 independent partial loads per lane in flight, combined in a fixed order
+        double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        if (i <= j) {
+            const double *pi = part + (int64_t)i * nb;
+            int b = lane;
+            for (; b + 7 * 64 < nb; b += 8 * 64) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) a[u] += pi[b + u * 64];
+            }
+            for (int u = 0; b < nb; b += 64, ++u) a[u] += pi[b];
+        }
+        double v = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
         v = wave_sum(v);
         if (lane != 0) continue;
         if (mode == 1) st->red[i] = v;  // multi-rank: local sums (zero past j), all-reduced next
@@ -207,40 +233,56 @@ k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int6
 
 // ---- h_{j+1,j}, Givens rotations, residual estimate, cycle control ------------------------------
 __global__ void __launch_bounds__(1024)
-k_gm_norm_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ st, int mode)
+k_gm_norm_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ st, int mode,
+              GmresState *__restrict__ poll)
 {
+    constexpr int LD = kGmMaxRestart;
     __shared__ double sh[1024 / 64];
-    if (st->cycle_done) return;  // uniform: every thread reads the same flag before the reduction
-    const double sum = mode == 2 ? st->red[0] : sum_partials(part, nb, sh);
+    __shared__ double hc[kGmMaxRestart + 1], cs[kGmMaxRestart], sn[kGmMaxRestart];
+    if (st->cycle_done) {  // uniform: every thread reads the same flag before the reduction
+        if (threadIdx.x == 0 && mode != 1) post_poll(st, poll);
+        return;
+    }
+    const int j = st->j;
+    // the Hessenberg column and the rotations so far, loaded in parallel into LDS: the serial
+    // rotation sequence below then runs on LDS instead of dependent global loads
+    if ((int)threadIdx.x <= j) hc[threadIdx.x] = st->H[threadIdx.x * LD + j];
+    if ((int)threadIdx.x < j) {
+        cs[threadIdx.x] = st->cs[threadIdx.x];
+        sn[threadIdx.x] = st->sn[threadIdx.x];
+    }
+    const double sum = mode == 2 ? st->red[0] : sum_partials(part, nb, sh);  // (contains a barrier)
+    if (mode == 2) __syncthreads();
     if (threadIdx.x != 0) return;
     if (mode == 1) {  // multi-rank: local sum, all-reduced before the mode-2 launch
         st->red[0] = sum;
         return;
     }
-    constexpr int LD = kGmMaxRestart;
-    const int j = st->j;
-    double *H = st->H;
     const double hn = sqrt(sum);
-    H[(j + 1) * LD + j] = hn;
+    hc[j + 1] = hn;
     for (int i = 0; i < j; ++i) {
-        const double a = H[i * LD + j], c2 = H[(i + 1) * LD + j];
-        H[i * LD + j] = st->cs[i] * a + st->sn[i] * c2;
-        H[(i + 1) * LD + j] = -st->sn[i] * a + st->cs[i] * c2;
+        const double a = hc[i], c2 = hc[i + 1];
+        hc[i] = cs[i] * a + sn[i] * c2;
+        hc[i + 1] = -sn[i] * a + cs[i] * c2;
     }
-    const double a = H[j * LD + j], c2 = H[(j + 1) * LD + j];
+    const double a = hc[j], c2 = hc[j + 1];
     const double rr = sqrt(a * a + c2 * c2);
-    st->cs[j] = (rr == 0.0) ? 1.0 : a / rr;
-    st->sn[j] = (rr == 0.0) ? 0.0 : c2 / rr;
-    H[j * LD + j] = rr;
-    H[(j + 1) * LD + j] = 0.0;
-    st->g[j + 1] = -st->sn[j] * st->g[j];
-    st->g[j] = st->cs[j] * st->g[j];
-    st->res = fabs(st->g[j + 1]);
+    const double cj = (rr == 0.0) ? 1.0 : a / rr, sj = (rr == 0.0) ? 0.0 : c2 / rr;
+    st->cs[j] = cj;
+    st->sn[j] = sj;
+    hc[j] = rr;
+    hc[j + 1] = 0.0;
+    for (int i = 0; i <= j + 1; ++i) st->H[i * LD + j] = hc[i];
+    const double gj = st->g[j];
+    st->g[j + 1] = -sj * gj;
+    st->g[j] = cj * gj;
+    st->res = fabs(-sj * gj);
     st->kk = j + 1;
     st->its += 1;
     st->s[j + 1] = (hn != 0.0) ? 1.0 / hn : 0.0;
     st->j = j + 1;
     if (hn == 0.0 || st->res <= st->ttol || j + 1 == st->m || st->its >= st->max_it) st->cycle_done = 1;
+    post_poll(st, poll);
 }
 
 // ---- end of cycle: y = H_k^{-1} g_k (every block, redundantly: k <= 64), x += sum_i y_i s_i V_i --
@@ -272,15 +314,17 @@ k_gm_update(double *__restrict__ x, const double *__restrict__ V, int64_t n, int
     }
 }
 
-__global__ void k_gm_cycle_end(GmresState *__restrict__ st)
+__global__ void k_gm_cycle_end(GmresState *__restrict__ st, GmresState *__restrict__ poll)
 {
-    if (st->done) return;
-    if (st->res <= st->ttol) {
-        st->converged = 1;
-        st->done = 1;
-    } else if (st->its >= st->max_it) {
-        st->done = 1;
+    if (!st->done) {
+        if (st->res <= st->ttol) {
+            st->converged = 1;
+            st->done = 1;
+        } else if (st->its >= st->max_it) {
+            st->done = 1;
+        }
     }
+    post_poll(st, poll);
 }
 
 __global__ void k_gm_init(GmresState *__restrict__ st, int m, int max_it)
@@ -311,23 +355,24 @@ static int64_t owned_from(const cdfem_ctx *c) { return c->zlo_shared ? c->Lx * c
 static double *red_of(GmresState *st) { return st->red; }
 
 hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
-                              double *part, GmresState *st, bool first, double rtol, double atol)
+                              double *part, GmresState *st, bool first, double rtol, double atol, GmresState *poll)
 {
     const int nb = gmres_blocks(c->nl);
     const bool mr = multi_rank(c);
     hipLaunchKernelGGL(k_gm_residual, dim3(nb), dim3(kRedThreads), 0, c->stream, b, Ax, dinv, v0,
                        (int64_t)c->nl, owned_from(c), part, st);
     hipLaunchKernelGGL(k_gm_start, dim3(1), dim3(1024), 0, c->stream, part, nb, st, first ? 1 : 0, rtol, atol,
-                       mr ? 1 : 0);
+                       mr ? 1 : 0, mr ? nullptr : poll);
     if (mr) {
         comm_allreduce(c, red_of(st), 1);
-        hipLaunchKernelGGL(k_gm_start, dim3(1), dim3(1024), 0, c->stream, part, nb, st, first ? 1 : 0, rtol, atol, 2);
+        hipLaunchKernelGGL(k_gm_start, dim3(1), dim3(1024), 0, c->stream, part, nb, st, first ? 1 : 0, rtol, atol, 2,
+                           poll);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m)
+                          GmresState *st, int m, GmresState *poll)
 {
     const int nb = gmres_blocks(c->nl);
     const int64_t n = c->nl;
@@ -340,19 +385,20 @@ hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V
         hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2);
     }
     hipLaunchKernelGGL(k_gm_pass2, dim3(nb), dim3(kRedThreads), 0, c->stream, w, V, n, ldv, owned_from(c), part, st);
-    hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, mr ? 1 : 0);
+    hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, mr ? 1 : 0,
+                       mr ? nullptr : poll);
     if (mr) {
         comm_allreduce(c, red_of(st), 1);
-        hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2);
+        hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2, poll);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st)
+hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st, GmresState *poll)
 {
     const int nb = gmres_blocks(c->nl);
     hipLaunchKernelGGL(k_gm_update, dim3(nb), dim3(kRedThreads), 0, c->stream, x, V, (int64_t)c->nl, ldv, st);
-    hipLaunchKernelGGL(k_gm_cycle_end, dim3(1), dim3(1), 0, c->stream, st);
+    hipLaunchKernelGGL(k_gm_cycle_end, dim3(1), dim3(1), 0, c->stream, st, poll);
     return hipGetLastError();
 }
 
