@@ -123,9 +123,14 @@ void prof_mark(cdfem_ctx *c, int k, bool begin)
         s.ev.push_back(e);
     }
     if (begin) {
+        // recorded now AND armed: a CDFEM_LAUNCH before the end mark re-records the pair tightly
+        // around its own dispatch; any other launch leaves the plain event interval
         HIPCHK(hipEventRecord(s.ev[2 * s.used], c->stream));
+        c->ext_ev[0] = s.ev[2 * s.used];
+        c->ext_ev[1] = s.ev[2 * s.used + 1];
     } else {
-        HIPCHK(hipEventRecord(s.ev[2 * s.used + 1], c->stream));
+        if (c->ext_ev[0]) HIPCHK(hipEventRecord(s.ev[2 * s.used + 1], c->stream));  // not consumed
+        c->ext_ev[0] = c->ext_ev[1] = nullptr;
         s.used++;
     }
 }

@@ -12,6 +12,7 @@
 // Every wave reads 512 contiguous bytes per qdata component, so the dominant stream is fully
 // coalesced; the x gather is served by L2/MALL (x is 17 MB at 64^3 p=2).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -186,7 +187,24 @@ struct cdfem_ctx {
     bool profile = false;
     cdfem::ProfileSlot prof[CDFEM_K_COUNT];
     unsigned prof_mask = ~0u;  // kernels that get HIP events while profiling (set_option profile_mask)
+    hipEvent_t ext_ev[2] = {};  // armed by prof_mark(begin): the next CDFEM_LAUNCH records these
+                                // events at its own dispatch start / end (hipExtLaunchKernelGGL)
 };
+
+// Launch on the context stream; when a profiling mark is armed (prof_mark), the kernel records the
+// mark's event pair itself at dispatch start and completion (hipExtLaunchKernelGGL), so the timed
+// interval is the kernel alone, without the ~5-10 us an event record adds ahead of a ~100 us
+// kernel.  Used for the dominant (roofline) kernels.
+#define CDFEM_LAUNCH(c, kernel, grid, block, shm, ...)                                                       \
+    do {                                                                                                     \
+        if ((c)->ext_ev[0]) {                                                                                \
+            hipExtLaunchKernelGGL(kernel, grid, block, shm, (c)->stream, (c)->ext_ev[0], (c)->ext_ev[1], 0,   \
+                                  __VA_ARGS__);                                                              \
+            (c)->ext_ev[0] = (c)->ext_ev[1] = nullptr;                                                       \
+        } else {                                                                                             \
+            hipLaunchKernelGGL(kernel, grid, block, shm, (c)->stream, __VA_ARGS__);                          \
+        }                                                                                                    \
+    } while (0)
 
 namespace cdfem {
 

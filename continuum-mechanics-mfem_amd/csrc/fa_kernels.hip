@@ -460,16 +460,17 @@ unsigned sell_grid(const cdfem_ctx *c) { return (unsigned)((c->nslices + 3) / 4)
 
 hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y)
 {
-    hipLaunchKernelGGL((k_sell_spmv<false>), dim3(sell_grid(c)), dim3(256), 0, c->stream, c->d_sptr, c->d_srows,
-                       c->d_scols, constrained ? c->d_svals_c : c->d_svals, x, y, c->nslices, nullptr, nullptr);
+    CDFEM_LAUNCH(c, (k_sell_spmv<false>), dim3(sell_grid(c)), dim3(256), 0, c->d_sptr, c->d_srows, c->d_scols,
+                 constrained ? c->d_svals_c : c->d_svals, x, y, c->nslices, (double *)nullptr,
+                 (const KrylovState *)nullptr);
     return hipGetLastError();
 }
 
 // q = A_c d and the den partials, then the MFEM CG den step (one-block finalizer)
 hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q)
 {
-    hipLaunchKernelGGL((k_sell_spmv<true>), dim3(sell_grid(c)), dim3(256), 0, c->stream, c->d_sptr, c->d_srows,
-                       c->d_scols, c->d_svals_c, d, q, c->nslices, c->d_part, c->d_state);
+    CDFEM_LAUNCH(c, (k_sell_spmv<true>), dim3(sell_grid(c)), dim3(256), 0, c->d_sptr, c->d_srows, c->d_scols,
+                 (const double *)c->d_svals_c, d, q, c->nslices, c->d_part, (const KrylovState *)c->d_state);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_den_fin(c, (int)sell_grid(c));

@@ -288,18 +288,18 @@ static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con
     geo.ess = c->d_ess;
     if (c->epencil) {
         if (con)
-            hipLaunchKernelGGL((k_apply3d_tile<D1, Q1, K, true, true>), grid, block, 0, c->stream, c->d_map, x,
-                               c->d_qd, Ye, T, c->ne, geo, st);
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true>), grid, block, 0, c->d_map, x, c->d_qd,
+                         Ye, T, c->ne, geo, st);
         else
-            hipLaunchKernelGGL((k_apply3d_tile<D1, Q1, K, false, true>), grid, block, 0, c->stream, c->d_map, x,
-                               c->d_qd, Ye, T, c->ne, geo, st);
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, true>), grid, block, 0, c->d_map, x, c->d_qd,
+                         Ye, T, c->ne, geo, st);
     } else {
         if (con)
-            hipLaunchKernelGGL((k_apply3d_tile<D1, Q1, K, true, false>), grid, block, 0, c->stream, c->d_map, x,
-                               c->d_qd, Ye, T, c->ne, geo, st);
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, false>), grid, block, 0, c->d_map, x, c->d_qd,
+                         Ye, T, c->ne, geo, st);
         else
-            hipLaunchKernelGGL((k_apply3d_tile<D1, Q1, K, false, false>), grid, block, 0, c->stream, c->d_map, x,
-                               c->d_qd, Ye, T, c->ne, geo, st);
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, false>), grid, block, 0, c->d_map, x, c->d_qd,
+                         Ye, T, c->ne, geo, st);
     }
     return hipGetLastError();
 }
