@@ -1167,6 +1167,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 6) throw ArgError("brick_variant must be 0..6");
             c->brick_variant = value;
 
+        } else if (k == "brick_xcd") {
+            if (value < 0 || value > 1) throw ArgError("brick_xcd must be 0 or 1");
+            c->brick_xcd = value;
         } else if (k == "profile_mask") {
             c->prof_mask = (unsigned)value;
         } else if (k == "brick_waves") {

@@ -193,8 +193,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "brick_waves": 1 or 2 — register budget of the structured Mult kernel (waves per SIMD).
  * "profile_mask": bit k set = kernel slot k (CDFEM_K_*) gets HIP events while profiling is on
  *                 (default all; events around every kernel cost ~1 us each on the stream).
- * "brick_variant": 0, 1, 2 — element core of the structured CG kernel (unrolled / plane loop /
- *                  low-register).                                                               */
+ * "brick_variant": 0..6 — element core of the structured CG kernel (unrolled / plane loop /
+ *                  low-register; 3-5 the same at 2 waves per SIMD; 6 temporal qdata loads).
+ * "brick_xcd": 1 (default) — XCD-contiguous brick order of the structured CG kernel; 0 = the
+ *              dispatcher's round-robin order.                                                  */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
 
 /* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */
