@@ -28,7 +28,7 @@ __device__ inline double block_sum(double v, double *sh)
     if (lane == 0) sh[w] = v;
     __syncthreads();
     if (threadIdx.x < 64) {
-        v = (threadIdx.x < (blockDim.x >> 6)) ? sh[threadIdx.x] : 0.0;
+        v = (threadIdx.x < ((blockDim.x + 63) >> 6)) ? sh[threadIdx.x] : 0.0;
         v = wave_sum(v);
     }
     return v;
