@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=None, help="elements per direction (per-rank slab depth); "
+    ap.add_argument("--elems", dest="n", type=int, default=None, help="elements per direction (per-rank slab depth); "
                     "default 64 (c2) / 128 (c3)")
     ap.add_argument("--order", type=int, default=None, help="default 2 (c2) / 4 (c3)")
     ap.add_argument("--cg-iters", type=int, default=None, help="default 100 (c2) / 20 (c3)")
