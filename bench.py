@@ -256,8 +256,6 @@ def main():
     if args.path == "brick" or p >= 3:
         ctx.set_structured(n, n, nzr)  # p >= 3: structured E->L (no position arrays)
     if world > 1:
-        if args.path != "brick":
-            raise SystemExit("multi-GPU runs use the structured brick path")
         if args.comm == "rccl":
             # RCCL communicator over xGMI; the id travels over the gloo control group
             obj = [cdfem.comm_unique_id() if rank == 0 else None]

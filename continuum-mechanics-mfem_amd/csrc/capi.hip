@@ -381,9 +381,17 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
         dinv = c->d_dinv;
     }
     const int check = p.check_every > 0 ? p.check_every : 16;
+    const bool mr = multi_rank(c);
+    double *red = c->d_state->red;  // device scalars awaiting the all-reduce (multi-rank)
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
-    HIPCHK(launch_cg_init(c, dB, x, r, z, d, dinv, p.rel_tol, p.abs_tol, p.max_iter));
+    if (mr) {
+        HIPCHK(launch_cg_init_nofin(c, dB, x, r, z, d, dinv));
+        comm_allreduce(c, red + 2, 1);
+        HIPCHK(launch_init_step(c, p.rel_tol, p.abs_tol, p.max_iter));
+    } else {
+        HIPCHK(launch_cg_init(c, dB, x, r, z, d, dinv, p.rel_tol, p.abs_tol, p.max_iter));
+    }
     // z = A d ; den = (d, z) and the MFEM den step
     auto apply = [&] {
         prof_mark(c, CDFEM_K_APPLY, true);
@@ -395,7 +403,16 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
         HIPCHK(launch_apply_st(c, d, c->d_Ye, true, c->d_state));
         prof_mark(c, CDFEM_K_APPLY, false);
         prof_mark(c, CDFEM_K_E2L, true);
-        HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 1));
+        if (mr) {  // slab partition: interface sums, essential rows reset, owned den all-reduced
+            HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 0));
+            interface_sum(c, z);
+            HIPCHK(launch_set_ess(c, z, d));
+            HIPCHK(launch_den_local(c, d, z));
+            comm_allreduce(c, red + 0, 1);
+            HIPCHK(launch_den_step(c));
+        } else {
+            HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 1));
+        }
         prof_mark(c, CDFEM_K_E2L, false);
     };
     apply();
@@ -404,6 +421,10 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
         for (int k = 0; k < check && launched < p.max_iter; ++k, ++launched) {
             prof_mark(c, CDFEM_K_UPDATE, true);
             HIPCHK(launch_cg_update(c, x, r, z, d, dinv));
+            if (mr) {
+                comm_allreduce(c, red + 1, 1);
+                HIPCHK(launch_update_step(c));
+            }
             prof_mark(c, CDFEM_K_UPDATE, false);
             prof_mark(c, CDFEM_K_DIRECTION, true);
             HIPCHK(launch_cg_direction(c, z, d));
@@ -716,7 +737,7 @@ int cdfem_set_slab(cdfem_ctx *c, int zlo_shared, int zhi_shared)
 {
     return guarded(c, [&] {
         if (!c->structured) throw StateError("cdfem_mesh_set_structured must precede cdfem_set_slab");
-        if (!use_brick(c)) throw UnsupportedError("multi-rank slabs use the structured brick path (3D, p <= 2)");
+        if (c->dim != 3) throw UnsupportedError("multi-rank slabs are 3D z-slabs");
         if ((zlo_shared || zhi_shared) && !c->comm) throw StateError("attach a communicator first");
         c->zlo_shared = zlo_shared != 0;
         c->zhi_shared = zhi_shared != 0;

@@ -259,6 +259,8 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
                                   const double *dinv, const double *remote_lo, const double *remote_hi);
 // generic deterministic dot into host-visible scalar via state (used by GMRES / tests)
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out);
+// multi-rank CG: rank-local (d, q) over owned entries into the state's den slot (all-reduce next)
+hipError_t launch_den_local(cdfem_ctx *c, const double *d, const double *q);
 
 // ---- communication (comm.hip) -----------------------------------------------------------------
 void comm_destroy(cdfem_ctx *c);

@@ -243,7 +243,7 @@ k_cg_den_fin(const double *__restrict__ part, int n, KrylovState *__restrict__ s
 template <bool STORE_Z>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update(double *__restrict__ x, double *__restrict__ r, double *__restrict__ z,
-            const double *__restrict__ d, const double *__restrict__ dinv, int64_t n,
+            const double *__restrict__ d, const double *__restrict__ dinv, int64_t n, int64_t skip_lo,
             double *__restrict__ part, KrylovState *__restrict__ st)
 {
     __shared__ double sh[kRedThreads / 64];
@@ -266,8 +266,8 @@ k_cg_update(double *__restrict__ x, double *__restrict__ r, double *__restrict__
         reinterpret_cast<double2 *>(x)[i] = xv;
         reinterpret_cast<double2 *>(r)[i] = rv;
         if (STORE_Z) reinterpret_cast<double2 *>(z)[i] = make_double2(z0, z1);
-        acc += rv.x * z0;
-        acc += rv.y * z1;
+        if (2 * i >= skip_lo) acc += rv.x * z0;  // shared plane owned by the rank below
+        if (2 * i + 1 >= skip_lo) acc += rv.y * z1;
     }
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
         const int64_t i = n - 1;
@@ -276,7 +276,7 @@ k_cg_update(double *__restrict__ x, double *__restrict__ r, double *__restrict__
         r[i] = ri;
         const double zi = dinv ? dinv[i] * ri : ri;
         if (STORE_Z) z[i] = zi;
-        acc += ri * zi;
+        if (i >= skip_lo) acc += ri * zi;
     }
     store_partial(block_sum(acc, sh), part);
 }
@@ -337,14 +337,15 @@ __global__ void k_dinv(const uint8_t *__restrict__ ess, const double *__restrict
         dinv[i] = ess[i] ? 1.0 : 1.0 / diag[i];
 }
 
-// deterministic dot: partials, then k_dot_fin
+// deterministic dot over entries [skip_lo, n): partials, then k_dot_fin / k_fin_sum
 __global__ void __launch_bounds__(kRedThreads)
-k_dot(const double *__restrict__ a, const double *__restrict__ b, int64_t n, double *__restrict__ part)
+k_dot(const double *__restrict__ a, const double *__restrict__ b, int64_t n, int64_t skip_lo,
+      double *__restrict__ part)
 {
     __shared__ double sh[kRedThreads / 64];
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    for (int64_t i = skip_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         acc += a[i] * b[i];
     store_partial(block_sum(acc, sh), part);
 }
@@ -510,7 +511,8 @@ hipError_t launch_cg_update(cdfem_ctx *c, double *x, double *r, double *z, const
 {
     const unsigned g = red_grid(c, c->nl);
     hipLaunchKernelGGL(k_cg_update<true>, dim3(g), dim3(kRedThreads), 0, c->stream, x, r, z, d, dinv,
-                       c->nl, c->d_part, c->d_state);
+                       c->nl, (int64_t)(c->zlo_shared ? c->Lx * c->Ly : 0), c->d_part, c->d_state);
+    if (multi_rank(c)) return launch_fin_sum(c, (int)g, 1);  // all-reduced, then the update step
     hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g, c->d_state);
     return hipGetLastError();
 }
@@ -521,7 +523,7 @@ hipError_t launch_cg_update_noz(cdfem_ctx *c, double *x, double *r, const double
     // k_cg_update reads "z" as A d: pass q there; the z output is not written
     const unsigned g = red_grid(c, c->nl);
     hipLaunchKernelGGL(k_cg_update<false>, dim3(g), dim3(kRedThreads), 0, c->stream, x, r,
-                       const_cast<double *>(q), d, dinv, c->nl, c->d_part, c->d_state);
+                       const_cast<double *>(q), d, dinv, c->nl, (int64_t)0, c->d_part, c->d_state);
     hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g, c->d_state);
     return hipGetLastError();
 }
@@ -548,9 +550,17 @@ hipError_t launch_cg_direction(cdfem_ctx *c, const double *z, double *d)
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out)
 {
     const unsigned g = red_grid(c, c->nl);
-    hipLaunchKernelGGL(k_dot, dim3(g), dim3(kRedThreads), 0, c->stream, a, b, c->nl, c->d_part);
+    hipLaunchKernelGGL(k_dot, dim3(g), dim3(kRedThreads), 0, c->stream, a, b, c->nl, (int64_t)0, c->d_part);
     hipLaunchKernelGGL(k_dot_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g, d_out);
     return hipGetLastError();
+}
+
+hipError_t launch_den_local(cdfem_ctx *c, const double *d, const double *q)
+{
+    const unsigned g = red_grid(c, c->nl);
+    const int64_t skip = c->zlo_shared ? c->Lx * c->Ly : 0;
+    hipLaunchKernelGGL(k_dot, dim3(g), dim3(kRedThreads), 0, c->stream, d, q, c->nl, skip, c->d_part);
+    return launch_fin_sum(c, (int)g, 0);
 }
 
 }  // namespace cdfem

@@ -379,3 +379,64 @@ def test_gpu_gmres_two_ranks_one_device(tmp_path):
     yg = np.concatenate([y0, y1[plane:]])
     np.testing.assert_allclose(y1[:plane], y0[-plane:], rtol=0, atol=1e-13 * np.abs(yf).max())
     assert np.abs(yg - yf).max() <= 1e-13 * np.abs(yf).max()
+
+
+# ---------------------------------------------------------------------------------------------
+# High order (p = 4) slabs: the generic CG (tile apply, E-vector, lattice E->L) with interface sums
+# and all-reduced scalars, and GMRES, on 2 processes sharing one GPU, against one context.
+NH, PH, NZH = 3, 4, 4
+
+
+def _gpu_ho_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    import cdfem
+    dist = _init(rank, world, port)
+    per = NZH // world
+    m = cdfem.box_mesh(3, (NH, NH, NZH), PH, z_range=(rank * per, (rank + 1) * per))
+    ctx = cdfem.Context(0)
+    ctx.upload_mesh(m).set_structured(NH, NH, per)
+    ctx.comm_init_torch()
+    ctx.set_slab(rank > 0, rank < world - 1)
+    ctx.pa_setup(kinds=cdfem.DIFFUSION | cdfem.MASS, kappa=KAPPA, mass=S)
+    b = np.random.default_rng(500 + rank).uniform(-1, 1, m.nl)
+    np.save(os.path.join(out_dir, f"b{rank}.npy"), b)
+    _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+    X, info = ctx.solve(B, method="cg", rel_tol=1e-12, max_iter=2000, check_every=5)
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), X)
+    np.save(os.path.join(out_dir, f"its{rank}.npy"), np.array([info["iterations"], info["converged"]]))
+    ctx.pa_setup(kinds=7, kappa=KAPPA, alpha=1.0, conv=CONV, mass=S)
+    _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+    X, info = ctx.solve(B, method="gmres", pc="jacobi", rel_tol=1e-10, abs_tol=1e-12, max_iter=500, restart=10)
+    np.save(os.path.join(out_dir, f"g{rank}.npy"), X)
+    np.save(os.path.join(out_dir, f"gits{rank}.npy"), np.array([info["iterations"], info["converged"]]))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_high_order_two_ranks_one_device(tmp_path):
+    import cdfem
+    world = 2
+    mp.start_processes(_gpu_ho_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    plane = (PH * NH + 1) ** 2
+    bfull = _gathered_rhs(tmp_path, plane)
+    m = cdfem.box_mesh(3, (NH, NH, NZH), PH)
+    with cdfem.Context(0) as ctx:
+        ctx.upload_mesh(m).set_structured(NH, NH, NZH)
+        ctx.pa_setup(kinds=cdfem.DIFFUSION | cdfem.MASS, kappa=KAPPA, mass=S)
+        _, B = ctx.form_linear_system(np.zeros(m.nl), bfull)
+        xs, info = ctx.solve(B, method="cg", rel_tol=1e-12, max_iter=2000)
+        ctx.pa_setup(kinds=7, kappa=KAPPA, alpha=1.0, conv=CONV, mass=S)
+        _, B = ctx.form_linear_system(np.zeros(m.nl), bfull)
+        gs, ginfo = ctx.solve(B, method="gmres", pc="jacobi", rel_tol=1e-10, abs_tol=1e-12, max_iter=500,
+                              restart=10)
+    for xname, itname, ref, rinfo, tol in (("x", "its", xs, info, 1e-10), ("g", "gits", gs, ginfo, 1e-8)):
+        x0, x1 = np.load(tmp_path / f"{xname}0.npy"), np.load(tmp_path / f"{xname}1.npy")
+        its = np.load(tmp_path / f"{itname}0.npy")
+        assert its[1] and abs(int(its[0]) - rinfo["iterations"]) <= 1
+        np.testing.assert_allclose(x1[:plane], x0[-plane:], rtol=0, atol=1e-12 * np.abs(x0).max())
+        xg = np.concatenate([x0, x1[plane:]])
+        assert np.linalg.norm(xg - ref) <= tol * np.linalg.norm(ref)
