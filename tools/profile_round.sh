@@ -14,6 +14,7 @@ case $CFG in
   c2) SHORT="--cg-iters 20";;
   c3) SHORT="--cg-iters 4 --gmres-iters 0";;
   c4) SHORT="--gmres-iters 30";;
+  c5) SHORT="--cg-iters 10 --gmres-iters 0";;
 esac
 timeout -k 10 900 python bench.py --config $CFG --steps 5 --warmup 1 > $OUT/bench.json 2> $OUT/bench.err || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/stats -o run --output-format csv -- python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-profile-events > $OUT/stats.log 2>&1 || exit $?
