@@ -109,21 +109,37 @@ k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__rest
         for (int a = 0; a < nzp; ++a)
             for (int b = 0; b < nyp; ++b)
                 erow[ne_rows++] = (((int64_t)(ez[a] * D1 + lz[a]) * bx.ny + ey[b]) * D1 + ly[b]) * ew;
+        for (int k = ne_rows; k < 4; ++k) erow[k] = erow[0];
         const int64_t lrow = (int64_t)r * bx.Lx;
-#pragma unroll 3
+#pragma unroll 2
         for (uint32_t gx = lane; gx < bx.Lx; gx += 64) {
             const uint32_t ex = gx / P, lx = gx - ex * P;
             const bool left = lx == 0 && ex > 0, right = lx != 0 || ex < bx.nx;
             const int64_t i = lrow + gx;
-            double v = 0.0;
-            for (int k = 0; k < ne_rows; ++k) {
-                const double *er = Ye + erow[k] + gx + ex;
-                if (left) v += er[-1];
-                if (right) v += er[0];
+            // every load issued before the sums (clamped addresses): up to 8 E-vector entries,
+            // the essential flag and x in flight together
+            // (an absent neighbour reads the present entry instead: no address leaves the row)
+            const int64_t cl = left ? -1 : 0, cr = right ? 0 : -1;
+            double el[4], er[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const double *e0 = Ye + erow[k] + gx + ex;
+                el[k] = e0[cl];
+                er[k] = e0[cr];
             }
-            if (CON && ess[i]) v = x[i];
+            const bool is_ess = CON && ess[i];
+            const double xi = (CON || CG) ? x[i] : 0.0;
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k < ne_rows) {
+                    if (left) v += el[k];
+                    if (right) v += er[k];
+                }
+            }
+            if (is_ess) v = xi;
             y[i] = v;
-            if (CG) acc += v * x[i];
+            if (CG) acc += v * xi;
         }
     }
     if (!CG) return;
