@@ -613,10 +613,100 @@ ORC_API int orc_cg(const orc_csr *A, const double *dinv, const double *b, double
  * zero initial guess, KSPConvergedDefault on the preconditioned residual norm:
  * converged when rnorm <= max(rtol * rnorm0, atol).  Input/petsc.opts:2-6.
  */
+/*
+ * ILU(0) [PETSc-ext]: PCILU with zero fill in the natural ordering, no pivoting and no shift (the
+ * single-rank meaning of "-pc_type bjacobi -sub_pc_type ilu", Input/petsc_circle.opts:6-8).  IKJ
+ * elimination restricted to the pattern of A:
+ *   for i: for k < i in row i (ascending): a_ik /= a_kk;  a_ij -= a_ik a_kj for j > k in both rows
+ * L (unit diagonal) and U share A's pattern.  Defining property, pinned in tests: (L U)_ij = a_ij
+ * for every (i, j) in the pattern.
+ */
+ORC_API orc_csr *orc_ilu0(const orc_csr *A)
+{
+    orc_csr *F = (orc_csr *)calloc(1, sizeof(orc_csr));
+    F->n = A->n;
+    F->nnz = A->nnz;
+    F->rp = (int64_t *)malloc(sizeof(int64_t) * (A->n + 1));
+    F->col = (int32_t *)malloc(sizeof(int32_t) * A->nnz);
+    F->val = (double *)malloc(sizeof(double) * A->nnz);
+    memcpy(F->rp, A->rp, sizeof(int64_t) * (A->n + 1));
+    memcpy(F->col, A->col, sizeof(int32_t) * A->nnz);
+    memcpy(F->val, A->val, sizeof(double) * A->nnz);
+    int64_t *diag = (int64_t *)malloc(sizeof(int64_t) * A->n);
+    for (int64_t i = 0; i < A->n; i++) {
+        diag[i] = -1;
+        for (int64_t p = F->rp[i]; p < F->rp[i + 1]; p++)
+            if (F->col[p] == i) diag[i] = p;
+    }
+    for (int64_t i = 0; i < F->n; i++) {
+        for (int64_t pk = F->rp[i]; pk < F->rp[i + 1] && F->col[pk] < i; pk++) {
+            const int64_t k = F->col[pk];
+            const double lik = F->val[pk] / F->val[diag[k]];
+            F->val[pk] = lik;
+            /* a_ij -= l_ik u_kj for j > k present in row i and row k (sorted merge) */
+            int64_t pi = pk + 1, pu = diag[k] + 1;
+            while (pi < F->rp[i + 1] && pu < F->rp[k + 1]) {
+                if (F->col[pi] < F->col[pu]) pi++;
+                else if (F->col[pi] > F->col[pu]) pu++;
+                else { F->val[pi] -= lik * F->val[pu]; pi++; pu++; }
+            }
+        }
+    }
+    free(diag);
+    return F;
+}
+
+/* z = (L U)^{-1} r: forward sweep with the unit lower part, backward with the upper part; each
+ * row sums in ascending column order */
+ORC_API void orc_ilu_solve(const orc_csr *F, const double *r, double *z)
+{
+    const int64_t n = F->n;
+    for (int64_t i = 0; i < n; i++) {
+        double v = r[i];
+        for (int64_t p = F->rp[i]; p < F->rp[i + 1] && F->col[p] < i; p++) v -= F->val[p] * z[F->col[p]];
+        z[i] = v;
+    }
+    for (int64_t i = n - 1; i >= 0; i--) {
+        double v = z[i], d = 1.0;
+        for (int64_t p = F->rp[i]; p < F->rp[i + 1]; p++) {
+            if (F->col[p] > i) v -= F->val[p] * z[F->col[p]];
+            else if (F->col[p] == i) d = F->val[p];
+        }
+        z[i] = v / d;
+    }
+}
+
+/* left preconditioner of GMRES: Jacobi (dinv), ILU(0) (ilu) or none; v <- M^{-1} v */
+static void gmres_pc(const double *dinv, const orc_csr *ilu, int64_t n, double *v, double *tmp)
+{
+    if (ilu) {
+        memcpy(tmp, v, sizeof(double) * n);
+        orc_ilu_solve(ilu, tmp, v);
+    } else if (dinv) {
+        for (int64_t i = 0; i < n; i++) v[i] *= dinv[i];
+    }
+}
+
+static int gmres_core(const orc_csr *A, const double *dinv, const orc_csr *ilu, const double *b, double *x,
+                      int m, double rtol, double atol, int max_it, int *iters, double *final_norm);
+
 ORC_API int orc_gmres(const orc_csr *A, const double *dinv, const double *b, double *x, int m,
                       double rtol, double atol, int max_it, int *iters, double *final_norm)
 {
+    return gmres_core(A, dinv, NULL, b, x, m, rtol, atol, max_it, iters, final_norm);
+}
+
+ORC_API int orc_gmres_ilu(const orc_csr *A, const orc_csr *ilu, const double *b, double *x, int m,
+                          double rtol, double atol, int max_it, int *iters, double *final_norm)
+{
+    return gmres_core(A, NULL, ilu, b, x, m, rtol, atol, max_it, iters, final_norm);
+}
+
+static int gmres_core(const orc_csr *A, const double *dinv, const orc_csr *ilu, const double *b, double *x,
+                      int m, double rtol, double atol, int max_it, int *iters, double *final_norm)
+{
     const int64_t n = A->n;
+    double *tmp = (double *)malloc(sizeof(double) * n);
     double *V = (double *)malloc(sizeof(double) * n * (m + 1));
     double *w = (double *)malloc(sizeof(double) * n);
     double *H = (double *)calloc((size_t)(m + 1) * m, sizeof(double));
@@ -628,10 +718,8 @@ ORC_API int orc_gmres(const orc_csr *A, const double *dinv, const double *b, dou
     for (;;) {
         /* preconditioned initial residual of this cycle: V0 = M^{-1}(b - A x) */
         orc_csr_spmv(A, x, w);
-        for (int64_t i = 0; i < n; i++) {
-            double r = b[i] - w[i];
-            V[i] = dinv ? dinv[i] * r : r;
-        }
+        for (int64_t i = 0; i < n; i++) V[i] = b[i] - w[i];
+        gmres_pc(dinv, ilu, n, V, tmp);
         double beta = sqrt(dot(n, V, V));
         res = beta;
         if (first) { ttol = fmax(rtol * beta, atol); first = 0; }
@@ -645,7 +733,7 @@ ORC_API int orc_gmres(const orc_csr *A, const double *dinv, const double *b, dou
             its++;
             double *vj = V + (size_t)j * n, *vn = V + (size_t)(j + 1) * n;
             orc_csr_spmv(A, vj, w);
-            if (dinv) for (int64_t i = 0; i < n; i++) w[i] *= dinv[i];
+            gmres_pc(dinv, ilu, n, w, tmp);
             /* classical Gram-Schmidt: all projections from the same w */
             for (int i = 0; i <= j; i++) H[i * m + j] = dot(n, w, V + (size_t)i * n);
             for (int i = 0; i <= j; i++) {
@@ -688,7 +776,7 @@ ORC_API int orc_gmres(const orc_csr *A, const double *dinv, const double *b, dou
     }
     *iters = its;
     *final_norm = res;
-    free(V); free(w); free(H); free(cs); free(sn); free(g); free(y);
+    free(V); free(w); free(H); free(cs); free(sn); free(g); free(y); free(tmp);
     return converged;
 }
 

@@ -58,6 +58,11 @@ def lib():
         L.orc_csr_diag.argtypes = [C.c_void_p, dp]
         L.orc_cg.argtypes = [C.c_void_p, dp, dp, dp, C.c_double, C.c_double, C.c_int, ip, dp]
         L.orc_gmres.argtypes = [C.c_void_p, dp, dp, dp, C.c_int, C.c_double, C.c_double, C.c_int, ip, dp]
+        L.orc_ilu0.restype = C.c_void_p
+        L.orc_ilu0.argtypes = [C.c_void_p]
+        L.orc_ilu_solve.argtypes = [C.c_void_p, dp, dp]
+        L.orc_gmres_ilu.argtypes = [C.c_void_p, C.c_void_p, dp, dp, C.c_int, C.c_double, C.c_double, C.c_int,
+                                    ip, dp]
         L.orc_mms_u.argtypes = [dp, dp]
         L.orc_mms_u.restype = C.c_double
         L.orc_mms_f.argtypes = [dp, dp]
@@ -304,6 +309,27 @@ def gmres(A: CSR, b, dinv=None, restart=30, rtol=1e-10, atol=1e-12, max_it=500):
     it, fn = C.c_int(0), C.c_double(0)
     di = None if dinv is None else _d(np.ascontiguousarray(dinv, dtype=np.float64))
     conv = lib().orc_gmres(A.h, di, _d(b), _d(x), restart, rtol, atol, max_it, C.byref(it), C.byref(fn))
+    return x, dict(converged=bool(conv), iterations=it.value, final_norm=fn.value)
+
+
+def ilu0(A: CSR) -> CSR:
+    """ILU(0) factors in A's pattern (unit-lower L and U packed), PETSc PCILU semantics."""
+    return CSR(lib().orc_ilu0(A.h))
+
+
+def ilu_solve(F: CSR, r):
+    r = np.ascontiguousarray(r, dtype=np.float64)
+    z = np.zeros(F.n)
+    lib().orc_ilu_solve(F.h, _d(r), _d(z))
+    return z
+
+
+def gmres_ilu(A: CSR, b, F: CSR, restart=30, rtol=1e-10, atol=1e-12, max_it=500):
+    """GMRES(m) left-preconditioned with ILU(0) factors F (Input/petsc_circle.opts)."""
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(A.n)
+    it, fn = C.c_int(0), C.c_double(0)
+    conv = lib().orc_gmres_ilu(A.h, F.h, _d(b), _d(x), restart, rtol, atol, max_it, C.byref(it), C.byref(fn))
     return x, dict(converged=bool(conv), iterations=it.value, final_norm=fn.value)
 
 
