@@ -966,6 +966,19 @@ public:
     }
 };
 
+// PETSc's PCILU (zero fill, natural ordering) as a preconditioner marker: "-pc_type bjacobi
+// -sub_pc_type ilu" (Input/petsc_circle.opts:6-8) on one rank, or "-pc_type ilu".  Factored once per
+// operator on the device (ilu_kernels.hip) and applied inside the device GMRES.
+class ILUPreconditioner : public Solver {
+public:
+    ILUPreconditioner() = default;
+    void SetOperator(const Operator &) override {}
+    void Mult(const Vector &, Vector &) const override
+    {
+        throw std::logic_error("ILUPreconditioner is applied inside the device solver");
+    }
+};
+
 class IterativeSolver : public Solver {
 public:
     void SetRelTol(double r) { rel_tol = r; }
@@ -978,7 +991,12 @@ public:
         if (!oper) throw std::invalid_argument("solver operator must come from BilinearForm::FormLinearSystem");
         height = width = op.Height();
     }
-    void SetPreconditioner(Solver &pc) { jacobi = dynamic_cast<OperatorJacobiSmoother *>(&pc) != nullptr; }
+    void SetPreconditioner(Solver &pc)
+    {
+        pc_kind = dynamic_cast<OperatorJacobiSmoother *>(&pc) ? CDFEM_PC_JACOBI
+                : dynamic_cast<ILUPreconditioner *>(&pc)     ? CDFEM_PC_ILU
+                                                              : CDFEM_PC_NONE;
+    }
     bool GetConverged() const { return converged; }
     int GetNumIterations() const { return final_iter; }
     double GetFinalNorm() const { return final_norm; }
@@ -990,7 +1008,7 @@ protected:
         if (!oper) throw std::logic_error("SetOperator was not called");
         cdfem_solver_params prm{};
         prm.method = method;
-        prm.pc = jacobi ? CDFEM_PC_JACOBI : CDFEM_PC_NONE;
+        prm.pc = pc_kind;
         prm.max_iter = max_iter;
         prm.restart = restart;
         prm.rel_tol = rel_tol;
@@ -1013,7 +1031,7 @@ protected:
     const ConstrainedPAOperator *oper = nullptr;
     double rel_tol = 0.0, abs_tol = 0.0;
     int max_iter = 10, print_level = -1;
-    bool jacobi = false;
+    int pc_kind = CDFEM_PC_NONE;
     mutable bool converged = false;
     mutable int final_iter = 0;
     mutable double final_norm = 0.0, seconds = 0.0;
@@ -1039,7 +1057,7 @@ private:
 // ---- PETSc-named front end (linear_convection_diffusion_2D.cpp:268-282, :364-375) --------------
 // MFEMInitializePetsc reads the same option keys the reference's Input/petsc.opts sets:
 // -ksp_type {gmres, cg}, -ksp_rtol, -ksp_atol, -ksp_max_it, -ksp_gmres_restart, -pc_type
-// {jacobi, none}.  Defaults are PETSc's (gmres, restart 30, rtol 1e-5, atol 1e-50, max_it 1e4,
+// {jacobi, none, ilu, bjacobi with -sub_pc_type ilu (-sub_ksp_type preonly)}.  Defaults are PETSc's (gmres, restart 30, rtol 1e-5, atol 1e-50, max_it 1e4,
 // pc jacobi for the reference's runs is set by the file).
 struct PetscOptionsStore {
     std::map<std::string, std::string> kv;
@@ -1102,8 +1120,18 @@ public:
         solver_->SetAbsTol(std::stod(o.Get("-ksp_atol", "1e-50")));
         solver_->SetMaxIter(std::stoi(o.Get("-ksp_max_it", "10000")));
         const std::string pc = o.Get("-pc_type", "jacobi");
-        if (pc == "jacobi") solver_->SetPreconditioner(jac_);
-        else if (pc != "none") throw std::invalid_argument("unsupported -pc_type " + pc);
+        if (pc == "jacobi") {
+            solver_->SetPreconditioner(jac_);
+        } else if (pc == "ilu" || pc == "bjacobi") {
+            // one rank: block Jacobi has a single block, solved by its sub-PC (preonly + ILU)
+            const std::string sub = pc == "ilu" ? "ilu" : o.Get("-sub_pc_type", "ilu");
+            const std::string subksp = o.Get("-sub_ksp_type", "preonly");
+            if (sub != "ilu" || subksp != "preonly")
+                throw std::invalid_argument("unsupported block-Jacobi sub solver " + subksp + "/" + sub);
+            solver_->SetPreconditioner(ilu_);
+        } else if (pc != "none") {
+            throw std::invalid_argument("unsupported -pc_type " + pc);
+        }
         SetOperator(A);
     }
     void SetOperator(const Operator &op) override
@@ -1122,6 +1150,7 @@ public:
 private:
     std::unique_ptr<IterativeSolver> solver_;
     OperatorJacobiSmoother jac_;
+    ILUPreconditioner ilu_;
 };
 
 }  // namespace mfem

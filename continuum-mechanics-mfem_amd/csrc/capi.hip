@@ -97,6 +97,7 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_cpos); dfree(c->d_vals); dfree(c->d_vals_c); dfree(c->d_Ee);
     dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_svals);
     dfree(c->d_svals_c);
+    ilu_free(c);
     c->nslices = c->nstored = 0;
     c->geom = 0;
     c->fa_ready = false;
@@ -471,9 +472,14 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
         for (auto &e : c->gm_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     const double *dinv = nullptr;
+    const bool ilu = p.pc == CDFEM_PC_ILU;
     if (p.pc == CDFEM_PC_JACOBI) {
         ensure_dinv(c);
         dinv = c->d_dinv;
+    } else if (ilu) {
+        if (!c->fa_ready) throw UnsupportedError("ILU(0) needs an assembled operator (cdfem_fa_setup)");
+        if (multi_rank(c)) throw UnsupportedError("ILU(0) on a multi-rank partition");
+        ilu_setup(c);
     }
     double *x = c->d_w[2], *w = c->d_w[4], *V = c->d_gm, *part = c->d_gm_part;
     GmresState *st = c->d_gmst, *poll = c->h_gmpoll;
@@ -491,14 +497,23 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     for (bool first = true;; first = false) {
         // v0 = M^{-1}(b - A x); x = 0 on the first cycle, so A x is skipped there
         if (!first) op_apply_global(c, x, w, true);
-        HIPCHK(launch_gm_residual(c, dB, first ? nullptr : w, dinv, V, part, st, first, p.rel_tol, p.abs_tol,
-                                  &poll[0]));
+        if (ilu) {  // v0 = (LU)^{-1} (b - A x): the residual into w, the sweeps into ilu.z
+            if (first) HIPCHK(hipMemcpyAsync(w, dB, n * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+            else HIPCHK(launch_axpby(c, 1.0, dB, -1.0, w));
+            HIPCHK(ilu_apply(c));
+            HIPCHK(launch_gm_residual(c, c->ilu.z, nullptr, nullptr, V, part, st, first, p.rel_tol, p.abs_tol,
+                                      &poll[0]));
+        } else {
+            HIPCHK(launch_gm_residual(c, dB, first ? nullptr : w, dinv, V, part, st, first, p.rel_tol, p.abs_tol,
+                                      &poll[0]));
+        }
         post(0);
         if (wait(0).done) break;
         for (int j = 0; j < m; ++j) {
             op_apply_global(c, V + (int64_t)j * n, w, true);
+            if (ilu) HIPCHK(ilu_apply(c));  // w <- (LU)^{-1} A v_j, in ilu.z
             prof_mark(c, CDFEM_K_ORTH, true);
-            HIPCHK(launch_gm_orth(c, w, dinv, V, n, part, st, m, &poll[j & 1]));
+            HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, n, part, st, m, &poll[j & 1]));
             prof_mark(c, CDFEM_K_ORTH, false);
             post(j & 1);
             if (j > 0 && wait((j - 1) & 1).cycle_done) break;
@@ -1007,6 +1022,7 @@ int cdfem_fa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kap
         c->fa_ready = true;
         c->pa_ready = false;
         c->dinv_ready = false;
+        ilu_free(c);  // factors belong to the previous operator
         return CDFEM_OK;
     });
 }
@@ -1107,7 +1123,10 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
         require_pa(c);
         if (!p || !B || !X || !res) throw ArgError("null argument");
         if (p->max_iter < 0) throw ArgError("max_iter < 0");
-        if (p->pc != CDFEM_PC_NONE && p->pc != CDFEM_PC_JACOBI) throw ArgError("unknown preconditioner");
+        if (p->pc != CDFEM_PC_NONE && p->pc != CDFEM_PC_JACOBI && p->pc != CDFEM_PC_ILU)
+            throw ArgError("unknown preconditioner");
+        if (p->pc == CDFEM_PC_ILU && p->method != CDFEM_GMRES)
+            throw UnsupportedError("ILU(0) preconditions GMRES (a nonsymmetric preconditioner for CG)");
         *res = cdfem_solver_result{};
         const double *dB = dev_in(c, B, where, c->d_w[6], c->nl);
         double *dX = where == CDFEM_DEVICE ? X : c->d_w[1];

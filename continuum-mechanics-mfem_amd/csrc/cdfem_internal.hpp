@@ -86,6 +86,17 @@ struct GmresState {
 };
 constexpr size_t kGmPollBytes = 32;
 
+// ILU(0) preconditioner state (ilu_kernels.hip)
+struct IluState {
+    bool ready = false;
+    double *F = nullptr;                 // factors in the CSR pattern (unit-lower L, U packed)
+    int32_t *rows_l = nullptr, *rows_u = nullptr;  // rows grouped by level
+    std::vector<int32_t> ptr_l, ptr_u;   // level pointers (host)
+    double *z = nullptr;                 // output of one application
+    hipGraph_t graph = nullptr;          // the captured forward + backward sweeps
+    hipGraphExec_t exec = nullptr;
+};
+
 struct Comm;  // comm.hip
 
 struct ProfileSlot {
@@ -161,6 +172,7 @@ struct cdfem_ctx {
     int64_t nslices = 0, nstored = 0;   // SELL-64 copy (the SpMV layout)
     int32_t *d_sptr = nullptr, *d_srows = nullptr, *d_scols = nullptr, *d_smap = nullptr;
     double *d_svals = nullptr, *d_svals_c = nullptr;
+    cdfem::IluState ilu;                // ILU(0) of the eliminated matrix (GMRES pc = ILU)
 
     // partial assembly
     unsigned kinds = 0;
@@ -311,6 +323,10 @@ hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V
                           GmresState *st, int m, GmresState *poll);
 hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st, GmresState *poll);
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
+// ILU(0) (ilu_kernels.hip): factor + capture once per operator; apply: ilu.z = (LU)^{-1} d_w[4]
+void ilu_setup(cdfem_ctx *c);
+void ilu_free(cdfem_ctx *c);
+hipError_t ilu_apply(cdfem_ctx *c);
 // f64 compute-rate probes: mode 0 VALU v_fma_f64, 1 v_mfma_f64_16x16x4_f64; *flops per launch
 hipError_t launch_fp64_probe(cdfem_ctx *c, int mode, double *out, double *flops);
 

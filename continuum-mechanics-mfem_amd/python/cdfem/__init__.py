@@ -27,7 +27,8 @@ HEADER_PATH = os.path.abspath(os.path.join(_PKG_ROOT, "..", "include", "cdfem.h"
 DIFFUSION, CONVECTION, MASS = 1, 2, 4
 HOST, DEVICE = 0, 1
 CG, GMRES = 0, 1
-PC_NONE, PC_JACOBI = 0, 1
+PC_NONE, PC_JACOBI, PC_ILU = 0, 1, 2
+_PCS = {"none": PC_NONE, "jacobi": PC_JACOBI, "ilu": PC_ILU}
 RULE_OPERATOR, RULE_LINEARFORM, RULE_ERROR = 0, 1, 2
 K_APPLY, K_E2L, K_UPDATE, K_DIRECTION, K_ORTH = 0, 1, 2, 3, 4
 
@@ -355,7 +356,7 @@ class Context:
 
     def solve(self, B, method="cg", pc="jacobi", rel_tol=1e-12, abs_tol=0.0, max_iter=500, restart=30,
               check_every=16, raise_on_fail=False):
-        prm = SolverParams(CG if method == "cg" else GMRES, PC_JACOBI if pc == "jacobi" else PC_NONE,
+        prm = SolverParams(CG if method == "cg" else GMRES, _PCS[pc],
                            int(max_iter), int(restart), float(rel_tol), float(abs_tol), int(check_every), 0)
         res = SolverResult()
         B = _f64(B)
@@ -437,7 +438,7 @@ class Context:
 
     def solve_device(self, dB, dX, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=100,
                      restart=30, check_every=0):
-        prm = SolverParams(CG if method == "cg" else GMRES, PC_JACOBI if pc == "jacobi" else PC_NONE,
+        prm = SolverParams(CG if method == "cg" else GMRES, _PCS[pc],
                            int(max_iter), int(restart), float(rel_tol), float(abs_tol),
                            int(check_every if check_every else max_iter), 0)
         res = SolverResult()

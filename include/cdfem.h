@@ -50,7 +50,7 @@ enum { CDFEM_DIFFUSION = 1, CDFEM_CONVECTION = 2, CDFEM_MASS = 4 };
 enum { CDFEM_HOST = 0, CDFEM_DEVICE = 1 };
 /* Krylov methods and preconditioners */
 enum { CDFEM_CG = 0, CDFEM_GMRES = 1 };
-enum { CDFEM_PC_NONE = 0, CDFEM_PC_JACOBI = 1 };
+enum { CDFEM_PC_NONE = 0, CDFEM_PC_JACOBI = 1, CDFEM_PC_ILU = 2 };
 /* quadrature rules whose points the host may need for coefficient evaluation */
 enum { CDFEM_RULE_OPERATOR = 0, CDFEM_RULE_LINEARFORM = 1, CDFEM_RULE_ERROR = 2 };
 /* kernel ids for cdfem_profile_read */
@@ -153,11 +153,13 @@ int cdfem_form_linear_system(cdfem_ctx *ctx, const double *x, const double *b, d
  * KSPGMRES (left PC, classical Gram-Schmidt, restart, ||M^{-1} r|| <= max(rtol ||M^{-1}b||, atol)).
  * X on input is ignored (zero initial guess, iterative_mode = false), on output the solution.
  * GMRES: restart 1..64; iterations = inner steps; final_norm = last preconditioned residual
- * estimate (PETSc rnorm); single rank only in this version (CDFEM_ERR_UNSUPPORTED otherwise).
+ * estimate (PETSc rnorm).  CDFEM_PC_ILU = ILU(0), natural ordering, no shift: PETSc
+ * "-pc_type bjacobi -sub_pc_type ilu" on one rank (Input/petsc_circle.opts:6-8); GMRES on assembled
+ * (cdfem_fa_setup) operators, single rank.  Multi-rank slabs: CG and GMRES with none / Jacobi.
  * Returns CDFEM_ERR_NOT_CONVERGED (result filled) when max_iter is reached.                     */
 typedef struct {
     int method;        /* CDFEM_CG / CDFEM_GMRES */
-    int pc;            /* CDFEM_PC_NONE / CDFEM_PC_JACOBI */
+    int pc;            /* CDFEM_PC_NONE / CDFEM_PC_JACOBI / CDFEM_PC_ILU (GMRES on FA operators) */
     int max_iter;
     int restart;       /* GMRES restart (PETSc default 30) */
     double rel_tol;

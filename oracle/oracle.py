@@ -194,15 +194,19 @@ def dof_coords_simplex(mesh):
     return xyz
 
 
-def solve_mms_simplex(mesh, prm, kappa, s, c, alpha=1.0, tol=1e-10, atol=1e-12, max_it=500):
-    """C4 driver sequence on the oracle: FA CSR, FormLinearSystem, GMRES(30) + Jacobi, L2 error."""
+def solve_mms_simplex(mesh, prm, kappa, s, c, alpha=1.0, tol=1e-10, atol=1e-12, max_it=500, pc="jacobi"):
+    """C4 driver sequence on the oracle: FA CSR, FormLinearSystem, GMRES(30) + Jacobi (Input/petsc.opts)
+    or + ILU(0) (pc="ilu": Input/petsc_circle.opts), L2 error."""
     A = fa_assemble_simplex(mesh, kappa=kappa, alpha=alpha, s=s, c=c)
     b = lf_assemble_simplex(mesh, prm)
     u = np.zeros(mesh.nl)
     xyz = dof_coords_simplex(mesh)
     u[mesh.ess] = mms_u(prm, xyz[mesh.ess])
     Ac, B = form_linear_system(A, mesh.bdr, u, b)
-    X, info = gmres(Ac, B, dinv=1.0 / Ac.diag(), rtol=tol, atol=atol, max_it=max_it)
+    if pc == "ilu":
+        X, info = gmres_ilu(Ac, B, ilu0(Ac), rtol=tol, atol=atol, max_it=max_it)
+    else:
+        X, info = gmres(Ac, B, dinv=1.0 / Ac.diag(), rtol=tol, atol=atol, max_it=max_it)
     return X, info, l2_error_simplex(mesh, X, prm)
 
 

@@ -115,6 +115,41 @@ def test_driver_gmsh_p3_reference_configuration(exe, tmp_path):
     assert abs(out["l2_abs"] - l2) <= 1e-6 * l2
 
 
+@pytest.mark.gpu
+def test_driver_gmsh_block_jacobi_ilu_options(exe, tmp_path):
+    """The circle variant's solver options (Input/petsc_circle.opts: gmres, rtol 1e-10, atol 1e-12,
+    max_it 2000, bjacobi + preonly/ilu) on a gmsh triangle mesh: ILU(0) on the device against the
+    oracle's ILU(0)-preconditioned GMRES of the same sequence."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import gmsh_synth
+    import cdfem
+    from oracle import oracle as O
+    opts = ("-ksp_type gmres\n-ksp_rtol 1.0e-10\n-ksp_atol 1.0e-12\n-ksp_max_it 2000\n"
+            "-pc_type bjacobi\n-sub_ksp_type preonly\n-sub_pc_type ilu\n")
+    msh = str(tmp_path / "square.msh")
+    gmsh_synth.write_square(msh, 10, perturb=0.2, seed=5)
+    rc, out, err = _run(["-d", "2", "-mesh", msh, "-p", "2", "-c", "1,-2,0", "-m", "3,3,3"], opts, tmp_path)
+    assert rc == 0, err
+    m = cdfem.gmsh_mesh(msh, 2)
+
+    class OM:
+        pass
+    om = OM()
+    om.dim, om.p, om.ne, om.nl, om.verts, om.dofmap, om.ess = 2, 2, m.ne, m.nl, m.verts, m.dofmap, m.ess
+    om.bdr = np.zeros(m.nl, dtype=np.int32)
+    om.bdr[m.ess] = 1
+    prm = O.mms_params(O.MMS_SIN, 2, kappa=0.1, s=1.0, c=(1.0, -2.0), modes=(3, 3, 3), p=2)
+    _, info, l2 = O.solve_mms_simplex(om, prm, 0.1, 1.0, (1.0, -2.0), max_it=2000, pc="ilu")
+    _, info_j, _ = O.solve_mms_simplex(om, prm, 0.1, 1.0, (1.0, -2.0), max_it=2000)
+    assert out["converged"] == 1 and abs(out["iterations"] - info["iterations"]) <= 1
+    assert info["iterations"] < info_j["iterations"]
+    assert abs(out["l2_abs"] - l2) <= 1e-6 * l2
+    bad = opts.replace("-sub_pc_type ilu", "-sub_pc_type lu")
+    rc, _, err = _run(["-d", "2", "-mesh", msh, "-p", "2"], bad, tmp_path)
+    assert rc == 3 and "sub solver" in err
+
+
 def _oracle_diffusion_mms(mesh, simplex, alpha, dt, T):
     """diffusion_mms.cpp:289-459 on the oracle: backward Euler, GMRES(30)+Jacobi per step."""
     from oracle import oracle as O

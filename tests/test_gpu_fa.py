@@ -188,3 +188,43 @@ def test_fa_c4_full_size_properties(gpu_ctx):
     true = np.linalg.norm(dinv * r)
     assert abs(true - info["final_norm"]) <= 1e-6 * true
     assert info["final_norm"] <= 1e-3 * info["initial_norm"]
+
+
+@pytest.mark.parametrize("dim,n,p,pert", [(2, 8, 2, 0.15), (3, 4, 2, 0.1), (2, 10, 1, 0.1)])
+def test_fa_gmres_ilu_parity(gpu_ctx, dim, n, p, pert):
+    """GMRES left-preconditioned with ILU(0) (Input/petsc_circle.opts: bjacobi + ilu, one block per
+    rank) against the oracle's ILU(0) GMRES: fixed steps across restarts to 1e-11, converged to the
+    reference's tolerances with the same iteration count (+-1); ILU needs fewer steps than Jacobi."""
+    gm, om, A = _setup(gpu_ctx, dim, n, p, pert)
+    rng = np.random.default_rng(11)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    F = O.ilu0(Ac)
+    xo, io = O.gmres_ilu(Ac, Bo, F, restart=7, rtol=0.0, atol=0.0, max_it=25)
+    xg, ig = gpu_ctx.solve(B, method="gmres", pc="ilu", restart=7, rel_tol=0.0, abs_tol=0.0, max_iter=25)
+    assert io["iterations"] == ig["iterations"] == 25
+    assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
+    xo, io = O.gmres_ilu(Ac, Bo, F, restart=30, rtol=1e-10, atol=1e-12, max_it=2000)
+    xg, ig = gpu_ctx.solve(B, method="gmres", pc="ilu", restart=30, rel_tol=1e-10, abs_tol=1e-12, max_iter=2000)
+    assert io["converged"] and ig["converged"] and abs(io["iterations"] - ig["iterations"]) <= 1
+    assert np.linalg.norm(xg - xo) <= 1e-8 * np.linalg.norm(xo)
+    _, ij = gpu_ctx.solve(B, method="gmres", pc="jacobi", restart=30, rel_tol=1e-10, abs_tol=1e-12, max_iter=2000)
+    assert ig["iterations"] < ij["iterations"]
+    # repeated solves reuse the factors and the captured sweep graph: bitwise identical
+    xg2, _ = gpu_ctx.solve(B, method="gmres", pc="ilu", restart=30, rel_tol=1e-10, abs_tol=1e-12, max_iter=2000)
+    np.testing.assert_array_equal(xg, xg2)
+
+
+def test_ilu_rejected_for_cg_and_pa(gpu_ctx):
+    gm, om, A = _setup(gpu_ctx, 2, 3, 1, 0.0)
+    B = np.ones(om.nl)
+    with pytest.raises(cdfem.CdfemError):
+        gpu_ctx.solve(B, method="cg", pc="ilu")
+    m = cdfem.box_mesh(2, 3, 1)
+    gpu_ctx.upload_mesh(m)
+    gpu_ctx.pa_setup(kinds=5, kappa=0.1, mass=1.0)
+    with pytest.raises(cdfem.CdfemError):
+        gpu_ctx.solve(np.ones(m.nl), method="gmres", pc="ilu")
