@@ -251,16 +251,27 @@ def main():
         nzr, nz = n, n * world
     mesh = cdfem.box_mesh(3, (n, n, nz), p, z_range=(rank * nzr, (rank + 1) * nzr), with_coords=False)
     ndev = cdfem.device_count()
-    ctx = cdfem.Context(local % ndev if args.comm == "host" else local)
+    ctx = cdfem.Context(local % ndev)  # one rank per GPU on a node; ranks share a GPU only in rehearsals
     ctx.upload_mesh(mesh)
     if args.path == "brick" or p >= 3:
         ctx.set_structured(n, n, nzr)  # p >= 3: structured E->L (no position arrays)
     if world > 1:
         if args.comm == "rccl":
-            # RCCL communicator over xGMI; the id travels over the gloo control group
+            # RCCL communicator over xGMI; the id travels over the gloo control group.  Every rank
+            # reports whether its init succeeded; if any failed, all ranks fall back to the
+            # host-callback communicator (same results, slower exchange) and the JSON line says so
             obj = [cdfem.comm_unique_id() if rank == 0 else None]
             pg.broadcast_object_list(obj, src=0)
-            ctx.comm_init_rccl(rank, world, obj[0])
+            err = None
+            try:
+                ctx.comm_init_rccl(rank, world, obj[0])
+            except cdfem.CdfemError as e:
+                err = str(e)
+            if allmax(pg, 1.0 if err else 0.0) > 0.0:
+                print(f"rank {rank}: RCCL communicator unavailable ({err or 'failed on another rank'}); "
+                      "falling back to host callbacks", file=sys.stderr, flush=True)
+                ctx.comm_init_torch()
+                args.comm = "host (RCCL init failed)"
         else:
             ctx.comm_init_torch()
         ctx.set_slab(rank > 0, rank < world - 1)
