@@ -379,3 +379,38 @@ def test_brick_full_size_matches_generic(gpu_ctx):
     gpu_ctx.pa_setup(kinds=7, kappa=0.1, conv=C3, mass=1.0)
     y_brk = gpu_ctx.mult(x, constrained=True)
     assert _relmax(y_brk, y_gen) <= 1e-14
+
+
+def test_config_c1_reference_case(gpu_ctx):
+    """BASELINE configs[0]: the reference's CPU-runnable case, 2D 64 x 64 quads, H1 order 1, the
+    driver's MMS (linear_convection_diffusion_2D.cpp:159-215, Input/input_2d.yaml: kappa 0.1,
+    s 1, c (1, -2), modes 3, 3).  The reference solves it with full assembly on the CPU; here the
+    same system goes through the GPU path.  The SPD part (c = 0) under CG and the full operator
+    under GMRES(30) + Jacobi (Input/petsc.opts) against the oracle's FA restatement: the same
+    iteration counts (+-1), solutions to the stopping-tolerance bound and equal L2 errors."""
+    n, p = 64, 1
+    om, gm = _mesh_pair(2, n, p)
+    for c, solver in (((0.0, 0.0), "cg"), ((1.0, -2.0), "gmres")):
+        kinds = 5 if solver == "cg" else 7
+        ctx = _ctx(gpu_ctx, gm, kinds, c=c)
+        xq = ctx.quadrature_points(cdfem.RULE_LINEARFORM)
+        b = ctx.lf_assemble(_mms_f_numpy(xq, 2, c=c).reshape(-1))
+        prm = O.mms_params(O.MMS_SIN, 2, kappa=0.1, s=1.0, c=c, p=p)
+        u = np.zeros(om.nl)
+        u[om.ess] = O.mms_u(prm, om.dof_coords()[om.ess])
+        _, B = ctx.form_linear_system(u, b)
+        A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=c, kinds=_kinds_to_oracle(kinds))
+        Ac, Bo = O.form_linear_system(A, om.bdr, u, O.lf_assemble(om, prm))
+        assert np.abs(B - Bo).max() <= 1e-13 * np.abs(Bo).max()
+        if solver == "cg":
+            xg, ig = ctx.solve(B, method="cg", rel_tol=1e-12, max_iter=2000)
+            xo, io = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=1e-12, max_iter=2000)
+            tol = 1e-10
+        else:
+            xg, ig = ctx.solve(B, method="gmres", restart=30, rel_tol=1e-10, abs_tol=1e-12, max_iter=2000)
+            xo, io = O.gmres(Ac, Bo, dinv=1.0 / Ac.diag(), restart=30, rtol=1e-10, atol=1e-12, max_it=2000)
+            tol = 1e-8
+        assert ig["converged"] and io["converged"] and abs(ig["iterations"] - io["iterations"]) <= 1
+        assert np.linalg.norm(xg - xo) <= tol * np.linalg.norm(xo)
+        eg, eo = O.l2_error(om, xg, prm), O.l2_error(om, xo, prm)
+        assert abs(eg - eo) <= 1e-6 * eo and eo < 1e-2
