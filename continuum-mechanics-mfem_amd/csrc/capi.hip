@@ -95,7 +95,7 @@ void free_mesh(cdfem_ctx *c)
     for (auto &b : c->d_if) dfree(b);
     dfree(c->d_stab); dfree(c->d_stab_lf); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);
     dfree(c->d_cpos); dfree(c->d_vals); dfree(c->d_vals_c); dfree(c->d_Ee);
-    dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_svals);
+    dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_sdel); dfree(c->d_svals);
     dfree(c->d_svals_c);
     ilu_free(c);
     c->nslices = c->nstored = 0;
@@ -997,6 +997,10 @@ int cdfem_fa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kap
             HIPCHK(hipMemcpyAsync(c->d_srows, P.srows.data(), P.srows.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_scols, P.scols.data(), P.scols.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_smap, P.smap.data(), P.smap.size() * 4, hipMemcpyHostToDevice, c->stream));
+            if (!P.sdel.empty()) {
+                c->d_sdel = dalloc<int16_t>(P.sdel.size());
+                HIPCHK(hipMemcpyAsync(c->d_sdel, P.sdel.data(), P.sdel.size() * 2, hipMemcpyHostToDevice, c->stream));
+            }
             HIPCHK(hipStreamSynchronize(c->stream));  // P's host buffers die at scope exit
         }
         const size_t neq = (size_t)c->ne * c->nq_simplex;
@@ -1210,6 +1214,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "brick_xcd") {
             if (value < 0 || value > 1) throw ArgError("brick_xcd must be 0 or 1");
             c->brick_xcd = value;
+        } else if (k == "spmv_index16") {
+            if (value < 0 || value > 1) throw ArgError("spmv_index16 must be 0 or 1");
+            c->spmv_index16 = value;
         } else if (k == "profile_mask") {
             c->prof_mask = (unsigned)value;
         } else if (k == "brick_waves") {
@@ -1260,7 +1267,8 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
         const double nl = (double)c->nl, ne = (double)c->ne, nd = c->nd;
         if (c->fa_ready) {  // CSR SpMV: values + columns + row pointers + x + y
             if (k != CDFEM_K_APPLY) throw ArgError("FA operators report the SpMV (CDFEM_K_APPLY) only");
-            *bytes = 12.0 * (double)c->nnz + 4.0 * (nl + 1) + 16.0 * nl;  // (SELL adds < 1 % padding)
+            // (SELL adds < 1 % padding; 16-bit column deltas when the bandwidth fits)
+            *bytes = (spmv_delta(c) ? 10.0 : 12.0) * (double)c->nnz + 4.0 * (nl + 1) + 16.0 * nl;
             return CDFEM_OK;
         }
         const double nq = nq_of(c, c->rule_op);

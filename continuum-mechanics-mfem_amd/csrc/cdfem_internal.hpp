@@ -171,6 +171,8 @@ struct cdfem_ctx {
     double *d_Ee = nullptr;             // element matrices [blk][nd*nd][64]
     int64_t nslices = 0, nstored = 0;   // SELL-64 copy (the SpMV layout)
     int32_t *d_sptr = nullptr, *d_srows = nullptr, *d_scols = nullptr, *d_smap = nullptr;
+    int16_t *d_sdel = nullptr;          // 16-bit column deltas (null when the bandwidth does not fit)
+    int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     double *d_svals = nullptr, *d_svals_c = nullptr;
     cdfem::IluState ilu;                // ILU(0) of the eliminated matrix (GMRES pc = ILU)
 
@@ -302,6 +304,7 @@ struct FaPattern {
     std::vector<int32_t> srows;  // [nslices * 64] original row of (slice, lane), -1 = padding
     std::vector<int32_t> scols;  // [stored] column, slice-major then entry-major then lane
     std::vector<int32_t> smap;   // [stored] CSR index of the stored entry, -1 = padding
+    std::vector<int16_t> sdel;   // [stored] column - row when every |column - row| < 2^15, else empty
 };
 FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl);
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, double kappa, double alpha, const double *conv,
@@ -312,6 +315,7 @@ hipError_t launch_sell_fill(cdfem_ctx *c);
 hipError_t launch_csr_diag(cdfem_ctx *c, double *d);
 hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y);
 hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q);
+bool spmv_delta(const cdfem_ctx *c);
 
 // GMRES(m) (gmres.hip)
 int gmres_blocks(int64_t n);

@@ -198,7 +198,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "brick_variant": 0..6 — element core of the structured CG kernel (unrolled / plane loop /
  *                  low-register; 3-5 the same at 2 waves per SIMD; 6 temporal qdata loads).
  * "brick_xcd": 1 (default) — XCD-contiguous brick order of the structured CG kernel; 0 = the
- *              dispatcher's round-robin order.                                                  */
+ *              dispatcher's round-robin order.
+ * "spmv_index16": 1 (default) — the assembled-operator SpMV streams 16-bit column deltas when
+ *                 every |column - row| < 2^15; 0 = 32-bit columns.                             */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
 
 /* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */

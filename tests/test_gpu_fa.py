@@ -190,6 +190,47 @@ def test_fa_c4_full_size_properties(gpu_ctx):
     assert info["final_norm"] <= 1e-3 * info["initial_norm"]
 
 
+def test_fa_spmv_index16_matches_int32(gpu_ctx):
+    """The SpMV's 16-bit column deltas (set_option "spmv_index16", the default) give the same bits
+    as 32-bit columns, for Mult, the constrained Mult and a CG solve; a random DoF numbering
+    (bandwidth > 2^15) falls back to 32-bit columns and gives the permuted result."""
+    gm = cdfem.kuhn_mesh(3, 16, 2, perturb=0.1)      # 35,937 DoFs, lattice bandwidth 2,180
+    rng = np.random.default_rng(16)
+    x = rng.uniform(-1, 1, gm.nl)
+    b = rng.uniform(-1, 1, gm.nl)
+    res = {}
+    try:
+        for flag in (1, 0):
+            gpu_ctx.set_option("spmv_index16", flag)
+            gpu_ctx.upload_mesh(gm)
+            gpu_ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            _, B = gpu_ctx.form_linear_system(np.zeros(gm.nl), b)
+            X, info = gpu_ctx.solve(B, method="gmres", restart=30, rel_tol=0.0, abs_tol=0.0, max_iter=40)
+            res[flag] = (gpu_ctx.mult(x), gpu_ctx.mult(x, constrained=True), X,
+                         gpu_ctx.kernel_bytes(cdfem.K_APPLY))
+        for a, c in zip(res[1][:3], res[0][:3]):
+            np.testing.assert_array_equal(a, c)
+        nnz = len(gpu_ctx.fa_csr()[1])
+        assert res[0][3] - res[1][3] == 2.0 * nnz       # 10 instead of 12 bytes per entry
+        # random numbering: deltas overflow 16 bits, the 32-bit path runs even with the option on
+        gpu_ctx.set_option("spmv_index16", 1)
+        perm = rng.permutation(gm.nl).astype(np.int32)
+        xyzp = np.empty_like(gm.dof_xyz)
+        xyzp[perm] = gm.dof_xyz
+        gp = cdfem.Mesh(gm.dim, gm.order, gm.verts, perm[gm.dofmap], gm.nl, perm[gm.ess], xyzp,
+                        simplex=True)
+        gpu_ctx.upload_mesh(gp)
+        gpu_ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+        assert gpu_ctx.kernel_bytes(cdfem.K_APPLY) == res[0][3]
+        xp = np.empty_like(x)
+        xp[perm] = x
+        yp = gpu_ctx.mult(xp)
+        y = res[1][0]
+        assert np.abs(yp[perm] - y).max() <= 1e-13 * np.abs(y).max()
+    finally:
+        gpu_ctx.set_option("spmv_index16", 1)
+
+
 @pytest.mark.parametrize("dim,n,p,pert", [(2, 8, 2, 0.15), (3, 4, 2, 0.1), (2, 10, 1, 0.1)])
 def test_fa_gmres_ilu_parity(gpu_ctx, dim, n, p, pert):
     """GMRES left-preconditioned with ILU(0) (Input/petsc_circle.opts: bjacobi + ilu, one block per
