@@ -218,6 +218,12 @@ def main_c4(args):
                     "other_kernels_avg_us": {"gmres_orth": round(o_ms / max(o_cnt, 1) * 1e3, 2)}}
     rp, _, _ = ctx.fa_csr()
     nnz = int(rp[-1])
+    if roof is not None:
+        # SURVEY.md 8(d) prices the SpMV at 12 B per nonzero (32-bit columns); the kernel streams
+        # 16-bit column deltas, so the bytes it must move (algorithmic_bytes_per_launch) are fewer
+        sb = 12.0 * nnz + 4.0 * (mesh.nl + 1) + 16.0 * mesh.nl
+        roof["survey_bytes_per_launch"] = sb
+        roof["survey_frac"] = round(sb / (roof["avg_launch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     cpu = None
     if not args.no_cpu_baseline:
         try:

@@ -90,7 +90,7 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_verts); dfree(c->d_map); dfree(c->d_e2l_off); dfree(c->d_e2l_pos);
     dfree(c->d_ess); dfree(c->d_ess_list); dfree(c->d_qd); dfree(c->d_Ye); dfree(c->d_dinv);
     for (auto &w : c->d_w) dfree(w);
-    dfree(c->d_part); dfree(c->d_gm); dfree(c->d_gm_part);
+    dfree(c->d_part); dfree(c->d_tpart); dfree(c->d_gm); dfree(c->d_gm_part);
     dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones); dfree(c->d_dalt);
     for (auto &b : c->d_if) dfree(b);
     dfree(c->d_stab); dfree(c->d_stab_lf); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);
@@ -384,6 +384,10 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     const int check = p.check_every > 0 ? p.check_every : 16;
     const bool mr = multi_rank(c);
     double *red = c->d_state->red;  // device scalars awaiting the all-reduce (multi-rank)
+    // high order on a structured box, one rank: den from the apply's E-vector, E->L fused into the
+    // update (ho_kernels.hip k_apply3d_tile<DEN>, vec_kernels.hip k_e2l_box<UPD>)
+    const bool fused = !mr && !c->fa_ready && c->cg_fused && tile_den_ok(c) && e2l_box_ok(c);
+    if (fused && !c->d_tpart) c->d_tpart = dalloc<double>(tile_den_blocks(c));
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     if (mr) {
@@ -396,6 +400,14 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     // z = A d ; den = (d, z) and the MFEM den step
     auto apply = [&] {
         prof_mark(c, CDFEM_K_APPLY, true);
+        if (fused) {  // Ye = A_c d and den; q stays an E-vector until the update
+            HIPCHK(launch_apply_den(c, d, c->d_Ye, c->d_state, c->d_tpart));
+            prof_mark(c, CDFEM_K_APPLY, false);
+            prof_mark(c, CDFEM_K_E2L, true);
+            HIPCHK(launch_den_from_partials(c, c->d_tpart, tile_den_blocks(c)));
+            prof_mark(c, CDFEM_K_E2L, false);
+            return;
+        }
         if (c->fa_ready) {
             HIPCHK(launch_spmv_cg(c, d, z));
             prof_mark(c, CDFEM_K_APPLY, false);
@@ -421,7 +433,8 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     for (;;) {
         for (int k = 0; k < check && launched < p.max_iter; ++k, ++launched) {
             prof_mark(c, CDFEM_K_UPDATE, true);
-            HIPCHK(launch_cg_update(c, x, r, z, d, dinv));
+            if (fused) HIPCHK(launch_e2l_cg_update(c, c->d_Ye, d, x, r, z, dinv));
+            else HIPCHK(launch_cg_update(c, x, r, z, d, dinv));
             if (mr) {
                 comm_allreduce(c, red + 1, 1);
                 HIPCHK(launch_update_step(c));
@@ -1214,6 +1227,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "brick_xcd") {
             if (value < 0 || value > 1) throw ArgError("brick_xcd must be 0 or 1");
             c->brick_xcd = value;
+        } else if (k == "cg_fused") {
+            if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
+            c->cg_fused = value;
         } else if (k == "spmv_index16") {
             if (value < 0 || value > 1) throw ArgError("spmv_index16 must be 0 or 1");
             c->spmv_index16 = value;

@@ -171,7 +171,9 @@ struct cdfem_ctx {
     double *d_Ee = nullptr;             // element matrices [blk][nd*nd][64]
     int64_t nslices = 0, nstored = 0;   // SELL-64 copy (the SpMV layout)
     int32_t *d_sptr = nullptr, *d_srows = nullptr, *d_scols = nullptr, *d_smap = nullptr;
+    double *d_tpart = nullptr;          // den partials of the fused high-order CG apply (one per tile block)
     int16_t *d_sdel = nullptr;          // 16-bit column deltas (null when the bandwidth does not fit)
+    int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     double *d_svals = nullptr, *d_svals_c = nullptr;
     cdfem::IluState ilu;                // ILU(0) of the eliminated matrix (GMRES pc = ILU)
@@ -316,6 +318,14 @@ hipError_t launch_csr_diag(cdfem_ctx *c, double *d);
 hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y);
 hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q);
 bool spmv_delta(const cdfem_ctx *c);
+// fused high-order CG iteration (ho_kernels.hip / vec_kernels.hip)
+bool tile_den_ok(const cdfem_ctx *c);
+int tile_den_blocks(const cdfem_ctx *c);
+hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part);
+bool e2l_box_ok(const cdfem_ctx *c);
+hipError_t launch_den_from_partials(cdfem_ctx *c, const double *in, int64_t n);
+hipError_t launch_e2l_cg_update(cdfem_ctx *c, const double *Ye, const double *d, double *x, double *r, double *z,
+                                const double *dinv);
 
 // GMRES(m) (gmres.hip)
 int gmres_blocks(int64_t n);

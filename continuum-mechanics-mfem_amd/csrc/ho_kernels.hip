@@ -34,22 +34,30 @@
 
 #include "cdfem_internal.hpp"
 #include "pa_core.hpp"
+#include "reduce.hpp"
 
 namespace cdfem {
 
 // structured-box geometry of the lattice gather / pencil E-vector (LAT = true)
 struct TileGeo {
     HoLayout ho;
-    uint32_t Lx, Ly;
+    uint32_t Lx, Ly, nz;
     const uint8_t *ess;
 };
 
-template <int D1, int Q1, unsigned K, bool CON, bool LAT>
+// DEN (CG mode, structured box, constrained): the block also publishes its share of
+// den = (d, A_c d) from the E-vector it writes, sum_e sum_l d~[map(e,l)] Ye[e,l] (d~ = d with the
+// essential entries zeroed), plus d_i^2 for each essential DoF i counted once, in the element
+// that owns it (the highest element index along each axis).  That is exactly (d, q) with q the
+// constrained L-vector, so the E->L sum no longer has to precede the den step and can be fused
+// into the CG update (k_e2l_box<UPD>).
+template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN>
 __global__ void __launch_bounds__(256)
 k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qd,
                double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const TileGeo geo,
-               const KrylovState *__restrict__ st)
+               const KrylovState *__restrict__ st, double *__restrict__ part)
 {
+    static_assert(!DEN || (CON && LAT), "den partials need the constrained lattice path");
     if (st != nullptr && st->done) return;
     using L = QLayout<K, 3>;
     constexpr int NC = L::nc, NP = NC / 2, QQ = Q1 * Q1, ND = D1 * D1 * D1;
@@ -245,6 +253,7 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     }
     __syncthreads();
     // stage x^T -> E-vector: threads (dx = tx, dy = ty)
+    double dacc = 0.0;
     if (valid && tx < D1 && ty < D1) {
         double cb[Q1], cg[Q1];
 #pragma unroll
@@ -271,12 +280,23 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
                 y += cb[qx] * Bf[j] + cg[qx] * Bf[D1 * D1 * Q1 + j];
             }
             ye[dz * zs] = y;
+            if constexpr (DEN) {
+                constexpr int P = D1 - 1;
+                const bool own = (tx < P || ex == geo.ho.nx - 1) && (ty < P || ey == geo.ho.ny - 1) &&
+                                 (dz < P || ez == geo.nz - 1);
+                dacc += m[dz] != 0 ? (own ? xr[dz] * xr[dz] : 0.0) : xr[dz] * y;
+            }
         }
+    }
+    if constexpr (DEN) {
+        __shared__ double shd[256 / 64];
+        store_partial(block_sum(dacc, shd), part);
     }
 }
 
 template <int D1, int Q1, unsigned K>
-static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
+static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
+                             double *den_part)
 {
     const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
     constexpr int EPB = 256 / (Q1 * Q1);
@@ -285,36 +305,42 @@ static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con
     geo.ho = ho_layout(c);
     geo.Lx = (uint32_t)c->Lx;
     geo.Ly = (uint32_t)c->Ly;
+    geo.nz = c->epencil ? (uint32_t)(c->ne / ((int64_t)geo.ho.nx * geo.ho.ny)) : 0;
     geo.ess = c->d_ess;
-    if (c->epencil) {
+    if (den_part) {
+        if (!c->epencil || !con) return hipErrorInvalidValue;
+        CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true>), grid, block, 0, c->d_map, x, c->d_qd, Ye, T,
+                     c->ne, geo, st, den_part);
+    } else if (c->epencil) {
         if (con)
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st);
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, false>), grid, block, 0, c->d_map, x, c->d_qd,
+                         Ye, T, c->ne, geo, st, (double *)nullptr);
         else
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, true>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st);
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, true, false>), grid, block, 0, c->d_map, x, c->d_qd,
+                         Ye, T, c->ne, geo, st, (double *)nullptr);
     } else {
         if (con)
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, false>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st);
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, false, false>), grid, block, 0, c->d_map, x, c->d_qd,
+                         Ye, T, c->ne, geo, st, (double *)nullptr);
         else
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, false>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st);
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, false, false>), grid, block, 0, c->d_map, x,
+                         c->d_qd, Ye, T, c->ne, geo, st, (double *)nullptr);
     }
     return hipGetLastError();
 }
 
 template <int D1, int Q1>
-static hipError_t tile_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
+static hipError_t tile_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
+                          double *den_part)
 {
     switch (c->kinds) {
-    case 1: return tile_kinds<D1, Q1, 1>(c, x, Ye, con, st);
-    case 2: return tile_kinds<D1, Q1, 2>(c, x, Ye, con, st);
-    case 3: return tile_kinds<D1, Q1, 3>(c, x, Ye, con, st);
-    case 4: return tile_kinds<D1, Q1, 4>(c, x, Ye, con, st);
-    case 5: return tile_kinds<D1, Q1, 5>(c, x, Ye, con, st);
-    case 6: return tile_kinds<D1, Q1, 6>(c, x, Ye, con, st);
-    case 7: return tile_kinds<D1, Q1, 7>(c, x, Ye, con, st);
+    case 1: return tile_kinds<D1, Q1, 1>(c, x, Ye, con, st, den_part);
+    case 2: return tile_kinds<D1, Q1, 2>(c, x, Ye, con, st, den_part);
+    case 3: return tile_kinds<D1, Q1, 3>(c, x, Ye, con, st, den_part);
+    case 4: return tile_kinds<D1, Q1, 4>(c, x, Ye, con, st, den_part);
+    case 5: return tile_kinds<D1, Q1, 5>(c, x, Ye, con, st, den_part);
+    case 6: return tile_kinds<D1, Q1, 6>(c, x, Ye, con, st, den_part);
+    case 7: return tile_kinds<D1, Q1, 7>(c, x, Ye, con, st, den_part);
     default: return hipErrorInvalidValue;
     }
 }
@@ -322,8 +348,29 @@ static hipError_t tile_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, c
 hipError_t launch_apply_wpe(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st)
 {
     const int q1 = c->rule_op.q1;
-    if (c->p == 3 && q1 == 5) return tile_dq<4, 5>(c, x, Ye, con, st);
-    if (c->p == 4 && q1 == 6) return tile_dq<5, 6>(c, x, Ye, con, st);
+    if (c->p == 3 && q1 == 5) return tile_dq<4, 5>(c, x, Ye, con, st, nullptr);
+    if (c->p == 4 && q1 == 6) return tile_dq<5, 6>(c, x, Ye, con, st, nullptr);
+    return hipErrorInvalidValue;
+}
+
+int tile_den_blocks(const cdfem_ctx *c)
+{
+    const int q1 = c->rule_op.q1;
+    return (int)((c->ne + 256 / (q1 * q1) - 1) / (256 / (q1 * q1)));
+}
+
+bool tile_den_ok(const cdfem_ctx *c)
+{
+    const int q1 = c->rule_op.q1;
+    return c->dim == 3 && c->epencil && c->structured && ((c->p == 3 && q1 == 5) || (c->p == 4 && q1 == 6));
+}
+
+// CG mode: Ye = A_c d (E-vector) and the den partials (one per block) into part
+hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part)
+{
+    const int q1 = c->rule_op.q1;
+    if (c->p == 3 && q1 == 5) return tile_dq<4, 5>(c, d, Ye, true, st, part);
+    if (c->p == 4 && q1 == 6) return tile_dq<5, 6>(c, d, Ye, true, st, part);
     return hipErrorInvalidValue;
 }
 

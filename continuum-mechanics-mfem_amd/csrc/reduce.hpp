@@ -1,7 +1,6 @@
 // reduce.hpp — deterministic block / grid reductions and the MFEM CG "den" step (device code).
 //
-// Grid reductions: every block publishes one partial; the LAST arriving block (agent-scope
-// release before the ticket, acquire after it: MI355X_MICROARCH.md "Valid forms") sums the
+// Grid reductions: every block publishes one partial; a one-block finalize kernel sums the
 // partials in index order, so the result is bitwise reproducible and independent of dispatch
 // order and XCD placement.
 #pragma once

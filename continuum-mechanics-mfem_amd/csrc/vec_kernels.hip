@@ -82,18 +82,25 @@ __device__ __forceinline__ int axis_pairs(uint32_t g, uint32_t n, int *el, int *
     return k;
 }
 
-template <bool CON, bool CG, int P>
+// UPD (CG mode with the den already known from the apply, k_apply3d_tile<DEN>): the E->L sum
+// q_i is consumed in place by the CG update instead of being stored:
+//   x_i += alpha d_i, r_i -= alpha q_i, y_i = z_i = M^-1 r_i, partial (r, z)
+// (x here is d; xs, r, dinv are the solution, residual and Jacobi inverse).
+template <bool CON, bool CG, int P, bool UPD = false>
 __global__ void __launch_bounds__(kRedThreads)
 k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__restrict__ Ye,
           const double *__restrict__ x, double *__restrict__ y, int64_t nl, double *__restrict__ part,
-          KrylovState *__restrict__ st)
+          KrylovState *__restrict__ st, double *__restrict__ xs = nullptr, double *__restrict__ res = nullptr,
+          const double *__restrict__ dinv = nullptr)
 {
+    static_assert(!UPD || (CON && CG), "the fused update is the constrained CG mode");
     // one wave per x-row (gy, gz) of the dof lattice (grid-stride over rows): the y / z element
     // pairs are uniform across the wave, lanes run along x, and the row's contributions are one
     // contiguous run of the pencil E-vector (entries gx + ex - 1 and gx + ex, ex = gx / P)
     constexpr int D1 = P + 1;
     __shared__ double sh[kRedThreads / 64];
     if (CG && st->done) return;
+    const double alpha = UPD ? st->alpha : 0.0;
     double acc = 0.0;
     const int lane = threadIdx.x & 63;
     const uint32_t rows = bx.Ly * (uint32_t)(nl / ((int64_t)bx.Lx * bx.Ly));
@@ -129,6 +136,12 @@ k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__rest
             }
             const bool is_ess = CON && ess[i];
             const double xi = (CON || CG) ? x[i] : 0.0;
+            double si = 0.0, ri = 0.0, mi = 1.0;
+            if constexpr (UPD) {
+                si = xs[i];
+                ri = res[i];
+                if (dinv) mi = dinv[i];
+            }
             double v = 0.0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -138,8 +151,17 @@ k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__rest
                 }
             }
             if (is_ess) v = xi;
-            y[i] = v;
-            if (CG) acc += v * xi;
+            if constexpr (UPD) {
+                xs[i] = si + alpha * xi;
+                ri -= alpha * v;
+                res[i] = ri;
+                const double zi = mi * ri;
+                y[i] = zi;
+                acc += ri * zi;
+            } else {
+                y[i] = v;
+                if (CG) acc += v * xi;
+            }
         }
     }
     if (!CG) return;
@@ -393,6 +415,73 @@ hipError_t launch_update_fin(cdfem_ctx *c, int nparts)
 {
     hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, nparts, c->d_state);
     return hipGetLastError();
+}
+
+static BoxE2L box_e2l(const cdfem_ctx *c)
+{
+    BoxE2L bx;
+    bx.Lx = (uint32_t)c->Lx;
+    bx.Ly = (uint32_t)c->Ly;
+    bx.nx = (uint32_t)c->sx;
+    bx.ny = (uint32_t)c->sy;
+    bx.nz = (uint32_t)c->sz;
+    bx.fLx = make_fastdiv(bx.Lx);
+    bx.fLxy = make_fastdiv(bx.Lx * bx.Ly);
+    return bx;
+}
+
+static dim3 box_grid(const cdfem_ctx *c) { return dim3((unsigned)std::min<int64_t>((c->Ly * c->Lz + 3) / 4, 65536)); }
+
+bool e2l_box_ok(const cdfem_ctx *c)
+{
+    return c->structured && c->qlay == 1 && c->nl < ((int64_t)1 << 32) && (c->p == 3 || c->p == 4);
+}
+
+// grid partials in[0..n) -> part[0..kDenStage) (fixed ranges, fixed order), then the den step
+__global__ void __launch_bounds__(kRedThreads)
+k_part_reduce(const double *__restrict__ in, int64_t n, double *__restrict__ part, const KrylovState *__restrict__ st)
+{
+    __shared__ double sh[kRedThreads / 64];
+    if (st->done) return;
+    const int64_t chunk = (n + gridDim.x - 1) / gridDim.x, b0 = (int64_t)blockIdx.x * chunk;
+    const int64_t b1 = b0 + chunk < n ? b0 + chunk : n;
+    double v = 0.0;
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) v += in[i];
+    store_partial(block_sum(v, sh), part);
+}
+
+constexpr int kDenStage = 256;
+
+hipError_t launch_den_from_partials(cdfem_ctx *c, const double *in, int64_t n)
+{
+    hipLaunchKernelGGL(k_part_reduce, dim3(kDenStage), dim3(kRedThreads), 0, c->stream, in, n, c->d_part,
+                       (const KrylovState *)c->d_state);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_den_fin(c, kDenStage);
+}
+
+template <int P>
+static hipError_t launch_e2l_update_p(cdfem_ctx *c, const double *Ye, const double *d, double *x, double *r,
+                                      double *z, const double *dinv)
+{
+    const dim3 g = box_grid(c), b(kRedThreads);
+    hipLaunchKernelGGL((k_e2l_box<true, true, P, true>), g, b, 0, c->stream, box_e2l(c), c->d_ess, Ye, d, z, c->nl,
+                       c->d_part, c->d_state, x, r, dinv);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g.x, c->d_state);
+    return hipGetLastError();
+}
+
+// fused E->L sum + CG update (single rank, den already stepped): x += alpha d, r -= alpha q,
+// z = M^-1 r, betanom and the MFEM convergence test
+hipError_t launch_e2l_cg_update(cdfem_ctx *c, const double *Ye, const double *d, double *x, double *r, double *z,
+                                const double *dinv)
+{
+    if (!e2l_box_ok(c)) return hipErrorInvalidValue;
+    if (c->p == 3) return launch_e2l_update_p<3>(c, Ye, d, x, r, z, dinv);
+    return launch_e2l_update_p<4>(c, Ye, d, x, r, z, dinv);
 }
 
 template <int P>

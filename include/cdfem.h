@@ -199,6 +199,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *                  low-register; 3-5 the same at 2 waves per SIMD; 6 temporal qdata loads).
  * "brick_xcd": 1 (default) — XCD-contiguous brick order of the structured CG kernel; 0 = the
  *              dispatcher's round-robin order.
+ * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
+ *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
+ *             E->L kernel (results agree to rounding).
  * "spmv_index16": 1 (default) — the assembled-operator SpMV streams 16-bit column deltas when
  *                 every |column - row| < 2^15; 0 = 32-bit columns.                             */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);

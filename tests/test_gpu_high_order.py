@@ -91,6 +91,62 @@ def test_ho_cg_parity(gpu_ctx):
     assert np.linalg.norm(xg - xo) <= 1e-8 * np.linalg.norm(xo)
 
 
+@pytest.mark.parametrize("n,p,pert", [(3, 4, 0.1), (3, 3, 0.15)])
+def test_ho_fused_cg_parity(gpu_ctx, n, p, pert):
+    """Structured boxes run the fused high-order CG iteration (den from the apply's E-vector, E->L
+    inside the update): fixed iterates against the oracle with non-zero essential values (so the
+    essential DoFs' d_i^2 term of den is exercised), and against the unfused path."""
+    om = O.BoxMesh(3, n, p, perturb=pert)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(5))
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    rng = np.random.default_rng(12)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, io = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=50)
+    out = {}
+    try:
+        for fused in (1, 0):
+            gpu_ctx.set_option("cg_fused", fused)
+            gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+            gpu_ctx.pa_setup(kinds=5, kappa=0.1, mass=1.0)
+            _, B = gpu_ctx.form_linear_system(u, b)
+            out[fused] = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=50, check_every=7)
+    finally:
+        gpu_ctx.set_option("cg_fused", 1)
+    for fused, (xg, ig) in out.items():
+        assert io["iterations"] == ig["iterations"] == 50
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), fused
+    # the residual norms agree to rounding relative to the initial norm (after 50 iterations the
+    # small p = 3 case has converged to ~1e-12, where only rounding is left)
+    assert abs(out[1][1]["final_norm"] - out[0][1]["final_norm"]) <= 1e-12 * out[0][1]["initial_norm"]
+
+
+@pytest.mark.parametrize("shape,p", [((4, 3, 5), 4), ((5, 4, 3), 3)])
+def test_ho_fused_cg_box_shapes(gpu_ctx, shape, p):
+    """Fused vs unfused high-order CG on non-cubic boxes (the essential-DoF ownership rule on each
+    axis), converging to tolerance with the same iteration count and solution."""
+    m = cdfem.box_mesh(3, shape, p, perturb=0.1, with_coords=False)
+    rng = np.random.default_rng(13)
+    u = np.zeros(m.nl)
+    u[m.ess] = rng.uniform(-1, 1, len(m.ess))
+    b = rng.uniform(-1, 1, m.nl)
+    out = {}
+    try:
+        for fused in (1, 0):
+            gpu_ctx.set_option("cg_fused", fused)
+            gpu_ctx.upload_mesh(m).set_structured(*shape)
+            gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=(0.0, 0.0, 0.0), mass=1.0)
+            _, B = gpu_ctx.form_linear_system(u, b)
+            out[fused] = gpu_ctx.solve(B, method="cg", rel_tol=1e-12, abs_tol=0.0, max_iter=2000)
+    finally:
+        gpu_ctx.set_option("cg_fused", 1)
+    (x1, i1), (x0, i0) = out[1], out[0]
+    assert i1["converged"] and i0["converged"] and abs(i1["iterations"] - i0["iterations"]) <= 1
+    assert np.linalg.norm(x1 - x0) <= 1e-10 * np.linalg.norm(x0)
+
+
 def test_ho_mms_error_matches_oracle(gpu_ctx):
     n, p = 3, 4
     om = O.BoxMesh(3, n, p)
