@@ -487,16 +487,8 @@ hipError_t launch_e2l_cg_update(cdfem_ctx *c, const double *Ye, const double *d,
 template <int P>
 static hipError_t launch_e2l_box(cdfem_ctx *c, const double *Ye, const double *x, double *y, bool con, int cg_mode)
 {
-    const int64_t rows = c->Ly * c->Lz;
-    const dim3 g((unsigned)std::min<int64_t>((rows + 3) / 4, 65536)), b(kRedThreads);
-    BoxE2L bx;
-    bx.Lx = (uint32_t)c->Lx;
-    bx.Ly = (uint32_t)c->Ly;
-    bx.nx = (uint32_t)c->sx;
-    bx.ny = (uint32_t)c->sy;
-    bx.nz = (uint32_t)c->sz;
-    bx.fLx = make_fastdiv(bx.Lx);
-    bx.fLxy = make_fastdiv(bx.Lx * bx.Ly);
+    const dim3 g = box_grid(c), b(kRedThreads);
+    const BoxE2L bx = box_e2l(c);
     if (cg_mode) {
         hipLaunchKernelGGL((k_e2l_box<true, true, P>), g, b, 0, c->stream, bx, c->d_ess, Ye, x, y, c->nl, c->d_part,
                            c->d_state);
@@ -516,10 +508,8 @@ static hipError_t launch_e2l_box(cdfem_ctx *c, const double *Ye, const double *x
 hipError_t launch_e2l(cdfem_ctx *c, const double *Ye, const double *x, double *y, bool con,
                       int cg_mode)
 {
-    if (c->structured && c->qlay == 1 && c->nl < ((int64_t)1 << 32)) {
-        if (c->p == 3) return launch_e2l_box<3>(c, Ye, x, y, con, cg_mode);
-        if (c->p == 4) return launch_e2l_box<4>(c, Ye, x, y, con, cg_mode);
-    }
+    if (e2l_box_ok(c)) return c->p == 3 ? launch_e2l_box<3>(c, Ye, x, y, con, cg_mode)
+                                        : launch_e2l_box<4>(c, Ye, x, y, con, cg_mode);
     const dim3 g(red_grid(c, c->nl)), b(kRedThreads);
     if (cg_mode) {
         hipLaunchKernelGGL((k_e2l<true, true>), g, b, 0, c->stream, c->d_e2l_off, c->d_e2l_pos,
