@@ -29,6 +29,7 @@ struct BrickGeom {
     int nbx, nby, nbz;  // bricks per axis
     int Lx, Ly, Lz;     // dof lattice per axis
     int xcd;            // 1: XCD-contiguous brick order (default; set_option "brick_xcd")
+    int bz0, bzs;       // k_brick_cg: the launch covers brick layers bz0, bz0 + bzs, ... (all: 0, 1)
 };
 
 // workgroup b runs on XCD b % 8; with xcd = 1 each XCD takes a contiguous range of bricks, so a
@@ -251,7 +252,7 @@ bool brick_supported(int dim, int p) { return dim == 3 && (p == 1 || p == 2); }
 
 static BrickGeom geom_of(const cdfem_ctx *c)
 {
-    return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd};
+    return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1};
 }
 
 static dim3 faces_grid(const cdfem_ctx *c)
@@ -364,8 +365,11 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     if (st->done) return;
     const double beta = st->beta;
     const int t = threadIdx.x;
-    const int b = brick_id(g);
-    const int bx = b % g.nbx, by = (b / g.nbx) % g.nby, bz = b / (g.nbx * g.nby);
+    // launch-local brick -> global brick (a launch covers every g.bzs-th layer from g.bz0)
+    const int bl = brick_id(g), nxy = g.nbx * g.nby;
+    const int bz = g.bz0 + (bl / nxy) * g.bzs;
+    const int b = bl % nxy + nxy * bz;
+    const int bx = b % g.nbx, by = (b / g.nbx) % g.nby;
     const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
     const bool lastx = bx == g.nbx - 1, lasty = by == g.nby - 1, lastz = bz == g.nbz - 1;
 
@@ -524,15 +528,33 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
     if (threadIdx.x == 0) part[blockIdx.x] = bs;
 }
 
+// one launch of k_brick_cg over brick layers bz0, bz0 + bzs, ... (nlay of them) on stream s;
+// the whole slab (0, 1, nbz) on the context stream goes through CDFEM_LAUNCH (profiling events)
+struct BrickRun {
+    int bz0, bzs, nlay;
+    hipStream_t s;
+};
+
 template <int D1, int Q1, unsigned K>
 static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *dinv,
-                                   const double *d_old, double *d_new, double *q)
+                                   const double *d_old, double *d_new, double *q, const BrickRun &run)
 {
     const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
-    const BrickGeom g = geom_of(c);
+    BrickGeom g = geom_of(c);
+    g.bz0 = run.bz0;
+    g.bzs = run.bzs;
+    const dim3 grid((unsigned)(c->nbx * c->nby * run.nlay)), block(64);
+    const bool whole = run.nlay == c->nbz && run.s == c->stream;
 #define CDFEM_L(V)                                                                                  \
-    CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, V>), dim3(c->nblk), dim3(64), 0, r, dinv, d_old, d_new, q,        \
-                 c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state)
+    do {                                                                                            \
+        if (whole)                                                                                  \
+            CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, V>), grid, block, 0, r, dinv, d_old, d_new, q,   \
+                         c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);  \
+        else                                                                                        \
+            hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, V>), grid, block, 0, run.s, r, dinv, d_old,    \
+                               d_new, q, c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared,          \
+                               c->d_part, c->d_state);                                              \
+    } while (0)
     switch (c->brick_variant) {
     case 1: CDFEM_L(1); break;
     case 2: CDFEM_L(2); break;
@@ -546,25 +568,42 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     return hipGetLastError();
 }
 
-hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                            double *d_new, double *q)
+static hipError_t brick_cg2_run(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
+                                double *d_new, double *q, const BrickRun &run)
 {
     const int q1 = c->rule_op.q1;
 #define CDFEM_K(D1_, Q1_)                                                                           \
     switch (c->kinds) {                                                                             \
-    case 1: return brick_cg2_launch<D1_, Q1_, 1>(c, r, dinv, d_old, d_new, q);                      \
-    case 2: return brick_cg2_launch<D1_, Q1_, 2>(c, r, dinv, d_old, d_new, q);                      \
-    case 3: return brick_cg2_launch<D1_, Q1_, 3>(c, r, dinv, d_old, d_new, q);                      \
-    case 4: return brick_cg2_launch<D1_, Q1_, 4>(c, r, dinv, d_old, d_new, q);                      \
-    case 5: return brick_cg2_launch<D1_, Q1_, 5>(c, r, dinv, d_old, d_new, q);                      \
-    case 6: return brick_cg2_launch<D1_, Q1_, 6>(c, r, dinv, d_old, d_new, q);                      \
-    case 7: return brick_cg2_launch<D1_, Q1_, 7>(c, r, dinv, d_old, d_new, q);                      \
+    case 1: return brick_cg2_launch<D1_, Q1_, 1>(c, r, dinv, d_old, d_new, q, run);                 \
+    case 2: return brick_cg2_launch<D1_, Q1_, 2>(c, r, dinv, d_old, d_new, q, run);                 \
+    case 3: return brick_cg2_launch<D1_, Q1_, 3>(c, r, dinv, d_old, d_new, q, run);                 \
+    case 4: return brick_cg2_launch<D1_, Q1_, 4>(c, r, dinv, d_old, d_new, q, run);                 \
+    case 5: return brick_cg2_launch<D1_, Q1_, 5>(c, r, dinv, d_old, d_new, q, run);                 \
+    case 6: return brick_cg2_launch<D1_, Q1_, 6>(c, r, dinv, d_old, d_new, q, run);                 \
+    case 7: return brick_cg2_launch<D1_, Q1_, 7>(c, r, dinv, d_old, d_new, q, run);                 \
     default: return hipErrorInvalidValue;                                                           \
     }
     if (c->p == 1 && q1 == 3) { CDFEM_K(2, 3) }
     if (c->p == 2 && q1 == 4) { CDFEM_K(3, 4) }
 #undef CDFEM_K
     return hipErrorInvalidValue;
+}
+
+hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
+                            double *d_new, double *q)
+{
+    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, 1, c->nbz, c->stream});
+}
+
+// the first and last brick layers (the shared planes' partial sums) on stream s, the interior
+// layers on the context stream; nbz >= 3
+hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
+                                  double *d_new, double *q, hipStream_t s)
+{
+    if (c->nbz < 3) return hipErrorInvalidValue;
+    const hipError_t e = brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, c->nbz - 1, 2, s});
+    if (e != hipSuccess) return e;
+    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{1, 1, c->nbz - 2, c->stream});
 }
 
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
@@ -639,16 +678,17 @@ k_pack_qplanes(const double *__restrict__ q, const double *__restrict__ face, co
     }
 }
 
-hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q)
+hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q, hipStream_t s)
 {
     const BrickGeom g = geom_of(c);
     const int n = (int)(c->Lx * c->Ly);
     const dim3 grid((n + 255) / 256), block(256);
+    if (!s) s = c->stream;
     if (c->p == 1)
-        hipLaunchKernelGGL(k_pack_qplanes<kBrick * 1 + 1>, grid, block, 0, c->stream, q, c->d_face, g,
+        hipLaunchKernelGGL(k_pack_qplanes<kBrick * 1 + 1>, grid, block, 0, s, q, c->d_face, g,
                            c->zlo_shared, c->zhi_shared, c->d_if[0], c->d_if[2], c->d_state);
     else if (c->p == 2)
-        hipLaunchKernelGGL(k_pack_qplanes<kBrick * 2 + 1>, grid, block, 0, c->stream, q, c->d_face, g,
+        hipLaunchKernelGGL(k_pack_qplanes<kBrick * 2 + 1>, grid, block, 0, s, q, c->d_face, g,
                            c->zlo_shared, c->zhi_shared, c->d_if[0], c->d_if[2], c->d_state);
     else
         return hipErrorInvalidValue;

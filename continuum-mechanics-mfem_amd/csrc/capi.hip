@@ -322,7 +322,31 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     } else {
         HIPCHK(launch_cg_init(c, dB, x, r, q, dprev, dinv, p.rel_tol, p.abs_tol, p.max_iter));
     }
+    // slab partition: the shared planes' partial sums come from the first and last brick layers
+    // only, so those layers run first on a side stream, whose pack + exchange then overlap the
+    // interior layers on the main stream.  Same kernels, same sums: bitwise equal
+    // to the one-launch form.  Profiling keeps the one-launch form (one timed apply kernel).
+    const bool overlap = mr && c->mr_overlap && !c->profile && c->nbz >= 3;
+    if (overlap && !c->stream2) {
+        HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+        for (auto &e : c->ov_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     auto apply = [&] {
+        if (overlap) {
+            HIPCHK(hipEventRecord(c->ov_ev[0], c->stream));
+            HIPCHK(hipStreamWaitEvent(c->stream2, c->ov_ev[0], 0));
+            // boundary layers on the side stream, interior layers queued on the main stream
+            // before the (possibly host-blocking) exchange is issued
+            HIPCHK(launch_brick_cg2_split(c, r, dinv, dprev, dcur, q, c->stream2));
+            HIPCHK(launch_pack_qplanes(c, q, c->stream2));
+            comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], c->Lx * c->Ly, c->stream2);
+            HIPCHK(hipEventRecord(c->ov_ev[1], c->stream2));
+            HIPCHK(hipStreamWaitEvent(c->stream, c->ov_ev[1], 0));
+            HIPCHK(launch_fin_sum(c, c->nblk, 0));
+            comm_allreduce(c, red + 0, 1);
+            HIPCHK(launch_den_step(c));
+            return;
+        }
         prof_mark(c, CDFEM_K_APPLY, true);
         HIPCHK(launch_brick_cg2(c, r, dinv, dprev, dcur, q));
         prof_mark(c, CDFEM_K_APPLY, false);
@@ -601,6 +625,9 @@ void cdfem_destroy(cdfem_ctx *c)
         if (e) (void)hipEventDestroy(e);
     for (auto &s : c->prof)
         for (auto e : s.ev) (void)hipEventDestroy(e);
+    for (auto e : c->ov_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1227,6 +1254,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "brick_xcd") {
             if (value < 0 || value > 1) throw ArgError("brick_xcd must be 0 or 1");
             c->brick_xcd = value;
+        } else if (k == "mr_overlap") {
+            if (value < 0 || value > 1) throw ArgError("mr_overlap must be 0 or 1");
+            c->mr_overlap = value;
         } else if (k == "cg_fused") {
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;

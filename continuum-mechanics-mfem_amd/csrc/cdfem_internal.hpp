@@ -173,6 +173,9 @@ struct cdfem_ctx {
     int32_t *d_sptr = nullptr, *d_srows = nullptr, *d_scols = nullptr, *d_smap = nullptr;
     double *d_tpart = nullptr;          // den partials of the fused high-order CG apply (one per tile block)
     int16_t *d_sdel = nullptr;          // 16-bit column deltas (null when the bandwidth does not fit)
+    int mr_overlap = 1;                 // set_option "mr_overlap": slab CG exchange overlapped with interior bricks
+    hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
+    hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     double *d_svals = nullptr, *d_svals_c = nullptr;
@@ -282,7 +285,7 @@ hipError_t launch_den_local(cdfem_ctx *c, const double *d, const double *q);
 void comm_destroy(cdfem_ctx *c);
 void comm_allreduce(cdfem_ctx *c, double *dbuf, int n);
 void comm_exchange(cdfem_ctx *c, const double *send_lo, double *recv_lo, const double *send_hi,
-                   double *recv_hi, int64_t n);
+                   double *recv_hi, int64_t n, hipStream_t s = nullptr);
 void interface_sum(cdfem_ctx *c, double *v);  // L-vector interface planes summed over ranks
 inline bool multi_rank(const cdfem_ctx *c) { return c->nranks > 1; }
 // split CG finalizers for the multi-rank path: local sum -> all-reduce -> step
@@ -293,7 +296,9 @@ hipError_t launch_init_step(cdfem_ctx *c, double rel_tol, double abs_tol, int ma
 hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double *r, double *z, double *d,
                                 const double *dinv);
 // pack the local partial sums of q on the shared interface planes into d_if[0] / d_if[2]
-hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q);
+hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q, hipStream_t s = nullptr);
+hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
+                                  double *d_new, double *q, hipStream_t s);
 
 // ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
 // full assembly on simplices (fa_kernels.hip)

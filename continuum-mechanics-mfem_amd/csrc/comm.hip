@@ -81,38 +81,39 @@ void comm_allreduce(cdfem_ctx *c, double *dbuf, int n)
 // exchange interface planes with the neighbours: send_lo -> rank-1 (recv into its recv_hi) and
 // send_hi -> rank+1; n doubles per plane
 void comm_exchange(cdfem_ctx *c, const double *send_lo, double *recv_lo, const double *send_hi,
-                   double *recv_hi, int64_t n)
+                   double *recv_hi, int64_t n, hipStream_t s)
 {
+    if (!s) s = c->stream;
     Comm *m = c->comm;
     if (!m || m->nranks == 1) return;
     const bool lo = m->rank > 0, hi = m->rank < m->nranks - 1;
     if (m->nccl) {
         nccl_check(ncclGroupStart(), "ncclGroupStart");
         if (lo) {
-            nccl_check(ncclSend(send_lo, n, ncclDouble, m->rank - 1, m->nccl, c->stream), "ncclSend");
-            nccl_check(ncclRecv(recv_lo, n, ncclDouble, m->rank - 1, m->nccl, c->stream), "ncclRecv");
+            nccl_check(ncclSend(send_lo, n, ncclDouble, m->rank - 1, m->nccl, s), "ncclSend");
+            nccl_check(ncclRecv(recv_lo, n, ncclDouble, m->rank - 1, m->nccl, s), "ncclRecv");
         }
         if (hi) {
-            nccl_check(ncclSend(send_hi, n, ncclDouble, m->rank + 1, m->nccl, c->stream), "ncclSend");
-            nccl_check(ncclRecv(recv_hi, n, ncclDouble, m->rank + 1, m->nccl, c->stream), "ncclRecv");
+            nccl_check(ncclSend(send_hi, n, ncclDouble, m->rank + 1, m->nccl, s), "ncclSend");
+            nccl_check(ncclRecv(recv_hi, n, ncclDouble, m->rank + 1, m->nccl, s), "ncclRecv");
         }
         nccl_check(ncclGroupEnd(), "ncclGroupEnd");
         return;
     }
     double *h = host_staging(m, 4 * (size_t)n);
     double *hs_lo = h, *hr_lo = h + n, *hs_hi = h + 2 * n, *hr_hi = h + 3 * n;
-    if ((lo && hipMemcpyAsync(hs_lo, send_lo, n * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) ||
-        (hi && hipMemcpyAsync(hs_hi, send_hi, n * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
+    if ((lo && hipMemcpyAsync(hs_lo, send_lo, n * 8, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (hi && hipMemcpyAsync(hs_hi, send_hi, n * 8, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        hipStreamSynchronize(s) != hipSuccess)
         throw std::runtime_error("exchange staging failed");
     if (m->h_exchange(lo ? hs_lo : nullptr, lo ? hr_lo : nullptr, hi ? hs_hi : nullptr,
                       hi ? hr_hi : nullptr, n, m->user) != 0)
         throw std::runtime_error("host exchange callback failed");
-    if ((lo && hipMemcpyAsync(recv_lo, hr_lo, n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
-        (hi && hipMemcpyAsync(recv_hi, hr_hi, n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess))
+    if ((lo && hipMemcpyAsync(recv_lo, hr_lo, n * 8, hipMemcpyHostToDevice, s) != hipSuccess) ||
+        (hi && hipMemcpyAsync(recv_hi, hr_hi, n * 8, hipMemcpyHostToDevice, s) != hipSuccess))
         throw std::runtime_error("exchange staging failed");
     // the staging buffer is reused by the next call: complete the uploads first
-    if (hipStreamSynchronize(c->stream) != hipSuccess) throw std::runtime_error("exchange staging failed");
+    if (hipStreamSynchronize(s) != hipSuccess) throw std::runtime_error("exchange staging failed");
 }
 
 // ---- plane kernels ----------------------------------------------------------------------------

@@ -199,6 +199,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *                  low-register; 3-5 the same at 2 waves per SIMD; 6 temporal qdata loads).
  * "brick_xcd": 1 (default) — XCD-contiguous brick order of the structured CG kernel; 0 = the
  *              dispatcher's round-robin order.
+ * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
+ *               interface pack and the exchange run on a side stream under the interior layers;
+ *               0 = one launch, then the exchange (bitwise the same results).
  * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).

@@ -197,6 +197,46 @@ def test_gpu_two_ranks_one_device(tmp_path):
     assert np.linalg.norm(xg - xs) <= 1e-10 * np.linalg.norm(xs)
 
 
+def _gpu_overlap_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    import cdfem
+    dist = _init(rank, world, port)
+    n, per = 8, 12                       # 3 brick layers per rank: boundary + interior launches
+    m = cdfem.box_mesh(3, (n, n, per * world), P, z_range=(rank * per, (rank + 1) * per))
+    ctx = cdfem.Context(0)
+    ctx.upload_mesh(m).set_structured(n, n, per)
+    ctx.comm_init_torch()
+    ctx.set_slab(rank > 0, rank < world - 1)
+    ctx.pa_setup(kinds=cdfem.DIFFUSION | cdfem.MASS, kappa=KAPPA, mass=S)
+    b = np.random.default_rng(200 + rank).uniform(-1, 1, m.nl)
+    _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+    res = []
+    for ov in (1, 0, 1):
+        ctx.set_option("mr_overlap", ov)
+        X, info = ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=60, check_every=7)
+        res.append(X)
+    np.save(os.path.join(out_dir, f"ov{rank}.npy"), np.stack(res))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_overlapped_exchange_bitwise(tmp_path, world):
+    """Slab CG with the interface exchange overlapped with the interior brick layers (side
+    stream: first/last layers, pack, exchange; main stream: interior layers) gives the same bits
+    as the one-launch form, on end ranks and (world 3) on a middle rank with two neighbours."""
+    mp.start_processes(_gpu_overlap_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    for r in range(world):
+        x = np.load(tmp_path / f"ov{r}.npy")
+        assert np.isfinite(x).all() and np.abs(x[0]).max() > 0
+        np.testing.assert_array_equal(x[0], x[1])
+        np.testing.assert_array_equal(x[0], x[2])
+
+
 # ---------------------------------------------------------------------------------------------
 # GMRES(m) + left Jacobi (PETSc KSPGMRES semantics, Input/petsc.opts:2-6) on the slab partition,
 # full convection-diffusion-reaction operator (nonsymmetric).  The distributed restatement below
