@@ -199,6 +199,33 @@ k_gm_dots_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ 
     }
 }
 
+// ---- H[i][j] = s_i * sum_b part[i][b] (modes 0 / 1 of k_gm_dots_fin), one block per i ------------
+// Every projection's partials are summed by a block of its own (fixed order), so the step's
+// projections reduce in parallel instead of 16 at a time in one block.
+__global__ void __launch_bounds__(kRedThreads)
+k_gm_dots_fin_mb(const double *__restrict__ part, int nb, GmresState *__restrict__ st, int mode)
+{
+    __shared__ double sh[kRedThreads / 64];
+    if (st->cycle_done) return;
+    const int j = st->j, i = blockIdx.x;  // grid = m + 1
+    if (i > j) {
+        if (mode == 1 && threadIdx.x == 0) st->red[i] = 0.0;  // multi-rank: zero past j
+        return;
+    }
+    const double *pi = part + (int64_t)i * nb;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    int b = threadIdx.x;
+    for (; b + 3 * kRedThreads < nb; b += 4 * kRedThreads) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] += pi[b + u * kRedThreads];
+    }
+    for (int u = 0; b < nb; b += kRedThreads, ++u) a[u] += pi[b];
+    const double v = block_sum((a[0] + a[1]) + (a[2] + a[3]), sh);
+    if (threadIdx.x != 0) return;
+    if (mode == 1) st->red[i] = v;
+    else st->H[i * kGmMaxRestart + j] = st->s[i] * v;
+}
+
 // ---- pass 2: V_{j+1} = w - sum_i H[i][j] s_i V_i, partials of |V_{j+1}|^2 ------------------------
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int64_t ldv, int64_t skip_lo,
@@ -385,7 +412,7 @@ hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V
     const bool mr = multi_rank(c);
     hipLaunchKernelGGL((k_gm_pass1<kGmBatch>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv,
                        owned_from(c), part, nb, st);
-    hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, mr ? 1 : 0);
+    hipLaunchKernelGGL(k_gm_dots_fin_mb, dim3(m + 1), dim3(kRedThreads), 0, c->stream, part, nb, st, mr ? 1 : 0);
     if (mr) {
         comm_allreduce(c, red_of(st), m + 1);
         hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2);
