@@ -42,3 +42,28 @@ def test_mms_l2_rate(gpu_ctx, p, ns, min_rate):
     print(f"p={p} n={ns} L2={errs} rates={rates}")
     assert all(e > 0 for e in errs)
     assert rates[-1] >= min_rate, (errs, rates)
+
+
+def test_mms_l2_rate_tets_p2_gmres():
+    """C4 path (Kuhn tets, P2, GPU full assembly + FormLinearSystem + GMRES(30)/Jacobi on the full
+    convection-diffusion-reaction operator): L2 rate 3 under refinement."""
+    import cdfem as cd
+    C3 = (1.0, -2.0, 0.5)
+    errs = []
+    with cd.Context(0) as ctx:
+        for n in (4, 8):
+            gm = cd.kuhn_mesh(3, n, 2)
+            om = O.KuhnMesh(3, n, 2)
+            prm = O.mms_params(O.MMS_SIN, 3, kappa=0.1, s=1.0, c=C3, modes=(1, 1, 1), p=2)
+            b = O.lf_assemble_simplex(om, prm)
+            u = np.zeros(om.nl)
+            u[om.ess] = O.mms_u(prm, gm.dof_xyz[om.ess])
+            ctx.upload_mesh(gm)
+            ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            _, B = ctx.form_linear_system(u, b)
+            X, info = ctx.solve(B, method="gmres", restart=30, rel_tol=1e-12, abs_tol=0.0, max_iter=3000)
+            assert info["converged"]
+            errs.append(O.l2_error_simplex(om, X, prm))
+    rate = math.log2(errs[0] / errs[1])
+    print(f"tets P2 n=(4, 8) L2={errs} rate={rate}")
+    assert rate >= 2.7, errs
