@@ -126,9 +126,9 @@ def _cpu_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_slab_cg_matches_single_domain(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_slab_cg_matches_single_domain(tmp_path, world):
     from oracle import oracle as O
-    world = 2
     mp.start_processes(_cpu_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
                        start_method="spawn", join=True)
     full = O.BoxMesh(3, (N, N, NZ), P)
@@ -137,15 +137,19 @@ def test_slab_cg_matches_single_domain(tmp_path):
     Ac, Bo = O.form_linear_system(A, full.bdr, np.zeros(full.nl), O.lf_assemble(full, prm))
     xo, io = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=1e-12, max_iter=500)
     plane = (P * N + 1) ** 2
-    x0, x1 = np.load(tmp_path / "x0.npy"), np.load(tmp_path / "x1.npy")
+    xs = [np.load(tmp_path / f"x{r}.npy") for r in range(world)]
     per_rank = plane * (P * NZ // world)
-    xg = np.concatenate([x0, x1[plane:]])         # rank 1's first plane duplicates rank 0's last
+    # rank r's first plane duplicates rank r-1's last: the copies agree, the gathered vector is
+    # the single-domain solution
+    for r in range(1, world):
+        np.testing.assert_allclose(xs[r][:plane], xs[r - 1][-plane:], rtol=0, atol=1e-14)
+    xg = np.concatenate([xs[0]] + [x[plane:] for x in xs[1:]])
     assert len(xg) == full.nl
-    np.testing.assert_allclose(x1[:plane], x0[-plane:], rtol=0, atol=1e-14)   # consistent copies
     assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
-    its = int(np.load(tmp_path / "its0.npy")[0])
-    assert abs(its - io["iterations"]) <= 1
-    assert per_rank + plane == len(x0)
+    for r in range(world):
+        its = int(np.load(tmp_path / f"its{r}.npy")[0])
+        assert abs(its - io["iterations"]) <= 1
+        assert per_rank + plane == len(xs[r])
 
 
 # ---------------------------------------------------------------------------------------------
