@@ -470,13 +470,26 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
                   const double *__restrict__ face, const uint8_t *__restrict__ ess, const BrickGeom g,
                   const FastDiv fdx, const FastDiv fdxy, int zlo_shared,
                   const double *__restrict__ remote_lo, const double *__restrict__ remote_hi,
-                  double *__restrict__ part, const KrylovState *__restrict__ st)
+                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step)
 {
     constexpr int F = face_count<S>();
     constexpr int s1 = S - 1;
     __shared__ double sh[kRedThreads / 64];
     if (st->done) return;
-    const double alpha = st->alpha;
+    double alpha;
+    if (den_step) {
+        // multi-rank: the MFEM den step on the all-reduced den, folded in (no one-thread kernel
+        // between the all-reduce and the update).  Every block forms alpha = betanom / den as
+        // cg_den_step does; block 0 alone writes the state (den, nom, alpha; done if den == 0).
+        // No block reads a field block 0 writes, except done at entry, which only turns on
+        // when every block returns here anyway.
+        const double den = st->red[0];
+        if (blockIdx.x == 0 && threadIdx.x == 0) cg_den_step(st, den);
+        if (den == 0.0) return;
+        alpha = st->betanom / den;
+    } else {
+        alpha = st->alpha;
+    }
     const int n = g.Lx * g.Ly * g.Lz;
     const int plane = g.Lx * g.Ly;
     double acc = 0.0;
@@ -607,7 +620,8 @@ hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *d
 }
 
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
-                                  const double *dinv, const double *remote_lo, const double *remote_hi)
+                                  const double *dinv, const double *remote_lo, const double *remote_hi,
+                                  bool den_step)
 {
     const BrickGeom g = geom_of(c);
     const FastDiv fdx = make_fastdiv((uint32_t)c->Lx), fdxy = make_fastdiv((uint32_t)(c->Lx * c->Ly));
@@ -618,11 +632,11 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     if (c->p == 1)
         hipLaunchKernelGGL(k_cg_update_faces<kBrick * 1 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
                            x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
-                           remote_hi, c->d_part, c->d_state);
+                           remote_hi, c->d_part, c->d_state, (int)den_step);
     else if (c->p == 2)
         hipLaunchKernelGGL(k_cg_update_faces<kBrick * 2 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
                            x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
-                           remote_hi, c->d_part, c->d_state);
+                           remote_hi, c->d_part, c->d_state, (int)den_step);
     else
         return hipErrorInvalidValue;
     const hipError_t e = hipGetLastError();

@@ -343,8 +343,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             HIPCHK(hipEventRecord(c->ov_ev[1], c->stream2));
             HIPCHK(hipStreamWaitEvent(c->stream, c->ov_ev[1], 0));
             HIPCHK(launch_fin_sum(c, c->nblk, 0));
-            comm_allreduce(c, red + 0, 1);
-            HIPCHK(launch_den_step(c));
+            comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
             return;
         }
         prof_mark(c, CDFEM_K_APPLY, true);
@@ -356,8 +355,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             HIPCHK(launch_pack_qplanes(c, q));
             comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], c->Lx * c->Ly);
             HIPCHK(launch_fin_sum(c, c->nblk, 0));
-            comm_allreduce(c, red + 0, 1);
-            HIPCHK(launch_den_step(c));
+            comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
         } else {
             HIPCHK(launch_den_fin(c, c->nblk));
         }
@@ -370,7 +368,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             prof_mark(c, CDFEM_K_UPDATE, true);
             HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv,
                                           mr && c->zlo_shared ? c->d_if[1] : nullptr,
-                                          mr && c->zhi_shared ? c->d_if[3] : nullptr));
+                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr));
             if (mr) {
                 comm_allreduce(c, red + 1, 1);
                 HIPCHK(launch_update_step(c));

@@ -275,7 +275,8 @@ hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, c
                             double *d_new, double *q);
 // q from interior/face partials (+ remote interface sums), x += alpha d, r -= alpha q, betanom
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
-                                  const double *dinv, const double *remote_lo, const double *remote_hi);
+                                  const double *dinv, const double *remote_lo, const double *remote_hi,
+                                  bool den_step = false);
 // generic deterministic dot into host-visible scalar via state (used by GMRES / tests)
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out);
 // multi-rank CG: rank-local (d, q) over owned entries into the state's den slot (all-reduce next)
