@@ -83,6 +83,7 @@ struct GmresState {
     double g[kGmMaxRestart + 1], cs[kGmMaxRestart], sn[kGmMaxRestart];
     double H[(kGmMaxRestart + 1) * kGmMaxRestart];  // row-major, leading dimension kGmMaxRestart
     double red[kGmMaxRestart + 1];  // multi-rank: rank-local sums awaiting the all-reduce
+    double y[kGmMaxRestart];        // cycle end: the least-squares solution, scaled by s
 };
 constexpr size_t kGmPollBytes = 32;
 

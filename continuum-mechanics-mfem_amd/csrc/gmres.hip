@@ -319,6 +319,37 @@ k_gm_norm_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ 
 }
 
 // ---- end of cycle: y = H_k^{-1} g_k (every block, redundantly: k <= 64), x += sum_i y_i s_i V_i --
+// cycle end, once: y = H^{-1} g by back substitution (the serial order PETSc's KSPGMRESBuildSoln
+// uses), the Hessenberg triangle staged in LDS first, then scaled by the basis scales
+__global__ void __launch_bounds__(kRedThreads)
+k_gm_solve_y(GmresState *__restrict__ st)
+{
+    constexpr int LD = kGmMaxRestart;
+    __shared__ double h[kGmMaxRestart * kGmMaxRestart];
+    __shared__ double g[kGmMaxRestart];
+    if (st->done) return;
+    const int kk = st->kk;
+    for (int t = threadIdx.x; t < kk * kk; t += blockDim.x) {
+        const int i = t / kk, l = t - i * kk;
+        if (l >= i) h[i * LD + l] = st->H[i * LD + l];
+    }
+    if ((int)threadIdx.x < kk) g[threadIdx.x] = st->g[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    // y lives in LDS (a register array with run-time indices would go to scratch); the loads of a
+    // row are independent of the chain, so unrolling keeps them in flight ahead of the FMAs
+    double *y = g;  // g[i] is read once, before y[i] overwrites it
+    for (int i = kk - 1; i >= 0; --i) {
+        double acc = g[i];
+#pragma unroll 8
+        for (int l = i + 1; l < kk; ++l) acc -= h[i * LD + l] * y[l];
+        y[i] = acc / h[i * LD + i];
+    }
+    for (int i = 0; i < kk; ++i) st->y[i] = y[i] * st->s[i];
+}
+
+// x += sum_i y_i V_i (y from k_gm_solve_y), 4 basis vectors' loads in flight per batch; each
+// entry is summed in ascending i, as before the batching
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_update(double *__restrict__ x, const double *__restrict__ V, int64_t n, int64_t ldv,
             const GmresState *__restrict__ st)
@@ -326,24 +357,40 @@ k_gm_update(double *__restrict__ x, const double *__restrict__ V, int64_t n, int
     __shared__ double y[kGmMaxRestart];
     if (st->done) return;
     const int kk = st->kk;
-    if (threadIdx.x == 0) {
-        constexpr int LD = kGmMaxRestart;
-        for (int i = kk - 1; i >= 0; --i) {
-            double acc = st->g[i];
-            for (int l = i + 1; l < kk; ++l) acc -= st->H[i * LD + l] * y[l];
-            y[i] = acc / st->H[i * LD + i];
-        }
-        for (int i = 0; i < kk; ++i) y[i] *= st->s[i];
-    }
+    if ((int)threadIdx.x < kk) y[threadIdx.x] = st->y[threadIdx.x];
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * kGmChunk + threadIdx.x;
+    double v[kGmEPT];
 #pragma unroll
     for (int e = 0; e < kGmEPT; ++e) {
         const int64_t k = base + (int64_t)e * kRedThreads;
-        if (k >= n) continue;
-        double v = x[k];
-        for (int i = 0; i < kk; ++i) v += y[i] * V[(int64_t)i * ldv + k];
-        x[k] = v;
+        v[e] = k < n ? x[k] : 0.0;
+    }
+    int i = 0;
+    for (; i + 4 <= kk; i += 4) {
+        double vv[4][kGmEPT];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < kGmEPT; ++e) {
+                const int64_t k = base + (int64_t)e * kRedThreads;
+                vv[u][e] = k < n ? V[(int64_t)(i + u) * ldv + k] : 0.0;
+            }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < kGmEPT; ++e) v[e] += y[i + u] * vv[u][e];
+    }
+    for (; i < kk; ++i)
+#pragma unroll
+        for (int e = 0; e < kGmEPT; ++e) {
+            const int64_t k = base + (int64_t)e * kRedThreads;
+            if (k < n) v[e] += y[i] * V[(int64_t)i * ldv + k];
+        }
+#pragma unroll
+    for (int e = 0; e < kGmEPT; ++e) {
+        const int64_t k = base + (int64_t)e * kRedThreads;
+        if (k < n) x[k] = v[e];
     }
 }
 
@@ -430,6 +477,7 @@ hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V
 hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st, GmresState *poll)
 {
     const int nb = gmres_blocks(c->nl);
+    hipLaunchKernelGGL(k_gm_solve_y, dim3(1), dim3(kRedThreads), 0, c->stream, st);
     hipLaunchKernelGGL(k_gm_update, dim3(nb), dim3(kRedThreads), 0, c->stream, x, V, (int64_t)c->nl, ldv, st);
     hipLaunchKernelGGL(k_gm_cycle_end, dim3(1), dim3(1), 0, c->stream, st, poll);
     return hipGetLastError();
