@@ -279,7 +279,7 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
                 const int j = (dz * D1 + ty) * Q1 + qx;
                 y += cb[qx] * Bf[j] + cg[qx] * Bf[D1 * D1 * Q1 + j];
             }
-            ye[dz * zs] = y;
+            __builtin_nontemporal_store(y, &ye[dz * zs]);
             if constexpr (DEN) {
                 constexpr int P = D1 - 1;
                 const bool own = (tx < P || ex == geo.ho.nx - 1) && (ty < P || ey == geo.ho.ny - 1) &&

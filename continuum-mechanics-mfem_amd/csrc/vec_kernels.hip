@@ -151,12 +151,12 @@ k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__rest
                 }
             }
             if (is_ess) v = xi;
-            if constexpr (UPD) {
-                xs[i] = si + alpha * xi;
+            if constexpr (UPD) {  // outputs streamed out: next read after a full apply
+                __builtin_nontemporal_store(si + alpha * xi, &xs[i]);
                 ri -= alpha * v;
-                res[i] = ri;
+                __builtin_nontemporal_store(ri, &res[i]);
                 const double zi = mi * ri;
-                y[i] = zi;
+                __builtin_nontemporal_store(zi, &y[i]);
                 acc += ri * zi;
             } else {
                 y[i] = v;
@@ -337,8 +337,15 @@ k_cg_direction(const double *__restrict__ z, double *__restrict__ d, int64_t n,
     if (st->done) return;
     const double beta = st->beta;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        d[i] = z[i] + beta * d[i];
+    // 16-byte pairs; d is streamed out (the next apply gathers it from HBM in any case)
+    const int64_t n2 = n >> 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+        typedef double d2_t __attribute__((ext_vector_type(2)));
+        const d2_t zv = reinterpret_cast<const d2_t *>(z)[i];
+        const d2_t dv = reinterpret_cast<const d2_t *>(d)[i];
+        __builtin_nontemporal_store(zv + beta * dv, reinterpret_cast<d2_t *>(d) + i);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) d[n - 1] = z[n - 1] + beta * d[n - 1];
 }
 
 // ------------------------------------------------------------------------------------------------
