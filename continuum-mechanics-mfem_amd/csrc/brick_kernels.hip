@@ -532,9 +532,9 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         if (remote_lo && gz == 0) qi += remote_lo[rem];
         if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
         if (is_ess) qi = di;
-        x[gid] = xi + alpha * di;
+        __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
         const double ri = rold - alpha * qi;
-        r[gid] = ri;
+        __builtin_nontemporal_store(ri, &r[gid]);
         if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
     }
     const double bs = block_sum(acc, sh);
