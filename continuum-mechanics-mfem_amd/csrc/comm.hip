@@ -166,7 +166,10 @@ int cdfem_comm_init_rccl(cdfem_ctx *c, int rank, int nranks, const unsigned char
     Comm *m = new Comm();
     m->rank = rank;
     m->nranks = nranks;
-    if (nranks > 1) {
+    {
+        // a one-rank communicator is created too (its collectives are never issued: every
+        // exchange returns early at nranks == 1); tests/test_gpu_rccl.py initialises one beside a
+        // live context, as every rank of the N > 1 bench does
         ncclUniqueId u;
         for (int i = 0; i < NCCL_UNIQUE_ID_BYTES; ++i) u.internal[i] = (char)id[i];
         if (hipSetDevice(c->device) != hipSuccess) {
