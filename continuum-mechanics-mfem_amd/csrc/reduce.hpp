@@ -45,21 +45,20 @@ __device__ inline void store_partial(double block_total, double *part)
 // deterministic sum of part[0..n) by one block (fixed order), result valid in thread 0
 // The loads of a thread are issued kB at a time before any is added: the partials were just
 // written by blocks on all 8 XCDs, so each load is a far round trip, and a load-add loop pays one
-// per partial per thread.  The adds keep the loop's order, so the sum is bitwise the same.
+// per partial per thread.  The adds keep the loop's order (out-of-range slots add +0.0, which
+// leaves every sum unchanged), so the result is bitwise the same.
 __device__ inline double sum_partials(const double *part, int n, double *sh)
 {
     constexpr int kB = 8;
     const int bd = blockDim.x;
     double v = 0.0;
-    int i = threadIdx.x;
-    for (; i + (kB - 1) * bd < n; i += kB * bd) {
+    for (int i = threadIdx.x; i < n; i += kB * bd) {
         double a[kB];
 #pragma unroll
-        for (int k = 0; k < kB; ++k) a[k] = part[i + k * bd];
+        for (int k = 0; k < kB; ++k) a[k] = (i + k * bd < n) ? part[i + k * bd] : 0.0;
 #pragma unroll
         for (int k = 0; k < kB; ++k) v += a[k];
     }
-    for (; i < n; i += bd) v += part[i];
     return block_sum(v, sh);
 }
 
