@@ -76,3 +76,19 @@ def test_null_context_is_rejected():
     L = cdfem.lib()
     assert L.cdfem_synchronize(None) == cdfem.ERR_ARG
     assert L.cdfem_last_error(None) == b"null context"
+
+
+def test_rccl_selftest_built_against_rccl():
+    """The one-rank RCCL check the gpu tests run (tests/test_gpu_rccl.py) is built with the library
+    and links the same librccl as libcdfem.so (no GPU needed to check the link)."""
+    import os
+    import subprocess
+    lib_dir = os.path.join(os.path.dirname(__file__), "..", "continuum-mechanics-mfem_amd", "lib")
+    exe, so = os.path.join(lib_dir, "rccl_selftest"), os.path.join(lib_dir, "libcdfem.so")
+    assert os.path.exists(exe), "run __graft_entry__.build() first"
+
+    def rccl_of(path):
+        out = subprocess.run(["ldd", path], capture_output=True, text=True, check=True).stdout
+        return [ln.split("=>")[1].split()[0] for ln in out.splitlines() if "librccl" in ln]
+
+    assert rccl_of(exe) and rccl_of(exe) == rccl_of(so)
