@@ -73,6 +73,11 @@ def parse():
     return a
 
 
+def kinds_label(kinds):
+    """Integrator set of a kinds bit mask: 1 Diffusion, 2 Convection, 4 Mass (e.g. 7 -> D+C+M)."""
+    return "+".join(n for b, n in ((1, "D"), (2, "C"), (4, "M")) if kinds & b)
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -414,7 +419,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
             "scaling": "strong" if args.config == "c5" else "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"{n}x{n}x{nz} hex, H1 p={p}, PA D+C+M (kinds={args.kinds}), "
+            "config": {"workload": f"{n}x{n}x{nz} hex, H1 p={p}, PA {kinds_label(args.kinds)} (kinds={args.kinds}), "
                                    f"Jacobi-CG {args.cg_iters} it/step",
                        "dofs": total_dofs, "elements": n * n * nz, "cg_iters_per_step": args.cg_iters,
                        "parallelism": f"slab{world}" if world > 1 else "single", "path": args.path,
