@@ -368,6 +368,29 @@ def test_brick_cg_parity(gpu_ctx):
     gpu_ctx.set_option("brick_variant", 0)
 
 
+@pytest.mark.parametrize("n,p", [(8, 2), (9, 1)])
+def test_brick_cg_bench_operator_parity(gpu_ctx, n, p):
+    """The bench's operator (D+C+M, kinds=7, c = (1, -2, 0.5)) through the fused brick CG: fixed
+    Jacobi-CG iterates (tolerance 0, as bench.py times them) against the oracle's MFEM CGSolver
+    restatement on the same eliminated matrix, and bitwise repeatable."""
+    om = O.BoxMesh(3, n, p, perturb=0.1)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3)
+    b = np.random.default_rng(20261015).uniform(-1, 1, om.nl)
+    u = np.zeros(om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    assert _relmax(B, Bo) <= MULT_TOL
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    xg, ig = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    assert ig["iterations"] == 30
+    assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
+    xg2, _ = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    np.testing.assert_array_equal(xg, xg2)
+
+
 def test_brick_full_size_matches_generic(gpu_ctx):
     """64^3 p=2: brick and generic paths agree (different E->L summation order only)."""
     gm = cdfem.box_mesh(3, 64, 2, with_coords=False)
