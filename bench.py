@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cg-iters", type=int, default=None, help="default 100 (c2) / 20 (c3)")
     ap.add_argument("--kinds", type=int, default=7, help="1 diffusion | 2 convection | 4 mass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--spd-steps", type=int, default=2,
+                    help="informational CG line on the symmetric kK+sM operator (steps of 200 it); 0 = skip")
     ap.add_argument("--gmres-iters", type=int, default=60,
                     help="informational GMRES(30)+Jacobi line (the reference's solver); 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
@@ -82,6 +84,11 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # libcdfem.so (and through it the /opt/rocm librccl it links) is loaded BEFORE torch: torch
+    # bundles its own librccl with the same soname, which would otherwise be the one libcdfem
+    # binds to.  config.comm records the library actually used (cdfem_comm_info).
+    import cdfem
+    cdfem.lib()
     pg = None
     if world > 1:
         import torch.distributed as dist
@@ -105,13 +112,34 @@ def allmax(pg, v):
     return float(t.item())
 
 
+def host_cores(args):
+    """Threads for the CPU baseline and a description of the host.  The job's CPU share is the
+    scheduler affinity mask, further capped by OMP_NUM_THREADS when the harness sets it (the GPU
+    box reports the whole machine in nproc but grants each one-GPU job 16 threads)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    model = "?"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return (args.cpu_threads or share), {"host_nproc": os.cpu_count(), "affinity_cpus": aff,
+                                         "omp_num_threads": omp, "cpu_model": model}
+
+
 def cpu_baseline(args, n, p, kinds):
-    """Oracle (C restatement of the reference's CPU FA path) timed on this host's cores.  For p >= 3
-    the FA matrix of the full mesh is out of reach of the CPU (729-wide rows at p = 4), so the
-    sample is a 12^3 mesh of the same order (throughput per DoF-iteration is the reported unit)."""
+    """Oracle (C restatement of the reference's CPU FA path) timed on this host's cores: Jacobi-CG
+    (like-for-like with the GPU metric) and, on the same assembled matrix, GMRES(30)+Jacobi (the
+    reference's solver, Input/petsc.opts:2-6).  For p >= 3 the FA matrix of the full mesh is out of
+    reach of the CPU (729-wide rows at p = 4), so the sample is a 12^3 mesh of the same order
+    (throughput per DoF-iteration is the reported unit)."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    threads, host = host_cores(args)
     O.set_threads(threads)
     if p >= 3:
         n = min(n, 12)
@@ -134,16 +162,28 @@ def cpu_baseline(args, n, p, kinds):
     _, info = O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=n_it)
     dt = time.perf_counter() - t0
     its = info["iterations"]
+    # the reference's solver on the same matrix: GMRES(30) + Jacobi, fixed inner steps
+    t0 = time.perf_counter()
+    O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=5)
+    g_per = (time.perf_counter() - t0) / 5
+    g_it = int(min(3000, max(10, 0.5 * args.cpu_seconds / g_per)))
+    t0 = time.perf_counter()
+    _, ginfo = O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=g_it)
+    gdt = time.perf_counter() - t0
+    gits = ginfo["iterations"]
     return {"value": m.nl * its / dt, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
             "sample": f"oracle FA-CSR Jacobi-CG, {n}^3 hex p={p} ({m.nl} DoFs, nnz={Ac.nnz}), "
-                      f"{its} iterations timed ({dt:.2f} s); assembly+FormLinearSystem {t_asm:.1f} s untimed"}
+                      f"{its} iterations timed ({dt:.2f} s); assembly+FormLinearSystem {t_asm:.1f} s untimed",
+            "gmres": {"value": m.nl * gits / gdt, "unit": "DoF-iter/s",
+                      "sample": f"oracle FA-CSR GMRES(30)+Jacobi on the same matrix, {gits} inner steps ({gdt:.2f} s)"},
+            **host}
 
 
 def cpu_baseline_c4(args, n, p):
     """Oracle FA-CSR GMRES(30)/Jacobi on the same Kuhn mesh (bounded sample)."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    threads, host = host_cores(args)
     O.set_threads(threads)
     m = O.KuhnMesh(3, n, p)
     t0 = time.perf_counter()
@@ -163,7 +203,8 @@ def cpu_baseline_c4(args, n, p):
     its = info["iterations"]
     return {"value": m.nl * its / dt, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
             "sample": f"oracle FA-CSR GMRES(30)/Jacobi, Kuhn {n}^3x6 tets P{p} ({m.nl} DoFs, nnz={Ac.nnz}), "
-                      f"{its} iterations timed ({dt:.2f} s); assembly+FormLinearSystem {t_asm:.1f} s untimed"}
+                      f"{its} iterations timed ({dt:.2f} s); assembly+FormLinearSystem {t_asm:.1f} s untimed",
+            **host}
 
 
 def main_c4(args):
@@ -291,6 +332,7 @@ def main():
         else:
             ctx.comm_init_torch()
         ctx.set_slab(rank > 0, rank < world - 1)
+    comm_lib = cdfem.comm_info(ctx)
     c = (1.0, -2.0, 0.5)
     ctx.pa_setup(kinds=args.kinds, kappa=0.1, alpha=1.0, conv=c, mass=1.0)
 
@@ -401,6 +443,36 @@ def main():
               "orth_avg_us": round(o_ms / max(o_cnt, 1) * 1e3, 2),
               "orth_achieved_gbs": round(orth_bytes / (o_ms / max(o_cnt, 1) * 1e-3) / 1e9, 1) if o_cnt else None}
 
+    # informational: SURVEY §8d's symmetric CG operator kK + sM (c = 0), where CG is a convergent
+    # method; fixed 200 iterations per solve, same mesh
+    spd = None
+    if world == 1 and args.kinds == 7 and args.spd_steps > 0:
+        ctx.pa_setup(kinds=5, kappa=0.1, mass=1.0)
+        _, B5 = ctx.form_linear_system(np.zeros(mesh.nl), b)
+        dB5 = ctx.to_device(B5)
+
+        def sstep():
+            return ctx.solve_device(dB5, dX, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=200,
+                                    check_every=200)
+        sstep()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        sits = sum(sstep()["iterations"] for _ in range(args.spd_steps))
+        ctx.synchronize()
+        sdt = time.perf_counter() - t0
+        ctx.set_option("profile_mask", 1 << cdfem.K_APPLY)
+        ctx.profile(True)
+        sstep()
+        ctx.synchronize()
+        a_ms, a_cnt = ctx.profile_read(cdfem.K_APPLY)
+        ctx.profile(False)
+        sb = ctx.kernel_bytes(cdfem.K_APPLY)
+        s_us = a_ms / max(a_cnt, 1) * 1e3
+        spd = {"value": mesh.nl * sits / sdt, "unit": "DoF-iter/s", "operator": "kK+sM (kinds=5, c=0)",
+               "cg_iters_per_step": 200, "steps": args.spd_steps, "apply_avg_us": round(s_us, 2),
+               "apply_frac": round(sb / (s_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if a_cnt else None}
+        ctx.free(dB5)
+
     ntrue = mesh.nl  # per rank (slab L-vector); interface planes counted once below
     total_dofs = (p * n + 1) ** 2 * (p * nz + 1) if world > 1 else ntrue
     value = total_dofs * iters / dt_max
@@ -421,15 +493,23 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"{n}x{n}x{nz} hex, H1 p={p}, PA {kinds_label(args.kinds)} (kinds={args.kinds}), "
                                    f"Jacobi-CG {args.cg_iters} it/step",
+                       "operator_note": ("fixed-iteration Jacobi-CG on the BASELINE metric's convection-diffusion "
+                                         "operator: a bandwidth figure of the operator + CG vector work (CG has no "
+                                         "convergence meaning on the nonsymmetric D+C+M); solver-faithful lines are "
+                                         "'gmres' (the reference's GMRES(30)+Jacobi, same operator) and 'spd_cg' "
+                                         "(CG on the symmetric kK+sM, SURVEY 8d)") if args.kinds & 2 else
+                                        "fixed-iteration Jacobi-CG on a symmetric operator",
                        "dofs": total_dofs, "elements": n * n * nz, "cg_iters_per_step": args.cg_iters,
                        "parallelism": f"slab{world}" if world > 1 else "single", "path": args.path,
                        "series": "strong: fixed n^3 split into z-slabs" if args.config == "c5"
                                  else "weak: an n^3 slab per rank",
-                       **({"comm": args.comm} if world > 1 else {})},
+                       **({"comm": args.comm, "comm_lib": comm_lib} if world > 1 else {})},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if gm is not None:
             out["gmres"] = gm
+        if spd is not None:
+            out["spd_cg"] = spd
         if host_rate is not None:
             out["host_boundary_rate"] = {"value": host_rate, "unit": "DoF-iter/s",
                                          "note": "one solve with B/X in host memory (PCIe copies included)"}

@@ -98,6 +98,7 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_sdel); dfree(c->d_svals);
     dfree(c->d_svals_c);
     ilu_free(c);
+    partition_free(c);
     c->nslices = c->nstored = 0;
     c->geom = 0;
     c->fa_ready = false;
@@ -220,6 +221,25 @@ void require_pa(cdfem_ctx *c)
 {
     require_mesh(c);
     if (!c->pa_ready && !c->fa_ready) throw StateError("no operator: call cdfem_pa_setup or cdfem_fa_setup");
+}
+
+// a communicator of more than one rank needs a declared partition: the z-slab of a structured box
+// (cdfem_set_slab) or the general shared-dof lists (cdfem_set_shared).  Without one, the exchange
+// would read unset interface buffers and the ranks would take different Krylov branches.
+void require_partition(cdfem_ctx *c)
+{
+    if (!multi_rank(c)) return;
+    if (c->part_mode == 1) {
+        if (!c->structured || !c->d_if[0]) throw StateError("slab partition incomplete: cdfem_set_slab after cdfem_mesh_set_structured");
+        if (c->fa_ready) throw UnsupportedError("slab partitions drive partial-assembly operators; use cdfem_set_shared for assembled ones");
+        return;
+    }
+    if (c->part_mode == 2) {
+        if (use_brick(c)) throw UnsupportedError("the structured brick kernels need a slab partition (cdfem_set_slab)");
+        return;
+    }
+    throw StateError("communicator attached (" + std::to_string(c->nranks) +
+                     " ranks) but no partition declared: call cdfem_set_slab or cdfem_set_shared");
 }
 
 // operator apply into y (device pointers): Ye = A_e x, y = E->L(Ye) [+ constraint]
@@ -430,16 +450,17 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
             prof_mark(c, CDFEM_K_E2L, false);
             return;
         }
-        if (c->fa_ready) {
+        if (c->fa_ready && !mr) {
             HIPCHK(launch_spmv_cg(c, d, z));
             prof_mark(c, CDFEM_K_APPLY, false);
             return;
         }
-        HIPCHK(launch_apply_st(c, d, c->d_Ye, true, c->d_state));
+        if (c->fa_ready) HIPCHK(launch_spmv(c, true, d, z));
+        else HIPCHK(launch_apply_st(c, d, c->d_Ye, true, c->d_state));
         prof_mark(c, CDFEM_K_APPLY, false);
         prof_mark(c, CDFEM_K_E2L, true);
-        if (mr) {  // slab partition: interface sums, essential rows reset, owned den all-reduced
-            HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 0));
+        if (mr) {  // rank partition: interface sums, essential rows reset, owned den all-reduced
+            if (!c->fa_ready) HIPCHK(launch_e2l(c, c->d_Ye, d, z, true, 0));
             interface_sum(c, z);
             HIPCHK(launch_set_ess(c, z, d));
             HIPCHK(launch_den_local(c, d, z));
@@ -792,15 +813,128 @@ int cdfem_set_slab(cdfem_ctx *c, int zlo_shared, int zhi_shared)
         if (!c->structured) throw StateError("cdfem_mesh_set_structured must precede cdfem_set_slab");
         if (c->dim != 3) throw UnsupportedError("multi-rank slabs are 3D z-slabs");
         if ((zlo_shared || zhi_shared) && !c->comm) throw StateError("attach a communicator first");
+        if (c->part_mode == 2) throw StateError("a general partition (cdfem_set_shared) is already declared");
         c->zlo_shared = zlo_shared != 0;
         c->zhi_shared = zhi_shared != 0;
         const int64_t n = c->Lx * c->Ly;
+        c->part_mode = 1;
+        c->skip_lo = c->zlo_shared ? n : 0;  // the lower plane is owned by the rank below
         for (auto &b : c->d_if) {
             dfree(b);
             b = dalloc<double>(n);
             HIPCHK(hipMemsetAsync(b, 0, n * 8, c->stream));
         }
         c->dinv_ready = false;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_set_shared(cdfem_ctx *c, int n_nbr, const int32_t *nbr_ranks, const int64_t *nbr_off,
+                     const int32_t *nbr_idx)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        if (!c->comm) throw StateError("attach a communicator first");
+        if (c->part_mode == 1) throw StateError("a slab partition (cdfem_set_slab) is already declared");
+        if (n_nbr < 0 || (n_nbr > 0 && (!nbr_ranks || !nbr_off || !nbr_idx))) throw ArgError("bad neighbour lists");
+        std::vector<int32_t> ranks(nbr_ranks, nbr_ranks + n_nbr);
+        std::vector<int64_t> off(nbr_off, nbr_off + n_nbr + 1);
+        if (n_nbr == 0) off.assign(1, 0);
+        if (off[0] != 0) throw ArgError("nbr_off[0] must be 0");
+        for (int k = 0; k < n_nbr; ++k) {
+            if (ranks[k] < 0 || ranks[k] >= c->nranks || ranks[k] == c->rank) throw ArgError("bad neighbour rank");
+            if (k > 0 && ranks[k] <= ranks[k - 1]) throw ArgError("neighbour ranks must be strictly ascending");
+            if (off[k + 1] <= off[k]) throw ArgError("every neighbour shares at least one dof");
+        }
+        const int64_t ntot = off[n_nbr];
+        if (ntot >= ((int64_t)1 << 31)) throw ArgError("too many shared entries");
+        std::vector<int32_t> idx(nbr_idx, nbr_idx + ntot);
+        // holders of every shared dof (ascending rank, this rank included) and the owner
+        std::vector<int32_t> first_rank(c->nl, INT32_MAX);
+        std::vector<std::vector<std::pair<int32_t, int32_t>>> contrib;  // per distinct dof: (rank, src)
+        std::vector<int32_t> slot(c->nl, -1), dofs;
+        for (int k = 0; k < n_nbr; ++k) {
+            std::vector<uint8_t> seen;
+            for (int64_t j = off[k]; j < off[k + 1]; ++j) {
+                const int32_t d = idx[j];
+                if (d < 0 || d >= c->nl) throw ArgError("shared dof out of range");
+                if (slot[d] < 0) {
+                    slot[d] = (int32_t)dofs.size();
+                    dofs.push_back(d);
+                    contrib.push_back({{c->rank, -1}});
+                }
+                auto &cl = contrib[slot[d]];
+                for (auto &pr : cl)
+                    if (pr.first == ranks[k]) throw ArgError("a dof appears twice in one neighbour list");
+                cl.push_back({ranks[k], (int32_t)j});
+                first_rank[d] = std::min(first_rank[d], ranks[k]);
+            }
+        }
+        // ownership: a dof held by a lower rank is not owned here; those dofs must be the prefix
+        int64_t n_not_owned = 0;
+        for (int32_t d : dofs)
+            if (first_rank[d] < c->rank) ++n_not_owned;
+        for (int32_t d : dofs)
+            if ((first_rank[d] < c->rank) != (d < n_not_owned))
+                throw ArgError("local numbering must list the dofs owned by lower ranks first (owned true dofs = suffix)");
+        std::vector<int32_t> soff(1, 0), src, owner;
+        for (size_t i = 0; i < dofs.size(); ++i) {
+            auto cl = contrib[i];
+            std::sort(cl.begin(), cl.end());
+            for (auto &pr : cl) src.push_back(pr.second);
+            soff.push_back((int32_t)src.size());
+            owner.push_back(cl.front().first == c->rank ? -1 : cl.front().second);
+        }
+        partition_free(c);
+        c->nbr_rank = ranks;
+        c->nbr_off = off;
+        c->n_shd = (int32_t)dofs.size();
+        c->d_sh_idx = dalloc<int32_t>(ntot);
+        c->d_sh_send = dalloc<double>(ntot);
+        c->d_sh_recv = dalloc<double>(ntot);
+        c->d_shd = dalloc<int32_t>(dofs.size());
+        c->d_shd_off = dalloc<int32_t>(soff.size());
+        c->d_shd_src = dalloc<int32_t>(src.size());
+        c->d_shd_owner = dalloc<int32_t>(owner.size());
+        if (ntot) HIPCHK(hipMemcpyAsync(c->d_sh_idx, idx.data(), ntot * 4, hipMemcpyHostToDevice, c->stream));
+        if (!dofs.empty()) {
+            HIPCHK(hipMemcpyAsync(c->d_shd, dofs.data(), dofs.size() * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->d_shd_src, src.data(), src.size() * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->d_shd_owner, owner.data(), owner.size() * 4, hipMemcpyHostToDevice, c->stream));
+        }
+        HIPCHK(hipMemcpyAsync(c->d_shd_off, soff.data(), soff.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->part_mode = 2;
+        c->skip_lo = n_not_owned;
+        c->dinv_ready = false;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_true_size(cdfem_ctx *c, int64_t *ntrue, int64_t *first_owned)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        if (ntrue) *ntrue = c->nl - c->skip_lo;
+        if (first_owned) *first_owned = c->skip_lo;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_prolongate(cdfem_ctx *c, const double *X, double *x, int where)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        require_partition(c);
+        if (!X || !x) throw ArgError("null vector");
+        const int64_t nt = c->nl - c->skip_lo;
+        double *dx = where == CDFEM_DEVICE ? x : c->d_w[1];
+        HIPCHK(hipMemsetAsync(dx, 0, c->skip_lo * 8, c->stream));
+        HIPCHK(hipMemcpyAsync(dx + c->skip_lo, X, nt * 8, where == CDFEM_DEVICE ? hipMemcpyDeviceToDevice
+                                                                                 : hipMemcpyHostToDevice, c->stream));
+        interface_copy_owner(c, dx);
+        dev_out(c, x, where, dx, c->nl);
+        HIPCHK(hipStreamSynchronize(c->stream));
         return CDFEM_OK;
     });
 }
@@ -1087,6 +1221,7 @@ int cdfem_pa_mult(cdfem_ctx *c, const double *x, double *y, int constrained, int
 {
     return guarded(c, [&] {
         require_pa(c);
+        require_partition(c);
         if (!x || !y) throw ArgError("null vector");
         const double *dx = dev_in(c, x, where, c->d_w[0], c->nl);
         double *dy = where == CDFEM_DEVICE ? y : c->d_w[1];
@@ -1139,6 +1274,7 @@ int cdfem_form_linear_system(cdfem_ctx *c, const double *x, const double *b, dou
 {
     return guarded(c, [&] {
         require_pa(c);
+        require_partition(c);
         if (!x || !b || !X || !B) throw ArgError("null vector");
         const double *dx = dev_in(c, x, where, c->d_w[0], c->nl);
         const double *db = dev_in(c, b, where, c->d_w[1], c->nl);
@@ -1163,6 +1299,7 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
 {
     return guarded(c, [&] {
         require_pa(c);
+        require_partition(c);
         if (!p || !B || !X || !res) throw ArgError("null argument");
         if (p->max_iter < 0) throw ArgError("max_iter < 0");
         if (p->pc != CDFEM_PC_NONE && p->pc != CDFEM_PC_JACOBI && p->pc != CDFEM_PC_ILU)

@@ -45,6 +45,8 @@ int simplex_ndofs(int dim, int p);
 void simplex_basis(int dim, int p, const double *xi, double *phi, double *dphi);
 extern const int kSimplexEdge[6][2];
 double p3_edge_t(int k);
+// element partition helpers (partition.cpp, host only)
+void partition_rcb(int dim, int ne, int nv, const double *elem_verts, int nranks, int32_t *part);
 void p3_tri_nodes(double (*X)[2]);
 extern const int kTriEdge[3][2];
 Rule1D make_rule(int p, int q1);
@@ -149,6 +151,22 @@ struct cdfem_ctx {
     cdfem::Comm *comm = nullptr;        // rank communicator (comm.hip), nullptr on one GPU
     int rank = 0, nranks = 1;
     double *d_if[4] = {};               // interface planes: send_lo, recv_lo, send_hi, recv_hi
+    // rank partition of the L-vector: 0 none, 1 z-slab (cdfem_set_slab), 2 general element
+    // partition (cdfem_set_shared).  Both number the dofs owned by a lower rank first, so the
+    // owned (true) dofs are the suffix [skip_lo, nl) and every dot product skips the prefix.
+    int part_mode = 0;
+    int64_t skip_lo = 0;
+    // general partition: per neighbour rank (ascending) the shared local dofs, same order on both
+    // sides; send/recv buffers concatenated in neighbour order
+    std::vector<int32_t> nbr_rank;
+    std::vector<int64_t> nbr_off;       // [n_nbr + 1]
+    int32_t *d_sh_idx = nullptr;        // [n_sh] local dof of send/recv slot
+    double *d_sh_send = nullptr, *d_sh_recv = nullptr;
+    int32_t n_shd = 0;                  // distinct shared dofs
+    int32_t *d_shd = nullptr;           // [n_shd] their local index
+    int32_t *d_shd_off = nullptr;       // [n_shd + 1] contributions, ascending rank (own = -1)
+    int32_t *d_shd_src = nullptr;       //   source: -1 own partial, else recv slot
+    int32_t *d_shd_owner = nullptr;     // [n_shd] recv slot of the owner's copy, -1 if owned here
 
     // rules
     cdfem::Rule1D rule_op, rule_lf, rule_err;
@@ -289,6 +307,9 @@ void comm_allreduce(cdfem_ctx *c, double *dbuf, int n);
 void comm_exchange(cdfem_ctx *c, const double *send_lo, double *recv_lo, const double *send_hi,
                    double *recv_hi, int64_t n, hipStream_t s = nullptr);
 void interface_sum(cdfem_ctx *c, double *v);  // L-vector interface planes summed over ranks
+// non-owned shared entries of an L-vector <- the owner's value (MFEM P applied to R v)
+void interface_copy_owner(cdfem_ctx *c, double *v);
+void partition_free(cdfem_ctx *c);
 inline bool multi_rank(const cdfem_ctx *c) { return c->nranks > 1; }
 // split CG finalizers for the multi-rank path: local sum -> all-reduce -> step
 hipError_t launch_fin_sum(cdfem_ctx *c, int nparts, int slot);

@@ -13,9 +13,11 @@
 // Two backends: RCCL (stream-ordered, no host sync: the production path over xGMI) and host
 // callbacks (device->host staging + user functions, e.g. torch.distributed/gloo or MPI; used to
 // test the distributed kernels with several processes on ONE GPU, which RCCL refuses).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdio>
 #include <stdexcept>
 #include <string>
 
@@ -29,6 +31,8 @@ struct Comm {
     cdfem_allreduce_fn h_allreduce = nullptr;
     cdfem_exchange_fn h_exchange = nullptr;
     void *user = nullptr;
+    cdfem_nbr_exchange_fn h_nbr = nullptr;  // general partition (host backend)
+    void *nbr_user = nullptr;
     double *h_buf = nullptr;  // pinned staging for the host backend
     size_t h_cap = 0;
 };
@@ -86,7 +90,10 @@ void comm_exchange(cdfem_ctx *c, const double *send_lo, double *recv_lo, const d
     if (!s) s = c->stream;
     Comm *m = c->comm;
     if (!m || m->nranks == 1) return;
-    const bool lo = m->rank > 0, hi = m->rank < m->nranks - 1;
+    // the neighbours are the ones the slab declared (cdfem_set_slab), not the rank arithmetic
+    const bool lo = c->zlo_shared != 0, hi = c->zhi_shared != 0;
+    if ((lo && m->rank == 0) || (hi && m->rank == m->nranks - 1))
+        throw std::runtime_error("slab declares a neighbour rank that does not exist");
     if (m->nccl) {
         nccl_check(ncclGroupStart(), "ncclGroupStart");
         if (lo) {
@@ -131,10 +138,132 @@ __global__ void k_add_plane(double *__restrict__ v, int64_t plane_off, int64_t n
     if (i < n) v[plane_off + i] += in[i];
 }
 
+__global__ void k_copy_plane(double *__restrict__ v, int64_t plane_off, int64_t n, const double *__restrict__ in)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[plane_off + i] = in[i];
+}
+
+// ---- general partition (cdfem_set_shared) ---------------------------------------------------------
+__global__ void k_sh_pack(const double *__restrict__ v, const int32_t *__restrict__ idx, int64_t n,
+                          double *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = v[idx[i]];
+}
+
+// v[d] = sum of every holder's partial in ascending rank order (own partial at src = -1): every
+// rank forms the same sum in the same order, so all copies of a shared dof are bitwise equal
+__global__ void k_sh_sum(double *__restrict__ v, const int32_t *__restrict__ dofs, const int32_t *__restrict__ off,
+                         const int32_t *__restrict__ src, int32_t n, const double *__restrict__ recv)
+{
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t d = dofs[i];
+    const double own = v[d];
+    double acc = 0.0;
+    for (int32_t k = off[i]; k < off[i + 1]; ++k) {
+        const int32_t s = src[k];
+        acc += s < 0 ? own : recv[s];
+    }
+    v[d] = acc;
+}
+
+// non-owned shared dofs take the owner's copy
+__global__ void k_sh_copy_owner(double *__restrict__ v, const int32_t *__restrict__ dofs,
+                                const int32_t *__restrict__ owner, int32_t n, const double *__restrict__ recv)
+{
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && owner[i] >= 0) v[dofs[i]] = recv[owner[i]];
+}
+
+// send[nbr_off[k]..) -> nbr_rank[k], recv[nbr_off[k]..) <- nbr_rank[k], for every neighbour
+static void comm_exchange_nbr(cdfem_ctx *c, hipStream_t s)
+{
+    Comm *m = c->comm;
+    const int nn = (int)c->nbr_rank.size();
+    if (nn == 0) return;
+    const int64_t ntot = c->nbr_off[nn];
+    if (m->nccl) {
+        nccl_check(ncclGroupStart(), "ncclGroupStart");
+        for (int k = 0; k < nn; ++k) {
+            const int64_t o = c->nbr_off[k], cnt = c->nbr_off[k + 1] - o;
+            nccl_check(ncclSend(c->d_sh_send + o, cnt, ncclDouble, c->nbr_rank[k], m->nccl, s), "ncclSend");
+            nccl_check(ncclRecv(c->d_sh_recv + o, cnt, ncclDouble, c->nbr_rank[k], m->nccl, s), "ncclRecv");
+        }
+        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+        return;
+    }
+    if (!m->h_nbr) throw std::runtime_error("host communicator has no neighbour exchange (cdfem_comm_set_host_nbr_exchange)");
+    double *h = host_staging(m, 2 * (size_t)ntot);
+    if (hipMemcpyAsync(h, c->d_sh_send, ntot * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        throw std::runtime_error("exchange staging failed");
+    if (m->h_nbr(nn, c->nbr_rank.data(), c->nbr_off.data(), h, h + ntot, m->nbr_user) != 0)
+        throw std::runtime_error("host neighbour exchange callback failed");
+    if (hipMemcpyAsync(c->d_sh_recv, h + ntot, ntot * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        throw std::runtime_error("exchange staging failed");
+}
+
+static void shared_pack_exchange(cdfem_ctx *c, const double *v)
+{
+    const int64_t ntot = c->nbr_off.empty() ? 0 : c->nbr_off.back();
+    if (ntot > 0)
+        hipLaunchKernelGGL(k_sh_pack, dim3((unsigned)((ntot + 255) / 256)), dim3(256), 0, c->stream, v, c->d_sh_idx,
+                           ntot, c->d_sh_send);
+    comm_exchange_nbr(c, c->stream);
+}
+
+void partition_free(cdfem_ctx *c)
+{
+    for (int32_t **p : {&c->d_sh_idx, &c->d_shd, &c->d_shd_off, &c->d_shd_src, &c->d_shd_owner}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    for (double **p : {&c->d_sh_send, &c->d_sh_recv}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    c->nbr_rank.clear();
+    c->nbr_off.clear();
+    c->n_shd = 0;
+    c->part_mode = 0;
+    c->skip_lo = 0;
+}
+
+// non-owned shared entries <- the owner's value (slab: the lower plane from the rank below)
+void interface_copy_owner(cdfem_ctx *c, double *v)
+{
+    if (!c->comm || c->comm->nranks == 1) return;
+    if (c->part_mode == 2) {
+        shared_pack_exchange(c, v);
+        if (c->n_shd > 0)
+            hipLaunchKernelGGL(k_sh_copy_owner, dim3((unsigned)((c->n_shd + 255) / 256)), dim3(256), 0, c->stream, v,
+                               c->d_shd, c->d_shd_owner, c->n_shd, c->d_sh_recv);
+        return;
+    }
+    if (c->part_mode != 1) return;
+    const int64_t n = c->Lx * c->Ly, off_hi = (c->Lz - 1) * n;
+    const dim3 g((unsigned)((n + 255) / 256)), b(256);
+    if (c->zlo_shared) hipLaunchKernelGGL(k_get_plane, g, b, 0, c->stream, v, (int64_t)0, n, c->d_if[0]);
+    if (c->zhi_shared) hipLaunchKernelGGL(k_get_plane, g, b, 0, c->stream, v, off_hi, n, c->d_if[2]);
+    comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], n);
+    if (c->zlo_shared) hipLaunchKernelGGL(k_copy_plane, g, b, 0, c->stream, v, (int64_t)0, n, c->d_if[1]);
+}
+
 // sum of the interface planes of an L-vector over the ranks sharing them (MFEM P^T then P)
 void interface_sum(cdfem_ctx *c, double *v)
 {
     if (!c->comm || c->comm->nranks == 1) return;
+    if (c->part_mode == 2) {
+        shared_pack_exchange(c, v);
+        if (c->n_shd > 0)
+            hipLaunchKernelGGL(k_sh_sum, dim3((unsigned)((c->n_shd + 255) / 256)), dim3(256), 0, c->stream, v, c->d_shd,
+                               c->d_shd_off, c->d_shd_src, c->n_shd, c->d_sh_recv);
+        return;
+    }
+    if (c->part_mode != 1) return;
     const int64_t n = c->Lx * c->Ly, off_hi = (c->Lz - 1) * n;
     const dim3 g((unsigned)((n + 255) / 256)), b(256);
     if (c->zlo_shared) hipLaunchKernelGGL(k_get_plane, g, b, 0, c->stream, v, (int64_t)0, n, c->d_if[0]);
@@ -187,6 +316,31 @@ int cdfem_comm_init_rccl(cdfem_ctx *c, int rank, int nranks, const unsigned char
     c->rank = rank;
     c->nranks = nranks;
     return CDFEM_OK;
+}
+
+int cdfem_comm_set_host_nbr_exchange(cdfem_ctx *c, cdfem_nbr_exchange_fn fn, void *user)
+{
+    if (!c || !fn) return CDFEM_ERR_ARG;
+    if (!c->comm || c->comm->nccl) {
+        c->err = "cdfem_comm_set_host_nbr_exchange: attach a host communicator first (cdfem_comm_init_host)";
+        return CDFEM_ERR_STATE;
+    }
+    c->comm->h_nbr = fn;
+    c->comm->nbr_user = user;
+    return CDFEM_OK;
+}
+
+int cdfem_comm_info(const cdfem_ctx *c, char *buf, size_t n)
+{
+    if (!buf || n == 0) return CDFEM_ERR_ARG;
+    int v = 0;
+    (void)ncclGetVersion(&v);
+    Dl_info info{};
+    const char *path = dladdr(reinterpret_cast<void *>(&ncclGetVersion), &info) && info.dli_fname
+                           ? info.dli_fname : "?";
+    const char *backend = !c || !c->comm ? "none" : c->comm->nccl ? "rccl" : "host";
+    const int w = std::snprintf(buf, n, "backend=%s rccl_version=%d rccl_path=%s", backend, v, path);
+    return (w < 0 || (size_t)w >= n) ? CDFEM_ERR_ARG : CDFEM_OK;
 }
 
 int cdfem_comm_init_host(cdfem_ctx *c, int rank, int nranks, cdfem_allreduce_fn allreduce,

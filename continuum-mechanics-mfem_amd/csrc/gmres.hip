@@ -431,7 +431,7 @@ hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it)
 
 // multi-rank: partial sums -> local sum (mode 1) -> all-reduce over ranks -> scalar logic (mode 2);
 // every rank then runs the same scalar arithmetic on the same sums and takes the same branches
-static int64_t owned_from(const cdfem_ctx *c) { return c->zlo_shared ? c->Lx * c->Ly : 0; }
+static int64_t owned_from(const cdfem_ctx *c) { return c->skip_lo; }
 static double *red_of(GmresState *st) { return st->red; }
 
 hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,

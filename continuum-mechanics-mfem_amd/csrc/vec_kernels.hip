@@ -578,7 +578,7 @@ hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double
                                 const double *dinv)
 {
     const unsigned g = red_grid(c, c->nl);
-    const int64_t skip = c->zlo_shared ? c->Lx * c->Ly : 0;
+    const int64_t skip = c->skip_lo;
     hipLaunchKernelGGL(k_cg_init, dim3(g), dim3(kRedThreads), 0, c->stream, B, x, r, z, d, dinv, c->nl,
                        skip, c->d_part);
     return launch_fin_sum(c, (int)g, 2);
@@ -613,7 +613,7 @@ hipError_t launch_cg_update(cdfem_ctx *c, double *x, double *r, double *z, const
 {
     const unsigned g = red_grid(c, c->nl);
     hipLaunchKernelGGL(k_cg_update<true>, dim3(g), dim3(kRedThreads), 0, c->stream, x, r, z, d, dinv,
-                       c->nl, (int64_t)(c->zlo_shared ? c->Lx * c->Ly : 0), c->d_part, c->d_state);
+                       c->nl, c->skip_lo, c->d_part, c->d_state);
     if (multi_rank(c)) return launch_fin_sum(c, (int)g, 1);  // all-reduced, then the update step
     hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, (int)g, c->d_state);
     return hipGetLastError();
@@ -660,7 +660,7 @@ hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_
 hipError_t launch_den_local(cdfem_ctx *c, const double *d, const double *q)
 {
     const unsigned g = red_grid(c, c->nl);
-    const int64_t skip = c->zlo_shared ? c->Lx * c->Ly : 0;
+    const int64_t skip = c->skip_lo;
     hipLaunchKernelGGL(k_dot, dim3(g), dim3(kRedThreads), 0, c->stream, d, q, c->nl, skip, c->d_part);
     return launch_fin_sum(c, (int)g, 0);
 }

@@ -55,6 +55,8 @@ class SolverResult(C.Structure):
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
                           C.POINTER(C.c_double), C.c_int64, C.c_void_p)
+NBR_EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                              C.POINTER(C.c_double), C.c_void_p)
 
 _lib = None
 _dp = C.POINTER(C.c_double)
@@ -94,6 +96,16 @@ def _declare(L):
         "cdfem_comm_init_rccl": (C.c_int, [vp, C.c_int, C.c_int, C.c_char_p]),
         "cdfem_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, ALLREDUCE_FN, EXCHANGE_FN, vp]),
         "cdfem_set_slab": (C.c_int, [vp, C.c_int, C.c_int]),
+        "cdfem_set_shared": (C.c_int, [vp, C.c_int, _ip, C.POINTER(i64), _ip]),
+        "cdfem_comm_set_host_nbr_exchange": (C.c_int, [vp, NBR_EXCHANGE_FN, vp]),
+        "cdfem_true_size": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i64)]),
+        "cdfem_prolongate": (C.c_int, [vp, vp, vp, C.c_int]),
+        "cdfem_comm_info": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
+        "cdfem_partition_rcb": (C.c_int, [C.c_int, C.c_int, C.c_int, _dp, C.c_int, _ip]),
+        "cdfem_local_space_sizes": (C.c_int, [C.c_int, C.c_int, i64, _ip, _ip, C.c_int, C.POINTER(C.c_int),
+                                              C.POINTER(i64), C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(i64)]),
+        "cdfem_local_space": (C.c_int, [C.c_int, C.c_int, i64, _ip, _ip, C.c_int, _ip, _ip, C.POINTER(i64), _ip,
+                                        C.POINTER(i64), _ip]),
         "cdfem_box_sizes": (C.c_int, [C.c_int] * 7 + [C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int)]),
         "cdfem_box_mesh": (C.c_int, [C.c_int] * 7 + [C.c_double, _dp, _ip, _ip, _dp]),
         "cdfem_mesh_upload_simplex": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, _dp, i64, _ip, C.c_int, _ip]),
@@ -140,6 +152,15 @@ def comm_unique_id() -> bytes:
     if rc:
         raise CdfemError(rc, "ncclGetUniqueId failed")
     return buf.raw
+
+
+def comm_info(ctx=None) -> dict:
+    """Backend, RCCL version and the librccl file libcdfem.so is bound to in this process."""
+    buf = C.create_string_buffer(4096)
+    rc = lib().cdfem_comm_info(ctx.h if ctx is not None else None, buf, len(buf))
+    if rc:
+        raise CdfemError(rc, "cdfem_comm_info failed")
+    return dict(kv.split("=", 1) for kv in buf.value.decode().split(" "))
 
 
 def _f64(a):
@@ -232,6 +253,59 @@ def gmsh_mesh(path, order, ess_attrs=None) -> Mesh:
     m = Mesh(d, order, verts, dofmap, nl.value, np.nonzero(sel)[0].astype(np.int32), xyz, simplex=True)
     m.bdr_mask = mask
     return m
+
+
+def partition_rcb(mesh: Mesh, nranks) -> np.ndarray:
+    """Element -> rank (recursive coordinate bisection of the element centroids; ParMesh's partition)."""
+    verts = _f64(mesh.verts)
+    part = np.zeros(mesh.ne, dtype=np.int32)
+    rc = lib().cdfem_partition_rcb(mesh.dim, mesh.ne, verts.shape[1], _p(verts), int(nranks), part.ctypes.data_as(_ip))
+    if rc:
+        raise CdfemError(rc, "cdfem_partition_rcb failed")
+    return part
+
+
+@dataclass
+class LocalSpace:
+    """The rank-local piece of a partitioned mesh (cdfem_local_space): a Mesh in local numbering
+    (dofs owned by lower ranks first), its global element / dof ids and the shared-dof lists."""
+    mesh: Mesh
+    elems: np.ndarray
+    l2g: np.ndarray
+    nbr_ranks: np.ndarray
+    nbr_off: np.ndarray
+    nbr_idx: np.ndarray
+    n_not_owned: int
+
+
+def local_space(mesh: Mesh, part, rank) -> LocalSpace:
+    L = lib()
+    dm = _i32(mesh.dofmap)
+    part = _i32(part)
+    ne_loc, nl_loc, n_nbr, n_sh, n_no = C.c_int(), C.c_int64(), C.c_int(), C.c_int64(), C.c_int64()
+    args = (mesh.ne, dm.shape[1], int(mesh.nl), dm.ctypes.data_as(_ip), part.ctypes.data_as(_ip), int(rank))
+    rc = L.cdfem_local_space_sizes(*args, C.byref(ne_loc), C.byref(nl_loc), C.byref(n_nbr), C.byref(n_sh), C.byref(n_no))
+    if rc:
+        raise CdfemError(rc, f"cdfem_local_space_sizes failed for rank {rank}")
+    elems = np.zeros(ne_loc.value, dtype=np.int32)
+    loc = np.zeros((ne_loc.value, dm.shape[1]), dtype=np.int32)
+    l2g = np.zeros(nl_loc.value, dtype=np.int64)
+    nr = np.zeros(n_nbr.value, dtype=np.int32)
+    no = np.zeros(n_nbr.value + 1, dtype=np.int64)
+    ni = np.zeros(max(n_sh.value, 1), dtype=np.int32)
+    rc = L.cdfem_local_space(*args, elems.ctypes.data_as(_ip), loc.ctypes.data_as(_ip),
+                             l2g.ctypes.data_as(C.POINTER(C.c_int64)), nr.ctypes.data_as(_ip),
+                             no.ctypes.data_as(C.POINTER(C.c_int64)), ni.ctypes.data_as(_ip))
+    if rc:
+        raise CdfemError(rc, f"cdfem_local_space failed for rank {rank}")
+    g2l = np.full(mesh.nl, -1, dtype=np.int64)
+    g2l[l2g] = np.arange(len(l2g))
+    ess = g2l[mesh.ess]
+    ess = np.sort(ess[ess >= 0]).astype(np.int32)
+    xyz = mesh.dof_xyz[l2g] if mesh.dof_xyz is not None else None
+    m = Mesh(mesh.dim, mesh.order, np.ascontiguousarray(mesh.verts[elems]), loc, len(l2g), ess, xyz,
+             simplex=mesh.simplex)
+    return LocalSpace(m, elems, l2g, nr, no, ni[: n_sh.value], int(n_no.value))
 
 
 class Context:
@@ -410,11 +484,53 @@ class Context:
             except Exception:
                 return 1
 
-        self._cb = (ALLREDUCE_FN(allreduce), EXCHANGE_FN(exchange))  # keep alive
+        def nbr_exchange(n_nbr, ranks, off, send, recv, _user):
+            try:
+                reqs, outs = [], []
+                tot = off[n_nbr]
+                sa = np.ctypeslib.as_array(send, (tot,)).copy()
+                for k in range(n_nbr):
+                    a, b, r = off[k], off[k + 1], ranks[k]
+                    reqs.append(dist.isend(torch.from_numpy(sa[a:b].copy()), r, group=group))
+                    t = torch.empty(b - a, dtype=torch.float64)
+                    reqs.append(dist.irecv(t, r, group=group))
+                    outs.append((a, b, t))
+                for q in reqs:
+                    q.wait()
+                ra = np.ctypeslib.as_array(recv, (tot,))
+                for a, b, t in outs:
+                    ra[a:b] = t.numpy()
+                return 0
+            except Exception:
+                return 1
+
+        self._cb = (ALLREDUCE_FN(allreduce), EXCHANGE_FN(exchange), NBR_EXCHANGE_FN(nbr_exchange))  # keep alive
         self._chk(self.L.cdfem_comm_init_host(self.h, rank, world, self._cb[0], self._cb[1], None))
+        self._chk(self.L.cdfem_comm_set_host_nbr_exchange(self.h, self._cb[2], None))
 
     def set_slab(self, zlo_shared, zhi_shared):
         self._chk(self.L.cdfem_set_slab(self.h, int(bool(zlo_shared)), int(bool(zhi_shared))))
+
+    def set_shared(self, ls: LocalSpace):
+        """General partition: the shared-dof lists of this rank's LocalSpace."""
+        nr, no, ni = _i32(ls.nbr_ranks), np.ascontiguousarray(ls.nbr_off, dtype=np.int64), _i32(ls.nbr_idx)
+        if len(ni) == 0:
+            ni = np.zeros(1, dtype=np.int32)
+        self._chk(self.L.cdfem_set_shared(self.h, len(nr), nr.ctypes.data_as(_ip),
+                                          no.ctypes.data_as(C.POINTER(C.c_int64)), ni.ctypes.data_as(_ip)))
+
+    def true_size(self):
+        """(number of true dofs, first owned L-dof): the T-vector is the L-vector suffix."""
+        nt, f = C.c_int64(), C.c_int64()
+        self._chk(self.L.cdfem_true_size(self.h, C.byref(nt), C.byref(f)))
+        return nt.value, f.value
+
+    def prolongate(self, X):
+        """x = P X (owned entries from X, the other shared entries from their owner rank)."""
+        X = _f64(X)
+        x = np.zeros(self.nl)
+        self._chk(self.L.cdfem_prolongate(self.h, X.ctypes.data, x.ctypes.data, HOST))
+        return x
 
     # -- device-resident variants (benchmarks) ------------------------------------------------------
     def alloc(self, nbytes):

@@ -233,6 +233,35 @@ int cdfem_comm_init_host(cdfem_ctx *ctx, int rank, int nranks, cdfem_allreduce_f
                          cdfem_exchange_fn exchange, void *user);
 int cdfem_set_slab(cdfem_ctx *ctx, int zlo_shared, int zhi_shared);
 
+/* General element partition of any conforming mesh (ParMesh(MPI_COMM_WORLD, *mesh) and the
+ * ParFiniteElementSpace shared-dof groups, linear_convection_diffusion_2D.cpp:300,312; used where the
+ * mesh is not a structured box, e.g. the reference's gmsh triangles).  After uploading its local mesh
+ * and attaching a communicator, each rank lists per neighbour rank (strictly ascending) the local dofs
+ * it shares with that rank, in the same order on both sides (ascending global id).  A shared dof is
+ * OWNED by the lowest rank holding it, and the local numbering must list the dofs owned by lower ranks
+ * first: the true dofs are the suffix of the L-vector (cdfem_local_space produces this numbering).
+ * Shared sums add every holder's partial in ascending rank order, so all copies are bitwise equal.
+ * nbr_off: n_nbr + 1 offsets into nbr_idx (n_nbr = 0: a rank that shares nothing).                 */
+int cdfem_set_shared(cdfem_ctx *ctx, int n_nbr, const int32_t *nbr_ranks, const int64_t *nbr_off,
+                     const int32_t *nbr_idx);
+/* Host backend of the general partition: send[nbr_off[k] .. nbr_off[k+1]) goes to nbr_ranks[k] and
+ * recv[same range] receives from it (MPI_Isend/Irecv, gloo, ...).  RCCL contexts need none.      */
+typedef int (*cdfem_nbr_exchange_fn)(int n_nbr, const int32_t *nbr_ranks, const int64_t *nbr_off,
+                                     const double *send, double *recv, void *user);
+int cdfem_comm_set_host_nbr_exchange(cdfem_ctx *ctx, cdfem_nbr_exchange_fn fn, void *user);
+
+/* True dofs (MFEM T-vector) = the owned L-dofs, the suffix [first_owned, nl) of the L-vector
+ * (slab: the lower interface plane belongs to the rank below; one rank: everything).
+ * replaces: ParFiniteElementSpace::TrueVSize / GetTrueDofs (:313,353).                          */
+int cdfem_true_size(cdfem_ctx *ctx, int64_t *ntrue, int64_t *first_owned);
+/* x = P X: the L-vector (nl) of the true-dof vector X (ntrue): owned entries from X, the other
+ * shared entries received from their owner.  replaces: RecoverFEMSolution's P (:377).           */
+int cdfem_prolongate(cdfem_ctx *ctx, const double *X, double *x, int where);
+
+/* Communicator report: "backend=<none|rccl|host> rccl_version=<ncclGetVersion> rccl_path=<file>",
+ * the RCCL build libcdfem.so is bound to in this process (ctx may be NULL).                      */
+int cdfem_comm_info(const cdfem_ctx *ctx, char *buf, size_t n);
+
 /* ---- structured mesh helper (host only, no device needed) ---------------------------------------
  * Box [0,1]^dim into nx*ny(*nz) quads/hexes with the conventions above; rank-slab variant for
  * the element-partitioned multi-GPU path: elements with iz in [z0, z1) only, dofs renumbered
@@ -245,6 +274,21 @@ int cdfem_box_mesh(int dim, int nx, int ny, int nz, int order, int z0, int z1, d
 /* Kuhn simplex mesh of [0,1]^dim (config C4): n^dim cubes, dim! simplices each, P1/P2 dofs on the
  * (order n + 1)^dim lattice; perturb moves interior vertices (returns CDFEM_ERR_ARG if that inverts
  * an element).  Host only.                                                                      */
+/* Element partition for the general path (host only): recursive coordinate bisection of the element
+ * centroids into nranks parts, part[e] = rank (MFEM's ParMesh calls METIS, which is absent here; any
+ * partition defines the same global operator).  Deterministic: every rank computes the same one.  */
+int cdfem_partition_rcb(int dim, int ne, int nv, const double *elem_verts, int nranks, int32_t *part);
+/* The rank-local H1 space of a partition (host only): elems = the rank's elements (ascending global
+ * index), loc_dofs = their dofs in local numbering (dofs owned by lower ranks first, then the owned
+ * ones, each by ascending global id), l2g = global id of each local dof, and the neighbour lists that
+ * cdfem_set_shared takes.                                                                        */
+int cdfem_local_space_sizes(int ne, int nd, int64_t nldofs, const int32_t *elem_dofs, const int32_t *part,
+                            int rank, int *ne_loc, int64_t *nl_loc, int *n_nbr, int64_t *n_shared,
+                            int64_t *n_not_owned);
+int cdfem_local_space(int ne, int nd, int64_t nldofs, const int32_t *elem_dofs, const int32_t *part, int rank,
+                      int32_t *elems, int32_t *loc_dofs, int64_t *l2g, int32_t *nbr_ranks, int64_t *nbr_off,
+                      int32_t *nbr_idx);
+
 int cdfem_kuhn_sizes(int dim, int n, int order, int *ne, int64_t *nldofs, int *n_ess);
 int cdfem_kuhn_mesh(int dim, int n, int order, double perturb, double *elem_verts, int32_t *elem_dofs,
                     int32_t *ess_dofs, double *dof_xyz);

@@ -484,3 +484,59 @@ def test_gpu_high_order_two_ranks_one_device(tmp_path):
         np.testing.assert_allclose(x1[:plane], x0[-plane:], rtol=0, atol=1e-12 * np.abs(x0).max())
         xg = np.concatenate([x0, x1[plane:]])
         assert np.linalg.norm(xg - ref) <= tol * np.linalg.norm(ref)
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE configs[4] (C5) per-rank work: each rank owns a 256 x 256 x 32 slab of the 256^3 p = 2
+# mesh (the 8-GPU partition).  Two such slabs on two host-communicator ranks sharing one GPU, brick
+# CG on the full D+C+M operator, against one context holding the 256 x 256 x 64 union.
+C5_N, C5_PER, C5_ITERS = 256, 32, 20
+
+
+def _gpu_c5_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    import cdfem
+    dist = _init(rank, world, port)
+    m = cdfem.box_mesh(3, (C5_N, C5_N, C5_PER * world), P, z_range=(rank * C5_PER, (rank + 1) * C5_PER),
+                       with_coords=False)
+    ctx = cdfem.Context(0)
+    ctx.upload_mesh(m).set_structured(C5_N, C5_N, C5_PER)
+    ctx.comm_init_torch()
+    ctx.set_slab(rank > 0, rank < world - 1)
+    ctx.pa_setup(kinds=7, kappa=KAPPA, alpha=1.0, conv=CONV, mass=S)
+    b = np.random.default_rng(700 + rank).uniform(-1, 1, m.nl)
+    np.save(os.path.join(out_dir, f"b{rank}.npy"), b)
+    _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+    X, info = ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=C5_ITERS,
+                        check_every=C5_ITERS)
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), X)
+    np.save(os.path.join(out_dir, f"its{rank}.npy"), np.array([info["iterations"]]))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_c5_per_rank_slabs(tmp_path):
+    """C5's per-GPU slab (256 x 256 x 32, p = 2, D+C+M) through the multi-rank brick CG: 20 fixed
+    Jacobi-CG iterates on 2 ranks == one context on 256 x 256 x 64 (1e-12), and the shared plane
+    is bitwise the same on both ranks."""
+    import cdfem
+    world = 2
+    mp.start_processes(_gpu_c5_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    plane = (P * C5_N + 1) ** 2
+    bfull = _gathered_rhs(tmp_path, plane)
+    m = cdfem.box_mesh(3, (C5_N, C5_N, C5_PER * world), P, with_coords=False)
+    with cdfem.Context(0) as ctx:
+        ctx.upload_mesh(m).set_structured(C5_N, C5_N, C5_PER * world)
+        ctx.pa_setup(kinds=7, kappa=KAPPA, alpha=1.0, conv=CONV, mass=S)
+        _, B = ctx.form_linear_system(np.zeros(m.nl), bfull)
+        xs, info = ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=C5_ITERS,
+                             check_every=C5_ITERS)
+    x0, x1 = np.load(tmp_path / "x0.npy"), np.load(tmp_path / "x1.npy")
+    assert int(np.load(tmp_path / "its0.npy")[0]) == info["iterations"] == C5_ITERS
+    np.testing.assert_array_equal(x1[:plane], x0[-plane:])
+    xg = np.concatenate([x0, x1[plane:]])
+    assert np.linalg.norm(xg - xs) <= 1e-12 * np.linalg.norm(xs)

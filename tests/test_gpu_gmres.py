@@ -111,3 +111,42 @@ def test_gmres_all_essential(gpu_ctx):
     xs, info = gpu_ctx.solve(B, method="gmres", rel_tol=1e-12, max_iter=10)
     assert info["converged"] and info["iterations"] == 1
     np.testing.assert_allclose(xs, u, rtol=0, atol=1e-14 * u.max())
+
+
+TIGHT = [("hex p=2 brick", 3, 6, 2, 0.0, True), ("hex p=2 generic", 3, 4, 2, 0.15, False),
+         ("hex p=4 structured", 3, 3, 4, 0.0, True), ("hex p=4 generic", 3, 3, 4, 0.1, False),
+         ("quad p=3", 2, 6, 3, 0.15, False)]
+
+
+@pytest.mark.parametrize("name,dim,n,p,pert,structured", TIGHT)
+def test_gmres_tight_solution_parity_pa(gpu_ctx, name, dim, n, p, pert, structured):
+    """SURVEY §8d ladder step 3 for the reference's own solver: GMRES(30) + Jacobi on the full
+    nonsymmetric D+C+M operator, GPU and oracle both solved to rtol 1e-13: solutions within 1e-10
+    relative L2 (north-star tolerance)."""
+    om, Ac, Bo, B = _system(gpu_ctx, dim, n, p, pert, structured=structured)
+    dinv = 1.0 / Ac.diag()
+    xo, io = O.gmres(Ac, Bo, dinv=dinv, restart=30, rtol=1e-13, atol=0.0, max_it=5000)
+    xg, ig = gpu_ctx.solve(B, method="gmres", pc="jacobi", restart=30, rel_tol=1e-13, abs_tol=0.0,
+                           max_iter=5000)
+    assert io["converged"] and ig["converged"], (io, ig)
+    assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
+
+
+def test_gmres_tight_solution_parity_fa_tets(gpu_ctx):
+    """The same bar on the assembled path (C4's FA CSR on Kuhn tets, P2)."""
+    om = O.KuhnMesh(3, 4, 2, perturb=0.1)
+    gm = cdfem.Mesh(3, 2, om.verts, om.dofmap, om.nl, om.ess, simplex=True)
+    gpu_ctx.upload_mesh(gm)
+    gpu_ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    A = O.fa_assemble_simplex(om, kappa=0.1, alpha=1.0, s=1.0, c=C3)
+    rng = np.random.default_rng(9)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    xo, io = O.gmres(Ac, Bo, dinv=1.0 / Ac.diag(), restart=30, rtol=1e-13, atol=0.0, max_it=5000)
+    xg, ig = gpu_ctx.solve(B, method="gmres", pc="jacobi", restart=30, rel_tol=1e-13, abs_tol=0.0,
+                           max_iter=5000)
+    assert io["converged"] and ig["converged"], (io, ig)
+    assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
