@@ -997,17 +997,33 @@ int cdfem_quadrature_points(cdfem_ctx *c, int rule, double *xyz, int where)
     });
 }
 
-int cdfem_pa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kappa_q, double alpha,
-                   const double *conv, const double *conv_q, double mass, const double *mass_q)
+// device copy of an optional host coefficient array (freed by the caller)
+static double *upload_opt(cdfem_ctx *c, const double *h, size_t n)
+{
+    if (!h) return nullptr;
+    double *d = dalloc<double>(n);
+    HIPCHK(hipMemcpyAsync(d, h, n * 8, hipMemcpyHostToDevice, c->stream));
+    return d;
+}
+
+static void check_form(const cdfem_ctx *c, const cdfem_form_coeffs *f)
+{
+    if (!f) throw ArgError("null form");
+    if (f->kinds == 0 || f->kinds > 7) throw ArgError("kinds must be a non-empty DIFFUSION|CONVECTION|MASS mask");
+    if ((f->kinds & CDFEM_CONVECTION) && !f->conv && !f->conv_q) throw ArgError("convection needs a velocity");
+    (void)c;
+}
+
+static int pa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
 {
     return guarded(c, [&] {
         require_mesh(c);
-        if (kinds == 0 || kinds > 7) throw ArgError("kinds must be a non-empty DIFFUSION|CONVECTION|MASS mask");
-        if ((kinds & CDFEM_CONVECTION) && !conv && !conv_q) throw ArgError("convection needs a velocity");
+        check_form(c, f);
         if (c->geom != 0) throw UnsupportedError("simplex meshes use full assembly: cdfem_fa_setup");
         if (!apply_supported(c->dim, c->p))
             throw UnsupportedError("no PA apply kernel built for dim=" + std::to_string(c->dim) +
                                    " order=" + std::to_string(c->p));
+        const unsigned kinds = f->kinds;
         dfree(c->d_qd);
         c->kinds = kinds;
         c->ncomp = ((kinds & CDFEM_DIFFUSION) ? c->dim * (c->dim + 1) / 2 : 0) +
@@ -1016,27 +1032,35 @@ int cdfem_pa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kap
         c->d_qd = c->qlay == 1 ? dalloc<double>((size_t)c->ne * c->rule_op.q1 * qd_ho_plane(c->ncomp, c->rule_op.q1))
                                : dalloc<double>((size_t)c->nblk * nq * c->ncomp * kLanes);
         const size_t neq = (size_t)c->ne * nq;
-        double *dk = nullptr, *dc = nullptr, *dm = nullptr;
-        if (kappa_q) {
-            dk = dalloc<double>(neq);
-            HIPCHK(hipMemcpyAsync(dk, kappa_q, neq * 8, hipMemcpyHostToDevice, c->stream));
-        }
-        if (conv_q) {
-            dc = dalloc<double>(neq * c->dim);
-            HIPCHK(hipMemcpyAsync(dc, conv_q, neq * c->dim * 8, hipMemcpyHostToDevice, c->stream));
-        }
-        if (mass_q) {
-            dm = dalloc<double>(neq);
-            HIPCHK(hipMemcpyAsync(dm, mass_q, neq * 8, hipMemcpyHostToDevice, c->stream));
-        }
-        HIPCHK(launch_setup_qdata(c, dk, kappa, alpha, conv, dc, dm, mass));
+        double *dk = upload_opt(c, f->kappa_q, neq), *dkm = upload_opt(c, f->kappa_mat_q, neq * c->dim * (c->dim + 1) / 2);
+        double *dc = upload_opt(c, f->conv_q, neq * c->dim), *dm = upload_opt(c, f->mass_q, neq);
+        HIPCHK(launch_setup_qdata(c, dk, dkm, f->kappa, f->alpha, f->conv, dc, dm, f->mass));
         HIPCHK(hipStreamSynchronize(c->stream));
-        dfree(dk); dfree(dc); dfree(dm);
+        dfree(dk); dfree(dkm); dfree(dc); dfree(dm);
         c->pa_ready = true;
         c->fa_ready = false;
         c->dinv_ready = false;
         return CDFEM_OK;
     });
+}
+
+static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f);
+
+int cdfem_pa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f) { return pa_setup_form(c, f); }
+int cdfem_fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f) { return fa_setup_form(c, f); }
+
+int cdfem_pa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kappa_q, double alpha,
+                   const double *conv, const double *conv_q, double mass, const double *mass_q)
+{
+    const cdfem_form_coeffs f{kinds, kappa, kappa_q, nullptr, alpha, conv, conv_q, mass, mass_q};
+    return pa_setup_form(c, &f);
+}
+
+int cdfem_fa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kappa_q, double alpha,
+                   const double *conv, const double *conv_q, double mass, const double *mass_q)
+{
+    const cdfem_form_coeffs f{kinds, kappa, kappa_q, nullptr, alpha, conv, conv_q, mass, mass_q};
+    return fa_setup_form(c, &f);
 }
 
 int cdfem_mesh_upload_simplex(cdfem_ctx *c, int dim, int order, int ne, const double *elem_verts,
@@ -1131,13 +1155,12 @@ int cdfem_mesh_upload_simplex(cdfem_ctx *c, int dim, int order, int ne, const do
     });
 }
 
-int cdfem_fa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kappa_q, double alpha,
-                   const double *conv, const double *conv_q, double mass, const double *mass_q)
+static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
 {
     return guarded(c, [&] {
         require_mesh(c);
-        if (kinds == 0 || kinds > 7) throw ArgError("kinds must be a non-empty DIFFUSION|CONVECTION|MASS mask");
-        if ((kinds & CDFEM_CONVECTION) && !conv && !conv_q) throw ArgError("convection needs a velocity");
+        check_form(c, f);
+        const unsigned kinds = f->kinds;
         if (c->geom != 1) throw UnsupportedError("full assembly is implemented for simplex meshes");
         if (!c->d_rowptr) {  // CSR pattern + contribution lists: once per mesh
             FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl);
@@ -1176,25 +1199,14 @@ int cdfem_fa_setup(cdfem_ctx *c, unsigned kinds, double kappa, const double *kap
             HIPCHK(hipStreamSynchronize(c->stream));  // P's host buffers die at scope exit
         }
         const size_t neq = (size_t)c->ne * c->nq_simplex;
-        double *dk = nullptr, *dc = nullptr, *dm = nullptr;
-        if (kappa_q) {
-            dk = dalloc<double>(neq);
-            HIPCHK(hipMemcpyAsync(dk, kappa_q, neq * 8, hipMemcpyHostToDevice, c->stream));
-        }
-        if (conv_q) {
-            dc = dalloc<double>(neq * c->dim);
-            HIPCHK(hipMemcpyAsync(dc, conv_q, neq * c->dim * 8, hipMemcpyHostToDevice, c->stream));
-        }
-        if (mass_q) {
-            dm = dalloc<double>(neq);
-            HIPCHK(hipMemcpyAsync(dm, mass_q, neq * 8, hipMemcpyHostToDevice, c->stream));
-        }
+        double *dk = upload_opt(c, f->kappa_q, neq), *dkm = upload_opt(c, f->kappa_mat_q, neq * c->dim * (c->dim + 1) / 2);
+        double *dc = upload_opt(c, f->conv_q, neq * c->dim), *dm = upload_opt(c, f->mass_q, neq);
         c->kinds = kinds;
-        HIPCHK(launch_simplex_elem(c, dk, kappa, alpha, conv, dc, dm, mass));
+        HIPCHK(launch_simplex_elem(c, dk, dkm, f->kappa, f->alpha, f->conv, dc, dm, f->mass));
         HIPCHK(launch_fa_assemble(c));
         HIPCHK(launch_sell_fill(c));
         HIPCHK(hipStreamSynchronize(c->stream));
-        dfree(dk); dfree(dc); dfree(dm);
+        dfree(dk); dfree(dkm); dfree(dc); dfree(dm);
         c->fa_ready = true;
         c->pa_ready = false;
         c->dinv_ready = false;
@@ -1221,11 +1233,13 @@ int cdfem_pa_mult(cdfem_ctx *c, const double *x, double *y, int constrained, int
 {
     return guarded(c, [&] {
         require_pa(c);
-        require_partition(c);
+        if (constrained != 2) require_partition(c);
         if (!x || !y) throw ArgError("null vector");
+        if (constrained < 0 || constrained > 2) throw ArgError("constrained must be 0, 1 or 2 (local)");
         const double *dx = dev_in(c, x, where, c->d_w[0], c->nl);
         double *dy = where == CDFEM_DEVICE ? y : c->d_w[1];
-        op_apply_global(c, dx, dy, constrained != 0);  // shared planes: neighbours' partial sums added
+        if (constrained == 2) op_apply(c, dx, dy, false);  // rank-local partial sums (no exchange)
+        else op_apply_global(c, dx, dy, constrained != 0);  // shared dofs: neighbours' partial sums added
         dev_out(c, y, where, dy, c->nl);
         prof_collect(c);
         return CDFEM_OK;

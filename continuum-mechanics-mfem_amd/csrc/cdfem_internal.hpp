@@ -248,7 +248,7 @@ struct cdfem_ctx {
 namespace cdfem {
 
 // ---- kernel launchers (pa_kernels.hip) -------------------------------------------------------
-hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, double kappa, double alpha,
+hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, const double *d_kmat_q, double kappa, double alpha,
                               const double *conv, const double *d_conv_q, const double *d_mass_q,
                               double mass);
 hipError_t launch_apply(cdfem_ctx *c, const double *x, double *Ye, bool constrained);
@@ -337,8 +337,8 @@ struct FaPattern {
     std::vector<int16_t> sdel;   // [stored] column - row when every |column - row| < 2^15, else empty
 };
 FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl);
-hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, double kappa, double alpha, const double *conv,
-                               const double *cq, const double *mq, double mass);
+hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq, double kappa, double alpha,
+                               const double *conv, const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);
 hipError_t launch_simplex_lf(cdfem_ctx *c, const double *fq, double *Ye);
 hipError_t launch_sell_fill(cdfem_ctx *c);

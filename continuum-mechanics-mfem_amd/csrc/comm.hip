@@ -35,6 +35,7 @@ struct Comm {
     void *nbr_user = nullptr;
     double *h_buf = nullptr;  // pinned staging for the host backend
     size_t h_cap = 0;
+    int refs = 1;             // contexts using this communicator (cdfem_comm_share)
 };
 
 static void nccl_check(ncclResult_t r, const char *what)
@@ -45,9 +46,11 @@ static void nccl_check(ncclResult_t r, const char *what)
 void comm_destroy(cdfem_ctx *c)
 {
     if (!c->comm) return;
-    if (c->comm->nccl) (void)ncclCommDestroy(c->comm->nccl);
-    if (c->comm->h_buf) (void)hipHostFree(c->comm->h_buf);
-    delete c->comm;
+    if (--c->comm->refs == 0) {
+        if (c->comm->nccl) (void)ncclCommDestroy(c->comm->nccl);
+        if (c->comm->h_buf) (void)hipHostFree(c->comm->h_buf);
+        delete c->comm;
+    }
     c->comm = nullptr;
     c->rank = 0;
     c->nranks = 1;
@@ -327,6 +330,25 @@ int cdfem_comm_set_host_nbr_exchange(cdfem_ctx *c, cdfem_nbr_exchange_fn fn, voi
     }
     c->comm->h_nbr = fn;
     c->comm->nbr_user = user;
+    return CDFEM_OK;
+}
+
+int cdfem_comm_share(cdfem_ctx *dst, const cdfem_ctx *src)
+{
+    if (!dst || !src || dst == src) return CDFEM_ERR_ARG;
+    if (!src->comm) {
+        dst->err = "cdfem_comm_share: the source context has no communicator";
+        return CDFEM_ERR_STATE;
+    }
+    if (src->comm->nccl && src->device != dst->device) {
+        dst->err = "cdfem_comm_share: an RCCL communicator is bound to the source context's device";
+        return CDFEM_ERR_ARG;
+    }
+    comm_destroy(dst);
+    dst->comm = src->comm;
+    dst->comm->refs++;
+    dst->rank = src->rank;
+    dst->nranks = src->nranks;
     return CDFEM_OK;
 }
 

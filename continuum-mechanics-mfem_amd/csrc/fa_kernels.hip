@@ -195,7 +195,8 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
 template <int DIM, int P>
 __global__ void __launch_bounds__(64)
 k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *__restrict__ stab, unsigned kinds,
-               double kappa, const double *__restrict__ kq, double alpha, double c0, double c1, double c2,
+               double kappa, const double *__restrict__ kq, const double *__restrict__ kmq, double alpha, double c0,
+               double c1, double c2,
                const double *__restrict__ cq, double mass, const double *__restrict__ mq, double *__restrict__ Ee)
 {
     constexpr int ND = P == 1 ? DIM + 1 : P == 2 ? (DIM + 1) * (DIM + 2) / 2 : 10;
@@ -237,16 +238,41 @@ k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *_
         const double W = w_t[q];
         double D[DIM][DIM] = {}, Cv[DIM] = {}, Ms = 0.0;
         if (kinds & CDFEM_DIFFUSION) {
-            const double f = W * (kq ? kq[(size_t)e * nq + q] : kappa) / det;
+            const double kap = kq ? kq[(size_t)e * nq + q] : kappa;
+            if (kmq) {  // MatrixCoefficient: W adj(J) K adj(J)^T / det J with K = kap I + K_q
+                constexpr int NS = DIM * (DIM + 1) / 2;
+                const double *km = kmq + ((size_t)e * nq + q) * NS;
+                double K[DIM][DIM];
 #pragma unroll
-            for (int a = 0; a < DIM; ++a)
+                for (int k = 0, m = 0; k < DIM; ++k)
 #pragma unroll
-                for (int b = 0; b < DIM; ++b) {
-                    double s = 0.0;
+                    for (int l = k; l < DIM; ++l, ++m) K[k][l] = K[l][k] = km[m] + (k == l ? kap : 0.0);
 #pragma unroll
-                    for (int k = 0; k < DIM; ++k) s += A[a][k] * A[b][k];
-                    D[a][b] = f * s;
-                }
+                for (int a = 0; a < DIM; ++a)
+#pragma unroll
+                    for (int b = 0; b < DIM; ++b) {
+                        double s = 0.0;
+#pragma unroll
+                        for (int k = 0; k < DIM; ++k) {
+                            double t = 0.0;
+#pragma unroll
+                            for (int l = 0; l < DIM; ++l) t += K[k][l] * A[b][l];
+                            s += A[a][k] * t;
+                        }
+                        D[a][b] = W * s / det;
+                    }
+            } else {
+                const double f = W * kap / det;
+#pragma unroll
+                for (int a = 0; a < DIM; ++a)
+#pragma unroll
+                    for (int b = 0; b < DIM; ++b) {
+                        double s = 0.0;
+#pragma unroll
+                        for (int k = 0; k < DIM; ++k) s += A[a][k] * A[b][k];
+                        D[a][b] = f * s;
+                    }
+            }
         }
         if (kinds & CDFEM_CONVECTION) {
 #pragma unroll
@@ -418,14 +444,14 @@ k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows,
 }
 
 // ---- launchers ---------------------------------------------------------------------------------
-hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, double kappa, double alpha, const double *conv,
-                               const double *cq, const double *mq, double mass)
+hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq, double kappa, double alpha,
+                               const double *conv, const double *cq, const double *mq, double mass)
 {
     const dim3 g((c->ne + 63) / 64), b(64);
     const double c0 = conv ? conv[0] : 0.0, c1 = conv ? conv[1] : 0.0, c2 = (conv && c->dim == 3) ? conv[2] : 0.0;
 #define CDFEM_SIMPLEX(D, P)                                                                              \
     hipLaunchKernelGGL((k_simplex_elem<D, P>), g, b, 0, c->stream, c->d_verts, c->ne, c->nq_simplex,     \
-                       c->d_stab, c->kinds, kappa, kq, alpha, c0, c1, c2, cq, mass, mq, c->d_Ee)
+                       c->d_stab, c->kinds, kappa, kq, kmq, alpha, c0, c1, c2, cq, mass, mq, c->d_Ee)
     if (c->dim == 3 && c->p == 1) CDFEM_SIMPLEX(3, 1);
     else if (c->dim == 3 && c->p == 2) CDFEM_SIMPLEX(3, 2);
     else if (c->dim == 2 && c->p == 1) CDFEM_SIMPLEX(2, 1);

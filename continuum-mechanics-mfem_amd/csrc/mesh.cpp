@@ -287,7 +287,20 @@ struct Gmsh {
     int ne = 0;
 };
 
-bool read_gmsh(const char *path, int order, Gmsh &G, std::string &err)
+// simplex topology: vertices (increasing gmsh node id among the nodes of domain elements), domain
+// elements as vertex indices re-oriented to det J > 0, boundary elements (vertex indices) + tags
+struct Topo {
+    int dim = 0;
+    std::vector<double> vxyz;        // nvert * dim
+    std::vector<int32_t> ev;         // ne * (dim + 1)
+    std::vector<int32_t> bv;         // nbe * dim
+    std::vector<int32_t> battr;      // nbe
+    int64_t nvert() const { return dim ? (int64_t)vxyz.size() / dim : 0; }
+    int ne() const { return dim ? (int)(ev.size() / (dim + 1)) : 0; }
+    int nbe() const { return (int)battr.size(); }
+};
+
+bool parse_gmsh(const char *path, Topo &T, std::string &err)
 {
     std::FILE *f = std::fopen(path, "r");
     if (!f) { err = "cannot open mesh file"; return false; }
@@ -331,37 +344,63 @@ bool read_gmsh(const char *path, int order, Gmsh &G, std::string &err)
     std::fclose(f);
     const bool has_tet = std::any_of(els.begin(), els.end(), [](const El &e) { return e.type == 4; });
     const int dim = has_tet ? 3 : 2, dtype = has_tet ? 4 : 2, btype = has_tet ? 2 : 1;
-    if (order < 1 || order > (dim == 2 ? 3 : 2)) { err = "unsupported order for this mesh"; return false; }
-    G.dim = dim; G.order = order; G.nv = dim + 1; G.nd = cdfem::simplex_ndofs(dim, order);
-    // vertex dofs: nodes used by domain elements, increasing node id
-    std::map<long, int32_t> vdof;
+    T = Topo();
+    T.dim = dim;
+    std::map<long, int32_t> vid;
     for (const El &e : els)
         if (e.type == dtype)
-            for (long v : e.v) vdof[v] = 0;
+            for (long v : e.v) vid[v] = 0;
     int32_t k = 0;
-    for (auto &kv : vdof) {
-        if (!nodes.count(kv.first)) { err = "element references an unknown node"; return false; }
+    for (auto &kv : vid) {
+        auto it = nodes.find(kv.first);
+        if (it == nodes.end()) { err = "element references an unknown node"; return false; }
         kv.second = k++;
+        for (int d = 0; d < dim; ++d) T.vxyz.push_back(it->second[d]);
     }
-    const int64_t nvd = k;
-    const int nedge_loc = dim == 3 ? 6 : 3, ne_dofs = order - 1;
-    std::map<std::pair<int32_t, int32_t>, int32_t> edge;  // (lo, hi) vertex dof -> edge index
-    std::vector<std::array<long, 4>> tv;
     for (const El &e : els) {
         if (e.type != dtype) continue;
-        std::array<long, 4> v{};
-        for (int i = 0; i <= dim; ++i) v[i] = e.v[i];
-        // orientation: det J > 0
-        const auto &a = nodes[v[0]], &b = nodes[v[1]], &c = nodes[v[2]];
+        for (int i = 0; i <= dim; ++i) T.ev.push_back(vid[e.v[i]]);
+    }
+    for (const El &e : els) {
+        if (e.type != btype || e.tag < 1 || e.tag > 31) continue;
+        bool inside = true;
+        for (long n : e.v) inside = inside && vid.count(n);
+        if (!inside) continue;
+        for (long n : e.v) T.bv.push_back(vid[n]);
+        T.battr.push_back(e.tag);
+    }
+    if (T.ne() == 0) { err = "mesh has no domain elements"; return false; }
+    return true;
+}
+
+// H1 Lagrange space of order p on a simplex topology.  Numbering: vertex dofs = vertex index, then
+// (order - 1) dofs per edge (edges in order of first appearance, dofs along the direction of
+// increasing vertex dof), then P3 triangle interiors.  Elements are re-oriented to det J > 0.
+bool build_space(const Topo &T, int order, Gmsh &G, std::string &err)
+{
+    const int dim = T.dim;
+    if (order < 1 || order > (dim == 2 ? 3 : 2)) { err = "unsupported order for this mesh"; return false; }
+    G = Gmsh();
+    G.dim = dim; G.order = order; G.nv = dim + 1; G.nd = cdfem::simplex_ndofs(dim, order);
+    const int64_t nvd = T.nvert();
+    const int nedge_loc = dim == 3 ? 6 : 3, ne_dofs = order - 1;
+    auto pos = [&](int32_t v, int d) { return T.vxyz[(size_t)v * dim + d]; };
+    std::map<std::pair<int32_t, int32_t>, int32_t> edge;  // (lo, hi) vertex dof -> edge index
+    std::vector<std::array<int32_t, 4>> tv;
+    for (int e = 0; e < T.ne(); ++e) {
+        std::array<int32_t, 4> v{};
+        for (int i = 0; i <= dim; ++i) v[i] = T.ev[(size_t)e * (dim + 1) + i];
+        for (int i = 0; i <= dim; ++i)
+            if (v[i] < 0 || v[i] >= nvd) { err = "element vertex out of range"; return false; }
         double det;
         if (dim == 2) {
-            det = (b[0] - a[0]) * (c[1] - a[1]) - (b[1] - a[1]) * (c[0] - a[0]);
+            det = (pos(v[1], 0) - pos(v[0], 0)) * (pos(v[2], 1) - pos(v[0], 1)) -
+                  (pos(v[1], 1) - pos(v[0], 1)) * (pos(v[2], 0) - pos(v[0], 0));
             if (det < 0) std::swap(v[1], v[2]);
         } else {
-            const auto &d = nodes[v[3]];
-            const double J[3][3] = {{b[0] - a[0], c[0] - a[0], d[0] - a[0]},
-                                    {b[1] - a[1], c[1] - a[1], d[1] - a[1]},
-                                    {b[2] - a[2], c[2] - a[2], d[2] - a[2]}};
+            double J[3][3];
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) J[r][c] = pos(v[c + 1], r) - pos(v[0], r);
             det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
                   J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
             if (det < 0) std::swap(v[2], v[3]);
@@ -372,14 +411,12 @@ bool read_gmsh(const char *path, int order, Gmsh &G, std::string &err)
             for (int ed = 0; ed < nedge_loc; ++ed) {
                 const int la = dim == 3 ? cdfem::kSimplexEdge[ed][0] : cdfem::kTriEdge[ed][0];
                 const int lb = dim == 3 ? cdfem::kSimplexEdge[ed][1] : cdfem::kTriEdge[ed][1];
-                int32_t ga = vdof[v[la]], gb = vdof[v[lb]];
+                int32_t ga = v[la], gb = v[lb];
                 if (ga > gb) std::swap(ga, gb);
                 edge.emplace(std::make_pair(ga, gb), (int32_t)edge.size());
             }
     }
     G.ne = (int)tv.size();
-    if (G.ne == 0) { err = "mesh has no domain elements"; return false; }
-    // edge indices by first appearance (std::map emplace keeps the first index; renumber in order)
     const int64_t nedges = (int64_t)edge.size();
     const int64_t nint = (dim == 2 && order == 3) ? G.ne : 0;
     G.nl = nvd + nedges * ne_dofs + nint;
@@ -387,32 +424,28 @@ bool read_gmsh(const char *path, int order, Gmsh &G, std::string &err)
     G.verts.assign((size_t)G.ne * G.nv * dim, 0.0);
     G.xyz.assign((size_t)G.nl * dim, 0.0);
     G.bmask.assign(G.nl, 0);
-    auto pos = [&](long node, int d) { return nodes[node][d]; };
-    for (auto &kv : vdof)
-        for (int d = 0; d < dim; ++d) G.xyz[(size_t)kv.second * dim + d] = pos(kv.first, d);
-    std::vector<long> dof_node(nvd);
-    for (auto &kv : vdof) dof_node[kv.second] = kv.first;
+    for (int64_t v = 0; v < nvd; ++v)
+        for (int d = 0; d < dim; ++d) G.xyz[(size_t)v * dim + d] = pos((int32_t)v, d);
     auto edge_t = [&](int kk) { return order == 2 ? 0.5 : cdfem::p3_edge_t(kk); };
     for (auto &kv : edge) {
         const int32_t ga = kv.first.first, gb = kv.first.second;
         for (int kk = 0; kk < ne_dofs; ++kk) {
             const int64_t g = nvd + (int64_t)kv.second * ne_dofs + kk;
             const double t = edge_t(kk);
-            for (int d = 0; d < dim; ++d)
-                G.xyz[(size_t)g * dim + d] = pos(dof_node[ga], d) + t * (pos(dof_node[gb], d) - pos(dof_node[ga], d));
+            for (int d = 0; d < dim; ++d) G.xyz[(size_t)g * dim + d] = pos(ga, d) + t * (pos(gb, d) - pos(ga, d));
         }
     }
     for (int e = 0; e < G.ne; ++e) {
         const auto &v = tv[e];
         int32_t *ld = &G.dofs[(size_t)e * G.nd];
         for (int i = 0; i <= dim; ++i) {
-            ld[i] = vdof[v[i]];
+            ld[i] = v[i];
             for (int d = 0; d < dim; ++d) G.verts[((size_t)e * G.nv + i) * dim + d] = pos(v[i], d);
         }
         for (int ed = 0; ed < nedge_loc && ne_dofs > 0; ++ed) {
             const int la = dim == 3 ? cdfem::kSimplexEdge[ed][0] : cdfem::kTriEdge[ed][0];
             const int lb = dim == 3 ? cdfem::kSimplexEdge[ed][1] : cdfem::kTriEdge[ed][1];
-            const int32_t ga = vdof[v[la]], gb = vdof[v[lb]];
+            const int32_t ga = v[la], gb = v[lb];
             const bool fwd = ga < gb;
             const int32_t id = edge[{std::min(ga, gb), std::max(ga, gb)}];
             for (int kk = 0; kk < ne_dofs; ++kk)
@@ -421,28 +454,47 @@ bool read_gmsh(const char *path, int order, Gmsh &G, std::string &err)
         if (nint) {
             const int64_t g = nvd + nedges * ne_dofs + e;
             ld[G.nd - 1] = (int32_t)g;
-            for (int d = 0; d < dim; ++d)
-                G.xyz[(size_t)g * dim + d] = (pos(v[0], d) + pos(v[1], d) + pos(v[2], d)) / 3.0;
+            for (int d = 0; d < dim; ++d) G.xyz[(size_t)g * dim + d] = (pos(v[0], d) + pos(v[1], d) + pos(v[2], d)) / 3.0;
         }
     }
-    // boundary attributes
-    for (const El &e : els) {
-        if (e.type != btype || e.tag < 1 || e.tag > 31) continue;
-        const int32_t bit = 1 << (e.tag - 1);
-        std::vector<int32_t> bv;
-        for (long n : e.v) {
-            auto it = vdof.find(n);
-            if (it == vdof.end()) continue;
-            bv.push_back(it->second);
-            G.bmask[it->second] |= bit;
-        }
-        for (size_t i = 0; i < bv.size() && ne_dofs > 0; ++i)
-            for (size_t j = i + 1; j < bv.size(); ++j) {
+    // boundary attributes: vertices and edge dofs of the boundary elements
+    for (int b = 0; b < T.nbe(); ++b) {
+        const int32_t bit = 1 << (T.battr[b] - 1);
+        const int32_t *bv = &T.bv[(size_t)b * dim];
+        for (int i = 0; i < dim; ++i) G.bmask[bv[i]] |= bit;
+        for (int i = 0; i < dim && ne_dofs > 0; ++i)
+            for (int j = i + 1; j < dim; ++j) {
                 auto it = edge.find({std::min(bv[i], bv[j]), std::max(bv[i], bv[j])});
                 if (it == edge.end()) continue;
                 for (int kk = 0; kk < ne_dofs; ++kk) G.bmask[nvd + (int64_t)it->second * ne_dofs + kk] |= bit;
             }
     }
+    return true;
+}
+
+bool read_gmsh(const char *path, int order, Gmsh &G, std::string &err)
+{
+    Topo T;
+    return parse_gmsh(path, T, err) && build_space(T, order, G, err);
+}
+
+bool topo_from_args(int dim, int64_t nvert, const double *vxyz, int ne, const int32_t *elem_v, int nbe,
+                    const int32_t *bdr_v, const int32_t *bdr_attr, Topo &T)
+{
+    if ((dim != 2 && dim != 3) || nvert < 1 || ne < 1 || !vxyz || !elem_v || nbe < 0 || (nbe > 0 && (!bdr_v || !bdr_attr)))
+        return false;
+    T = Topo();
+    T.dim = dim;
+    T.vxyz.assign(vxyz, vxyz + nvert * dim);
+    T.ev.assign(elem_v, elem_v + (size_t)ne * (dim + 1));
+    if (nbe > 0) {
+        T.bv.assign(bdr_v, bdr_v + (size_t)nbe * dim);
+        T.battr.assign(bdr_attr, bdr_attr + nbe);
+    }
+    for (int32_t a : T.battr)
+        if (a < 1 || a > 31) return false;
+    for (int32_t v : T.bv)
+        if (v < 0 || v >= nvert) return false;
     return true;
 }
 
@@ -467,6 +519,60 @@ int cdfem_gmsh_mesh(const char *path, int order, double *elem_verts, int32_t *el
     Gmsh G;
     std::string err;
     if (!read_gmsh(path, order, G, err)) return CDFEM_ERR_ARG;
+    if (elem_verts) std::copy(G.verts.begin(), G.verts.end(), elem_verts);
+    if (elem_dofs) std::copy(G.dofs.begin(), G.dofs.end(), elem_dofs);
+    if (dof_bdr_mask) std::copy(G.bmask.begin(), G.bmask.end(), dof_bdr_mask);
+    if (dof_xyz) std::copy(G.xyz.begin(), G.xyz.end(), dof_xyz);
+    return CDFEM_OK;
+}
+
+int cdfem_gmsh_topology_sizes(const char *path, int *dim, int64_t *nvert, int *ne, int *nbe)
+{
+    if (!path) return CDFEM_ERR_ARG;
+    Topo T;
+    std::string err;
+    if (!parse_gmsh(path, T, err)) return CDFEM_ERR_ARG;
+    if (dim) *dim = T.dim;
+    if (nvert) *nvert = T.nvert();
+    if (ne) *ne = T.ne();
+    if (nbe) *nbe = T.nbe();
+    return CDFEM_OK;
+}
+
+int cdfem_gmsh_topology(const char *path, double *vxyz, int32_t *elem_v, int32_t *bdr_v, int32_t *bdr_attr)
+{
+    if (!path) return CDFEM_ERR_ARG;
+    Topo T;
+    std::string err;
+    if (!parse_gmsh(path, T, err)) return CDFEM_ERR_ARG;
+    if (vxyz) std::copy(T.vxyz.begin(), T.vxyz.end(), vxyz);
+    if (elem_v) std::copy(T.ev.begin(), T.ev.end(), elem_v);
+    if (bdr_v) std::copy(T.bv.begin(), T.bv.end(), bdr_v);
+    if (bdr_attr) std::copy(T.battr.begin(), T.battr.end(), bdr_attr);
+    return CDFEM_OK;
+}
+
+int cdfem_simplex_space_sizes(int dim, int64_t nvert, const double *vxyz, int ne, const int32_t *elem_v, int order,
+                              int64_t *nldofs)
+{
+    Topo T;
+    Gmsh G;
+    std::string err;
+    if (!topo_from_args(dim, nvert, vxyz, ne, elem_v, 0, nullptr, nullptr, T) || !build_space(T, order, G, err))
+        return CDFEM_ERR_ARG;
+    if (nldofs) *nldofs = G.nl;
+    return CDFEM_OK;
+}
+
+int cdfem_simplex_space(int dim, int64_t nvert, const double *vxyz, int ne, const int32_t *elem_v, int nbe,
+                        const int32_t *bdr_v, const int32_t *bdr_attr, int order, double *elem_verts,
+                        int32_t *elem_dofs, int32_t *dof_bdr_mask, double *dof_xyz)
+{
+    Topo T;
+    Gmsh G;
+    std::string err;
+    if (!topo_from_args(dim, nvert, vxyz, ne, elem_v, nbe, bdr_v, bdr_attr, T) || !build_space(T, order, G, err))
+        return CDFEM_ERR_ARG;
     if (elem_verts) std::copy(G.verts.begin(), G.verts.end(), elem_verts);
     if (elem_dofs) std::copy(G.dofs.begin(), G.dofs.end(), elem_dofs);
     if (dof_bdr_mask) std::copy(G.bmask.begin(), G.bmask.end(), dof_bdr_mask);

@@ -242,8 +242,8 @@ template <int DIM>
 __global__ void __launch_bounds__(256)
 k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm, int ne, int nblk, int qlay,
               const Rule1D r, unsigned kinds,
-              int nc, double kappa, const double *__restrict__ kappa_q, double alpha, double c0,
-              double c1, double c2, const double *__restrict__ conv_q, double mass,
+              int nc, double kappa, const double *__restrict__ kappa_q, const double *__restrict__ kmat_q,
+              double alpha, double c0, double c1, double c2, const double *__restrict__ conv_q, double mass,
               const double *__restrict__ mass_q, double *__restrict__ qd)
 {
     const int q1 = r.q1;
@@ -274,13 +274,31 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
     int o = 0;
     if (kinds & CDFEM_DIFFUSION) {
         const double kap = kappa_q ? kappa_q[eq] : kappa;
-        const double s = W * kap / det;
-        for (int i = 0; i < DIM; ++i)
-            for (int j = i; j < DIM; ++j) {
-                double acc = 0.0;
-                for (int k = 0; k < DIM; ++k) acc += A[i][k] * A[j][k];
-                put(o++, s * acc);
-            }
+        if (kmat_q) {  // MatrixCoefficient: D = W adj(J) K adj(J)^T / det J, K = kap I + K_q (symmetric)
+            constexpr int NS = DIM * (DIM + 1) / 2;
+            double K[3][3];
+            for (int k = 0, m = 0; k < DIM; ++k)
+                for (int l = k; l < DIM; ++l, ++m) K[k][l] = K[l][k] = kmat_q[eq * NS + m] + (k == l ? kap : 0.0);
+            const double s = W / det;
+            for (int i = 0; i < DIM; ++i)
+                for (int j = i; j < DIM; ++j) {
+                    double acc = 0.0;
+                    for (int k = 0; k < DIM; ++k) {
+                        double t = 0.0;
+                        for (int l = 0; l < DIM; ++l) t += K[k][l] * A[j][l];
+                        acc += A[i][k] * t;
+                    }
+                    put(o++, s * acc);
+                }
+        } else {
+            const double s = W * kap / det;
+            for (int i = 0; i < DIM; ++i)
+                for (int j = i; j < DIM; ++j) {
+                    double acc = 0.0;
+                    for (int k = 0; k < DIM; ++k) acc += A[i][k] * A[j][k];
+                    put(o++, s * acc);
+                }
+        }
     }
     if (kinds & CDFEM_CONVECTION) {
         double cv[3] = {c0, c1, c2};
@@ -419,7 +437,7 @@ k_lf_elem(const double *__restrict__ verts, const int32_t *__restrict__ perm, in
 // ------------------------------------------------------------------------------------------------
 static inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
-hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, double kappa, double alpha,
+hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, const double *d_kmat_q, double kappa, double alpha,
                               const double *conv, const double *d_conv_q, const double *d_mass_q,
                               double mass)
 {
@@ -431,11 +449,11 @@ hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, double kapp
     if (c->dim == 3)
         hipLaunchKernelGGL(k_setup_qdata<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
                            c->d_verts, c->d_perm, c->ne, c->nblk, c->qlay, c->rule_op, c->kinds, c->ncomp, kappa,
-                           d_kappa_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
+                           d_kappa_q, d_kmat_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
     else
         hipLaunchKernelGGL(k_setup_qdata<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
                            c->d_verts, c->d_perm, c->ne, c->nblk, c->qlay, c->rule_op, c->kinds, c->ncomp, kappa,
-                           d_kappa_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
+                           d_kappa_q, d_kmat_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
     return hipGetLastError();
 }
 

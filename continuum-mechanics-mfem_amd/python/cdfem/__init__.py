@@ -52,6 +52,12 @@ class SolverResult(C.Structure):
                 ("initial_norm", C.c_double), ("seconds", C.c_double)]
 
 
+class FormCoeffs(C.Structure):
+    _fields_ = [("kinds", C.c_uint), ("kappa", C.c_double), ("kappa_q", C.POINTER(C.c_double)),
+                ("kappa_mat_q", C.POINTER(C.c_double)), ("alpha", C.c_double), ("conv", C.POINTER(C.c_double)),
+                ("conv_q", C.POINTER(C.c_double)), ("mass", C.c_double), ("mass_q", C.POINTER(C.c_double))]
+
+
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
                           C.POINTER(C.c_double), C.c_int64, C.c_void_p)
@@ -81,6 +87,15 @@ def _declare(L):
         "cdfem_quadrature_points": (C.c_int, [vp, C.c_int, _dp, C.c_int]),
         "cdfem_pa_setup": (C.c_int, [vp, C.c_uint, C.c_double, _dp, C.c_double, _dp, _dp, C.c_double, _dp]),
         "cdfem_pa_mult": (C.c_int, [vp, vp, vp, C.c_int, C.c_int]),
+        "cdfem_pa_setup_form": (C.c_int, [vp, C.POINTER(FormCoeffs)]),
+        "cdfem_fa_setup_form": (C.c_int, [vp, C.POINTER(FormCoeffs)]),
+        "cdfem_comm_share": (C.c_int, [vp, vp]),
+        "cdfem_gmsh_topology_sizes": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int),
+                                                C.POINTER(C.c_int)]),
+        "cdfem_gmsh_topology": (C.c_int, [C.c_char_p, _dp, _ip, _ip, _ip]),
+        "cdfem_simplex_space_sizes": (C.c_int, [C.c_int, i64, _dp, C.c_int, _ip, C.c_int, C.POINTER(i64)]),
+        "cdfem_simplex_space": (C.c_int, [C.c_int, i64, _dp, C.c_int, _ip, C.c_int, _ip, _ip, C.c_int, _dp, _ip, _ip,
+                                          _dp]),
         "cdfem_pa_diagonal": (C.c_int, [vp, vp, C.c_int]),
         "cdfem_lf_assemble": (C.c_int, [vp, vp, vp, C.c_int]),
         "cdfem_form_linear_system": (C.c_int, [vp, vp, vp, vp, vp, C.c_int]),
@@ -370,27 +385,29 @@ class Context:
         return xyz
 
     # -- operator ------------------------------------------------------------------------------
-    def pa_setup(self, kinds=DIFFUSION | CONVECTION | MASS, kappa=1.0, alpha=1.0, conv=None, mass=1.0,
-                 kappa_q=None, conv_q=None, mass_q=None):
+    def _form(self, kinds, kappa, alpha, conv, mass, kappa_q, kmat_q, conv_q, mass_q):
         cv = None
         if conv is not None:
             cv = np.zeros(3)
             cv[: len(conv)] = conv
-        keep = [_f64(a) if a is not None else None for a in (kappa_q, conv_q, mass_q)]
-        self._chk(self.L.cdfem_pa_setup(self.h, kinds, float(kappa), _p(keep[0]), float(alpha), _p(cv),
-                                        _p(keep[1]), float(mass), _p(keep[2])))
+        keep = [cv] + [_f64(a) if a is not None else None for a in (kappa_q, kmat_q, conv_q, mass_q)]
+        f = FormCoeffs(int(kinds), float(kappa), _p(keep[1]), _p(keep[2]), float(alpha), _p(keep[0]), _p(keep[3]),
+                       float(mass), _p(keep[4]))
+        return f, keep
+
+    def pa_setup(self, kinds=DIFFUSION | CONVECTION | MASS, kappa=1.0, alpha=1.0, conv=None, mass=1.0,
+                 kappa_q=None, conv_q=None, mass_q=None, kmat_q=None):
+        """Partial assembly of the Diffusion (+ optional symmetric MatrixCoefficient kmat_q, components
+        xx,xy,yy / xx,xy,xz,yy,yz,zz per point: K = kappa I + K_q), Convection and Mass integrators."""
+        f, keep = self._form(kinds, kappa, alpha, conv, mass, kappa_q, kmat_q, conv_q, mass_q)
+        self._chk(self.L.cdfem_pa_setup_form(self.h, C.byref(f)))
         return self
 
     def fa_setup(self, kinds=DIFFUSION | CONVECTION | MASS, kappa=1.0, alpha=1.0, conv=None, mass=1.0,
-                 kappa_q=None, conv_q=None, mass_q=None):
+                 kappa_q=None, conv_q=None, mass_q=None, kmat_q=None):
         """Full assembly (CSR on the GPU) of the same form; simplex meshes."""
-        cv = None
-        if conv is not None:
-            cv = np.zeros(3)
-            cv[: len(conv)] = conv
-        keep = [_f64(a) if a is not None else None for a in (kappa_q, conv_q, mass_q)]
-        self._chk(self.L.cdfem_fa_setup(self.h, kinds, float(kappa), _p(keep[0]), float(alpha), _p(cv),
-                                        _p(keep[1]), float(mass), _p(keep[2])))
+        f, keep = self._form(kinds, kappa, alpha, conv, mass, kappa_q, kmat_q, conv_q, mass_q)
+        self._chk(self.L.cdfem_fa_setup_form(self.h, C.byref(f)))
         return self
 
     def fa_csr(self, constrained=False):

@@ -3,7 +3,7 @@
  *
  * One opaque context per GPU (per process / rank).  All entry points return CDFEM_OK (0) or an
  * error code; the message is in cdfem_last_error(ctx).  No C++ exception crosses this boundary;
- * the C++ mfem-compatible layer (include/cdfem/mfem_compat.hpp) turns a non-zero status into
+ * the C++ MFEM-shaped layer (continuum-mechanics-mfem_amd/cpp/cdfem_mfem.hpp) turns a status into
  * std::runtime_error, which the reference drivers already map to exit code 3
  * (linear_convection_diffusion_2D.cpp:435-442).
  *
@@ -107,6 +107,25 @@ int cdfem_pa_setup(cdfem_ctx *ctx, unsigned kinds, double kappa, const double *k
                    double alpha, const double *conv, const double *conv_q, double mass,
                    const double *mass_q);
 
+/* The same setup with every coefficient form in one struct, including a MatrixCoefficient for the
+ * diffusion: DiffusionIntegrator(MatrixCoefficient&) (diffusion_mms_ale.cpp:474-496,1019), the ALE
+ * metric alpha dt / J cof(A) cof(A)^T.  The diffusion tensor at a point is K = k I + K_q with k =
+ * kappa_q[i] (or kappa) and K_q the symmetric tensor kappa_mat_q[i] (NULL: 0), stored as
+ * xx, xy, yy (2D) / xx, xy, xz, yy, yz, zz (3D); qdata D = W adj(J) K adj(J)^T / det J keeps its
+ * dim(dim+1)/2 components.  Non-symmetric matrix coefficients are not accepted (the shim checks).  */
+typedef struct {
+    unsigned kinds;
+    double kappa;
+    const double *kappa_q;      /* ne*nq, or NULL */
+    const double *kappa_mat_q;  /* ne*nq*dim(dim+1)/2, or NULL */
+    double alpha;
+    const double *conv;         /* 3 doubles (unused components 0) */
+    const double *conv_q;       /* ne*nq*dim, or NULL */
+    double mass;
+    const double *mass_q;       /* ne*nq, or NULL */
+} cdfem_form_coeffs;
+int cdfem_pa_setup_form(cdfem_ctx *ctx, const cdfem_form_coeffs *form);
+
 /* ---- full assembly on simplex meshes (BASELINE config C4: unstructured tetrahedra) -------------
  * replaces: the same ParMesh / H1_FECollection(p, dim) / ParFiniteElementSpace calls on a triangle
  * or tetrahedral mesh (gmsh input, Input/input_2d.yaml:1), and ParBilinearForm::Assemble +
@@ -125,11 +144,14 @@ int cdfem_mesh_upload_simplex(cdfem_ctx *ctx, int dim, int order, int ne, const 
                               int64_t nldofs, const int32_t *elem_dofs, int n_ess, const int32_t *ess_dofs);
 int cdfem_fa_setup(cdfem_ctx *ctx, unsigned kinds, double kappa, const double *kappa_q, double alpha,
                    const double *conv, const double *conv_q, double mass, const double *mass_q);
+int cdfem_fa_setup_form(cdfem_ctx *ctx, const cdfem_form_coeffs *form);
 int cdfem_fa_csr(cdfem_ctx *ctx, int constrained, int64_t *nnz, int32_t *rowptr, int32_t *cols, double *vals);
 
-/* replaces: Operator::Mult / BilinearForm::Mult (diffusion_mms.cpp:430) when constrained == 0,
- * and the ConstrainedOperator built by FormLinearSystem (:349-351) when constrained != 0
- * (input essential entries treated as 0, output y[ess] = x[ess]).                              */
+/* replaces: Operator::Mult on the assembled operator when constrained == 0 (shared dofs summed over
+ * the ranks: P^T A P on a consistent L-vector), the ConstrainedOperator built by FormLinearSystem
+ * (:349-351) when constrained == 1 (input essential entries treated as 0, output y[ess] = x[ess]),
+ * and BilinearForm::Mult on a ParBilinearForm (diffusion_mms.cpp:430) when constrained == 2: the
+ * rank-local product, a partial L-vector (no exchange; the same as 0 on one rank).             */
 int cdfem_pa_mult(cdfem_ctx *ctx, const double *x, double *y, int constrained, int where);
 
 /* replaces: BilinearForm::AssembleDiagonal (PA) — unconstrained operator diagonal.             */
@@ -249,6 +271,9 @@ int cdfem_set_shared(cdfem_ctx *ctx, int n_nbr, const int32_t *nbr_ranks, const 
 typedef int (*cdfem_nbr_exchange_fn)(int n_nbr, const int32_t *nbr_ranks, const int64_t *nbr_off,
                                      const double *send, double *recv, void *user);
 int cdfem_comm_set_host_nbr_exchange(cdfem_ctx *ctx, cdfem_nbr_exchange_fn fn, void *user);
+/* dst uses src's communicator (reference counted): every form of one ParFiniteElementSpace is its
+ * own context, and they share one RCCL communicator instead of bootstrapping one each.          */
+int cdfem_comm_share(cdfem_ctx *dst, const cdfem_ctx *src);
 
 /* True dofs (MFEM T-vector) = the owned L-dofs, the suffix [first_owned, nl) of the L-vector
  * (slab: the lower interface plane belongs to the rank below; one rank: everything).
@@ -303,6 +328,19 @@ int cdfem_kuhn_mesh(int dim, int n, int order, double perturb, double *elem_vert
 int cdfem_gmsh_sizes(const char *path, int order, int *dim, int *ne, int64_t *nldofs);
 int cdfem_gmsh_mesh(const char *path, int order, double *elem_verts, int32_t *elem_dofs, int32_t *dof_bdr_mask,
                     double *dof_xyz);
+/* The same in two steps, for callers that refine or partition the mesh first (Mesh /
+ * UniformRefinement / ParMesh, linear_convection_diffusion_2D.cpp:290-305): the gmsh file's simplex
+ * topology (vertices in increasing node id, xyz nvert*dim; domain elements ne*(dim+1) vertex indices;
+ * boundary elements nbe*dim vertex indices with their physical tags), and the H1 space of order p on
+ * any such topology (the arrays of cdfem_gmsh_mesh; boundary masks from the tagged boundary
+ * elements).  Host only.                                                                        */
+int cdfem_gmsh_topology_sizes(const char *path, int *dim, int64_t *nvert, int *ne, int *nbe);
+int cdfem_gmsh_topology(const char *path, double *vxyz, int32_t *elem_v, int32_t *bdr_v, int32_t *bdr_attr);
+int cdfem_simplex_space_sizes(int dim, int64_t nvert, const double *vxyz, int ne, const int32_t *elem_v, int order,
+                              int64_t *nldofs);
+int cdfem_simplex_space(int dim, int64_t nvert, const double *vxyz, int ne, const int32_t *elem_v, int nbe,
+                        const int32_t *bdr_v, const int32_t *bdr_attr, int order, double *elem_verts,
+                        int32_t *elem_dofs, int32_t *dof_bdr_mask, double *dof_xyz);
 
 /* Host helpers: the collapsed-Gauss simplex rule (returns the point count; xi/w may be NULL to
  * query it) and the nodal simplex basis phi [npts][nd], dphi [npts][nd][dim] in the local dof

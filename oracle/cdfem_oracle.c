@@ -308,7 +308,53 @@ typedef struct {
 typedef struct {
     double kappa, alpha, s, c[3];
     int use_diff, use_conv, use_mass;
+    /* per-quadrature-point values of ONE element (NULL: the constants above), point order of the
+     * element rule: Coefficient kappa_q, symmetric MatrixCoefficient K_q (xx,xy,yy / xx,xy,xz,yy,yz,zz;
+     * K = kappa I + K_q, diffusion_mms_ale.cpp:474-496), VectorCoefficient c_q, Coefficient s_q */
+    const double *kq, *kmq, *cq, *sq;
 } orc_coef;
+
+/* D = W adj(J) K adj(J)^T / det J, Cv = W alpha adj(J) c, M = W s det J at point q  [MFEM-ext PA qdata] */
+static void point_coef(int dim, const orc_coef *cf, int q, double W, double detJ, double A[3][3],
+                       double D[3][3], double Cv[3], double *M)
+{
+    const int ns = dim * (dim + 1) / 2;
+    if (cf->use_diff) {
+        const double kap = cf->kq ? cf->kq[q] : cf->kappa;
+        double K[3][3] = {{0}};
+        for (int k = 0, m = 0; k < dim; k++)
+            for (int l = k; l < dim; l++, m++) {
+                const double v = (cf->kmq ? cf->kmq[(size_t)q * ns + m] : 0.0) + (k == l ? kap : 0.0);
+                K[k][l] = K[l][k] = v;
+            }
+        for (int i = 0; i < dim; i++)
+            for (int j = 0; j < dim; j++) {
+                double acc = 0.0;
+                for (int k = 0; k < dim; k++)
+                    for (int l = 0; l < dim; l++) acc += A[i][k] * K[k][l] * A[j][l];
+                D[i][j] = W * acc / detJ;
+            }
+    }
+    if (cf->use_conv)
+        for (int i = 0; i < dim; i++) {
+            double acc = 0.0;
+            for (int k = 0; k < dim; k++) acc += A[i][k] * (cf->cq ? cf->cq[(size_t)q * dim + k] : cf->c[k]);
+            Cv[i] = W * cf->alpha * acc;
+        }
+    if (cf->use_mass) *M = W * (cf->sq ? cf->sq[q] : cf->s) * detJ;
+}
+
+/* the coefficient set of element e (per-point arrays offset by e * nq) */
+static orc_coef coef_of(const orc_coef *cf, int dim, int64_t e, int nq)
+{
+    orc_coef r = *cf;
+    const size_t o = (size_t)e * nq;
+    if (cf->kq) r.kq = cf->kq + o;
+    if (cf->kmq) r.kmq = cf->kmq + o * (dim * (dim + 1) / 2);
+    if (cf->cq) r.cq = cf->cq + o * dim;
+    if (cf->sq) r.sq = cf->sq + o;
+    return r;
+}
 
 /* Element matrix (row = test, col = trial), nd x nd, for element with vertices V. */
 static void element_matrix(int dim, int p, const double *V, const orc_coef *cf, int nq,
@@ -331,20 +377,7 @@ static void element_matrix(int dim, int p, const double *V, const orc_coef *cf, 
         double detJ = adjugate(dim, J, A);
         /* D = W kappa adj adj^T / detJ ; Cv = W alpha adj c ; M = W s detJ   [MFEM-ext PA qdata] */
         double D[3][3] = {{0}}, Cv[3] = {0}, M = 0.0;
-        if (cf->use_diff)
-            for (int i = 0; i < dim; i++)
-                for (int j = 0; j < dim; j++) {
-                    double acc = 0.0;
-                    for (int k = 0; k < dim; k++) acc += A[i][k] * A[j][k];
-                    D[i][j] = W * cf->kappa * acc / detJ;
-                }
-        if (cf->use_conv)
-            for (int i = 0; i < dim; i++) {
-                double acc = 0.0;
-                for (int k = 0; k < dim; k++) acc += A[i][k] * cf->c[k];
-                Cv[i] = W * cf->alpha * acc;
-            }
-        if (cf->use_mass) M = W * cf->s * detJ;
+        point_coef(dim, cf, qx + nq * (qy + nq * qz), W, detJ, A, D, Cv, &M);
         tensor_basis(dim, p, B, G, qi, phi, gphi);
         for (int j = 0; j < nd; j++) {
             double Dg[3] = {0, 0, 0};
@@ -451,15 +484,17 @@ static orc_csr *csr_from_elements(int nd, int ne, const int *dofmap, int64_t nl,
 }
 
 /* Build the CSR matrix sum_e A_e for tensor (quad/hex) elements. */
-ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, const int *dofmap,
-                                 int64_t nl, double kappa, double alpha, double s, const double *c,
-                                 int kinds)
+/* the same with per-quadrature-point coefficients (NULL arrays: the constants); point order per
+ * element: lexicographic tensor points (qx fastest) of the operator rule, as cdfem_quadrature_points */
+ORC_API orc_csr *orc_fa_assemble_q(int dim, int p, int ne, const double *verts, const int *dofmap,
+                                   int64_t nl, double kappa, const double *kq, const double *kmq, double alpha,
+                                   const double *c, const double *cq, double s, const double *sq, int kinds)
 {
     const int d1 = p + 1;
     const int nd = (dim == 3) ? d1 * d1 * d1 : d1 * d1;
     const int nv = (dim == 3) ? 8 : 4;
     orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
-                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0};
+                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0, kq, kmq, cq, sq};
     /* one shared rule: Diffusion/Convection/Mass coincide on Q1 tensor elements (checked) */
     int nq = orc_rule_npts(0, dim, p);
     if (orc_rule_npts(1, dim, p) != nq || orc_rule_npts(2, dim, p) != nq) return NULL;
@@ -467,13 +502,23 @@ ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, co
     tables(p, nq, B, G, pts, wts);
 
     double *Ae = (double *)malloc(sizeof(double) * (size_t)ne * nd * nd);
+    const int nqe = (dim == 3) ? nq * nq * nq : nq * nq;
     #pragma omp parallel for schedule(static)
-    for (int e = 0; e < ne; e++)
-        element_matrix(dim, p, verts + (size_t)e * nv * dim, &cf, nq, B, G, pts, wts,
+    for (int e = 0; e < ne; e++) {
+        const orc_coef ce = coef_of(&cf, dim, e, nqe);
+        element_matrix(dim, p, verts + (size_t)e * nv * dim, &ce, nq, B, G, pts, wts,
                        Ae + (size_t)e * nd * nd);
+    }
     orc_csr *A = csr_from_elements(nd, ne, dofmap, nl, Ae);
     free(Ae);
     return A;
+}
+
+ORC_API orc_csr *orc_fa_assemble(int dim, int p, int ne, const double *verts, const int *dofmap,
+                                 int64_t nl, double kappa, double alpha, double s, const double *c,
+                                 int kinds)
+{
+    return orc_fa_assemble_q(dim, p, ne, verts, dofmap, nl, kappa, NULL, NULL, alpha, c, NULL, s, NULL, kinds);
 }
 
 ORC_API void orc_csr_free(orc_csr *A)
@@ -976,7 +1021,7 @@ ORC_API void orc_ebe_mult(int dim, int p, int ne, const double *verts, const int
     const int nv = (dim == 3) ? 8 : 4;
     const int nq = orc_rule_npts(0, dim, p);
     orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
-                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0};
+                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0, NULL, NULL, NULL, NULL};
     double B[64], G[64], pts[8], wts[8];
     tables(p, nq, B, G, pts, wts);
     double *ye = (double *)malloc(sizeof(double) * (size_t)ne * nd);
@@ -1264,20 +1309,7 @@ static void simplex_element_matrix(int dim, int p, const double *V, const orc_co
     for (int q = 0; q < nq; q++) {
         const double W = wq[q];
         double D[3][3] = {{0}}, Cv[3] = {0}, M = 0.0;
-        if (cf->use_diff)
-            for (int i = 0; i < dim; i++)
-                for (int j = 0; j < dim; j++) {
-                    double acc = 0.0;
-                    for (int k = 0; k < dim; k++) acc += A[i][k] * A[j][k];
-                    D[i][j] = W * cf->kappa * acc / detJ;
-                }
-        if (cf->use_conv)
-            for (int i = 0; i < dim; i++) {
-                double acc = 0.0;
-                for (int k = 0; k < dim; k++) acc += A[i][k] * cf->c[k];
-                Cv[i] = W * cf->alpha * acc;
-            }
-        if (cf->use_mass) M = W * cf->s * detJ;
+        point_coef(dim, cf, q, W, detJ, A, D, Cv, &M);
         simplex_basis(dim, p, xi + (size_t)q * dim, phi, dphi);
         for (int j = 0; j < nd; j++) {
             double Dg[3] = {0, 0, 0}, cg = 0.0;
@@ -1296,26 +1328,37 @@ static void simplex_element_matrix(int dim, int p, const double *V, const orc_co
 }
 
 /* FA CSR of the convection-diffusion-reaction form on P1/P2 simplices (rule: n = p + 2). */
-ORC_API orc_csr *orc_fa_assemble_simplex(int dim, int p, int ne, const double *verts, const int *dofmap,
-                                         int64_t nl, double kappa, double alpha, double s, const double *c,
-                                         int kinds)
+ORC_API orc_csr *orc_fa_assemble_simplex_q(int dim, int p, int ne, const double *verts, const int *dofmap,
+                                           int64_t nl, double kappa, const double *kq, const double *kmq,
+                                           double alpha, const double *c, const double *cq, double s,
+                                           const double *sq, int kinds)
 {
     p3_init();
     const int nd = orc_simplex_nd(dim, p);
     if (nd < 0 || (dim != 2 && dim != 3)) return NULL;
     orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
-                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0};
+                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0, kq, kmq, cq, sq};
     const int n1 = p + 2;
     double xi[16 * 16 * 16 * 3 / 16], wq[16 * 16 * 16 / 16];  /* n1 <= 4: 64 points */
     const int nq = orc_simplex_rule(dim, n1, xi, wq);
     double *Ae = (double *)malloc(sizeof(double) * (size_t)ne * nd * nd);
     #pragma omp parallel for schedule(static)
-    for (int e = 0; e < ne; e++)
-        simplex_element_matrix(dim, p, verts + (size_t)e * (dim + 1) * dim, &cf, nq, xi, wq,
+    for (int e = 0; e < ne; e++) {
+        const orc_coef ce = coef_of(&cf, dim, e, nq);
+        simplex_element_matrix(dim, p, verts + (size_t)e * (dim + 1) * dim, &ce, nq, xi, wq,
                                Ae + (size_t)e * nd * nd);
+    }
     orc_csr *A = csr_from_elements(nd, ne, dofmap, nl, Ae);
     free(Ae);
     return A;
+}
+
+ORC_API orc_csr *orc_fa_assemble_simplex(int dim, int p, int ne, const double *verts, const int *dofmap,
+                                         int64_t nl, double kappa, double alpha, double s, const double *c,
+                                         int kinds)
+{
+    return orc_fa_assemble_simplex_q(dim, p, ne, verts, dofmap, nl, kappa, NULL, NULL, alpha, c, NULL, s, NULL,
+                                     kinds);
 }
 
 /* DomainLF b_i = int f phi_i and ||u_h - u||_L2 on affine simplices with the MMS data of

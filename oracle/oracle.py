@@ -46,6 +46,11 @@ def lib():
         L.orc_fa_assemble.restype = C.c_void_p
         L.orc_fa_assemble.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, C.c_int64, C.c_double,
                                       C.c_double, C.c_double, dp, C.c_int]
+        for nm in ("orc_fa_assemble_q", "orc_fa_assemble_simplex_q"):
+            f = getattr(L, nm)
+            f.restype = C.c_void_p
+            f.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, C.c_int64, C.c_double, dp, dp, C.c_double, dp, dp,
+                          C.c_double, dp, C.c_int]
         L.orc_csr_free.argtypes = [C.c_void_p]
         L.orc_csr_n.argtypes = [C.c_void_p]
         L.orc_csr_n.restype = C.c_int64
@@ -259,6 +264,28 @@ def _conv(c, dim):
     return cc
 
 
+def _opt(a):
+    return None if a is None else np.ascontiguousarray(a, dtype=np.float64)
+
+
+def fa_assemble_q(mesh, kappa=0.0, kappa_q=None, kmat_q=None, alpha=1.0, c=None, c_q=None, s=0.0, s_q=None,
+                  kinds=DIFFUSION | CONVECTION | MASS, simplex=False):
+    """FA CSR with per-quadrature-point coefficients (arrays element-major in the operator rule's point
+    order; None: the constant).  kmat_q: the symmetric MatrixCoefficient of DiffusionIntegrator,
+    K = kappa I + K_q, components xx,xy,yy (2D) / xx,xy,xz,yy,yz,zz (3D)."""
+    cc = _conv(c, mesh.dim)
+    arrs = [_opt(a) for a in (kappa_q, kmat_q, c_q, s_q)]
+    ptr = [None if a is None else _d(a) for a in arrs]
+    verts = np.ascontiguousarray(mesh.verts, dtype=np.float64)
+    dofmap = np.ascontiguousarray(mesh.dofmap, dtype=np.int32)
+    f = lib().orc_fa_assemble_simplex_q if simplex else lib().orc_fa_assemble_q
+    h = f(mesh.dim, mesh.p, mesh.ne, _d(verts), _i(dofmap), mesh.nl, float(kappa), ptr[0], ptr[1], float(alpha),
+          _d(cc), ptr[2], float(s), ptr[3], kinds)
+    if not h:
+        raise RuntimeError("orc_fa_assemble_q: unsupported element / rule")
+    return CSR(h)
+
+
 def fa_assemble(mesh: BoxMesh, kappa=1.0, alpha=1.0, s=1.0, c=None, kinds=DIFFUSION | CONVECTION | MASS):
     cc = _conv(c, mesh.dim)
     h = lib().orc_fa_assemble(mesh.dim, mesh.p, mesh.ne, _d(mesh.verts), _i(mesh.dofmap), mesh.nl,
@@ -412,3 +439,74 @@ def set_threads(n):
 
 def num_threads():
     return lib().orc_num_threads()
+
+
+# ---- ALE diffusion MMS coefficients (diffusion_mms_ale.cpp:213-440, 455-558) -------------------------
+# Restated from the reference's AleMap: A(xhat, t) maps the reference square onto Omega(t); the
+# driver assembles on the reference mesh  Mass(J) + Diffusion(alpha dt / J cof cof^T)
+# + Convection(phi_hat, -1) + Mass(-div phi_hat)  (:1017-1023).
+ALE_MAPS = ("identity", "accuracy_a", "accuracy_b")
+
+
+def _ale_amp(kind, t):
+    return 0.5 * np.sin(np.pi * t) if kind == "accuracy_a" else np.sin(np.pi * t)   # :411-414, :436-439
+
+
+def _ale_g(z):      # AccuracyAShape_, :417-421
+    h = ((-z + 1.5) * z - 0.5) * z
+    return np.sin(np.pi * h)
+
+
+def _ale_gp(z):     # AccuracyAShapeD1_, :422-427
+    h = ((-z + 1.5) * z - 0.5) * z
+    hp = (-3.0 * z + 3.0) * z - 0.5
+    return np.pi * np.cos(np.pi * h) * hp
+
+
+def ale_gradient(kind, xy, t):
+    """G = dA/dxhat (MapGradient, :252-287) at points xy (n, 2): (n, 2, 2)."""
+    x, y = xy[:, 0], xy[:, 1]
+    G = np.zeros((len(xy), 2, 2))
+    if kind == "identity":
+        G[:, 0, 0] = G[:, 1, 1] = 1.0
+    elif kind == "accuracy_a":
+        a = _ale_amp(kind, t)
+        G[:, 0, 0] = 1.0 + a * _ale_gp(x)
+        G[:, 1, 1] = 1.0 + a * _ale_gp(y)
+    else:
+        a = _ale_amp(kind, t)
+        ax, ay, dax, day = x * (1 - x), y * (1 - y), 1 - 2 * x, 1 - 2 * y
+        G[:, 0, 0] = 1.0 + a * dax * ay
+        G[:, 0, 1] = a * ax * day
+        G[:, 1, 0] = a * dax * ay
+        G[:, 1, 1] = 1.0 + a * ax * day
+    return G
+
+
+def ale_coefficients(kind, xy, t_old, t_new, alpha, dt):
+    """Per-point coefficients of the ALE left-hand side at t_new: J (AleJacobianCoefficient, :455-469),
+    the metric alpha dt / J cof(G) cof(G)^T as xx,xy,yy (AleMetricTensorCoefficient, :474-502), the
+    integrated grid flux phi_hat and its divergence (IntegratedMappedGridFlux, :338-407)."""
+    G = ale_gradient(kind, xy, t_new)
+    J = G[:, 0, 0] * G[:, 1, 1] - G[:, 0, 1] * G[:, 1, 0]
+    Cf = np.zeros_like(G)                       # MapCofactor, :290-299
+    Cf[:, 0, 0], Cf[:, 0, 1], Cf[:, 1, 0], Cf[:, 1, 1] = G[:, 1, 1], -G[:, 0, 1], -G[:, 1, 0], G[:, 0, 0]
+    M = np.einsum("nij,nkj->nik", Cf, Cf) * (alpha * dt / J)[:, None, None]
+    metric = np.stack([M[:, 0, 0], M[:, 0, 1], M[:, 1, 1]], axis=1)
+    x, y = xy[:, 0], xy[:, 1]
+    phi = np.zeros((len(xy), 2))
+    div = np.zeros(len(xy))
+    if kind == "accuracy_a":
+        a0, a1 = _ale_amp(kind, t_old), _ale_amp(kind, t_new)
+        i1, i2 = a1 - a0, 0.5 * (a1 * a1 - a0 * a0)
+        gx, gxp, gy, gyp = _ale_g(x), _ale_gp(x), _ale_g(y), _ale_gp(y)
+        phi[:, 0] = gx * (i1 + i2 * gyp)
+        phi[:, 1] = gy * (i1 + i2 * gxp)
+        div = i1 * (gxp + gyp) + 2.0 * i2 * gxp * gyp
+    elif kind == "accuracy_b":
+        i1 = _ale_amp(kind, t_new) - _ale_amp(kind, t_old)
+        ax, ay, dax, day = x * (1 - x), y * (1 - y), 1 - 2 * x, 1 - 2 * y
+        q = ax * ay
+        phi[:, 0] = phi[:, 1] = i1 * q
+        div = i1 * (dax * ay + ax * day)
+    return J, metric, phi, div
