@@ -1,40 +1,56 @@
 // convection_diffusion — steady convection-diffusion-reaction MMS solve through the MFEM-shaped
-// host API (cdfem_mfem.hpp) on the MI355X kernels.
+// host API (cdfem_mfem.hpp via mfem.hpp) on the MI355X kernels, one MPI rank per GPU.
 //
-// Follows the hot-path sequence of myapps/convection_diffusion/linear_convection_diffusion_2D.cpp
-// (:300-392): mesh + H1 space, all-boundary Dirichlet, Diffusion + Convection + Mass integrators,
-// DomainLF forcing, boundary projection of the exact solution, FormLinearSystem, a
-// PetscLinearSolver configured from a PETSc options file (Input/petsc.opts keys), solve,
-// RecoverFEMSolution, L2 error.  The problem is the reference's MMS u = sin(n pi x) sin(m pi y)
-// (:159-170), extended with sin(l pi z) in 3D; the forcing is the reference's (:174-205) plus the
-// z terms.  Configuration comes from the command line instead of YAML (out of scope).
+// The main() below is the reference driver's own sequence, myapps/convection_diffusion/
+// linear_convection_diffusion_2D.cpp:238-446, with its call forms unchanged: Mpi::Init / Hypre::Init
+// / Mpi::WorldRank, OptionsParser, MFEMInitializePetsc(options file), Device("cpu"),
+// make_unique<Mesh>(file, 1, 1) + UniformRefinement, make_unique<ParMesh>(MPI_COMM_WORLD, *mesh),
+// MFEM_VERIFY, ParFiniteElementSpace::GlobalTrueVSize, GetEssentialTrueDofs, the three domain
+// integrators, ParLinearForm, ProjectBdrCoefficient, FormLinearSystem, Ah.As<HypreParMatrix>(),
+// PetscParMatrix(MPI_COMM_WORLD, A, PETSC_MATAIJ), PetscLinearSolver, RecoverFEMSolution,
+// ComputeL2Error / ComputeGlobalLpNorm.  What differs: configuration from the command line instead
+// of YAML (out of scope), a generated box when no mesh file is given, the 3D extension of
+// the MMS (sin(l pi z) factor), and no ParaView / CSV output.
 //
-//   convection_diffusion [-d dim] [-n elems | -mesh file.msh] [-p order] [-k kappa] [-s reaction]
-//                        [-c cx,cy,cz] [-m n,m,l] [-opts petsc.opts] [-pl print_level]
-// Output (stdout, one "key value" per line): dofs, iterations, converged, final_norm, l2_abs,
-// l2_rel, solve_seconds.  Exit code 3 on error (as the reference drivers, :435-442).
+//   mpirun -np N convection_diffusion [-d dim] [-n elems | -mesh file.msh] [-p order] [-rs levels]
+//       [-rp levels] [-k kappa] [-s reaction] [-c cx,cy,cz] [-m n,m,l] [-opts petsc.opts] [-pl level]
+// Output (rank 0, stdout, one "key value" per line): dofs, ranks, iterations, converged, final_norm,
+// l2_abs, l2_rel, solve_seconds.  Exit code 3 on error (as the reference drivers, :435-442).
 #include <cmath>
 #include <cstdio>
-#include <cstring>
-#include <exception>
+#include <fstream>
+#include <memory>
 #include <string>
 
-#include "cdfem_mfem.hpp"
+#include "mfem.hpp"
 
-using namespace cdfem::mfem;
+using namespace std;
+using namespace mfem;
 
 namespace {
 
+// the reference's Input/petsc.opts:2-6 (its default options file), used when no file is found
+void default_petsc_options()
+{
+    auto &o = PetscOptions().kv;
+    o.emplace("-ksp_type", "gmres");
+    o.emplace("-ksp_rtol", "1.0e-10");
+    o.emplace("-ksp_atol", "1.0e-12");
+    o.emplace("-ksp_max_it", "500");
+    o.emplace("-pc_type", "jacobi");
+}
+
 struct Params {
-    int dim = 2, n = 16, order = 2, print_level = 0;
+    int dim = 2, n = 16, order = 2, rs = 0, rp = 0, print_level = 0;
     double kappa = 0.1, reaction = 1.0, c[3] = {1.0, -2.0, 0.5};
     int modes[3] = {3, 3, 3};
-    std::string opts, mesh;
+    string opts = "Input/petsc.opts", mesh, cstr, mstr;
 };
 
-class ExactSolution : public Coefficient {
+// u = sin(n pi x) sin(m pi y) [sin(l pi z)]  (:159-175)
+class ExactSolutionCoefficient : public Coefficient {
 public:
-    ExactSolution(int dim, const int *m) : dim_(dim), m_{m[0], m[1], m[2]} {}
+    ExactSolutionCoefficient(int dim, const int *m) : dim_(dim), m_{m[0], m[1], m[2]} {}
     real_t Eval(ElementTransformation &T, const IntegrationPoint &ip) override
     {
         Vector x;
@@ -49,10 +65,10 @@ private:
     int m_[3];
 };
 
-// f = -kappa Lap u + c . grad u + s u for the product of sines
-class Forcing : public Coefficient {
+// f = -kappa Lap u + c . grad u + s u for the product of sines (:177-215 and its 3D extension)
+class ForcingCoefficient : public Coefficient {
 public:
-    explicit Forcing(const Params &p) : p_(p) {}
+    explicit ForcingCoefficient(const Params &p) : p_(p) {}
     real_t Eval(ElementTransformation &T, const IntegrationPoint &ip) override
     {
         Vector x;
@@ -80,109 +96,136 @@ private:
     const Params &p_;
 };
 
-void parse_triplet(const char *s, double *out)
-{
-    std::sscanf(s, "%lf,%lf,%lf", &out[0], &out[1], &out[2]);
-}
-
-Params parse(int argc, char **argv)
-{
-    Params p;
-    for (int i = 1; i + 1 < argc; i += 2) {
-        const std::string k = argv[i];
-        const char *v = argv[i + 1];
-        if (k == "-d") p.dim = std::atoi(v);
-        else if (k == "-n") p.n = std::atoi(v);
-        else if (k == "-p") p.order = std::atoi(v);
-        else if (k == "-k") p.kappa = std::atof(v);
-        else if (k == "-s") p.reaction = std::atof(v);
-        else if (k == "-c") parse_triplet(v, p.c);
-        else if (k == "-m") std::sscanf(v, "%d,%d,%d", &p.modes[0], &p.modes[1], &p.modes[2]);
-        else if (k == "-opts") p.opts = v;
-        else if (k == "-mesh") p.mesh = v;
-        else if (k == "-pl") p.print_level = std::atoi(v);
-        else throw std::invalid_argument("unknown option " + k);
-    }
-    if (p.dim != 2 && p.dim != 3) throw std::invalid_argument("-d must be 2 or 3");
-    return p;
-}
-
 }  // namespace
 
-int main(int argc, char **argv)
+int main(int argc, char *argv[])
 {
+    Mpi::Init(argc, argv);
+    Hypre::Init();
+    const int myid = Mpi::WorldRank();
+
+    Params prm;
+    OptionsParser args(argc, argv);
+    args.AddOption(&prm.dim, "-d", "--dim", "Dimension of the generated box (2 or 3).");
+    args.AddOption(&prm.n, "-n", "--elems", "Elements per direction of the generated box.");
+    args.AddOption(&prm.mesh, "-mesh", "--mesh", "gmsh v2.2 mesh file (replaces the box).");
+    args.AddOption(&prm.order, "-p", "--order", "H1 order.");
+    args.AddOption(&prm.rs, "-rs", "--serial-ref-levels", "Uniform refinements before the partition.");
+    args.AddOption(&prm.rp, "-rp", "--par-ref-levels", "Uniform refinements after the partition.");
+    args.AddOption(&prm.kappa, "-k", "--kappa", "Diffusion coefficient.");
+    args.AddOption(&prm.reaction, "-s", "--reaction", "Reaction coefficient.");
+    args.AddOption(&prm.cstr, "-c", "--convection", "Velocity cx,cy[,cz].");
+    args.AddOption(&prm.mstr, "-m", "--modes", "MMS modes n,m[,l].");
+    args.AddOption(&prm.opts, "-opts", "--petsc-options", "PETSc options file.");
+    args.AddOption(&prm.print_level, "-pl", "--print-level", "Solver print level.");
+    args.Parse();
+    if (!args.Good()) {
+        if (myid == 0) args.PrintUsage(cerr);
+        return 1;
+    }
+    if (!prm.cstr.empty()) std::sscanf(prm.cstr.c_str(), "%lf,%lf,%lf", &prm.c[0], &prm.c[1], &prm.c[2]);
+    if (!prm.mstr.empty()) std::sscanf(prm.mstr.c_str(), "%d,%d,%d", &prm.modes[0], &prm.modes[1], &prm.modes[2]);
+
+    // :268-282, options file (the reference's default path; its values when the file is absent)
+    const char *petsc_file_to_use = nullptr;
+    if (!prm.opts.empty() && ifstream(prm.opts).good()) petsc_file_to_use = prm.opts.c_str();
+    else default_petsc_options();
+    MFEMInitializePetsc(&argc, &argv, petsc_file_to_use, NULL);
+
+    int exit_code = 0;
     try {
-        const Params prm = parse(argc, argv);
-        MFEMInitializePetsc(&argc, &argv, prm.opts.empty() ? nullptr : prm.opts.c_str(), nullptr);
+        if (prm.dim != 2 && prm.dim != 3) throw invalid_argument("-d must be 2 or 3");
+        Device device("cpu");
+        if (myid == 0 && prm.print_level > 0) device.Print(cerr);
 
-        // -mesh: a gmsh file as in the reference's inputs (Input/input_2d.yaml: mesh_file), else a box
-        Mesh mesh = !prm.mesh.empty() ? Mesh(prm.mesh.c_str(), 1, 1)
-                    : prm.dim == 2   ? Mesh::MakeCartesian2D(prm.n, prm.n, Element::QUADRILATERAL)
-                                     : Mesh::MakeCartesian3D(prm.n, prm.n, prm.n, Element::HEXAHEDRON);
-        if (!prm.mesh.empty() && mesh.Dimension() != prm.dim)
-            throw std::invalid_argument("-d does not match the mesh file's dimension");
+        unique_ptr<Mesh> mesh = !prm.mesh.empty() ? make_unique<Mesh>(prm.mesh.c_str(), 1, 1)
+                                : prm.dim == 2 ? make_unique<Mesh>(Mesh::MakeCartesian2D(prm.n, prm.n, Element::QUADRILATERAL))
+                                               : make_unique<Mesh>(Mesh::MakeCartesian3D(prm.n, prm.n, prm.n, Element::HEXAHEDRON));
+        if (mesh->Dimension() != prm.dim) throw runtime_error("-d does not match the mesh file's dimension");
+        for (int l = 0; l < prm.rs; l++) mesh->UniformRefinement();
+
+        unique_ptr<ParMesh> pmesh = make_unique<ParMesh>(MPI_COMM_WORLD, *mesh);
+        mesh.reset();
+        for (int l = 0; l < prm.rp; l++) pmesh->UniformRefinement();
+
+        MFEM_VERIFY(pmesh->bdr_attributes.Size() > 0, "Mesh must define boundary attributes.");
+
         H1_FECollection fec(prm.order, prm.dim);
-        ParFiniteElementSpace fespace(&mesh, &fec);
+        ParFiniteElementSpace fespace(pmesh.get(), &fec);
+        const HYPRE_BigInt global_true_dofs = fespace.GlobalTrueVSize();
 
-        Array<int> ess_bdr(mesh.bdr_attributes.Max());
+        Array<int> ess_bdr(pmesh->bdr_attributes.Max());
         ess_bdr = 1;
         Array<int> ess_tdof_list;
         fespace.GetEssentialTrueDofs(ess_bdr, ess_tdof_list);
 
-        ExactSolution exact(prm.dim, prm.modes);
-        Forcing forcing(prm);
-        Vector cvec(prm.dim);
-        for (int i = 0; i < prm.dim; ++i) cvec[i] = prm.c[i];
-        VectorConstantCoefficient convection(cvec);
-        ConstantCoefficient kappa(prm.kappa), reaction(prm.reaction);
+        ExactSolutionCoefficient exact_coeff(prm.dim, prm.modes);
+        ForcingCoefficient forcing_coeff(prm);
+        Vector c_vec(prm.dim);
+        for (int i = 0; i < prm.dim; ++i) c_vec[i] = prm.c[i];
+        VectorConstantCoefficient convection_coeff(c_vec);
+        ConstantCoefficient kappa_coeff(prm.kappa);
+        ConstantCoefficient reaction_coeff(prm.reaction);
 
         ParBilinearForm a(&fespace);
-        a.AddDomainIntegrator(new DiffusionIntegrator(kappa));
-        a.AddDomainIntegrator(new ConvectionIntegrator(convection));
-        a.AddDomainIntegrator(new MassIntegrator(reaction));
+        a.AddDomainIntegrator(new DiffusionIntegrator(kappa_coeff));
+        a.AddDomainIntegrator(new ConvectionIntegrator(convection_coeff));
+        a.AddDomainIntegrator(new MassIntegrator(reaction_coeff));
         a.Assemble();
 
         ParLinearForm b(&fespace);
-        b.AddDomainIntegrator(new DomainLFIntegrator(forcing));
+        b.AddDomainIntegrator(new DomainLFIntegrator(forcing_coeff));
         b.Assemble();
 
         ParGridFunction u(&fespace);
         u = 0.0;
-        u.ProjectBdrCoefficient(exact, ess_bdr);
+        u.ProjectBdrCoefficient(exact_coeff, ess_bdr);
 
         OperatorHandle Ah(Operator::Hypre_ParCSR);
         Vector X, B;
         a.FormLinearSystem(ess_tdof_list, u, b, Ah, X, B);
 
-        HypreParMatrix *A_true = Ah.As<HypreParMatrix>();
-        if (!A_true) throw std::runtime_error("Expected the constrained operator from FormLinearSystem");
-        PetscParMatrix A_petsc(0, A_true, Operator::PETSC_MATAIJ);
-        PetscLinearSolver solver(A_petsc);
-        solver.SetPrintLevel(prm.print_level);
-        solver.Mult(B, X);
+        int iterations = 0;
+        bool converged = true;
+        double final_norm = 0.0, seconds = 0.0;
+        const int true_size = fespace.TrueVSize();
+        const bool all_essential = (ess_tdof_list.Size() == true_size);
+        if (!all_essential) {
+            HypreParMatrix *A_true = Ah.As<HypreParMatrix>();
+            MFEM_VERIFY(A_true != nullptr, "Expected HypreParMatrix from FormLinearSystem.");
+
+            PetscParMatrix A_petsc(MPI_COMM_WORLD, A_true, Operator::PETSC_MATAIJ);
+            PetscLinearSolver solver(A_petsc);
+            solver.SetPrintLevel(prm.print_level);
+            solver.Mult(B, X);
+            iterations = solver.GetNumIterations();
+            final_norm = solver.GetFinalNorm();
+            seconds = solver.GetSolveSeconds();
+            converged = solver.GetConverged();
+            MFEM_VERIFY(solver.GetConverged(), "PETSc solver did not converge. Iterations="
+                                                   << solver.GetNumIterations() << ", residual=" << solver.GetFinalNorm());
+        }
 
         a.RecoverFEMSolution(X, b, u);
 
         const int order_quad = std::max(2, 2 * prm.order + 3);
-        const IntegrationRule *irs[Geometry::NumGeom] = {};
-        for (int g = 0; g < Geometry::NumGeom; ++g) irs[g] = &IntRules.Get(g, order_quad);
-        const double abs_l2 = u.ComputeL2Error(exact, irs);
-        const double exact_l2 = ComputeGlobalLpNorm(2, exact, mesh, irs);
+        const IntegrationRule *irs[Geometry::NumGeom];
+        for (int g = 0; g < Geometry::NumGeom; g++) irs[g] = &IntRules.Get(g, order_quad);
 
-        std::printf("dofs %d\niterations %d\nconverged %d\nfinal_norm %.17g\nl2_abs %.17g\nl2_rel %.17g\n"
-                    "solve_seconds %.6g\n",
-                    fespace.GetTrueVSize(), solver.GetNumIterations(), solver.GetConverged() ? 1 : 0,
-                    solver.GetFinalNorm(), abs_l2, exact_l2 > 1e-14 ? abs_l2 / exact_l2 : 0.0,
-                    solver.GetSolveSeconds());
-        if (!solver.GetConverged()) {
-            std::fprintf(stderr, "solver did not converge: iterations=%d residual=%g\n",
-                         solver.GetNumIterations(), solver.GetFinalNorm());
-            return 3;
-        }
-        MFEMFinalizePetsc();
-        return 0;
-    } catch (const std::exception &e) {
-        std::fprintf(stderr, "error: %s\n", e.what());
-        return 3;
+        const double abs_l2 = u.ComputeL2Error(exact_coeff, irs);
+        const double exact_l2 = ComputeGlobalLpNorm(2, exact_coeff, *pmesh, irs);
+        const double rel_l2 = (exact_l2 > 1.0e-14) ? abs_l2 / exact_l2 : 0.0;
+
+        if (myid == 0)
+            std::printf("dofs %lld\nranks %d\niterations %d\nconverged %d\nfinal_norm %.17g\nl2_abs %.17g\n"
+                        "l2_rel %.17g\nsolve_seconds %.6g\n",
+                        (long long)global_true_dofs, Mpi::WorldSize(), iterations, converged ? 1 : 0, final_norm,
+                        abs_l2, rel_l2, seconds);
+    } catch (const exception &e) {
+        if (myid == 0) cerr << "Error: " << e.what() << endl;
+        exit_code = 3;
     }
+
+    MFEMFinalizePetsc();
+    return exit_code;
 }
