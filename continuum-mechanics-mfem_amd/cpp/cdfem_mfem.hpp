@@ -1698,14 +1698,16 @@ private:
             (*this)[i] = q.Eval(T, ip);
         }
     }
-    // simplices: collapsed Gauss with n = p + 3 points per direction (exact to degree 2p + 6 - dim
-    // >= the driver's max(2, 2p + 3) in 2D), the product's nodal basis
-    double L2Simplex(Coefficient *exact, Coefficient *weight, bool exact_only) const
+    // simplices: MFEM's rule IntRules.Get(TRIANGLE / TETRAHEDRON, order), the order of irs[geom]
+    // or max(2, 2p + 3) (cdfem_simplex_rule_order), with the product's nodal basis
+    double L2Simplex(Coefficient *exact, Coefficient *weight, const IntegrationRule *irs[], bool exact_only) const
     {
         const int dim = fes_->GetMesh()->Dimension(), p = fes_->GetOrder(), nd = fes_->NumElementDofs();
-        const int nq = cdfem_simplex_rule(dim, p + 3, nullptr, nullptr);
+        const int geom = dim == 3 ? Geometry::TETRAHEDRON : Geometry::TRIANGLE;
+        const int order = (irs && irs[geom]) ? irs[geom]->GetOrder() : std::max(2, 2 * p + 3);
+        const int nq = cdfem_simplex_rule_order(dim, order, nullptr, nullptr);
         std::vector<double> xi((size_t)nq * dim), w(nq), phi((size_t)nq * nd);
-        cdfem_simplex_rule(dim, p + 3, xi.data(), w.data());
+        cdfem_simplex_rule_order(dim, order, xi.data(), w.data());
         check(cdfem_simplex_basis(dim, p, nq, xi.data(), phi.data(), nullptr), nullptr, "cdfem_simplex_basis");
         const std::vector<double> &V = fes_->ElementVertices();
         const std::vector<int32_t> &D = fes_->ElementDofs();
@@ -1742,7 +1744,7 @@ private:
     // this rank's sum of squares (the callers all-reduce it)
     double L2(Coefficient *exact, Coefficient *weight, const IntegrationRule *irs[], bool exact_only) const
     {
-        if (fes_->Simplex()) return L2Simplex(exact, weight, exact_only);
+        if (fes_->Simplex()) return L2Simplex(exact, weight, irs, exact_only);
         const int dim = fes_->GetMesh()->Dimension(), p = fes_->GetOrder(), d1 = p + 1;
         const int geom = dim == 3 ? Geometry::CUBE : Geometry::SQUARE;
         const int order = (irs && irs[geom]) ? irs[geom]->GetOrder() : std::max(2, 2 * p + 3);
@@ -1814,7 +1816,7 @@ using ParGridFunction = GridFunction;
 inline double ComputeGlobalLpNorm(double p, Coefficient &exact, Mesh &mesh, const IntegrationRule *irs[])
 {
     if (p != 2.0) throw std::invalid_argument("ComputeGlobalLpNorm: only p = 2");
-    H1_FECollection fec(mesh.Cartesian() ? 1 : 2, mesh.Dimension());  // simplex rule n = p + 3 >= 5
+    H1_FECollection fec(1, mesh.Dimension());  // exact_only: the basis is not evaluated
     FiniteElementSpace fes(&mesh, &fec);
     GridFunction z(&fes);
     return z.ComputeL2Norm(exact, irs);

@@ -10,10 +10,13 @@
 // PetscParMatrix(MPI_COMM_WORLD, A, PETSC_MATAIJ), PetscLinearSolver, RecoverFEMSolution,
 // ComputeL2Error / ComputeGlobalLpNorm.  What differs: configuration from the command line instead
 // of YAML (out of scope), a generated box when no mesh file is given, the 3D extension of
-// the MMS (sin(l pi z) factor), and no ParaView / CSV output.
+// the MMS (sin(l pi z) factor), and no ParaView / CSV output.  -mms radial runs the
+// circle variant instead (linear_convection_diffusion_2D_circle.cpp: u = (r^2-1) cos 2 pi r on the
+// unit disk, ValidateUnitCircleMesh, :122-215).
 //
 //   mpirun -np N convection_diffusion [-d dim] [-n elems | -mesh file.msh] [-p order] [-rs levels]
-//       [-rp levels] [-k kappa] [-s reaction] [-c cx,cy,cz] [-m n,m,l] [-opts petsc.opts] [-pl level]
+//       [-rp levels] [-k kappa] [-s reaction] [-c cx,cy,cz] [-m n,m,l] [-mms sin|radial]
+//       [-opts petsc.opts] [-pl level]
 // Output (rank 0, stdout, one "key value" per line): dofs, ranks, iterations, converged, final_norm,
 // l2_abs, l2_rel, solve_seconds.  Exit code 3 on error (as the reference drivers, :435-442).
 #include <cmath>
@@ -44,8 +47,66 @@ struct Params {
     int dim = 2, n = 16, order = 2, rs = 0, rp = 0, print_level = 0;
     double kappa = 0.1, reaction = 1.0, c[3] = {1.0, -2.0, 0.5};
     int modes[3] = {3, 3, 3};
-    string opts = "Input/petsc.opts", mesh, cstr, mstr;
+    string opts = "Input/petsc.opts", mesh, cstr, mstr, mms = "sin";
 };
+
+// the circle variant's radial MMS, linear_convection_diffusion_2D_circle.cpp:140-215:
+// u = (r^2 - 1) cos(2 pi r), f = -kappa Lap u + c . grad u + s u with the r -> 0 limits
+constexpr double kAlpha = 2.0 * M_PI;
+constexpr double kSmallR = 1.0e-12;
+double ExactU(double r) { return (r * r - 1.0) * std::cos(kAlpha * r); }
+double ExactU_r(double r) { return 2.0 * r * std::cos(kAlpha * r) - kAlpha * (r * r - 1.0) * std::sin(kAlpha * r); }
+double ExactU_rr(double r)
+{
+    return 2.0 * std::cos(kAlpha * r) - 4.0 * kAlpha * r * std::sin(kAlpha * r) -
+           kAlpha * kAlpha * (r * r - 1.0) * std::cos(kAlpha * r);
+}
+double ExactLaplacian(double r) { return r > kSmallR ? ExactU_rr(r) + ExactU_r(r) / r : 2.0 * (2.0 + kAlpha * kAlpha); }
+
+class RadialExactCoefficient : public Coefficient {
+public:
+    real_t Eval(ElementTransformation &T, const IntegrationPoint &ip) override
+    {
+        Vector x;
+        T.Transform(ip, x);
+        return ExactU(std::sqrt(x[0] * x[0] + x[1] * x[1]));
+    }
+};
+
+class RadialForcingCoefficient : public Coefficient {
+public:
+    explicit RadialForcingCoefficient(const Params &p) : p_(p) {}
+    real_t Eval(ElementTransformation &T, const IntegrationPoint &ip) override
+    {
+        Vector x;
+        T.Transform(ip, x);
+        const double r = std::sqrt(x[0] * x[0] + x[1] * x[1]);
+        double ux = 0.0, uy = 0.0;
+        if (r > kSmallR) {
+            const double radial_scale = ExactU_r(r) / r;
+            ux = radial_scale * x[0];
+            uy = radial_scale * x[1];
+        }
+        return -p_.kappa * ExactLaplacian(r) + p_.c[0] * ux + p_.c[1] * uy + p_.reaction * ExactU(r);
+    }
+
+private:
+    const Params &p_;
+};
+
+// _circle.cpp:122-138
+void ValidateUnitCircleMesh(const ParMesh &pmesh, const double tol)
+{
+    double local_rmax = 0.0;
+    for (int i = 0; i < pmesh.GetNV(); i++) {
+        const double *v = pmesh.GetVertex(i);
+        local_rmax = std::max(local_rmax, std::sqrt(v[0] * v[0] + v[1] * v[1]));
+    }
+    double global_rmax = 0.0;
+    MPI_Allreduce(&local_rmax, &global_rmax, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    MFEM_VERIFY(std::abs(global_rmax - 1.0) <= tol,
+                "Expected unit-circle mesh (max radius near 1). Found max radius " << global_rmax << ".");
+}
 
 // u = sin(n pi x) sin(m pi y) [sin(l pi z)]  (:159-175)
 class ExactSolutionCoefficient : public Coefficient {
@@ -116,6 +177,8 @@ int main(int argc, char *argv[])
     args.AddOption(&prm.reaction, "-s", "--reaction", "Reaction coefficient.");
     args.AddOption(&prm.cstr, "-c", "--convection", "Velocity cx,cy[,cz].");
     args.AddOption(&prm.mstr, "-m", "--modes", "MMS modes n,m[,l].");
+    args.AddOption(&prm.mms, "-mms", "--mms", "Manufactured solution: sin (the square driver) or radial "
+                                              "(the circle driver, 2D unit disk).");
     args.AddOption(&prm.opts, "-opts", "--petsc-options", "PETSc options file.");
     args.AddOption(&prm.print_level, "-pl", "--print-level", "Solver print level.");
     args.Parse();
@@ -135,6 +198,9 @@ int main(int argc, char *argv[])
     int exit_code = 0;
     try {
         if (prm.dim != 2 && prm.dim != 3) throw invalid_argument("-d must be 2 or 3");
+        const bool radial = prm.mms == "radial";
+        if (!radial && prm.mms != "sin") throw invalid_argument("-mms must be sin or radial");
+        if (radial && prm.dim != 2) throw invalid_argument("-mms radial is the 2D circle problem");
         Device device("cpu");
         if (myid == 0 && prm.print_level > 0) device.Print(cerr);
 
@@ -149,6 +215,7 @@ int main(int argc, char *argv[])
         for (int l = 0; l < prm.rp; l++) pmesh->UniformRefinement();
 
         MFEM_VERIFY(pmesh->bdr_attributes.Size() > 0, "Mesh must define boundary attributes.");
+        if (radial) ValidateUnitCircleMesh(*pmesh, 1.0e-8);
 
         H1_FECollection fec(prm.order, prm.dim);
         ParFiniteElementSpace fespace(pmesh.get(), &fec);
@@ -159,8 +226,12 @@ int main(int argc, char *argv[])
         Array<int> ess_tdof_list;
         fespace.GetEssentialTrueDofs(ess_bdr, ess_tdof_list);
 
-        ExactSolutionCoefficient exact_coeff(prm.dim, prm.modes);
-        ForcingCoefficient forcing_coeff(prm);
+        ExactSolutionCoefficient sin_exact(prm.dim, prm.modes);
+        ForcingCoefficient sin_forcing(prm);
+        RadialExactCoefficient radial_exact;
+        RadialForcingCoefficient radial_forcing(prm);
+        Coefficient &exact_coeff = radial ? static_cast<Coefficient &>(radial_exact) : sin_exact;
+        Coefficient &forcing_coeff = radial ? static_cast<Coefficient &>(radial_forcing) : sin_forcing;
         Vector c_vec(prm.dim);
         for (int i = 0; i < prm.dim; ++i) c_vec[i] = prm.c[i];
         VectorConstantCoefficient convection_coeff(c_vec);

@@ -155,6 +155,46 @@ int simplex_rule(int dim, int n, std::vector<double> &xi, std::vector<double> &w
     return nq;
 }
 
+// MFEM's tabulated simplex rules (IntRules.Get(TRIANGLE / TETRAHEDRON, order), intrules.cpp),
+// generated and verified by tools/simplex_rules.py: exact to their degree in double precision.
+#include "simplex_rules.inc"
+
+int mfem_simplex_rule(int dim, int order, std::vector<double> &xi, std::vector<double> &w)
+{
+    static const double *tri[] = {k_tri1, k_tri1, k_tri2, k_tri3, k_tri4, k_tri5, k_tri6, k_tri7, k_tri8, k_tri9};
+    static const int ntri[] = {1, 1, 3, 4, 6, 7, 12, 12, 16, 19};
+    static const double *tet[] = {k_tet1, k_tet1, k_tet2, k_tet3, k_tet4, k_tet5, k_tet6};
+    static const int ntet[] = {1, 1, 4, 5, 11, 14, 24};
+    if (order < 0) order = 0;
+    const double *t = nullptr;
+    int n = 0;
+    if (dim == 2 && order <= 9) {
+        t = tri[order];
+        n = ntri[order];
+    } else if (dim == 3 && order <= 6) {
+        t = tet[order];
+        n = ntet[order];
+    } else {
+        return 0;
+    }
+    xi.assign((size_t)n * dim, 0.0);
+    w.assign(n, 0.0);
+    for (int q = 0; q < n; ++q) {
+        for (int k = 0; k < dim; ++k) xi[(size_t)q * dim + k] = t[q * (dim + 1) + k];
+        w[q] = t[q * (dim + 1) + dim];
+    }
+    return n;
+}
+
+int simplex_rule_for_order(int dim, int order, std::vector<double> &xi, std::vector<double> &w)
+{
+    const int n = mfem_simplex_rule(dim, order, xi, w);
+    if (n > 0) return n;
+    // beyond MFEM's tables here: collapsed Gauss exact to the order (n points per direction, exact
+    // to degree 2n - 1 in the first direction after the Duffy factor)
+    return simplex_rule(dim, (order + dim) / 2 + 1, xi, w);
+}
+
 int simplex_ndofs(int dim, int p)
 {
     if (p == 1) return dim + 1;

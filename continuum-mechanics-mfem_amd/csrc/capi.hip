@@ -1111,9 +1111,9 @@ int cdfem_mesh_upload_simplex(cdfem_ctx *c, int dim, int order, int ne, const do
             }
             tab[(size_t)nq * nd * (dim + 1) + q] = w[q];
         }
-        // linear-form rule (n = p + 3) tables
+        // linear-form rule: DomainLFIntegrator's default order 2p, MFEM's tabulated simplex rule
         std::vector<double> wl;
-        c->nq_lf = simplex_rule(dim, order + 3, c->h_sxi_lf, wl);
+        c->nq_lf = simplex_rule_for_order(dim, 2 * order, c->h_sxi_lf, wl);
         std::vector<double> tab_lf((size_t)c->nq_lf * (nd + 1));
         for (int q = 0; q < c->nq_lf; ++q) {
             double phi[10], dphi[30];

@@ -41,6 +41,10 @@ void gll_nodes(int p, double *x);
 void gauss_legendre(int n, double *x, double *w);
 // simplices (basis.cpp)
 int simplex_rule(int dim, int n, std::vector<double> &xi, std::vector<double> &w);
+// MFEM's tabulated triangle (order <= 9) / tetrahedron (order <= 6) rules; 0 when not tabulated
+int mfem_simplex_rule(int dim, int order, std::vector<double> &xi, std::vector<double> &w);
+// the rule IntRules.Get(simplex, order) returns: MFEM's table, else collapsed Gauss of that order
+int simplex_rule_for_order(int dim, int order, std::vector<double> &xi, std::vector<double> &w);
 int simplex_ndofs(int dim, int p);
 void simplex_basis(int dim, int p, const double *xi, double *phi, double *dphi);
 extern const int kSimplexEdge[6][2];

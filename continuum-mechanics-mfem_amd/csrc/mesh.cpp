@@ -582,6 +582,16 @@ int cdfem_simplex_space(int dim, int64_t nvert, const double *vxyz, int ne, cons
 
 // host helpers: the simplex rule and nodal basis the kernels use (for host-side functionals such as
 // ComputeL2Error, linear_convection_diffusion_2D.cpp:383-392)
+int cdfem_simplex_rule_order(int dim, int order, double *xi, double *w)
+{
+    if (dim != 2 && dim != 3) return -1;
+    std::vector<double> x, ww;
+    const int nq = cdfem::simplex_rule_for_order(dim, order, x, ww);
+    if (xi) std::copy(x.begin(), x.end(), xi);
+    if (w) std::copy(ww.begin(), ww.end(), w);
+    return nq;
+}
+
 int cdfem_simplex_rule(int dim, int n, double *xi, double *w)
 {
     if ((dim != 2 && dim != 3) || n < 1 || n > 16) return -CDFEM_ERR_ARG;

@@ -135,7 +135,9 @@ int cdfem_pa_setup_form(cdfem_ctx *ctx, const cdfem_form_coeffs *form);
  * ne*(dim+1)*dim, elem_dofs ne*nd with nd = dim+1 (P1) / (dim+1)(dim+2)/2 (P2) / 10 (P3 triangle),
  * local order: vertices, then edge nodes along a->b for edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3)
  * [2D: (0,1),(0,2),(1,2)], then the P3 centroid; det J > 0 required.  cdfem_lf_assemble works on
- * simplex meshes with f sampled at the CDFEM_RULE_LINEARFORM points (collapsed Gauss, n = p + 3).
+ * simplex meshes with f sampled at the CDFEM_RULE_LINEARFORM points (MFEM's tabulated rule of order
+ * 2p, cdfem_simplex_rule_order).  The operator rule is collapsed Gauss with n = p + 2 (exact for the
+ * constant-coefficient integrands; see DESIGN.md §1 for variable coefficients).
  * cdfem_fa_setup: same coefficients as cdfem_pa_setup (per-point arrays on the OPERATOR rule);
  * assembles A (CSR, columns sorted) and the eliminated matrix of FormLinearSystem on the GPU.
  * Afterwards cdfem_pa_mult / cdfem_pa_diagonal / cdfem_form_linear_system / cdfem_solve run on the
@@ -346,6 +348,11 @@ int cdfem_simplex_space(int dim, int64_t nvert, const double *vxyz, int ne, cons
  * query it) and the nodal simplex basis phi [npts][nd], dphi [npts][nd][dim] in the local dof
  * order above — for host-side functionals (ComputeL2Error, :383-392).                         */
 int cdfem_simplex_rule(int dim, int n, double *xi, double *w);
+/* The rule IntRules.Get(TRIANGLE / TETRAHEDRON, order) returns in MFEM: its tabulated symmetric rules
+ * (triangles order <= 9, tetrahedra order <= 6; tools/simplex_rules.py), else a collapsed-Gauss rule
+ * exact to that order.  Returns the point count (xi / w may be NULL to query it).  The linear-form
+ * rule of cdfem_mesh_upload_simplex is this rule at order 2p (DomainLFIntegrator's default).     */
+int cdfem_simplex_rule_order(int dim, int order, double *xi, double *w);
 int cdfem_simplex_basis(int dim, int order, int npts, const double *xi, double *phi, double *dphi);
 
 #ifdef __cplusplus

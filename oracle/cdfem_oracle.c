@@ -835,8 +835,27 @@ static int gmres_core(const orc_csr *A, const double *dinv, const orc_csr *ilu, 
  *      (linear_convection_diffusion_2D.cpp:159-215; z factor is the 3D extension)
  *   2: u = prod_d g(x_d), g(t) = sum_k a_k t^k, degree p: in the FE space -> exact Galerkin
  *   3: u = sin(t) cos(2(x-.5)^2 + 2(y-.5)^2), f = u_t - alpha Lap u   (diffusion_mms.cpp:136-178)
+ *   4: u = (r^2 - 1) cos(2 pi r) on the unit disk, f = -kappa Lap u + c.grad u + s u
+ *      (linear_convection_diffusion_2D_circle.cpp:140-215, including its r -> 0 limits)
  * prm: [kind, kappa, s, alpha, c0, c1, c2, n, m, l, t, p, dim]
  */
+#define ORC_RAD_ALPHA (2.0 * ORC_PI)   /* kAlpha, _circle.cpp:140 */
+#define ORC_RAD_SMALL 1.0e-12          /* kSmallR, _circle.cpp:141 */
+static double rad_u(double r) { return (r * r - 1.0) * cos(ORC_RAD_ALPHA * r); }
+static double rad_ur(double r)
+{
+    return 2.0 * r * cos(ORC_RAD_ALPHA * r) - ORC_RAD_ALPHA * (r * r - 1.0) * sin(ORC_RAD_ALPHA * r);
+}
+static double rad_urr(double r)
+{
+    return 2.0 * cos(ORC_RAD_ALPHA * r) - 4.0 * ORC_RAD_ALPHA * r * sin(ORC_RAD_ALPHA * r) -
+           ORC_RAD_ALPHA * ORC_RAD_ALPHA * (r * r - 1.0) * cos(ORC_RAD_ALPHA * r);
+}
+static double rad_lap(double r)
+{
+    if (r > ORC_RAD_SMALL) return rad_urr(r) + rad_ur(r) / r;
+    return 2.0 * (2.0 + ORC_RAD_ALPHA * ORC_RAD_ALPHA);  /* lim r->0, _circle.cpp:168-169 */
+}
 static void poly1d(int p, double t, double *g, double *dg, double *d2g)
 {
     /* fixed, non-symmetric coefficients: a_k = (k + 1) / (k + 2) * (-1)^k + 0.25 */
@@ -866,6 +885,7 @@ ORC_API double orc_mms_u(const double *prm, const double *x)
         double dx = x[0] - 0.5, dy = x[1] - 0.5;
         return sin(prm[10]) * cos(2.0 * dx * dx + 2.0 * dy * dy);
     }
+    if (kind == 4) return rad_u(sqrt(x[0] * x[0] + x[1] * x[1]));
     return 0.0;
 }
 
@@ -908,6 +928,16 @@ ORC_API double orc_mms_f(const double *prm, const double *x)
         double ut = cos(t) * cos(q);
         double lap = sin(t) * (-16.0 * r2 * cos(q) - 8.0 * sin(q));
         return ut - alpha * lap;
+    }
+    if (kind == 4) {  /* _circle.cpp:191-214 (alpha = 1 there) */
+        const double r = sqrt(x[0] * x[0] + x[1] * x[1]);
+        double ux = 0.0, uy = 0.0;
+        if (r > ORC_RAD_SMALL) {
+            const double sc = rad_ur(r) / r;
+            ux = sc * x[0];
+            uy = sc * x[1];
+        }
+        return -kappa * rad_lap(r) + alpha * (c[0] * ux + c[1] * uy) + s * rad_u(r);
     }
     return 0.0;
 }
@@ -1165,6 +1195,31 @@ ORC_API int orc_simplex_rule(int dim, int n, double *xi, double *w)
     return nq;
 }
 
+/* MFEM's tabulated simplex rules, IntRules.Get(TRIANGLE, order <= 9) / (TETRAHEDRON, order <= 6)
+ * [MFEM-ext intrules.cpp], as generated and verified by tools/simplex_rules.py (symmetric orbits with
+ * the published parameters, refined to double precision on the moment equations).  Beyond the
+ * tables: the collapsed rule exact to that order.  Returns the point count. */
+#include "simplex_rules.inc"
+
+ORC_API int orc_simplex_rule_order(int dim, int order, double *xi, double *w)
+{
+    static const double *tri[] = {k_tri1, k_tri1, k_tri2, k_tri3, k_tri4, k_tri5, k_tri6, k_tri7, k_tri8, k_tri9};
+    static const int ntri[] = {1, 1, 3, 4, 6, 7, 12, 12, 16, 19};
+    static const double *tet[] = {k_tet1, k_tet1, k_tet2, k_tet3, k_tet4, k_tet5, k_tet6};
+    static const int ntet[] = {1, 1, 4, 5, 11, 14, 24};
+    if (order < 0) order = 0;
+    const double *t = NULL;
+    int n = 0;
+    if (dim == 2 && order <= 9) { t = tri[order]; n = ntri[order]; }
+    else if (dim == 3 && order <= 6) { t = tet[order]; n = ntet[order]; }
+    else return orc_simplex_rule(dim, (order + dim) / 2 + 1, xi, w);
+    for (int q = 0; q < n; q++) {
+        for (int k = 0; k < dim; k++) xi[q * dim + k] = t[q * (dim + 1) + k];
+        w[q] = t[q * (dim + 1) + dim];
+    }
+    return n;
+}
+
 /* Reference basis at xi: phi[nd], dphi[nd][dim] (d/dxi_k), barycentric lambda_0 = 1 - sum xi.
  * Local order: vertices 0..dim, then (P2) edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3) [2D: (0,1),
  * (0,2),(1,2)]. */
@@ -1362,7 +1417,7 @@ ORC_API orc_csr *orc_fa_assemble_simplex(int dim, int p, int ne, const double *v
 }
 
 /* DomainLF b_i = int f phi_i and ||u_h - u||_L2 on affine simplices with the MMS data of
- * orc_mms_f / orc_mms_u; rules: collapsed Gauss with n = p + 3 (exact to degree 2p + 6 - dim). */
+ * orc_mms_f / orc_mms_u; rules: MFEM's simplex rules of order 2p (LF) and max(2, 2p + 3) (error). */
 static void simplex_point(int dim, const double *V, const double *xi, double *x, double *det)
 {
     double J[3][3] = {{0}}, A[3][3];
@@ -1381,9 +1436,10 @@ ORC_API void orc_lf_assemble_simplex(int dim, int p, int ne, const double *verts
                                      int64_t nl, const double *prm, double *b)
 {
     p3_init();
-    const int nd = orc_simplex_nd(dim, p), n1 = p + 3;
+    /* DomainLFIntegrator default order 2p on MFEM's simplex rule [MFEM-ext] */
+    const int nd = orc_simplex_nd(dim, p);
     double xi[7 * 7 * 7 * 3], wq[7 * 7 * 7];
-    const int nq = orc_simplex_rule(dim, n1, xi, wq);
+    const int nq = orc_simplex_rule_order(dim, 2 * p, xi, wq);
     double *be = (double *)malloc(sizeof(double) * (size_t)ne * nd);
     #pragma omp parallel for schedule(static)
     for (int e = 0; e < ne; e++) {
@@ -1406,9 +1462,10 @@ ORC_API double orc_l2_error_simplex(int dim, int p, int ne, const double *verts,
                                     const double *u, const double *prm)
 {
     p3_init();
-    const int nd = orc_simplex_nd(dim, p), n1 = p + 3;
+    /* the drivers' error rule IntRules.Get(g, max(2, 2p + 3)) (linear_convection_diffusion_2D.cpp:383-388) */
+    const int nd = orc_simplex_nd(dim, p);
     double xi[7 * 7 * 7 * 3], wq[7 * 7 * 7];
-    const int nq = orc_simplex_rule(dim, n1, xi, wq);
+    const int nq = orc_simplex_rule_order(dim, 2 * p + 3 > 2 ? 2 * p + 3 : 2, xi, wq);
     double err = 0.0;
     #pragma omp parallel for reduction(+ : err) schedule(static)
     for (int e = 0; e < ne; e++) {

@@ -80,6 +80,7 @@ def lib():
                                    C.c_double, C.c_double, dp, C.c_int, dp, dp]
         L.orc_simplex_nd.argtypes = [C.c_int, C.c_int]
         L.orc_simplex_rule.argtypes = [C.c_int, C.c_int, dp, dp]
+        L.orc_simplex_rule_order.argtypes = [C.c_int, C.c_int, dp, dp]
         L.orc_mesh_kuhn_sizes.argtypes = [C.c_int, C.c_int, C.c_int, ip, lp]
         L.orc_mesh_kuhn.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, dp, ip, ip]
         L.orc_fa_assemble_simplex.restype = C.c_void_p
@@ -213,6 +214,13 @@ def solve_mms_simplex(mesh, prm, kappa, s, c, alpha=1.0, tol=1e-10, atol=1e-12, 
     else:
         X, info = gmres(Ac, B, dinv=1.0 / Ac.diag(), rtol=tol, atol=atol, max_it=max_it)
     return X, info, l2_error_simplex(mesh, X, prm)
+
+
+def simplex_rule_order(dim, order):
+    """MFEM's IntRules.Get(simplex, order) (tabulated; collapsed Gauss beyond the tables)."""
+    xi, w = np.zeros(64 * dim), np.zeros(64)
+    nq = lib().orc_simplex_rule_order(dim, order, _d(xi), _d(w))
+    return xi[: nq * dim].reshape(nq, dim), w[:nq]
 
 
 def simplex_rule(dim, n):
@@ -364,7 +372,7 @@ def gmres_ilu(A: CSR, b, F: CSR, restart=30, rtol=1e-10, atol=1e-12, max_it=500)
     return x, dict(converged=bool(conv), iterations=it.value, final_norm=fn.value)
 
 
-MMS_SIN, MMS_POLY, MMS_DIFFUSION_T = 1, 2, 3
+MMS_SIN, MMS_POLY, MMS_DIFFUSION_T, MMS_RADIAL = 1, 2, 3, 4
 
 
 def mms_params(kind, dim, kappa=0.1, s=1.0, alpha=1.0, c=(1.0, -2.0, 0.5), modes=(3, 3, 3), t=0.0, p=1):

@@ -85,3 +85,80 @@ def read_triangles(path):
         else:
             i += 1
     return nodes, tris
+
+
+def write_circle(path, nr, perturb=0.15, seed=0, shift_ids=500):
+    """Unit disk as the reference's Mesh/unit_circle.geo describes it (centre (0,0), radius 1, one
+    boundary curve with physical tag 1, domain tag 1): nr concentric rings of 6k vertices, the outer
+    ring exactly on r = 1, annuli triangulated by merging the two rings by angle (6 nr^2 triangles).
+    Interior vertices are jittered; every fourth triangle is written clockwise."""
+    rng = np.random.default_rng(seed)
+    rings = [[(0.0, 0.0)]]
+    for k in range(1, nr + 1):
+        n = 6 * k
+        off = 0.5 * (k % 2) * 2 * np.pi / n
+        ring = []
+        for j in range(n):
+            a = off + 2 * np.pi * j / n
+            r = k / nr
+            if k < nr:
+                r += perturb / nr * rng.uniform(-0.5, 0.5)
+                a += perturb * np.pi / n * rng.uniform(-0.5, 0.5)
+            ring.append((float(r * np.cos(a)), float(r * np.sin(a))))
+        rings.append(ring)
+    ids, xy = [], []
+    for k, ring in enumerate(rings):
+        ids.append([])
+        for j, (x, y) in enumerate(ring):
+            nid = shift_ids + 2 * len(xy)
+            ids[k].append(nid)
+            xy.append((nid, x, y))
+
+    def ang(p):
+        return np.arctan2(p[1], p[0]) % (2 * np.pi)
+
+    tris = []
+    for j in range(6):  # fan around the centre
+        tris.append((ids[0][0], ids[1][j], ids[1][(j + 1) % 6]))
+    for k in range(2, nr + 1):
+        inner, outer = rings[k - 1], rings[k]
+        m, n = len(inner), len(outer)
+        ai = [ang(p) for p in inner]
+        bo = [ang(p) for p in outer]
+        # start both walks at the smallest angle of each ring
+        i0, j0 = int(np.argmin(ai)), int(np.argmin(bo))
+        a_un = [ai[(i0 + t) % m] + (2 * np.pi if (i0 + t) % m < i0 else 0.0) for t in range(m + 1)]
+        a_un[m] = a_un[0] + 2 * np.pi
+        b_un = [bo[(j0 + t) % n] + (2 * np.pi if (j0 + t) % n < j0 else 0.0) for t in range(n + 1)]
+        b_un[n] = b_un[0] + 2 * np.pi
+        i = j = 0
+        while i < m or j < n:
+            I, I1 = ids[k - 1][(i0 + i) % m], ids[k - 1][(i0 + i + 1) % m]
+            J, J1 = ids[k][(j0 + j) % n], ids[k][(j0 + j + 1) % n]
+            if j < n and (i == m or b_un[j + 1] <= a_un[i + 1]):
+                tris.append((I, J, J1))
+                j += 1
+            else:
+                tris.append((I, J, I1))
+                i += 1
+    els = []
+    outer_ids = ids[nr]
+    for j in range(len(outer_ids)):
+        els.append((1, 1, outer_ids[j], outer_ids[(j + 1) % len(outer_ids)]))
+    for t, tri in enumerate(tris):
+        if t % 4 == 3:
+            tri = (tri[0], tri[2], tri[1])
+        els.append((2, 1) + tuple(tri))
+    with open(path, "w") as f:
+        f.write("$MeshFormat\n2.2 0 8\n$EndMeshFormat\n")
+        f.write('$PhysicalNames\n2\n1 1 "boundary"\n2 1 "domain"\n$EndPhysicalNames\n')
+        f.write(f"$Nodes\n{len(xy)}\n")
+        for nid, x, y in xy:
+            f.write(f"{nid} {x!r} {y!r} 0\n")
+        f.write("$EndNodes\n")
+        f.write(f"$Elements\n{len(els)}\n")
+        for e, el in enumerate(els, start=1):
+            typ, tag, *nodes = el
+            f.write(f"{e} {typ} 2 {tag} {tag} " + " ".join(str(v) for v in nodes) + "\n")
+        f.write("$EndElements\n")
+    return {"n_nodes": len(xy), "n_tri": len(tris), "n_bdr_edges": len(outer_ids)}

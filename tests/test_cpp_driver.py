@@ -313,3 +313,54 @@ def test_diffusion_mms_mpi_matches_one_rank(tmp_path, kind):
     assert abs(par["gmres_iterations"] - one["gmres_iterations"]) <= 2 * one["steps"]
     assert abs(par["final_l2"] - one["final_l2"]) <= 1e-7 * one["final_l2"]
     assert abs(par["final_linf"] - one["final_linf"]) <= 1e-6 * one["final_linf"]
+
+
+CIRCLE_OPTS = ("-ksp_type gmres\n-ksp_rtol 1.0e-10\n-ksp_atol 1.0e-12\n-ksp_max_it 2000\n"
+               "-pc_type bjacobi\n-sub_ksp_type preonly\n-sub_pc_type ilu\n")   # Input/petsc_circle.opts
+
+
+def _oracle_mesh_of(m, order):
+    class OM:
+        pass
+    om = OM()
+    om.dim, om.p, om.ne, om.nl, om.verts, om.dofmap, om.ess = 2, order, m.ne, m.nl, m.verts, m.dofmap, m.ess
+    om.bdr = np.zeros(m.nl, dtype=np.int32)
+    om.bdr[m.ess] = 1
+    return om
+
+
+@pytest.mark.gpu
+def test_driver_circle_reference_configuration(exe, tmp_path):
+    """The circle variant's default run (Input/input_2d_circle.yaml: order 3, kappa 1, s 1, c (1,1),
+    Input/petsc_circle.opts: GMRES + block-Jacobi/ILU) with the radial MMS
+    (linear_convection_diffusion_2D_circle.cpp:140-215) on a synthetic gmsh unit disk, against the
+    oracle's restatement; then 2 MPI ranks (Jacobi, block-Jacobi ILU per rank is not provided) against
+    one rank."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import gmsh_synth
+    import cdfem
+    from oracle import oracle as O
+    msh = str(tmp_path / "unit_circle.msh")
+    gmsh_synth.write_circle(msh, 16, perturb=0.2, seed=3)
+    args = ["-d", "2", "-mesh", msh, "-p", "3", "-k", "1", "-s", "1", "-c", "1,1,0", "-mms", "radial"]
+    rc, out, err = _run(args, CIRCLE_OPTS, tmp_path)
+    assert rc == 0, err
+    m = cdfem.gmsh_mesh(msh, 3)
+    om = _oracle_mesh_of(m, 3)
+    prm = O.mms_params(O.MMS_RADIAL, 2, kappa=1.0, s=1.0, c=(1.0, 1.0), p=3)
+    _, info, l2 = O.solve_mms_simplex(om, prm, 1.0, 1.0, (1.0, 1.0), max_it=2000, pc="ilu")
+    assert int(out["dofs"]) == m.nl
+    assert out["converged"] == 1 and abs(out["iterations"] - info["iterations"]) <= 1
+    assert abs(out["l2_abs"] - l2) <= 1e-6 * l2
+    jac = CIRCLE_OPTS.replace("bjacobi", "jacobi")
+    rc1, one, err1 = _run(args, jac, tmp_path)
+    rc2, two, err2 = _run(args, jac, tmp_path, np_ranks=2)
+    assert rc1 == 0 and rc2 == 0, err1 + err2
+    assert abs(two["iterations"] - one["iterations"]) <= 2
+    assert abs(two["l2_abs"] - one["l2_abs"]) <= 1e-7 * one["l2_abs"]
+    # the circle check of the driver (ValidateUnitCircleMesh) rejects the unit square
+    sq = str(tmp_path / "sq.msh")
+    gmsh_synth.write_square(sq, 4)
+    rc, _, err = _run(["-d", "2", "-mesh", sq, "-p", "1", "-mms", "radial"], jac, tmp_path)
+    assert rc == 3 and "unit-circle" in err

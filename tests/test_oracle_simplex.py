@@ -10,6 +10,7 @@ There are no MFEM outputs to pin against (parity unpinned vs MFE
   * the product's Kuhn mesh generator (cdfem_kuhn_mesh, host code) reproduces the oracle's.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -169,3 +170,72 @@ def test_ilu0_gmres_converges_faster_than_jacobi():
     r = np.random.default_rng(4).uniform(-1, 1, m.nl)
     z = O.ilu_solve(F, r)
     assert np.abs(_ilu_lu(F) @ z - r).max() <= 1e-11 * np.abs(r).max()
+
+
+def test_radial_mms_on_synthetic_disk_converges():
+    """Circle variant MMS (linear_convection_diffusion_2D_circle.cpp:140-215) through the oracle on the
+    synthetic gmsh disk: the L2 error falls under refinement (P2 on a polygonal domain: the boundary
+    approximation limits the rate to about 2) and the forcing matches a finite-difference restatement."""
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.dirname(__file__))
+    import gmsh_synth
+    import cdfem
+    from oracle import oracle as O
+    errs = []
+    for nr in (6, 12):
+        path = f"/tmp/cdfem_disk_{nr}.msh"
+        gmsh_synth.write_circle(path, nr, perturb=0.0)
+        m = cdfem.gmsh_mesh(path, 2)
+
+        class OM:
+            pass
+        om = OM()
+        om.dim, om.p, om.ne, om.nl, om.verts, om.dofmap, om.ess = 2, 2, m.ne, m.nl, m.verts, m.dofmap, m.ess
+        om.bdr = np.zeros(m.nl, dtype=np.int32)
+        om.bdr[m.ess] = 1
+        prm = O.mms_params(O.MMS_RADIAL, 2, kappa=1.0, s=1.0, c=(1.0, 1.0), p=2)
+        _, info, l2 = O.solve_mms_simplex(om, prm, 1.0, 1.0, (1.0, 1.0), max_it=2000)
+        assert info["converged"]
+        errs.append(l2)
+    assert np.log2(errs[0] / errs[1]) >= 1.8, errs
+    # forcing = -Lap u + c.grad u + u, checked by central differences at a few points
+    prm = O.mms_params(O.MMS_RADIAL, 2, kappa=1.0, s=1.0, c=(1.0, 1.0), p=2)
+    pts = np.array([[0.3, 0.1], [-0.5, 0.4], [0.05, -0.7], [0.0, 0.0]])
+    h = 1e-4
+    for x in pts:
+        u = lambda p: O.mms_u(prm, np.array([p]))[0]  # noqa: E731
+        ex, ey = np.array([h, 0.0]), np.array([0.0, h])
+        lap = (u(x + ex) + u(x - ex) + u(x + ey) + u(x - ey) - 4 * u(x)) / h ** 2
+        gx, gy = (u(x + ex) - u(x - ex)) / (2 * h), (u(x + ey) - u(x - ey)) / (2 * h)
+        f = O.mms_f(prm, np.array([x]))[0]
+        assert abs(f - (-lap + gx + gy + u(x))) <= 1e-4 * max(1.0, abs(f))
+
+
+@pytest.mark.parametrize("dim,orders", [(2, range(0, 10)), (3, range(0, 7))])
+def test_mfem_simplex_rules_exact_and_shared(dim, orders):
+    """MFEM's tabulated simplex rules (tools/simplex_rules.py): the product's table
+    (cdfem_simplex_rule_order) equals the oracle's, has MFEM's point counts, positive-or-documented
+    weights, points inside the simplex, and integrates every monomial of the order exactly."""
+    import ctypes as C
+    import itertools
+    import cdfem
+    L = cdfem.lib()
+    L.cdfem_simplex_rule_order.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    counts = {2: [1, 1, 3, 4, 6, 7, 12, 12, 16, 19], 3: [1, 1, 4, 5, 11, 14, 24]}
+    for order in orders:
+        xo, wo = O.simplex_rule_order(dim, order)
+        n = L.cdfem_simplex_rule_order(dim, order, None, None)
+        xi, w = np.zeros(n * dim), np.zeros(n)
+        L.cdfem_simplex_rule_order(dim, order, xi.ctypes.data_as(C.POINTER(C.c_double)),
+                                   w.ctypes.data_as(C.POINTER(C.c_double)))
+        assert n == len(wo) == counts[dim][order]
+        np.testing.assert_array_equal(xi.reshape(n, dim), xo)
+        np.testing.assert_array_equal(w, wo)
+        assert (xo >= -1e-15).all() and (xo.sum(axis=1) <= 1 + 1e-15).all()
+        for tot in range(order + 1):
+            for e in itertools.product(range(tot + 1), repeat=dim):
+                if sum(e) != tot:
+                    continue
+                exact = math.prod(math.factorial(k) for k in e) / math.factorial(dim + tot)
+                assert abs(np.sum(wo * np.prod(xo ** np.array(e), axis=1)) - exact) <= 1e-15
