@@ -57,18 +57,19 @@ def parse():
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--path", choices=["brick", "generic"], default=None,
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "c5w"], default="c2",
                     help="c2: 64^3 hex p=2 PA + CG (BASELINE metric config; N>1: weak scaling, a 64^3 slab "
                          "per rank); c3: 128^3 hex p=4 PA + CG (configs[2]); c4: Kuhn 55^3 x 6 tets P2, FA CSR "
                          "+ GMRES(30)/Jacobi (configs[3]); c5: 256^3 hex p=2 PA + CG split into N z-slabs "
-                         "(configs[4] at N=8: 256 x 256 x 32 per rank)")
+                         "(configs[4] at N=8: 256 x 256 x 32 per rank); c5w: SURVEY 8e's weak series, a "
+                         "256 x 256 x 32 slab per rank (N=8: the C5 mesh)")
     ap.add_argument("--tet-n", type=int, default=55, help="c4: cubes per direction (6 tets each)")
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N>1 data-path communicator: rccl (production, one GPU per rank) or host "
                          "(gloo callbacks; rehearses the N>1 flow with several ranks on one GPU)")
     a = ap.parse_args()
     c3 = a.config == "c3"
-    a.n = a.n or (128 if c3 else 256 if a.config == "c5" else 64)
+    a.n = a.n or (128 if c3 else 256 if a.config in ("c5", "c5w") else 64)
     a.order = a.order or (4 if c3 else 2)
     a.cg_iters = a.cg_iters or (20 if c3 else 100)
     a.path = a.path or ("brick" if a.order <= 2 else "generic")
@@ -303,6 +304,9 @@ def main():
         if n % world:
             raise SystemExit(f"c5: {n} element layers do not split over {world} ranks")
         nzr, nz = n // world, n
+    elif args.config == "c5w":
+        # SURVEY 8e weak series: an n x n x n/8 slab per rank (256 x 256 x 32), N = 8 is C5's 256^3
+        nzr, nz = n // 8, (n // 8) * world
     else:
         # weak scaling: rank r owns elements iz in [r n, (r+1) n) of an n x n x (world n) mesh
         nzr, nz = n, n * world
@@ -502,6 +506,7 @@ def main():
                        "dofs": total_dofs, "elements": n * n * nz, "cg_iters_per_step": args.cg_iters,
                        "parallelism": f"slab{world}" if world > 1 else "single", "path": args.path,
                        "series": "strong: fixed n^3 split into z-slabs" if args.config == "c5"
+                                 else "weak: an n x n x n/8 slab per rank (SURVEY 8e)" if args.config == "c5w"
                                  else "weak: an n^3 slab per rank",
                        **({"comm": args.comm, "comm_lib": comm_lib} if world > 1 else {})},
             "roofline": roof, "cpu_baseline": cpu,
