@@ -96,6 +96,8 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_stab); dfree(c->d_stab_lf); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);
     dfree(c->d_cpos); dfree(c->d_vals); dfree(c->d_vals_c); dfree(c->d_Ee);
     dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_sdel); dfree(c->d_svals);
+    dfree(c->d_rperm); dfree(c->d_pv[0]); dfree(c->d_pv[1]); dfree(c->d_dinv_p);
+    c->d_rperm = nullptr; c->d_pv[0] = c->d_pv[1] = nullptr; c->d_dinv_p = nullptr;
     dfree(c->d_svals_c);
     ilu_free(c);
     partition_free(c);
@@ -314,6 +316,16 @@ void ensure_dinv(cdfem_ctx *c)
     c->dinv_ready = true;
 }
 
+// the Jacobi scale in the order the running solve uses (mesh order, or the permuted SpMV order)
+const double *solver_dinv(cdfem_ctx *c)
+{
+    ensure_dinv(c);
+    if (!c->perm_space) return c->d_dinv;
+    if (!c->d_dinv_p) c->d_dinv_p = dalloc<double>(c->nl);
+    HIPCHK(launch_perm(c, true, c->d_dinv, c->d_dinv_p));
+    return c->d_dinv_p;
+}
+
 // brick-path CG (MFEM CGSolver arithmetic): per iteration k_brick_cg (direction + apply + den
 // partials) -> den finalizer -> k_cg_update_faces (q assembly + x, r update + betanom partials) ->
 // betanom finalizer.  The search direction alternates between two buffers.
@@ -418,11 +430,7 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
               cdfem_solver_result &res)
 {
     double *x = c->d_w[2], *r = c->d_w[3], *z = c->d_w[4], *d = c->d_w[5];
-    const double *dinv = nullptr;
-    if (p.pc == CDFEM_PC_JACOBI) {
-        ensure_dinv(c);
-        dinv = c->d_dinv;
-    }
+    const double *dinv = p.pc == CDFEM_PC_JACOBI ? solver_dinv(c) : nullptr;
     const int check = p.check_every > 0 ? p.check_every : 16;
     const bool mr = multi_rank(c);
     double *red = c->d_state->red;  // device scalars awaiting the all-reduce (multi-rank)
@@ -530,8 +538,7 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     const double *dinv = nullptr;
     const bool ilu = p.pc == CDFEM_PC_ILU;
     if (p.pc == CDFEM_PC_JACOBI) {
-        ensure_dinv(c);
-        dinv = c->d_dinv;
+        dinv = solver_dinv(c);
     } else if (ilu) {
         if (!c->fa_ready) throw UnsupportedError("ILU(0) needs an assembled operator (cdfem_fa_setup)");
         if (multi_rank(c)) throw UnsupportedError("ILU(0) on a multi-rank partition");
@@ -1163,7 +1170,8 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
         const unsigned kinds = f->kinds;
         if (c->geom != 1) throw UnsupportedError("full assembly is implemented for simplex meshes");
         if (!c->d_rowptr) {  // CSR pattern + contribution lists: once per mesh
-            FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl);
+            // a multi-rank partition keeps the mesh order (its shared-dof exchange indexes L-vectors)
+            FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl, multi_rank(c) ? 0 : c->sell_mode);
             c->nnz = P.nnz;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
             c->d_cols = dalloc<int32_t>(P.cols.size());
@@ -1180,7 +1188,7 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             HIPCHK(hipMemcpyAsync(c->d_coff, P.coff.data(), P.coff.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_cpos, P.cpos.data(), P.cpos.size() * 4, hipMemcpyHostToDevice, c->stream));
             c->nslices = (int64_t)P.sptr.size() - 1;
-            if ((c->nslices + 3) / 4 > kSpmvMaxBlocks) throw UnsupportedError("matrix too large for the SpMV grid");
+            if ((c->nslices + 3) / 4 + 8 > kSpmvMaxBlocks) throw UnsupportedError("matrix too large for the SpMV grid");
             c->nstored = P.sptr.back();
             c->d_sptr = dalloc<int32_t>(P.sptr.size());
             c->d_srows = dalloc<int32_t>(P.srows.size());
@@ -1192,6 +1200,11 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             HIPCHK(hipMemcpyAsync(c->d_srows, P.srows.data(), P.srows.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_scols, P.scols.data(), P.scols.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_smap, P.smap.data(), P.smap.size() * 4, hipMemcpyHostToDevice, c->stream));
+            if (!P.perm.empty()) {
+                c->d_rperm = dalloc<int32_t>(P.perm.size());
+                HIPCHK(hipMemcpyAsync(c->d_rperm, P.perm.data(), P.perm.size() * 4, hipMemcpyHostToDevice, c->stream));
+                for (auto &v : c->d_pv) v = dalloc<double>(c->nl);
+            }
             if (!P.sdel.empty()) {
                 c->d_sdel = dalloc<int16_t>(P.sdel.size());
                 HIPCHK(hipMemcpyAsync(c->d_sdel, P.sdel.data(), P.sdel.size() * 2, hipMemcpyHostToDevice, c->stream));
@@ -1321,17 +1334,36 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
         if (p->pc == CDFEM_PC_ILU && p->method != CDFEM_GMRES)
             throw UnsupportedError("ILU(0) preconditions GMRES (a nonsymmetric preconditioner for CG)");
         *res = cdfem_solver_result{};
+        if (p->method != CDFEM_CG && p->method != CDFEM_GMRES) throw ArgError("unknown method");
         const double *dB = dev_in(c, B, where, c->d_w[6], c->nl);
         double *dX = where == CDFEM_DEVICE ? X : c->d_w[1];
+        // permuted SpMV layout (sell_plan.cpp): the Krylov iteration runs in the SpMV's order, B in
+        // and X out are permuted once per solve.  ILU(0) factors the matrix in mesh order (PETSc's
+        // natural ordering), so it keeps the mesh order and permutes around each apply instead.
+        const bool pspace = c->fa_ready && c->d_rperm && !multi_rank(c) && p->pc != CDFEM_PC_ILU;
+        struct SpaceGuard {
+            cdfem_ctx *c;
+            ~SpaceGuard() { c->perm_space = false; }
+        } guard{c};
+        const double *dBs = dB;
+        double *dXs = dX;
+        if (pspace) {
+            HIPCHK(launch_perm(c, true, dB, c->d_pv[0]));
+            dBs = c->d_pv[0];
+            dXs = c->d_pv[1];
+            c->perm_space = true;
+        }
         if (p->method == CDFEM_CG) {
             if (use_brick(c))
-                solve_cg_brick(c, *p, dB, dX, *res);
+                solve_cg_brick(c, *p, dBs, dXs, *res);
             else
-                solve_cg(c, *p, dB, dX, *res);
-        } else if (p->method == CDFEM_GMRES) {
-            solve_gmres(c, *p, dB, dX, *res);
+                solve_cg(c, *p, dBs, dXs, *res);
         } else {
-            throw ArgError("unknown method");
+            solve_gmres(c, *p, dBs, dXs, *res);
+        }
+        if (pspace) {
+            c->perm_space = false;
+            HIPCHK(launch_perm(c, false, dXs, dX));
         }
         dev_out(c, X, where, dX, c->nl);
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -1409,6 +1441,15 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "cg_fused") {
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;
+        } else if (k == "sell_order") {  // read when the FA pattern is built (once per mesh)
+            if (value < 0 || value > 3) throw ArgError("sell_order must be 0 (legacy), 1 (natural), 2 (RCM) or 3 (auto)");
+            c->sell_mode = value;
+        } else if (k == "spmv_variant") {
+            if (value < 0 || value > 3) throw ArgError("spmv_variant must be 0..3");
+            c->spmv_variant = value;
+        } else if (k == "spmv_xcd") {
+            if (value < 0 || value > 1) throw ArgError("spmv_xcd must be 0 or 1");
+            c->spmv_xcd = value;
         } else if (k == "spmv_index16") {
             if (value < 0 || value > 1) throw ArgError("spmv_index16 must be 0 or 1");
             c->spmv_index16 = value;

@@ -201,6 +201,13 @@ struct cdfem_ctx {
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
+    int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
+    int spmv_variant = 0;               // set_option "spmv_variant": SpMV inner loop (A/B: 0 U4, 1 U4 pipelined, 2 U8 pipelined, 3 U8)
+    int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD
+    int32_t *d_rperm = nullptr;         // permuted SpMV: new row -> mesh row (null: legacy layout)
+    double *d_pv[2] = {};               // permuted-space scratch (apply in mesh order; solve B / X)
+    bool perm_space = false;            // inside a solve that runs in the permuted order
+    double *d_dinv_p = nullptr;         // the Jacobi scale in permuted order (during such a solve)
     double *d_svals = nullptr, *d_svals_c = nullptr;
     cdfem::IluState ilu;                // ILU(0) of the eliminated matrix (GMRES pc = ILU)
 
@@ -339,8 +346,18 @@ struct FaPattern {
     std::vector<int32_t> scols;  // [stored] column, slice-major then entry-major then lane
     std::vector<int32_t> smap;   // [stored] CSR index of the stored entry, -1 = padding
     std::vector<int16_t> sdel;   // [stored] column - row when every |column - row| < 2^15, else empty
+    std::vector<int32_t> perm;   // permuted SpMV (sell_plan.cpp): new row -> mesh row; empty = legacy
 };
-FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl);
+// SpMV row order (sell_plan.cpp): mode 0 legacy, 1 natural + windows, 2 RCM + windows, 3 auto
+struct SellPlan {
+    int mode = 0, base = 0;
+    int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0;
+    std::vector<int32_t> perm;   // new -> old (empty: legacy layout)
+};
+std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
+SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode);
+void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl);
+FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl, int sell_mode);
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq, double kappa, double alpha,
                                const double *conv, const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);
@@ -349,6 +366,8 @@ hipError_t launch_sell_fill(cdfem_ctx *c);
 hipError_t launch_csr_diag(cdfem_ctx *c, double *d);
 hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y);
 hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q);
+// permuted SpMV layout: dst = src gathered into the SpMV order (to_spmv_order) or scattered back
+hipError_t launch_perm(cdfem_ctx *c, bool to_spmv_order, const double *src, double *dst);
 bool spmv_delta(const cdfem_ctx *c);
 // fused high-order CG iteration (ho_kernels.hip / vec_kernels.hip)
 bool tile_den_ok(const cdfem_ctx *c);

@@ -48,7 +48,7 @@ static inline int64_t ee_index(int e, int i, int j, int nd)
     return ((int64_t)(e / kLanes) * nd * nd + (int64_t)i * nd + j) * kLanes + e % kLanes;
 }
 
-FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int64_t nl)
+FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int64_t nl, int sell_mode)
 {
     // dof -> incidences (e * nd + l), ascending
     std::vector<int64_t> cnt(nl + 1, 0);
@@ -129,64 +129,9 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
             }
         }
     });
-    // SELL-64 with a global stable sort by row length (descending): Kuhn P2 rows take a handful
-    // of distinct lengths, so the padding is < 1 %.  Within a row the entries keep CSR order.
-    std::vector<int32_t> order(nl);
-    for (int64_t i = 0; i < nl; ++i) order[i] = (int32_t)i;
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-        return rowptr[a + 1] - rowptr[a] > rowptr[b + 1] - rowptr[b];
-    });
-    const int64_t ns = (nl + kLanes - 1) / kLanes;
-    P.sptr.assign(ns + 1, 0);
-    P.srows.assign(ns * kLanes, -1);
-    int64_t stored = 0;
-    for (int64_t sl = 0; sl < ns; ++sl) {
-        int len = 0;
-        for (int l = 0; l < kLanes && sl * kLanes + l < nl; ++l) {
-            const int32_t r = order[sl * kLanes + l];
-            P.srows[sl * kLanes + l] = r;
-            len = std::max(len, rowptr[r + 1] - rowptr[r]);
-        }
-        stored += (int64_t)len * kLanes;
-        if (stored >= ((int64_t)1 << 31)) throw std::runtime_error("SELL storage exceeds int32 indexing");
-        P.sptr[sl + 1] = (int32_t)stored;
-    }
-    P.scols.assign(stored, 0);
-    P.smap.assign(stored, -1);
-    for (int64_t sl = 0; sl < ns; ++sl) {
-        const int len = (P.sptr[sl + 1] - P.sptr[sl]) / kLanes;
-        for (int l = 0; l < kLanes; ++l) {
-            const int32_t r = P.srows[sl * kLanes + l];
-            for (int j = 0; j < len; ++j) {
-                const int64_t t = P.sptr[sl] + (int64_t)j * kLanes + l;
-                if (r >= 0 && j < rowptr[r + 1] - rowptr[r]) {
-                    P.scols[t] = cols[rowptr[r] + j];
-                    P.smap[t] = rowptr[r] + j;
-                } else {
-                    P.scols[t] = r >= 0 ? r : 0;  // padding: a valid column, value 0
-                }
-            }
-        }
-    }
-    // column - row in 16 bits (padding: delta 0 from max(row, 0), the same column as above).  A
-    // lattice numbering keeps every delta within one or two z-planes, so for the Kuhn meshes the
-    // SpMV streams 10 instead of 12 bytes per stored entry.
-    bool fits = true;
-    for (int64_t sl = 0; sl < ns && fits; ++sl)
-        for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t) {
-            const int32_t r = P.srows[sl * kLanes + (t - P.sptr[sl]) % kLanes];
-            const int64_t d = (int64_t)P.scols[t] - (r >= 0 ? r : 0);
-            if (d < -32768 || d > 32767) { fits = false; break; }
-        }
-    if (fits) {
-        P.sdel.resize(stored);
-        for (int64_t sl = 0; sl < ns; ++sl)
-            for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t) {
-                const int32_t r = P.srows[sl * kLanes + (t - P.sptr[sl]) % kLanes];
-                P.sdel[t] = (int16_t)(P.scols[t] - (r >= 0 ? r : 0));
-            }
-    }
+    // SpMV layout: SELL-64 over the rows in the plan's order (sell_plan.cpp)
     P.rowptr = std::move(rowptr);
+    sell_build(P, nl, sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode));
     return P;
 }
 
@@ -397,50 +342,109 @@ k_sell_fill(const int32_t *__restrict__ smap, const double *__restrict__ vals, c
 
 // y = A x on the SELL-64 layout: one wave per 64-row slice, one lane per row, entries of a row
 // summed in CSR order; every value/column load is one coalesced wave access.  CI = int32_t:
-// absolute columns; CI = int16_t: column = max(row, 0) + delta (10 instead of 12 streamed bytes
-// per entry).  CG mode: partials of (x, y) and early exit once the Krylov state is done.
-template <bool CG, typename CI>
+// absolute columns; CI = int16_t: column = lane base + delta (10 instead of 12 streamed bytes per
+// entry).  PERM: the permuted layout (sell_plan.cpp), lane row = slice * 64 + lane in the SpMV's own
+// order (no row index stream, whole-line y stores); otherwise the row comes from srows.  xcd_per > 0:
+// workgroup b runs on XCD b mod 8, so logical block (b mod 8) * xcd_per + b / 8 gives every XCD one
+// contiguous slice range and its L2 sees each x line once.  CG mode: partials of (x, y) and early
+// exit once the Krylov state is done.
+// U entries per lane per step; PIPE: the next step's value/column loads are issued before this
+// step's x gathers are consumed, so a wave has one memory round trip per step instead of two.
+template <bool CG, typename CI, bool PERM, int U, bool PIPE>
 __global__ void __launch_bounds__(256)
 k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows, const CI *__restrict__ scols,
             const double *__restrict__ svals, const double *__restrict__ x, double *__restrict__ y, int64_t nslices,
-            double *__restrict__ part, const KrylovState *__restrict__ st)
+            int64_t n, int xcd_per, double *__restrict__ part, const KrylovState *__restrict__ st)
 {
     constexpr bool DELTA = sizeof(CI) == 2;
     __shared__ double sh[256 / 64];
     if (CG && st->done) return;
     const int lane = threadIdx.x & 63;
-    const int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t lb = xcd_per > 0 ? (int64_t)(blockIdx.x & 7) * xcd_per + (blockIdx.x >> 3) : blockIdx.x;
+    const int64_t sl = lb * 4 + (threadIdx.x >> 6);
     double dd = 0.0;
     if (sl < nslices) {
         const int32_t b = sptr[sl], len = (sptr[sl + 1] - b) >> 6;
-        const int32_t row = srows[sl * 64 + lane];
-        const double *xr = DELTA ? x + (row >= 0 ? row : 0) : x;
+        int64_t row, base;
+        if (PERM) {
+            row = sl * 64 + lane;
+            base = row < n ? row : n - 1;
+        } else {
+            row = srows[sl * 64 + lane];
+            base = row >= 0 ? row : 0;
+        }
+        const bool valid = PERM ? row < n : row >= 0;
+        const double *xr = DELTA ? x + base : x;
         const double *v = svals + b + lane;
         const CI *cidx = scols + b + lane;
+        // values and columns are streamed once per SpMV: non-temporal, x stays in L2
         double a0 = 0.0;
         int j = 0;
-        for (; j + 4 <= len; j += 4) {  // 4 independent loads in flight per lane
-            // values and columns are streamed once per SpMV: non-temporal, x stays in L2
-            const double v0 = __builtin_nontemporal_load(v + (j + 0) * 64), v1 = __builtin_nontemporal_load(v + (j + 1) * 64),
-                         v2 = __builtin_nontemporal_load(v + (j + 2) * 64), v3 = __builtin_nontemporal_load(v + (j + 3) * 64);
-            const int32_t c0 = __builtin_nontemporal_load(cidx + (j + 0) * 64),
-                          c1 = __builtin_nontemporal_load(cidx + (j + 1) * 64),
-                          c2 = __builtin_nontemporal_load(cidx + (j + 2) * 64),
-                          c3 = __builtin_nontemporal_load(cidx + (j + 3) * 64);
-            a0 = fma(v0, xr[c0], a0);
-            a0 = fma(v1, xr[c1], a0);
-            a0 = fma(v2, xr[c2], a0);
-            a0 = fma(v3, xr[c3], a0);
+        if constexpr (PIPE) {
+            double vv[U];
+            int32_t cc[U];
+            if (len >= U) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    cc[k] = __builtin_nontemporal_load(cidx + k * 64);
+                    vv[k] = __builtin_nontemporal_load(v + k * 64);
+                }
+            }
+            for (; j + U <= len; j += U) {
+                double xg[U];
+#pragma unroll
+                for (int k = 0; k < U; ++k) xg[k] = xr[cc[k]];
+                const bool more = j + 2 * U <= len;  // wave-uniform
+                if (more) {
+#pragma unroll
+                    for (int k = 0; k < U; ++k) {
+                        cc[k] = __builtin_nontemporal_load(cidx + (j + U + k) * 64);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < U; ++k) a0 = fma(vv[k], xg[k], a0);
+                if (more) {
+#pragma unroll
+                    for (int k = 0; k < U; ++k) vv[k] = __builtin_nontemporal_load(v + (j + U + k) * 64);
+                }
+            }
+        } else {
+            for (; j + U <= len; j += U) {  // U independent loads in flight per lane
+                double vv[U];
+                int32_t cc[U];
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    vv[k] = __builtin_nontemporal_load(v + (j + k) * 64);
+                    cc[k] = __builtin_nontemporal_load(cidx + (j + k) * 64);
+                }
+#pragma unroll
+                for (int k = 0; k < U; ++k) a0 = fma(vv[k], xr[cc[k]], a0);
+            }
         }
         for (; j < len; ++j)
             a0 = fma(__builtin_nontemporal_load(v + j * 64), xr[(int32_t)__builtin_nontemporal_load(cidx + j * 64)], a0);
         const double acc = a0;
-        if (row >= 0) {
+        if (valid) {
             y[row] = acc;
             if (CG) dd = acc * x[row];
         }
     }
     if (CG) store_partial(block_sum(dd, sh), part);
+}
+
+// permuted layout: xp[i] = x[perm[i]] into the SpMV order, y[perm[i]] = yp[i] back to mesh order
+__global__ void __launch_bounds__(256)
+k_perm_gather(const int32_t *__restrict__ perm, const double *__restrict__ x, double *__restrict__ xp, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) xp[i] = x[perm[i]];
+}
+
+__global__ void __launch_bounds__(256)
+k_perm_scatter(const int32_t *__restrict__ perm, const double *__restrict__ yp, double *__restrict__ y, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[perm[i]] = yp[i];
 }
 
 // ---- launchers ---------------------------------------------------------------------------------
@@ -503,34 +507,77 @@ hipError_t launch_sell_fill(cdfem_ctx *c)
     return hipGetLastError();
 }
 
-unsigned sell_grid(const cdfem_ctx *c) { return (unsigned)((c->nslices + 3) / 4); }
+// logical SpMV blocks (4 slices each) and the launched grid: with the XCD mapping the grid is
+// padded to a multiple of 8 (the extra blocks find no slice)
+static unsigned sell_blocks(const cdfem_ctx *c) { return (unsigned)((c->nslices + 3) / 4); }
+static int sell_xcd_per(const cdfem_ctx *c) { return c->spmv_xcd ? (int)((sell_blocks(c) + 7) / 8) : 0; }
+unsigned sell_grid(const cdfem_ctx *c) { return c->spmv_xcd ? 8u * (unsigned)sell_xcd_per(c) : sell_blocks(c); }
 
 bool spmv_delta(const cdfem_ctx *c) { return c->d_sdel && c->spmv_index16; }
 
+template <bool CG>
+static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, double *y, double *part,
+                        const KrylovState *st)
+{
+    const dim3 g(sell_grid(c)), b(256);
+    const int per = sell_xcd_per(c);
+    const bool perm = c->d_rperm != nullptr;
+#define CDFEM_SPMV1(CI, PM, U, PIPE)                                                                             \
+    CDFEM_LAUNCH(c, (k_sell_spmv<CG, CI, PM, U, PIPE>), g, b, 0, c->d_sptr, c->d_srows,                            \
+                 (const CI *)(sizeof(CI) == 2 ? (const void *)c->d_sdel : (const void *)c->d_scols), vals, x, y,  \
+                 c->nslices, (int64_t)c->nl, per, part, st)
+#define CDFEM_SPMV(CI, PM)                                                                                       \
+    do {                                                                                                         \
+        switch (c->spmv_variant) {                                                                               \
+        case 1: CDFEM_SPMV1(CI, PM, 4, true); break;                                                             \
+        case 2: CDFEM_SPMV1(CI, PM, 8, true); break;                                                             \
+        case 3: CDFEM_SPMV1(CI, PM, 8, false); break;                                                            \
+        default: CDFEM_SPMV1(CI, PM, 4, false); break;                                                           \
+        }                                                                                                        \
+    } while (0)
+    if (spmv_delta(c)) {
+        if (perm) CDFEM_SPMV(int16_t, true);
+        else CDFEM_SPMV(int16_t, false);
+    } else {
+        if (perm) CDFEM_SPMV(int32_t, true);
+        else CDFEM_SPMV(int32_t, false);
+    }
+#undef CDFEM_SPMV1
+#undef CDFEM_SPMV
+}
+
+// y = A x in the mesh's dof order.  Permuted layout: inside a permuted-order solve (perm_space)
+// the vectors already are in the SpMV order; otherwise x is gathered and y scattered around it.
 hipError_t launch_spmv(cdfem_ctx *c, bool constrained, const double *x, double *y)
 {
-    if (spmv_delta(c))
-        CDFEM_LAUNCH(c, (k_sell_spmv<false, int16_t>), dim3(sell_grid(c)), dim3(256), 0, c->d_sptr, c->d_srows,
-                     (const int16_t *)c->d_sdel, constrained ? c->d_svals_c : c->d_svals, x, y, c->nslices,
-                     (double *)nullptr, (const KrylovState *)nullptr);
-    else
-        CDFEM_LAUNCH(c, (k_sell_spmv<false, int32_t>), dim3(sell_grid(c)), dim3(256), 0, c->d_sptr, c->d_srows,
-                     (const int32_t *)c->d_scols, constrained ? c->d_svals_c : c->d_svals, x, y, c->nslices,
-                     (double *)nullptr, (const KrylovState *)nullptr);
+    const double *vals = constrained ? c->d_svals_c : c->d_svals;
+    if (!c->d_rperm || c->perm_space) {
+        spmv_launch<false>(c, vals, x, y, nullptr, nullptr);
+        return hipGetLastError();
+    }
+    const dim3 g((unsigned)((c->nl + 255) / 256)), b(256);
+    hipLaunchKernelGGL(k_perm_gather, g, b, 0, c->stream, c->d_rperm, x, c->d_pv[0], (int64_t)c->nl);
+    spmv_launch<false>(c, vals, c->d_pv[0], c->d_pv[1], nullptr, nullptr);
+    hipLaunchKernelGGL(k_perm_scatter, g, b, 0, c->stream, c->d_rperm, c->d_pv[1], y, (int64_t)c->nl);
     return hipGetLastError();
 }
 
-// q = A_c d and the den partials, then the MFEM CG den step (one-block finalizer)
+hipError_t launch_perm(cdfem_ctx *c, bool to_spmv_order, const double *src, double *dst)
+{
+    const dim3 g((unsigned)((c->nl + 255) / 256)), b(256);
+    if (to_spmv_order)
+        hipLaunchKernelGGL(k_perm_gather, g, b, 0, c->stream, c->d_rperm, src, dst, (int64_t)c->nl);
+    else
+        hipLaunchKernelGGL(k_perm_scatter, g, b, 0, c->stream, c->d_rperm, src, dst, (int64_t)c->nl);
+    return hipGetLastError();
+}
+
+// q = A_c d and the den partials, then the MFEM CG den step (one-block finalizer).  Vectors in the
+// SpMV order (a permuted layout only inside a permuted-order solve).
 hipError_t launch_spmv_cg(cdfem_ctx *c, const double *d, double *q)
 {
-    if (spmv_delta(c))
-        CDFEM_LAUNCH(c, (k_sell_spmv<true, int16_t>), dim3(sell_grid(c)), dim3(256), 0, c->d_sptr, c->d_srows,
-                     (const int16_t *)c->d_sdel, (const double *)c->d_svals_c, d, q, c->nslices, c->d_part,
-                     (const KrylovState *)c->d_state);
-    else
-        CDFEM_LAUNCH(c, (k_sell_spmv<true, int32_t>), dim3(sell_grid(c)), dim3(256), 0, c->d_sptr, c->d_srows,
-                     (const int32_t *)c->d_scols, (const double *)c->d_svals_c, d, q, c->nslices, c->d_part,
-                     (const KrylovState *)c->d_state);
+    if (c->d_rperm && !c->perm_space) return hipErrorInvalidValue;
+    spmv_launch<true>(c, c->d_svals_c, d, q, c->d_part, (const KrylovState *)c->d_state);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_den_fin(c, (int)sell_grid(c));

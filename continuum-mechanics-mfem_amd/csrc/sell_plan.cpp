@@ -1,0 +1,347 @@
+// sell_plan.cpp — row order and SELL-64 layout of the assembled (FA) operator's SpMV (host only).
+//
+// The reference's assembled path (HypreParMatrix -> PETSc MATAIJ, linear_convection_diffusion_2D.cpp
+// :349-375) multiplies in the mesh's own dof numbering.  Here the SpMV runs on a row/column
+// permutation of the same matrix, A' = P A P^T, chosen for the GPU:
+//   base order  the mesh numbering ("natural") or reverse Cuthill-McKee of the CSR graph (for
+//               shuffled / unstructured numberings: a small bandwidth keeps the x gathers L2-local
+//               and the 16-bit column deltas valid);
+//   windows     the base order cut into windows of W rows; inside a window the rows are grouped by
+//               length (descending) and by stencil signature (rows with the same relative column
+//               pattern, i.e. the same dof type of a lattice), then by base position.
+// A 64-row slice is then 64 consecutive rows of one length and, away from class boundaries, one
+// stencil: the y stores are whole cache lines, the x gather of every stored column is one short
+// contiguous run, and the padding stays under a few percent.  W is the largest candidate for which
+// every |column' - row'| fits the 16-bit delta stream.  Every row keeps its CSR entry order, so each
+// row sum is bitwise the one of the unpermuted SpMV; only the Krylov dot products see the new order.
+//
+// sell_plan_mode: 0 = legacy (mesh rows, global length sort, row index per lane),
+//                 1 = natural base + windows, 2 = RCM base + windows, 3 = auto (RCM when its
+//                 bandwidth is under half the natural one).
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+#include <vector>
+
+#include "cdfem_internal.hpp"
+
+namespace cdfem {
+
+namespace {
+
+template <class F>
+void par_for(int64_t n, F &&f)
+{
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int64_t chunk = (n + hw - 1) / hw;
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < hw; ++t) {
+        const int64_t lo = t * chunk, hi = std::min(n, lo + chunk);
+        if (lo >= hi) break;
+        th.emplace_back([&, lo, hi] { f(lo, hi); });
+    }
+    for (auto &x : th) x.join();
+}
+
+inline uint64_t mix64(uint64_t z)
+{
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// max |pos[col] - pos[row]| over the pattern (pos = identity when empty)
+int64_t bandwidth(int64_t nl, const int32_t *rowptr, const int32_t *cols, const std::vector<int32_t> &pos)
+{
+    std::vector<int64_t> part(16, 0);
+    std::vector<std::thread> th;
+    const int64_t chunk = (nl + 15) / 16;
+    for (int t = 0; t < 16; ++t)
+        th.emplace_back([&, t] {
+            int64_t m = 0;
+            for (int64_t i = t * chunk; i < std::min(nl, (t + 1) * chunk); ++i) {
+                const int64_t pi = pos.empty() ? i : pos[i];
+                for (int32_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+                    const int64_t pc = pos.empty() ? cols[k] : pos[cols[k]];
+                    m = std::max(m, pc > pi ? pc - pi : pi - pc);
+                }
+            }
+            part[t] = m;
+        });
+    for (auto &x : th) x.join();
+    return *std::max_element(part.begin(), part.end());
+}
+
+// BFS levels from s over unvisited-marked rows; returns the last visited row and the depth
+int64_t bfs_far(int64_t nl, const int32_t *rowptr, const int32_t *cols, int32_t s, std::vector<int32_t> &lev,
+                int32_t *far_out)
+{
+    std::fill(lev.begin(), lev.end(), -1);
+    std::vector<int32_t> q{s};
+    lev[s] = 0;
+    int32_t far = s;
+    for (size_t h = 0; h < q.size(); ++h) {
+        const int32_t u = q[h];
+        if (lev[u] > lev[far] || (lev[u] == lev[far] && rowptr[u + 1] - rowptr[u] < rowptr[far + 1] - rowptr[far]))
+            far = u;
+        for (int32_t k = rowptr[u]; k < rowptr[u + 1]; ++k)
+            if (lev[cols[k]] < 0) {
+                lev[cols[k]] = lev[u] + 1;
+                q.push_back(cols[k]);
+            }
+    }
+    *far_out = far;
+    (void)nl;
+    return lev[far];
+}
+
+}  // namespace
+
+// reverse Cuthill-McKee order (order[k] = row at position k): per connected component a
+// pseudo-peripheral start (repeated BFS to the farthest, lowest-degree row), neighbours visited in
+// ascending degree then ascending index, whole sequence reversed.  Deterministic.
+std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols)
+{
+    std::vector<int32_t> order;
+    order.reserve(nl);
+    std::vector<char> seen(nl, 0);
+    std::vector<int32_t> lev(nl, -1), nb;
+    auto deg = [&](int32_t r) { return rowptr[r + 1] - rowptr[r]; };
+    for (int64_t s0 = 0; s0 < nl; ++s0) {
+        if (seen[s0]) continue;
+        int32_t s = (int32_t)s0, far;
+        int64_t d = bfs_far(nl, rowptr, cols, s, lev, &far);
+        for (int it = 0; it < 8; ++it) {  // pseudo-peripheral node
+            int32_t f2;
+            const int64_t d2 = bfs_far(nl, rowptr, cols, far, lev, &f2);
+            if (d2 <= d) break;
+            s = far;
+            far = f2;
+            d = d2;
+        }
+        const size_t h0 = order.size();
+        order.push_back(s);
+        seen[s] = 1;
+        for (size_t h = h0; h < order.size(); ++h) {
+            const int32_t u = order[h];
+            nb.clear();
+            for (int32_t k = rowptr[u]; k < rowptr[u + 1]; ++k)
+                if (!seen[cols[k]]) {
+                    seen[cols[k]] = 1;
+                    nb.push_back(cols[k]);
+                }
+            std::sort(nb.begin(), nb.end(), [&](int32_t a, int32_t b) {
+                return deg(a) != deg(b) ? deg(a) < deg(b) : a < b;
+            });
+            order.insert(order.end(), nb.begin(), nb.end());
+        }
+    }
+    std::reverse(order.begin(), order.end());
+    return order;
+}
+
+SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode)
+{
+    SellPlan pl;
+    pl.mode = mode;
+    if (mode == 0 || nl == 0) return pl;
+    if (mode < 0 || mode > 3) throw std::runtime_error("sell_plan: bad mode");
+    // base order
+    std::vector<int32_t> bo, bp;  // base position -> row, row -> base position (empty: identity)
+    pl.bw_natural = bandwidth(nl, rowptr, cols, {});
+    bool rcm = mode == 2;
+    if (mode >= 2) {
+        bo = rcm_order(nl, rowptr, cols);
+        bp.resize(nl);
+        for (int64_t k = 0; k < nl; ++k) bp[bo[k]] = (int32_t)k;
+        pl.bw_rcm = bandwidth(nl, rowptr, cols, bp);
+        if (mode == 3) rcm = 2 * pl.bw_rcm < pl.bw_natural;
+        if (!rcm) {
+            bo.clear();
+            bp.clear();
+        }
+    }
+    pl.base = rcm ? 2 : 1;
+    auto B = [&](int64_t r) -> int64_t { return bp.empty() ? r : bp[r]; };
+    auto R = [&](int64_t k) -> int32_t { return bo.empty() ? (int32_t)k : bo[k]; };
+    // stencil signature: row length + order-independent hash of the base-order column offsets
+    std::vector<uint64_t> sig(nl);
+    par_for(nl, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) {
+            uint64_t h = 0;
+            for (int32_t k = rowptr[i]; k < rowptr[i + 1]; ++k) h += mix64((uint64_t)(B(cols[k]) - B(i)));
+            sig[i] = h;
+        }
+    });
+    auto len = [&](int32_t r) { return rowptr[r + 1] - rowptr[r]; };
+    std::vector<int32_t> perm(nl), inv(nl);
+    auto build = [&](int64_t W) {
+        const int64_t nw = (nl + W - 1) / W;
+        par_for(nw, [&](int64_t w0, int64_t w1) {
+            std::vector<int32_t> rows, bys;
+            for (int64_t w = w0; w < w1; ++w) {
+                const int64_t s = w * W, e = std::min(nl, s + W);
+                rows.clear();
+                for (int64_t k = s; k < e; ++k) rows.push_back(R(k));
+                // frequent signatures (>= one slice of rows in the window) form classes; the
+                // rest (boundary rows) stay in base order inside their length group
+                bys = rows;
+                std::sort(bys.begin(), bys.end(), [&](int32_t a, int32_t b) { return sig[a] < sig[b]; });
+                std::vector<std::pair<uint64_t, char>> cls;
+                for (size_t a = 0; a < bys.size();) {
+                    size_t b = a;
+                    while (b < bys.size() && sig[bys[b]] == sig[bys[a]]) ++b;
+                    cls.push_back({sig[bys[a]], (char)(b - a >= (size_t)kLanes)});
+                    a = b;
+                }
+                auto frequent = [&](int32_t r) {
+                    const auto it = std::lower_bound(cls.begin(), cls.end(), std::make_pair(sig[r], (char)0),
+                                                     [](const auto &x, const auto &y) { return x.first < y.first; });
+                    return it->second != 0;
+                };
+                std::vector<std::pair<char, int32_t>> key(rows.size());
+                for (size_t a = 0; a < rows.size(); ++a) key[a] = {(char)(frequent(rows[a]) ? 0 : 1), rows[a]};
+                std::vector<int32_t> idx(rows.size());
+                for (size_t a = 0; a < idx.size(); ++a) idx[a] = (int32_t)a;
+                std::sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) {
+                    const int32_t ra = rows[a], rb = rows[b];
+                    if (len(ra) != len(rb)) return len(ra) > len(rb);
+                    if (key[a].first != key[b].first) return key[a].first < key[b].first;
+                    if (key[a].first == 0 && sig[ra] != sig[rb]) return sig[ra] < sig[rb];
+                    return a < b;  // base position
+                });
+                for (size_t a = 0; a < idx.size(); ++a) perm[s + a] = rows[idx[a]];
+            }
+        });
+        for (int64_t k = 0; k < nl; ++k) inv[perm[k]] = (int32_t)k;
+        return bandwidth(nl, rowptr, cols, inv);
+    };
+    // the largest window whose deltas fit 16 bits; 4096 with 32-bit columns when none does
+    int64_t chosen = 0;
+    for (int64_t W : {32768, 16384, 8192, 4096, 2048, 1024, 512}) {
+        const int64_t d = build(W);
+        if (d <= 32767) {
+            chosen = W;
+            pl.max_delta = d;
+            break;
+        }
+    }
+    if (!chosen) {
+        chosen = 4096;
+        pl.max_delta = build(chosen);
+    }
+    pl.window = chosen;
+    pl.perm = std::move(perm);
+    return pl;
+}
+
+// SELL-64 over the rows in plan order (identity when the plan is empty -> legacy global length sort)
+void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
+{
+    const std::vector<int32_t> &rowptr = P.rowptr, &cols = P.cols;
+    const int64_t ns = (nl + kLanes - 1) / kLanes;
+    std::vector<int32_t> order(nl), inv;
+    if (pl.perm.empty()) {  // legacy: global stable sort by row length, row index per lane
+        for (int64_t i = 0; i < nl; ++i) order[i] = (int32_t)i;
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+            return rowptr[a + 1] - rowptr[a] > rowptr[b + 1] - rowptr[b];
+        });
+    } else {
+        order = pl.perm;
+        inv.resize(nl);
+        for (int64_t k = 0; k < nl; ++k) inv[order[k]] = (int32_t)k;
+        P.perm = pl.perm;
+    }
+    const bool permuted = !inv.empty();
+    P.sptr.assign(ns + 1, 0);
+    if (!permuted) P.srows.assign(ns * kLanes, -1);
+    int64_t stored = 0;
+    for (int64_t sl = 0; sl < ns; ++sl) {
+        int len = 0;
+        for (int l = 0; l < kLanes && sl * kLanes + l < nl; ++l) {
+            const int32_t r = order[sl * kLanes + l];
+            if (!permuted) P.srows[sl * kLanes + l] = r;
+            len = std::max(len, rowptr[r + 1] - rowptr[r]);
+        }
+        stored += (int64_t)len * kLanes;
+        if (stored >= ((int64_t)1 << 31)) throw std::runtime_error("SELL storage exceeds int32 indexing");
+        P.sptr[sl + 1] = (int32_t)stored;
+    }
+    P.scols.assign(stored, 0);
+    P.smap.assign(stored, -1);
+    // lane's own index in the SpMV's row space (the base of its column deltas): the original row
+    // (legacy) or the new row; padding lanes take max(row, 0) (legacy) / nl - 1 (permuted)
+    auto lane_base = [&](int64_t sl, int l) -> int64_t {
+        const int64_t k = sl * kLanes + l;
+        if (permuted) return std::min<int64_t>(k, nl - 1);
+        const int32_t r = P.srows[k];
+        return r >= 0 ? r : 0;
+    };
+    par_for(ns, [&](int64_t s0, int64_t s1) {
+        for (int64_t sl = s0; sl < s1; ++sl) {
+            const int len = (P.sptr[sl + 1] - P.sptr[sl]) / kLanes;
+            for (int l = 0; l < kLanes; ++l) {
+                const int64_t k = sl * kLanes + l;
+                const int32_t r = k < nl ? order[k] : -1;
+                for (int j = 0; j < len; ++j) {
+                    const int64_t t = P.sptr[sl] + (int64_t)j * kLanes + l;
+                    if (r >= 0 && j < rowptr[r + 1] - rowptr[r]) {
+                        const int32_t c = cols[rowptr[r] + j];
+                        P.scols[t] = permuted ? inv[c] : c;
+                        P.smap[t] = rowptr[r] + j;
+                    } else {
+                        P.scols[t] = (int32_t)lane_base(sl, l);  // padding: a valid column, value 0
+                    }
+                }
+            }
+        }
+    });
+    // column - lane base in 16 bits when every delta fits (10 instead of 12 streamed bytes/entry)
+    bool fits = true;
+    for (int64_t sl = 0; sl < ns && fits; ++sl)
+        for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t) {
+            const int64_t d = (int64_t)P.scols[t] - lane_base(sl, (t - P.sptr[sl]) % kLanes);
+            if (d < -32768 || d > 32767) { fits = false; break; }
+        }
+    if (fits) {
+        P.sdel.resize(stored);
+        for (int64_t sl = 0; sl < ns; ++sl)
+            for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t)
+                P.sdel[t] = (int16_t)(P.scols[t] - lane_base(sl, (t - P.sptr[sl]) % kLanes));
+    }
+}
+
+}  // namespace cdfem
+
+extern "C" {
+
+// host-only plan of the FA SpMV order (tests / tools): perm (new -> old row) of nl entries, and
+// info[0..5] = base (0 legacy, 1 natural, 2 RCM), window, max |delta|, natural bandwidth, RCM
+// bandwidth (0 when not computed), stored SELL entries / nnz * 1e6 (padding, parts per million)
+int cdfem_sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int32_t *perm, int64_t *info)
+{
+    try {
+        if (nl < 0 || (nl > 0 && (!rowptr || !cols)) || !perm || !info) return CDFEM_ERR_ARG;
+        cdfem::SellPlan pl = cdfem::sell_plan(nl, rowptr, cols, mode);
+        cdfem::FaPattern P;
+        P.rowptr.assign(rowptr, rowptr + nl + 1);
+        P.cols.assign(cols, cols + rowptr[nl]);
+        P.nnz = rowptr[nl];
+        cdfem::sell_build(P, nl, pl);
+        for (int64_t k = 0; k < nl; ++k) perm[k] = pl.perm.empty() ? (int32_t)k : pl.perm[k];
+        info[0] = pl.perm.empty() ? 0 : pl.base;
+        info[1] = pl.window;
+        info[2] = pl.max_delta;
+        info[3] = pl.bw_natural;
+        info[4] = pl.bw_rcm;
+        info[5] = P.nnz ? (int64_t)((double)P.sptr.back() / (double)P.nnz * 1e6) : 0;
+        return CDFEM_OK;
+    } catch (const std::exception &) {
+        return CDFEM_ERR_ARG;
+    }
+}
+
+}  // extern "C"

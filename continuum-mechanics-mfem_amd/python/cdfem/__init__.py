@@ -117,6 +117,7 @@ def _declare(L):
         "cdfem_prolongate": (C.c_int, [vp, vp, vp, C.c_int]),
         "cdfem_comm_info": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
         "cdfem_partition_rcb": (C.c_int, [C.c_int, C.c_int, C.c_int, _dp, C.c_int, _ip]),
+        "cdfem_sell_plan": (C.c_int, [i64, _ip, _ip, C.c_int, _ip, C.POINTER(i64)]),
         "cdfem_local_space_sizes": (C.c_int, [C.c_int, C.c_int, i64, _ip, _ip, C.c_int, C.POINTER(C.c_int),
                                               C.POINTER(i64), C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(i64)]),
         "cdfem_local_space": (C.c_int, [C.c_int, C.c_int, i64, _ip, _ip, C.c_int, _ip, _ip, C.POINTER(i64), _ip,
@@ -278,6 +279,27 @@ def partition_rcb(mesh: Mesh, nranks) -> np.ndarray:
     if rc:
         raise CdfemError(rc, "cdfem_partition_rcb failed")
     return part
+
+
+SELL_ORDER = {"legacy": 0, "natural": 1, "rcm": 2, "auto": 3}
+
+
+def sell_plan(rowptr, cols, mode="auto"):
+    """Row order of the FA SpMV (host only; sell_plan.cpp): returns (perm, info) with perm[new] =
+    mesh row and info = {base, window, max_delta, bw_natural, bw_rcm, padding}."""
+    rp, cl = _i32(rowptr), _i32(cols)
+    nl = len(rp) - 1
+    perm = np.zeros(nl, dtype=np.int32)
+    info = np.zeros(6, dtype=np.int64)
+    rc = lib().cdfem_sell_plan(nl, rp.ctypes.data_as(_ip), cl.ctypes.data_as(_ip),
+                               SELL_ORDER.get(mode, mode), perm.ctypes.data_as(_ip),
+                               info.ctypes.data_as(C.POINTER(C.c_int64)))
+    if rc:
+        raise CdfemError(rc, "cdfem_sell_plan failed")
+    keys = ("base", "window", "max_delta", "bw_natural", "bw_rcm")
+    d = {k: int(v) for k, v in zip(keys, info[:5])}
+    d["padding"] = info[5] / 1e6
+    return perm, d
 
 
 @dataclass

@@ -192,8 +192,10 @@ def test_fa_c4_full_size_properties(gpu_ctx):
 
 def test_fa_spmv_index16_matches_int32(gpu_ctx):
     """The SpMV's 16-bit column deltas (set_option "spmv_index16", the default) give the same bits
-    as 32-bit columns, for Mult, the constrained Mult and a CG solve; a random DoF numbering
-    (bandwidth > 2^15) falls back to 32-bit columns and gives the permuted result."""
+    as 32-bit columns, for Mult, the constrained Mult and a CG solve.  A random DoF numbering
+    (bandwidth > 2^15) falls back to 32-bit columns when the SpMV keeps the mesh's base order
+    (sell_order 1) and is brought back into 16 bits by the reverse Cuthill-McKee order (sell_order 3,
+    the default); both give the permuted result."""
     gm = cdfem.kuhn_mesh(3, 16, 2, perturb=0.1)      # 35,937 DoFs, lattice bandwidth 2,180
     rng = np.random.default_rng(16)
     x = rng.uniform(-1, 1, gm.nl)
@@ -219,16 +221,21 @@ def test_fa_spmv_index16_matches_int32(gpu_ctx):
         xyzp[perm] = gm.dof_xyz
         gp = cdfem.Mesh(gm.dim, gm.order, gm.verts, perm[gm.dofmap], gm.nl, perm[gm.ess], xyzp,
                         simplex=True)
-        gpu_ctx.upload_mesh(gp)
-        gpu_ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
-        assert gpu_ctx.kernel_bytes(cdfem.K_APPLY) == res[0][3]
         xp = np.empty_like(x)
         xp[perm] = x
-        yp = gpu_ctx.mult(xp)
         y = res[1][0]
-        assert np.abs(yp[perm] - y).max() <= 1e-13 * np.abs(y).max()
+        # natural base order: the shuffled bandwidth overflows 16 bits -> 32-bit columns;
+        # auto (default): the reverse Cuthill-McKee base order brings the deltas back into 16 bits
+        for order, nbytes in ((1, res[0][3]), (3, res[1][3])):
+            gpu_ctx.set_option("sell_order", order)
+            gpu_ctx.upload_mesh(gp)
+            gpu_ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            assert gpu_ctx.kernel_bytes(cdfem.K_APPLY) == nbytes
+            yp = gpu_ctx.mult(xp)
+            assert np.abs(yp[perm] - y).max() <= 1e-13 * np.abs(y).max()
     finally:
         gpu_ctx.set_option("spmv_index16", 1)
+        gpu_ctx.set_option("sell_order", 3)
 
 
 @pytest.mark.parametrize("dim,n,p,pert", [(2, 8, 2, 0.15), (3, 4, 2, 0.1), (2, 10, 1, 0.1)])

@@ -1,14 +1,20 @@
-"""Interleaved in-process A/B of SpMV variants on the C4 workload (Kuhn tets, P2, FA CSR + GMRES),
-GPU box only.
+"""Interleaved in-process A/B of FA SpMV layouts on the C4 workload (Kuhn tets, P2, FA CSR +
+GMRES(30)/Jacobi), GPU box only.
 
-Usage: python tools/ab_c4.py [--rounds R] [--iters K] [--n N] [--variants spmv_variant=0,spmv_variant=1]
-Prints per-variant median SpMV launch time (HIP events), GMRES orthogonalisation time and the
-achieved algorithmic GB/s of the SpMV.
+Each variant is its own context (the SpMV layout is fixed when the FA pattern is built):
+    label:mesh:opt=val+opt=val...     mesh = natural | shuffled (random dof relabelling); options
+                                      set before the mesh upload (sell_order, spmv_xcd, spmv_variant)
+Prints per variant the median SpMV launch time (HIP events), the GMRES orthogonalisation time, the
+wall time per solve and the algorithmic GB/s of the SpMV; checks every variant's GMRES iterate
+against the first variant's (mapped through the relabelling).
+
+    python tools/ab_c4.py [--rounds R] [--iters K] [--n N] [--variants ...]
 """
 import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -20,46 +26,74 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=60)
 ap.add_argument("--n", type=int, default=55)
-ap.add_argument("--variants", default="spmv_variant=0,spmv_variant=1")
+ap.add_argument("--variants", default="legacy:natural:sell_order=0+spmv_xcd=0,auto:natural:sell_order=3,"
+                                      "shuf_legacy:shuffled:sell_order=0+spmv_xcd=0,shuf_auto:shuffled:sell_order=3")
 args = ap.parse_args()
 
-mesh = cdfem.kuhn_mesh(3, args.n, 2, with_coords=False)
-ctx = cdfem.Context(0)
-ctx.upload_mesh(mesh)
-ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=(1.0, -2.0, 0.5), mass=1.0)
-b = np.random.default_rng(20261015).uniform(-1, 1, mesh.nl)
-_, B = ctx.form_linear_system(np.zeros(mesh.nl), b)
-dB, dX = ctx.to_device(B), ctx.alloc(8 * mesh.nl)
-variants = [v.split("=") for v in args.variants.split(",")]
-res = {f"{k}={v}": {"spmv_us": [], "orth_us": []} for k, v in variants}
+base = cdfem.kuhn_mesh(3, args.n, 2, with_coords=False)
+g = np.random.default_rng(7).permutation(base.nl).astype(np.int32)   # shuffled label of mesh dof i
+shuffled = cdfem.Mesh(base.dim, base.order, base.verts, g[base.dofmap], base.nl, np.sort(g[base.ess]),
+                      None, simplex=True)
+b_nat = np.random.default_rng(20261015).uniform(-1, 1, base.nl)
+b_shuf = np.empty_like(b_nat)
+b_shuf[g] = b_nat
+
+variants = []
+for spec in args.variants.split(","):
+    label, mesh, opts = spec.split(":")
+    m = base if mesh == "natural" else shuffled
+    ctx = cdfem.Context(0)
+    for kv in filter(None, opts.split("+")):
+        k, val = kv.split("=")
+        ctx.set_option(k, int(val))
+    t0 = time.perf_counter()
+    ctx.upload_mesh(m)
+    ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=(1.0, -2.0, 0.5), mass=1.0)
+    setup_s = time.perf_counter() - t0
+    b = b_nat if mesh == "natural" else b_shuf
+    _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+    variants.append(dict(label=label, mesh=mesh, ctx=ctx, dB=ctx.to_device(B), dX=ctx.alloc(8 * m.nl),
+                         spmv_us=[], orth_us=[], solve_ms=[], setup_s=setup_s))
+    print(f"# {label}: setup {setup_s:.2f} s", flush=True)
+
 ref = None
 for rnd in range(args.rounds + 1):
-    for k, v in variants:
-        ctx.set_option(k, int(v))
+    for v in variants:
+        ctx = v["ctx"]
         ctx.set_option("profile_mask", (1 << cdfem.K_APPLY) | (1 << cdfem.K_ORTH))
         ctx.profile(True)
         ctx.synchronize()
-        ctx.solve_device(dB, dX, method="gmres", pc="jacobi", rel_tol=0.0, abs_tol=0.0,
+        t0 = time.perf_counter()
+        ctx.solve_device(v["dB"], v["dX"], method="gmres", pc="jacobi", rel_tol=0.0, abs_tol=0.0,
                          max_iter=args.iters, restart=30)
+        ctx.synchronize()
+        wall = (time.perf_counter() - t0) * 1e3
         a = ctx.profile_read(cdfem.K_APPLY)
         o = ctx.profile_read(cdfem.K_ORTH)
         ctx.profile(False)
-        x = ctx.from_device(dX, mesh.nl)
+        x = ctx.from_device(v["dX"], base.nl)
+        if v["mesh"] == "shuffled":
+            x = x[g]                          # back to the natural labels
         if ref is None:
             ref = x
-        assert np.abs(x - ref).max() <= 1e-10 * np.abs(ref).max()
+        err = float(np.abs(x - ref).max() / np.abs(ref).max())
+        assert err <= 1e-9, (v["label"], err)
         if rnd == 0:
             continue  # warm-up round
-        r = res[f"{k}={v}"]
-        r["spmv_us"].append(a[0] / max(a[1], 1) * 1e3)
-        r["orth_us"].append(o[0] / max(o[1], 1) * 1e3)
-bytes_spmv = ctx.kernel_bytes(cdfem.K_APPLY)
+        v["spmv_us"].append(a[0] / max(a[1], 1) * 1e3)
+        v["orth_us"].append(o[0] / max(o[1], 1) * 1e3)
+        v["solve_ms"].append(wall)
+        v["err"] = err
 out = {}
-for name, r in res.items():
-    med = {k: float(np.median(v)) for k, v in r.items()}
-    med["spmv_GBs"] = bytes_spmv / (med["spmv_us"] * 1e-6) / 1e9
-    out[name] = med
+for v in variants:
+    nbytes = v["ctx"].kernel_bytes(cdfem.K_APPLY)
+    med = {k: float(np.median(v[k])) for k in ("spmv_us", "orth_us", "solve_ms")}
+    med["spmv_GBs"] = nbytes / (med["spmv_us"] * 1e-6) / 1e9
+    med["setup_s"] = v["setup_s"]
+    med["max_rel_diff_vs_first"] = v.get("err", 0.0)
+    out[v["label"]] = med
 print(json.dumps(out, indent=1))
-ctx.free(dB)
-ctx.free(dX)
-ctx.close()
+for v in variants:
+    v["ctx"].free(v["dB"])
+    v["ctx"].free(v["dX"])
+    v["ctx"].close()
