@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--path", choices=["brick", "generic"], default=None,
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "c5w"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c4s", "c5", "c5w"], default="c2",
                     help="c2: 64^3 hex p=2 PA + CG (BASELINE metric config; N>1: weak scaling, a 64^3 slab "
                          "per rank); c3: 128^3 hex p=4 PA + CG (configs[2]); c4: Kuhn 55^3 x 6 tets P2, FA CSR "
                          "+ GMRES(30)/Jacobi (configs[3]); c5: 256^3 hex p=2 PA + CG split into N z-slabs "
@@ -213,6 +213,14 @@ def main_c4(args):
     import cdfem
     n, p = args.tet_n, 2
     mesh = cdfem.kuhn_mesh(3, n, p, with_coords=False)
+    shuffled = args.config == "c4s"
+    if shuffled:
+        # c4s: the same mesh with a random dof numbering (what a gmsh file without bandwidth
+        # reduction gives): the FA setup's SpMV order (sell_order auto) recovers the locality with
+        # reverse Cuthill-McKee and the Krylov solve runs in that order (sell_plan.cpp)
+        g = np.random.default_rng(7).permutation(mesh.nl).astype(np.int32)
+        mesh = cdfem.Mesh(mesh.dim, mesh.order, mesh.verts, g[mesh.dofmap], mesh.nl, np.sort(g[mesh.ess]),
+                          None, simplex=True)
     ctx = cdfem.Context(0)
     ctx.upload_mesh(mesh)
     t0 = time.perf_counter()
@@ -255,7 +263,8 @@ def main_c4(args):
             traffic = None
             if os.path.exists(args.traffic_json):
                 try:
-                    traffic = json.load(open(args.traffic_json)).get(f"c4_n{n}_p{p}", {}).get("hbm_bytes_per_launch")
+                    key = f"{'c4s' if shuffled else 'c4'}_n{n}_p{p}"
+                    traffic = json.load(open(args.traffic_json)).get(key, {}).get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(bytes_ / per / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -281,8 +290,10 @@ def main_c4(args):
            "value": mesh.nl * iters / dt, "unit": "DoF-iter/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-           "config": {"workload": f"C4: Kuhn {n}^3x6 tets P2, FA CSR (GPU-assembled) + GMRES(30)/Jacobi "
-                                  f"{iters_per_step} it/step", "dofs": mesh.nl, "elements": mesh.ne, "nnz": nnz,
+           "config": {"workload": f"{'C4s' if shuffled else 'C4'}: Kuhn {n}^3x6 tets P2"
+                                  f"{', shuffled dof numbering (RCM SpMV order)' if shuffled else ''}, FA CSR "
+                                  f"(GPU-assembled) + GMRES(30)/Jacobi {iters_per_step} it/step",
+                      "dofs": mesh.nl, "elements": mesh.ne, "nnz": nnz,
                       "fa_setup_s": round(t_setup, 3), "parallelism": "single"},
            "roofline": roof, "cpu_baseline": cpu}
     print(json.dumps(out), flush=True)
@@ -293,7 +304,7 @@ def main_c4(args):
 
 def main():
     args = parse()
-    if args.config == "c4":
+    if args.config in ("c4", "c4s"):
         return main_c4(args)
     world, rank, local, pg = dist_setup(args)
     import cdfem

@@ -102,6 +102,7 @@ void free_mesh(cdfem_ctx *c)
     ilu_free(c);
     partition_free(c);
     c->nslices = c->nstored = 0;
+    c->sell_windowed = false;
     c->geom = 0;
     c->fa_ready = false;
     c->nnz = 0;
@@ -1200,6 +1201,7 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             HIPCHK(hipMemcpyAsync(c->d_srows, P.srows.data(), P.srows.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_scols, P.scols.data(), P.scols.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_smap, P.smap.data(), P.smap.size() * 4, hipMemcpyHostToDevice, c->stream));
+            c->sell_windowed = P.windowed;
             if (!P.perm.empty()) {
                 c->d_rperm = dalloc<int32_t>(P.perm.size());
                 HIPCHK(hipMemcpyAsync(c->d_rperm, P.perm.data(), P.perm.size() * 4, hipMemcpyHostToDevice, c->stream));
@@ -1442,10 +1444,10 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;
         } else if (k == "sell_order") {  // read when the FA pattern is built (once per mesh)
-            if (value < 0 || value > 3) throw ArgError("sell_order must be 0 (legacy), 1 (natural), 2 (RCM) or 3 (auto)");
+            if (value < 0 || value > 4) throw ArgError("sell_order must be 0..4 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM)");
             c->sell_mode = value;
         } else if (k == "spmv_variant") {
-            if (value < 0 || value > 3) throw ArgError("spmv_variant must be 0..3");
+            if (value < 0 || value > 1) throw ArgError("spmv_variant must be 0 or 1");
             c->spmv_variant = value;
         } else if (k == "spmv_xcd") {
             if (value < 0 || value > 1) throw ArgError("spmv_xcd must be 0 or 1");

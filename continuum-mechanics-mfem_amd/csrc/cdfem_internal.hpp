@@ -202,9 +202,10 @@ struct cdfem_ctx {
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
-    int spmv_variant = 0;               // set_option "spmv_variant": SpMV inner loop (A/B: 0 U4, 1 U4 pipelined, 2 U8 pipelined, 3 U8)
-    int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD
-    int32_t *d_rperm = nullptr;         // permuted SpMV: new row -> mesh row (null: legacy layout)
+    int spmv_variant = 0;               // set_option "spmv_variant": SpMV inner loop, 0 = 4 loads in flight, 1 = software-pipelined (A/B)
+    int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD (windowed layout)
+    int32_t *d_rperm = nullptr;         // SpMV space order: space row -> mesh row (null: mesh order)
+    bool sell_windowed = false;         // slices cut from the space order (kernel row = slice * 64 + lane)
     double *d_pv[2] = {};               // permuted-space scratch (apply in mesh order; solve B / X)
     bool perm_space = false;            // inside a solve that runs in the permuted order
     double *d_dinv_p = nullptr;         // the Jacobi scale in permuted order (during such a solve)
@@ -346,13 +347,16 @@ struct FaPattern {
     std::vector<int32_t> scols;  // [stored] column, slice-major then entry-major then lane
     std::vector<int32_t> smap;   // [stored] CSR index of the stored entry, -1 = padding
     std::vector<int16_t> sdel;   // [stored] column - row when every |column - row| < 2^15, else empty
-    std::vector<int32_t> perm;   // permuted SpMV (sell_plan.cpp): new row -> mesh row; empty = legacy
+    std::vector<int32_t> perm;   // SpMV space order (sell_plan.cpp): space row -> mesh row; empty = mesh order
+    bool windowed = false;       // slices cut from the space order directly (no srows)
 };
-// SpMV row order (sell_plan.cpp): mode 0 legacy, 1 natural + windows, 2 RCM + windows, 3 auto
+// SpMV order (sell_plan.cpp): 0 natural + global sort, 1 natural + windows, 2 RCM + windows,
+// 3 auto (RCM + global or mode 0), 4 RCM + global
 struct SellPlan {
-    int mode = 0, base = 0;
+    int mode = 0, base = 1;
+    bool windowed = false;
     int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0;
-    std::vector<int32_t> perm;   // new -> old (empty: legacy layout)
+    std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
 };
 std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
 SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode);

@@ -348,85 +348,121 @@ k_sell_fill(const int32_t *__restrict__ smap, const double *__restrict__ vals, c
 // workgroup b runs on XCD b mod 8, so logical block (b mod 8) * xcd_per + b / 8 gives every XCD one
 // contiguous slice range and its L2 sees each x line once.  CG mode: partials of (x, y) and early
 // exit once the Krylov state is done.
+template <bool NT, class T>
+__device__ __forceinline__ T stream_load(const T *p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// One wave's 64-row slice: returns the row sum of its lane (row index and validity out).
 // U entries per lane per step; PIPE: the next step's value/column loads are issued before this
-// step's x gathers are consumed, so a wave has one memory round trip per step instead of two.
-template <bool CG, typename CI, bool PERM, int U, bool PIPE>
+// step's x gathers are consumed (one memory round trip per step instead of two).  NT: values and
+// columns are streamed once per SpMV: non-temporal loads, so x stays in L2.
+template <typename CI, bool PERM, int U, bool PIPE, bool NT>
+__device__ __forceinline__ double sell_slice(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows,
+                                             const CI *__restrict__ scols, const double *__restrict__ svals,
+                                             const double *__restrict__ x, int64_t n, int64_t sl, int lane,
+                                             int64_t &row, bool &valid)
+{
+    constexpr bool DELTA = sizeof(CI) == 2;
+    const int32_t b = sptr[sl], len = (sptr[sl + 1] - b) >> 6;
+    int64_t base;
+    if (PERM) {
+        row = sl * 64 + lane;
+        base = row < n ? row : n - 1;
+    } else {
+        row = srows[sl * 64 + lane];
+        base = row >= 0 ? row : 0;
+    }
+    valid = PERM ? row < n : row >= 0;
+    const double *xr = DELTA ? x + base : x;
+    const double *v = svals + b + lane;
+    const CI *cidx = scols + b + lane;
+    double a0 = 0.0;
+    int j = 0;
+    if constexpr (PIPE) {
+        double vv[U];
+        int32_t cc[U];
+        if (len >= U) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                cc[k] = stream_load<NT>(cidx + k * 64);
+                vv[k] = stream_load<NT>(v + k * 64);
+            }
+        }
+        for (; j + U <= len; j += U) {
+            double xg[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) xg[k] = xr[cc[k]];
+            const bool more = j + 2 * U <= len;  // wave-uniform
+            if (more) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) cc[k] = stream_load<NT>(cidx + (j + U + k) * 64);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) a0 = fma(vv[k], xg[k], a0);
+            if (more) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) vv[k] = stream_load<NT>(v + (j + U + k) * 64);
+            }
+        }
+    } else {
+        for (; j + U <= len; j += U) {  // U independent loads in flight per lane
+            double vv[U];
+            int32_t cc[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                vv[k] = stream_load<NT>(v + (j + k) * 64);
+                cc[k] = stream_load<NT>(cidx + (j + k) * 64);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) a0 = fma(vv[k], xr[cc[k]], a0);
+        }
+    }
+    for (; j < len; ++j) a0 = fma(stream_load<NT>(v + j * 64), xr[(int32_t)stream_load<NT>(cidx + j * 64)], a0);
+    return a0;
+}
+
+// y = A x on the SELL-64 layout: one wave per 64-row slice, one lane per row, entries of a row
+// summed in CSR order; every value/column load is one coalesced wave access.  CI = int32_t:
+// absolute columns; CI = int16_t: column = lane base + delta (10 instead of 12 streamed bytes per
+// entry).  PERM: the permuted layout (sell_plan.cpp), lane row = slice * 64 + lane in the SpMV's own
+// order (no row index stream, whole-line y stores); otherwise the row comes from srows.
+// Logical blocks (4 slices each): xcd_per > 0 gives XCD b mod 8 the contiguous range
+// [(b mod 8) * xcd_per, + xcd_per), so its L2 sees each x line once (the loop runs once per block
+// with the launchers' grids; it keeps any smaller grid correct).
+// CG mode: partials of (x, y) and early exit once the Krylov state is done.
+template <bool CG, typename CI, bool PERM, int U, bool PIPE, bool NT>
 __global__ void __launch_bounds__(256)
 k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows, const CI *__restrict__ scols,
             const double *__restrict__ svals, const double *__restrict__ x, double *__restrict__ y, int64_t nslices,
             int64_t n, int xcd_per, double *__restrict__ part, const KrylovState *__restrict__ st)
 {
-    constexpr bool DELTA = sizeof(CI) == 2;
     __shared__ double sh[256 / 64];
     if (CG && st->done) return;
     const int lane = threadIdx.x & 63;
-    const int64_t lb = xcd_per > 0 ? (int64_t)(blockIdx.x & 7) * xcd_per + (blockIdx.x >> 3) : blockIdx.x;
-    const int64_t sl = lb * 4 + (threadIdx.x >> 6);
+    const int64_t nlb = (nslices + 3) / 4;
+    int64_t lb, end, step;
+    if (xcd_per > 0) {
+        lb = (int64_t)(blockIdx.x & 7) * xcd_per + (blockIdx.x >> 3);
+        end = std::min<int64_t>(nlb, (int64_t)((blockIdx.x & 7) + 1) * xcd_per);
+        step = gridDim.x >> 3;
+    } else {
+        lb = blockIdx.x;
+        end = nlb;
+        step = gridDim.x;
+    }
     double dd = 0.0;
-    if (sl < nslices) {
-        const int32_t b = sptr[sl], len = (sptr[sl + 1] - b) >> 6;
-        int64_t row, base;
-        if (PERM) {
-            row = sl * 64 + lane;
-            base = row < n ? row : n - 1;
-        } else {
-            row = srows[sl * 64 + lane];
-            base = row >= 0 ? row : 0;
-        }
-        const bool valid = PERM ? row < n : row >= 0;
-        const double *xr = DELTA ? x + base : x;
-        const double *v = svals + b + lane;
-        const CI *cidx = scols + b + lane;
-        // values and columns are streamed once per SpMV: non-temporal, x stays in L2
-        double a0 = 0.0;
-        int j = 0;
-        if constexpr (PIPE) {
-            double vv[U];
-            int32_t cc[U];
-            if (len >= U) {
-#pragma unroll
-                for (int k = 0; k < U; ++k) {
-                    cc[k] = __builtin_nontemporal_load(cidx + k * 64);
-                    vv[k] = __builtin_nontemporal_load(v + k * 64);
-                }
-            }
-            for (; j + U <= len; j += U) {
-                double xg[U];
-#pragma unroll
-                for (int k = 0; k < U; ++k) xg[k] = xr[cc[k]];
-                const bool more = j + 2 * U <= len;  // wave-uniform
-                if (more) {
-#pragma unroll
-                    for (int k = 0; k < U; ++k) {
-                        cc[k] = __builtin_nontemporal_load(cidx + (j + U + k) * 64);
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < U; ++k) a0 = fma(vv[k], xg[k], a0);
-                if (more) {
-#pragma unroll
-                    for (int k = 0; k < U; ++k) vv[k] = __builtin_nontemporal_load(v + (j + U + k) * 64);
-                }
-            }
-        } else {
-            for (; j + U <= len; j += U) {  // U independent loads in flight per lane
-                double vv[U];
-                int32_t cc[U];
-#pragma unroll
-                for (int k = 0; k < U; ++k) {
-                    vv[k] = __builtin_nontemporal_load(v + (j + k) * 64);
-                    cc[k] = __builtin_nontemporal_load(cidx + (j + k) * 64);
-                }
-#pragma unroll
-                for (int k = 0; k < U; ++k) a0 = fma(vv[k], xr[cc[k]], a0);
-            }
-        }
-        for (; j < len; ++j)
-            a0 = fma(__builtin_nontemporal_load(v + j * 64), xr[(int32_t)__builtin_nontemporal_load(cidx + j * 64)], a0);
-        const double acc = a0;
+    for (; lb < end; lb += step) {
+        const int64_t sl = lb * 4 + (threadIdx.x >> 6);
+        if (sl >= nslices) continue;
+        int64_t row;
+        bool valid;
+        const double acc = sell_slice<CI, PERM, U, PIPE, NT>(sptr, srows, scols, svals, x, n, sl, lane, row, valid);
         if (valid) {
             y[row] = acc;
-            if (CG) dd = acc * x[row];
+            if (CG) dd += acc * x[row];
         }
     }
     if (CG) store_partial(block_sum(dd, sh), part);
@@ -507,11 +543,18 @@ hipError_t launch_sell_fill(cdfem_ctx *c)
     return hipGetLastError();
 }
 
-// logical SpMV blocks (4 slices each) and the launched grid: with the XCD mapping the grid is
-// padded to a multiple of 8 (the extra blocks find no slice)
+// logical SpMV blocks (4 slices each) and the launched grid (a multiple of 8 with the XCD ranges)
 static unsigned sell_blocks(const cdfem_ctx *c) { return (unsigned)((c->nslices + 3) / 4); }
-static int sell_xcd_per(const cdfem_ctx *c) { return c->spmv_xcd ? (int)((sell_blocks(c) + 7) / 8) : 0; }
-unsigned sell_grid(const cdfem_ctx *c) { return c->spmv_xcd ? 8u * (unsigned)sell_xcd_per(c) : sell_blocks(c); }
+static int sell_xcd_per(const cdfem_ctx *c)
+{
+    // contiguous per-XCD ranges pay on the windowed layout (1.00x traffic); the global length sort
+    // puts the longest rows first, and a range split would hand them all to XCD 0
+    return c->spmv_xcd && c->sell_windowed ? (int)((sell_blocks(c) + 7) / 8) : 0;
+}
+unsigned sell_grid(const cdfem_ctx *c)
+{
+    return sell_xcd_per(c) ? 8u * (unsigned)sell_xcd_per(c) : sell_blocks(c);
+}
 
 bool spmv_delta(const cdfem_ctx *c) { return c->d_sdel && c->spmv_index16; }
 
@@ -521,19 +564,15 @@ static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, doubl
 {
     const dim3 g(sell_grid(c)), b(256);
     const int per = sell_xcd_per(c);
-    const bool perm = c->d_rperm != nullptr;
-#define CDFEM_SPMV1(CI, PM, U, PIPE)                                                                             \
-    CDFEM_LAUNCH(c, (k_sell_spmv<CG, CI, PM, U, PIPE>), g, b, 0, c->d_sptr, c->d_srows,                            \
+    const bool perm = c->sell_windowed;
+#define CDFEM_SPMV1(CI, PM, U, PIPE, NT)                                                                         \
+    CDFEM_LAUNCH(c, (k_sell_spmv<CG, CI, PM, U, PIPE, NT>), g, b, 0, c->d_sptr, c->d_srows,                        \
                  (const CI *)(sizeof(CI) == 2 ? (const void *)c->d_sdel : (const void *)c->d_scols), vals, x, y,  \
                  c->nslices, (int64_t)c->nl, per, part, st)
 #define CDFEM_SPMV(CI, PM)                                                                                       \
     do {                                                                                                         \
-        switch (c->spmv_variant) {                                                                               \
-        case 1: CDFEM_SPMV1(CI, PM, 4, true); break;                                                             \
-        case 2: CDFEM_SPMV1(CI, PM, 8, true); break;                                                             \
-        case 3: CDFEM_SPMV1(CI, PM, 8, false); break;                                                            \
-        default: CDFEM_SPMV1(CI, PM, 4, false); break;                                                           \
-        }                                                                                                        \
+        if (c->spmv_variant == 1) CDFEM_SPMV1(CI, PM, 4, true, true);                                          \
+        else CDFEM_SPMV1(CI, PM, 4, false, true);                                                                \
     } while (0)
     if (spmv_delta(c)) {
         if (perm) CDFEM_SPMV(int16_t, true);

@@ -1,23 +1,25 @@
 // sell_plan.cpp — row order and SELL-64 layout of the assembled (FA) operator's SpMV (host only).
 //
 // The reference's assembled path (HypreParMatrix -> PETSc MATAIJ, linear_convection_diffusion_2D.cpp
-// :349-375) multiplies in the mesh's own dof numbering.  Here the SpMV runs on a row/column
-// permutation of the same matrix, A' = P A P^T, chosen for the GPU:
+// :349-375) multiplies in the mesh's own dof numbering.  Here the SpMV may run on a row/column
+// permutation of the same matrix, A' = P A P^T (the "space" order; the Krylov solve then runs in it,
+// capi.hip cdfem_solve), and the SELL-64 slices are cut from that space in one of two layouts:
 //   base order  the mesh numbering ("natural") or reverse Cuthill-McKee of the CSR graph (for
 //               shuffled / unstructured numberings: a small bandwidth keeps the x gathers L2-local
 //               and the 16-bit column deltas valid);
-//   windows     the base order cut into windows of W rows; inside a window the rows are grouped by
-//               length (descending) and by stencil signature (rows with the same relative column
-//               pattern, i.e. the same dof type of a lattice), then by base position.
-// A 64-row slice is then 64 consecutive rows of one length and, away from class boundaries, one
-// stencil: the y stores are whole cache lines, the x gather of every stored column is one short
-// contiguous run, and the padding stays under a few percent.  W is the largest candidate for which
-// every |column' - row'| fits the 16-bit delta stream.  Every row keeps its CSR entry order, so each
-// row sum is bitwise the one of the unpermuted SpMV; only the Krylov dot products see the new order.
+//   layout      global: rows sorted by length over the whole matrix, a row index per lane (the
+//               measured best on the lattice numbering);
+//               windows: the base order cut into windows of W rows, inside a window rows grouped
+//               by length (descending) and stencil signature, then base position; the space order
+//               IS the slice order (no row index stream, whole-line y stores, 1.00x HBM traffic),
+//               W the largest candidate for which every |column' - row'| fits 16 bits.
+// Every row keeps its CSR entry order, so each row sum is bitwise the one of the unpermuted SpMV;
+// only the Krylov dot products see the new order.
 //
-// sell_plan_mode: 0 = legacy (mesh rows, global length sort, row index per lane),
-//                 1 = natural base + windows, 2 = RCM base + windows, 3 = auto (RCM when its
-//                 bandwidth is under half the natural one).
+// sell_order: 0 = natural + global (the mesh order, no permutation), 1 = natural + windows,
+//             2 = RCM + windows, 3 = auto (mode 0 when the mesh order is banded: 16-bit deltas and
+//             bandwidth under nl / 8; else RCM + global when its bandwidth is under half the
+//             natural one), 4 = RCM + global.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -147,12 +149,15 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
 {
     SellPlan pl;
     pl.mode = mode;
+    pl.base = 1;
+    if (mode < 0 || mode > 4) throw std::runtime_error("sell_plan: bad mode");
     if (mode == 0 || nl == 0) return pl;
-    if (mode < 0 || mode > 3) throw std::runtime_error("sell_plan: bad mode");
     // base order
     std::vector<int32_t> bo, bp;  // base position -> row, row -> base position (empty: identity)
     pl.bw_natural = bandwidth(nl, rowptr, cols, {});
-    bool rcm = mode == 2;
+    bool rcm = mode == 2 || mode == 4;
+    // the mesh order is banded (16-bit deltas, bandwidth under nl / 8): mode 0 without the RCM pass
+    if (mode == 3 && pl.bw_natural <= 32767 && pl.bw_natural * 8 <= nl) return pl;
     if (mode >= 2) {
         bo = rcm_order(nl, rowptr, cols);
         bp.resize(nl);
@@ -165,6 +170,13 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
         }
     }
     pl.base = rcm ? 2 : 1;
+    if (mode >= 3) {  // global length sort over the base order: the space order is the base order
+        pl.windowed = false;
+        pl.max_delta = rcm ? pl.bw_rcm : pl.bw_natural;
+        pl.perm = std::move(bo);
+        return pl;
+    }
+    pl.windowed = true;
     auto B = [&](int64_t r) -> int64_t { return bp.empty() ? r : bp[r]; };
     auto R = [&](int64_t k) -> int32_t { return bo.empty() ? (int32_t)k : bo[k]; };
     // stencil signature: row length + order-independent hash of the base-order column offsets
@@ -238,33 +250,36 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
     return pl;
 }
 
-// SELL-64 over the rows in plan order (identity when the plan is empty -> legacy global length sort)
+// SELL-64 over the plan's space order (identity when pl.perm is empty): windowed -> slice k holds
+// space rows 64k.. (no row index), global -> space rows stably sorted by length, srows per lane
 void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
 {
     const std::vector<int32_t> &rowptr = P.rowptr, &cols = P.cols;
     const int64_t ns = (nl + kLanes - 1) / kLanes;
-    std::vector<int32_t> order(nl), inv;
-    if (pl.perm.empty()) {  // legacy: global stable sort by row length, row index per lane
-        for (int64_t i = 0; i < nl; ++i) order[i] = (int32_t)i;
-        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-            return rowptr[a + 1] - rowptr[a] > rowptr[b + 1] - rowptr[b];
-        });
-    } else {
-        order = pl.perm;
+    const std::vector<int32_t> &sp = pl.perm;  // space row -> mesh row
+    std::vector<int32_t> inv;                   // mesh row -> space row
+    if (!sp.empty()) {
         inv.resize(nl);
-        for (int64_t k = 0; k < nl; ++k) inv[order[k]] = (int32_t)k;
-        P.perm = pl.perm;
+        for (int64_t k = 0; k < nl; ++k) inv[sp[k]] = (int32_t)k;
+        P.perm = sp;
     }
-    const bool permuted = !inv.empty();
+    P.windowed = pl.windowed;
+    auto mrow = [&](int64_t q) -> int32_t { return sp.empty() ? (int32_t)q : sp[q]; };
+    auto rlen = [&](int64_t q) { const int32_t r = mrow(q); return rowptr[r + 1] - rowptr[r]; };
+    std::vector<int32_t> order(nl);  // slice position -> space row
+    for (int64_t i = 0; i < nl; ++i) order[i] = (int32_t)i;
+    if (!pl.windowed)
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return rlen(a) > rlen(b); });
+    const bool permuted = pl.windowed;  // kernel row = slice position (no srows)
     P.sptr.assign(ns + 1, 0);
     if (!permuted) P.srows.assign(ns * kLanes, -1);
     int64_t stored = 0;
     for (int64_t sl = 0; sl < ns; ++sl) {
         int len = 0;
         for (int l = 0; l < kLanes && sl * kLanes + l < nl; ++l) {
-            const int32_t r = order[sl * kLanes + l];
-            if (!permuted) P.srows[sl * kLanes + l] = r;
-            len = std::max(len, rowptr[r + 1] - rowptr[r]);
+            const int32_t q = order[sl * kLanes + l];
+            if (!permuted) P.srows[sl * kLanes + l] = q;
+            len = std::max(len, rlen(q));
         }
         stored += (int64_t)len * kLanes;
         if (stored >= ((int64_t)1 << 31)) throw std::runtime_error("SELL storage exceeds int32 indexing");
@@ -272,8 +287,8 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
     }
     P.scols.assign(stored, 0);
     P.smap.assign(stored, -1);
-    // lane's own index in the SpMV's row space (the base of its column deltas): the original row
-    // (legacy) or the new row; padding lanes take max(row, 0) (legacy) / nl - 1 (permuted)
+    // lane's own index in the space order (the base of its column deltas): its srows entry (global
+    // layout) or its slice position (windowed); padding lanes take max(row, 0) / nl - 1
     auto lane_base = [&](int64_t sl, int l) -> int64_t {
         const int64_t k = sl * kLanes + l;
         if (permuted) return std::min<int64_t>(k, nl - 1);
@@ -285,12 +300,12 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
             const int len = (P.sptr[sl + 1] - P.sptr[sl]) / kLanes;
             for (int l = 0; l < kLanes; ++l) {
                 const int64_t k = sl * kLanes + l;
-                const int32_t r = k < nl ? order[k] : -1;
+                const int32_t r = k < nl ? mrow(order[k]) : -1;  // mesh row
                 for (int j = 0; j < len; ++j) {
                     const int64_t t = P.sptr[sl] + (int64_t)j * kLanes + l;
                     if (r >= 0 && j < rowptr[r + 1] - rowptr[r]) {
                         const int32_t c = cols[rowptr[r] + j];
-                        P.scols[t] = permuted ? inv[c] : c;
+                        P.scols[t] = inv.empty() ? c : inv[c];
                         P.smap[t] = rowptr[r] + j;
                     } else {
                         P.scols[t] = (int32_t)lane_base(sl, l);  // padding: a valid column, value 0
@@ -318,9 +333,10 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
 
 extern "C" {
 
-// host-only plan of the FA SpMV order (tests / tools): perm (new -> old row) of nl entries, and
-// info[0..5] = base (0 legacy, 1 natural, 2 RCM), window, max |delta|, natural bandwidth, RCM
-// bandwidth (0 when not computed), stored SELL entries / nnz * 1e6 (padding, parts per million)
+// host-only plan of the FA SpMV order (tests / tools): perm (space row -> mesh row) of nl entries,
+// and info[0..5] = base (1 natural, 2 RCM), window rows (0: global length sort), max |column -
+// row| in the space order, natural bandwidth, RCM bandwidth (0 when not computed), stored SELL
+// entries / nnz * 1e6 (padding, parts per million)
 int cdfem_sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int32_t *perm, int64_t *info)
 {
     try {
@@ -332,7 +348,7 @@ int cdfem_sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int 
         P.nnz = rowptr[nl];
         cdfem::sell_build(P, nl, pl);
         for (int64_t k = 0; k < nl; ++k) perm[k] = pl.perm.empty() ? (int32_t)k : pl.perm[k];
-        info[0] = pl.perm.empty() ? 0 : pl.base;
+        info[0] = pl.base;
         info[1] = pl.window;
         info[2] = pl.max_delta;
         info[3] = pl.bw_natural;

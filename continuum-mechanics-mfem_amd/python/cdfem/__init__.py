@@ -281,12 +281,13 @@ def partition_rcb(mesh: Mesh, nranks) -> np.ndarray:
     return part
 
 
-SELL_ORDER = {"legacy": 0, "natural": 1, "rcm": 2, "auto": 3}
+SELL_ORDER = {"legacy": 0, "natural": 1, "rcm": 2, "auto": 3, "rcm_global": 4}
 
 
 def sell_plan(rowptr, cols, mode="auto"):
-    """Row order of the FA SpMV (host only; sell_plan.cpp): returns (perm, info) with perm[new] =
-    mesh row and info = {base, window, max_delta, bw_natural, bw_rcm, padding}."""
+    """Order of the FA SpMV (host only; sell_plan.cpp): returns (perm, info) with perm[space row] =
+    mesh row and info = {base (1 natural, 2 RCM), window (0: global length sort), max_delta,
+    bw_natural, bw_rcm, padding}."""
     rp, cl = _i32(rowptr), _i32(cols)
     nl = len(rp) - 1
     perm = np.zeros(nl, dtype=np.int32)

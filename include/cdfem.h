@@ -305,10 +305,12 @@ int cdfem_box_mesh(int dim, int nx, int ny, int nz, int order, int z0, int z1, d
  * centroids into nranks parts, part[e] = rank (MFEM's ParMesh calls METIS, which is absent here; any
  * partition defines the same global operator).  Deterministic: every rank computes the same one.  */
 int cdfem_partition_rcb(int dim, int ne, int nv, const double *elem_verts, int nranks, int32_t *part);
-/* Row order of the assembled operator's SpMV (host only; what cdfem_fa_setup builds with set_option
- * "sell_order" = mode: 0 legacy, 1 natural, 2 reverse Cuthill-McKee, 3 auto).  perm[new] = mesh row;
- * info[0..5] = base order (0 legacy, 1 natural, 2 RCM), window rows, max |column - row| in the new
- * order, natural bandwidth, RCM bandwidth (0 if not computed), stored SELL entries / nnz * 1e6.
+/* Order of the assembled operator's SpMV (host only; what cdfem_fa_setup builds with set_option
+ * "sell_order" = mode: 0 mesh order + global length sort, 1 natural + windows, 2 reverse
+ * Cuthill-McKee + windows, 3 auto (RCM + global when it halves the bandwidth, else 0), 4 RCM +
+ * global).  perm[space row] = mesh row; info[0..5] = base order (1 natural, 2 RCM), window rows
+ * (0: global length sort), max |column - row| in the space order, natural bandwidth, RCM
+ * bandwidth (0 if not computed), stored SELL entries / nnz * 1e6.
  * Internal layout choice with no reference counterpart (the reference multiplies in mesh order,
  * PETSc MatMult on MATAIJ); exported for tests and tools.  */
 int cdfem_sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int32_t *perm, int64_t *info);

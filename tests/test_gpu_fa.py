@@ -276,3 +276,48 @@ def test_ilu_rejected_for_cg_and_pa(gpu_ctx):
     gpu_ctx.pa_setup(kinds=5, kappa=0.1, mass=1.0)
     with pytest.raises(cdfem.CdfemError):
         gpu_ctx.solve(np.ones(m.nl), method="gmres", pc="ilu")
+
+
+@pytest.mark.parametrize("order", [2, 3, 4, 1])
+def test_fa_reordered_space_solves(gpu_ctx, order):
+    """The SpMV order (sell_order: 1 natural + windows, 2 RCM + windows, 3 auto = RCM + global on a
+    shuffled numbering, 4 RCM + global) on a randomly relabelled Kuhn P2 mesh: Krylov solves run in
+    the permuted space (B in / X out permuted once per solve).  Against the mesh-order SpMV
+    (sell_order 0) on the same shuffled mesh: Mult and constrained Mult bitwise (each row keeps its
+    CSR sum order); Jacobi GMRES and CG iterates to 1e-12 (only the dot-product order differs);
+    ILU(0) GMRES stays in the mesh order and is bitwise equal."""
+    gm = cdfem.kuhn_mesh(3, 8, 2, perturb=0.1)
+    rng = np.random.default_rng(31)
+    g = rng.permutation(gm.nl).astype(np.int32)
+    xyz = np.empty_like(gm.dof_xyz)
+    xyz[g] = gm.dof_xyz
+    sm = cdfem.Mesh(gm.dim, gm.order, gm.verts, g[gm.dofmap], gm.nl, np.sort(g[gm.ess]), xyz, simplex=True)
+    x = rng.uniform(-1, 1, sm.nl)
+    b = rng.uniform(-1, 1, sm.nl)
+    res = {}
+    try:
+        for so in (0, order):
+            gpu_ctx.set_option("sell_order", so)
+            gpu_ctx.upload_mesh(sm)
+            gpu_ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            _, B = gpu_ctx.form_linear_system(np.zeros(sm.nl), b)
+            r = [gpu_ctx.mult(x), gpu_ctx.mult(x, constrained=True)]
+            r.append(gpu_ctx.solve(B, method="gmres", pc="jacobi", restart=10, rel_tol=0.0, abs_tol=0.0,
+                                   max_iter=25)[0])
+            r.append(gpu_ctx.solve(B, method="gmres", pc="ilu", restart=10, rel_tol=0.0, abs_tol=0.0,
+                                   max_iter=15)[0])
+            gpu_ctx.fa_setup(kinds=5, kappa=0.1, mass=1.0)       # SPD: CG (den fused into the SpMV)
+            _, B2 = gpu_ctx.form_linear_system(np.zeros(sm.nl), b)
+            r.append(gpu_ctx.solve(B2, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30)[0])
+            xc, info = gpu_ctx.solve(B2, method="cg", pc="jacobi", rel_tol=1e-10, abs_tol=0.0, max_iter=500)
+            assert info["converged"]
+            r.append(xc)
+            res[so] = r
+        base, new = res[0], res[order]
+        np.testing.assert_array_equal(new[0], base[0])
+        np.testing.assert_array_equal(new[1], base[1])
+        for k in (2, 4, 5):
+            assert np.abs(new[k] - base[k]).max() <= 1e-12 * np.abs(base[k]).max(), k
+        np.testing.assert_array_equal(new[3], base[3])
+    finally:
+        gpu_ctx.set_option("sell_order", 3)

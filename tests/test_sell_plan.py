@@ -31,16 +31,19 @@ def _new_bandwidth(rp, cl, perm):
     return int(np.abs(inv[cl].astype(np.int64) - inv[rows]).max())
 
 
-@pytest.mark.parametrize("mode", ["legacy", "natural", "rcm", "auto"])
+@pytest.mark.parametrize("mode", ["legacy", "natural", "rcm", "auto", "rcm_global"])
 def test_plan_is_a_permutation(kuhn, mode):
     m, (rp, cl) = kuhn
     perm, info = cdfem.sell_plan(rp, cl, mode)
     assert np.array_equal(np.sort(perm), np.arange(m.nl))
     assert info["padding"] < 1.03
-    if mode == "legacy":
-        assert info["base"] == 0 and np.array_equal(perm, np.arange(m.nl))
+    if mode in ("legacy", "auto"):     # lattice numbering: the mesh order, global length sort
+        assert info["base"] == 1 and info["window"] == 0 and np.array_equal(perm, np.arange(m.nl))
+    elif mode == "rcm_global":
+        assert info["base"] == 2 and info["window"] == 0
+        assert info["max_delta"] == _new_bandwidth(rp, cl, perm) <= 32767
     else:
-        assert info["base"] in (1, 2) and info["window"] >= 512
+        assert info["base"] == (2 if mode == "rcm" else 1) and info["window"] >= 512
         assert info["max_delta"] == _new_bandwidth(rp, cl, perm) <= 32767
 
 
@@ -63,7 +66,7 @@ def test_shuffled_numbering_recovered_by_rcm(kuhn):
     _, nat = cdfem.sell_plan(rp2, cl2, "natural")
     perm, auto = cdfem.sell_plan(rp2, cl2, "auto")
     assert nat["bw_natural"] > m.nl // 2               # the shuffle destroyed the locality
-    assert auto["base"] == 2 and auto["bw_rcm"] < 2 * nat["bw_natural"] // 10
+    assert auto["base"] == 2 and auto["window"] == 0 and auto["bw_rcm"] < 2 * nat["bw_natural"] // 10
     assert auto["max_delta"] <= 32767
     perm2, _ = cdfem.sell_plan(rp2, cl2, "auto")
     assert np.array_equal(perm, perm2)                 # deterministic

@@ -79,7 +79,7 @@ def main():
     tj = json.load(open(p)) if os.path.exists(p) else {}
     wl = cfg["workload"]
     if wl.startswith("C4"):
-        key = f"c4_n{int(wl.split('Kuhn ')[1].split('^')[0])}_p2"
+        key = f"{wl.split(':')[0].lower()}_n{int(wl.split('Kuhn ')[1].split('^')[0])}_p2"
     else:
         n = int(wl.split("x")[0])
         order = int(wl.split("p=")[1].split(",")[0])
