@@ -471,21 +471,60 @@ class ElementTransformation {
 public:
     int ElementNo = -1;
     int Attribute = 1;
-    void Transform(const IntegrationPoint &, Vector &x) const
+    // a point transformation (the library evaluates coefficients at physical points: X is fixed),
+    // or an affine boundary element X0 + xi E0 + eta E1 (Mesh::GetBdrElementTransformation)
+    void Transform(const IntegrationPoint &ip, Vector &x) const
     {
         x.SetSize(dim_);
-        for (int k = 0; k < dim_; ++k) x[k] = X_[k];
+        for (int k = 0; k < dim_; ++k) x[k] = X_[k] + ip.x * E_[0][k] + ip.y * E_[1][k];
     }
     void SetPoint(int dim, const double *X)
     {
         dim_ = dim;
-        for (int k = 0; k < dim; ++k) X_[k] = X[k];
+        geom_ = Geometry::POINT;
+        for (int k = 0; k < dim; ++k) {
+            X_[k] = X[k];
+            E_[0][k] = E_[1][k] = 0.0;
+        }
     }
+    void SetAffine(int dim, Geometry::Type geom, const double *X0, const double *E0, const double *E1)
+    {
+        dim_ = dim;
+        geom_ = geom;
+        for (int k = 0; k < dim; ++k) {
+            X_[k] = X0[k];
+            E_[0][k] = E0 ? E0[k] : 0.0;
+            E_[1][k] = E1 ? E1[k] : 0.0;
+        }
+    }
+    Geometry::Type GetGeometryType() const { return geom_; }
 
 private:
     int dim_ = 0;
+    Geometry::Type geom_ = Geometry::POINT;
     double X_[3] = {0, 0, 0};
+    double E_[2][3] = {{0, 0, 0}, {0, 0, 0}};
 };
+
+// MFEM's Geometries (reference-element data): GetCenter, as BuildXDirichletBoundaryMarker uses it
+// (linear_convection_diffusion_1D.cpp:242)
+struct GeometryRefs {
+    const IntegrationPoint &GetCenter(int geom) const
+    {
+        static const IntegrationPoint c[Geometry::NumGeom] = {
+            {0.0, 0.0, 0.0, 1.0},                       // POINT
+            {0.5, 0.0, 0.0, 1.0},                       // SEGMENT
+            {1.0 / 3.0, 1.0 / 3.0, 0.0, 0.5},           // TRIANGLE
+            {0.5, 0.5, 0.0, 1.0},                       // SQUARE
+            {0.25, 0.25, 0.25, 1.0 / 6.0},              // TETRAHEDRON
+            {0.5, 0.5, 0.5, 1.0},                       // CUBE
+            {1.0 / 3.0, 1.0 / 3.0, 0.5, 0.5},           // PRISM
+            {0.4, 0.4, 0.2, 1.0 / 3.0}};                // PYRAMID
+        if (geom < 0 || geom >= Geometry::NumGeom) throw std::invalid_argument("GetCenter: geometry");
+        return c[geom];
+    }
+};
+inline const GeometryRefs Geometries{};
 
 // ---- coefficients --------------------------------------------------------------------------------
 class Coefficient {
@@ -778,7 +817,62 @@ public:
         vbuf_[2] = dim_ == 3 ? s_[2] * (double)iz / n_[2] : 0.0;
         return vbuf_;
     }
-    int GetNBE() const { return cartesian_ ? 0 : (int)battr_.size(); }
+    // boundary elements: the gmsh file's (segments in 2D, triangles in 3D), or the Cartesian box's
+    // faces in MFEM's attribute order (2D: bottom, right, top, left; 3D: z=0, y=0, x=sx, y=sy, x=0,
+    // z=sz)
+    int GetNBE() const
+    {
+        if (!cartesian_) return (int)battr_.size();
+        if (dim_ == 2) return 2 * (n_[0] + n_[1]);
+        return 2 * (n_[0] * n_[1] + n_[0] * n_[2] + n_[1] * n_[2]);
+    }
+    int GetBdrAttribute(int i) const
+    {
+        if (i < 0 || i >= GetNBE()) throw std::out_of_range("GetBdrAttribute");
+        if (!cartesian_) return battr_[(size_t)i];
+        int a = 0, j = 0;
+        CartesianFace(i, a, j);
+        return a;
+    }
+    ElementTransformation *GetBdrElementTransformation(int i) const
+    {
+        if (i < 0 || i >= GetNBE()) throw std::out_of_range("GetBdrElementTransformation");
+        double X0[3] = {0, 0, 0}, E0[3] = {0, 0, 0}, E1[3] = {0, 0, 0};
+        if (!cartesian_) {
+            const int nv = dim_;  // vertices per boundary element
+            const int32_t *b = &bv_[(size_t)i * nv];
+            for (int k = 0; k < dim_; ++k) {
+                X0[k] = vxyz_[(size_t)b[0] * dim_ + k];
+                E0[k] = vxyz_[(size_t)b[1] * dim_ + k] - X0[k];
+                if (nv == 3) E1[k] = vxyz_[(size_t)b[2] * dim_ + k] - X0[k];
+            }
+            btr_.SetAffine(dim_, dim_ == 2 ? Geometry::SEGMENT : Geometry::TRIANGLE, X0, E0, nv == 3 ? E1 : nullptr);
+        } else {
+            int a = 0, j = 0;
+            CartesianFace(i, a, j);
+            // the face's fixed axis / position and its two running axes
+            static const int fixed3[6] = {2, 1, 0, 1, 0, 2}, fixed2[4] = {1, 0, 1, 0};
+            const int fx = dim_ == 2 ? fixed2[a - 1] : fixed3[a - 1];
+            const bool hi = dim_ == 2 ? (a == 2 || a == 3) : (a == 3 || a == 4 || a == 6);
+            int run[2] = {-1, -1}, nr = 0;
+            for (int k = 0; k < dim_; ++k)
+                if (k != fx) run[nr++] = k;
+            X0[fx] = hi ? s_[fx] : 0.0;
+            const int i0 = j % n_[run[0]], i1 = nr > 1 ? j / n_[run[0]] : 0;
+            const double h0 = s_[run[0]] / n_[run[0]];
+            X0[run[0]] = i0 * h0;
+            E0[run[0]] = h0;
+            if (nr > 1) {
+                const double h1 = s_[run[1]] / n_[run[1]];
+                X0[run[1]] = i1 * h1;
+                E1[run[1]] = h1;
+            }
+            btr_.SetAffine(dim_, dim_ == 2 ? Geometry::SEGMENT : Geometry::SQUARE, X0, E0, nr > 1 ? E1 : nullptr);
+        }
+        btr_.ElementNo = i;
+        btr_.Attribute = GetBdrAttribute(i);
+        return &btr_;
+    }
     // uniform refinement: boxes halve h; triangles split into 4 (red refinement), boundary segments in 2
     virtual void UniformRefinement() { Refine(nullptr); }
 
@@ -821,6 +915,23 @@ protected:
     {
         if (nx < 1 || ny < 1 || nz < 1) throw std::invalid_argument("Mesh: element counts must be >= 1");
         SetAttributes();
+    }
+    // Cartesian boundary element i -> attribute a and its index j within that face
+    void CartesianFace(int i, int &a, int &j) const
+    {
+        int cnt[6];
+        if (dim_ == 2) {
+            cnt[0] = n_[0]; cnt[1] = n_[1]; cnt[2] = n_[0]; cnt[3] = n_[1];
+        } else {
+            cnt[0] = n_[0] * n_[1]; cnt[1] = n_[0] * n_[2]; cnt[2] = n_[1] * n_[2];
+            cnt[3] = n_[0] * n_[2]; cnt[4] = n_[1] * n_[2]; cnt[5] = n_[0] * n_[1];
+        }
+        j = i;
+        for (a = 1; a <= 2 * dim_; ++a) {
+            if (j < cnt[a - 1]) return;
+            j -= cnt[a - 1];
+        }
+        throw std::out_of_range("boundary element");
     }
     int64_t LatticeVertices() const
     {
@@ -896,6 +1007,7 @@ protected:
     std::vector<double> vxyz_;
     std::vector<int32_t> ev_, bv_, battr_;
     mutable double vbuf_[3] = {0, 0, 0};
+    mutable ElementTransformation btr_;
 };
 
 // ParMesh(MPI_COMM_WORLD, *mesh) (:300): the ranks' share of the elements.  A 3D box whose z element

@@ -868,6 +868,33 @@ static void poly1d(int p, double t, double *g, double *dg, double *d2g)
     }
 }
 
+/* kind 5: the erfc solution of c_t + c_x = c_xx / Pe on x > 0 with c(0, t) = 1, c(x, 0) = 0
+ * (linear_convection_diffusion_1D.cpp:128-166; exp(a) erfc(b) through the asymptotic series past
+ * b = 26, :128-144).  Pe in the kappa slot, t in the t slot; no forcing. */
+static double exp_times_erfc(double a, double b)
+{
+    if (b > 26.0) {
+        const double ib = 1.0 / b, ib2 = ib * ib;
+        const double er = ib / sqrt(ORC_PI) * (1.0 - 0.5 * ib2 + 0.75 * ib2 * ib2);
+        const double expo = a - b * b;
+        if (expo < -745.0) return 0.0;
+        if (expo > 709.0) return INFINITY;
+        return exp(expo) * er;
+    }
+    if (a > 709.0) return INFINITY;
+    return exp(a) * erfc(b);
+}
+static double erfc_profile(double x, double t, double pe)
+{
+    if (t <= 0.0) return 0.0;
+    const double diff = t / pe, root = sqrt(diff);
+    const double a1 = (x - t) / (2.0 * root), a2 = (x + t) / (2.0 * root);
+    const double gauss = -((x - t) * (x - t)) / (4.0 * diff);
+    const double c = 0.5 * erfc(a1) + sqrt(t * pe / ORC_PI) * exp(gauss) -
+                     0.5 * (1.0 + pe * x + pe * t) * exp_times_erfc(pe * x, a2);
+    return isfinite(c) ? c : 0.0;
+}
+
 ORC_API double orc_mms_u(const double *prm, const double *x)
 {
     int kind = (int)prm[0], dim = (int)prm[12];
@@ -886,6 +913,7 @@ ORC_API double orc_mms_u(const double *prm, const double *x)
         return sin(prm[10]) * cos(2.0 * dx * dx + 2.0 * dy * dy);
     }
     if (kind == 4) return rad_u(sqrt(x[0] * x[0] + x[1] * x[1]));
+    if (kind == 5) return erfc_profile(x[0], prm[10], prm[1]);
     return 0.0;
 }
 

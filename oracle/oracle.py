@@ -372,7 +372,7 @@ def gmres_ilu(A: CSR, b, F: CSR, restart=30, rtol=1e-10, atol=1e-12, max_it=500)
     return x, dict(converged=bool(conv), iterations=it.value, final_norm=fn.value)
 
 
-MMS_SIN, MMS_POLY, MMS_DIFFUSION_T, MMS_RADIAL = 1, 2, 3, 4
+MMS_SIN, MMS_POLY, MMS_DIFFUSION_T, MMS_RADIAL, MMS_ERFC = 1, 2, 3, 4, 5
 
 
 def mms_params(kind, dim, kappa=0.1, s=1.0, alpha=1.0, c=(1.0, -2.0, 0.5), modes=(3, 3, 3), t=0.0, p=1):
@@ -518,3 +518,46 @@ def ale_coefficients(kind, xy, t_old, t_new, alpha, dt):
         phi[:, 0] = phi[:, 1] = i1 * q
         div = i1 * (dax * ay + ax * day)
     return J, metric, phi, div
+
+
+def transient_three_peclet(mesh, dt, t_final, peclet=(1.0, 10.0, 100.0), simplex=False, rtol=1e-10, atol=1e-12,
+                           max_it=500):
+    """linear_convection_diffusion_1D.cpp:375-400,537-576 on the oracle: three uncoupled backward-Euler
+    systems (M + dt C(beta = (1, 0)) + (dt / Pe) K) c_k^{n+1} = M c_k^n on the unit square, Dirichlet
+    on x = 0 and x = 1 (BuildXDirichletBoundaryMarker, :219-266) set to the erfc solution (MMS_ERFC,
+    :128-166) at t^{n+1}, GMRES(30) + Jacobi per block (Input/petsc.opts).  Returns, per block, the
+    final absolute and relative L2 errors (order max(2, 2p + 3), :483-510) and the GMRES iterations."""
+    p = mesh.p
+    if simplex:
+        xyz = dof_coords_simplex(mesh)
+        asm = fa_assemble_simplex
+        err = l2_error_simplex
+    else:
+        xyz = mesh.dof_coords()
+        asm = fa_assemble
+        err = l2_error
+    ess = (np.abs(xyz[:, 0]) <= 1e-8) | (np.abs(xyz[:, 0] - 1.0) <= 1e-8)
+    marker = ess.astype(np.int32)
+    M = asm(mesh, s=1.0, kinds=MASS)
+    A = [asm(mesh, kappa=dt / pe, alpha=dt, s=1.0, c=(1.0, 0.0), kinds=DIFFUSION | CONVECTION | MASS) for pe in peclet]
+    c = [np.zeros(mesh.nl) for _ in peclet]
+    nsteps = int(np.ceil(t_final / dt - 1e-12))
+    its = [0, 0, 0]
+    for step in range(1, nsteps + 1):
+        t = step * dt
+        for k, pe in enumerate(peclet):
+            rhs = M.mult(c[k])
+            u = c[k].copy()
+            u[ess] = mms_u(mms_params(MMS_ERFC, 2, kappa=pe, t=t, p=p), xyz[ess])
+            Ac, B = form_linear_system(A[k], marker, u, rhs)
+            c[k], info = gmres(Ac, B, dinv=1.0 / Ac.diag(), rtol=rtol, atol=atol, max_it=max_it)
+            assert info["converged"]
+            its[k] += info["iterations"]
+    t = nsteps * dt
+    out = []
+    for k, pe in enumerate(peclet):
+        prm = mms_params(MMS_ERFC, 2, kappa=pe, t=t, p=p)
+        a = err(mesh, c[k], prm)
+        nrm = err(mesh, np.zeros(mesh.nl), prm)
+        out.append((a, a / nrm if nrm > 1e-14 else 0.0))
+    return out, its, nsteps, c
