@@ -352,7 +352,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
            const Tab<D1, Q1> T, const BrickGeom g, int zlo_shared, double *__restrict__ part,
-           const KrylovState *__restrict__ st)
+           const KrylovState *__restrict__ st, double *__restrict__ xs)
 {
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
@@ -364,6 +364,10 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     __shared__ double s_out[S3];
     if (st->done) return;
     const double beta = st->beta;
+    // x-fold: the previous iteration's x += alpha d_old, for the dofs this brick writes (d_old is
+    // already in registers for the new direction); pending unless this is the first apply
+    const bool fold = xs != nullptr && st->reserved[0] != 0;
+    const double alpha_prev = st->alpha;
     const int t = threadIdx.x;
     // launch-local brick -> global brick (a launch covers every g.bzs-th layer from g.bz0)
     const int bl = brick_id(g), nxy = g.nbx * g.nby;
@@ -379,7 +383,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     // Measured (tools/ab.py, in process): 241.1 vs 242.4 us per launch for the per-row form; the
     // other waves of the CU hide most of that latency.
     constexpr int NI = (S3 + 63) / 64;
-    double rv[NI], mv[NI], ov[NI];
+    double rv[NI], mv[NI], ov[NI], xv[NI];
     uint8_t ev[NI];
     int64_t gidv[NI];
 #pragma unroll
@@ -394,6 +398,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         mv[k] = dinv[gid];
         ov[k] = d_old[gid];
         ev[k] = ess[gid];
+        if (fold) xv[k] = __builtin_nontemporal_load(xs + gid);  // issued with the patch (one round trip)
     }
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
@@ -409,6 +414,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
             const bool writer = (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
             if (writer) {
                 d_new[gid] = dn;
+                if (fold) __builtin_nontemporal_store(xv[k] + alpha_prev * ov[k], xs + gid);
                 if (e && !(zlo_shared && gz == 0)) den += dn * dn;  // (A_c d)_i = d_i on ess dofs
             }
             v = e ? 0.0 : dn;
@@ -470,7 +476,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
                   const double *__restrict__ face, const uint8_t *__restrict__ ess, const BrickGeom g,
                   const FastDiv fdx, const FastDiv fdxy, int zlo_shared,
                   const double *__restrict__ remote_lo, const double *__restrict__ remote_hi,
-                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step)
+                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step, int fold_x)
 {
     constexpr int F = face_count<S>();
     constexpr int s1 = S - 1;
@@ -500,8 +506,10 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         const int gx = rem - gy * g.Lx;
         // every load is issued before any is consumed: which of q / the face partials holds this
         // dof's row sum depends on its lattice position only, and the essential flag selects last
-        const double di = d[gid], xi = x[gid], rold = r[gid], mi = dinv[gid];
+        // x-fold: x += alpha d moves to the next apply (k_brick_cg) and d is needed on ess rows only
         const bool is_ess = ess[gid] != 0;
+        const double di = (!fold_x || is_ess) ? d[gid] : 0.0, xi = fold_x ? 0.0 : x[gid];
+        const double rold = r[gid], mi = dinv[gid];
         double qi;
         if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
             int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
@@ -532,7 +540,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         if (remote_lo && gz == 0) qi += remote_lo[rem];
         if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
         if (is_ess) qi = di;
-        __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
+        if (!fold_x) __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
         const double ri = rold - alpha * qi;
         __builtin_nontemporal_store(ri, &r[gid]);
         if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
@@ -562,11 +570,12 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     do {                                                                                            \
         if (whole)                                                                                  \
             CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, V>), grid, block, 0, r, dinv, d_old, d_new, q,   \
-                         c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);  \
+                         c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state,   \
+                         c->xfold_x);                                                                \
         else                                                                                        \
             hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, V>), grid, block, 0, run.s, r, dinv, d_old,    \
                                d_new, q, c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared,          \
-                               c->d_part, c->d_state);                                              \
+                               c->d_part, c->d_state, c->xfold_x);                                  \
     } while (0)
     switch (c->brick_variant) {
     case 1: CDFEM_L(1); break;
@@ -632,17 +641,38 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     if (c->p == 1)
         hipLaunchKernelGGL(k_cg_update_faces<kBrick * 1 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
                            x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
-                           remote_hi, c->d_part, c->d_state, (int)den_step);
+                           remote_hi, c->d_part, c->d_state, (int)den_step, (int)(c->xfold_x != nullptr));
     else if (c->p == 2)
         hipLaunchKernelGGL(k_cg_update_faces<kBrick * 2 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
                            x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
-                           remote_hi, c->d_part, c->d_state, (int)den_step);
+                           remote_hi, c->d_part, c->d_state, (int)den_step, (int)(c->xfold_x != nullptr));
     else
         return hipErrorInvalidValue;
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (multi_rank(c)) return launch_fin_sum(c, (int)grid, 1);
     return launch_update_fin(c, (int)grid);
+}
+
+// x-fold flush after the CG loop: the last executed update's x += alpha_k d_k (k = iter - 1; d_k
+// sits in dA for even k, dB for odd k: the host alternates the two direction buffers)
+__global__ void __launch_bounds__(256)
+k_cg_xflush(double *__restrict__ x, const double *__restrict__ dA, const double *__restrict__ dB, int64_t n,
+            const KrylovState *__restrict__ st)
+{
+    if (st->reserved[0] == 0) return;
+    const double alpha = st->alpha;
+    const double *d = ((st->iter - 1) & 1) == 0 ? dA : dB;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        x[i] = x[i] + alpha * d[i];
+}
+
+hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *dA, const double *dB)
+{
+    const int64_t need = (c->nl + 255) / 256;
+    hipLaunchKernelGGL(k_cg_xflush, dim3((unsigned)(need < 8192 ? need : 8192)), dim3(256), 0, c->stream, x, dA, dB,
+                       (int64_t)c->nl, c->d_state);
+    return hipGetLastError();
 }
 
 // local partial sums of q = A d on the shared interface planes (what the neighbour must add)

@@ -346,6 +346,14 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     const int check = p.check_every > 0 ? p.check_every : 16;
     const bool mr = multi_rank(c);
     double *red = c->d_state->red;  // device scalars awaiting the all-reduce
+    // x-fold: iteration k's x += alpha_k d_k is done by apply k + 1 (which already streams d_k) and
+    // the last one by k_cg_xflush; the update then streams 40 instead of 57 B/dof
+    struct FoldGuard {
+        cdfem_ctx *c;
+        ~FoldGuard() { c->xfold_x = nullptr; }
+    } fold_guard{c};
+    c->xfold_x = c->cg_xfold ? x : nullptr;
+    double *const d_even = dcur, *const d_odd = dprev;  // apply k writes direction k here
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     if (mr) {
@@ -414,6 +422,10 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (c->h_state->done || launched >= p.max_iter) break;
+    }
+    if (c->xfold_x) {
+        HIPCHK(launch_cg_xflush(c, x, d_even, d_odd));
+        HIPCHK(hipStreamSynchronize(c->stream));
     }
     const auto t1 = std::chrono::steady_clock::now();
     prof_collect(c);
@@ -1446,6 +1458,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "sell_order") {  // read when the FA pattern is built (once per mesh)
             if (value < 0 || value > 4) throw ArgError("sell_order must be 0..4 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM)");
             c->sell_mode = value;
+        } else if (k == "cg_xfold") {
+            if (value < 0 || value > 1) throw ArgError("cg_xfold must be 0 or 1");
+            c->cg_xfold = value;
         } else if (k == "spmv_variant") {
             if (value < 0 || value > 1) throw ArgError("spmv_variant must be 0 or 1");
             c->spmv_variant = value;

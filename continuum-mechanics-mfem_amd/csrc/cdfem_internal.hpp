@@ -200,6 +200,8 @@ struct cdfem_ctx {
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
+    int cg_xfold = 1;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply
+    double *xfold_x = nullptr;          // the solution vector while a folded brick CG loop runs
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
     int spmv_variant = 0;               // set_option "spmv_variant": SpMV inner loop, 0 = 4 loads in flight, 1 = software-pipelined (A/B)
@@ -332,6 +334,8 @@ hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double
                                 const double *dinv);
 // pack the local partial sums of q on the shared interface planes into d_if[0] / d_if[2]
 hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q, hipStream_t s = nullptr);
+// brick CG x-fold: flush the pending x += alpha d after the loop (dA / dB: the even / odd directions)
+hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *dA, const double *dB);
 hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
                                   double *d_new, double *q, hipStream_t s);
 

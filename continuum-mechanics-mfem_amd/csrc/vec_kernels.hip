@@ -205,6 +205,7 @@ __device__ inline void cg_init_logic(KrylovState *st, double nom, double rel_tol
     st->done = 0;
     st->first_den = 1;  // next den is the initial one
     st->beta = 0.0;
+    st->reserved[0] = 0;  // no x update pending (brick CG x-fold)
     if (nom < 0.0) {             // preconditioner not positive definite
         st->done = 1;
         st->final_iter = 0;
@@ -219,6 +220,7 @@ __device__ inline void cg_init_logic(KrylovState *st, double nom, double rel_tol
 __device__ inline void cg_update_logic(KrylovState *st, double betanom)
 {
     st->betanom = betanom;
+    st->reserved[0] = 1;  // brick CG x-fold: this iteration's x += alpha d is pending (next apply / flush)
     const int i = st->iter;
     if (betanom < 0.0) {
         st->done = 1; st->converged = 0; st->final_iter = i;

@@ -391,6 +391,35 @@ def test_brick_cg_bench_operator_parity(gpu_ctx, n, p):
     np.testing.assert_array_equal(xg, xg2)
 
 
+@pytest.mark.parametrize("max_iter,rel_tol,check", [(30, 0.0, 16), (31, 0.0, 7), (2000, 1e-10, 16), (1, 0.0, 16),
+                                                     (0, 0.0, 16)])
+def test_brick_cg_xfold_bitwise(gpu_ctx, max_iter, rel_tol, check):
+    """set_option("cg_xfold"): iteration k's x += alpha_k d_k moves into apply k + 1 and the last one
+    into the flush after the loop.  Same arithmetic on the same operands: the solution is bitwise
+    the unfolded one, whether the loop stops at max_iter (even / odd counts), on convergence, or
+    before the first update (max_iter 0 / 1); with essential values set (d on ess rows)."""
+    n, p = 8, 2
+    om = O.BoxMesh(3, n, p, perturb=0.1)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    rng = np.random.default_rng(77)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    _, B = gpu_ctx.form_linear_system(u, rng.uniform(-1, 1, om.nl))
+    out = {}
+    try:
+        for fold in (0, 1):
+            gpu_ctx.set_option("cg_xfold", fold)
+            out[fold] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=rel_tol, abs_tol=0.0,
+                                      max_iter=max_iter, check_every=check)
+    finally:
+        gpu_ctx.set_option("cg_xfold", 1)
+    (x0, i0), (x1, i1) = out[0], out[1]
+    assert i0["iterations"] == i1["iterations"] and i0["converged"] == i1["converged"]
+    np.testing.assert_array_equal(x1, x0)
+
+
 def test_brick_full_size_matches_generic(gpu_ctx):
     """64^3 p=2: brick and generic paths agree (different E->L summation order only)."""
     gm = cdfem.box_mesh(3, 64, 2, with_coords=False)
