@@ -414,7 +414,7 @@ def test_brick_cg_xfold_bitwise(gpu_ctx, max_iter, rel_tol, check):
             out[fold] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=rel_tol, abs_tol=0.0,
                                       max_iter=max_iter, check_every=check)
     finally:
-        gpu_ctx.set_option("cg_xfold", 1)
+        gpu_ctx.set_option("cg_xfold", 0)
     (x0, i0), (x1, i1) = out[0], out[1]
     assert i0["iterations"] == i1["iterations"] and i0["converged"] == i1["converged"]
     np.testing.assert_array_equal(x1, x0)
