@@ -1184,7 +1184,12 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
         if (c->geom != 1) throw UnsupportedError("full assembly is implemented for simplex meshes");
         if (!c->d_rowptr) {  // CSR pattern + contribution lists: once per mesh
             // a multi-rank partition keeps the mesh order (its shared-dof exchange indexes L-vectors)
-            FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl, multi_rank(c) ? 0 : c->sell_mode);
+            // dof coordinates for the geometric SpMV order (simplex geometry is on the host)
+            std::vector<double> xyz;
+            if (!multi_rank(c) && (c->sell_mode == 3 || c->sell_mode == 5) && !c->h_verts.empty())
+                xyz = simplex_dof_coords(c->dim, c->p, c->ne, c->nd, c->nl, c->h_verts, c->h_dofs);
+            FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl, multi_rank(c) ? 0 : c->sell_mode, c->dim,
+                                           xyz.empty() ? nullptr : xyz.data());
             c->nnz = P.nnz;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
             c->d_cols = dalloc<int32_t>(P.cols.size());
@@ -1456,7 +1461,8 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;
         } else if (k == "sell_order") {  // read when the FA pattern is built (once per mesh)
-            if (value < 0 || value > 4) throw ArgError("sell_order must be 0..4 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM)");
+            if (value < 0 || value > 5)
+                throw ArgError("sell_order must be 0..5 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric)");
             c->sell_mode = value;
         } else if (k == "cg_xfold") {
             if (value < 0 || value > 1) throw ArgError("cg_xfold must be 0 or 1");

@@ -355,17 +355,22 @@ struct FaPattern {
     bool windowed = false;       // slices cut from the space order directly (no srows)
 };
 // SpMV order (sell_plan.cpp): 0 natural + global sort, 1 natural + windows, 2 RCM + windows,
-// 3 auto (RCM + global or mode 0), 4 RCM + global
+// 3 auto (mode 0, geometric or RCM + global), 4 RCM + global, 5 geometric + global
 struct SellPlan {
-    int mode = 0, base = 1;
+    int mode = 0, base = 1;  // base: 1 natural, 2 RCM, 3 geometric
     bool windowed = false;
-    int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0;
+    int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0, bw_geometric = 0;
     std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
 };
 std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
-SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode);
+SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim = 0,
+                   const double *xyz = nullptr);
+// dof coordinates of a simplex space (P1, P2, triangle P3 nodes; element-affine map), nl * dim
+std::vector<double> simplex_dof_coords(int dim, int p, int ne, int nd, int64_t nl, const std::vector<double> &verts,
+                                       const std::vector<int32_t> &dofs);
 void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl);
-FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl, int sell_mode);
+FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl, int sell_mode,
+                           int dim = 0, const double *dof_xyz = nullptr);
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq, double kappa, double alpha,
                                const double *conv, const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);

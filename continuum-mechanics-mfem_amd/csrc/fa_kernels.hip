@@ -48,7 +48,8 @@ static inline int64_t ee_index(int e, int i, int j, int nd)
     return ((int64_t)(e / kLanes) * nd * nd + (int64_t)i * nd + j) * kLanes + e % kLanes;
 }
 
-FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int64_t nl, int sell_mode)
+FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int64_t nl, int sell_mode, int dim,
+                           const double *dof_xyz)
 {
     // dof -> incidences (e * nd + l), ascending
     std::vector<int64_t> cnt(nl + 1, 0);
@@ -131,7 +132,7 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     });
     // SpMV layout: SELL-64 over the rows in the plan's order (sell_plan.cpp)
     P.rowptr = std::move(rowptr);
-    sell_build(P, nl, sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode));
+    sell_build(P, nl, sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode, dim, dof_xyz));
     return P;
 }
 

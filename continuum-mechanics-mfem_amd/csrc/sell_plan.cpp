@@ -4,9 +4,11 @@
 // :349-375) multiplies in the mesh's own dof numbering.  Here the SpMV may run on a row/column
 // permutation of the same matrix, A' = P A P^T (the "space" order; the Krylov solve then runs in it,
 // capi.hip cdfem_solve), and the SELL-64 slices are cut from that space in one of two layouts:
-//   base order  the mesh numbering ("natural") or reverse Cuthill-McKee of the CSR graph (for
-//               shuffled / unstructured numberings: a small bandwidth keeps the x gathers L2-local
-//               and the 16-bit column deltas valid);
+//   base order  the mesh numbering ("natural"), a geometric order (dof coordinates quantised to
+//               the mean dof spacing, sorted by (z, y, x): a lattice's own order whatever the
+//               numbering, and a slab order on unstructured meshes), or reverse Cuthill-McKee of the
+//               CSR graph (when no coordinates are given).  A small bandwidth keeps the x gathers
+//               L2-local and the 16-bit column deltas valid;
 //   layout      global: rows sorted by length over the whole matrix, a row index per lane (the
 //               measured best on the lattice numbering);
 //               windows: the base order cut into windows of W rows, inside a window rows grouped
@@ -18,9 +20,12 @@
 //
 // sell_order: 0 = natural + global (the mesh order, no permutation), 1 = natural + windows,
 //             2 = RCM + windows, 3 = auto (mode 0 when the mesh order is banded: 16-bit deltas and
-//             bandwidth under nl / 8; else RCM + global when its bandwidth is under half the
-//             natural one), 4 = RCM + global.
+//             bandwidth under nl / 8; else the geometric order when coordinates are given and it
+//             is banded that way; else RCM + global when its bandwidth is under half the natural
+//             one), 4 = RCM + global, 5 = geometric + global.
 #include <algorithm>
+#include <array>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
@@ -145,19 +150,104 @@ std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t 
     return order;
 }
 
-SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode)
+std::vector<double> simplex_dof_coords(int dim, int p, int ne, int nd, int64_t nl, const std::vector<double> &verts,
+                                       const std::vector<int32_t> &dofs)
+{
+    // reference nodes (vertex 0 at the origin, vertex k at e_k), in the local dof order
+    std::vector<std::array<double, 3>> ref;
+    for (int v = 0; v <= dim; ++v) {
+        std::array<double, 3> x{0, 0, 0};
+        if (v > 0) x[v - 1] = 1.0;
+        ref.push_back(x);
+    }
+    if (dim == 2 && p == 3) {
+        double X[10][2];
+        p3_tri_nodes(X);
+        ref.clear();
+        for (auto &r : X) ref.push_back({r[0], r[1], 0.0});
+    } else if (p == 2) {
+        const int ne_ = dim == 3 ? 6 : 3;
+        for (int e = 0; e < ne_; ++e) {
+            const int a = dim == 3 ? kSimplexEdge[e][0] : kTriEdge[e][0], b = dim == 3 ? kSimplexEdge[e][1] : kTriEdge[e][1];
+            std::array<double, 3> x{0, 0, 0};
+            for (int k = 0; k < 3; ++k) x[k] = 0.5 * (ref[a][k] + ref[b][k]);
+            ref.push_back(x);
+        }
+    }
+    if ((int)ref.size() != nd) throw std::runtime_error("simplex_dof_coords: unsupported element");
+    std::vector<double> xyz((size_t)nl * dim, 0.0);
+    for (int e = 0; e < ne; ++e) {
+        const double *V = &verts[(size_t)e * (dim + 1) * dim];
+        for (int l = 0; l < nd; ++l) {
+            const int64_t g = dofs[(size_t)e * nd + l];
+            for (int k = 0; k < dim; ++k) {
+                double x = V[k];
+                for (int m = 0; m < dim; ++m) x += ref[l][m] * (V[(m + 1) * dim + k] - V[k]);
+                xyz[(size_t)g * dim + k] = x;
+            }
+        }
+    }
+    return xyz;
+}
+
+// geometric order: dof coordinates quantised to the mean dof spacing h = (box volume / nl)^(1/dim)
+// and sorted by (z cell, y cell, x); ties by mesh index (deterministic)
+std::vector<int32_t> geometric_order(int64_t nl, int dim, const double *xyz)
+{
+    double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+    for (int k = 0; k < dim; ++k) {
+        lo[k] = hi[k] = xyz[k];
+        for (int64_t i = 1; i < nl; ++i) {
+            lo[k] = std::min(lo[k], xyz[i * dim + k]);
+            hi[k] = std::max(hi[k], xyz[i * dim + k]);
+        }
+    }
+    double vol = 1.0;
+    for (int k = 0; k < dim; ++k) vol *= std::max(hi[k] - lo[k], 1e-300);
+    const double h = std::pow(vol / (double)std::max<int64_t>(nl, 1), 1.0 / dim);
+    std::vector<int64_t> cz(nl), cy(nl);
+    for (int64_t i = 0; i < nl; ++i) {
+        cy[i] = dim >= 2 ? std::llround((xyz[i * dim + 1] - lo[1]) / h) : 0;
+        cz[i] = dim >= 3 ? std::llround((xyz[i * dim + 2] - lo[2]) / h) : 0;
+    }
+    std::vector<int32_t> order(nl);
+    for (int64_t i = 0; i < nl; ++i) order[i] = (int32_t)i;
+    std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+        if (cz[a] != cz[b]) return cz[a] < cz[b];
+        if (cy[a] != cy[b]) return cy[a] < cy[b];
+        const double xa = xyz[(int64_t)a * dim], xb = xyz[(int64_t)b * dim];
+        return xa != xb ? xa < xb : a < b;
+    });
+    return order;
+}
+
+SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim, const double *xyz)
 {
     SellPlan pl;
     pl.mode = mode;
     pl.base = 1;
-    if (mode < 0 || mode > 4) throw std::runtime_error("sell_plan: bad mode");
+    if (mode < 0 || mode > 5) throw std::runtime_error("sell_plan: bad mode");
+    if (mode == 5 && !xyz) throw std::runtime_error("sell_plan: the geometric order needs dof coordinates");
     if (mode == 0 || nl == 0) return pl;
     // base order
     std::vector<int32_t> bo, bp;  // base position -> row, row -> base position (empty: identity)
     pl.bw_natural = bandwidth(nl, rowptr, cols, {});
+    auto banded = [&](int64_t bw) { return bw <= 32767 && bw * 8 <= nl; };
+    if ((mode == 3 || mode == 5) && xyz && dim >= 1 && dim <= 3 && !(mode == 3 && banded(pl.bw_natural))) {
+        std::vector<int32_t> go = geometric_order(nl, dim, xyz), gp(nl);
+        for (int64_t k = 0; k < nl; ++k) gp[go[k]] = (int32_t)k;
+        pl.bw_geometric = bandwidth(nl, rowptr, cols, gp);
+        if (mode == 5 || banded(pl.bw_geometric)) {
+            pl.base = 3;
+            pl.windowed = false;
+            pl.max_delta = pl.bw_geometric;
+            pl.perm = std::move(go);
+            return pl;
+        }
+    }
     bool rcm = mode == 2 || mode == 4;
     // the mesh order is banded (16-bit deltas, bandwidth under nl / 8): mode 0 without the RCM pass
-    if (mode == 3 && pl.bw_natural <= 32767 && pl.bw_natural * 8 <= nl) return pl;
+    if (mode == 3 && banded(pl.bw_natural)) return pl;
     if (mode >= 2) {
         bo = rcm_order(nl, rowptr, cols);
         bp.resize(nl);
@@ -334,14 +424,16 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
 extern "C" {
 
 // host-only plan of the FA SpMV order (tests / tools): perm (space row -> mesh row) of nl entries,
-// and info[0..5] = base (1 natural, 2 RCM), window rows (0: global length sort), max |column -
-// row| in the space order, natural bandwidth, RCM bandwidth (0 when not computed), stored SELL
-// entries / nnz * 1e6 (padding, parts per million)
-int cdfem_sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int32_t *perm, int64_t *info)
+// and info[0..6] = base (1 natural, 2 RCM, 3 geometric), window rows (0: global length sort), max
+// |column - row| in the space order, natural bandwidth, RCM bandwidth (0 when not computed),
+// stored SELL entries / nnz * 1e6 (padding, parts per million), geometric bandwidth (0 when not
+// computed)
+int cdfem_sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim, const double *xyz,
+                    int32_t *perm, int64_t *info)
 {
     try {
         if (nl < 0 || (nl > 0 && (!rowptr || !cols)) || !perm || !info) return CDFEM_ERR_ARG;
-        cdfem::SellPlan pl = cdfem::sell_plan(nl, rowptr, cols, mode);
+        cdfem::SellPlan pl = cdfem::sell_plan(nl, rowptr, cols, mode, dim, xyz);
         cdfem::FaPattern P;
         P.rowptr.assign(rowptr, rowptr + nl + 1);
         P.cols.assign(cols, cols + rowptr[nl]);
@@ -354,6 +446,7 @@ int cdfem_sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int 
         info[3] = pl.bw_natural;
         info[4] = pl.bw_rcm;
         info[5] = P.nnz ? (int64_t)((double)P.sptr.back() / (double)P.nnz * 1e6) : 0;
+        info[6] = pl.bw_geometric;
         return CDFEM_OK;
     } catch (const std::exception &) {
         return CDFEM_ERR_ARG;

@@ -117,7 +117,7 @@ def _declare(L):
         "cdfem_prolongate": (C.c_int, [vp, vp, vp, C.c_int]),
         "cdfem_comm_info": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
         "cdfem_partition_rcb": (C.c_int, [C.c_int, C.c_int, C.c_int, _dp, C.c_int, _ip]),
-        "cdfem_sell_plan": (C.c_int, [i64, _ip, _ip, C.c_int, _ip, C.POINTER(i64)]),
+        "cdfem_sell_plan": (C.c_int, [i64, _ip, _ip, C.c_int, C.c_int, _dp, _ip, C.POINTER(i64)]),
         "cdfem_local_space_sizes": (C.c_int, [C.c_int, C.c_int, i64, _ip, _ip, C.c_int, C.POINTER(C.c_int),
                                               C.POINTER(i64), C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(i64)]),
         "cdfem_local_space": (C.c_int, [C.c_int, C.c_int, i64, _ip, _ip, C.c_int, _ip, _ip, C.POINTER(i64), _ip,
@@ -281,25 +281,27 @@ def partition_rcb(mesh: Mesh, nranks) -> np.ndarray:
     return part
 
 
-SELL_ORDER = {"legacy": 0, "natural": 1, "rcm": 2, "auto": 3, "rcm_global": 4}
+SELL_ORDER = {"legacy": 0, "natural": 1, "rcm": 2, "auto": 3, "rcm_global": 4, "geometric": 5}
 
 
-def sell_plan(rowptr, cols, mode="auto"):
+def sell_plan(rowptr, cols, mode="auto", xyz=None):
     """Order of the FA SpMV (host only; sell_plan.cpp): returns (perm, info) with perm[space row] =
-    mesh row and info = {base (1 natural, 2 RCM), window (0: global length sort), max_delta,
-    bw_natural, bw_rcm, padding}."""
+    mesh row and info = {base (1 natural, 2 RCM, 3 geometric), window (0: global length sort),
+    max_delta, bw_natural, bw_rcm, padding, bw_geometric}; xyz = (nl, dim) dof coordinates or None."""
     rp, cl = _i32(rowptr), _i32(cols)
     nl = len(rp) - 1
     perm = np.zeros(nl, dtype=np.int32)
-    info = np.zeros(6, dtype=np.int64)
+    info = np.zeros(7, dtype=np.int64)
+    X = None if xyz is None else _f64(xyz)
     rc = lib().cdfem_sell_plan(nl, rp.ctypes.data_as(_ip), cl.ctypes.data_as(_ip),
-                               SELL_ORDER.get(mode, mode), perm.ctypes.data_as(_ip),
-                               info.ctypes.data_as(C.POINTER(C.c_int64)))
+                               SELL_ORDER.get(mode, mode), 0 if X is None else X.shape[1], _p(X),
+                               perm.ctypes.data_as(_ip), info.ctypes.data_as(C.POINTER(C.c_int64)))
     if rc:
         raise CdfemError(rc, "cdfem_sell_plan failed")
     keys = ("base", "window", "max_delta", "bw_natural", "bw_rcm")
     d = {k: int(v) for k, v in zip(keys, info[:5])}
     d["padding"] = info[5] / 1e6
+    d["bw_geometric"] = int(info[6])
     return perm, d
 
 

@@ -307,13 +307,16 @@ int cdfem_box_mesh(int dim, int nx, int ny, int nz, int order, int z0, int z1, d
 int cdfem_partition_rcb(int dim, int ne, int nv, const double *elem_verts, int nranks, int32_t *part);
 /* Order of the assembled operator's SpMV (host only; what cdfem_fa_setup builds with set_option
  * "sell_order" = mode: 0 mesh order + global length sort, 1 natural + windows, 2 reverse
- * Cuthill-McKee + windows, 3 auto (RCM + global when it halves the bandwidth, else 0), 4 RCM +
- * global).  perm[space row] = mesh row; info[0..5] = base order (1 natural, 2 RCM), window rows
- * (0: global length sort), max |column - row| in the space order, natural bandwidth, RCM
- * bandwidth (0 if not computed), stored SELL entries / nnz * 1e6.
+ * Cuthill-McKee + windows, 3 auto (the mesh order when banded, else the geometric order when xyz is
+ * given and banded, else RCM + global when it halves the bandwidth), 4 RCM + global, 5 geometric +
+ * global).  xyz: nl * dim dof coordinates or NULL (cdfem_fa_setup passes the simplex space's nodes).
+ * perm[space row] = mesh row; info[0..6] = base order (1 natural, 2 RCM, 3 geometric), window rows
+ * (0: global length sort), max |column - row| in the space order, natural bandwidth, RCM bandwidth
+ * (0 if not computed), stored SELL entries / nnz * 1e6, geometric bandwidth (0 if not computed).
  * Internal layout choice with no reference counterpart (the reference multiplies in mesh order,
  * PETSc MatMult on MATAIJ); exported for tests and tools.  */
-int cdfem_sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int32_t *perm, int64_t *info);
+int cdfem_sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim, const double *xyz,
+                    int32_t *perm, int64_t *info);
 /* The rank-local H1 space of a partition (host only): elems = the rank's elements (ascending global
  * index), loc_dofs = their dofs in local numbering (dofs owned by lower ranks first, then the owned
  * ones, each by ascending global id), l2g = global id of each local dof, and the neighbour lists that

@@ -20,7 +20,7 @@ def _pattern(dofmap, nl):
 
 @pytest.fixture(scope="module")
 def kuhn():
-    m = cdfem.kuhn_mesh(3, 14, 2, with_coords=False)
+    m = cdfem.kuhn_mesh(3, 14, 2, with_coords=True)
     return m, _pattern(m.dofmap, m.nl)
 
 
@@ -93,3 +93,24 @@ def test_bad_mode_rejected(kuhn):
     _, (rp, cl) = kuhn
     with pytest.raises(cdfem.CdfemError):
         cdfem.sell_plan(rp, cl, 7)
+
+
+def test_shuffled_numbering_recovered_by_geometric_order(kuhn):
+    """With dof coordinates (what cdfem_fa_setup passes for simplex spaces) auto takes the geometric
+    order: coordinates quantised to the mean dof spacing, sorted by (z, y, x).  On a shuffled lattice
+    that is the lattice's own order, so the bandwidth is the natural one's."""
+    m, (rp, cl) = kuhn
+    g = np.random.default_rng(5).permutation(m.nl).astype(np.int32)
+    rp2, cl2 = _pattern(g[m.dofmap], m.nl)
+    xyz = np.empty_like(m.dof_xyz)
+    xyz[g] = m.dof_xyz
+    perm, info = cdfem.sell_plan(rp2, cl2, "auto", xyz=xyz)
+    _, nat = cdfem.sell_plan(rp, cl, "rcm_global")
+    assert info["base"] == 3 and info["window"] == 0
+    assert info["bw_geometric"] == info["max_delta"] == nat["bw_natural"]
+    np.testing.assert_array_equal(perm, g)          # the lattice order: space row k = mesh row g[k]
+    # lattice numbering: auto keeps the mesh order (no coordinates needed, no permutation)
+    p0, i0 = cdfem.sell_plan(rp, cl, "auto", xyz=m.dof_xyz)
+    assert i0["base"] == 1 and np.array_equal(p0, np.arange(m.nl))
+    with pytest.raises(cdfem.CdfemError):
+        cdfem.sell_plan(rp, cl, "geometric")         # the geometric order needs coordinates
