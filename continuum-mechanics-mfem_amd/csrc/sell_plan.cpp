@@ -15,8 +15,10 @@
 //               by length (descending) and stencil signature, then base position; the space order
 //               IS the slice order (no row index stream, whole-line y stores, 1.00x HBM traffic),
 //               W the largest candidate for which every |column' - row'| fits 16 bits.
-// Every row keeps its CSR entry order, so each row sum is bitwise the one of the unpermuted SpMV;
-// only the Krylov dot products see the new order.
+// In the mesh order every row keeps its CSR entry order (bitwise the CSR sums).  In a permuted space
+// a row's entries are summed in ascending space column, so that the j-th entries of a slice's rows
+// are the same stencil neighbour (coalesced x gathers); the sums then differ from the CSR order's by
+// rounding only, and the Krylov dot products run in the space order.
 //
 // sell_order: 0 = natural + global (the mesh order, no permutation), 1 = natural + windows,
 //             2 = RCM + windows, 3 = auto (mode 0 when the mesh order is banded: 16-bit deltas and
@@ -386,17 +388,26 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
         return r >= 0 ? r : 0;
     };
     par_for(ns, [&](int64_t s0, int64_t s1) {
+        std::vector<int32_t> ent;
         for (int64_t sl = s0; sl < s1; ++sl) {
             const int len = (P.sptr[sl + 1] - P.sptr[sl]) / kLanes;
             for (int l = 0; l < kLanes; ++l) {
                 const int64_t k = sl * kLanes + l;
                 const int32_t r = k < nl ? mrow(order[k]) : -1;  // mesh row
+                // a row's entries in ascending space column: in a permuted space the j-th entries
+                // of a slice's rows are then the same stencil neighbour (one short contiguous run
+                // of x per gather); the mesh order keeps its CSR order (bitwise the CSR sums)
+                ent.clear();
+                if (r >= 0)
+                    for (int32_t q = rowptr[r]; q < rowptr[r + 1]; ++q) ent.push_back(q);
+                if (!inv.empty())
+                    std::sort(ent.begin(), ent.end(), [&](int32_t a, int32_t b) { return inv[cols[a]] < inv[cols[b]]; });
                 for (int j = 0; j < len; ++j) {
                     const int64_t t = P.sptr[sl] + (int64_t)j * kLanes + l;
-                    if (r >= 0 && j < rowptr[r + 1] - rowptr[r]) {
-                        const int32_t c = cols[rowptr[r] + j];
+                    if (r >= 0 && j < (int)ent.size()) {
+                        const int32_t c = cols[ent[j]];
                         P.scols[t] = inv.empty() ? c : inv[c];
-                        P.smap[t] = rowptr[r] + j;
+                        P.smap[t] = ent[j];
                     } else {
                         P.scols[t] = (int32_t)lane_base(sl, l);  // padding: a valid column, value 0
                     }

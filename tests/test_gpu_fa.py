@@ -278,14 +278,16 @@ def test_ilu_rejected_for_cg_and_pa(gpu_ctx):
         gpu_ctx.solve(np.ones(m.nl), method="gmres", pc="ilu")
 
 
-@pytest.mark.parametrize("order", [2, 3, 4, 1])
+@pytest.mark.parametrize("order", [2, 3, 4, 5, 1])
 def test_fa_reordered_space_solves(gpu_ctx, order):
-    """The SpMV order (sell_order: 1 natural + windows, 2 RCM + windows, 3 auto = RCM + global on a
-    shuffled numbering, 4 RCM + global) on a randomly relabelled Kuhn P2 mesh: Krylov solves run in
+    """The SpMV order (sell_order: 1 natural + windows, 2 RCM + windows, 3 auto = geometric + global
+    on a shuffled numbering, 4 RCM + global, 5 geometric + global) on a randomly relabelled Kuhn P2
+    mesh: Krylov solves run in
     the permuted space (B in / X out permuted once per solve).  Against the mesh-order SpMV
-    (sell_order 0) on the same shuffled mesh: Mult and constrained Mult bitwise (each row keeps its
-    CSR sum order); Jacobi GMRES and CG iterates to 1e-12 (only the dot-product order differs);
-    ILU(0) GMRES stays in the mesh order and is bitwise equal."""
+    (sell_order 0) on the same shuffled mesh: Mult and constrained Mult to 1e-14 (a row sums its
+    entries in space-column order instead of CSR order), Jacobi GMRES and CG iterates to 1e-12 (the
+    dot products run in the space order), ILU(0) GMRES (mesh-order factors, the permuted SpMV around
+    each apply) to 1e-12."""
     gm = cdfem.kuhn_mesh(3, 8, 2, perturb=0.1)
     rng = np.random.default_rng(31)
     g = rng.permutation(gm.nl).astype(np.int32)
@@ -314,10 +316,9 @@ def test_fa_reordered_space_solves(gpu_ctx, order):
             r.append(xc)
             res[so] = r
         base, new = res[0], res[order]
-        np.testing.assert_array_equal(new[0], base[0])
-        np.testing.assert_array_equal(new[1], base[1])
-        for k in (2, 4, 5):
+        for k in (0, 1):
+            assert np.abs(new[k] - base[k]).max() <= 1e-14 * np.abs(base[k]).max(), k
+        for k in (2, 3, 4, 5):
             assert np.abs(new[k] - base[k]).max() <= 1e-12 * np.abs(base[k]).max(), k
-        np.testing.assert_array_equal(new[3], base[3])
     finally:
         gpu_ctx.set_option("sell_order", 3)
