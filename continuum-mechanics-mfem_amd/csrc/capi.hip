@@ -1464,6 +1464,10 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 5)
                 throw ArgError("sell_order must be 0..5 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric)");
             c->sell_mode = value;
+        } else if (k == "diag_sf") {
+            if (value < 0 || value > 1) throw ArgError("diag_sf must be 0 or 1");
+            c->diag_sf = value;
+            c->dinv_ready = false;
         } else if (k == "cg_xfold") {
             if (value < 0 || value > 1) throw ArgError("cg_xfold must be 0 or 1");
             c->cg_xfold = value;

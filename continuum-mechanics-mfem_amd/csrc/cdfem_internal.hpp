@@ -200,6 +200,7 @@ struct cdfem_ctx {
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
+    int diag_sf = 1;                    // set_option "diag_sf": sum-factorised PA diagonal (0: per-entry quadrature loop)
     int cg_xfold = 0;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply (A/B)
     double *xfold_x = nullptr;          // the solution vector while a folded brick CG loop runs
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present

@@ -398,6 +398,130 @@ k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int
     else Ye[t] = acc;  // t == (b*nd + l)*64 + lane
 }
 
+// PA diagonal, sum-factorised (MFEM's PA AssembleDiagonal): thread per (element, i1[, i2]) computing
+// the D1 entries along the last axis.  Every term of the operator is a component c of the qdata
+// times a product of 1D factors, one per axis: F_d(q, i) = u_d(q, i) v_d(q, i) with u, v = G when the
+// term differentiates along d, else B, so
+//   diag(i) = sum_terms mult * sum_{q_last} F_last * (... sum_{q1} F_1 * qd_c(q)).
+// Terms: diffusion c = (a, b) with a <= b (off-diagonal twice), convection c = oC + k with (k, none),
+// mass (none, none).  ~D1^(dim-1) threads read each element's qdata once (wave broadcast) and do
+// 10 Q1^dim FMAs each, against D1^dim Q1^dim (30 flops) for the per-entry form.
+// D1T / Q1T > 0: compile-time sizes (the loops unroll and each qdata row is loaded before its sums);
+// 0: the rule's run-time sizes
+template <int DIM, int D1T, int Q1T>
+__global__ void __launch_bounds__(256)
+k_diag_sf(const double *__restrict__ qd, const int32_t *__restrict__ perm, int ne, int nblk, int nd, int qlay,
+          const HoLayout ho, const Rule1D r, unsigned kinds, int nc, double *__restrict__ Ye)
+{
+    const int d1 = D1T > 0 ? D1T : r.d1, q1 = Q1T > 0 ? Q1T : r.q1;
+    const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
+    const int nt = DIM == 3 ? d1 * d1 : d1;  // threads per element
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t npos = qlay == 1 ? (int64_t)ne : (int64_t)nblk * kLanes;
+    if (t >= npos * nt) return;
+    const int64_t pos = t / nt;
+    const int it = (int)(t - pos * nt);
+    const int i1 = it % d1, i2 = DIM == 3 ? it / d1 : 0;
+    const int b = qlay == 1 ? 0 : (int)(pos / kLanes), lane = qlay == 1 ? 0 : (int)(pos % kLanes);
+    const int e = qlay == 1 ? (int)pos : perm[pos];
+    auto out = [&](int i3, double v) {
+        const int l = DIM == 3 ? i1 + d1 * (i2 + d1 * i3) : i1 + d1 * i3;
+        if (qlay == 1) Ye[ho_eidx(ho, (uint32_t)e, l)] = v;
+        else Ye[((size_t)b * nd + l) * kLanes + lane] = v;
+    };
+    if (e < 0 || e >= ne) {
+        for (int i3 = 0; i3 < d1; ++i3) out(i3, 0.0);
+        return;
+    }
+    // qdata of component c at (qx, qy, qz) = base_c + qz * sz + (qx + q1 qy) * sxy (cheap strides)
+    const size_t plane = qd_ho_plane(nc, q1);
+    auto cbase = [&](int c, size_t &sxy, size_t &sz) -> const double * {
+        if (qlay == 1) {
+            const int qq2 = q1 * q1;
+            const bool pair = c < (nc & ~1);
+            sxy = pair ? 2 : 1;
+            sz = DIM == 3 ? plane : 0;
+            return qd + (size_t)e * q1 * plane + (pair ? (size_t)(c >> 1) * qq2 * 2 + (c & 1) : (size_t)(nc & ~1) * qq2);
+        }
+        sxy = (size_t)nc * kLanes;
+        sz = (size_t)q1 * q1 * nc * kLanes;
+        return qd + (size_t)b * nq * nc * kLanes + qd_offset(c, lane, nc);
+    };
+    // this thread's 1D factors along the first axes (i1, i2 fixed)
+    double B1[kMaxQ1], G1[kMaxQ1], B2[kMaxQ1], G2[kMaxQ1];
+    for (int q = 0; q < q1; ++q) {
+        B1[q] = r.B[q][i1];
+        G1[q] = r.G[q][i1];
+        B2[q] = r.B[q][i2];
+        G2[q] = r.G[q][i2];
+    }
+    // term list: component, derivative axes a, b (-1 = none), multiplicity
+    int tc[10], ta[10], tb[10];
+    double tm[10];
+    int nterm = 0;
+    if (kinds & CDFEM_DIFFUSION) {
+        int c = 0;
+        for (int a = 0; a < DIM; ++a)
+            for (int bb = a; bb < DIM; ++bb, ++c) {
+                tc[nterm] = c; ta[nterm] = a; tb[nterm] = bb; tm[nterm] = a == bb ? 1.0 : 2.0; ++nterm;
+            }
+    }
+    const int oC = (kinds & CDFEM_DIFFUSION) ? DIM * (DIM + 1) / 2 : 0;
+    const int oM = oC + ((kinds & CDFEM_CONVECTION) ? DIM : 0);
+    if (kinds & CDFEM_CONVECTION)
+        for (int k = 0; k < DIM; ++k) {
+            tc[nterm] = oC + k; ta[nterm] = k; tb[nterm] = -1; tm[nterm] = 1.0; ++nterm;
+        }
+    if (kinds & CDFEM_MASS) {
+        tc[nterm] = oM; ta[nterm] = -1; tb[nterm] = -1; tm[nterm] = 1.0; ++nterm;
+    }
+    double acc[kMaxD1];
+    for (int i3 = 0; i3 < d1; ++i3) acc[i3] = 0.0;
+    const int last = DIM - 1;
+    for (int s = 0; s < nterm; ++s) {
+        const int a = ta[s], bb = tb[s];
+        size_t sxy, sz;
+        const double *qc = cbase(tc[s], sxy, sz);
+        double f1[kMaxQ1], f2[kMaxQ1];
+        for (int q = 0; q < q1; ++q) {
+            f1[q] = (a == 0 ? G1[q] : B1[q]) * (bb == 0 ? G1[q] : B1[q]);
+            f2[q] = (a == 1 ? G2[q] : B2[q]) * (bb == 1 ? G2[q] : B2[q]);
+        }
+#pragma unroll
+        for (int qz = 0; qz < (Q1T > 0 ? Q1T : kMaxQ1); ++qz) {  // the last axis' quadrature index
+            if (Q1T == 0 && qz >= q1) break;
+            double szs = 0.0;
+            if (DIM == 3) {
+                const double *qp = qc + qz * sz;
+#pragma unroll
+                for (int qy = 0; qy < (Q1T > 0 ? Q1T : kMaxQ1); ++qy) {
+                    if (Q1T == 0 && qy >= q1) break;
+                    double v[Q1T > 0 ? Q1T : kMaxQ1];
+#pragma unroll
+                    for (int qx = 0; qx < (Q1T > 0 ? Q1T : kMaxQ1); ++qx)
+                        if (Q1T > 0 || qx < q1) v[qx] = qp[(size_t)(qx + q1 * qy) * sxy];
+                    double sx = 0.0;
+#pragma unroll
+                    for (int qx = 0; qx < (Q1T > 0 ? Q1T : kMaxQ1); ++qx)
+                        if (Q1T > 0 || qx < q1) sx += f1[qx] * v[qx];
+                    szs += f2[qy] * sx;
+                }
+            } else {
+#pragma unroll
+                for (int qx = 0; qx < (Q1T > 0 ? Q1T : kMaxQ1); ++qx)
+                    if (Q1T > 0 || qx < q1) szs += f1[qx] * qc[(size_t)(qx + q1 * qz) * sxy];
+            }
+            szs *= tm[s];
+            for (int i3 = 0; i3 < d1; ++i3) {
+                const double u = a == last ? r.G[qz][i3] : r.B[qz][i3];
+                const double v = bb == last ? r.G[qz][i3] : r.B[qz][i3];
+                acc[i3] += u * v * szs;
+            }
+        }
+    }
+    for (int i3 = 0; i3 < d1; ++i3) out(i3, acc[i3]);
+}
+
 // linear form, element part: be_l = sum_q W detJ f_q phi_l; thread per (block, l, lane)
 template <int DIM>
 __global__ void __launch_bounds__(256)
@@ -472,6 +596,35 @@ hipError_t launch_quad_points(cdfem_ctx *c, const Rule1D &r, double *xyz)
 
 hipError_t launch_diag_elem(cdfem_ctx *c, double *Ye)
 {
+    if (c->diag_sf) {  // sum-factorised (default)
+        const int d1 = c->rule_op.d1, q1 = c->rule_op.q1;
+        const int64_t npos = c->qlay == 1 ? (int64_t)c->ne : (int64_t)c->nblk * kLanes;
+        const int64_t n = npos * (c->dim == 3 ? d1 * d1 : d1);
+        const dim3 g(grid_for(n, 256)), bs(256);
+#define CDFEM_DSF(DIM_, D1_, Q1_)                                                                        \
+    hipLaunchKernelGGL((k_diag_sf<DIM_, D1_, Q1_>), g, bs, 0, c->stream, c->d_qd, c->d_perm, c->ne, c->nblk, \
+                       c->nd, c->qlay, ho_layout(c), c->rule_op, c->kinds, c->ncomp, Ye)
+        const bool three = c->dim == 3;
+        if (d1 == q1 - 1 && d1 >= 2 && d1 <= 5) {  // the Gauss n = p + 2 rules of the operators
+            if (three) {
+                if (d1 == 2) CDFEM_DSF(3, 2, 3);
+                else if (d1 == 3) CDFEM_DSF(3, 3, 4);
+                else if (d1 == 4) CDFEM_DSF(3, 4, 5);
+                else CDFEM_DSF(3, 5, 6);
+            } else {
+                if (d1 == 2) CDFEM_DSF(2, 2, 3);
+                else if (d1 == 3) CDFEM_DSF(2, 3, 4);
+                else if (d1 == 4) CDFEM_DSF(2, 4, 5);
+                else CDFEM_DSF(2, 5, 6);
+            }
+        } else if (three) {
+            CDFEM_DSF(3, 0, 0);
+        } else {
+            CDFEM_DSF(2, 0, 0);
+        }
+#undef CDFEM_DSF
+        return hipGetLastError();
+    }
     const int64_t n = (int64_t)c->nblk * c->nd * kLanes;
     if (c->dim == 3)
         hipLaunchKernelGGL(k_diag_elem<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
