@@ -1393,7 +1393,7 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
 int cdfem_stream_bench(cdfem_ctx *c, int mode, size_t bytes, int reps, double *gbps)
 {
     return guarded(c, [&] {
-        if (!gbps || reps < 1 || mode < 0 || mode > 9) throw ArgError("bad stream bench arguments");
+        if (!gbps || reps < 1 || mode < 0 || mode > 13) throw ArgError("bad stream bench arguments");
         int64_t n = (int64_t)(bytes / 16) * 2;
         if (mode >= 3) n = n / 40960 * 40960;  // whole 320 KiB chunks
         double *a = dalloc<double>(n), *b = dalloc<double>(n);
@@ -1413,7 +1413,11 @@ int cdfem_stream_bench(cdfem_ctx *c, int mode, size_t bytes, int reps, double *g
         (void)hipEventDestroy(e1);
         dfree(a);
         dfree(b);
-        const double moved = (mode == 2 ? 2.0 : 1.0) * 8.0 * (double)n * reps;
+        double moved = (mode == 2 ? 2.0 : 1.0) * 8.0 * (double)n * reps;
+        if (mode >= 10) {  // skewed chunks: whole 320 KiB chunks at a stride of 320 KiB + skew
+            const int64_t skew[4] = {32, 64, 128, 512};
+            moved = 8.0 * 40960.0 * (double)(n / (40960 + skew[mode - 10])) * reps;
+        }
         *gbps = moved / (ms * 1e-3) / 1e9;
         return CDFEM_OK;
     });

@@ -38,13 +38,14 @@ __global__ void __launch_bounds__(256) k_stream_copy(const double *__restrict__ 
 // LDS per block so that at most one wave runs per SIMD (the brick kernel's occupancy).
 constexpr int64_t kChunkDoubles = 40960;  // 320 KiB
 template <int U, bool PAD>
-__global__ void __launch_bounds__(64) k_stream_chunk(const double *__restrict__ a, int64_t nchunks, double *out)
+__global__ void __launch_bounds__(64) k_stream_chunk(const double *__restrict__ a, int64_t nchunks, double *out,
+                                                     int64_t stride = kChunkDoubles)
 {
     __shared__ double pad[PAD ? 4992 : 1];
     if (threadIdx.x == 64) pad[0] = 0.0;  // never true: keeps the allocation
     const int64_t b = blockIdx.x;
     if (b >= nchunks) return;
-    const double2 *p = reinterpret_cast<const double2 *>(a + b * kChunkDoubles) + threadIdx.x;
+    const double2 *p = reinterpret_cast<const double2 *>(a + b * stride) + threadIdx.x;
     constexpr int iters = (int)(kChunkDoubles / 128);
     double s = 0.0;
     for (int i = 0; i < iters; i += U) {
@@ -144,6 +145,12 @@ hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int
     case 6: hipLaunchKernelGGL((k_stream_chunk<4, true>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
     case 7: hipLaunchKernelGGL((k_stream_chunk<32, true>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
     case 8: hipLaunchKernelGGL((k_stream_ileave<8>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
+    case 10: case 11: case 12: case 13: {  // chunk U8, one wave per SIMD, chunks skewed by 256 B..4 KiB
+        const int64_t skew[4] = {32, 64, 128, 512};
+        const int64_t st = kChunkDoubles + skew[mode - 10], nc2 = n / st;
+        hipLaunchKernelGGL((k_stream_chunk<8, true>), dim3(nc2), dim3(64), 0, c->stream, a, nc2, b, st);
+        break;
+    }
     case 9: hipLaunchKernelGGL((k_stream_ileave<4>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
     case 0: hipLaunchKernelGGL(k_stream_read<16>, grid, block, 0, c->stream, a, n, b); break;
     case 1: hipLaunchKernelGGL(k_stream_read<8>, grid, block, 0, c->stream, a, n, b); break;
