@@ -303,6 +303,8 @@ static hipError_t brick_kinds(cdfem_ctx *c, const double *x, const double *dinv,
     case 5: return brick_launch<D1, Q1, 5, MODE>(c, x, dinv, d, y, which);
     case 6: return brick_launch<D1, Q1, 6, MODE>(c, x, dinv, d, y, which);
     case 7: return brick_launch<D1, Q1, 7, MODE>(c, x, dinv, d, y, which);
+    case 5 | kMassFromD: return brick_launch<D1, Q1, 5 | kMassFromD, MODE>(c, x, dinv, d, y, which);
+    case 7 | kMassFromD: return brick_launch<D1, Q1, 7 | kMassFromD, MODE>(c, x, dinv, d, y, which);
     default: return hipErrorInvalidValue;
     }
 }
@@ -603,6 +605,8 @@ static hipError_t brick_cg2_run(cdfem_ctx *c, const double *r, const double *din
     case 5: return brick_cg2_launch<D1_, Q1_, 5>(c, r, dinv, d_old, d_new, q, run);                 \
     case 6: return brick_cg2_launch<D1_, Q1_, 6>(c, r, dinv, d_old, d_new, q, run);                 \
     case 7: return brick_cg2_launch<D1_, Q1_, 7>(c, r, dinv, d_old, d_new, q, run);                 \
+    case 5 | kMassFromD: return brick_cg2_launch<D1_, Q1_, 5 | kMassFromD>(c, r, dinv, d_old, d_new, q, run); \
+    case 7 | kMassFromD: return brick_cg2_launch<D1_, Q1_, 7 | kMassFromD>(c, r, dinv, d_old, d_new, q, run); \
     default: return hipErrorInvalidValue;                                                           \
     }
     if (c->p == 1 && q1 == 3) { CDFEM_K(2, 3) }

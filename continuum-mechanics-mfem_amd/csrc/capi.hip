@@ -1043,11 +1043,16 @@ static int pa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
         if (!apply_supported(c->dim, c->p))
             throw UnsupportedError("no PA apply kernel built for dim=" + std::to_string(c->dim) +
                                    " order=" + std::to_string(c->p));
-        const unsigned kinds = f->kinds;
+        // 3D, constant kappa != 0 and s, no matrix coefficient: the mass weight comes from the
+        // diffusion block (one qdata component less per point; QLayout::kMD in pa_core.hpp)
+        const bool from_d = c->mass_from_d && c->dim == 3 && (f->kinds & CDFEM_DIFFUSION) && (f->kinds & CDFEM_MASS) &&
+                            !f->kappa_q && !f->kappa_mat_q && !f->mass_q && f->kappa != 0.0 && std::isfinite(f->kappa);
+        const unsigned kinds = f->kinds | (from_d ? kMassFromD : 0u);
         dfree(c->d_qd);
         c->kinds = kinds;
+        c->rule_op.mscale = from_d ? f->mass / (f->kappa * f->kappa * f->kappa) : 0.0;
         c->ncomp = ((kinds & CDFEM_DIFFUSION) ? c->dim * (c->dim + 1) / 2 : 0) +
-                   ((kinds & CDFEM_CONVECTION) ? c->dim : 0) + ((kinds & CDFEM_MASS) ? 1 : 0);
+                   ((kinds & CDFEM_CONVECTION) ? c->dim : 0) + ((kinds & CDFEM_MASS) && !from_d ? 1 : 0);
         const int nq = nq_of(c, c->rule_op);
         c->d_qd = c->qlay == 1 ? dalloc<double>((size_t)c->ne * c->rule_op.q1 * qd_ho_plane(c->ncomp, c->rule_op.q1))
                                : dalloc<double>((size_t)c->nblk * nq * c->ncomp * kLanes);
@@ -1468,6 +1473,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 5)
                 throw ArgError("sell_order must be 0..5 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric)");
             c->sell_mode = value;
+        } else if (k == "mass_from_d") {  // read at the next cdfem_pa_setup
+            if (value < 0 || value > 1) throw ArgError("mass_from_d must be 0 or 1");
+            c->mass_from_d = value;
         } else if (k == "diag_sf") {
             if (value < 0 || value > 1) throw ArgError("diag_sf must be 0 or 1");
             c->diag_sf = value;

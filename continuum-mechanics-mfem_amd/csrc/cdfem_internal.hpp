@@ -28,8 +28,12 @@ constexpr int kMaxD1 = 6;
 constexpr int kMaxQ1 = 8;
 
 // 1D tables for one quadrature rule: B[q][d] = phi_d(xi_q), G[q][d] = phi_d'(xi_q), points, weights
+// kinds bit (internal, 3D PA with constant kappa and s): the mass weight is not stored but derived
+// from the diffusion block, M = s det(D) / (W^2 kappa^3) (pa_core.hpp, QLayout::kMD)
+constexpr unsigned kMassFromD = 8u;
 struct Rule1D {
     int d1 = 0, q1 = 0;
+    double mscale = 0.0;                // s / kappa^3 when the mass weight is derived (kMassFromD)
     double B[kMaxQ1][kMaxD1] = {};
     double G[kMaxQ1][kMaxD1] = {};
     double pts[kMaxQ1] = {};
@@ -200,6 +204,7 @@ struct cdfem_ctx {
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
+    int mass_from_d = 0;                // set_option "mass_from_d": derive the 3D mass weight from D (constant kappa, s; A/B, measured slower)
     int diag_sf = 1;                    // set_option "diag_sf": sum-factorised PA diagonal (0: per-entry quadrature loop)
     int cg_xfold = 0;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply (A/B)
     double *xfold_x = nullptr;          // the solution vector while a folded brick CG loop runs

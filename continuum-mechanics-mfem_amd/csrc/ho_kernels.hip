@@ -72,6 +72,16 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 
     const int le = threadIdx.x / QQ, t = threadIdx.x - le * QQ;
     const int tx = t % Q1, ty = t / Q1;
+    double wxy = 0.0;  // 1 / (w_tx w_ty)^2 of this thread's point column (derived mass weight)
+    if constexpr (L::kMD) {
+        double wx = 0.0, wy = 0.0;
+#pragma unroll
+        for (int k = 0; k < Q1; ++k) {
+            if (k == tx) wx = T.iw2[k];
+            if (k == ty) wy = T.iw2[k];
+        }
+        wxy = wx * wy;
+    }
     const int e = blockIdx.x * EPB + le;
     const bool valid = le < EPB && e < ne;
     if (threadIdx.x < Q1 * D1) {
@@ -212,6 +222,9 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
         }
         if constexpr (L::kC) v0 += qv[qz][L::oC] * ux + qv[qz][L::oC + 1] * uy + qv[qz][L::oC + 2] * uz;
         if constexpr (L::kM) v0 += qv[qz][L::oM] * u;
+        if constexpr (L::kMD)
+            v0 += T.mscale * (wxy * T.iw2[qz]) *
+                  det_sym3(qv[qz][0], qv[qz][1], qv[qz][2], qv[qz][3], qv[qz][4], qv[qz][5]) * u;
 #pragma unroll
         for (int dz = 0; dz < D1; ++dz) {
             const double bz = T.B[qz][dz], gz = T.G[qz][dz];
@@ -341,6 +354,8 @@ static hipError_t tile_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, c
     case 5: return tile_kinds<D1, Q1, 5>(c, x, Ye, con, st, den_part);
     case 6: return tile_kinds<D1, Q1, 6>(c, x, Ye, con, st, den_part);
     case 7: return tile_kinds<D1, Q1, 7>(c, x, Ye, con, st, den_part);
+    case 5 | kMassFromD: return tile_kinds<D1, Q1, 5 | kMassFromD>(c, x, Ye, con, st, den_part);
+    case 7 | kMassFromD: return tile_kinds<D1, Q1, 7 | kMassFromD>(c, x, Ye, con, st, den_part);
     default: return hipErrorInvalidValue;
     }
 }

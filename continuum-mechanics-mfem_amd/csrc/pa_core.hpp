@@ -12,6 +12,8 @@ template <int D1, int Q1>
 struct Tab {
     double B[Q1][D1];
     double G[Q1][D1];
+    double iw2[Q1];   // 1 / w_q^2 of the 1D rule (derived mass weight)
+    double mscale;    // s / kappa^3 (derived mass weight), else 0
 };
 
 template <int D1, int Q1>
@@ -23,6 +25,8 @@ static Tab<D1, Q1> make_tab(const Rule1D &r)
             t.B[q][d] = r.B[q][d];
             t.G[q][d] = r.G[q][d];
         }
+    for (int q = 0; q < Q1; ++q) t.iw2[q] = 1.0 / (r.wts[q] * r.wts[q]);
+    t.mscale = r.mscale;
     return t;
 }
 
@@ -31,7 +35,11 @@ template <unsigned K, int DIM>
 struct QLayout {
     static constexpr bool kD = (K & CDFEM_DIFFUSION) != 0;
     static constexpr bool kC = (K & CDFEM_CONVECTION) != 0;
-    static constexpr bool kM = (K & CDFEM_MASS) != 0;
+    // kMD: the mass weight W s detJ is derived from the diffusion block (kinds bit kMassFromD, 3D,
+    // constant kappa and s): det D = (W kappa)^3 detJ, so M = s det(D) / (W^2 kappa^3) -- one qdata
+    // component less to stream (q_c 9 instead of 10 for D+C+M)
+    static constexpr bool kMD = DIM == 3 && (K & kMassFromD) != 0 && (K & CDFEM_MASS) != 0 && (K & CDFEM_DIFFUSION) != 0;
+    static constexpr bool kM = (K & CDFEM_MASS) != 0 && !kMD;
     static constexpr int nD = kD ? DIM * (DIM + 1) / 2 : 0;
     static constexpr int oC = nD;
     static constexpr int oM = oC + (kC ? DIM : 0);
@@ -48,6 +56,12 @@ __host__ __device__ constexpr int qd_offset(int c, int lane, int nc)
 }
 
 typedef double v2d_t __attribute__((ext_vector_type(2)));
+
+// det of the symmetric 3x3 [d00 d01 d02; d01 d11 d12; d02 d12 d22] stored as (d00, d01, d02, d11, d12, d22)
+__host__ __device__ inline double det_sym3(double d00, double d01, double d02, double d11, double d12, double d22)
+{
+    return d00 * (d11 * d22 - d12 * d12) - d01 * (d01 * d22 - d12 * d02) + d02 * (d01 * d12 - d11 * d02);
+}
 
 // NT: non-temporal (streaming) loads — qdata is read once per Mult, so it must not displace the
 // L-vectors that neighbouring elements / bricks re-read from L2.  Measured on k_brick_cg (64^3,
@@ -158,6 +172,9 @@ __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restr
                 }
                 if constexpr (L::kC) vv = qv[L::oC] * ux + qv[L::oC + 1] * uy + qv[L::oC + 2] * uz;
                 if constexpr (L::kM) vv += qv[L::oM] * u;
+                if constexpr (L::kMD)
+                    vv += T.mscale * (T.iw2[qx] * T.iw2[qy] * T.iw2[qz]) *
+                          det_sym3(qv[0], qv[1], qv[2], qv[3], qv[4], qv[5]) * u;
                 // transposed contraction in x
 #pragma unroll
                 for (int dx = 0; dx < D1; ++dx) {
@@ -265,6 +282,9 @@ __device__ __forceinline__ void elem_apply3d_lr(const XL &xl, const double *__re
                 }
                 if constexpr (L::kC) vv = qv[L::oC] * ux + qv[L::oC + 1] * uy + qv[L::oC + 2] * uz;
                 if constexpr (L::kM) vv += qv[L::oM] * u;
+                if constexpr (L::kMD)
+                    vv += T.mscale * (T.iw2[qx] * T.iw2[qy] * T.iw2[qz]) *
+                          det_sym3(qv[0], qv[1], qv[2], qv[3], qv[4], qv[5]) * u;
 #pragma unroll
                 for (int dx = 0; dx < D1; ++dx) {
                     if constexpr (L::kD) {

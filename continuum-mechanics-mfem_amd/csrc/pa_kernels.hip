@@ -310,7 +310,7 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
             put(o++, W * alpha * acc);
         }
     }
-    if (kinds & CDFEM_MASS) {
+    if ((kinds & CDFEM_MASS) && !(kinds & kMassFromD)) {  // derived from D otherwise (QLayout::kMD)
         const double s = mass_q ? mass_q[eq] : mass;
         put(o++, W * s * det);
     }
@@ -392,7 +392,17 @@ k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int
             for (int k = 0; k < DIM; ++k) cg += qq(oC + k) * g[k];
             acc += phi * cg;
         }
-        if (kinds & CDFEM_MASS) acc += qq(oM) * phi * phi;
+        if (kinds & CDFEM_MASS) {
+            double m;
+            if (kinds & kMassFromD) {  // M = s det(D) / (W^2 kappa^3)
+                const int qx = q % q1, qy = (q / q1) % q1, qz = q / (q1 * q1);
+                const double W = r.wts[qx] * r.wts[qy] * r.wts[qz];
+                m = r.mscale * det_sym3(qq(0), qq(1), qq(2), qq(3), qq(4), qq(5)) / (W * W);
+            } else {
+                m = qq(oM);
+            }
+            acc += m * phi * phi;
+        }
     }
     if (qlay == 1) Ye[ho_eidx(ho, (uint32_t)e, l)] = acc;
     else Ye[t] = acc;  // t == (b*nd + l)*64 + lane
@@ -472,16 +482,22 @@ k_diag_sf(const double *__restrict__ qd, const int32_t *__restrict__ perm, int n
         for (int k = 0; k < DIM; ++k) {
             tc[nterm] = oC + k; ta[nterm] = k; tb[nterm] = -1; tm[nterm] = 1.0; ++nterm;
         }
-    if (kinds & CDFEM_MASS) {
-        tc[nterm] = oM; ta[nterm] = -1; tb[nterm] = -1; tm[nterm] = 1.0; ++nterm;
+    const bool mass_from_d = DIM == 3 && (kinds & kMassFromD) && (kinds & CDFEM_MASS) && (kinds & CDFEM_DIFFUSION);
+    if (kinds & CDFEM_MASS) {  // component -1: the mass weight derived from D (QLayout::kMD)
+        tc[nterm] = mass_from_d ? -1 : oM; ta[nterm] = -1; tb[nterm] = -1; tm[nterm] = 1.0; ++nterm;
     }
+    const double *dbase[6] = {};
+    size_t dsxy = 0, dsz = 0;
+    if (mass_from_d)
+        for (int k = 0; k < 6; ++k) dbase[k] = cbase(k, dsxy, dsz);
     double acc[kMaxD1];
     for (int i3 = 0; i3 < d1; ++i3) acc[i3] = 0.0;
     const int last = DIM - 1;
     for (int s = 0; s < nterm; ++s) {
         const int a = ta[s], bb = tb[s];
-        size_t sxy, sz;
-        const double *qc = cbase(tc[s], sxy, sz);
+        size_t sxy = 0, sz = 0;
+        const bool derived = tc[s] < 0;
+        const double *qc = derived ? nullptr : cbase(tc[s], sxy, sz);
         double f1[kMaxQ1], f2[kMaxQ1];
         for (int q = 0; q < q1; ++q) {
             f1[q] = (a == 0 ? G1[q] : B1[q]) * (bb == 0 ? G1[q] : B1[q]);
@@ -492,14 +508,24 @@ k_diag_sf(const double *__restrict__ qd, const int32_t *__restrict__ perm, int n
             if (Q1T == 0 && qz >= q1) break;
             double szs = 0.0;
             if (DIM == 3) {
-                const double *qp = qc + qz * sz;
+                const double *qp = derived ? nullptr : qc + qz * sz;
 #pragma unroll
                 for (int qy = 0; qy < (Q1T > 0 ? Q1T : kMaxQ1); ++qy) {
                     if (Q1T == 0 && qy >= q1) break;
                     double v[Q1T > 0 ? Q1T : kMaxQ1];
 #pragma unroll
                     for (int qx = 0; qx < (Q1T > 0 ? Q1T : kMaxQ1); ++qx)
-                        if (Q1T > 0 || qx < q1) v[qx] = qp[(size_t)(qx + q1 * qy) * sxy];
+                        if (Q1T > 0 || qx < q1) {
+                            if (derived) {
+                                const size_t o = qz * dsz + (size_t)(qx + q1 * qy) * dsxy;
+                                const double w = r.wts[qx] * r.wts[qy] * r.wts[qz];
+                                v[qx] = r.mscale *
+                                        det_sym3(dbase[0][o], dbase[1][o], dbase[2][o], dbase[3][o], dbase[4][o], dbase[5][o]) /
+                                        (w * w);
+                            } else {
+                                v[qx] = qp[(size_t)(qx + q1 * qy) * sxy];
+                            }
+                        }
                     double sx = 0.0;
 #pragma unroll
                     for (int qx = 0; qx < (Q1T > 0 ? Q1T : kMaxQ1); ++qx)
@@ -682,6 +708,8 @@ static hipError_t apply_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, 
     case 5: return apply_kinds<DIM, D1, Q1, 5>(c, x, Ye, con, st);
     case 6: return apply_kinds<DIM, D1, Q1, 6>(c, x, Ye, con, st);
     case 7: return apply_kinds<DIM, D1, Q1, 7>(c, x, Ye, con, st);
+    case 5 | kMassFromD: return apply_kinds<DIM, D1, Q1, 5 | kMassFromD>(c, x, Ye, con, st);
+    case 7 | kMassFromD: return apply_kinds<DIM, D1, Q1, 7 | kMassFromD>(c, x, Ye, con, st);
     default: return hipErrorInvalidValue;
     }
 }

@@ -219,13 +219,23 @@ def test_mms_solution_error_matches_oracle(gpu_ctx):
 
 def test_variable_coefficients(gpu_ctx):
     """kappa(x), s(x), c(x) sampled at quadrature points (host Coefficient::Eval) vs constant ones
-    scaled: a constant field passed per point must equal the constant path bitwise."""
+    scaled: a constant field passed per point must equal the constant path bitwise when the
+    constant path stores the mass weight (set_option mass_from_d 0, the default), and to rounding
+    when it derives it from the diffusion block (mass_from_d 1: M = s det(D) / (W^2 kappa^3))."""
     om, gm = _mesh_pair(3, 3, 2, 0.1)
     ctx = gpu_ctx.upload_mesh(gm)
     nq = ctx.rule_size(cdfem.RULE_OPERATOR)
     x = np.random.default_rng(2).uniform(-1, 1, om.nl)
-    ctx.pa_setup(kinds=7, kappa=0.3, alpha=1.0, conv=C3, mass=2.0)
-    y_const = ctx.mult(x)
+    try:
+        ctx.set_option("mass_from_d", 0)
+        ctx.pa_setup(kinds=7, kappa=0.3, alpha=1.0, conv=C3, mass=2.0)
+        y_const = ctx.mult(x)
+        ctx.set_option("mass_from_d", 1)
+        ctx.pa_setup(kinds=7, kappa=0.3, alpha=1.0, conv=C3, mass=2.0)
+        y_derived = ctx.mult(x)
+    finally:
+        ctx.set_option("mass_from_d", 0)
+    assert np.abs(y_derived - y_const).max() <= 1e-14 * np.abs(y_const).max()
     ctx.pa_setup(kinds=7, kappa=0.0, alpha=1.0, conv=(0, 0, 0), mass=0.0,
                  kappa_q=np.full(om.ne * nq, 0.3), conv_q=np.tile(C3, om.ne * nq),
                  mass_q=np.full(om.ne * nq, 2.0))
