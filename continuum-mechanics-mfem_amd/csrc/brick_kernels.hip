@@ -378,7 +378,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const int bx = b % g.nbx, by = (b / g.nbx) % g.nby;
     const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
     const bool lastx = bx == g.nbx - 1, lasty = by == g.nby - 1, lastz = bz == g.nbz - 1;
-
+    const double *q0 = qd + (size_t)b * NQ * NC * kLanes;
     double den = 0.0;
     // patch gather: every load of the patch is issued before any is consumed (clamped indices,
     // no branches between them): one memory latency per brick instead of one per patch row.
@@ -429,7 +429,6 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const int ex = t & 3, ey = (t >> 2) & 3, ez = t >> 4;
     const int o0 = P * ez * S2 + P * ey * S + P * ex;
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
-    const double *q0 = qd + (size_t)b * NQ * NC * kLanes;
     double Y[D1][D1][D1];
     if constexpr (VAR == 6)
         elem_apply3d<D1, Q1, K, decltype(xl), Q1, false>(xl, q0, t, T, Y);  // temporal qdata loads (A/B)

@@ -94,9 +94,24 @@ __device__ __forceinline__ void load_qp(const double *__restrict__ qp, int lane,
 // plane's worth of it live in registers.  QZU = unroll factor of the quadrature-plane loop
 // (Q1: straight-line code, the compiler hoists qdata loads across planes; 1: one plane's loads
 // in flight, ~250 VGPRs at p = 2, two waves per SIMD).
+// QS: qdata source, qs(q, qv) fills point q's NC components (q is a compile-time constant when the
+// plane loop is unrolled); the default reads global memory (load_qp)
+template <int D1, int Q1, unsigned K, typename XL, int QZU, typename QS>
+__device__ __forceinline__ void elem_apply3d_qs(const XL &xl, const QS &qs, const Tab<D1, Q1> &T,
+                                                double (&Y)[D1][D1][D1]);
+
 template <int D1, int Q1, unsigned K, typename XL, int QZU = Q1, bool NT = true>
 __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restrict__ q0, int lane,
                                              const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
+{
+    constexpr int NC = QLayout<K, 3>::nc;
+    elem_apply3d_qs<D1, Q1, K, XL, QZU>(
+        xl, [&](int q, double (&qv)[NC]) { load_qp<NC, NT>(q0 + (size_t)q * NC * kLanes, lane, qv); }, T, Y);
+}
+
+template <int D1, int Q1, unsigned K, typename XL, int QZU, typename QS>
+__device__ __forceinline__ void elem_apply3d_qs(const XL &xl, const QS &qs, const Tab<D1, Q1> &T,
+                                                double (&Y)[D1][D1][D1])
 {
     using L = QLayout<K, 3>;
     constexpr int NC = L::nc;
@@ -163,7 +178,7 @@ __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restr
                 }
                 const int q = qx + Q1 * (qy + Q1 * qz);
                 double qv[NC];
-                load_qp<NC, NT>(q0 + (size_t)q * NC * kLanes, lane, qv);
+                qs(q, qv);
                 double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
                 if constexpr (L::kD) {
                     gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;
