@@ -230,7 +230,17 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).
  * "spmv_index16": 1 (default) — the assembled-operator SpMV streams 16-bit column deltas when
- *                 every |column - row| < 2^15; 0 = 32-bit columns.                             */
+ *                 every |column - row| < 2^15; 0 = 32-bit columns.
+ * "sell_order": 0..5, default 3 (auto) — the FA SpMV's order, read when the pattern is built
+ *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan).  A permuted order runs the
+ *               Krylov solve in that order (Mult to rounding, iterates to 1e-12).
+ * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
+ * "spmv_variant": 0 (default) / 1 — SpMV inner loop (4 loads in flight / software-pipelined; A/B).
+ * "diag_sf": 1 (default) — sum-factorised PA diagonal; 0 = per-entry quadrature loop.
+ * "cg_xfold": 0 (default) / 1 — structured CG: fold x += alpha d into the next apply (bitwise the
+ *             same; measured slower, A/B).
+ * "mass_from_d": 0 (default) / 1 — 3D PA with constant kappa, s: derive the mass weight from the
+ *                diffusion block instead of storing it (read at cdfem_pa_setup; measured slower).  */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
 
 /* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */
