@@ -347,7 +347,8 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // sums of the interface planes; nullptr on a single GPU).
 // ================================================================================================
 // VAR % 3 = element core: 0 elem_apply3d fully unrolled; 1 elem_apply3d, plane loop; 2 low-register
-// core.  VAR >= 3: the same cores compiled for 2 waves per SIMD (<= 256 registers).
+// core.  VAR 3..5: the same cores compiled for 2 waves per SIMD (<= 256 registers).  6: temporal
+// qdata loads.  7: unrolled core with the first qdata points issued under the patch gather.
 template <int D1, int Q1, unsigned K, int VAR>
 __global__ void __launch_bounds__(64, (VAR >= 3 && VAR <= 5) ? 2 : 1)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
@@ -402,6 +403,17 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         ev[k] = ess[gid];
         if (fold) xv[k] = __builtin_nontemporal_load(xs + gid);  // issued with the patch (one round trip)
     }
+    // VAR 7: qdata of the element's first kPre quadrature points, issued after the patch loads (the
+    // patch consumption waits only for the loads before them) and before the LDS stage; 48 patch +
+    // 5 * kPre qdata loads stay within the 63 outstanding vector loads of a wave
+    constexpr int kPre = VAR == 7 ? 3 : 1;
+    double pre[kPre][NC];
+    if constexpr (VAR == 7) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int qq = 0; qq < kPre; ++qq) load_qp<NC, true>(q0 + (size_t)qq * NC * kLanes, t, pre[qq]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const int i = t + 64 * k;
@@ -430,7 +442,19 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const int o0 = P * ez * S2 + P * ey * S + P * ex;
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
     double Y[D1][D1][D1];
-    if constexpr (VAR == 6)
+    if constexpr (VAR == 7) {
+        // the first kPre points' qdata was issued right behind the patch gather (pre), so the
+        // stream is already in flight while the patch is formed and staged
+        auto qs = [&](int qq, double (&qv)[NC]) {
+            if (qq < kPre) {
+#pragma unroll
+                for (int c = 0; c < NC; ++c) qv[c] = pre[qq < kPre ? qq : 0][c];
+            } else {
+                load_qp<NC, true>(q0 + (size_t)qq * NC * kLanes, t, qv);
+            }
+        };
+        elem_apply3d_qs<D1, Q1, K, decltype(xl), Q1>(xl, qs, T, Y);
+    } else if constexpr (VAR == 6)
         elem_apply3d<D1, Q1, K, decltype(xl), Q1, false>(xl, q0, t, T, Y);  // temporal qdata loads (A/B)
     else if constexpr (VAR % 3 == 2)
         elem_apply3d_lr<D1, Q1, K, decltype(xl), 1>(xl, q0, t, T, Y);
@@ -585,6 +609,7 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     case 4: CDFEM_L(4); break;
     case 5: CDFEM_L(5); break;
     case 6: CDFEM_L(6); break;
+    case 7: CDFEM_L(7); break;
     default: CDFEM_L(0); break;
     }
 #undef CDFEM_L

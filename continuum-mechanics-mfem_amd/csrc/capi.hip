@@ -1398,7 +1398,7 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
 int cdfem_stream_bench(cdfem_ctx *c, int mode, size_t bytes, int reps, double *gbps)
 {
     return guarded(c, [&] {
-        if (!gbps || reps < 1 || mode < 0 || mode > 13) throw ArgError("bad stream bench arguments");
+        if (!gbps || reps < 1 || mode < 0 || mode > 17) throw ArgError("bad stream bench arguments");
         int64_t n = (int64_t)(bytes / 16) * 2;
         if (mode >= 3) n = n / 40960 * 40960;  // whole 320 KiB chunks
         double *a = dalloc<double>(n), *b = dalloc<double>(n);
@@ -1419,7 +1419,11 @@ int cdfem_stream_bench(cdfem_ctx *c, int mode, size_t bytes, int reps, double *g
         dfree(a);
         dfree(b);
         double moved = (mode == 2 ? 2.0 : 1.0) * 8.0 * (double)n * reps;
-        if (mode >= 10) {  // skewed chunks: whole 320 KiB chunks at a stride of 320 KiB + skew
+        if (mode == 14 || mode == 15) {  // workgroup chunks: whole groups of 4 / 2 chunks
+            const int64_t nw = mode == 14 ? 4 : 2;
+            moved = 8.0 * 40960.0 * (double)(n / 40960 / nw * nw) * reps;
+        }
+        if (mode >= 10 && mode <= 13) {  // skewed chunks: whole 320 KiB chunks at a stride of 320 KiB + skew
             const int64_t skew[4] = {32, 64, 128, 512};
             moved = 8.0 * 40960.0 * (double)(n / (40960 + skew[mode - 10])) * reps;
         }
@@ -1457,7 +1461,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         if (!key) throw ArgError("key is null");
         const std::string k(key);
         if (k == "brick_variant") {
-            if (value < 0 || value > 6) throw ArgError("brick_variant must be 0..6");
+            if (value < 0 || value > 7) throw ArgError("brick_variant must be 0..7");
             c->brick_variant = value;
 
         } else if (k == "brick_xcd") {
@@ -1466,6 +1470,10 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "mr_overlap") {
             if (value < 0 || value > 1) throw ArgError("mr_overlap must be 0 or 1");
             c->mr_overlap = value;
+        } else if (k == "ho_mfma") {
+            if (value != 0 && value != 1 && value != 3 && value != 15)
+                throw ArgError("ho_mfma must be 0, 1, 3 or 15");
+            c->ho_mfma = value;
         } else if (k == "cg_fused") {
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;

@@ -203,6 +203,7 @@ struct cdfem_ctx {
     int mr_overlap = 1;                 // set_option "mr_overlap": slab CG exchange overlapped with interior bricks
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
+    int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int mass_from_d = 0;                // set_option "mass_from_d": derive the 3D mass weight from D (constant kappa, s; A/B, measured slower)
     int diag_sf = 1;                    // set_option "diag_sf": sum-factorised PA diagonal (0: per-entry quadrature loop)

@@ -51,7 +51,46 @@ struct TileGeo {
 // that owns it (the highest element index along each axis).  That is exactly (d, q) with q the
 // constrained L-vector, so the E->L sum no longer has to precede the den step and can be fused
 // into the CG update (k_e2l_box<UPD>).
-template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN>
+typedef double v4d_t __attribute__((ext_vector_type(4)));
+
+// One block-wide GEMM on the matrix cores: out(row, col) = sum_k a(row, k) b(k, col) for
+// row < ROWS (the block's elements stacked), k < 4 KS, col < 16, as v_mfma_f64_16x16x4_f64 tiles of
+// 16 rows; the four waves of the block take row tiles round-robin.  a() and b() return 0 outside
+// the operator; o(row, col, v) stores (and drops padding columns).  Lane maps (MI355X f64 MFMA):
+// A[l & 15][k = l >> 4], B[k = l >> 4][l & 15], D[(l >> 4) + 4 r][l & 15].
+template <int ROWS, int KS, typename FA, typename FB, typename FO>
+__device__ __forceinline__ void block_mfma(const FA &a, const FB &b, const FO &o)
+{
+    constexpr int NTL = (ROWS + 15) / 16;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, kq = lane >> 4, col = lane & 15;
+    double bop[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) bop[ks] = b(ks * 4 + kq, col);
+    for (int tt = wv; tt < NTL; tt += 4) {
+        const int rho = tt * 16 + col;
+        v4d_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const double av = rho < ROWS ? a(rho, ks * 4 + kq) : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bop[ks], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = tt * 16 + kq + 4 * r;
+            if (row < ROWS) o(row, col, acc[r]);
+        }
+    }
+}
+
+// The tile apply's LDS stages as block GEMMs (MF bit k = stage on the matrix cores):
+//   bit 0  stage x    [BX | GX](e dz dy, qx)      = X(e dz dy, dx) . [B | G]^T(dx, qx)
+//   bit 1  stage y    [bb | gb](e dz qx, qy)      = BX(e dz qx, dy) . [B | G]^T(dy, qy),
+//                      bg(e dz qx, qy)           = GX(e dz qx, dy) . B^T(dy, qy)
+//   bit 2  stage y^T  [ZB | ZG](e dz qx, dy)      = [W0 | Wy | Wx](e dz qx, qy) . [[B 0]; [G 0]; [0 B]](qy, dy)
+//   bit 3  stage x^T  Y(e dz dy, dx)              = [ZB | ZG](e dz dy, qx) . [B; G](qx, dx)
+// Each writes LDS; the VALU z stage and quadrature-point operator stay per thread.
+
+template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, int MF>
 __global__ void __launch_bounds__(256)
 k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qd,
                double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const TileGeo geo,
@@ -150,8 +189,20 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
         A[gthr ? (dz * D1 + ty) * D1 + tx : ND + t * D1 + dz] = zero ? 0.0 : xr[dz];
     }
     __syncthreads();
-    // stage x: threads (qx = tx, dy = ty)
-    if (valid && ty < D1) {
+    // stage x: threads (qx = tx, dy = ty), or the matrix cores (MF & 1)
+    constexpr int DD = D1 * D1, DQ = D1 * Q1;
+    if constexpr ((MF & 1) != 0) {
+        static_assert(2 * Q1 <= 16, "one tile of output columns");
+        block_mfma<EPB * DD, (D1 + 3) / 4>(
+            [&](int row, int k) { return k < D1 ? bufA[row / DD][(row % DD) * D1 + k] : 0.0; },
+            [&](int k, int col) {
+                return k >= D1 ? 0.0 : col < Q1 ? sBt[col * D1 + k] : col < 2 * Q1 ? sGt[(col - Q1) * D1 + k] : 0.0;
+            },
+            [&](int row, int col, double v) {
+                if (col < 2 * Q1)
+                    bufB[row / DD][(col < Q1 ? 0 : DD * Q1) + (row % DD) * Q1 + (col < Q1 ? col : col - Q1)] = v;
+            });
+    } else if (valid && ty < D1) {
         double b[D1], g[D1];
 #pragma unroll
         for (int dx = 0; dx < D1; ++dx) {
@@ -174,7 +225,40 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     __syncthreads();
     // stage y: threads (qx = tx, qy = ty), column over dz in registers
     double bb[D1], bg[D1], gb[D1];
-    {
+    if constexpr ((MF & 2) != 0) {
+        // rows (e, dz, qx); the results land in bufA (X is dead) at the slots this thread's z
+        // stage later overwrites with W0 / Wx / Wy, so reading them back needs no extra barrier
+        auto ain = [&](int off) {
+            return [&, off](int row, int k) {
+                if (k >= D1) return 0.0;
+                const int e = row / DQ, r = row % DQ, dz = r / Q1, qx = r % Q1;
+                return bufB[e][off + (dz * D1 + k) * Q1 + qx];
+            };
+        };
+        block_mfma<EPB * DQ, (D1 + 3) / 4>(
+            ain(0),
+            [&](int k, int col) {
+                return k >= D1 ? 0.0 : col < Q1 ? sBt[col * D1 + k] : col < 2 * Q1 ? sGt[(col - Q1) * D1 + k] : 0.0;
+            },
+            [&](int row, int col, double v) {
+                const int e = row / DQ, r = row % DQ, dz = r / Q1, qx = r % Q1;
+                if (col < Q1) bufA[e][dz * QQ + col * Q1 + qx] = v;                        // bb
+                else if (col < 2 * Q1) bufA[e][(2 * D1 + dz) * QQ + (col - Q1) * Q1 + qx] = v;  // gb
+            });
+        block_mfma<EPB * DQ, (D1 + 3) / 4>(
+            ain(DD * Q1), [&](int k, int col) { return k < D1 && col < Q1 ? sBt[col * D1 + k] : 0.0; },
+            [&](int row, int col, double v) {
+                const int e = row / DQ, r = row % DQ, dz = r / Q1, qx = r % Q1;
+                if (col < Q1) bufA[e][(D1 + dz) * QQ + col * Q1 + qx] = v;  // bg
+            });
+        __syncthreads();
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            bb[dz] = A[dz * QQ + t];
+            bg[dz] = A[(D1 + dz) * QQ + t];
+            gb[dz] = A[(2 * D1 + dz) * QQ + t];
+        }
+    } else {
         double by[D1], gy[D1];
 #pragma unroll
         for (int dy = 0; dy < D1; ++dy) {
@@ -244,7 +328,30 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     }
     __syncthreads();
     // stage y^T: threads (qx = tx, dy = ty); BX / GX (bufB) were last read in stage y
-    if (valid && ty < D1) {
+    if constexpr ((MF & 4) != 0) {
+        // rows (e, dz, qx), k = (W0 | Wy | Wx, qy) padded to 4 KS, cols (ZB | ZG, dy)
+        constexpr int KY = 3 * Q1;
+        block_mfma<EPB * DQ, (KY + 3) / 4>(
+            [&](int row, int k) {
+                if (k >= KY) return 0.0;
+                const int e = row / DQ, r = row % DQ, dz = r / Q1, qx = r % Q1;
+                const int which = k / Q1, qy = k % Q1;  // 0: W0, 1: Wy, 2: Wx
+                const int blk = which == 0 ? 0 : which == 1 ? 2 : 1;
+                return bufA[e][(blk * D1 + dz) * QQ + qy * Q1 + qx];
+            },
+            [&](int k, int col) {
+                if (k >= KY || col >= 2 * D1) return 0.0;
+                const int which = k / Q1, qy = k % Q1;
+                if (col < D1) return which == 0 ? sBt[qy * D1 + col] : which == 1 ? sGt[qy * D1 + col] : 0.0;
+                return which == 2 ? sBt[qy * D1 + col - D1] : 0.0;
+            },
+            [&](int row, int col, double v) {
+                if (col >= 2 * D1) return;
+                const int e = row / DQ, r = row % DQ, dz = r / Q1, qx = r % Q1;
+                const int dy = col < D1 ? col : col - D1;
+                bufB[e][(col < D1 ? 0 : DD * Q1) + (dz * D1 + dy) * Q1 + qx] = v;
+            });
+    } else if (valid && ty < D1) {
         double cb[Q1], cg[Q1];
 #pragma unroll
         for (int qy = 0; qy < Q1; ++qy) {
@@ -266,6 +373,22 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     }
     __syncthreads();
     // stage x^T -> E-vector: threads (dx = tx, dy = ty)
+    if constexpr ((MF & 8) != 0) {
+        // rows (e, dz, dy), k = (ZB | ZG, qx), cols dx; Y into bufA (W0 / Wx / Wy are dead)
+        block_mfma<EPB * DD, (2 * Q1 + 3) / 4>(
+            [&](int row, int k) {
+                if (k >= 2 * Q1) return 0.0;
+                const int e = row / DD, r = row % DD;
+                return bufB[e][(k < Q1 ? 0 : DD * Q1) + r * Q1 + (k < Q1 ? k : k - Q1)];
+            },
+            [&](int k, int col) {
+                return k >= 2 * Q1 || col >= D1 ? 0.0 : k < Q1 ? sBt[k * D1 + col] : sGt[(k - Q1) * D1 + col];
+            },
+            [&](int row, int col, double v) {
+                if (col < D1) bufA[row / DD][(row % DD) * D1 + col] = v;
+            });
+        __syncthreads();
+    }
     double dacc = 0.0;
     if (valid && tx < D1 && ty < D1) {
         double cb[Q1], cg[Q1];
@@ -287,10 +410,14 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 #pragma unroll
         for (int dz = 0; dz < D1; ++dz) {
             double y = 0.0;
+            if constexpr ((MF & 8) != 0) {
+                y = A[(dz * D1 + ty) * D1 + tx];
+            } else {
 #pragma unroll
-            for (int qx = 0; qx < Q1; ++qx) {
-                const int j = (dz * D1 + ty) * Q1 + qx;
-                y += cb[qx] * Bf[j] + cg[qx] * Bf[D1 * D1 * Q1 + j];
+                for (int qx = 0; qx < Q1; ++qx) {
+                    const int j = (dz * D1 + ty) * Q1 + qx;
+                    y += cb[qx] * Bf[j] + cg[qx] * Bf[D1 * D1 * Q1 + j];
+                }
             }
             __builtin_nontemporal_store(y, &ye[dz * zs]);
             if constexpr (DEN) {
@@ -307,8 +434,8 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     }
 }
 
-template <int D1, int Q1, unsigned K>
-static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
+template <int D1, int Q1, unsigned K, int MF>
+static hipError_t tile_kinds_mf(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
                              double *den_part)
 {
     const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
@@ -322,24 +449,36 @@ static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con
     geo.ess = c->d_ess;
     if (den_part) {
         if (!c->epencil || !con) return hipErrorInvalidValue;
-        CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true>), grid, block, 0, c->d_map, x, c->d_qd, Ye, T,
+        CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true, MF>), grid, block, 0, c->d_map, x, c->d_qd, Ye, T,
                      c->ne, geo, st, den_part);
     } else if (c->epencil) {
         if (con)
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, false>), grid, block, 0, c->d_map, x, c->d_qd,
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
                          Ye, T, c->ne, geo, st, (double *)nullptr);
         else
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, true, false>), grid, block, 0, c->d_map, x, c->d_qd,
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, true, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
                          Ye, T, c->ne, geo, st, (double *)nullptr);
     } else {
         if (con)
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, false, false>), grid, block, 0, c->d_map, x, c->d_qd,
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, false, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
                          Ye, T, c->ne, geo, st, (double *)nullptr);
         else
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, false, false>), grid, block, 0, c->d_map, x,
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, false, false, MF>), grid, block, 0, c->d_map, x,
                          c->d_qd, Ye, T, c->ne, geo, st, (double *)nullptr);
     }
     return hipGetLastError();
+}
+
+template <int D1, int Q1, unsigned K>
+static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
+                             double *den_part)
+{
+    switch (c->ho_mfma) {
+    case 1: return tile_kinds_mf<D1, Q1, K, 1>(c, x, Ye, con, st, den_part);
+    case 3: return tile_kinds_mf<D1, Q1, K, 3>(c, x, Ye, con, st, den_part);
+    case 15: return tile_kinds_mf<D1, Q1, K, 15>(c, x, Ye, con, st, den_part);
+    default: return tile_kinds_mf<D1, Q1, K, 0>(c, x, Ye, con, st, den_part);
+    }
 }
 
 template <int D1, int Q1>

@@ -80,6 +80,45 @@ __global__ void __launch_bounds__(64) k_stream_ileave(const double *__restrict__
     if (s == 12345.678) out[0] = s + pad[0];
 }
 
+// Workgroup chunks: NW waves of one workgroup stream ONE contiguous chunk of NW x 320 KiB together,
+// NW KiB per step (wave w reads the w-th KiB), 81 KiB of LDS per workgroup so one workgroup runs
+// per CU (one wave per SIMD at NW = 4): the qdata pattern of a kernel with four waves per brick.
+template <int U, int NW>
+__global__ void __launch_bounds__(64 * NW) k_stream_wgchunk(const double *__restrict__ a, int64_t nchunks, double *out)
+{
+    __shared__ double pad[10368];
+    if (threadIdx.x == 64 * NW) pad[0] = 0.0;
+    const int64_t b = blockIdx.x;
+    if (b >= nchunks) return;
+    const double2 *p = reinterpret_cast<const double2 *>(a + b * NW * kChunkDoubles) + threadIdx.x;
+    constexpr int iters = (int)(kChunkDoubles / 128);
+    double s = 0.0;
+    for (int i = 0; i < iters; i += U) {
+        double2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = p[(int64_t)(i + u) * 64 * NW];
+#pragma unroll
+        for (int u = 0; u < U; ++u) s += v[u].x + v[u].y;
+    }
+    if (s == 12345.678) out[0] = s + pad[0];
+}
+
+// Grid-stride 16-byte read with 64-thread blocks and 39 KB of LDS each (one wave per SIMD, 1024
+// waves): the grid-stride pattern at the brick kernel's occupancy.
+__global__ void __launch_bounds__(64) k_stream_read_1wave(const double *__restrict__ a, int64_t n, double *out)
+{
+    __shared__ double pad[4992];
+    if (threadIdx.x == 64) pad[0] = 0.0;
+    double s = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const double2 *a2 = reinterpret_cast<const double2 *>(a);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 2; i += stride) {
+        const double2 v = a2[i];
+        s += v.x + v.y;
+    }
+    if (s == 12345.678) out[0] = s + pad[0];
+}
+
 // ---- f64 compute-rate probes (VALU vs MFMA for the high-order contractions) ----
 // VALU: 8 independent v_fma_f64 chains per lane.  MFMA: 4 independent v_mfma_f64_16x16x4_f64
 // accumulators per wave (16 x 16 x 4 x 2 = 2048 flop per instruction).  ITERS loop trips; the
@@ -152,6 +191,10 @@ hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int
         break;
     }
     case 9: hipLaunchKernelGGL((k_stream_ileave<4>), dim3(nch), dim3(64), 0, c->stream, a, nch, b); break;
+    case 14: hipLaunchKernelGGL((k_stream_wgchunk<8, 4>), dim3(nch / 4), dim3(256), 0, c->stream, a, nch / 4, b); break;
+    case 15: hipLaunchKernelGGL((k_stream_wgchunk<8, 2>), dim3(nch / 2), dim3(128), 0, c->stream, a, nch / 2, b); break;
+    case 16: hipLaunchKernelGGL(k_stream_read_1wave, dim3(1024), dim3(64), 0, c->stream, a, n, b); break;
+    case 17: hipLaunchKernelGGL(k_stream_read_1wave, dim3(4096), dim3(64), 0, c->stream, a, n, b); break;
     case 0: hipLaunchKernelGGL(k_stream_read<16>, grid, block, 0, c->stream, a, n, b); break;
     case 1: hipLaunchKernelGGL(k_stream_read<8>, grid, block, 0, c->stream, a, n, b); break;
     case 2: hipLaunchKernelGGL(k_stream_copy, grid, block, 0, c->stream, a, b, n); break;

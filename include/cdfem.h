@@ -207,7 +207,10 @@ int cdfem_solve(cdfem_ctx *ctx, const cdfem_solver_params *prm, const double *B,
  * `bytes`-sized buffer, `reps` launches; returns achieved GB/s (bytes moved / time).
  * Modes 3-7: per-wave private 320 KiB chunks (16 B/lane), 8/16/8/4/32 loads in flight; 3, 4, 6, 7
  * limited to one wave per SIMD by an LDS reservation, 5 unrestricted.  Modes 8, 9: the same
- * per-wave work (8 / 4 loads in flight, one wave per SIMD) on an interleaved layout.            */
+ * per-wave work (8 / 4 loads in flight, one wave per SIMD) on an interleaved layout.  Modes 10-13:
+ * mode 3 with chunks skewed by 256 B / 512 B / 1 KiB / 4 KiB.  Modes 14, 15: 4 (one workgroup per
+ * CU) / 2 waves of a workgroup streaming one shared chunk, 4 / 2 KiB per step.  Modes 16, 17: the
+ * 16-byte grid-stride read with 64-thread blocks at one wave per SIMD, 1024 / 4096 blocks.       */
 int cdfem_stream_bench(cdfem_ctx *ctx, int mode, size_t bytes, int reps, double *gbps);
 
 /* f64 compute-rate probe (diagnostic; backs DESIGN.md's VALU-vs-MFMA choice for the high-order
@@ -219,13 +222,17 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "brick_waves": 1 or 2 — register budget of the structured Mult kernel (waves per SIMD).
  * "profile_mask": bit k set = kernel slot k (CDFEM_K_*) gets HIP events while profiling is on
  *                 (default all; events around every kernel cost ~1 us each on the stream).
- * "brick_variant": 0..6 — element core of the structured CG kernel (unrolled / plane loop /
- *                  low-register; 3-5 the same at 2 waves per SIMD; 6 temporal qdata loads).
+ * "brick_variant": 0..7 — element core of the structured CG kernel (unrolled / plane loop /
+ *                  low-register; 3-5 the same at 2 waves per SIMD; 6 temporal qdata loads;
+ *                  7 the first qdata points issued under the patch gather).
  * "brick_xcd": 1 (default) — XCD-contiguous brick order of the structured CG kernel; 0 = the
  *              dispatcher's round-robin order.
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
  *               interface pack and the exchange run on a side stream under the interior layers;
  *               0 = one launch, then the exchange (bitwise the same results).
+ * "ho_mfma": 0 (default) — the LDS stages of the high-order (3D p = 3, 4) tile apply as block GEMMs on
+ *            v_mfma_f64_16x16x4_f64: 1 = stage x, 3 = x and y, 15 = x, y, y^T and x^T (results agree
+ *            to rounding).
  * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).

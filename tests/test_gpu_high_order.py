@@ -207,3 +207,64 @@ def test_ho_c3_full_size_fused_cg(gpu_ctx):
     true = np.sqrt(r @ (r / d))
     assert abs(true - info["final_norm"]) <= 1e-6 * true
 
+
+
+@pytest.mark.parametrize("n,p,pert,structured", [(2, 3, 0.1, False), (3, 3, 0.0, True), (3, 4, 0.15, False),
+                                                 (4, 4, 0.0, True), (5, 4, 0.1, False)])
+@pytest.mark.parametrize("kinds", [7, 5, 2])
+@pytest.mark.parametrize("mf", [1, 3, 15])
+def test_ho_mfma_stages_parity(gpu_ctx, n, p, pert, structured, kinds, mf):
+    """set_option("ho_mfma", mf): the tile apply's LDS stages as block GEMMs on
+    v_mfma_f64_16x16x4_f64 (1: stage x; 3: x and y; 15: x, y, y^T and x^T).  Mult and constrained
+    Mult against the oracle (1e-13) and against the VALU stages (summation order only: 1e-14);
+    includes a partly filled last block."""
+    om = O.BoxMesh(3, n, p, perturb=pert)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(kinds))
+    x = np.random.default_rng(31).uniform(-1, 1, om.nl)
+    xz = x.copy()
+    xz[om.ess] = 0.0
+    yo = A.mult(x)
+    yc = A.mult(xz)
+    yc[om.ess] = x[om.ess]
+    out = {}
+    try:
+        for m in (0, mf):
+            gpu_ctx.set_option("ho_mfma", m)
+            gpu_ctx.upload_mesh(gm)
+            if structured:
+                gpu_ctx.set_structured(n, n, n)
+            gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            out[m] = (gpu_ctx.mult(x), gpu_ctx.mult(x, constrained=True))
+    finally:
+        gpu_ctx.set_option("ho_mfma", 0)
+    y, ycg = out[mf]
+    assert np.abs(y - yo).max() <= 1e-13 * np.abs(yo).max()
+    assert np.abs(ycg - yc).max() <= 1e-13 * np.abs(yc).max()
+    assert np.abs(y - out[0][0]).max() <= 1e-14 * np.abs(yo).max()
+
+
+@pytest.mark.parametrize("n,p", [(3, 4), (4, 3)])
+@pytest.mark.parametrize("mf", [1, 15])
+def test_ho_mfma_fused_cg_parity(gpu_ctx, n, p, mf):
+    """The fused high-order CG iteration with the MFMA stages: 50 fixed Jacobi-CG iterates with
+    non-zero essential values against the oracle (1e-11)."""
+    om = O.BoxMesh(3, n, p, perturb=0.1)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(5))
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    rng = np.random.default_rng(14)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, io = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=50)
+    try:
+        gpu_ctx.set_option("ho_mfma", mf)
+        gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+        gpu_ctx.pa_setup(kinds=5, kappa=0.1, mass=1.0)
+        _, B = gpu_ctx.form_linear_system(u, b)
+        xg, ig = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=50, check_every=7)
+    finally:
+        gpu_ctx.set_option("ho_mfma", 0)
+    assert io["iterations"] == ig["iterations"] == 50
+    assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)

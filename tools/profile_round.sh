@@ -12,9 +12,9 @@ OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p $OUT
 case $CFG in
   c2) SHORT="--cg-iters 20 --spd-steps 0";;
-  c3) SHORT="--cg-iters 4 --gmres-iters 0";;
+  c3) SHORT="--cg-iters 4 --gmres-iters 0 --spd-steps 0";;
   c4|c4s) SHORT="--gmres-iters 30";;
-  c5) SHORT="--cg-iters 10 --gmres-iters 0";;
+  c5) SHORT="--cg-iters 10 --gmres-iters 0 --spd-steps 0";;
 esac
 timeout -k 10 900 python bench.py --config $CFG --steps 5 --warmup 1 > $OUT/bench.json 2> $OUT/bench.err || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/stats -o run --output-format csv -- python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-profile-events --spd-steps 0 > $OUT/stats.log 2>&1 || exit $?
