@@ -494,6 +494,242 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     if (t == 0) part[b] = den;
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_brick_cg4 (brick_variant 8, p = 2): the same brick CG step with FOUR waves per brick and one
+// quadrature plane per lane.  Wave w takes the brick's element layer ez = w (16 elements); lane
+// (el, qz) = (lane & 15, lane >> 4) contracts its element's patch in z for plane qz only, runs the
+// 16 points of that plane (qdata point (qx, qy, qz) of element e is one lane of the brick block's
+// 16-byte loads, so a wave load reads four 256-byte runs) and the transposed x / y contractions,
+// and forms the plane's share of Y; the four planes are summed by an xor butterfly (lanes 16 and 32
+// apart), which leaves the same full Y on all four lanes of the element.  E->L: the 27 local dofs
+// fall into the 8 parity classes of (dx, dy, dz) mod 2; two element-local dofs of different classes
+// never land on the same patch position for any two elements (positions differ by 2 x the element
+// offset), so the four lanes of an element add four different classes at once: 8 barrier rounds
+// instead of 27.  ~1/4 of the per-lane registers of k_brick_cg, four times the waves.
+// Per element and dof the additions of the plane contributions run in a different order than in
+// k_brick_cg (rounding differences only).
+template <int D1, int Q1, unsigned K>
+__global__ void __launch_bounds__(256)
+k_brick_cg4(const double *__restrict__ r, const double *__restrict__ dinv, const double *__restrict__ d_old,
+            double *__restrict__ d_new, double *__restrict__ q, double *__restrict__ face,
+            const double *__restrict__ qd, const uint8_t *__restrict__ ess, const Tab<D1, Q1> T,
+            const BrickGeom g, int zlo_shared, double *__restrict__ part, const KrylovState *__restrict__ st)
+{
+    static_assert(D1 == 3 && Q1 == 4, "one quadrature plane per lane quarter: p = 2");
+    using L = QLayout<K, 3>;
+    static_assert(!L::kMD, "derived mass weight not supported here");
+    constexpr int P = D1 - 1;
+    constexpr int S = kBrick * P + 1;
+    constexpr int S2 = S * S, S3 = S * S * S;
+    constexpr int F = face_count<S>();
+    constexpr int NC = L::nc;
+    constexpr int NQ = Q1 * Q1 * Q1;
+    __shared__ double s_in[S3];
+    __shared__ double s_out[S3];
+    __shared__ double s_red[4];
+    if (st->done) return;
+    const double beta = st->beta;
+    const int t = threadIdx.x;
+    const int bl = brick_id(g), nxy = g.nbx * g.nby;
+    const int bz = g.bz0 + (bl / nxy) * g.bzs;
+    const int b = bl % nxy + nxy * bz;
+    const int bx = b % g.nbx, by = (b / g.nbx) % g.nby;
+    const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
+    const bool lastx = bx == g.nbx - 1, lasty = by == g.nby - 1, lastz = bz == g.nbz - 1;
+    const double *q0 = qd + (size_t)b * NQ * NC * kLanes;
+    double den = 0.0;
+    // patch gather, 256 threads: every load issued before any is consumed
+    constexpr int NI = (S3 + 255) / 256;
+    double rv[NI], mv[NI], ov[NI];
+    uint8_t ev[NI];
+    int64_t gidv[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int i = t + 256 * k;
+        const int px = i % S, py = (i / S) % S, pz = i / S2;
+        const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
+        const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
+        const int64_t gid = in ? gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz) : 0;
+        gidv[k] = in ? gid : -1;
+        rv[k] = r[gid];
+        mv[k] = dinv[gid];
+        ov[k] = d_old[gid];
+        ev[k] = ess[gid];
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int i = t + 256 * k;
+        if (i >= S3) break;
+        const int px = i % S, py = (i / S) % S, pz = i / S2;
+        const int gz = gz0 + pz;
+        double v = 0.0;
+        if (gidv[k] >= 0) {
+            const int64_t gid = gidv[k];
+            const double dn = mv[k] * rv[k] + beta * ov[k];
+            const bool e = ev[k] != 0;
+            const bool writer = (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
+            if (writer) {
+                d_new[gid] = dn;
+                if (e && !(zlo_shared && gz == 0)) den += dn * dn;  // (A_c d)_i = d_i on ess dofs
+            }
+            v = e ? 0.0 : dn;
+        }
+        s_in[i] = v;
+        s_out[i] = 0.0;
+    }
+    __syncthreads();
+
+    const int lane = t & 63, qz = lane >> 4;
+    const int e = (t >> 6) * 16 + (lane & 15);  // element of the brick (lane index of its qdata block)
+    const int ex = e & 3, ey = (e >> 2) & 3, ez = e >> 4;
+    const int o0 = P * ez * S2 + P * ey * S + P * ex;
+    // this lane's plane of the z tables (T is uniform; qz selects per lane)
+    double bzt[D1], gzt[D1];
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz) {
+        bzt[dz] = qz == 0 ? T.B[0][dz] : qz == 1 ? T.B[1][dz] : qz == 2 ? T.B[2][dz] : T.B[3][dz];
+        gzt[dz] = qz == 0 ? T.G[0][dz] : qz == 1 ? T.G[1][dz] : qz == 2 ? T.G[2][dz] : T.G[3][dz];
+    }
+    // contract z for plane qz
+    double T0[D1][D1], Tz[D1][D1];
+#pragma unroll
+    for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) {
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int dz = 0; dz < D1; ++dz) {
+                const double xv = s_in[o0 + dz * S2 + dy * S + dx];
+                s0 += bzt[dz] * xv;
+                s1 += gzt[dz] * xv;
+            }
+            T0[dy][dx] = s0;
+            Tz[dy][dx] = s1;
+        }
+    double RT[D1][D1], RTz[D1][D1];
+#pragma unroll
+    for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) { RT[dy][dx] = 0.0; RTz[dy][dx] = 0.0; }
+    const double *qp0 = q0 + (size_t)(Q1 * Q1 * qz) * NC * kLanes;
+#pragma unroll
+    for (int qy = 0; qy < Q1; ++qy) {
+        double a[D1], ay[D1], az[D1];
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) {
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+            for (int dy = 0; dy < D1; ++dy) {
+                s0 += T.B[qy][dy] * T0[dy][dx];
+                s1 += T.G[qy][dy] * T0[dy][dx];
+                s2 += T.B[qy][dy] * Tz[dy][dx];
+            }
+            a[dx] = s0; ay[dx] = s1; az[dx] = s2;
+        }
+        double Rv[D1], Ry[D1], Rz[D1];
+#pragma unroll
+        for (int dx = 0; dx < D1; ++dx) { Rv[dx] = 0.0; Ry[dx] = 0.0; Rz[dx] = 0.0; }
+#pragma unroll
+        for (int qx = 0; qx < Q1; ++qx) {
+            double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                u += T.B[qx][dx] * a[dx];
+                ux += T.G[qx][dx] * a[dx];
+                uy += T.B[qx][dx] * ay[dx];
+                uz += T.B[qx][dx] * az[dx];
+            }
+            double qv[NC];
+            load_qp<NC, true>(qp0 + (size_t)(qx + Q1 * qy) * NC * kLanes, e, qv);
+            double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
+            if constexpr (L::kD) {
+                gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;
+                gy = qv[1] * ux + qv[3] * uy + qv[4] * uz;
+                gz = qv[2] * ux + qv[4] * uy + qv[5] * uz;
+            }
+            if constexpr (L::kC) vv = qv[L::oC] * ux + qv[L::oC + 1] * uy + qv[L::oC + 2] * uz;
+            if constexpr (L::kM) vv += qv[L::oM] * u;
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                if constexpr (L::kD) {
+                    Rv[dx] += T.B[qx][dx] * vv + T.G[qx][dx] * gx;
+                    Ry[dx] += T.B[qx][dx] * gy;
+                    Rz[dx] += T.B[qx][dx] * gz;
+                } else {
+                    Rv[dx] += T.B[qx][dx] * vv;
+                }
+            }
+        }
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                if constexpr (L::kD) {
+                    RT[dy][dx] += T.B[qy][dy] * Rv[dx] + T.G[qy][dy] * Ry[dx];
+                    RTz[dy][dx] += T.B[qy][dy] * Rz[dx];
+                } else {
+                    RT[dy][dx] += T.B[qy][dy] * Rv[dx];
+                }
+            }
+    }
+    // this plane's share of Y, then the sum over the four planes (xor butterfly: every lane of the
+    // element ends with the same value)
+    double Y[D1][D1][D1];
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) {
+                double y = L::kD ? bzt[dz] * RT[dy][dx] + gzt[dz] * RTz[dy][dx] : bzt[dz] * RT[dy][dx];
+                y += __shfl_xor(y, 16, 64);
+                y += __shfl_xor(y, 32, 64);
+                Y[dz][dy][dx] = y;
+            }
+    // E->L in 8 rounds: lane quarter qz adds the local dofs of its parity classes
+    //   qz 0: (e,e,e) 8 dofs; 1: (o,e,e) + (e,o,o) + (o,o,o) 7; 2: (e,o,e) + (o,e,o) 6; 3: (e,e,o) + (o,o,e) 6
+    // ((dx, dy, dz) mod 2, e = even, o = odd), in a fixed order per quarter
+    constexpr int kRounds = 8;
+    constexpr signed char kStep[4][kRounds][3] = {
+        {{0, 0, 0}, {2, 0, 0}, {0, 2, 0}, {2, 2, 0}, {0, 0, 2}, {2, 0, 2}, {0, 2, 2}, {2, 2, 2}},
+        {{1, 0, 0}, {1, 2, 0}, {1, 0, 2}, {1, 2, 2}, {0, 1, 1}, {2, 1, 1}, {1, 1, 1}, {-1, 0, 0}},
+        {{0, 1, 0}, {2, 1, 0}, {0, 1, 2}, {2, 1, 2}, {1, 0, 1}, {1, 2, 1}, {-1, 0, 0}, {-1, 0, 0}},
+        {{0, 0, 1}, {2, 0, 1}, {0, 2, 1}, {2, 2, 1}, {1, 1, 0}, {1, 1, 2}, {-1, 0, 0}, {-1, 0, 0}}};
+#pragma unroll
+    for (int k = 0; k < kRounds; ++k) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            constexpr int dummy = 0;
+            (void)dummy;
+            if (qz == g4 && kStep[g4][k][0] >= 0) {
+                const int dx = kStep[g4][k][0], dy = kStep[g4][k][1], dz = kStep[g4][k][2];
+                const int o = o0 + dz * S2 + dy * S + dx;
+                const double y = Y[dz][dy][dx];
+                den += s_in[o] * y;
+                s_out[o] += y;
+            }
+        }
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int i = t + 256 * k;
+        if (i >= S3) break;
+        const int px = i % S, py = (i / S) % S, pz = i / S2;
+        const double v = s_out[i];
+        if (px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1) {
+            face[(size_t)b * F + face_index<S>(px, py, pz)] = v;
+            continue;
+        }
+        const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
+        if (gx >= g.Lx || gy >= g.Ly || gz >= g.Lz) continue;
+        q[gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz)] = v;  // ess rows: replaced by d in the update
+    }
+    den = block_sum(den, s_red);
+    if (t == 0) part[b] = den;
+}
+
 template <int S>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ q,
@@ -591,6 +827,17 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     g.bzs = run.bzs;
     const dim3 grid((unsigned)(c->nbx * c->nby * run.nlay)), block(64);
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
+    if constexpr (D1 == 3 && Q1 == 4 && !QLayout<K, 3>::kMD) {
+        if (c->brick_variant == 8 && !c->xfold_x) {  // four waves per brick (k_brick_cg4)
+            if (whole)
+                CDFEM_LAUNCH(c, (k_brick_cg4<D1, Q1, K>), grid, dim3(256), 0, r, dinv, d_old, d_new, q, c->d_face,
+                             c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);
+            else
+                hipLaunchKernelGGL((k_brick_cg4<D1, Q1, K>), grid, dim3(256), 0, run.s, r, dinv, d_old, d_new, q,
+                                   c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);
+            return hipGetLastError();
+        }
+    }
 #define CDFEM_L(V)                                                                                  \
     do {                                                                                            \
         if (whole)                                                                                  \

@@ -451,6 +451,12 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     // update (ho_kernels.hip k_apply3d_tile<DEN>, vec_kernels.hip k_e2l_box<UPD>)
     const bool fused = !mr && !c->fa_ready && c->cg_fused && tile_den_ok(c) && e2l_box_ok(c);
     if (fused && !c->d_tpart) c->d_tpart = dalloc<double>(tile_den_blocks(c));
+    // fused + dfold: the direction d = z + beta d_old is formed inside the next apply's gather and
+    // written by each dof's owner element into the other direction buffer (dcur <-> dnext)
+    const bool dfold = fused && c->cg_dfold;
+    if (dfold && !c->d_dalt) c->d_dalt = dalloc<double>(c->nl);
+    double *dnext = dfold ? c->d_dalt : nullptr;
+    bool first_apply = true;
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     if (mr) {
@@ -464,7 +470,13 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     auto apply = [&] {
         prof_mark(c, CDFEM_K_APPLY, true);
         if (fused) {  // Ye = A_c d and den; q stays an E-vector until the update
-            HIPCHK(launch_apply_den(c, d, c->d_Ye, c->d_state, c->d_tpart));
+            if (dfold && !first_apply) {
+                HIPCHK(launch_apply_den(c, z, c->d_Ye, c->d_state, c->d_tpart, d, dnext));
+                std::swap(d, dnext);  // the update and the next apply read the new direction
+            } else {
+                HIPCHK(launch_apply_den(c, d, c->d_Ye, c->d_state, c->d_tpart));
+            }
+            first_apply = false;
             prof_mark(c, CDFEM_K_APPLY, false);
             prof_mark(c, CDFEM_K_E2L, true);
             HIPCHK(launch_den_from_partials(c, c->d_tpart, tile_den_blocks(c)));
@@ -504,9 +516,11 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
                 HIPCHK(launch_update_step(c));
             }
             prof_mark(c, CDFEM_K_UPDATE, false);
-            prof_mark(c, CDFEM_K_DIRECTION, true);
-            HIPCHK(launch_cg_direction(c, z, d));
-            prof_mark(c, CDFEM_K_DIRECTION, false);
+            if (!dfold) {
+                prof_mark(c, CDFEM_K_DIRECTION, true);
+                HIPCHK(launch_cg_direction(c, z, d));
+                prof_mark(c, CDFEM_K_DIRECTION, false);
+            }
             apply();
         }
         HIPCHK(hipMemcpyAsync(c->h_state, c->d_state, sizeof(KrylovState), hipMemcpyDeviceToHost,
@@ -1461,7 +1475,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         if (!key) throw ArgError("key is null");
         const std::string k(key);
         if (k == "brick_variant") {
-            if (value < 0 || value > 7) throw ArgError("brick_variant must be 0..7");
+            if (value < 0 || value > 8) throw ArgError("brick_variant must be 0..8");
             c->brick_variant = value;
 
         } else if (k == "brick_xcd") {
@@ -1471,9 +1485,12 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 1) throw ArgError("mr_overlap must be 0 or 1");
             c->mr_overlap = value;
         } else if (k == "ho_mfma") {
-            if (value != 0 && value != 1 && value != 3 && value != 15)
-                throw ArgError("ho_mfma must be 0, 1, 3 or 15");
+            if (value != 0 && value != 1 && value != 3 && value != 8 && value != 9 && value != 15)
+                throw ArgError("ho_mfma must be 0, 1, 3, 8, 9 or 15");
             c->ho_mfma = value;
+        } else if (k == "cg_dfold") {
+            if (value < 0 || value > 1) throw ArgError("cg_dfold must be 0 or 1");
+            c->cg_dfold = value;
         } else if (k == "cg_fused") {
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;

@@ -204,6 +204,7 @@ struct cdfem_ctx {
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
+    int cg_dfold = 0;                   // set_option "cg_dfold": fused CG forms d = z + beta d in the apply's gather (measured slower, off)
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int mass_from_d = 0;                // set_option "mass_from_d": derive the 3D mass weight from D (constant kappa, s; A/B, measured slower)
     int diag_sf = 1;                    // set_option "diag_sf": sum-factorised PA diagonal (0: per-entry quadrature loop)
@@ -392,7 +393,9 @@ bool spmv_delta(const cdfem_ctx *c);
 // fused high-order CG iteration (ho_kernels.hip / vec_kernels.hip)
 bool tile_den_ok(const cdfem_ctx *c);
 int tile_den_blocks(const cdfem_ctx *c);
-hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part);
+// dold != nullptr: d = z + beta dold formed in the gather (d argument = z), written to dout
+hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part,
+                            const double *dold = nullptr, double *dout = nullptr);
 bool e2l_box_ok(const cdfem_ctx *c);
 hipError_t launch_den_from_partials(cdfem_ctx *c, const double *in, int64_t n);
 hipError_t launch_e2l_cg_update(cdfem_ctx *c, const double *Ye, const double *d, double *x, double *r, double *z,

@@ -26,10 +26,11 @@
 // whole element's qdata (Q1 planes) is issued at kernel entry, in flight behind the gather and the
 // x / y stages.  Streaming (non-temporal) loads keep the L-vector in L2 for the gathers.
 //
-// MFMA is not used: on gfx950 the f64 MFMA rate equals the f64 vector FMA rate
-// (MI355X_MICROARCH.md), and these contractions (6x5 by 5xN) fill at most 6/16 x 5/8 of a
-// 16x16x4 f64 tile; the kernel is bounded by the qdata stream (8 * 10 * 216 bytes per element
-// against ~20 k FMA).
+// MFMA (set_option "ho_mfma", off by default): the four LDS stages also exist as block-wide GEMMs
+// on v_mfma_f64_16x16x4_f64 (block_mfma below).  On gfx950 the f64 MFMA rate is ~1.2x the f64
+// vector FMA rate and these contractions fill at most half of a 16x16x4 tile; the kernel is
+// bounded by the qdata stream (8 * 10 * 216 bytes per element against ~20 k FMA), so one stage on
+// the matrix cores measures even and more stages measure slower.
 #include <hip/hip_runtime.h>
 
 #include "cdfem_internal.hpp"
@@ -90,13 +91,18 @@ __device__ __forceinline__ void block_mfma(const FA &a, const FB &b, const FO &o
 //   bit 3  stage x^T  Y(e dz dy, dx)              = [ZB | ZG](e dz dy, qx) . [B; G](qx, dx)
 // Each writes LDS; the VALU z stage and quadrature-point operator stay per thread.
 
-template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, int MF>
+// DIR (with DEN): the CG direction is formed in the gather, d = z + beta d_old with x = z and
+// x2 = d_old (st->beta from the update's finalizer), and the element that owns a dof writes it to
+// dout (a different buffer than x2: other elements still gather d_old) -- no separate direction pass.
+template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, int MF, bool DIR = false>
 __global__ void __launch_bounds__(256)
 k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qd,
                double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const TileGeo geo,
-               const KrylovState *__restrict__ st, double *__restrict__ part)
+               const KrylovState *__restrict__ st, double *__restrict__ part,
+               const double *__restrict__ x2 = nullptr, double *__restrict__ dout = nullptr)
 {
     static_assert(!DEN || (CON && LAT), "den partials need the constrained lattice path");
+    static_assert(!DIR || DEN, "the folded direction runs in the fused CG apply");
     if (st != nullptr && st->done) return;
     using L = QLayout<K, 3>;
     constexpr int NC = L::nc, NP = NC / 2, QQ = Q1 * Q1, ND = D1 * D1 * D1;
@@ -140,19 +146,21 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     const int ec = valid ? e : ne - 1;
     const int gx = tx < D1 ? tx : D1 - 1, gy = ty < D1 ? ty : D1 - 1;
     uint32_t ex = 0, ey = 0, ez = 0;
-    double xr[D1];
+    double xr[D1], xo[DIR ? D1 : 1];
     int32_t m[D1];  // LAT: ess flag; map path: map entry
+    size_t g0 = 0, sz = 0;
     if constexpr (LAT) {
         const uint32_t r = fdiv((uint32_t)ec, geo.ho.fnx);
         ex = (uint32_t)ec - r * geo.ho.nx;
         ez = fdiv(r, geo.ho.fny);
         ey = r - ez * geo.ho.ny;
         constexpr int P = D1 - 1;
-        const size_t g0 = (size_t)(ex * P + gx) + (size_t)geo.Lx * ((ey * P + gy) + (size_t)geo.Ly * (ez * P));
-        const size_t sz = (size_t)geo.Lx * geo.Ly;
+        g0 = (size_t)(ex * P + gx) + (size_t)geo.Lx * ((ey * P + gy) + (size_t)geo.Ly * (ez * P));
+        sz = (size_t)geo.Lx * geo.Ly;
 #pragma unroll
         for (int dz = 0; dz < D1; ++dz) {
             xr[dz] = x[g0 + dz * sz];
+            if constexpr (DIR) xo[dz] = x2[g0 + dz * sz];
             m[dz] = CON ? geo.ess[g0 + dz * sz] : 0;
         }
     } else {
@@ -178,6 +186,18 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
                 qv[qz][2 * p + 1] = w.y;
             }
             if constexpr (NC & 1) qv[qz][NC - 1] = __builtin_nontemporal_load(qp + 2 * NP * QQ + t);
+        }
+    }
+    if constexpr (DIR) {
+        // d = z + beta d_old (k_cg_direction's formula), written once by the dof's owner element
+        const double beta = st->beta;
+        constexpr int P = D1 - 1;
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            xr[dz] = xr[dz] + beta * xo[dz];
+            const bool own = gthr && (tx < P || ex == geo.ho.nx - 1) && (ty < P || ey == geo.ho.ny - 1) &&
+                             (dz < P || ez == geo.nz - 1);
+            if (own) __builtin_nontemporal_store(xr[dz], dout + g0 + dz * sz);
         }
     }
     // unconditional store (a conditional one lets the compiler sink the gather loads behind the
@@ -436,7 +456,7 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 
 template <int D1, int Q1, unsigned K, int MF>
 static hipError_t tile_kinds_mf(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
-                             double *den_part)
+                             double *den_part, const double *dold = nullptr, double *dout = nullptr)
 {
     const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
     constexpr int EPB = 256 / (Q1 * Q1);
@@ -449,33 +469,40 @@ static hipError_t tile_kinds_mf(cdfem_ctx *c, const double *x, double *Ye, bool 
     geo.ess = c->d_ess;
     if (den_part) {
         if (!c->epencil || !con) return hipErrorInvalidValue;
-        CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true, MF>), grid, block, 0, c->d_map, x, c->d_qd, Ye, T,
-                     c->ne, geo, st, den_part);
+        if (dold)
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true, MF, true>), grid, block, 0, c->d_map, x,
+                         c->d_qd, Ye, T, c->ne, geo, st, den_part, dold, dout);
+        else
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true, MF>), grid, block, 0, c->d_map, x, c->d_qd,
+                         Ye, T, c->ne, geo, st, den_part, (const double *)nullptr, (double *)nullptr);
     } else if (c->epencil) {
         if (con)
             CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st, (double *)nullptr);
+                         Ye, T, c->ne, geo, st, (double *)nullptr, (const double *)nullptr, (double *)nullptr);
         else
             CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, true, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st, (double *)nullptr);
+                         Ye, T, c->ne, geo, st, (double *)nullptr, (const double *)nullptr, (double *)nullptr);
     } else {
         if (con)
             CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, false, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st, (double *)nullptr);
+                         Ye, T, c->ne, geo, st, (double *)nullptr, (const double *)nullptr, (double *)nullptr);
         else
             CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, false, false, MF>), grid, block, 0, c->d_map, x,
-                         c->d_qd, Ye, T, c->ne, geo, st, (double *)nullptr);
+                         c->d_qd, Ye, T, c->ne, geo, st, (double *)nullptr, (const double *)nullptr, (double *)nullptr);
     }
     return hipGetLastError();
 }
 
 template <int D1, int Q1, unsigned K>
 static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
-                             double *den_part)
+                             double *den_part, const double *dold, double *dout)
 {
+    if (dold) return tile_kinds_mf<D1, Q1, K, 0>(c, x, Ye, con, st, den_part, dold, dout);
     switch (c->ho_mfma) {
     case 1: return tile_kinds_mf<D1, Q1, K, 1>(c, x, Ye, con, st, den_part);
     case 3: return tile_kinds_mf<D1, Q1, K, 3>(c, x, Ye, con, st, den_part);
+    case 8: return tile_kinds_mf<D1, Q1, K, 8>(c, x, Ye, con, st, den_part);
+    case 9: return tile_kinds_mf<D1, Q1, K, 9>(c, x, Ye, con, st, den_part);
     case 15: return tile_kinds_mf<D1, Q1, K, 15>(c, x, Ye, con, st, den_part);
     default: return tile_kinds_mf<D1, Q1, K, 0>(c, x, Ye, con, st, den_part);
     }
@@ -483,18 +510,18 @@ static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con
 
 template <int D1, int Q1>
 static hipError_t tile_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
-                          double *den_part)
+                          double *den_part, const double *dold = nullptr, double *dout = nullptr)
 {
     switch (c->kinds) {
-    case 1: return tile_kinds<D1, Q1, 1>(c, x, Ye, con, st, den_part);
-    case 2: return tile_kinds<D1, Q1, 2>(c, x, Ye, con, st, den_part);
-    case 3: return tile_kinds<D1, Q1, 3>(c, x, Ye, con, st, den_part);
-    case 4: return tile_kinds<D1, Q1, 4>(c, x, Ye, con, st, den_part);
-    case 5: return tile_kinds<D1, Q1, 5>(c, x, Ye, con, st, den_part);
-    case 6: return tile_kinds<D1, Q1, 6>(c, x, Ye, con, st, den_part);
-    case 7: return tile_kinds<D1, Q1, 7>(c, x, Ye, con, st, den_part);
-    case 5 | kMassFromD: return tile_kinds<D1, Q1, 5 | kMassFromD>(c, x, Ye, con, st, den_part);
-    case 7 | kMassFromD: return tile_kinds<D1, Q1, 7 | kMassFromD>(c, x, Ye, con, st, den_part);
+    case 1: return tile_kinds<D1, Q1, 1>(c, x, Ye, con, st, den_part, dold, dout);
+    case 2: return tile_kinds<D1, Q1, 2>(c, x, Ye, con, st, den_part, dold, dout);
+    case 3: return tile_kinds<D1, Q1, 3>(c, x, Ye, con, st, den_part, dold, dout);
+    case 4: return tile_kinds<D1, Q1, 4>(c, x, Ye, con, st, den_part, dold, dout);
+    case 5: return tile_kinds<D1, Q1, 5>(c, x, Ye, con, st, den_part, dold, dout);
+    case 6: return tile_kinds<D1, Q1, 6>(c, x, Ye, con, st, den_part, dold, dout);
+    case 7: return tile_kinds<D1, Q1, 7>(c, x, Ye, con, st, den_part, dold, dout);
+    case 5 | kMassFromD: return tile_kinds<D1, Q1, 5 | kMassFromD>(c, x, Ye, con, st, den_part, dold, dout);
+    case 7 | kMassFromD: return tile_kinds<D1, Q1, 7 | kMassFromD>(c, x, Ye, con, st, den_part, dold, dout);
     default: return hipErrorInvalidValue;
     }
 }
@@ -520,11 +547,12 @@ bool tile_den_ok(const cdfem_ctx *c)
 }
 
 // CG mode: Ye = A_c d (E-vector) and the den partials (one per block) into part
-hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part)
+hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part,
+                            const double *dold, double *dout)
 {
     const int q1 = c->rule_op.q1;
-    if (c->p == 3 && q1 == 5) return tile_dq<4, 5>(c, d, Ye, true, st, part);
-    if (c->p == 4 && q1 == 6) return tile_dq<5, 6>(c, d, Ye, true, st, part);
+    if (c->p == 3 && q1 == 5) return tile_dq<4, 5>(c, d, Ye, true, st, part, dold, dout);
+    if (c->p == 4 && q1 == 6) return tile_dq<5, 6>(c, d, Ye, true, st, part, dold, dout);
     return hipErrorInvalidValue;
 }
 

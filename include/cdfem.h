@@ -231,8 +231,12 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               interface pack and the exchange run on a side stream under the interior layers;
  *               0 = one launch, then the exchange (bitwise the same results).
  * "ho_mfma": 0 (default) — the LDS stages of the high-order (3D p = 3, 4) tile apply as block GEMMs on
- *            v_mfma_f64_16x16x4_f64: 1 = stage x, 3 = x and y, 15 = x, y, y^T and x^T (results agree
+ *            v_mfma_f64_16x16x4_f64, bit 0 = stage x, 1 = y, 2 = y^T, 3 = x^T; the masks 1, 3, 8, 9
+ *            and 15 are built (results agree
  *            to rounding).
+ * "cg_dfold": 0 (default) — 1 = in the fused high-order CG (cg_fused) the direction d = z + beta d
+ *             is formed in the next apply's gather and written by each dof's owner element, with no
+ *             direction pass (same arithmetic; measured slower at C3).
  * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).

@@ -476,3 +476,40 @@ def test_config_c1_reference_case(gpu_ctx):
         assert np.linalg.norm(xg - xo) <= tol * np.linalg.norm(xo)
         eg, eo = O.l2_error(om, xg, prm), O.l2_error(om, xo, prm)
         assert abs(eg - eo) <= 1e-6 * eo and eo < 1e-2
+
+
+@pytest.mark.parametrize("shape,kinds", [((8, 8, 8), 7), ((8, 8, 8), 5), ((9, 6, 7), 7), ((4, 4, 12), 1)])
+def test_brick_cg4_parity(gpu_ctx, shape, kinds):
+    """brick_variant 8 (k_brick_cg4: four waves per brick, one quadrature plane per lane, butterfly
+    plane sum, parity-class E->L) and 7 (qdata issued under the patch gather): fixed Jacobi-CG
+    iterates with essential values against the oracle (1e-11) and against variant 0 (1e-12), on
+    cubes, partial bricks and every kinds mask it serves; bitwise repeatable."""
+    nx, ny, nz = shape
+    p = 2
+    om = O.BoxMesh(3, shape, p, perturb=0.1)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    gpu_ctx.upload_mesh(gm).set_structured(nx, ny, nz)
+    gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    ko = (O.DIFFUSION if kinds & 1 else 0) | (O.CONVECTION if kinds & 2 else 0) | (O.MASS if kinds & 4 else 0)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=ko)
+    rng = np.random.default_rng(33)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
+    out = {}
+    try:
+        for v in (0, 7, 8):
+            gpu_ctx.set_option("brick_variant", v)
+            out[v] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40,
+                                   check_every=11)
+        x8b, _ = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=11)
+    finally:
+        gpu_ctx.set_option("brick_variant", 0)
+    for v, (xg, ig) in out.items():
+        assert ig["iterations"] == 40, v
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), v
+        assert np.linalg.norm(xg - out[0][0]) <= 1e-12 * np.linalg.norm(xo), v
+    np.testing.assert_array_equal(x8b, out[8][0])
