@@ -508,8 +508,8 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
 // instead of 27.  ~1/4 of the per-lane registers of k_brick_cg, four times the waves.
 // Per element and dof the additions of the plane contributions run in a different order than in
 // k_brick_cg (rounding differences only).
-template <int D1, int Q1, unsigned K>
-__global__ void __launch_bounds__(256)
+template <int D1, int Q1, unsigned K, int WPS>
+__global__ void __launch_bounds__(256, WPS)
 k_brick_cg4(const double *__restrict__ r, const double *__restrict__ dinv, const double *__restrict__ d_old,
             double *__restrict__ d_new, double *__restrict__ q, double *__restrict__ face,
             const double *__restrict__ qd, const uint8_t *__restrict__ ess, const Tab<D1, Q1> T,
@@ -828,13 +828,23 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const dim3 grid((unsigned)(c->nbx * c->nby * run.nlay)), block(64);
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
     if constexpr (D1 == 3 && Q1 == 4 && !QLayout<K, 3>::kMD) {
-        if (c->brick_variant == 8 && !c->xfold_x) {  // four waves per brick (k_brick_cg4)
-            if (whole)
-                CDFEM_LAUNCH(c, (k_brick_cg4<D1, Q1, K>), grid, dim3(256), 0, r, dinv, d_old, d_new, q, c->d_face,
-                             c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);
-            else
-                hipLaunchKernelGGL((k_brick_cg4<D1, Q1, K>), grid, dim3(256), 0, run.s, r, dinv, d_old, d_new, q,
-                                   c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);
+        // four waves per brick (k_brick_cg4); variants 9 / 10 ask the register allocator for 3 / 4
+        // waves per SIMD (<= 168 / 128 VGPRs)
+        if (c->brick_variant >= 8 && c->brick_variant <= 10 && !c->xfold_x) {
+#define CDFEM_L4(WPS)                                                                                   \
+    do {                                                                                                \
+        if (whole)                                                                                      \
+            CDFEM_LAUNCH(c, (k_brick_cg4<D1, Q1, K, WPS>), grid, dim3(256), 0, r, dinv, d_old, d_new, q, \
+                         c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);    \
+        else                                                                                            \
+            hipLaunchKernelGGL((k_brick_cg4<D1, Q1, K, WPS>), grid, dim3(256), 0, run.s, r, dinv, d_old, \
+                               d_new, q, c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part,  \
+                               c->d_state);                                                            \
+    } while (0)
+            if (c->brick_variant == 9) CDFEM_L4(3);
+            else if (c->brick_variant == 10) CDFEM_L4(4);
+            else CDFEM_L4(1);
+#undef CDFEM_L4
             return hipGetLastError();
         }
     }

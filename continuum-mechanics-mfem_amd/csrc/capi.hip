@@ -1475,7 +1475,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         if (!key) throw ArgError("key is null");
         const std::string k(key);
         if (k == "brick_variant") {
-            if (value < 0 || value > 8) throw ArgError("brick_variant must be 0..8");
+            if (value < 0 || value > 10) throw ArgError("brick_variant must be 0..10");
             c->brick_variant = value;
 
         } else if (k == "brick_xcd") {

@@ -222,9 +222,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "brick_waves": 1 or 2 — register budget of the structured Mult kernel (waves per SIMD).
  * "profile_mask": bit k set = kernel slot k (CDFEM_K_*) gets HIP events while profiling is on
  *                 (default all; events around every kernel cost ~1 us each on the stream).
- * "brick_variant": 0..7 — element core of the structured CG kernel (unrolled / plane loop /
+ * "brick_variant": 0..10 — element core of the structured CG kernel (unrolled / plane loop /
  *                  low-register; 3-5 the same at 2 waves per SIMD; 6 temporal qdata loads;
- *                  7 the first qdata points issued under the patch gather).
+ *                  7 the first qdata points issued under the patch gather; 8-10 four waves per
+ *                  brick, one quadrature plane per lane, at 2 / 3 / 4 waves per SIMD, p = 2).
  * "brick_xcd": 1 (default) — XCD-contiguous brick order of the structured CG kernel; 0 = the
  *              dispatcher's round-robin order.
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the

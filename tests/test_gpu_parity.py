@@ -501,7 +501,7 @@ def test_brick_cg4_parity(gpu_ctx, shape, kinds):
     xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
     out = {}
     try:
-        for v in (0, 7, 8):
+        for v in (0, 7, 8, 9, 10):
             gpu_ctx.set_option("brick_variant", v)
             out[v] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40,
                                    check_every=11)
