@@ -737,12 +737,19 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
                   const double *__restrict__ face, const uint8_t *__restrict__ ess, const BrickGeom g,
                   const FastDiv fdx, const FastDiv fdxy, int zlo_shared,
                   const double *__restrict__ remote_lo, const double *__restrict__ remote_hi,
-                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step, int fold_x)
+                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step, int fold_x,
+                  const double *__restrict__ dprev)
 {
     constexpr int F = face_count<S>();
     constexpr int s1 = S - 1;
     __shared__ double sh[kRedThreads / 64];
     if (st->done) return;
+    // cg_x2 (dprev != nullptr): iteration i odd skips x (as the x-fold does), i even adds both
+    // pending terms, x + a_{i-1} d_{i-1} + a_i d_i, in the order the unpaired updates would
+    const bool x2_odd = dprev != nullptr && (st->iter & 1) != 0;
+    const bool x2_even = dprev != nullptr && !x2_odd;
+    const double alpha_prev = x2_even ? st->x2_alpha : 0.0;
+    fold_x = fold_x || x2_odd;
     double alpha;
     if (den_step) {
         // multi-rank: the MFEM den step on the all-reduced den, folded in (no one-thread kernel
@@ -770,6 +777,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         // x-fold: x += alpha d moves to the next apply (k_brick_cg) and d is needed on ess rows only
         const bool is_ess = ess[gid] != 0;
         const double di = (!fold_x || is_ess) ? d[gid] : 0.0, xi = fold_x ? 0.0 : x[gid];
+        const double dpi = x2_even ? dprev[gid] : 0.0;
         const double rold = r[gid], mi = dinv[gid];
         double qi;
         if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
@@ -801,7 +809,12 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         if (remote_lo && gz == 0) qi += remote_lo[rem];
         if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
         if (is_ess) qi = di;
-        if (!fold_x) __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
+        if (x2_even) {
+            const double x1 = xi + alpha_prev * dpi;
+            __builtin_nontemporal_store(x1 + alpha * di, &x[gid]);
+        } else if (!fold_x) {
+            __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
+        }
         const double ri = rold - alpha * qi;
         __builtin_nontemporal_store(ri, &r[gid]);
         if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
@@ -915,7 +928,7 @@ hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *d
 
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
                                   const double *dinv, const double *remote_lo, const double *remote_hi,
-                                  bool den_step)
+                                  bool den_step, const double *dprev)
 {
     const BrickGeom g = geom_of(c);
     const FastDiv fdx = make_fastdiv((uint32_t)c->Lx), fdxy = make_fastdiv((uint32_t)(c->Lx * c->Ly));
@@ -926,11 +939,11 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     if (c->p == 1)
         hipLaunchKernelGGL(k_cg_update_faces<kBrick * 1 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
                            x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
-                           remote_hi, c->d_part, c->d_state, (int)den_step, (int)(c->xfold_x != nullptr));
+                           remote_hi, c->d_part, c->d_state, (int)den_step, (int)(c->xfold_x != nullptr), dprev);
     else if (c->p == 2)
         hipLaunchKernelGGL(k_cg_update_faces<kBrick * 2 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
                            x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
-                           remote_hi, c->d_part, c->d_state, (int)den_step, (int)(c->xfold_x != nullptr));
+                           remote_hi, c->d_part, c->d_state, (int)den_step, (int)(c->xfold_x != nullptr), dprev);
     else
         return hipErrorInvalidValue;
     const hipError_t e = hipGetLastError();
@@ -950,6 +963,24 @@ k_cg_xflush(double *__restrict__ x, const double *__restrict__ dA, const double 
     const double *d = ((st->iter - 1) & 1) == 0 ? dA : dB;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         x[i] = x[i] + alpha * d[i];
+}
+
+// cg_x2 flush: an odd last update left its x += alpha d pending (d: its direction buffer)
+__global__ void __launch_bounds__(256)
+k_cg_x2flush(double *__restrict__ x, const double *__restrict__ d, int64_t n, const KrylovState *__restrict__ st)
+{
+    if (st->reserved[1] == 0) return;
+    const double alpha = st->x2_alpha;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        x[i] = x[i] + alpha * d[i];
+}
+
+hipError_t launch_cg_x2flush(cdfem_ctx *c, double *x, const double *d)
+{
+    const int64_t need = (c->nl + 255) / 256;
+    hipLaunchKernelGGL(k_cg_x2flush, dim3((unsigned)(need < 8192 ? need : 8192)), dim3(256), 0, c->stream, x, d,
+                       (int64_t)c->nl, c->d_state);
+    return hipGetLastError();
 }
 
 hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *dA, const double *dB)

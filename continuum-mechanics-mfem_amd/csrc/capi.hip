@@ -354,6 +354,10 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     } fold_guard{c};
     c->xfold_x = c->cg_xfold ? x : nullptr;
     double *const d_even = dcur, *const d_odd = dprev;  // apply k writes direction k here
+    // cg_x2: x is updated by every second iteration with both pending terms (not with the x-fold);
+    // an odd last iteration's term is flushed after the loop (odd iterations' directions live in
+    // d_even = d_dalt, the buffer the first apply writes)
+    const bool x2 = c->cg_x2 && !c->cg_xfold;
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     if (mr) {
@@ -409,7 +413,8 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             prof_mark(c, CDFEM_K_UPDATE, true);
             HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv,
                                           mr && c->zlo_shared ? c->d_if[1] : nullptr,
-                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr));
+                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr,
+                                          x2 ? dprev : nullptr));
             if (mr) {
                 comm_allreduce(c, red + 1, 1);
                 HIPCHK(launch_update_step(c));
@@ -425,6 +430,10 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     }
     if (c->xfold_x) {
         HIPCHK(launch_cg_xflush(c, x, d_even, d_odd));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    if (x2) {
+        HIPCHK(launch_cg_x2flush(c, x, d_even));
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     const auto t1 = std::chrono::steady_clock::now();
@@ -1505,6 +1514,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 1) throw ArgError("diag_sf must be 0 or 1");
             c->diag_sf = value;
             c->dinv_ready = false;
+        } else if (k == "cg_x2") {
+            if (value < 0 || value > 1) throw ArgError("cg_x2 must be 0 or 1");
+            c->cg_x2 = value;
         } else if (k == "cg_xfold") {
             if (value < 0 || value > 1) throw ArgError("cg_xfold must be 0 or 1");
             c->cg_xfold = value;

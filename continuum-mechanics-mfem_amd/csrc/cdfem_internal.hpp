@@ -77,7 +77,8 @@ struct KrylovState {
     double nom, nom0, den, alpha, beta, betanom, r0;
     double red[4];  // rank-local reductions awaiting the all-reduce (0 den, 1 betanom, 2 nom)
     int iter, done, converged, final_iter, max_iter, first_den;
-    unsigned reserved[4];
+    unsigned reserved[4];  // [0] x-fold pending; [1] paired-x (cg_x2) pending
+    double x2_alpha;       // cg_x2: alpha of the last update (its x += alpha d is pending if reserved[1])
 };
 
 // Device-side GMRES(m) state (gmres.hip).  The first 32 bytes are what the host polls.
@@ -204,6 +205,7 @@ struct cdfem_ctx {
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
+    int cg_x2 = 0;                      // set_option "cg_x2": brick CG updates x every second iteration (two terms)
     int cg_dfold = 0;                   // set_option "cg_dfold": fused CG forms d = z + beta d in the apply's gather (measured slower, off)
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int mass_from_d = 0;                // set_option "mass_from_d": derive the 3D mass weight from D (constant kappa, s; A/B, measured slower)
@@ -315,9 +317,10 @@ hipError_t launch_update_fin(cdfem_ctx *c, int nparts);
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
                             double *d_new, double *q);
 // q from interior/face partials (+ remote interface sums), x += alpha d, r -= alpha q, betanom
+// dprev != nullptr (cg_x2): x is updated only by even iterations, x += a_{i-1} dprev + a_i d
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
                                   const double *dinv, const double *remote_lo, const double *remote_hi,
-                                  bool den_step = false);
+                                  bool den_step = false, const double *dprev = nullptr);
 // generic deterministic dot into host-visible scalar via state (used by GMRES / tests)
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out);
 // multi-rank CG: rank-local (d, q) over owned entries into the state's den slot (all-reduce next)
@@ -344,6 +347,8 @@ hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double
 hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q, hipStream_t s = nullptr);
 // brick CG x-fold: flush the pending x += alpha d after the loop (dA / dB: the even / odd directions)
 hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *dA, const double *dB);
+// cg_x2: the pending x += alpha d of an odd last update (d = that update's direction buffer)
+hipError_t launch_cg_x2flush(cdfem_ctx *c, double *x, const double *d);
 hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
                                   double *d_new, double *q, hipStream_t s);
 

@@ -249,6 +249,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
  * "spmv_variant": 0 (default) / 1 — SpMV inner loop (4 loads in flight / software-pipelined; A/B).
  * "diag_sf": 1 (default) — sum-factorised PA diagonal; 0 = per-entry quadrature loop.
+ * "cg_x2": 0 (default) / 1 — structured CG: x is updated by every second iteration with both
+ *          pending terms (x + a_{i-1} d_{i-1} + a_i d_i; an odd last iteration is flushed after the
+ *          loop), bitwise the per-iteration update; not combined with cg_xfold.
  * "cg_xfold": 0 (default) / 1 — structured CG: fold x += alpha d into the next apply (bitwise the
  *             same; measured slower, A/B).
  * "mass_from_d": 0 (default) / 1 — 3D PA with constant kappa, s: derive the mass weight from the

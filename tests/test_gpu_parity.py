@@ -513,3 +513,32 @@ def test_brick_cg4_parity(gpu_ctx, shape, kinds):
         assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), v
         assert np.linalg.norm(xg - out[0][0]) <= 1e-12 * np.linalg.norm(xo), v
     np.testing.assert_array_equal(x8b, out[8][0])
+
+
+@pytest.mark.parametrize("max_iter,rel_tol,check", [(30, 0.0, 16), (31, 0.0, 7), (2000, 1e-10, 16), (2000, 1e-9, 5),
+                                                     (1, 0.0, 16), (2, 0.0, 16), (0, 0.0, 16)])
+def test_brick_cg_x2_bitwise(gpu_ctx, max_iter, rel_tol, check):
+    """set_option("cg_x2"): odd iterations leave x alone, even ones add both pending terms
+    (x + a_{i-1} d_{i-1} + a_i d_i, in that order), and an odd last iteration is flushed after the
+    loop.  The same adds in the same order: bitwise the per-iteration update, for even and odd
+    stopping points, on convergence and before the first update; with essential values set."""
+    n, p = 8, 2
+    om = O.BoxMesh(3, n, p, perturb=0.1)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    rng = np.random.default_rng(78)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    _, B = gpu_ctx.form_linear_system(u, rng.uniform(-1, 1, om.nl))
+    out = {}
+    try:
+        for x2 in (0, 1):
+            gpu_ctx.set_option("cg_x2", x2)
+            out[x2] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=rel_tol, abs_tol=0.0,
+                                    max_iter=max_iter, check_every=check)
+    finally:
+        gpu_ctx.set_option("cg_x2", 0)
+    (x0, i0), (x1, i1) = out[0], out[1]
+    assert i0["iterations"] == i1["iterations"] and i0["converged"] == i1["converged"]
+    np.testing.assert_array_equal(x1, x0)
