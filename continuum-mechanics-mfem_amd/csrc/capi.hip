@@ -103,6 +103,7 @@ void free_mesh(cdfem_ctx *c)
     partition_free(c);
     c->nslices = c->nstored = 0;
     c->sell_windowed = false;
+    c->sell_xcd_sorted = false;
     c->geom = 0;
     c->fa_ready = false;
     c->nnz = 0;
@@ -1216,7 +1217,8 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             std::vector<double> xyz;
             if (!multi_rank(c) && (c->sell_mode == 3 || c->sell_mode == 5) && !c->h_verts.empty())
                 xyz = simplex_dof_coords(c->dim, c->p, c->ne, c->nd, c->nl, c->h_verts, c->h_dofs);
-            FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl, multi_rank(c) ? 0 : c->sell_mode, c->dim,
+            FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl,
+                                           multi_rank(c) ? 0 : (c->sell_mode | (c->spmv_xcd_sort ? 0x100 : 0)), c->dim,
                                            xyz.empty() ? nullptr : xyz.data());
             c->nnz = P.nnz;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
@@ -1247,6 +1249,7 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             HIPCHK(hipMemcpyAsync(c->d_scols, P.scols.data(), P.scols.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_smap, P.smap.data(), P.smap.size() * 4, hipMemcpyHostToDevice, c->stream));
             c->sell_windowed = P.windowed;
+            c->sell_xcd_sorted = P.xcd_sorted;
             if (!P.perm.empty()) {
                 c->d_rperm = dalloc<int32_t>(P.perm.size());
                 HIPCHK(hipMemcpyAsync(c->d_rperm, P.perm.data(), P.perm.size() * 4, hipMemcpyHostToDevice, c->stream));
@@ -1523,6 +1526,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "spmv_variant") {
             if (value < 0 || value > 1) throw ArgError("spmv_variant must be 0 or 1");
             c->spmv_variant = value;
+        } else if (k == "spmv_xcd_sort") {  // read when the FA pattern is built
+            if (value < 0 || value > 1) throw ArgError("spmv_xcd_sort must be 0 or 1");
+            c->spmv_xcd_sort = value;
         } else if (k == "spmv_xcd") {
             if (value < 0 || value > 1) throw ArgError("spmv_xcd must be 0 or 1");
             c->spmv_xcd = value;

@@ -218,6 +218,8 @@ struct cdfem_ctx {
     int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD (windowed layout)
     int32_t *d_rperm = nullptr;         // SpMV space order: space row -> mesh row (null: mesh order)
     bool sell_windowed = false;         // slices cut from the space order (kernel row = slice * 64 + lane)
+    bool sell_xcd_sorted = false;       // global layout sorted per XCD row range (spmv_xcd_sort)
+    int spmv_xcd_sort = 0;              // set_option "spmv_xcd_sort" (read when the FA pattern is built)
     double *d_pv[2] = {};               // permuted-space scratch (apply in mesh order; solve B / X)
     bool perm_space = false;            // inside a solve that runs in the permuted order
     double *d_dinv_p = nullptr;         // the Jacobi scale in permuted order (during such a solve)
@@ -366,12 +368,14 @@ struct FaPattern {
     std::vector<int16_t> sdel;   // [stored] column - row when every |column - row| < 2^15, else empty
     std::vector<int32_t> perm;   // SpMV space order (sell_plan.cpp): space row -> mesh row; empty = mesh order
     bool windowed = false;       // slices cut from the space order directly (no srows)
+    bool xcd_sorted = false;     // rows length-sorted inside 8 contiguous ranges of 256-row multiples
 };
 // SpMV order (sell_plan.cpp): 0 natural + global sort, 1 natural + windows, 2 RCM + windows,
 // 3 auto (mode 0, geometric or RCM + global), 4 RCM + global, 5 geometric + global
 struct SellPlan {
     int mode = 0, base = 1;  // base: 1 natural, 2 RCM, 3 geometric
     bool windowed = false;
+    bool xcd_sort = false;   // global layout: length sort inside 8 contiguous row ranges (one per XCD)
     int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0, bw_geometric = 0;
     std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
 };

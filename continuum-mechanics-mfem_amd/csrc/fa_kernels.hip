@@ -132,7 +132,10 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     });
     // SpMV layout: SELL-64 over the rows in the plan's order (sell_plan.cpp)
     P.rowptr = std::move(rowptr);
-    sell_build(P, nl, sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode, dim, dof_xyz));
+    // sell_mode bit 8: the global layout's length sort per XCD row range (set_option spmv_xcd_sort)
+    SellPlan pl = sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode & 0xff, dim, dof_xyz);
+    pl.xcd_sort = (sell_mode & 0x100) != 0;
+    sell_build(P, nl, pl);
     return P;
 }
 
@@ -550,7 +553,7 @@ static int sell_xcd_per(const cdfem_ctx *c)
 {
     // contiguous per-XCD ranges pay on the windowed layout (1.00x traffic); the global length sort
     // puts the longest rows first, and a range split would hand them all to XCD 0
-    return c->spmv_xcd && c->sell_windowed ? (int)((sell_blocks(c) + 7) / 8) : 0;
+    return (c->spmv_xcd && c->sell_windowed) || c->sell_xcd_sorted ? (int)((sell_blocks(c) + 7) / 8) : 0;
 }
 unsigned sell_grid(const cdfem_ctx *c)
 {

@@ -247,6 +247,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan).  A permuted order runs the
  *               Krylov solve in that order (Mult to rounding, iterates to 1e-12).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
+ * "spmv_xcd_sort": 0 (default) / 1 — global SpMV layout sorted by row length inside 8 contiguous
+ *                  row ranges, one per XCD, instead of over the whole matrix (read when the FA
+ *                  pattern is built; bitwise the same SpMV).
  * "spmv_variant": 0 (default) / 1 — SpMV inner loop (4 loads in flight / software-pipelined; A/B).
  * "diag_sf": 1 (default) — sum-factorised PA diagonal; 0 = per-entry quadrature loop.
  * "cg_x2": 0 (default) / 1 — structured CG: x is updated by every second iteration with both
