@@ -730,7 +730,7 @@ k_brick_cg4(const double *__restrict__ r, const double *__restrict__ dinv, const
     if (t == 0) part[b] = den;
 }
 
-template <int S>
+template <int S, bool X2>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ q,
                   const double *__restrict__ d, const double *__restrict__ dinv,
@@ -746,8 +746,8 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
     if (st->done) return;
     // cg_x2 (dprev != nullptr): iteration i odd skips x (as the x-fold does), i even adds both
     // pending terms, x + a_{i-1} d_{i-1} + a_i d_i, in the order the unpaired updates would
-    const bool x2_odd = dprev != nullptr && (st->iter & 1) != 0;
-    const bool x2_even = dprev != nullptr && !x2_odd;
+    const bool x2_odd = X2 && (st->iter & 1) != 0;
+    const bool x2_even = X2 && !x2_odd;
     const double alpha_prev = x2_even ? st->x2_alpha : 0.0;
     fold_x = fold_x || x2_odd;
     double alpha;
@@ -777,7 +777,8 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         // x-fold: x += alpha d moves to the next apply (k_brick_cg) and d is needed on ess rows only
         const bool is_ess = ess[gid] != 0;
         const double di = (!fold_x || is_ess) ? d[gid] : 0.0, xi = fold_x ? 0.0 : x[gid];
-        const double dpi = x2_even ? dprev[gid] : 0.0;
+        double dpi = 0.0;
+        if constexpr (X2) dpi = x2_even ? dprev[gid] : 0.0;
         const double rold = r[gid], mi = dinv[gid];
         double qi;
         if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
@@ -809,7 +810,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         if (remote_lo && gz == 0) qi += remote_lo[rem];
         if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
         if (is_ess) qi = di;
-        if (x2_even) {
+        if (X2 && x2_even) {
             const double x1 = xi + alpha_prev * dpi;
             __builtin_nontemporal_store(x1 + alpha * di, &x[gid]);
         } else if (!fold_x) {
@@ -936,16 +937,21 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     // loads, so every dof's chain must be in flight at once
     const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
     const unsigned grid = (unsigned)(need < 16384 ? need : 16384);
-    if (c->p == 1)
-        hipLaunchKernelGGL(k_cg_update_faces<kBrick * 1 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
-                           x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
-                           remote_hi, c->d_part, c->d_state, (int)den_step, (int)(c->xfold_x != nullptr), dprev);
+#define CDFEM_UPD(S_, X2_)                                                                                \
+    hipLaunchKernelGGL((k_cg_update_faces<S_, X2_>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, q, d,   \
+                       dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, c->d_part, \
+                       c->d_state, (int)den_step, (int)(c->xfold_x != nullptr), dprev)
+    if (c->p == 1 && dprev)
+        CDFEM_UPD(kBrick * 1 + 1, true);
+    else if (c->p == 1)
+        CDFEM_UPD(kBrick * 1 + 1, false);
+    else if (c->p == 2 && dprev)
+        CDFEM_UPD(kBrick * 2 + 1, true);
     else if (c->p == 2)
-        hipLaunchKernelGGL(k_cg_update_faces<kBrick * 2 + 1>, dim3(grid), dim3(kRedThreads), 0, c->stream,
-                           x, r, q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo,
-                           remote_hi, c->d_part, c->d_state, (int)den_step, (int)(c->xfold_x != nullptr), dprev);
+        CDFEM_UPD(kBrick * 2 + 1, false);
     else
         return hipErrorInvalidValue;
+#undef CDFEM_UPD
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (multi_rank(c)) return launch_fin_sum(c, (int)grid, 1);
