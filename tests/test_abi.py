@@ -92,3 +92,19 @@ def test_rccl_selftest_built_against_rccl():
         return [ln.split("=>")[1].split()[0] for ln in out.splitlines() if "librccl" in ln]
 
     assert rccl_of(exe) and rccl_of(exe) == rccl_of(so)
+
+
+def test_every_option_key_is_documented():
+    """Every key cdfem_set_option accepts (capi.hip) is documented with its default in
+    include/cdfem.h, and an unknown key is refused (no silent no-op switches)."""
+    import os
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "continuum-mechanics-mfem_amd", "csrc", "capi.hip")).read()
+    hdr = open(os.path.join(root, "include", "cdfem.h")).read()
+    keys = sorted(set(re.findall(r'k == "([a-z_0-9]+)"', src)))
+    assert len(keys) >= 15
+    missing = [k for k in keys if f'"{k}"' not in hdr]
+    assert not missing, missing
+    # refusal of an unknown key needs a context, i.e. a GPU: pinned by the source instead
+    assert 'unknown option' in src
