@@ -95,10 +95,12 @@ void free_mesh(cdfem_ctx *c)
     for (auto &b : c->d_if) dfree(b);
     dfree(c->d_stab); dfree(c->d_stab_lf); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);
     dfree(c->d_cpos); dfree(c->d_vals); dfree(c->d_vals_c); dfree(c->d_Ee);
-    dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_sdel); dfree(c->d_svals);
+    dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_sdel_base); dfree(c->d_svals);
+    c->d_sdel = nullptr;
     dfree(c->d_rperm); dfree(c->d_pv[0]); dfree(c->d_pv[1]); dfree(c->d_dinv_p);
     c->d_rperm = nullptr; c->d_pv[0] = c->d_pv[1] = nullptr; c->d_dinv_p = nullptr;
-    dfree(c->d_svals_c);
+    dfree(c->d_svals_c_base);
+    c->d_svals_c = nullptr;
     ilu_free(c);
     partition_free(c);
     c->nslices = c->nstored = 0;
@@ -1243,7 +1245,10 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             c->d_scols = dalloc<int32_t>(P.scols.size());
             c->d_smap = dalloc<int32_t>(P.smap.size());
             c->d_svals = dalloc<double>(c->nstored);
-            c->d_svals_c = dalloc<double>(c->nstored);
+            // sell_offset: the solve's value stream starts sell_offset bytes into its allocation
+            // (placement A/B)
+            c->d_svals_c_base = dalloc<double>(c->nstored + c->sell_offset / 8);
+            c->d_svals_c = c->d_svals_c_base + c->sell_offset / 8;
             HIPCHK(hipMemcpyAsync(c->d_sptr, P.sptr.data(), P.sptr.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_srows, P.srows.data(), P.srows.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_scols, P.scols.data(), P.scols.size() * 4, hipMemcpyHostToDevice, c->stream));
@@ -1256,7 +1261,8 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
                 for (auto &v : c->d_pv) v = dalloc<double>(c->nl);
             }
             if (!P.sdel.empty()) {
-                c->d_sdel = dalloc<int16_t>(P.sdel.size());
+                c->d_sdel_base = dalloc<int16_t>(P.sdel.size() + c->sell_offset / 2);
+                c->d_sdel = c->d_sdel_base + c->sell_offset / 2;
                 HIPCHK(hipMemcpyAsync(c->d_sdel, P.sdel.data(), P.sdel.size() * 2, hipMemcpyHostToDevice, c->stream));
             }
             HIPCHK(hipStreamSynchronize(c->stream));  // P's host buffers die at scope exit
@@ -1529,6 +1535,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "spmv_xcd_sort") {  // read when the FA pattern is built
             if (value < 0 || value > 1) throw ArgError("spmv_xcd_sort must be 0 or 1");
             c->spmv_xcd_sort = value;
+        } else if (k == "sell_offset") {  // read when the FA operator is set up
+            if (value < 0 || value > (4 << 20) || value % 256) throw ArgError("sell_offset must be a multiple of 256 in [0, 4 MiB]");
+            c->sell_offset = value;
         } else if (k == "spmv_xcd") {
             if (value < 0 || value > 1) throw ArgError("spmv_xcd must be 0 or 1");
             c->spmv_xcd = value;

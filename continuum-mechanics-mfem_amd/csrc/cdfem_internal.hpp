@@ -220,6 +220,9 @@ struct cdfem_ctx {
     bool sell_windowed = false;         // slices cut from the space order (kernel row = slice * 64 + lane)
     bool sell_xcd_sorted = false;       // global layout sorted per XCD row range (spmv_xcd_sort)
     int spmv_xcd_sort = 0;              // set_option "spmv_xcd_sort" (read when the FA pattern is built)
+    int sell_offset = 0;                // set_option "sell_offset": bytes the SpMV's value / delta streams start past their allocation
+    double *d_svals_c_base = nullptr;   // allocations behind d_svals_c / d_sdel (sell_offset)
+    int16_t *d_sdel_base = nullptr;
     double *d_pv[2] = {};               // permuted-space scratch (apply in mesh order; solve B / X)
     bool perm_space = false;            // inside a solve that runs in the permuted order
     double *d_dinv_p = nullptr;         // the Jacobi scale in permuted order (during such a solve)

@@ -247,6 +247,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan).  A permuted order runs the
  *               Krylov solve in that order (Mult to rounding, iterates to 1e-12).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
+ * "sell_offset": 0 (default) — bytes (a multiple of 256, at most 4 MiB) by which the SpMV's
+ *                constrained value stream and 16-bit delta stream start past their allocations
+ *                (read at cdfem_fa_setup; a placement A/B switch, same results).
  * "spmv_xcd_sort": 0 (default) / 1 — global SpMV layout sorted by row length inside 8 contiguous
  *                  row ranges, one per XCD, instead of over the whole matrix (read when the FA
  *                  pattern is built; bitwise the same SpMV).
