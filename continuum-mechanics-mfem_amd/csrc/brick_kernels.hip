@@ -61,7 +61,9 @@ constexpr int face_count() { return 2 * S * S + (S - 2) * (4 * S - 4); }
 
 // MODE 0: y = A x;  MODE 1: y = A_c x (ConstrainedOperator);  MODE 2: CG-fused (x := r)
 // W: minimum waves per SIMD requested from the register allocator (1: unconstrained, 2: <= 256
-// VGPR+AGPR so two bricks share a SIMD; selected at run time, CDFEM_BRICK_WAVES, default 2)
+// VGPR+AGPR so two bricks share a SIMD, at 124 B/lane of spills; selected at run time,
+// CDFEM_BRICK_WAVES / set_option "brick_waves", default 1: 241.5 vs 272.2 us per C2 apply in the
+// GMRES leg, tools/ab_gmres.py, profiles/r02_ab_c2_gmres_brick_waves.txt)
 template <int D1, int Q1, unsigned K, int MODE, int W>
 __global__ void __launch_bounds__(64, W)
 k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double *__restrict__ d,

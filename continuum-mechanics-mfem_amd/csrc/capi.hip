@@ -662,7 +662,7 @@ int cdfem_create(int device, cdfem_ctx **out)
     cdfem_ctx *c = new (std::nothrow) cdfem_ctx();
     if (!c) return CDFEM_ERR_HIP;
     c->device = device;
-    if (const char *w = std::getenv("CDFEM_BRICK_WAVES")) c->brick_waves = std::atoi(w) == 1 ? 1 : 2;
+    if (const char *w = std::getenv("CDFEM_BRICK_WAVES")) c->brick_waves = std::atoi(w) == 2 ? 2 : 1;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_state, sizeof(KrylovState)) != hipSuccess ||

@@ -152,7 +152,7 @@ struct cdfem_ctx {
     double *d_ones = nullptr;           // all-ones vector (unpreconditioned brick CG)
     double *d_dalt = nullptr;           // second search-direction buffer (brick CG)
     int nface = 0;                      // F
-    int brick_waves = 2;                // register budget of k_brick3d (CDFEM_BRICK_WAVES)
+    int brick_waves = 1;                // register budget of k_brick3d (CDFEM_BRICK_WAVES); 1: no spills, measured faster
     int brick_xcd = 1;                  // k_brick_cg brick order: 0 dispatch, 1 XCD-contiguous (default)
     int brick_variant = 0;              // element core of k_brick_cg (0 unrolled, 1 plane loop, 2 low-reg)
     int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)

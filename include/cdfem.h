@@ -219,7 +219,8 @@ int cdfem_stream_bench(cdfem_ctx *ctx, int mode, size_t bytes, int reps, double 
 int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
 
 /* ---- tuning knobs (performance only; results identical to rounding) --------------------------
- * "brick_waves": 1 or 2 — register budget of the structured Mult kernel (waves per SIMD).
+ * "brick_waves": 1 (default) or 2 — register budget of the structured Mult kernel (waves per SIMD;
+ *                2 spills 124 B per lane and measured 11 % slower in the C2 GMRES leg).
  * "profile_mask": bit k set = kernel slot k (CDFEM_K_*) gets HIP events while profiling is on
  *                 (default all; events around every kernel cost ~1 us each on the stream).
  * "brick_variant": 0..10 — element core of the structured CG kernel (unrolled / plane loop /
