@@ -561,11 +561,14 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     const int m = p.restart > 0 ? p.restart : 30;
     if (m > kGmMaxRestart) throw ArgError("restart > 64");
     const int64_t n = c->nl;
+    // basis leading dimension padded to 32 doubles: every basis vector starts on a 256-byte
+    // boundary, so a wave's 512-byte load of v_i covers 4 cache lines, not 5 (odd n)
+    const int64_t ldv = (n + 31) / 32 * 32;
     const int nb = gmres_blocks(n);
     if (c->gm_cap < m) {
         dfree(c->d_gm);
         dfree(c->d_gm_part);
-        c->d_gm = dalloc<double>((size_t)(m + 1) * n);
+        c->d_gm = dalloc<double>((size_t)(m + 1) * ldv);
         c->d_gm_part = dalloc<double>((size_t)(m + 1) * nb);
         c->gm_cap = m;
     }
@@ -612,16 +615,16 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
         post(0);
         if (wait(0).done) break;
         for (int j = 0; j < m; ++j) {
-            op_apply_global(c, V + (int64_t)j * n, w, true);
+            op_apply_global(c, V + (int64_t)j * ldv, w, true);
             if (ilu) HIPCHK(ilu_apply(c));  // w <- (LU)^{-1} A v_j, in ilu.z
             prof_mark(c, CDFEM_K_ORTH, true);
-            HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, n, part, st, m, &poll[j & 1]));
+            HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, ldv, part, st, m, &poll[j & 1]));
             prof_mark(c, CDFEM_K_ORTH, false);
             post(j & 1);
             if (j > 0 && wait((j - 1) & 1).cycle_done) break;
         }
         prof_mark(c, CDFEM_K_UPDATE, true);
-        HIPCHK(launch_gm_update(c, x, V, n, st, &poll[0]));
+        HIPCHK(launch_gm_update(c, x, V, ldv, st, &poll[0]));
         prof_mark(c, CDFEM_K_UPDATE, false);
         post(0);
         if (wait(0).done) break;
