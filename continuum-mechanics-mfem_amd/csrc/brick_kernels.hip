@@ -701,8 +701,6 @@ k_brick_cg4(const double *__restrict__ r, const double *__restrict__ dinv, const
     for (int k = 0; k < kRounds; ++k) {
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-            constexpr int dummy = 0;
-            (void)dummy;
             if (qz == g4 && kStep[g4][k][0] >= 0) {
                 const int dx = kStep[g4][k][0], dy = kStep[g4][k][1], dz = kStep[g4][k][2];
                 const int o = o0 + dz * S2 + dy * S + dx;
