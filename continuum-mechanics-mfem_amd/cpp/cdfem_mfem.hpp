@@ -41,7 +41,7 @@
 // partial sums).  FormLinearSystem returns true-dof vectors X, B (the dofs this rank owns: the lowest
 // rank holding a shared dof owns it) and the constrained operator P^T A P on them; RecoverFEMSolution
 // is x = P X.  The ranks exchange through RCCL when every rank has its own GPU, otherwise through MPI
-// (CDFEM_COMM=rccl|host overrides).  Multi-rank ILU (PETSc bjacobi per rank) is not provided.
+// (CDFEM_COMM=rccl|host overrides).  -pc_type bjacobi on several ranks: one ILU(0) block per rank.
 #pragma once
 
 #include <mpi.h>
@@ -1225,6 +1225,7 @@ public:
     bool OnMarkedBoundary(int i, const Array<int> &marker, int dim) const
     {
         if (simplex_) {
+            // attributes above 31 cannot occur: the gmsh reader and cdfem_simplex_space reject them
             for (int a = 1; a <= marker.Size() && a <= 31; ++a)
                 if (marker[a - 1] && (bmask_[(size_t)i] & (1 << (a - 1)))) return true;
             return false;
@@ -1954,8 +1955,9 @@ public:
 };
 
 // PETSc's PCILU (zero fill, natural ordering) as a preconditioner marker: "-pc_type bjacobi
-// -sub_pc_type ilu" (Input/petsc_circle.opts:6-8) on one rank, or "-pc_type ilu".  Factored once per
-// operator on the device (ilu_kernels.hip) and applied inside the device GMRES.
+// -sub_pc_type ilu" (Input/petsc_circle.opts:6-8; on several ranks one block per rank, the owned
+// diagonal block of the global matrix), or "-pc_type ilu" on one rank.  Factored once per operator
+// on the device (ilu_kernels.hip) and applied inside the device GMRES.
 class ILUPreconditioner : public Solver {
 public:
     ILUPreconditioner() = default;
@@ -2165,24 +2167,27 @@ private:
         solver_->SetMaxIter(maxit_ >= 0 ? maxit_ : std::stoi(Opt("ksp_max_it", "10000")));
         solver_->SetPrintLevel(print_);
         const FiniteElementSpace *fes = cop.Form()->FESpace();
-        const bool ilu_ok = fes->Simplex() && fes->NRanks() == 1;  // assembled, one rank
+        const bool ilu_ok = fes->Simplex();  // assembled (one rank, or a general partition)
         std::string pc = Opt("pc_type", "");
-        if (pc.empty()) {  // PETSc's default preconditioner
-            pc = ilu_ok ? "ilu" : "jacobi";
+        if (pc.empty()) {  // PETSc's default preconditioner: ILU on one rank, block Jacobi + ILU on several
+            pc = ilu_ok ? (fes->NRanks() == 1 ? "ilu" : "bjacobi") : "jacobi";
             if (!ilu_ok && Mpi::Root())
                 std::fprintf(stderr, "note: no -%spc_type: PETSc's default ILU / block Jacobi is not available for this "
-                                     "operator; using Jacobi\n", prefix_.c_str());
+                                     "(matrix-free) operator; using Jacobi\n", prefix_.c_str());
         }
         if (pc == "jacobi") {
             solver_->SetPreconditioner(jac_);
         } else if (pc == "ilu" || pc == "bjacobi") {
-            // one rank: block Jacobi has a single block, solved by its sub-PC (preonly + ILU)
+            // block Jacobi: one block per rank (the owned diagonal block of the global matrix),
+            // solved by its sub-PC (preonly + ILU(0)); on one rank that is PCILU itself.  PETSc's
+            // PCILU has no parallel (MPIAIJ) factorisation, so -pc_type ilu needs one rank.
             const std::string sub = pc == "ilu" ? "ilu" : Opt("sub_pc_type", "ilu");
             const std::string subksp = Opt("sub_ksp_type", "preonly");
             if (sub != "ilu" || subksp != "preonly")
                 throw std::invalid_argument("unsupported block-Jacobi sub solver " + subksp + "/" + sub);
-            if (fes->NRanks() > 1)
-                throw std::invalid_argument("-pc_type " + pc + " on several ranks (block Jacobi per rank) is not provided");
+            if (pc == "ilu" && fes->NRanks() > 1)
+                throw std::invalid_argument("-pc_type ilu on several ranks (PETSc has no parallel ILU; use bjacobi)");
+            if (!ilu_ok) throw std::invalid_argument("-pc_type " + pc + " needs an assembled (simplex) operator");
             solver_->SetPreconditioner(ilu_);
         } else if (pc != "none") {
             throw std::invalid_argument("unsupported -" + prefix_ + "pc_type " + pc);

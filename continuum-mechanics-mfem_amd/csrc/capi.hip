@@ -583,7 +583,8 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
         dinv = solver_dinv(c);
     } else if (ilu) {
         if (!c->fa_ready) throw UnsupportedError("ILU(0) needs an assembled operator (cdfem_fa_setup)");
-        if (multi_rank(c)) throw UnsupportedError("ILU(0) on a multi-rank partition");
+        if (multi_rank(c) && c->part_mode != 2)
+            throw UnsupportedError("block-Jacobi ILU(0) needs a general partition (cdfem_set_shared)");
         ilu_setup(c);
     }
     double *x = c->d_w[2], *w = c->d_w[4], *V = c->d_gm, *part = c->d_gm_part;
@@ -937,6 +938,7 @@ int cdfem_set_shared(cdfem_ctx *c, int n_nbr, const int32_t *nbr_ranks, const in
         partition_free(c);
         c->nbr_rank = ranks;
         c->nbr_off = off;
+        c->h_sh_idx = idx;
         c->n_shd = (int32_t)dofs.size();
         c->d_sh_idx = dalloc<int32_t>(ntot);
         c->d_sh_send = dalloc<double>(ntot);

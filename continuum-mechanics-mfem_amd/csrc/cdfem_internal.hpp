@@ -105,6 +105,13 @@ struct IluState {
     int32_t *rows_l = nullptr, *rows_u = nullptr;  // rows grouped by level
     std::vector<int32_t> ptr_l, ptr_u;   // level pointers (host)
     double *z = nullptr;                 // output of one application
+    // multi-rank (PETSc bjacobi, one ILU(0) block per rank): the factored matrix is the owned
+    // diagonal block of the global eliminated matrix, on rows/columns [skip_lo, nl), in its own
+    // pattern; the sweeps write the owned part of z and the owners' values are then copied to the
+    // non-owned shared entries
+    bool block = false;
+    int32_t *rp = nullptr, *cols = nullptr, *diag = nullptr;  // block pattern (owned; else the CSR's)
+    int64_t nnz = 0;
     hipGraph_t graph = nullptr;          // the captured forward + backward sweeps
     hipGraphExec_t exec = nullptr;
 };
@@ -169,6 +176,7 @@ struct cdfem_ctx {
     // sides; send/recv buffers concatenated in neighbour order
     std::vector<int32_t> nbr_rank;
     std::vector<int64_t> nbr_off;       // [n_nbr + 1]
+    std::vector<int32_t> h_sh_idx;      // [n_sh] local dof of send/recv slot (host copy)
     int32_t *d_sh_idx = nullptr;        // [n_sh] local dof of send/recv slot
     double *d_sh_send = nullptr, *d_sh_recv = nullptr;
     int32_t n_shd = 0;                  // distinct shared dofs
@@ -339,6 +347,9 @@ void comm_exchange(cdfem_ctx *c, const double *send_lo, double *recv_lo, const d
 void interface_sum(cdfem_ctx *c, double *v);  // L-vector interface planes summed over ranks
 // non-owned shared entries of an L-vector <- the owner's value (MFEM P applied to R v)
 void interface_copy_owner(cdfem_ctx *c, double *v);
+// general partition: send[off[k]..off[k+1]) -> nbr_rank[k], recv[same range] <- it (device buffers)
+void comm_exchange_nbr_buf(cdfem_ctx *c, const std::vector<int64_t> &off, const double *dsend, double *drecv,
+                           hipStream_t s = nullptr);
 void partition_free(cdfem_ctx *c);
 inline bool multi_rank(const cdfem_ctx *c) { return c->nranks > 1; }
 // split CG finalizers for the multi-rank path: local sum -> all-reduce -> step

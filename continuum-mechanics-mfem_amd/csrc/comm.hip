@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "cdfem_internal.hpp"
 
@@ -81,7 +82,10 @@ void comm_allreduce(cdfem_ctx *c, double *dbuf, int n)
         hipStreamSynchronize(c->stream) != hipSuccess)
         throw std::runtime_error("allreduce staging failed");
     if (m->h_allreduce(h, n, m->user) != 0) throw std::runtime_error("host allreduce callback failed");
-    if (hipMemcpyAsync(dbuf, h, n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    // the staging buffer may be shared with other contexts (cdfem_comm_share): complete the
+    // upload before any other exchange can overwrite it
+    if (hipMemcpyAsync(dbuf, h, n * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
         throw std::runtime_error("allreduce staging failed");
 }
 
@@ -180,33 +184,42 @@ __global__ void k_sh_copy_owner(double *__restrict__ v, const int32_t *__restric
     if (i < n && owner[i] >= 0) v[dofs[i]] = recv[owner[i]];
 }
 
-// send[nbr_off[k]..) -> nbr_rank[k], recv[nbr_off[k]..) <- nbr_rank[k], for every neighbour
-static void comm_exchange_nbr(cdfem_ctx *c, hipStream_t s)
+// send[off[k]..off[k+1]) -> nbr_rank[k], recv[same range] <- nbr_rank[k], for every neighbour
+// (device buffers; the two ranks of a pair use the same count)
+void comm_exchange_nbr_buf(cdfem_ctx *c, const std::vector<int64_t> &off, const double *dsend, double *drecv,
+                           hipStream_t s)
 {
+    if (!s) s = c->stream;
     Comm *m = c->comm;
     const int nn = (int)c->nbr_rank.size();
-    if (nn == 0) return;
-    const int64_t ntot = c->nbr_off[nn];
+    if (nn == 0 || !m || m->nranks == 1) return;
+    const int64_t ntot = off[nn];
     if (m->nccl) {
         nccl_check(ncclGroupStart(), "ncclGroupStart");
         for (int k = 0; k < nn; ++k) {
-            const int64_t o = c->nbr_off[k], cnt = c->nbr_off[k + 1] - o;
-            nccl_check(ncclSend(c->d_sh_send + o, cnt, ncclDouble, c->nbr_rank[k], m->nccl, s), "ncclSend");
-            nccl_check(ncclRecv(c->d_sh_recv + o, cnt, ncclDouble, c->nbr_rank[k], m->nccl, s), "ncclRecv");
+            const int64_t o = off[k], cnt = off[k + 1] - o;
+            nccl_check(ncclSend(dsend + o, cnt, ncclDouble, c->nbr_rank[k], m->nccl, s), "ncclSend");
+            nccl_check(ncclRecv(drecv + o, cnt, ncclDouble, c->nbr_rank[k], m->nccl, s), "ncclRecv");
         }
         nccl_check(ncclGroupEnd(), "ncclGroupEnd");
         return;
     }
     if (!m->h_nbr) throw std::runtime_error("host communicator has no neighbour exchange (cdfem_comm_set_host_nbr_exchange)");
     double *h = host_staging(m, 2 * (size_t)ntot);
-    if (hipMemcpyAsync(h, c->d_sh_send, ntot * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(h, dsend, ntot * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         throw std::runtime_error("exchange staging failed");
-    if (m->h_nbr(nn, c->nbr_rank.data(), c->nbr_off.data(), h, h + ntot, m->nbr_user) != 0)
+    if (m->h_nbr(nn, c->nbr_rank.data(), off.data(), h, h + ntot, m->nbr_user) != 0)
         throw std::runtime_error("host neighbour exchange callback failed");
-    if (hipMemcpyAsync(c->d_sh_recv, h + ntot, ntot * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+    if (hipMemcpyAsync(drecv, h + ntot, ntot * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         throw std::runtime_error("exchange staging failed");
+}
+
+static void comm_exchange_nbr(cdfem_ctx *c, hipStream_t s)
+{
+    if (c->nbr_rank.empty()) return;
+    comm_exchange_nbr_buf(c, c->nbr_off, c->d_sh_send, c->d_sh_recv, s);
 }
 
 static void shared_pack_exchange(cdfem_ctx *c, const double *v)
@@ -230,6 +243,8 @@ void partition_free(cdfem_ctx *c)
     }
     c->nbr_rank.clear();
     c->nbr_off.clear();
+    c->h_sh_idx.clear();
+    ilu_free(c);  // a block-Jacobi factor belongs to the previous partition
     c->n_shd = 0;
     c->part_mode = 0;
     c->skip_lo = 0;

@@ -272,9 +272,12 @@ int cdfem_kuhn_mesh(int dim, int n, int order, double perturb, double *elem_vert
 // replaces: make_unique<Mesh>(params.mesh_file.c_str(), 1, 1) (linear_convection_diffusion_2D.cpp:290)
 // + H1_FECollection(order, dim) + ParFiniteElementSpace (:311-313) for simplex meshes.
 // Domain elements: triangles (2D) or tetrahedra (3D, when present); boundary elements: lines (2D) or
-// triangles (3D), physical tag = boundary attribute.  Numbering: vertex dofs in increasing gmsh node
-// id, then (order - 1) dofs per edge (edges in order of first appearance, dofs along the direction
-// of increasing vertex dof), then P3 triangle interiors.  Elements are re-oriented to det J > 0.
+// triangles (3D), physical tag = boundary attribute (1..31; a larger tag is an error, not a silently
+// dropped boundary).  Numbering (MFEM's, for triangles): vertex dofs in increasing gmsh node id,
+// triangles re-ordered as MFEM's Finalize does (mfem_finalize_triangle), then (order - 1) dofs per
+// edge (edges in order of first appearance, dofs along the direction of increasing vertex dof), then
+// P3 triangle interiors.  Tetrahedra are re-oriented to det J > 0 (MFEM's MarkTetMeshForRefinement
+// vertex order is not restated).
 namespace {
 
 struct Gmsh {
@@ -299,6 +302,34 @@ struct Topo {
     int ne() const { return dim ? (int)(ev.size() / (dim + 1)) : 0; }
     int nbe() const { return (int)battr.size(); }
 };
+
+// MFEM's vertex order for a triangle read from a file: Mesh(file, generate_edges = 1, refine = 1)
+// (linear_convection_diffusion_2D.cpp:290) finalizes with CheckElementOrientation(fix = true), which
+// swaps vertices 0 and 1 of a clockwise triangle, and then MarkTriMeshForRefinement, which rotates
+// every triangle so that its longest edge is 0-1 (Triangle::MarkEdge: squared lengths d0 = |v1-v0|^2,
+// d1 = |v2-v1|^2, d2 = |v2-v0|^2; keep if d0 >= d1 and d0 >= d2, else rotate by 1 if d1 > d0 and
+// d1 >= d2, else by 2).  The rotation fixes the order in which edges are first met, so it fixes the
+// edge-dof numbering, which PETSc's ILU(0) (Input/petsc_circle.opts:6-8) depends on.
+void mfem_finalize_triangle(const Topo &T, std::array<int32_t, 4> &v)
+{
+    auto P = [&](int i, int d) { return T.vxyz[(size_t)v[i] * 2 + d]; };
+    const double det = (P(1, 0) - P(0, 0)) * (P(2, 1) - P(0, 1)) - (P(1, 1) - P(0, 1)) * (P(2, 0) - P(0, 0));
+    if (det < 0.0) std::swap(v[0], v[1]);
+    auto sq = [](double a) { return a * a; };
+    const double d0 = sq(P(1, 0) - P(0, 0)) + sq(P(1, 1) - P(0, 1));
+    const double d1 = sq(P(2, 0) - P(1, 0)) + sq(P(2, 1) - P(1, 1));
+    const double d2 = sq(P(2, 0) - P(0, 0)) + sq(P(2, 1) - P(0, 1));
+    int shift;
+    if (d0 >= d1) {
+        if (d0 >= d2) return;
+        shift = 2;
+    } else {
+        shift = d1 >= d2 ? 1 : 2;
+    }
+    const std::array<int32_t, 4> o = v;
+    if (shift == 1) { v[0] = o[1]; v[1] = o[2]; v[2] = o[0]; }
+    else { v[0] = o[2]; v[1] = o[0]; v[2] = o[1]; }
+}
 
 bool parse_gmsh(const char *path, Topo &T, std::string &err)
 {
@@ -359,10 +390,17 @@ bool parse_gmsh(const char *path, Topo &T, std::string &err)
     }
     for (const El &e : els) {
         if (e.type != dtype) continue;
-        for (int i = 0; i <= dim; ++i) T.ev.push_back(vid[e.v[i]]);
+        std::array<int32_t, 4> v{};
+        for (int i = 0; i <= dim; ++i) v[i] = vid[e.v[i]];
+        if (dim == 2) mfem_finalize_triangle(T, v);
+        for (int i = 0; i <= dim; ++i) T.ev.push_back(v[i]);
     }
     for (const El &e : els) {
-        if (e.type != btype || e.tag < 1 || e.tag > 31) continue;
+        if (e.type != btype || e.tag < 1) continue;
+        if (e.tag > 31) {
+            err = "boundary physical tag " + std::to_string(e.tag) + " > 31: boundary attributes 1..31 are supported";
+            return false;
+        }
         bool inside = true;
         for (long n : e.v) inside = inside && vid.count(n);
         if (!inside) continue;
@@ -376,6 +414,8 @@ bool parse_gmsh(const char *path, Topo &T, std::string &err)
 // H1 Lagrange space of order p on a simplex topology.  Numbering: vertex dofs = vertex index, then
 // (order - 1) dofs per edge (edges in order of first appearance, dofs along the direction of
 // increasing vertex dof), then P3 triangle interiors.  Elements are re-oriented to det J > 0.
+const int kMfemTriEdge[3][2] = {{0, 1}, {1, 2}, {2, 0}};
+
 bool build_space(const Topo &T, int order, Gmsh &G, std::string &err)
 {
     const int dim = T.dim;
@@ -407,10 +447,13 @@ bool build_space(const Topo &T, int order, Gmsh &G, std::string &err)
         }
         if (det == 0.0) { err = "degenerate element"; return false; }
         tv.push_back(v);
+        // edges are numbered in order of first appearance, met in MFEM's local edge order
+        // (Geometry::Constants<TRIANGLE>::Edges = (0,1),(1,2),(2,0); tetrahedra (0,1),(0,2),(0,3),
+        // (1,2),(1,3),(2,3)), as Mesh::GetElementToEdgeTable's DSTable does
         if (ne_dofs > 0)
             for (int ed = 0; ed < nedge_loc; ++ed) {
-                const int la = dim == 3 ? cdfem::kSimplexEdge[ed][0] : cdfem::kTriEdge[ed][0];
-                const int lb = dim == 3 ? cdfem::kSimplexEdge[ed][1] : cdfem::kTriEdge[ed][1];
+                const int la = dim == 3 ? cdfem::kSimplexEdge[ed][0] : kMfemTriEdge[ed][0];
+                const int lb = dim == 3 ? cdfem::kSimplexEdge[ed][1] : kMfemTriEdge[ed][1];
                 int32_t ga = v[la], gb = v[lb];
                 if (ga > gb) std::swap(ga, gb);
                 edge.emplace(std::make_pair(ga, gb), (int32_t)edge.size());

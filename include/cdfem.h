@@ -366,9 +366,11 @@ int cdfem_kuhn_mesh(int dim, int n, int order, double perturb, double *elem_vert
 
 /* gmsh v2.2 ASCII simplex meshes (the reference's inputs, e.g. Mesh/unit_square.msh); replaces
  * Mesh(mesh_file, 1, 1) + H1_FECollection(order, dim) + ParFiniteElementSpace
- * (linear_convection_diffusion_2D.cpp:290,311-313).  Triangles (order 1-3) or tetrahedra (1-2),
- * re-oriented to det J > 0; dofs: vertices (increasing gmsh node id), then (order-1) per edge along
- * increasing vertex dof, then P3 triangle centroids.  dof_bdr_mask[i] has bit (a-1) set when dof i
+ * (linear_convection_diffusion_2D.cpp:290,311-313).  Triangles (order 1-3) in MFEM's vertex order
+ * (Finalize: orientation fix, then the longest edge first, Triangle::MarkEdge) or tetrahedra (1-2,
+ * re-oriented to det J > 0); dofs: vertices (increasing gmsh node id), then (order-1) per edge (edges
+ * numbered as MFEM first meets them) along increasing vertex dof, then P3 triangle centroids.
+ * Boundary physical tags must be 1..31 (a larger tag is an error).  dof_bdr_mask[i] has bit (a-1) set when dof i
  * lies on a boundary element of physical attribute a (GetEssentialTrueDofs with an ess_bdr marker).
  * Host only; the element arrays feed cdfem_mesh_upload_simplex.                               */
 int cdfem_gmsh_sizes(const char *path, int order, int *dim, int *ne, int64_t *nldofs);

@@ -535,6 +535,21 @@ ORC_API void orc_csr_export(const orc_csr *A, int64_t *rp, int32_t *col, double 
     memcpy(val, A->val, sizeof(double) * A->nnz);
 }
 
+/* a CSR from arrays (columns sorted within each row), for matrices the tests build themselves */
+ORC_API orc_csr *orc_csr_import(int64_t n, const int64_t *rp, const int32_t *col, const double *val)
+{
+    orc_csr *A = (orc_csr *)calloc(1, sizeof(orc_csr));
+    A->n = n;
+    A->nnz = rp[n];
+    A->rp = (int64_t *)malloc(sizeof(int64_t) * (n + 1));
+    A->col = (int32_t *)malloc(sizeof(int32_t) * (A->nnz ? A->nnz : 1));
+    A->val = (double *)malloc(sizeof(double) * (A->nnz ? A->nnz : 1));
+    memcpy(A->rp, rp, sizeof(int64_t) * (n + 1));
+    memcpy(A->col, col, sizeof(int32_t) * A->nnz);
+    memcpy(A->val, val, sizeof(double) * A->nnz);
+    return A;
+}
+
 ORC_API void orc_csr_spmv(const orc_csr *A, const double *x, double *y)
 {
     #pragma omp parallel for schedule(static)

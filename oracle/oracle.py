@@ -58,6 +58,8 @@ def lib():
         L.orc_csr_nnz.restype = C.c_int64
         L.orc_csr_export.argtypes = [C.c_void_p, lp, C.POINTER(C.c_int32), dp]
         L.orc_csr_spmv.argtypes = [C.c_void_p, dp, dp]
+        L.orc_csr_import.restype = C.c_void_p
+        L.orc_csr_import.argtypes = [C.c_int64, lp, C.POINTER(C.c_int32), dp]
         L.orc_form_linear_system.restype = C.c_void_p
         L.orc_form_linear_system.argtypes = [C.c_void_p, ip, dp, dp, dp]
         L.orc_csr_diag.argtypes = [C.c_void_p, dp]
@@ -200,16 +202,20 @@ def dof_coords_simplex(mesh):
     return xyz
 
 
-def solve_mms_simplex(mesh, prm, kappa, s, c, alpha=1.0, tol=1e-10, atol=1e-12, max_it=500, pc="jacobi"):
+def solve_mms_simplex(mesh, prm, kappa, s, c, alpha=1.0, tol=1e-10, atol=1e-12, max_it=500, pc="jacobi",
+                      blocks=None):
     """C4 driver sequence on the oracle: FA CSR, FormLinearSystem, GMRES(30) + Jacobi (Input/petsc.opts)
-    or + ILU(0) (pc="ilu": Input/petsc_circle.opts), L2 error."""
+    or + ILU(0) (pc="ilu": Input/petsc_circle.opts on one rank; with blocks, the per-rank owned dof
+    lists: block-Jacobi ILU(0), the same options under mpirun -np N), L2 error."""
     A = fa_assemble_simplex(mesh, kappa=kappa, alpha=alpha, s=s, c=c)
     b = lf_assemble_simplex(mesh, prm)
     u = np.zeros(mesh.nl)
     xyz = dof_coords_simplex(mesh)
     u[mesh.ess] = mms_u(prm, xyz[mesh.ess])
     Ac, B = form_linear_system(A, mesh.bdr, u, b)
-    if pc == "ilu":
+    if pc == "ilu" and blocks is not None:
+        X, info = gmres_bjacobi_ilu(Ac, B, blocks, rtol=tol, atol=atol, max_it=max_it)
+    elif pc == "ilu":
         X, info = gmres_ilu(Ac, B, ilu0(Ac), rtol=tol, atol=atol, max_it=max_it)
     else:
         X, info = gmres(Ac, B, dinv=1.0 / Ac.diag(), rtol=tol, atol=atol, max_it=max_it)
@@ -349,6 +355,38 @@ def gmres(A: CSR, b, dinv=None, restart=30, rtol=1e-10, atol=1e-12, max_it=500):
     di = None if dinv is None else _d(np.ascontiguousarray(dinv, dtype=np.float64))
     conv = lib().orc_gmres(A.h, di, _d(b), _d(x), restart, rtol, atol, max_it, C.byref(it), C.byref(fn))
     return x, dict(converged=bool(conv), iterations=it.value, final_norm=fn.value)
+
+
+def csr_from_scipy(S) -> CSR:
+    """An oracle CSR of a scipy matrix (columns sorted per row; explicit zeros kept)."""
+    S = S.tocsr()
+    S.sort_indices()
+    rp = np.ascontiguousarray(S.indptr, dtype=np.int64)
+    col = np.ascontiguousarray(S.indices, dtype=np.int32)
+    val = np.ascontiguousarray(S.data, dtype=np.float64)
+    return CSR(lib().orc_csr_import(len(rp) - 1, rp.ctypes.data_as(C.POINTER(C.c_int64)),
+                                    col.ctypes.data_as(C.POINTER(C.c_int32)), _d(val)))
+
+
+def gmres_bjacobi_ilu(Ac: CSR, b, blocks, restart=30, rtol=1e-10, atol=1e-12, max_it=500):
+    """PETSc KSPGMRES + PCBJACOBI with one ILU(0) block per rank (Input/petsc_circle.opts:6-8 under
+    mpirun -np N).  blocks: per rank, the global dofs it owns in its local (natural) order.  The
+    system is renumbered rank by rank (PETSc's global order: rank-contiguous rows), the
+    preconditioner is ILU(0) of the block-diagonal part (entries coupling two ranks dropped: ILU(0)
+    of a block-diagonal matrix is the per-block ILU(0)), GMRES runs on the renumbered system and the
+    solution is numbered back."""
+    import scipy.sparse as sp
+    perm = np.concatenate([np.asarray(bl, dtype=np.int64) for bl in blocks])
+    assert len(perm) == Ac.n and len(np.unique(perm)) == Ac.n
+    S = Ac.to_scipy()[perm][:, perm].tocoo()
+    owner = np.repeat(np.arange(len(blocks)), [len(bl) for bl in blocks])
+    keep = owner[S.row] == owner[S.col]
+    Ap = csr_from_scipy(S.tocsr())
+    Bd = csr_from_scipy(sp.csr_matrix((S.data[keep], (S.row[keep], S.col[keep])), shape=S.shape))
+    xp, info = gmres_ilu(Ap, np.asarray(b)[perm], ilu0(Bd), restart=restart, rtol=rtol, atol=atol, max_it=max_it)
+    x = np.zeros(Ac.n)
+    x[perm] = xp
+    return x, info
 
 
 def ilu0(A: CSR) -> CSR:

@@ -8,7 +8,8 @@ A gloo world-3 restatement runs the shared-dof sum in ascending rank order insid
 
 GPU (marked gpu): 2 and 3 processes on one device (host communicator over gloo), each holding its
 rank-local piece, against one context on the whole mesh: constrained Mult, fixed GMRES iterates,
-converged GMRES / CG, bitwise-equal shared copies, P X (prolongation) of the true dofs.
+converged GMRES / CG, bitwise-equal shared copies, P X (prolongation) of the true dofs; and PETSc's
+block-Jacobi ILU(0) (one block per rank) against the oracle's restatement on the reference circle.
 """
 import os
 import socket
@@ -349,3 +350,86 @@ def test_gpu_partition_state_errors(gpu_ctx):
         ctx.set_shared(bad)
     ctx.upload_mesh(m)   # leave the shared fixture context single-rank again
     ctx._chk(ctx.L.cdfem_comm_init_host(ctx.h, 0, 1, cbs[0], cbs[1], None))
+
+
+# ---- block-Jacobi ILU(0) on several ranks (Input/petsc_circle.opts:6-8 under mpirun -np N) ---------
+CIRCLE = dict(kappa=1.0, alpha=1.0, conv=(1.0, 1.0), mass=1.0)   # Input/input_2d_circle.yaml:7-10
+
+
+def _bj_mesh(path):
+    import cdfem
+    return cdfem.gmsh_mesh(path, 3)
+
+
+def _bj_worker(rank, world, port, path, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    import cdfem
+    dist = _init(rank, world, port)
+    ctx = cdfem.Context(0)
+    m = _bj_mesh(path)
+    part = cdfem.partition_rcb(m, world)
+    ls = cdfem.local_space(m, part, rank)
+    ctx.upload_mesh(ls.mesh)
+    ctx.comm_init_torch()
+    ctx.set_shared(ls)
+    ctx.fa_setup(kinds=7, **CIRCLE)
+    nl = ls.mesh.nl
+    owned = np.arange(nl) >= ls.n_not_owned
+    bg = np.random.default_rng(21).uniform(-1, 1, m.nl)
+    b = np.where(owned, bg[ls.l2g], 0.0)
+    _, B = ctx.form_linear_system(np.zeros(nl), b)
+    xf, _ = ctx.solve(B, method="gmres", pc="ilu", rel_tol=0.0, abs_tol=0.0, max_iter=25, restart=10)
+    xc, info = ctx.solve(B, method="gmres", pc="ilu", rel_tol=1e-10, abs_tol=1e-12, max_iter=2000, restart=30)
+    xc2, _ = ctx.solve(B, method="gmres", pc="ilu", rel_tol=1e-10, abs_tol=1e-12, max_iter=2000, restart=30)
+    np.savez(os.path.join(out_dir, f"bj_{rank}.npz"), l2g=ls.l2g, nno=np.array([ls.n_not_owned]), xf=xf, xc=xc,
+             xc2=xc2, its=np.array([info["iterations"], info["converged"]]))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_block_jacobi_ilu(tmp_path, world):
+    """PETSc bjacobi + ILU(0) per rank on the reference's Mesh/unit_circle.msh (P3, the circle
+    configuration's operator): 2 / 3 processes with the general partition against the oracle's
+    restatement (ILU(0) of the block-diagonal part in the ranks' owned order): 25 fixed GMRES(10)
+    iterates to 1e-11, the converged GMRES(30) solve (rtol 1e-10) to 1e-8 with iterations +-1,
+    shared copies bitwise equal, repeated solves bitwise equal."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import reference_meshes as R
+    from oracle import oracle as O
+    path = R.write_msh("circle", str(tmp_path / "unit_circle.msh"))
+    mp.start_processes(_bj_worker, args=(world, _free_port(), path, str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    m = _bj_mesh(path)
+
+    class OM:
+        pass
+    om = OM()
+    om.dim, om.p, om.ne, om.nl, om.verts, om.dofmap = 2, 3, m.ne, m.nl, m.verts, m.dofmap
+    A = O.fa_assemble_simplex(om, kappa=1.0, alpha=1.0, s=1.0, c=(1.0, 1.0))
+    bdr = np.zeros(m.nl, dtype=np.int32)
+    bdr[m.ess] = 1
+    bg = np.random.default_rng(21).uniform(-1, 1, m.nl)
+    Ac, Bo = O.form_linear_system(A, bdr, np.zeros(m.nl), bg)
+    ds = [np.load(tmp_path / f"bj_{r}.npz") for r in range(world)]
+    blocks = [d["l2g"][int(d["nno"][0]):] for d in ds]
+    xf_o, _ = O.gmres_bjacobi_ilu(Ac, Bo, blocks, restart=10, rtol=0.0, atol=0.0, max_it=25)
+    xc_o, io = O.gmres_bjacobi_ilu(Ac, Bo, blocks, restart=30, rtol=1e-10, atol=1e-12, max_it=2000)
+    # one block (one rank's plain ILU) gives other iterates: the split really changes the preconditioner
+    xf_1, i1 = O.gmres_ilu(Ac, Bo, O.ilu0(Ac), restart=10, rtol=0.0, atol=0.0, max_it=25)
+    assert np.linalg.norm(xf_1 - xf_o) > 1e-6 * np.linalg.norm(xf_o)
+    gather = {k: np.full(m.nl, np.nan) for k in ("xf", "xc")}
+    for d in ds:
+        l2g = d["l2g"]
+        for k in gather:
+            seen = ~np.isnan(gather[k][l2g])
+            np.testing.assert_array_equal(gather[k][l2g][seen], d[k][seen], err_msg=k)
+            gather[k][l2g] = d[k]
+        np.testing.assert_array_equal(d["xc"], d["xc2"])
+        assert d["its"][1] and abs(int(d["its"][0]) - io["iterations"]) <= 1, (d["its"], io)
+    assert np.linalg.norm(gather["xf"] - xf_o) <= 1e-11 * np.linalg.norm(xf_o)
+    assert np.linalg.norm(gather["xc"] - xc_o) <= 1e-8 * np.linalg.norm(xc_o)
