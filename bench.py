@@ -132,12 +132,40 @@ def host_cores(args):
                                          "omp_num_threads": omp, "cpu_model": model}
 
 
+CPU_SAMPLES = 5  # median of >= 5 timed samples after one warm-up
+
+
+def cpu_samples(run, dofs, seconds, max_it, min_it=10, calib_it=5):
+    """Time an oracle solver leg: calibrate on calib_it iterations, one untimed warm-up sample, then
+    CPU_SAMPLES timed samples of about seconds / CPU_SAMPLES each.  run(k) runs k iterations and
+    returns the iterations done.  Returns the median DoF-iter/s and the sample record."""
+    t0 = time.perf_counter()
+    run(calib_it)
+    per_it = (time.perf_counter() - t0) / calib_it
+    k = int(min(max_it, max(min_it, seconds / CPU_SAMPLES / per_it)))
+    run(k)  # warm-up sample
+    rates, total_t, total_it = [], 0.0, 0
+    for _ in range(CPU_SAMPLES):
+        t0 = time.perf_counter()
+        its = run(k)
+        dt = time.perf_counter() - t0
+        rates.append(dofs * its / dt)
+        total_t += dt
+        total_it += its
+    med = float(np.median(rates))
+    rec = {"samples": [round(r, 1) for r in rates], "median": med, "min": float(min(rates)),
+           "max": float(max(rates)), "spread": round((max(rates) - min(rates)) / med, 4),
+           "iterations_per_sample": k}
+    return med, rec, total_it, total_t
+
+
 def cpu_baseline(args, n, p, kinds):
     """Oracle (C restatement of the reference's CPU FA path) timed on this host's cores: Jacobi-CG
     (like-for-like with the GPU metric) and, on the same assembled matrix, GMRES(30)+Jacobi (the
-    reference's solver, Input/petsc.opts:2-6).  For p >= 3 the FA matrix of the full mesh is out of
-    reach of the CPU (729-wide rows at p = 4), so the sample is a 12^3 mesh of the same order
-    (throughput per DoF-iteration is the reported unit)."""
+    reference's solver, Input/petsc.opts:2-6).  Each leg: median of CPU_SAMPLES samples after a
+    warm-up (cpu_samples).  For p >= 3 the FA matrix of the full mesh is out of reach of the CPU
+    (729-wide rows at p = 4), so the sample is a 12^3 mesh of the same order (throughput per
+    DoF-iteration is the reported unit)."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     threads, host = host_cores(args)
@@ -154,34 +182,29 @@ def cpu_baseline(args, n, p, kinds):
     del A
     dinv = 1.0 / Ac.diag()
     t_asm = time.perf_counter() - t0
-    # calibrate on 10 iterations, then time a sample of about --cpu-seconds
-    t0 = time.perf_counter()
-    O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=10)
-    per_it = (time.perf_counter() - t0) / 10
-    n_it = int(min(20000, max(10, args.cpu_seconds / per_it)))
-    t0 = time.perf_counter()
-    _, info = O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=n_it)
-    dt = time.perf_counter() - t0
-    its = info["iterations"]
-    # the reference's solver on the same matrix: GMRES(30) + Jacobi, fixed inner steps
-    t0 = time.perf_counter()
-    O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=5)
-    g_per = (time.perf_counter() - t0) / 5
-    g_it = int(min(3000, max(10, 0.5 * args.cpu_seconds / g_per)))
-    t0 = time.perf_counter()
-    _, ginfo = O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=g_it)
-    gdt = time.perf_counter() - t0
-    gits = ginfo["iterations"]
-    return {"value": m.nl * its / dt, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
-            "sample": f"oracle FA-CSR Jacobi-CG, {n}^3 hex p={p} ({m.nl} DoFs, nnz={Ac.nnz}), "
-                      f"{its} iterations timed ({dt:.2f} s); assembly+FormLinearSystem {t_asm:.1f} s untimed",
-            "gmres": {"value": m.nl * gits / gdt, "unit": "DoF-iter/s",
-                      "sample": f"oracle FA-CSR GMRES(30)+Jacobi on the same matrix, {gits} inner steps ({gdt:.2f} s)"},
+
+    def cg(k):
+        return O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=k)[1]["iterations"]
+
+    def gmres(k):  # the reference's solver on the same matrix: GMRES(30) + Jacobi, fixed inner steps
+        return O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=k)[1]["iterations"]
+    v, rec, its, dt = cpu_samples(cg, m.nl, args.cpu_seconds, 20000, calib_it=10)
+    gv, grec, gits, gdt = cpu_samples(gmres, m.nl, 0.5 * args.cpu_seconds, 3000)
+    return {"value": v, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
+            "sample": f"oracle FA-CSR Jacobi-CG, {n}^3 hex p={p} ({m.nl} DoFs, nnz={Ac.nnz}): median of "
+                      f"{CPU_SAMPLES} samples of {rec['iterations_per_sample']} iterations after a warm-up "
+                      f"({its} iterations, {dt:.2f} s timed); assembly+FormLinearSystem {t_asm:.1f} s untimed",
+            **rec,
+            "gmres": {"value": gv, "unit": "DoF-iter/s",
+                      "sample": f"oracle FA-CSR GMRES(30)+Jacobi on the same matrix: median of {CPU_SAMPLES} "
+                                f"samples of {grec['iterations_per_sample']} inner steps ({gits} steps, "
+                                f"{gdt:.2f} s timed)", **grec},
             **host}
 
 
 def cpu_baseline_c4(args, n, p):
-    """Oracle FA-CSR GMRES(30)/Jacobi on the same Kuhn mesh (bounded sample)."""
+    """Oracle FA-CSR GMRES(30)/Jacobi on the same Kuhn mesh (bounded sample, median of
+    CPU_SAMPLES samples after a warm-up)."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     threads, host = host_cores(args)
@@ -194,18 +217,15 @@ def cpu_baseline_c4(args, n, p):
     del A
     dinv = 1.0 / Ac.diag()
     t_asm = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=5)
-    per_it = (time.perf_counter() - t0) / 5
-    n_it = int(min(3000, max(10, args.cpu_seconds / per_it)))
-    t0 = time.perf_counter()
-    _, info = O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=n_it)
-    dt = time.perf_counter() - t0
-    its = info["iterations"]
-    return {"value": m.nl * its / dt, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
-            "sample": f"oracle FA-CSR GMRES(30)/Jacobi, Kuhn {n}^3x6 tets P{p} ({m.nl} DoFs, nnz={Ac.nnz}), "
-                      f"{its} iterations timed ({dt:.2f} s); assembly+FormLinearSystem {t_asm:.1f} s untimed",
-            **host}
+
+    def gmres(k):
+        return O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=k)[1]["iterations"]
+    v, rec, its, dt = cpu_samples(gmres, m.nl, args.cpu_seconds, 3000)
+    return {"value": v, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
+            "sample": f"oracle FA-CSR GMRES(30)/Jacobi, Kuhn {n}^3x6 tets P{p} ({m.nl} DoFs, nnz={Ac.nnz}): median "
+                      f"of {CPU_SAMPLES} samples of {rec['iterations_per_sample']} iterations after a warm-up "
+                      f"({its} iterations, {dt:.2f} s timed); assembly+FormLinearSystem {t_asm:.1f} s untimed",
+            **rec, **host}
 
 
 def main_c4(args):

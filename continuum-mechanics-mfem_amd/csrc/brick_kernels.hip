@@ -60,12 +60,11 @@ template <int S>
 constexpr int face_count() { return 2 * S * S + (S - 2) * (4 * S - 4); }
 
 // MODE 0: y = A x;  MODE 1: y = A_c x (ConstrainedOperator);  MODE 2: CG-fused (x := r)
-// W: minimum waves per SIMD requested from the register allocator (1: unconstrained, 2: <= 256
-// VGPR+AGPR so two bricks share a SIMD, at 124 B/lane of spills; selected at run time,
-// CDFEM_BRICK_WAVES / set_option "brick_waves", default 1: 241.5 vs 272.2 us per C2 apply in the
-// GMRES leg, tools/ab_gmres.py, profiles/r02_ab_c2_gmres_brick_waves.txt)
-template <int D1, int Q1, unsigned K, int MODE, int W>
-__global__ void __launch_bounds__(64, W)
+// One wave per SIMD, unconstrained registers: 241.5 vs 272.2 us per C2 apply in the GMRES leg
+// against a two-waves-per-SIMD build (<= 256 registers, 124 B/lane of spills; tools/ab_gmres.py,
+// profiles/r02_ab_c2_gmres_brick_waves.txt).
+template <int D1, int Q1, unsigned K, int MODE>
+__global__ void __launch_bounds__(64, 1)
 k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double *__restrict__ d,
           double *__restrict__ y, double *__restrict__ face, const double *__restrict__ qd,
           const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g,
@@ -273,12 +272,8 @@ static hipError_t brick_launch(cdfem_ctx *c, const double *x, const double *dinv
     const BrickGeom g = geom_of(c);
     if (which & 1) {
         const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
-        if (c->brick_waves == 1)
-            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 1>), dim3(c->nblk), dim3(64), 0, c->stream, x,
-                               dinv, d, y, c->d_face, c->d_qd, c->d_ess, T, g, c->d_part, c->d_state);
-        else
-            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 2>), dim3(c->nblk), dim3(64), 0, c->stream, x,
-                               dinv, d, y, c->d_face, c->d_qd, c->d_ess, T, g, c->d_part, c->d_state);
+        hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv, d, y,
+                           c->d_face, c->d_qd, c->d_ess, T, g, c->d_part, c->d_state);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -305,8 +300,6 @@ static hipError_t brick_kinds(cdfem_ctx *c, const double *x, const double *dinv,
     case 5: return brick_launch<D1, Q1, 5, MODE>(c, x, dinv, d, y, which);
     case 6: return brick_launch<D1, Q1, 6, MODE>(c, x, dinv, d, y, which);
     case 7: return brick_launch<D1, Q1, 7, MODE>(c, x, dinv, d, y, which);
-    case 5 | kMassFromD: return brick_launch<D1, Q1, 5 | kMassFromD, MODE>(c, x, dinv, d, y, which);
-    case 7 | kMassFromD: return brick_launch<D1, Q1, 7 | kMassFromD, MODE>(c, x, dinv, d, y, which);
     default: return hipErrorInvalidValue;
     }
 }
@@ -348,16 +341,13 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // below, which owns it for the dot products (remote_lo / remote_hi carry the neighbours' partial
 // sums of the interface planes; nullptr on a single GPU).
 // ================================================================================================
-// VAR % 3 = element core: 0 elem_apply3d fully unrolled; 1 elem_apply3d, plane loop; 2 low-register
-// core.  VAR 3..5: the same cores compiled for 2 waves per SIMD (<= 256 registers).  6: temporal
-// qdata loads.  7: unrolled core with the first qdata points issued under the patch gather.
-template <int D1, int Q1, unsigned K, int VAR>
-__global__ void __launch_bounds__(64, (VAR >= 3 && VAR <= 5) ? 2 : 1)
+template <int D1, int Q1, unsigned K>
+__global__ void __launch_bounds__(64, 1)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
            const Tab<D1, Q1> T, const BrickGeom g, int zlo_shared, double *__restrict__ part,
-           const KrylovState *__restrict__ st, double *__restrict__ xs)
+           const KrylovState *__restrict__ st)
 {
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
@@ -369,10 +359,6 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     __shared__ double s_out[S3];
     if (st->done) return;
     const double beta = st->beta;
-    // x-fold: the previous iteration's x += alpha d_old, for the dofs this brick writes (d_old is
-    // already in registers for the new direction); pending unless this is the first apply
-    const bool fold = xs != nullptr && st->reserved[0] != 0;
-    const double alpha_prev = st->alpha;
     const int t = threadIdx.x;
     // launch-local brick -> global brick (a launch covers every g.bzs-th layer from g.bz0)
     const int bl = brick_id(g), nxy = g.nbx * g.nby;
@@ -388,7 +374,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     // Measured (tools/ab.py, in process): 241.1 vs 242.4 us per launch for the per-row form; the
     // other waves of the CU hide most of that latency.
     constexpr int NI = (S3 + 63) / 64;
-    double rv[NI], mv[NI], ov[NI], xv[NI];
+    double rv[NI], mv[NI], ov[NI];
     uint8_t ev[NI];
     int64_t gidv[NI];
 #pragma unroll
@@ -403,18 +389,6 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         mv[k] = dinv[gid];
         ov[k] = d_old[gid];
         ev[k] = ess[gid];
-        if (fold) xv[k] = __builtin_nontemporal_load(xs + gid);  // issued with the patch (one round trip)
-    }
-    // VAR 7: qdata of the element's first kPre quadrature points, issued after the patch loads (the
-    // patch consumption waits only for the loads before them) and before the LDS stage; 48 patch +
-    // 5 * kPre qdata loads stay within the 63 outstanding vector loads of a wave
-    constexpr int kPre = VAR == 7 ? 3 : 1;
-    double pre[kPre][NC];
-    if constexpr (VAR == 7) {
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int qq = 0; qq < kPre; ++qq) load_qp<NC, true>(q0 + (size_t)qq * NC * kLanes, t, pre[qq]);
-        __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
@@ -430,7 +404,6 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
             const bool writer = (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
             if (writer) {
                 d_new[gid] = dn;
-                if (fold) __builtin_nontemporal_store(xv[k] + alpha_prev * ov[k], xs + gid);
                 if (e && !(zlo_shared && gz == 0)) den += dn * dn;  // (A_c d)_i = d_i on ess dofs
             }
             v = e ? 0.0 : dn;
@@ -444,26 +417,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const int o0 = P * ez * S2 + P * ey * S + P * ex;
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
     double Y[D1][D1][D1];
-    if constexpr (VAR == 7) {
-        // the first kPre points' qdata was issued right behind the patch gather (pre), so the
-        // stream is already in flight while the patch is formed and staged
-        auto qs = [&](int qq, double (&qv)[NC]) {
-            if (qq < kPre) {
-#pragma unroll
-                for (int c = 0; c < NC; ++c) qv[c] = pre[qq < kPre ? qq : 0][c];
-            } else {
-                load_qp<NC, true>(q0 + (size_t)qq * NC * kLanes, t, qv);
-            }
-        };
-        elem_apply3d_qs<D1, Q1, K, decltype(xl), Q1>(xl, qs, T, Y);
-    } else if constexpr (VAR == 6)
-        elem_apply3d<D1, Q1, K, decltype(xl), Q1, false>(xl, q0, t, T, Y);  // temporal qdata loads (A/B)
-    else if constexpr (VAR % 3 == 2)
-        elem_apply3d_lr<D1, Q1, K, decltype(xl), 1>(xl, q0, t, T, Y);
-    else if constexpr (VAR % 3 == 1)
-        elem_apply3d<D1, Q1, K, decltype(xl), 1>(xl, q0, t, T, Y);
-    else
-        elem_apply3d<D1, Q1, K, decltype(xl), Q1>(xl, q0, t, T, Y);
+    elem_apply3d<D1, Q1, K, decltype(xl), Q1>(xl, q0, t, T, Y);
 
     // element-wise den contribution d0_e . (A_e d0_e) and deterministic in-LDS E->L
 #pragma unroll
@@ -496,260 +450,19 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     if (t == 0) part[b] = den;
 }
 
-// ------------------------------------------------------------------------------------------------
-// k_brick_cg4 (brick_variant 8, p = 2): the same brick CG step with FOUR waves per brick and one
-// quadrature plane per lane.  Wave w takes the brick's element layer ez = w (16 elements); lane
-// (el, qz) = (lane & 15, lane >> 4) contracts its element's patch in z for plane qz only, runs the
-// 16 points of that plane (qdata point (qx, qy, qz) of element e is one lane of the brick block's
-// 16-byte loads, so a wave load reads four 256-byte runs) and the transposed x / y contractions,
-// and forms the plane's share of Y; the four planes are summed by an xor butterfly (lanes 16 and 32
-// apart), which leaves the same full Y on all four lanes of the element.  E->L: the 27 local dofs
-// fall into the 8 parity classes of (dx, dy, dz) mod 2; two element-local dofs of different classes
-// never land on the same patch position for any two elements (positions differ by 2 x the element
-// offset), so the four lanes of an element add four different classes at once: 8 barrier rounds
-// instead of 27.  ~1/4 of the per-lane registers of k_brick_cg, four times the waves.
-// Per element and dof the additions of the plane contributions run in a different order than in
-// k_brick_cg (rounding differences only).
-template <int D1, int Q1, unsigned K, int WPS>
-__global__ void __launch_bounds__(256, WPS)
-k_brick_cg4(const double *__restrict__ r, const double *__restrict__ dinv, const double *__restrict__ d_old,
-            double *__restrict__ d_new, double *__restrict__ q, double *__restrict__ face,
-            const double *__restrict__ qd, const uint8_t *__restrict__ ess, const Tab<D1, Q1> T,
-            const BrickGeom g, int zlo_shared, double *__restrict__ part, const KrylovState *__restrict__ st)
-{
-    static_assert(D1 == 3 && Q1 == 4, "one quadrature plane per lane quarter: p = 2");
-    using L = QLayout<K, 3>;
-    static_assert(!L::kMD, "derived mass weight not supported here");
-    constexpr int P = D1 - 1;
-    constexpr int S = kBrick * P + 1;
-    constexpr int S2 = S * S, S3 = S * S * S;
-    constexpr int F = face_count<S>();
-    constexpr int NC = L::nc;
-    constexpr int NQ = Q1 * Q1 * Q1;
-    __shared__ double s_in[S3];
-    __shared__ double s_out[S3];
-    __shared__ double s_red[4];
-    if (st->done) return;
-    const double beta = st->beta;
-    const int t = threadIdx.x;
-    const int bl = brick_id(g), nxy = g.nbx * g.nby;
-    const int bz = g.bz0 + (bl / nxy) * g.bzs;
-    const int b = bl % nxy + nxy * bz;
-    const int bx = b % g.nbx, by = (b / g.nbx) % g.nby;
-    const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
-    const bool lastx = bx == g.nbx - 1, lasty = by == g.nby - 1, lastz = bz == g.nbz - 1;
-    const double *q0 = qd + (size_t)b * NQ * NC * kLanes;
-    double den = 0.0;
-    // patch gather, 256 threads: every load issued before any is consumed
-    constexpr int NI = (S3 + 255) / 256;
-    double rv[NI], mv[NI], ov[NI];
-    uint8_t ev[NI];
-    int64_t gidv[NI];
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int i = t + 256 * k;
-        const int px = i % S, py = (i / S) % S, pz = i / S2;
-        const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-        const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
-        const int64_t gid = in ? gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz) : 0;
-        gidv[k] = in ? gid : -1;
-        rv[k] = r[gid];
-        mv[k] = dinv[gid];
-        ov[k] = d_old[gid];
-        ev[k] = ess[gid];
-    }
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int i = t + 256 * k;
-        if (i >= S3) break;
-        const int px = i % S, py = (i / S) % S, pz = i / S2;
-        const int gz = gz0 + pz;
-        double v = 0.0;
-        if (gidv[k] >= 0) {
-            const int64_t gid = gidv[k];
-            const double dn = mv[k] * rv[k] + beta * ov[k];
-            const bool e = ev[k] != 0;
-            const bool writer = (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
-            if (writer) {
-                d_new[gid] = dn;
-                if (e && !(zlo_shared && gz == 0)) den += dn * dn;  // (A_c d)_i = d_i on ess dofs
-            }
-            v = e ? 0.0 : dn;
-        }
-        s_in[i] = v;
-        s_out[i] = 0.0;
-    }
-    __syncthreads();
-
-    const int lane = t & 63, qz = lane >> 4;
-    const int e = (t >> 6) * 16 + (lane & 15);  // element of the brick (lane index of its qdata block)
-    const int ex = e & 3, ey = (e >> 2) & 3, ez = e >> 4;
-    const int o0 = P * ez * S2 + P * ey * S + P * ex;
-    // this lane's plane of the z tables (T is uniform; qz selects per lane)
-    double bzt[D1], gzt[D1];
-#pragma unroll
-    for (int dz = 0; dz < D1; ++dz) {
-        bzt[dz] = qz == 0 ? T.B[0][dz] : qz == 1 ? T.B[1][dz] : qz == 2 ? T.B[2][dz] : T.B[3][dz];
-        gzt[dz] = qz == 0 ? T.G[0][dz] : qz == 1 ? T.G[1][dz] : qz == 2 ? T.G[2][dz] : T.G[3][dz];
-    }
-    // contract z for plane qz
-    double T0[D1][D1], Tz[D1][D1];
-#pragma unroll
-    for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < D1; ++dx) {
-            double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-            for (int dz = 0; dz < D1; ++dz) {
-                const double xv = s_in[o0 + dz * S2 + dy * S + dx];
-                s0 += bzt[dz] * xv;
-                s1 += gzt[dz] * xv;
-            }
-            T0[dy][dx] = s0;
-            Tz[dy][dx] = s1;
-        }
-    double RT[D1][D1], RTz[D1][D1];
-#pragma unroll
-    for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < D1; ++dx) { RT[dy][dx] = 0.0; RTz[dy][dx] = 0.0; }
-    const double *qp0 = q0 + (size_t)(Q1 * Q1 * qz) * NC * kLanes;
-#pragma unroll
-    for (int qy = 0; qy < Q1; ++qy) {
-        double a[D1], ay[D1], az[D1];
-#pragma unroll
-        for (int dx = 0; dx < D1; ++dx) {
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-#pragma unroll
-            for (int dy = 0; dy < D1; ++dy) {
-                s0 += T.B[qy][dy] * T0[dy][dx];
-                s1 += T.G[qy][dy] * T0[dy][dx];
-                s2 += T.B[qy][dy] * Tz[dy][dx];
-            }
-            a[dx] = s0; ay[dx] = s1; az[dx] = s2;
-        }
-        double Rv[D1], Ry[D1], Rz[D1];
-#pragma unroll
-        for (int dx = 0; dx < D1; ++dx) { Rv[dx] = 0.0; Ry[dx] = 0.0; Rz[dx] = 0.0; }
-#pragma unroll
-        for (int qx = 0; qx < Q1; ++qx) {
-            double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) {
-                u += T.B[qx][dx] * a[dx];
-                ux += T.G[qx][dx] * a[dx];
-                uy += T.B[qx][dx] * ay[dx];
-                uz += T.B[qx][dx] * az[dx];
-            }
-            double qv[NC];
-            load_qp<NC, true>(qp0 + (size_t)(qx + Q1 * qy) * NC * kLanes, e, qv);
-            double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
-            if constexpr (L::kD) {
-                gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;
-                gy = qv[1] * ux + qv[3] * uy + qv[4] * uz;
-                gz = qv[2] * ux + qv[4] * uy + qv[5] * uz;
-            }
-            if constexpr (L::kC) vv = qv[L::oC] * ux + qv[L::oC + 1] * uy + qv[L::oC + 2] * uz;
-            if constexpr (L::kM) vv += qv[L::oM] * u;
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) {
-                if constexpr (L::kD) {
-                    Rv[dx] += T.B[qx][dx] * vv + T.G[qx][dx] * gx;
-                    Ry[dx] += T.B[qx][dx] * gy;
-                    Rz[dx] += T.B[qx][dx] * gz;
-                } else {
-                    Rv[dx] += T.B[qx][dx] * vv;
-                }
-            }
-        }
-#pragma unroll
-        for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) {
-                if constexpr (L::kD) {
-                    RT[dy][dx] += T.B[qy][dy] * Rv[dx] + T.G[qy][dy] * Ry[dx];
-                    RTz[dy][dx] += T.B[qy][dy] * Rz[dx];
-                } else {
-                    RT[dy][dx] += T.B[qy][dy] * Rv[dx];
-                }
-            }
-    }
-    // this plane's share of Y, then the sum over the four planes (xor butterfly: every lane of the
-    // element ends with the same value)
-    double Y[D1][D1][D1];
-#pragma unroll
-    for (int dz = 0; dz < D1; ++dz)
-#pragma unroll
-        for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) {
-                double y = L::kD ? bzt[dz] * RT[dy][dx] + gzt[dz] * RTz[dy][dx] : bzt[dz] * RT[dy][dx];
-                y += __shfl_xor(y, 16, 64);
-                y += __shfl_xor(y, 32, 64);
-                Y[dz][dy][dx] = y;
-            }
-    // E->L in 8 rounds: lane quarter qz adds the local dofs of its parity classes
-    //   qz 0: (e,e,e) 8 dofs; 1: (o,e,e) + (e,o,o) + (o,o,o) 7; 2: (e,o,e) + (o,e,o) 6; 3: (e,e,o) + (o,o,e) 6
-    // ((dx, dy, dz) mod 2, e = even, o = odd), in a fixed order per quarter
-    constexpr int kRounds = 8;
-    constexpr signed char kStep[4][kRounds][3] = {
-        {{0, 0, 0}, {2, 0, 0}, {0, 2, 0}, {2, 2, 0}, {0, 0, 2}, {2, 0, 2}, {0, 2, 2}, {2, 2, 2}},
-        {{1, 0, 0}, {1, 2, 0}, {1, 0, 2}, {1, 2, 2}, {0, 1, 1}, {2, 1, 1}, {1, 1, 1}, {-1, 0, 0}},
-        {{0, 1, 0}, {2, 1, 0}, {0, 1, 2}, {2, 1, 2}, {1, 0, 1}, {1, 2, 1}, {-1, 0, 0}, {-1, 0, 0}},
-        {{0, 0, 1}, {2, 0, 1}, {0, 2, 1}, {2, 2, 1}, {1, 1, 0}, {1, 1, 2}, {-1, 0, 0}, {-1, 0, 0}}};
-#pragma unroll
-    for (int k = 0; k < kRounds; ++k) {
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            if (qz == g4 && kStep[g4][k][0] >= 0) {
-                const int dx = kStep[g4][k][0], dy = kStep[g4][k][1], dz = kStep[g4][k][2];
-                const int o = o0 + dz * S2 + dy * S + dx;
-                const double y = Y[dz][dy][dx];
-                den += s_in[o] * y;
-                s_out[o] += y;
-            }
-        }
-        __syncthreads();
-    }
-
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int i = t + 256 * k;
-        if (i >= S3) break;
-        const int px = i % S, py = (i / S) % S, pz = i / S2;
-        const double v = s_out[i];
-        if (px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1) {
-            face[(size_t)b * F + face_index<S>(px, py, pz)] = v;
-            continue;
-        }
-        const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-        if (gx >= g.Lx || gy >= g.Ly || gz >= g.Lz) continue;
-        q[gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz)] = v;  // ess rows: replaced by d in the update
-    }
-    den = block_sum(den, s_red);
-    if (t == 0) part[b] = den;
-}
-
-template <int S, bool X2>
+template <int S>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ q,
                   const double *__restrict__ d, const double *__restrict__ dinv,
                   const double *__restrict__ face, const uint8_t *__restrict__ ess, const BrickGeom g,
                   const FastDiv fdx, const FastDiv fdxy, int zlo_shared,
                   const double *__restrict__ remote_lo, const double *__restrict__ remote_hi,
-                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step, int fold_x,
-                  const double *__restrict__ dprev)
+                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step)
 {
     constexpr int F = face_count<S>();
     constexpr int s1 = S - 1;
     __shared__ double sh[kRedThreads / 64];
     if (st->done) return;
-    // cg_x2 (dprev != nullptr): iteration i odd skips x (as the x-fold does), i even adds both
-    // pending terms, x + a_{i-1} d_{i-1} + a_i d_i, in the order the unpaired updates would
-    const bool x2_odd = X2 && (st->iter & 1) != 0;
-    const bool x2_even = X2 && !x2_odd;
-    const double alpha_prev = x2_even ? st->x2_alpha : 0.0;
-    fold_x = fold_x || x2_odd;
     double alpha;
     if (den_step) {
         // multi-rank: the MFEM den step on the all-reduced den, folded in (no one-thread kernel
@@ -774,11 +487,8 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         const int gx = rem - gy * g.Lx;
         // every load is issued before any is consumed: which of q / the face partials holds this
         // dof's row sum depends on its lattice position only, and the essential flag selects last
-        // x-fold: x += alpha d moves to the next apply (k_brick_cg) and d is needed on ess rows only
         const bool is_ess = ess[gid] != 0;
-        const double di = (!fold_x || is_ess) ? d[gid] : 0.0, xi = fold_x ? 0.0 : x[gid];
-        double dpi = 0.0;
-        if constexpr (X2) dpi = x2_even ? dprev[gid] : 0.0;
+        const double di = d[gid], xi = x[gid];
         const double rold = r[gid], mi = dinv[gid];
         double qi;
         if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
@@ -810,12 +520,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         if (remote_lo && gz == 0) qi += remote_lo[rem];
         if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
         if (is_ess) qi = di;
-        if (X2 && x2_even) {
-            const double x1 = xi + alpha_prev * dpi;
-            __builtin_nontemporal_store(x1 + alpha * di, &x[gid]);
-        } else if (!fold_x) {
-            __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
-        }
+        __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
         const double ri = rold - alpha * qi;
         __builtin_nontemporal_store(ri, &r[gid]);
         if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
@@ -841,49 +546,12 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     g.bzs = run.bzs;
     const dim3 grid((unsigned)(c->nbx * c->nby * run.nlay)), block(64);
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
-    if constexpr (D1 == 3 && Q1 == 4 && !QLayout<K, 3>::kMD) {
-        // four waves per brick (k_brick_cg4); variants 9 / 10 ask the register allocator for 3 / 4
-        // waves per SIMD (<= 168 / 128 VGPRs)
-        if (c->brick_variant >= 8 && c->brick_variant <= 10 && !c->xfold_x) {
-#define CDFEM_L4(WPS)                                                                                   \
-    do {                                                                                                \
-        if (whole)                                                                                      \
-            CDFEM_LAUNCH(c, (k_brick_cg4<D1, Q1, K, WPS>), grid, dim3(256), 0, r, dinv, d_old, d_new, q, \
-                         c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);    \
-        else                                                                                            \
-            hipLaunchKernelGGL((k_brick_cg4<D1, Q1, K, WPS>), grid, dim3(256), 0, run.s, r, dinv, d_old, \
-                               d_new, q, c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part,  \
-                               c->d_state);                                                            \
-    } while (0)
-            if (c->brick_variant == 9) CDFEM_L4(3);
-            else if (c->brick_variant == 10) CDFEM_L4(4);
-            else CDFEM_L4(1);
-#undef CDFEM_L4
-            return hipGetLastError();
-        }
-    }
-#define CDFEM_L(V)                                                                                  \
-    do {                                                                                            \
-        if (whole)                                                                                  \
-            CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, V>), grid, block, 0, r, dinv, d_old, d_new, q,   \
-                         c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state,   \
-                         c->xfold_x);                                                                \
-        else                                                                                        \
-            hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, V>), grid, block, 0, run.s, r, dinv, d_old,    \
-                               d_new, q, c->d_face, c->d_qd, c->d_ess, T, g, c->zlo_shared,          \
-                               c->d_part, c->d_state, c->xfold_x);                                  \
-    } while (0)
-    switch (c->brick_variant) {
-    case 1: CDFEM_L(1); break;
-    case 2: CDFEM_L(2); break;
-    case 3: CDFEM_L(3); break;
-    case 4: CDFEM_L(4); break;
-    case 5: CDFEM_L(5); break;
-    case 6: CDFEM_L(6); break;
-    case 7: CDFEM_L(7); break;
-    default: CDFEM_L(0); break;
-    }
-#undef CDFEM_L
+    if (whole)
+        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K>), grid, block, 0, r, dinv, d_old, d_new, q, c->d_face, c->d_qd,
+                     c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);
+    else
+        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K>), grid, block, 0, run.s, r, dinv, d_old, d_new, q, c->d_face,
+                           c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);
     return hipGetLastError();
 }
 
@@ -900,8 +568,6 @@ static hipError_t brick_cg2_run(cdfem_ctx *c, const double *r, const double *din
     case 5: return brick_cg2_launch<D1_, Q1_, 5>(c, r, dinv, d_old, d_new, q, run);                 \
     case 6: return brick_cg2_launch<D1_, Q1_, 6>(c, r, dinv, d_old, d_new, q, run);                 \
     case 7: return brick_cg2_launch<D1_, Q1_, 7>(c, r, dinv, d_old, d_new, q, run);                 \
-    case 5 | kMassFromD: return brick_cg2_launch<D1_, Q1_, 5 | kMassFromD>(c, r, dinv, d_old, d_new, q, run); \
-    case 7 | kMassFromD: return brick_cg2_launch<D1_, Q1_, 7 | kMassFromD>(c, r, dinv, d_old, d_new, q, run); \
     default: return hipErrorInvalidValue;                                                           \
     }
     if (c->p == 1 && q1 == 3) { CDFEM_K(2, 3) }
@@ -929,7 +595,7 @@ hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *d
 
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
                                   const double *dinv, const double *remote_lo, const double *remote_hi,
-                                  bool den_step, const double *dprev)
+                                  bool den_step)
 {
     const BrickGeom g = geom_of(c);
     const FastDiv fdx = make_fastdiv((uint32_t)c->Lx), fdxy = make_fastdiv((uint32_t)(c->Lx * c->Ly));
@@ -937,18 +603,14 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     // loads, so every dof's chain must be in flight at once
     const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
     const unsigned grid = (unsigned)(need < 16384 ? need : 16384);
-#define CDFEM_UPD(S_, X2_)                                                                                \
-    hipLaunchKernelGGL((k_cg_update_faces<S_, X2_>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, q, d,   \
-                       dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, c->d_part, \
-                       c->d_state, (int)den_step, (int)(c->xfold_x != nullptr), dprev)
-    if (c->p == 1 && dprev)
-        CDFEM_UPD(kBrick * 1 + 1, true);
-    else if (c->p == 1)
-        CDFEM_UPD(kBrick * 1 + 1, false);
-    else if (c->p == 2 && dprev)
-        CDFEM_UPD(kBrick * 2 + 1, true);
+#define CDFEM_UPD(S_)                                                                                       \
+    hipLaunchKernelGGL((k_cg_update_faces<S_>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, q, d, dinv, \
+                       c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, c->d_part,     \
+                       c->d_state, (int)den_step)
+    if (c->p == 1)
+        CDFEM_UPD(kBrick * 1 + 1);
     else if (c->p == 2)
-        CDFEM_UPD(kBrick * 2 + 1, false);
+        CDFEM_UPD(kBrick * 2 + 1);
     else
         return hipErrorInvalidValue;
 #undef CDFEM_UPD
@@ -958,44 +620,6 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     return launch_update_fin(c, (int)grid);
 }
 
-// x-fold flush after the CG loop: the last executed update's x += alpha_k d_k (k = iter - 1; d_k
-// sits in dA for even k, dB for odd k: the host alternates the two direction buffers)
-__global__ void __launch_bounds__(256)
-k_cg_xflush(double *__restrict__ x, const double *__restrict__ dA, const double *__restrict__ dB, int64_t n,
-            const KrylovState *__restrict__ st)
-{
-    if (st->reserved[0] == 0) return;
-    const double alpha = st->alpha;
-    const double *d = ((st->iter - 1) & 1) == 0 ? dA : dB;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        x[i] = x[i] + alpha * d[i];
-}
-
-// cg_x2 flush: an odd last update left its x += alpha d pending (d: its direction buffer)
-__global__ void __launch_bounds__(256)
-k_cg_x2flush(double *__restrict__ x, const double *__restrict__ d, int64_t n, const KrylovState *__restrict__ st)
-{
-    if (st->reserved[1] == 0) return;
-    const double alpha = st->x2_alpha;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        x[i] = x[i] + alpha * d[i];
-}
-
-hipError_t launch_cg_x2flush(cdfem_ctx *c, double *x, const double *d)
-{
-    const int64_t need = (c->nl + 255) / 256;
-    hipLaunchKernelGGL(k_cg_x2flush, dim3((unsigned)(need < 8192 ? need : 8192)), dim3(256), 0, c->stream, x, d,
-                       (int64_t)c->nl, c->d_state);
-    return hipGetLastError();
-}
-
-hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *dA, const double *dB)
-{
-    const int64_t need = (c->nl + 255) / 256;
-    hipLaunchKernelGGL(k_cg_xflush, dim3((unsigned)(need < 8192 ? need : 8192)), dim3(256), 0, c->stream, x, dA, dB,
-                       (int64_t)c->nl, c->d_state);
-    return hipGetLastError();
-}
 
 // local partial sums of q = A d on the shared interface planes (what the neighbour must add)
 template <int S>

@@ -95,17 +95,16 @@ void free_mesh(cdfem_ctx *c)
     for (auto &b : c->d_if) dfree(b);
     dfree(c->d_stab); dfree(c->d_stab_lf); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);
     dfree(c->d_cpos); dfree(c->d_vals); dfree(c->d_vals_c); dfree(c->d_Ee);
-    dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_sdel_base); dfree(c->d_svals);
+    dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_sdel); dfree(c->d_svals);
     c->d_sdel = nullptr;
     dfree(c->d_rperm); dfree(c->d_pv[0]); dfree(c->d_pv[1]); dfree(c->d_dinv_p);
     c->d_rperm = nullptr; c->d_pv[0] = c->d_pv[1] = nullptr; c->d_dinv_p = nullptr;
-    dfree(c->d_svals_c_base);
+    dfree(c->d_svals_c);
     c->d_svals_c = nullptr;
     ilu_free(c);
     partition_free(c);
     c->nslices = c->nstored = 0;
     c->sell_windowed = false;
-    c->sell_xcd_sorted = false;
     c->geom = 0;
     c->fa_ready = false;
     c->nnz = 0;
@@ -349,18 +348,6 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     const int check = p.check_every > 0 ? p.check_every : 16;
     const bool mr = multi_rank(c);
     double *red = c->d_state->red;  // device scalars awaiting the all-reduce
-    // x-fold: iteration k's x += alpha_k d_k is done by apply k + 1 (which already streams d_k) and
-    // the last one by k_cg_xflush; the update then streams 40 instead of 57 B/dof
-    struct FoldGuard {
-        cdfem_ctx *c;
-        ~FoldGuard() { c->xfold_x = nullptr; }
-    } fold_guard{c};
-    c->xfold_x = c->cg_xfold ? x : nullptr;
-    double *const d_even = dcur, *const d_odd = dprev;  // apply k writes direction k here
-    // cg_x2: x is updated by every second iteration with both pending terms (not with the x-fold);
-    // an odd last iteration's term is flushed after the loop (odd iterations' directions live in
-    // d_even = d_dalt, the buffer the first apply writes)
-    const bool x2 = c->cg_x2 && !c->cg_xfold;
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     if (mr) {
@@ -416,8 +403,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             prof_mark(c, CDFEM_K_UPDATE, true);
             HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv,
                                           mr && c->zlo_shared ? c->d_if[1] : nullptr,
-                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr,
-                                          x2 ? dprev : nullptr));
+                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr));
             if (mr) {
                 comm_allreduce(c, red + 1, 1);
                 HIPCHK(launch_update_step(c));
@@ -430,14 +416,6 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (c->h_state->done || launched >= p.max_iter) break;
-    }
-    if (c->xfold_x) {
-        HIPCHK(launch_cg_xflush(c, x, d_even, d_odd));
-        HIPCHK(hipStreamSynchronize(c->stream));
-    }
-    if (x2) {
-        HIPCHK(launch_cg_x2flush(c, x, d_even));
-        HIPCHK(hipStreamSynchronize(c->stream));
     }
     const auto t1 = std::chrono::steady_clock::now();
     prof_collect(c);
@@ -463,12 +441,6 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     // update (ho_kernels.hip k_apply3d_tile<DEN>, vec_kernels.hip k_e2l_box<UPD>)
     const bool fused = !mr && !c->fa_ready && c->cg_fused && tile_den_ok(c) && e2l_box_ok(c);
     if (fused && !c->d_tpart) c->d_tpart = dalloc<double>(tile_den_blocks(c));
-    // fused + dfold: the direction d = z + beta d_old is formed inside the next apply's gather and
-    // written by each dof's owner element into the other direction buffer (dcur <-> dnext)
-    const bool dfold = fused && c->cg_dfold;
-    if (dfold && !c->d_dalt) c->d_dalt = dalloc<double>(c->nl);
-    double *dnext = dfold ? c->d_dalt : nullptr;
-    bool first_apply = true;
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     if (mr) {
@@ -482,13 +454,7 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     auto apply = [&] {
         prof_mark(c, CDFEM_K_APPLY, true);
         if (fused) {  // Ye = A_c d and den; q stays an E-vector until the update
-            if (dfold && !first_apply) {
-                HIPCHK(launch_apply_den(c, z, c->d_Ye, c->d_state, c->d_tpart, d, dnext));
-                std::swap(d, dnext);  // the update and the next apply read the new direction
-            } else {
-                HIPCHK(launch_apply_den(c, d, c->d_Ye, c->d_state, c->d_tpart));
-            }
-            first_apply = false;
+            HIPCHK(launch_apply_den(c, d, c->d_Ye, c->d_state, c->d_tpart));
             prof_mark(c, CDFEM_K_APPLY, false);
             prof_mark(c, CDFEM_K_E2L, true);
             HIPCHK(launch_den_from_partials(c, c->d_tpart, tile_den_blocks(c)));
@@ -528,11 +494,9 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
                 HIPCHK(launch_update_step(c));
             }
             prof_mark(c, CDFEM_K_UPDATE, false);
-            if (!dfold) {
-                prof_mark(c, CDFEM_K_DIRECTION, true);
-                HIPCHK(launch_cg_direction(c, z, d));
-                prof_mark(c, CDFEM_K_DIRECTION, false);
-            }
+            prof_mark(c, CDFEM_K_DIRECTION, true);
+            HIPCHK(launch_cg_direction(c, z, d));
+            prof_mark(c, CDFEM_K_DIRECTION, false);
             apply();
         }
         HIPCHK(hipMemcpyAsync(c->h_state, c->d_state, sizeof(KrylovState), hipMemcpyDeviceToHost,
@@ -666,7 +630,6 @@ int cdfem_create(int device, cdfem_ctx **out)
     cdfem_ctx *c = new (std::nothrow) cdfem_ctx();
     if (!c) return CDFEM_ERR_HIP;
     c->device = device;
-    if (const char *w = std::getenv("CDFEM_BRICK_WAVES")) c->brick_waves = std::atoi(w) == 2 ? 2 : 1;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_state, sizeof(KrylovState)) != hipSuccess ||
@@ -1074,16 +1037,11 @@ static int pa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
         if (!apply_supported(c->dim, c->p))
             throw UnsupportedError("no PA apply kernel built for dim=" + std::to_string(c->dim) +
                                    " order=" + std::to_string(c->p));
-        // 3D, constant kappa != 0 and s, no matrix coefficient: the mass weight comes from the
-        // diffusion block (one qdata component less per point; QLayout::kMD in pa_core.hpp)
-        const bool from_d = c->mass_from_d && c->dim == 3 && (f->kinds & CDFEM_DIFFUSION) && (f->kinds & CDFEM_MASS) &&
-                            !f->kappa_q && !f->kappa_mat_q && !f->mass_q && f->kappa != 0.0 && std::isfinite(f->kappa);
-        const unsigned kinds = f->kinds | (from_d ? kMassFromD : 0u);
+        const unsigned kinds = f->kinds;
         dfree(c->d_qd);
         c->kinds = kinds;
-        c->rule_op.mscale = from_d ? f->mass / (f->kappa * f->kappa * f->kappa) : 0.0;
         c->ncomp = ((kinds & CDFEM_DIFFUSION) ? c->dim * (c->dim + 1) / 2 : 0) +
-                   ((kinds & CDFEM_CONVECTION) ? c->dim : 0) + ((kinds & CDFEM_MASS) && !from_d ? 1 : 0);
+                   ((kinds & CDFEM_CONVECTION) ? c->dim : 0) + ((kinds & CDFEM_MASS) ? 1 : 0);
         const int nq = nq_of(c, c->rule_op);
         c->d_qd = c->qlay == 1 ? dalloc<double>((size_t)c->ne * c->rule_op.q1 * qd_ho_plane(c->ncomp, c->rule_op.q1))
                                : dalloc<double>((size_t)c->nblk * nq * c->ncomp * kLanes);
@@ -1225,7 +1183,7 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             if (!multi_rank(c) && (c->sell_mode == 3 || c->sell_mode == 5) && !c->h_verts.empty())
                 xyz = simplex_dof_coords(c->dim, c->p, c->ne, c->nd, c->nl, c->h_verts, c->h_dofs);
             FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl,
-                                           multi_rank(c) ? 0 : (c->sell_mode | (c->spmv_xcd_sort ? 0x100 : 0)), c->dim,
+                                           multi_rank(c) ? 0 : c->sell_mode, c->dim,
                                            xyz.empty() ? nullptr : xyz.data());
             c->nnz = P.nnz;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
@@ -1250,24 +1208,19 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             c->d_scols = dalloc<int32_t>(P.scols.size());
             c->d_smap = dalloc<int32_t>(P.smap.size());
             c->d_svals = dalloc<double>(c->nstored);
-            // sell_offset: the solve's value stream starts sell_offset bytes into its allocation
-            // (placement A/B)
-            c->d_svals_c_base = dalloc<double>(c->nstored + c->sell_offset / 8);
-            c->d_svals_c = c->d_svals_c_base + c->sell_offset / 8;
+            c->d_svals_c = dalloc<double>(c->nstored);
             HIPCHK(hipMemcpyAsync(c->d_sptr, P.sptr.data(), P.sptr.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_srows, P.srows.data(), P.srows.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_scols, P.scols.data(), P.scols.size() * 4, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(c->d_smap, P.smap.data(), P.smap.size() * 4, hipMemcpyHostToDevice, c->stream));
             c->sell_windowed = P.windowed;
-            c->sell_xcd_sorted = P.xcd_sorted;
             if (!P.perm.empty()) {
                 c->d_rperm = dalloc<int32_t>(P.perm.size());
                 HIPCHK(hipMemcpyAsync(c->d_rperm, P.perm.data(), P.perm.size() * 4, hipMemcpyHostToDevice, c->stream));
                 for (auto &v : c->d_pv) v = dalloc<double>(c->nl);
             }
             if (!P.sdel.empty()) {
-                c->d_sdel_base = dalloc<int16_t>(P.sdel.size() + c->sell_offset / 2);
-                c->d_sdel = c->d_sdel_base + c->sell_offset / 2;
+                c->d_sdel = dalloc<int16_t>(P.sdel.size());
                 HIPCHK(hipMemcpyAsync(c->d_sdel, P.sdel.data(), P.sdel.size() * 2, hipMemcpyHostToDevice, c->stream));
             }
             HIPCHK(hipStreamSynchronize(c->stream));  // P's host buffers die at scope exit
@@ -1497,11 +1450,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
     return guarded(c, [&] {
         if (!key) throw ArgError("key is null");
         const std::string k(key);
-        if (k == "brick_variant") {
-            if (value < 0 || value > 10) throw ArgError("brick_variant must be 0..10");
-            c->brick_variant = value;
-
-        } else if (k == "brick_xcd") {
+        if (k == "brick_xcd") {
             if (value < 0 || value > 1) throw ArgError("brick_xcd must be 0 or 1");
             c->brick_xcd = value;
         } else if (k == "mr_overlap") {
@@ -1511,9 +1460,6 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value != 0 && value != 1 && value != 3 && value != 8 && value != 9 && value != 15)
                 throw ArgError("ho_mfma must be 0, 1, 3, 8, 9 or 15");
             c->ho_mfma = value;
-        } else if (k == "cg_dfold") {
-            if (value < 0 || value > 1) throw ArgError("cg_dfold must be 0 or 1");
-            c->cg_dfold = value;
         } else if (k == "cg_fused") {
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;
@@ -1521,28 +1467,6 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 5)
                 throw ArgError("sell_order must be 0..5 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric)");
             c->sell_mode = value;
-        } else if (k == "mass_from_d") {  // read at the next cdfem_pa_setup
-            if (value < 0 || value > 1) throw ArgError("mass_from_d must be 0 or 1");
-            c->mass_from_d = value;
-        } else if (k == "diag_sf") {
-            if (value < 0 || value > 1) throw ArgError("diag_sf must be 0 or 1");
-            c->diag_sf = value;
-            c->dinv_ready = false;
-        } else if (k == "cg_x2") {
-            if (value < 0 || value > 1) throw ArgError("cg_x2 must be 0 or 1");
-            c->cg_x2 = value;
-        } else if (k == "cg_xfold") {
-            if (value < 0 || value > 1) throw ArgError("cg_xfold must be 0 or 1");
-            c->cg_xfold = value;
-        } else if (k == "spmv_variant") {
-            if (value < 0 || value > 1) throw ArgError("spmv_variant must be 0 or 1");
-            c->spmv_variant = value;
-        } else if (k == "spmv_xcd_sort") {  // read when the FA pattern is built
-            if (value < 0 || value > 1) throw ArgError("spmv_xcd_sort must be 0 or 1");
-            c->spmv_xcd_sort = value;
-        } else if (k == "sell_offset") {  // read when the FA operator is set up
-            if (value < 0 || value > (4 << 20) || value % 256) throw ArgError("sell_offset must be a multiple of 256 in [0, 4 MiB]");
-            c->sell_offset = value;
         } else if (k == "spmv_xcd") {
             if (value < 0 || value > 1) throw ArgError("spmv_xcd must be 0 or 1");
             c->spmv_xcd = value;
@@ -1551,9 +1475,6 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             c->spmv_index16 = value;
         } else if (k == "profile_mask") {
             c->prof_mask = (unsigned)value;
-        } else if (k == "brick_waves") {
-            if (value != 1 && value != 2) throw ArgError("brick_waves must be 1 or 2");
-            c->brick_waves = value;
         } else {
             throw ArgError("unknown option " + k);
         }

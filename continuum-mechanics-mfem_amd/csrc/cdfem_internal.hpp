@@ -28,12 +28,8 @@ constexpr int kMaxD1 = 6;
 constexpr int kMaxQ1 = 8;
 
 // 1D tables for one quadrature rule: B[q][d] = phi_d(xi_q), G[q][d] = phi_d'(xi_q), points, weights
-// kinds bit (internal, 3D PA with constant kappa and s): the mass weight is not stored but derived
-// from the diffusion block, M = s det(D) / (W^2 kappa^3) (pa_core.hpp, QLayout::kMD)
-constexpr unsigned kMassFromD = 8u;
 struct Rule1D {
     int d1 = 0, q1 = 0;
-    double mscale = 0.0;                // s / kappa^3 when the mass weight is derived (kMassFromD)
     double B[kMaxQ1][kMaxD1] = {};
     double G[kMaxQ1][kMaxD1] = {};
     double pts[kMaxQ1] = {};
@@ -77,8 +73,6 @@ struct KrylovState {
     double nom, nom0, den, alpha, beta, betanom, r0;
     double red[4];  // rank-local reductions awaiting the all-reduce (0 den, 1 betanom, 2 nom)
     int iter, done, converged, final_iter, max_iter, first_den;
-    unsigned reserved[4];  // [0] x-fold pending; [1] paired-x (cg_x2) pending
-    double x2_alpha;       // cg_x2: alpha of the last update (its x += alpha d is pending if reserved[1])
 };
 
 // Device-side GMRES(m) state (gmres.hip).  The first 32 bytes are what the host polls.
@@ -159,9 +153,7 @@ struct cdfem_ctx {
     double *d_ones = nullptr;           // all-ones vector (unpreconditioned brick CG)
     double *d_dalt = nullptr;           // second search-direction buffer (brick CG)
     int nface = 0;                      // F
-    int brick_waves = 1;                // register budget of k_brick3d (CDFEM_BRICK_WAVES); 1: no spills, measured faster
     int brick_xcd = 1;                  // k_brick_cg brick order: 0 dispatch, 1 XCD-contiguous (default)
-    int brick_variant = 0;              // element core of k_brick_cg (0 unrolled, 1 plane loop, 2 low-reg)
     int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)
     int zhi_shared = 0;                 // local gz=Lz-1 plane shared with the rank above
     cdfem::Comm *comm = nullptr;        // rank communicator (comm.hip), nullptr on one GPU
@@ -213,24 +205,12 @@ struct cdfem_ctx {
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
-    int cg_x2 = 0;                      // set_option "cg_x2": brick CG updates x every second iteration (two terms)
-    int cg_dfold = 0;                   // set_option "cg_dfold": fused CG forms d = z + beta d in the apply's gather (measured slower, off)
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
-    int mass_from_d = 0;                // set_option "mass_from_d": derive the 3D mass weight from D (constant kappa, s; A/B, measured slower)
-    int diag_sf = 1;                    // set_option "diag_sf": sum-factorised PA diagonal (0: per-entry quadrature loop)
-    int cg_xfold = 0;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply (A/B)
-    double *xfold_x = nullptr;          // the solution vector while a folded brick CG loop runs
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
-    int spmv_variant = 0;               // set_option "spmv_variant": SpMV inner loop, 0 = 4 loads in flight, 1 = software-pipelined (A/B)
     int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD (windowed layout)
     int32_t *d_rperm = nullptr;         // SpMV space order: space row -> mesh row (null: mesh order)
     bool sell_windowed = false;         // slices cut from the space order (kernel row = slice * 64 + lane)
-    bool sell_xcd_sorted = false;       // global layout sorted per XCD row range (spmv_xcd_sort)
-    int spmv_xcd_sort = 0;              // set_option "spmv_xcd_sort" (read when the FA pattern is built)
-    int sell_offset = 0;                // set_option "sell_offset": bytes the SpMV's value / delta streams start past their allocation
-    double *d_svals_c_base = nullptr;   // allocations behind d_svals_c / d_sdel (sell_offset)
-    int16_t *d_sdel_base = nullptr;
     double *d_pv[2] = {};               // permuted-space scratch (apply in mesh order; solve B / X)
     bool perm_space = false;            // inside a solve that runs in the permuted order
     double *d_dinv_p = nullptr;         // the Jacobi scale in permuted order (during such a solve)
@@ -330,10 +310,9 @@ hipError_t launch_update_fin(cdfem_ctx *c, int nparts);
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
                             double *d_new, double *q);
 // q from interior/face partials (+ remote interface sums), x += alpha d, r -= alpha q, betanom
-// dprev != nullptr (cg_x2): x is updated only by even iterations, x += a_{i-1} dprev + a_i d
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
                                   const double *dinv, const double *remote_lo, const double *remote_hi,
-                                  bool den_step = false, const double *dprev = nullptr);
+                                  bool den_step = false);
 // generic deterministic dot into host-visible scalar via state (used by GMRES / tests)
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out);
 // multi-rank CG: rank-local (d, q) over owned entries into the state's den slot (all-reduce next)
@@ -361,10 +340,6 @@ hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double
                                 const double *dinv);
 // pack the local partial sums of q on the shared interface planes into d_if[0] / d_if[2]
 hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q, hipStream_t s = nullptr);
-// brick CG x-fold: flush the pending x += alpha d after the loop (dA / dB: the even / odd directions)
-hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *dA, const double *dB);
-// cg_x2: the pending x += alpha d of an odd last update (d = that update's direction buffer)
-hipError_t launch_cg_x2flush(cdfem_ctx *c, double *x, const double *d);
 hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
                                   double *d_new, double *q, hipStream_t s);
 
@@ -382,14 +357,12 @@ struct FaPattern {
     std::vector<int16_t> sdel;   // [stored] column - row when every |column - row| < 2^15, else empty
     std::vector<int32_t> perm;   // SpMV space order (sell_plan.cpp): space row -> mesh row; empty = mesh order
     bool windowed = false;       // slices cut from the space order directly (no srows)
-    bool xcd_sorted = false;     // rows length-sorted inside 8 contiguous ranges of 256-row multiples
 };
 // SpMV order (sell_plan.cpp): 0 natural + global sort, 1 natural + windows, 2 RCM + windows,
 // 3 auto (mode 0, geometric or RCM + global), 4 RCM + global, 5 geometric + global
 struct SellPlan {
     int mode = 0, base = 1;  // base: 1 natural, 2 RCM, 3 geometric
     bool windowed = false;
-    bool xcd_sort = false;   // global layout: length sort inside 8 contiguous row ranges (one per XCD)
     int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0, bw_geometric = 0;
     std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
 };
@@ -416,9 +389,7 @@ bool spmv_delta(const cdfem_ctx *c);
 // fused high-order CG iteration (ho_kernels.hip / vec_kernels.hip)
 bool tile_den_ok(const cdfem_ctx *c);
 int tile_den_blocks(const cdfem_ctx *c);
-// dold != nullptr: d = z + beta dold formed in the gather (d argument = z), written to dout
-hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part,
-                            const double *dold = nullptr, double *dout = nullptr);
+hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part);
 bool e2l_box_ok(const cdfem_ctx *c);
 hipError_t launch_den_from_partials(cdfem_ctx *c, const double *in, int64_t n);
 hipError_t launch_e2l_cg_update(cdfem_ctx *c, const double *Ye, const double *d, double *x, double *r, double *z,

@@ -132,9 +132,7 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     });
     // SpMV layout: SELL-64 over the rows in the plan's order (sell_plan.cpp)
     P.rowptr = std::move(rowptr);
-    // sell_mode bit 8: the global layout's length sort per XCD row range (set_option spmv_xcd_sort)
-    SellPlan pl = sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode & 0xff, dim, dof_xyz);
-    pl.xcd_sort = (sell_mode & 0x100) != 0;
+    SellPlan pl = sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode, dim, dof_xyz);
     sell_build(P, nl, pl);
     return P;
 }
@@ -553,7 +551,7 @@ static int sell_xcd_per(const cdfem_ctx *c)
 {
     // contiguous per-XCD ranges pay on the windowed layout (1.00x traffic); the global length sort
     // puts the longest rows first, and a range split would hand them all to XCD 0
-    return (c->spmv_xcd && c->sell_windowed) || c->sell_xcd_sorted ? (int)((sell_blocks(c) + 7) / 8) : 0;
+    return c->spmv_xcd && c->sell_windowed ? (int)((sell_blocks(c) + 7) / 8) : 0;
 }
 unsigned sell_grid(const cdfem_ctx *c)
 {
@@ -569,15 +567,10 @@ static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, doubl
     const dim3 g(sell_grid(c)), b(256);
     const int per = sell_xcd_per(c);
     const bool perm = c->sell_windowed;
-#define CDFEM_SPMV1(CI, PM, U, PIPE, NT)                                                                         \
-    CDFEM_LAUNCH(c, (k_sell_spmv<CG, CI, PM, U, PIPE, NT>), g, b, 0, c->d_sptr, c->d_srows,                        \
+#define CDFEM_SPMV(CI, PM)                                                                                       \
+    CDFEM_LAUNCH(c, (k_sell_spmv<CG, CI, PM, 4, false, true>), g, b, 0, c->d_sptr, c->d_srows,                     \
                  (const CI *)(sizeof(CI) == 2 ? (const void *)c->d_sdel : (const void *)c->d_scols), vals, x, y,  \
                  c->nslices, (int64_t)c->nl, per, part, st)
-#define CDFEM_SPMV(CI, PM)                                                                                       \
-    do {                                                                                                         \
-        if (c->spmv_variant == 1) CDFEM_SPMV1(CI, PM, 4, true, true);                                          \
-        else CDFEM_SPMV1(CI, PM, 4, false, true);                                                                \
-    } while (0)
     if (spmv_delta(c)) {
         if (perm) CDFEM_SPMV(int16_t, true);
         else CDFEM_SPMV(int16_t, false);
@@ -585,7 +578,6 @@ static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, doubl
         if (perm) CDFEM_SPMV(int32_t, true);
         else CDFEM_SPMV(int32_t, false);
     }
-#undef CDFEM_SPMV1
 #undef CDFEM_SPMV
 }
 

@@ -91,18 +91,13 @@ __device__ __forceinline__ void block_mfma(const FA &a, const FB &b, const FO &o
 //   bit 3  stage x^T  Y(e dz dy, dx)              = [ZB | ZG](e dz dy, qx) . [B; G](qx, dx)
 // Each writes LDS; the VALU z stage and quadrature-point operator stay per thread.
 
-// DIR (with DEN): the CG direction is formed in the gather, d = z + beta d_old with x = z and
-// x2 = d_old (st->beta from the update's finalizer), and the element that owns a dof writes it to
-// dout (a different buffer than x2: other elements still gather d_old) -- no separate direction pass.
-template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, int MF, bool DIR = false>
+template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, int MF>
 __global__ void __launch_bounds__(256)
 k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qd,
                double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const TileGeo geo,
-               const KrylovState *__restrict__ st, double *__restrict__ part,
-               const double *__restrict__ x2 = nullptr, double *__restrict__ dout = nullptr)
+               const KrylovState *__restrict__ st, double *__restrict__ part)
 {
     static_assert(!DEN || (CON && LAT), "den partials need the constrained lattice path");
-    static_assert(!DIR || DEN, "the folded direction runs in the fused CG apply");
     if (st != nullptr && st->done) return;
     using L = QLayout<K, 3>;
     constexpr int NC = L::nc, NP = NC / 2, QQ = Q1 * Q1, ND = D1 * D1 * D1;
@@ -117,16 +112,6 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 
     const int le = threadIdx.x / QQ, t = threadIdx.x - le * QQ;
     const int tx = t % Q1, ty = t / Q1;
-    double wxy = 0.0;  // 1 / (w_tx w_ty)^2 of this thread's point column (derived mass weight)
-    if constexpr (L::kMD) {
-        double wx = 0.0, wy = 0.0;
-#pragma unroll
-        for (int k = 0; k < Q1; ++k) {
-            if (k == tx) wx = T.iw2[k];
-            if (k == ty) wy = T.iw2[k];
-        }
-        wxy = wx * wy;
-    }
     const int e = blockIdx.x * EPB + le;
     const bool valid = le < EPB && e < ne;
     if (threadIdx.x < Q1 * D1) {
@@ -146,7 +131,7 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     const int ec = valid ? e : ne - 1;
     const int gx = tx < D1 ? tx : D1 - 1, gy = ty < D1 ? ty : D1 - 1;
     uint32_t ex = 0, ey = 0, ez = 0;
-    double xr[D1], xo[DIR ? D1 : 1];
+    double xr[D1];
     int32_t m[D1];  // LAT: ess flag; map path: map entry
     size_t g0 = 0, sz = 0;
     if constexpr (LAT) {
@@ -160,7 +145,6 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 #pragma unroll
         for (int dz = 0; dz < D1; ++dz) {
             xr[dz] = x[g0 + dz * sz];
-            if constexpr (DIR) xo[dz] = x2[g0 + dz * sz];
             m[dz] = CON ? geo.ess[g0 + dz * sz] : 0;
         }
     } else {
@@ -186,18 +170,6 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
                 qv[qz][2 * p + 1] = w.y;
             }
             if constexpr (NC & 1) qv[qz][NC - 1] = __builtin_nontemporal_load(qp + 2 * NP * QQ + t);
-        }
-    }
-    if constexpr (DIR) {
-        // d = z + beta d_old (k_cg_direction's formula), written once by the dof's owner element
-        const double beta = st->beta;
-        constexpr int P = D1 - 1;
-#pragma unroll
-        for (int dz = 0; dz < D1; ++dz) {
-            xr[dz] = xr[dz] + beta * xo[dz];
-            const bool own = gthr && (tx < P || ex == geo.ho.nx - 1) && (ty < P || ey == geo.ho.ny - 1) &&
-                             (dz < P || ez == geo.nz - 1);
-            if (own) __builtin_nontemporal_store(xr[dz], dout + g0 + dz * sz);
         }
     }
     // unconditional store (a conditional one lets the compiler sink the gather loads behind the
@@ -326,9 +298,6 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
         }
         if constexpr (L::kC) v0 += qv[qz][L::oC] * ux + qv[qz][L::oC + 1] * uy + qv[qz][L::oC + 2] * uz;
         if constexpr (L::kM) v0 += qv[qz][L::oM] * u;
-        if constexpr (L::kMD)
-            v0 += T.mscale * (wxy * T.iw2[qz]) *
-                  det_sym3(qv[qz][0], qv[qz][1], qv[qz][2], qv[qz][3], qv[qz][4], qv[qz][5]) * u;
 #pragma unroll
         for (int dz = 0; dz < D1; ++dz) {
             const double bz = T.B[qz][dz], gz = T.G[qz][dz];
@@ -456,7 +425,7 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 
 template <int D1, int Q1, unsigned K, int MF>
 static hipError_t tile_kinds_mf(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
-                             double *den_part, const double *dold = nullptr, double *dout = nullptr)
+                             double *den_part)
 {
     const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
     constexpr int EPB = 256 / (Q1 * Q1);
@@ -469,35 +438,30 @@ static hipError_t tile_kinds_mf(cdfem_ctx *c, const double *x, double *Ye, bool 
     geo.ess = c->d_ess;
     if (den_part) {
         if (!c->epencil || !con) return hipErrorInvalidValue;
-        if (dold)
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true, MF, true>), grid, block, 0, c->d_map, x,
-                         c->d_qd, Ye, T, c->ne, geo, st, den_part, dold, dout);
-        else
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true, MF>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st, den_part, (const double *)nullptr, (double *)nullptr);
+        CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true, MF>), grid, block, 0, c->d_map, x, c->d_qd,
+                     Ye, T, c->ne, geo, st, den_part);
     } else if (c->epencil) {
         if (con)
             CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st, (double *)nullptr, (const double *)nullptr, (double *)nullptr);
+                         Ye, T, c->ne, geo, st, (double *)nullptr);
         else
             CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, true, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st, (double *)nullptr, (const double *)nullptr, (double *)nullptr);
+                         Ye, T, c->ne, geo, st, (double *)nullptr);
     } else {
         if (con)
             CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, false, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
-                         Ye, T, c->ne, geo, st, (double *)nullptr, (const double *)nullptr, (double *)nullptr);
+                         Ye, T, c->ne, geo, st, (double *)nullptr);
         else
             CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, false, false, MF>), grid, block, 0, c->d_map, x,
-                         c->d_qd, Ye, T, c->ne, geo, st, (double *)nullptr, (const double *)nullptr, (double *)nullptr);
+                         c->d_qd, Ye, T, c->ne, geo, st, (double *)nullptr);
     }
     return hipGetLastError();
 }
 
 template <int D1, int Q1, unsigned K>
 static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
-                             double *den_part, const double *dold, double *dout)
+                             double *den_part)
 {
-    if (dold) return tile_kinds_mf<D1, Q1, K, 0>(c, x, Ye, con, st, den_part, dold, dout);
     switch (c->ho_mfma) {
     case 1: return tile_kinds_mf<D1, Q1, K, 1>(c, x, Ye, con, st, den_part);
     case 3: return tile_kinds_mf<D1, Q1, K, 3>(c, x, Ye, con, st, den_part);
@@ -510,18 +474,16 @@ static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con
 
 template <int D1, int Q1>
 static hipError_t tile_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
-                          double *den_part, const double *dold = nullptr, double *dout = nullptr)
+                          double *den_part)
 {
     switch (c->kinds) {
-    case 1: return tile_kinds<D1, Q1, 1>(c, x, Ye, con, st, den_part, dold, dout);
-    case 2: return tile_kinds<D1, Q1, 2>(c, x, Ye, con, st, den_part, dold, dout);
-    case 3: return tile_kinds<D1, Q1, 3>(c, x, Ye, con, st, den_part, dold, dout);
-    case 4: return tile_kinds<D1, Q1, 4>(c, x, Ye, con, st, den_part, dold, dout);
-    case 5: return tile_kinds<D1, Q1, 5>(c, x, Ye, con, st, den_part, dold, dout);
-    case 6: return tile_kinds<D1, Q1, 6>(c, x, Ye, con, st, den_part, dold, dout);
-    case 7: return tile_kinds<D1, Q1, 7>(c, x, Ye, con, st, den_part, dold, dout);
-    case 5 | kMassFromD: return tile_kinds<D1, Q1, 5 | kMassFromD>(c, x, Ye, con, st, den_part, dold, dout);
-    case 7 | kMassFromD: return tile_kinds<D1, Q1, 7 | kMassFromD>(c, x, Ye, con, st, den_part, dold, dout);
+    case 1: return tile_kinds<D1, Q1, 1>(c, x, Ye, con, st, den_part);
+    case 2: return tile_kinds<D1, Q1, 2>(c, x, Ye, con, st, den_part);
+    case 3: return tile_kinds<D1, Q1, 3>(c, x, Ye, con, st, den_part);
+    case 4: return tile_kinds<D1, Q1, 4>(c, x, Ye, con, st, den_part);
+    case 5: return tile_kinds<D1, Q1, 5>(c, x, Ye, con, st, den_part);
+    case 6: return tile_kinds<D1, Q1, 6>(c, x, Ye, con, st, den_part);
+    case 7: return tile_kinds<D1, Q1, 7>(c, x, Ye, con, st, den_part);
     default: return hipErrorInvalidValue;
     }
 }
@@ -547,12 +509,11 @@ bool tile_den_ok(const cdfem_ctx *c)
 }
 
 // CG mode: Ye = A_c d (E-vector) and the den partials (one per block) into part
-hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part,
-                            const double *dold, double *dout)
+hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part)
 {
     const int q1 = c->rule_op.q1;
-    if (c->p == 3 && q1 == 5) return tile_dq<4, 5>(c, d, Ye, true, st, part, dold, dout);
-    if (c->p == 4 && q1 == 6) return tile_dq<5, 6>(c, d, Ye, true, st, part, dold, dout);
+    if (c->p == 3 && q1 == 5) return tile_dq<4, 5>(c, d, Ye, true, st, part);
+    if (c->p == 4 && q1 == 6) return tile_dq<5, 6>(c, d, Ye, true, st, part);
     return hipErrorInvalidValue;
 }
 

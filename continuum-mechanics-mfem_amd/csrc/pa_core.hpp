@@ -12,8 +12,6 @@ template <int D1, int Q1>
 struct Tab {
     double B[Q1][D1];
     double G[Q1][D1];
-    double iw2[Q1];   // 1 / w_q^2 of the 1D rule (derived mass weight)
-    double mscale;    // s / kappa^3 (derived mass weight), else 0
 };
 
 template <int D1, int Q1>
@@ -25,8 +23,6 @@ static Tab<D1, Q1> make_tab(const Rule1D &r)
             t.B[q][d] = r.B[q][d];
             t.G[q][d] = r.G[q][d];
         }
-    for (int q = 0; q < Q1; ++q) t.iw2[q] = 1.0 / (r.wts[q] * r.wts[q]);
-    t.mscale = r.mscale;
     return t;
 }
 
@@ -35,11 +31,7 @@ template <unsigned K, int DIM>
 struct QLayout {
     static constexpr bool kD = (K & CDFEM_DIFFUSION) != 0;
     static constexpr bool kC = (K & CDFEM_CONVECTION) != 0;
-    // kMD: the mass weight W s detJ is derived from the diffusion block (kinds bit kMassFromD, 3D,
-    // constant kappa and s): det D = (W kappa)^3 detJ, so M = s det(D) / (W^2 kappa^3) -- one qdata
-    // component less to stream (q_c 9 instead of 10 for D+C+M)
-    static constexpr bool kMD = DIM == 3 && (K & kMassFromD) != 0 && (K & CDFEM_MASS) != 0 && (K & CDFEM_DIFFUSION) != 0;
-    static constexpr bool kM = (K & CDFEM_MASS) != 0 && !kMD;
+    static constexpr bool kM = (K & CDFEM_MASS) != 0;
     static constexpr int nD = kD ? DIM * (DIM + 1) / 2 : 0;
     static constexpr int oC = nD;
     static constexpr int oM = oC + (kC ? DIM : 0);
@@ -57,16 +49,10 @@ __host__ __device__ constexpr int qd_offset(int c, int lane, int nc)
 
 typedef double v2d_t __attribute__((ext_vector_type(2)));
 
-// det of the symmetric 3x3 [d00 d01 d02; d01 d11 d12; d02 d12 d22] stored as (d00, d01, d02, d11, d12, d22)
-__host__ __device__ inline double det_sym3(double d00, double d01, double d02, double d11, double d12, double d22)
-{
-    return d00 * (d11 * d22 - d12 * d12) - d01 * (d01 * d22 - d12 * d02) + d02 * (d01 * d12 - d11 * d02);
-}
-
 // NT: non-temporal (streaming) loads — qdata is read once per Mult, so it must not displace the
 // L-vectors that neighbouring elements / bricks re-read from L2.  Measured on k_brick_cg (64^3,
 // p = 2): 283 -> 245 us per launch, and the following CG update 42.7 -> 35.5 us (its vectors
-// are still cached); tools/ab.py brick_variant 0 vs 6 (6 = temporal loads, kept for A/B).
+// are still cached; tools/ab.py, round 1).
 template <int NC, bool NT = false>
 __device__ __forceinline__ void load_qp(const double *__restrict__ qp, int lane, double (&v)[NC])
 {
@@ -94,24 +80,9 @@ __device__ __forceinline__ void load_qp(const double *__restrict__ qp, int lane,
 // plane's worth of it live in registers.  QZU = unroll factor of the quadrature-plane loop
 // (Q1: straight-line code, the compiler hoists qdata loads across planes; 1: one plane's loads
 // in flight, ~250 VGPRs at p = 2, two waves per SIMD).
-// QS: qdata source, qs(q, qv) fills point q's NC components (q is a compile-time constant when the
-// plane loop is unrolled); the default reads global memory (load_qp)
-template <int D1, int Q1, unsigned K, typename XL, int QZU, typename QS>
-__device__ __forceinline__ void elem_apply3d_qs(const XL &xl, const QS &qs, const Tab<D1, Q1> &T,
-                                                double (&Y)[D1][D1][D1]);
-
-template <int D1, int Q1, unsigned K, typename XL, int QZU = Q1, bool NT = true>
+template <int D1, int Q1, unsigned K, typename XL, int QZU = Q1>
 __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restrict__ q0, int lane,
                                              const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
-{
-    constexpr int NC = QLayout<K, 3>::nc;
-    elem_apply3d_qs<D1, Q1, K, XL, QZU>(
-        xl, [&](int q, double (&qv)[NC]) { load_qp<NC, NT>(q0 + (size_t)q * NC * kLanes, lane, qv); }, T, Y);
-}
-
-template <int D1, int Q1, unsigned K, typename XL, int QZU, typename QS>
-__device__ __forceinline__ void elem_apply3d_qs(const XL &xl, const QS &qs, const Tab<D1, Q1> &T,
-                                                double (&Y)[D1][D1][D1])
 {
     using L = QLayout<K, 3>;
     constexpr int NC = L::nc;
@@ -178,7 +149,7 @@ __device__ __forceinline__ void elem_apply3d_qs(const XL &xl, const QS &qs, cons
                 }
                 const int q = qx + Q1 * (qy + Q1 * qz);
                 double qv[NC];
-                qs(q, qv);
+                load_qp<NC, true>(q0 + (size_t)q * NC * kLanes, lane, qv);
                 double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
                 if constexpr (L::kD) {
                     gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;
@@ -187,9 +158,6 @@ __device__ __forceinline__ void elem_apply3d_qs(const XL &xl, const QS &qs, cons
                 }
                 if constexpr (L::kC) vv = qv[L::oC] * ux + qv[L::oC + 1] * uy + qv[L::oC + 2] * uz;
                 if constexpr (L::kM) vv += qv[L::oM] * u;
-                if constexpr (L::kMD)
-                    vv += T.mscale * (T.iw2[qx] * T.iw2[qy] * T.iw2[qz]) *
-                          det_sym3(qv[0], qv[1], qv[2], qv[3], qv[4], qv[5]) * u;
                 // transposed contraction in x
 #pragma unroll
                 for (int dx = 0; dx < D1; ++dx) {
@@ -229,105 +197,6 @@ __device__ __forceinline__ void elem_apply3d_qs(const XL &xl, const QS &qs, cons
                 }
     }
 
-}
-
-}  // namespace cdfem
-
-namespace cdfem {
-
-// Low-register variant of elem_apply3d: no per-plane intermediates (T0/Tz, RT/RTz).  For every
-// (qz, qy) pair the y/z-contracted input a[dx] = sum_{dz,dy} Bz By X is formed straight from the
-// loader (LDS) and the transposed result is folded straight into Y.  ~35% more FMAs, ~70 fewer
-// VGPRs; the loader is called 16x per element instead of 4x.
-template <int D1, int Q1, unsigned K, typename XL, int QZU = 1>
-__device__ __forceinline__ void elem_apply3d_lr(const XL &xl, const double *__restrict__ q0, int lane,
-                                                const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
-{
-    using L = QLayout<K, 3>;
-    constexpr int NC = L::nc;
-#pragma unroll
-    for (int dz = 0; dz < D1; ++dz)
-#pragma unroll
-        for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) Y[dz][dy][dx] = 0.0;
-#pragma unroll QZU
-    for (int qz = 0; qz < Q1; ++qz) {
-#pragma unroll
-        for (int qy = 0; qy < Q1; ++qy) {
-            double a[D1], ay[D1], az[D1];
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) { a[dx] = 0.0; ay[dx] = 0.0; az[dx] = 0.0; }
-#pragma unroll
-            for (int dz = 0; dz < D1; ++dz)
-#pragma unroll
-                for (int dy = 0; dy < D1; ++dy) {
-                    const double bb = T.B[qz][dz] * T.B[qy][dy];
-                    const double bg = T.B[qz][dz] * T.G[qy][dy];
-                    const double gb = T.G[qz][dz] * T.B[qy][dy];
-#pragma unroll
-                    for (int dx = 0; dx < D1; ++dx) {
-                        const double xv = xl(dz, dy, dx);
-                        a[dx] += bb * xv;
-                        ay[dx] += bg * xv;
-                        az[dx] += gb * xv;
-                    }
-                }
-            double Rv[D1], Ry[D1], Rz[D1];
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) { Rv[dx] = 0.0; Ry[dx] = 0.0; Rz[dx] = 0.0; }
-#pragma unroll
-            for (int qx = 0; qx < Q1; ++qx) {
-                double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
-#pragma unroll
-                for (int dx = 0; dx < D1; ++dx) {
-                    u += T.B[qx][dx] * a[dx];
-                    ux += T.G[qx][dx] * a[dx];
-                    uy += T.B[qx][dx] * ay[dx];
-                    uz += T.B[qx][dx] * az[dx];
-                }
-                const int q = qx + Q1 * (qy + Q1 * qz);
-                double qv[NC];
-                load_qp<NC, true>(q0 + (size_t)q * NC * kLanes, lane, qv);
-                double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
-                if constexpr (L::kD) {
-                    gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;
-                    gy = qv[1] * ux + qv[3] * uy + qv[4] * uz;
-                    gz = qv[2] * ux + qv[4] * uy + qv[5] * uz;
-                }
-                if constexpr (L::kC) vv = qv[L::oC] * ux + qv[L::oC + 1] * uy + qv[L::oC + 2] * uz;
-                if constexpr (L::kM) vv += qv[L::oM] * u;
-                if constexpr (L::kMD)
-                    vv += T.mscale * (T.iw2[qx] * T.iw2[qy] * T.iw2[qz]) *
-                          det_sym3(qv[0], qv[1], qv[2], qv[3], qv[4], qv[5]) * u;
-#pragma unroll
-                for (int dx = 0; dx < D1; ++dx) {
-                    if constexpr (L::kD) {
-                        Rv[dx] += T.B[qx][dx] * vv + T.G[qx][dx] * gx;
-                        Ry[dx] += T.B[qx][dx] * gy;
-                        Rz[dx] += T.B[qx][dx] * gz;
-                    } else {
-                        Rv[dx] += T.B[qx][dx] * vv;
-                    }
-                }
-            }
-#pragma unroll
-            for (int dz = 0; dz < D1; ++dz)
-#pragma unroll
-                for (int dy = 0; dy < D1; ++dy) {
-                    const double bb = T.B[qz][dz] * T.B[qy][dy];
-                    const double bg = T.B[qz][dz] * T.G[qy][dy];
-                    const double gb = T.G[qz][dz] * T.B[qy][dy];
-#pragma unroll
-                    for (int dx = 0; dx < D1; ++dx) {
-                        if constexpr (L::kD)
-                            Y[dz][dy][dx] += bb * Rv[dx] + bg * Ry[dx] + gb * Rz[dx];
-                        else
-                            Y[dz][dy][dx] += bb * Rv[dx];
-                    }
-                }
-        }
-    }
 }
 
 // exact unsigned division by a run-time divisor: n / d == (n * m) >> k for n < 2^31

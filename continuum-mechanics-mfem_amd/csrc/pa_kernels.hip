@@ -310,7 +310,7 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
             put(o++, W * alpha * acc);
         }
     }
-    if ((kinds & CDFEM_MASS) && !(kinds & kMassFromD)) {  // derived from D otherwise (QLayout::kMD)
+    if (kinds & CDFEM_MASS) {
         const double s = mass_q ? mass_q[eq] : mass;
         put(o++, W * s * det);
     }
@@ -392,160 +392,130 @@ k_diag_elem(const double *__restrict__ qd, const int32_t *__restrict__ perm, int
             for (int k = 0; k < DIM; ++k) cg += qq(oC + k) * g[k];
             acc += phi * cg;
         }
-        if (kinds & CDFEM_MASS) {
-            double m;
-            if (kinds & kMassFromD) {  // M = s det(D) / (W^2 kappa^3)
-                const int qx = q % q1, qy = (q / q1) % q1, qz = q / (q1 * q1);
-                const double W = r.wts[qx] * r.wts[qy] * r.wts[qz];
-                m = r.mscale * det_sym3(qq(0), qq(1), qq(2), qq(3), qq(4), qq(5)) / (W * W);
-            } else {
-                m = qq(oM);
-            }
-            acc += m * phi * phi;
-        }
+        if (kinds & CDFEM_MASS) acc += qq(oM) * phi * phi;
     }
     if (qlay == 1) Ye[ho_eidx(ho, (uint32_t)e, l)] = acc;
     else Ye[t] = acc;  // t == (b*nd + l)*64 + lane
 }
 
 // PA diagonal, sum-factorised (MFEM's PA AssembleDiagonal): thread per (element, i1[, i2]) computing
-// the D1 entries along the last axis.  Every term of the operator is a component c of the qdata
-// times a product of 1D factors, one per axis: F_d(q, i) = u_d(q, i) v_d(q, i) with u, v = G when the
-// term differentiates along d, else B, so
+// the D1 entries along the last axis.  Every term of the operator is a qdata component c times a
+// product of 1D factors, one per axis: F_d(q, i) = u_d(q, i) v_d(q, i) with u, v = G when the term
+// differentiates along d, else B, so
 //   diag(i) = sum_terms mult * sum_{q_last} F_last * (... sum_{q1} F_1 * qd_c(q)).
-// Terms: diffusion c = (a, b) with a <= b (off-diagonal twice), convection c = oC + k with (k, none),
-// mass (none, none).  ~D1^(dim-1) threads read each element's qdata once (wave broadcast) and do
-// 10 Q1^dim FMAs each, against D1^dim Q1^dim (30 flops) for the per-entry form.
-// D1T / Q1T > 0: compile-time sizes (the loops unroll and each qdata row is loaded before its sums);
-// 0: the rule's run-time sizes
-template <int DIM, int D1T, int Q1T>
-__global__ void __launch_bounds__(256)
-k_diag_sf(const double *__restrict__ qd, const int32_t *__restrict__ perm, int ne, int nblk, int nd, int qlay,
-          const HoLayout ho, const Rule1D r, unsigned kinds, int nc, double *__restrict__ Ye)
+// Terms (DiagTerms): diffusion c = (a, b) with a <= b (off-diagonal twice), convection c = oC + k
+// with (k, none), mass (none, none).  Everything (term list, sizes, factor types) is compile-time:
+// the loops unroll and no array is indexed at run time (no scratch).  The D1^(dim-1) threads of an
+// element are consecutive, so each qdata load of a wave is a broadcast of at most a few addresses
+// and an element's qdata is fetched from HBM once.  10 Q1^dim FMAs per thread and term class
+// against D1^dim Q1^dim for the per-entry form (k_diag_elem, kept for rules other than the
+// operators' n = p + 2).
+template <int DIM, unsigned K>
+struct DiagTerms {
+    static constexpr int nD = (K & CDFEM_DIFFUSION) ? DIM * (DIM + 1) / 2 : 0;
+    static constexpr int nC = (K & CDFEM_CONVECTION) ? DIM : 0;
+    static constexpr int n = nD + nC + ((K & CDFEM_MASS) ? 1 : 0);
+    // derivative axes a <= b of diffusion term t (components D00, D01, D02, D11, D12, D22 / D00, D01, D11)
+    static constexpr int da(int t) { return DIM == 3 ? (t < 3 ? 0 : t < 5 ? 1 : 2) : (t < 2 ? 0 : 1); }
+    static constexpr int db(int t) { return DIM == 3 ? (t < 3 ? t : t < 5 ? t - 2 : 2) : (t < 2 ? t : 1); }
+    static constexpr int a(int t) { return t < nD ? da(t) : t < nD + nC ? t - nD : -1; }
+    static constexpr int b(int t) { return t < nD ? db(t) : -1; }
+    static constexpr double mult(int t) { return t < nD && da(t) != db(t) ? 2.0 : 1.0; }
+    // qdata component of term t (its index in QLayout order: D, then C, then M)
+    static constexpr int comp(int t) { return t; }
+    // 1D factor along axis d: 0 = B B, 1 = G B, 2 = G G
+    static constexpr int type(int t, int d) { return (a(t) == d ? 1 : 0) + (b(t) == d ? 1 : 0); }
+};
+
+template <int D1, int Q1>
+__device__ __forceinline__ double diag_factor(const Tab<D1, Q1> &T, int type, int q, int i)
 {
-    const int d1 = D1T > 0 ? D1T : r.d1, q1 = Q1T > 0 ? Q1T : r.q1;
-    const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
-    const int nt = DIM == 3 ? d1 * d1 : d1;  // threads per element
+    const double bq = T.B[q][i], gq = T.G[q][i];
+    return type == 0 ? bq * bq : type == 1 ? gq * bq : gq * gq;
+}
+
+template <int DIM, int D1, int Q1, unsigned K>
+__global__ void __launch_bounds__(256)
+k_diag_sf(const double *__restrict__ qd, const int32_t *__restrict__ perm, int ne, int nblk, int qlay,
+          const HoLayout ho, const Tab<D1, Q1> T, double *__restrict__ Ye)
+{
+    using TT = DiagTerms<DIM, K>;
+    constexpr int NC = QLayout<K, DIM>::nc;
+    constexpr int ND = DIM == 3 ? D1 * D1 * D1 : D1 * D1;
+    constexpr int NQ = DIM == 3 ? Q1 * Q1 * Q1 : Q1 * Q1;
+    constexpr int NT = DIM == 3 ? D1 * D1 : D1;  // threads per element
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t npos = qlay == 1 ? (int64_t)ne : (int64_t)nblk * kLanes;
-    if (t >= npos * nt) return;
-    const int64_t pos = t / nt;
-    const int it = (int)(t - pos * nt);
-    const int i1 = it % d1, i2 = DIM == 3 ? it / d1 : 0;
+    if (t >= npos * NT) return;
+    const int64_t pos = t / NT;
+    const int it = (int)(t - pos * NT);
+    const int i1 = it % D1, i2 = DIM == 3 ? it / D1 : 0;
     const int b = qlay == 1 ? 0 : (int)(pos / kLanes), lane = qlay == 1 ? 0 : (int)(pos % kLanes);
     const int e = qlay == 1 ? (int)pos : perm[pos];
     auto out = [&](int i3, double v) {
-        const int l = DIM == 3 ? i1 + d1 * (i2 + d1 * i3) : i1 + d1 * i3;
+        const int l = DIM == 3 ? i1 + D1 * (i2 + D1 * i3) : i1 + D1 * i3;
         if (qlay == 1) Ye[ho_eidx(ho, (uint32_t)e, l)] = v;
-        else Ye[((size_t)b * nd + l) * kLanes + lane] = v;
+        else Ye[((size_t)b * ND + l) * kLanes + lane] = v;
     };
     if (e < 0 || e >= ne) {
-        for (int i3 = 0; i3 < d1; ++i3) out(i3, 0.0);
+#pragma unroll
+        for (int i3 = 0; i3 < D1; ++i3) out(i3, 0.0);
         return;
     }
-    // qdata of component c at (qx, qy, qz) = base_c + qz * sz + (qx + q1 qy) * sxy (cheap strides)
-    const size_t plane = qd_ho_plane(nc, q1);
+    // qdata of component c at (qx, qy[, qz]): base_c + qz * sz + (qx + Q1 qy) * sxy
+    const size_t plane = qd_ho_plane(NC, Q1);
     auto cbase = [&](int c, size_t &sxy, size_t &sz) -> const double * {
         if (qlay == 1) {
-            const int qq2 = q1 * q1;
-            const bool pair = c < (nc & ~1);
+            constexpr int QQ = Q1 * Q1;
+            const bool pair = c < (NC & ~1);
             sxy = pair ? 2 : 1;
             sz = DIM == 3 ? plane : 0;
-            return qd + (size_t)e * q1 * plane + (pair ? (size_t)(c >> 1) * qq2 * 2 + (c & 1) : (size_t)(nc & ~1) * qq2);
+            return qd + (size_t)e * Q1 * plane + (pair ? (size_t)(c >> 1) * QQ * 2 + (c & 1) : (size_t)(NC & ~1) * QQ);
         }
-        sxy = (size_t)nc * kLanes;
-        sz = (size_t)q1 * q1 * nc * kLanes;
-        return qd + (size_t)b * nq * nc * kLanes + qd_offset(c, lane, nc);
+        sxy = (size_t)NC * kLanes;
+        sz = (size_t)Q1 * Q1 * NC * kLanes;
+        return qd + (size_t)b * NQ * NC * kLanes + qd_offset(c, lane, NC);
     };
-    // this thread's 1D factors along the first axes (i1, i2 fixed)
-    double B1[kMaxQ1], G1[kMaxQ1], B2[kMaxQ1], G2[kMaxQ1];
-    for (int q = 0; q < q1; ++q) {
-        B1[q] = r.B[q][i1];
-        G1[q] = r.G[q][i1];
-        B2[q] = r.B[q][i2];
-        G2[q] = r.G[q][i2];
-    }
-    // term list: component, derivative axes a, b (-1 = none), multiplicity
-    int tc[10], ta[10], tb[10];
-    double tm[10];
-    int nterm = 0;
-    if (kinds & CDFEM_DIFFUSION) {
-        int c = 0;
-        for (int a = 0; a < DIM; ++a)
-            for (int bb = a; bb < DIM; ++bb, ++c) {
-                tc[nterm] = c; ta[nterm] = a; tb[nterm] = bb; tm[nterm] = a == bb ? 1.0 : 2.0; ++nterm;
-            }
-    }
-    const int oC = (kinds & CDFEM_DIFFUSION) ? DIM * (DIM + 1) / 2 : 0;
-    const int oM = oC + ((kinds & CDFEM_CONVECTION) ? DIM : 0);
-    if (kinds & CDFEM_CONVECTION)
-        for (int k = 0; k < DIM; ++k) {
-            tc[nterm] = oC + k; ta[nterm] = k; tb[nterm] = -1; tm[nterm] = 1.0; ++nterm;
-        }
-    const bool mass_from_d = DIM == 3 && (kinds & kMassFromD) && (kinds & CDFEM_MASS) && (kinds & CDFEM_DIFFUSION);
-    if (kinds & CDFEM_MASS) {  // component -1: the mass weight derived from D (QLayout::kMD)
-        tc[nterm] = mass_from_d ? -1 : oM; ta[nterm] = -1; tb[nterm] = -1; tm[nterm] = 1.0; ++nterm;
-    }
-    const double *dbase[6] = {};
-    size_t dsxy = 0, dsz = 0;
-    if (mass_from_d)
-        for (int k = 0; k < 6; ++k) dbase[k] = cbase(k, dsxy, dsz);
-    double acc[kMaxD1];
-    for (int i3 = 0; i3 < d1; ++i3) acc[i3] = 0.0;
-    const int last = DIM - 1;
-    for (int s = 0; s < nterm; ++s) {
-        const int a = ta[s], bb = tb[s];
+    constexpr int last = DIM - 1;
+    double acc[D1];
+#pragma unroll
+    for (int i3 = 0; i3 < D1; ++i3) acc[i3] = 0.0;
+#pragma unroll
+    for (int s = 0; s < TT::n; ++s) {
         size_t sxy = 0, sz = 0;
-        const bool derived = tc[s] < 0;
-        const double *qc = derived ? nullptr : cbase(tc[s], sxy, sz);
-        double f1[kMaxQ1], f2[kMaxQ1];
-        for (int q = 0; q < q1; ++q) {
-            f1[q] = (a == 0 ? G1[q] : B1[q]) * (bb == 0 ? G1[q] : B1[q]);
-            f2[q] = (a == 1 ? G2[q] : B2[q]) * (bb == 1 ? G2[q] : B2[q]);
+        const double *qc = cbase(TT::comp(s), sxy, sz);
+        double f1[Q1], f2[Q1];
+#pragma unroll
+        for (int q = 0; q < Q1; ++q) {
+            f1[q] = diag_factor(T, TT::type(s, 0), q, i1);
+            f2[q] = DIM == 3 ? diag_factor(T, TT::type(s, 1), q, i2) : 0.0;
         }
-#pragma unroll
-        for (int qz = 0; qz < (Q1T > 0 ? Q1T : kMaxQ1); ++qz) {  // the last axis' quadrature index
-            if (Q1T == 0 && qz >= q1) break;
+        // the last axis' quadrature index: not unrolled in 3D, so one plane's Q1^2 loads are in
+        // flight per step (fully unrolled, the compiler hoists all Q1^3 loads: up to 256 VGPRs + spills)
+        constexpr int kUz = DIM == 3 ? 1 : Q1;
+#pragma unroll kUz
+        for (int qz = 0; qz < Q1; ++qz) {
             double szs = 0.0;
-            if (DIM == 3) {
-                const double *qp = derived ? nullptr : qc + qz * sz;
+            if constexpr (DIM == 3) {
+                const double *qp = qc + qz * sz;
 #pragma unroll
-                for (int qy = 0; qy < (Q1T > 0 ? Q1T : kMaxQ1); ++qy) {
-                    if (Q1T == 0 && qy >= q1) break;
-                    double v[Q1T > 0 ? Q1T : kMaxQ1];
-#pragma unroll
-                    for (int qx = 0; qx < (Q1T > 0 ? Q1T : kMaxQ1); ++qx)
-                        if (Q1T > 0 || qx < q1) {
-                            if (derived) {
-                                const size_t o = qz * dsz + (size_t)(qx + q1 * qy) * dsxy;
-                                const double w = r.wts[qx] * r.wts[qy] * r.wts[qz];
-                                v[qx] = r.mscale *
-                                        det_sym3(dbase[0][o], dbase[1][o], dbase[2][o], dbase[3][o], dbase[4][o], dbase[5][o]) /
-                                        (w * w);
-                            } else {
-                                v[qx] = qp[(size_t)(qx + q1 * qy) * sxy];
-                            }
-                        }
+                for (int qy = 0; qy < Q1; ++qy) {
                     double sx = 0.0;
 #pragma unroll
-                    for (int qx = 0; qx < (Q1T > 0 ? Q1T : kMaxQ1); ++qx)
-                        if (Q1T > 0 || qx < q1) sx += f1[qx] * v[qx];
+                    for (int qx = 0; qx < Q1; ++qx) sx += f1[qx] * qp[(size_t)(qx + Q1 * qy) * sxy];
                     szs += f2[qy] * sx;
                 }
             } else {
 #pragma unroll
-                for (int qx = 0; qx < (Q1T > 0 ? Q1T : kMaxQ1); ++qx)
-                    if (Q1T > 0 || qx < q1) szs += f1[qx] * qc[(size_t)(qx + q1 * qz) * sxy];
+                for (int qx = 0; qx < Q1; ++qx) szs += f1[qx] * qc[(size_t)(qx + Q1 * qz) * sxy];
             }
-            szs *= tm[s];
-            for (int i3 = 0; i3 < d1; ++i3) {
-                const double u = a == last ? r.G[qz][i3] : r.B[qz][i3];
-                const double v = bb == last ? r.G[qz][i3] : r.B[qz][i3];
-                acc[i3] += u * v * szs;
-            }
+            szs *= TT::mult(s);
+#pragma unroll
+            for (int i3 = 0; i3 < D1; ++i3) acc[i3] += diag_factor(T, TT::type(s, last), qz, i3) * szs;
         }
     }
-    for (int i3 = 0; i3 < d1; ++i3) out(i3, acc[i3]);
+#pragma unroll
+    for (int i3 = 0; i3 < D1; ++i3) out(i3, acc[i3]);
 }
 
 // linear form, element part: be_l = sum_q W detJ f_q phi_l; thread per (block, l, lane)
@@ -620,37 +590,48 @@ hipError_t launch_quad_points(cdfem_ctx *c, const Rule1D &r, double *xyz)
     return hipGetLastError();
 }
 
+template <int DIM, int D1, int Q1>
+static bool diag_sf_kinds(cdfem_ctx *c, double *Ye)
+{
+    const int64_t npos = c->qlay == 1 ? (int64_t)c->ne : (int64_t)c->nblk * kLanes;
+    const int64_t n = npos * (DIM == 3 ? D1 * D1 : D1);
+    const dim3 g(grid_for(n, 256)), bs(256);
+    const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
+#define CDFEM_DSF(K_)                                                                                      \
+    hipLaunchKernelGGL((k_diag_sf<DIM, D1, Q1, K_>), g, bs, 0, c->stream, c->d_qd, c->d_perm, c->ne, c->nblk, \
+                       c->qlay, ho_layout(c), T, Ye)
+    switch (c->kinds) {
+    case 1: CDFEM_DSF(1); return true;
+    case 2: CDFEM_DSF(2); return true;
+    case 3: CDFEM_DSF(3); return true;
+    case 4: CDFEM_DSF(4); return true;
+    case 5: CDFEM_DSF(5); return true;
+    case 6: CDFEM_DSF(6); return true;
+    case 7: CDFEM_DSF(7); return true;
+    default: return false;
+    }
+#undef CDFEM_DSF
+}
+
 hipError_t launch_diag_elem(cdfem_ctx *c, double *Ye)
 {
-    if (c->diag_sf) {  // sum-factorised (default)
-        const int d1 = c->rule_op.d1, q1 = c->rule_op.q1;
-        const int64_t npos = c->qlay == 1 ? (int64_t)c->ne : (int64_t)c->nblk * kLanes;
-        const int64_t n = npos * (c->dim == 3 ? d1 * d1 : d1);
-        const dim3 g(grid_for(n, 256)), bs(256);
-#define CDFEM_DSF(DIM_, D1_, Q1_)                                                                        \
-    hipLaunchKernelGGL((k_diag_sf<DIM_, D1_, Q1_>), g, bs, 0, c->stream, c->d_qd, c->d_perm, c->ne, c->nblk, \
-                       c->nd, c->qlay, ho_layout(c), c->rule_op, c->kinds, c->ncomp, Ye)
-        const bool three = c->dim == 3;
-        if (d1 == q1 - 1 && d1 >= 2 && d1 <= 5) {  // the Gauss n = p + 2 rules of the operators
-            if (three) {
-                if (d1 == 2) CDFEM_DSF(3, 2, 3);
-                else if (d1 == 3) CDFEM_DSF(3, 3, 4);
-                else if (d1 == 4) CDFEM_DSF(3, 4, 5);
-                else CDFEM_DSF(3, 5, 6);
-            } else {
-                if (d1 == 2) CDFEM_DSF(2, 2, 3);
-                else if (d1 == 3) CDFEM_DSF(2, 3, 4);
-                else if (d1 == 4) CDFEM_DSF(2, 4, 5);
-                else CDFEM_DSF(2, 5, 6);
-            }
-        } else if (three) {
-            CDFEM_DSF(3, 0, 0);
+    const int d1 = c->rule_op.d1, q1 = c->rule_op.q1;
+    bool done = false;
+    if (d1 == q1 - 1) {  // the operators' Gauss n = p + 2 rules: sum-factorised, compile-time sizes
+        if (c->dim == 3) {
+            if (d1 == 2) done = diag_sf_kinds<3, 2, 3>(c, Ye);
+            else if (d1 == 3) done = diag_sf_kinds<3, 3, 4>(c, Ye);
+            else if (d1 == 4) done = diag_sf_kinds<3, 4, 5>(c, Ye);
+            else if (d1 == 5) done = diag_sf_kinds<3, 5, 6>(c, Ye);
         } else {
-            CDFEM_DSF(2, 0, 0);
+            if (d1 == 2) done = diag_sf_kinds<2, 2, 3>(c, Ye);
+            else if (d1 == 3) done = diag_sf_kinds<2, 3, 4>(c, Ye);
+            else if (d1 == 4) done = diag_sf_kinds<2, 4, 5>(c, Ye);
+            else if (d1 == 5) done = diag_sf_kinds<2, 5, 6>(c, Ye);
         }
-#undef CDFEM_DSF
-        return hipGetLastError();
     }
+    if (done) return hipGetLastError();
+    // any other rule: the per-entry quadrature loop
     const int64_t n = (int64_t)c->nblk * c->nd * kLanes;
     if (c->dim == 3)
         hipLaunchKernelGGL(k_diag_elem<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
@@ -708,8 +689,6 @@ static hipError_t apply_dq(cdfem_ctx *c, const double *x, double *Ye, bool con, 
     case 5: return apply_kinds<DIM, D1, Q1, 5>(c, x, Ye, con, st);
     case 6: return apply_kinds<DIM, D1, Q1, 6>(c, x, Ye, con, st);
     case 7: return apply_kinds<DIM, D1, Q1, 7>(c, x, Ye, con, st);
-    case 5 | kMassFromD: return apply_kinds<DIM, D1, Q1, 5 | kMassFromD>(c, x, Ye, con, st);
-    case 7 | kMassFromD: return apply_kinds<DIM, D1, Q1, 7 | kMassFromD>(c, x, Ye, con, st);
     default: return hipErrorInvalidValue;
     }
 }

@@ -67,7 +67,6 @@ __device__ inline double sum_partials(const double *part, int n, double *sh)
 __device__ inline void cg_den_step(KrylovState *st, double den)
 {
     st->den = den;
-    st->reserved[0] = 0;  // x-fold (brick CG): the apply before this den step folded the pending x update
     const int first = (st->first_den != 0);
     st->first_den = 0;
     if (den == 0.0) {

@@ -361,17 +361,7 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
     std::vector<int32_t> order(nl);  // slice position -> space row
     for (int64_t i = 0; i < nl; ++i) order[i] = (int32_t)i;
     auto by_len = [&](int32_t a, int32_t b) { return rlen(a) > rlen(b); };
-    P.xcd_sorted = !pl.windowed && pl.xcd_sort;
-    if (P.xcd_sorted) {
-        // 8 contiguous ranges of R rows (a multiple of 4 slices = one logical SpMV block), each
-        // sorted by length: XCD x runs range x (fa_kernels.hip sell_xcd_per), so its L2 sees its own
-        // part of x plus the halo, with the longest rows first as in the global sort
-        const int64_t R = (nl + 8 * 4 * kLanes - 1) / (8 * 4 * kLanes) * (4 * kLanes);
-        for (int64_t lo = 0; lo < nl; lo += R)
-            std::stable_sort(order.begin() + lo, order.begin() + std::min(nl, lo + R), by_len);
-    } else if (!pl.windowed) {
-        std::stable_sort(order.begin(), order.end(), by_len);
-    }
+    if (!pl.windowed) std::stable_sort(order.begin(), order.end(), by_len);
     const bool permuted = pl.windowed;  // kernel row = slice position (no srows)
     P.sptr.assign(ns + 1, 0);
     if (!permuted) P.srows.assign(ns * kLanes, -1);

@@ -205,9 +205,6 @@ __device__ inline void cg_init_logic(KrylovState *st, double nom, double rel_tol
     st->done = 0;
     st->first_den = 1;  // next den is the initial one
     st->beta = 0.0;
-    st->reserved[0] = 0;  // no x update pending (brick CG x-fold)
-    st->reserved[1] = 0;  // nor a paired one (cg_x2)
-    st->x2_alpha = 0.0;
     if (nom < 0.0) {             // preconditioner not positive definite
         st->done = 1;
         st->final_iter = 0;
@@ -222,11 +219,7 @@ __device__ inline void cg_init_logic(KrylovState *st, double nom, double rel_tol
 __device__ inline void cg_update_logic(KrylovState *st, double betanom)
 {
     st->betanom = betanom;
-    st->reserved[0] = 1;  // brick CG x-fold: this iteration's x += alpha d is pending (next apply / flush)
     const int i = st->iter;
-    // cg_x2: odd iterations leave their x += alpha d to the next (even) update or the flush
-    st->reserved[1] = (unsigned)(i & 1);
-    st->x2_alpha = st->alpha;
     if (betanom < 0.0) {
         st->done = 1; st->converged = 0; st->final_iter = i;
     } else if (betanom <= st->r0) {

@@ -219,14 +219,8 @@ int cdfem_stream_bench(cdfem_ctx *ctx, int mode, size_t bytes, int reps, double 
 int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
 
 /* ---- tuning knobs (performance only; results identical to rounding) --------------------------
- * "brick_waves": 1 (default) or 2 — register budget of the structured Mult kernel (waves per SIMD;
- *                2 spills 124 B per lane and measured 11 % slower in the C2 GMRES leg).
  * "profile_mask": bit k set = kernel slot k (CDFEM_K_*) gets HIP events while profiling is on
  *                 (default all; events around every kernel cost ~1 us each on the stream).
- * "brick_variant": 0..10 — element core of the structured CG kernel (unrolled / plane loop /
- *                  low-register; 3-5 the same at 2 waves per SIMD; 6 temporal qdata loads;
- *                  7 the first qdata points issued under the patch gather; 8-10 four waves per
- *                  brick, one quadrature plane per lane, at 2 / 3 / 4 waves per SIMD, p = 2).
  * "brick_xcd": 1 (default) — XCD-contiguous brick order of the structured CG kernel; 0 = the
  *              dispatcher's round-robin order.
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
@@ -234,11 +228,8 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               0 = one launch, then the exchange (bitwise the same results).
  * "ho_mfma": 0 (default) — the LDS stages of the high-order (3D p = 3, 4) tile apply as block GEMMs on
  *            v_mfma_f64_16x16x4_f64, bit 0 = stage x, 1 = y, 2 = y^T, 3 = x^T; the masks 1, 3, 8, 9
- *            and 15 are built (results agree
- *            to rounding).
- * "cg_dfold": 0 (default) — 1 = in the fused high-order CG (cg_fused) the direction d = z + beta d
- *             is formed in the next apply's gather and written by each dof's owner element, with no
- *             direction pass (same arithmetic; measured slower at C3).
+ *            and 15 are built (results agree to rounding; the north star's MFMA alternative,
+ *            measured even to slower).
  * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).
@@ -248,21 +239,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan).  A permuted order runs the
  *               Krylov solve in that order (Mult to rounding, iterates to 1e-12).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
- * "sell_offset": 0 (default) — bytes (a multiple of 256, at most 4 MiB) by which the SpMV's
- *                constrained value stream and 16-bit delta stream start past their allocations
- *                (read at cdfem_fa_setup; a placement A/B switch, same results).
- * "spmv_xcd_sort": 0 (default) / 1 — global SpMV layout sorted by row length inside 8 contiguous
- *                  row ranges, one per XCD, instead of over the whole matrix (read when the FA
- *                  pattern is built; bitwise the same SpMV).
- * "spmv_variant": 0 (default) / 1 — SpMV inner loop (4 loads in flight / software-pipelined; A/B).
- * "diag_sf": 1 (default) — sum-factorised PA diagonal; 0 = per-entry quadrature loop.
- * "cg_x2": 0 (default) / 1 — structured CG: x is updated by every second iteration with both
- *          pending terms (x + a_{i-1} d_{i-1} + a_i d_i; an odd last iteration is flushed after the
- *          loop), bitwise the per-iteration update; not combined with cg_xfold.
- * "cg_xfold": 0 (default) / 1 — structured CG: fold x += alpha d into the next apply (bitwise the
- *             same; measured slower, A/B).
- * "mass_from_d": 0 (default) / 1 — 3D PA with constant kappa, s: derive the mass weight from the
- *                diffusion block instead of storing it (read at cdfem_pa_setup; measured slower).  */
+ * Variants measured slower and removed in round 3 (their records stay under profiles/r02_ab_*):
+ * brick element cores 1-10 and the four-waves-per-brick kernel, x-fold / paired x updates, the
+ * folded high-order direction, the derived mass weight, per-XCD SpMV sort, SpMV stream offsets and
+ * the software-pipelined SpMV loop, the two-waves-per-SIMD structured Mult.                      */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
 
 /* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */

@@ -221,16 +221,6 @@ def _gpu_overlap_worker(rank, world, port, out_dir):
         ctx.set_option("mr_overlap", ov)
         X, info = ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=60, check_every=7)
         res.append(X)
-    # the round-2 options on the slab path: paired x updates (bitwise; even and odd stops, the odd
-    # one flushed after the loop) and the four-waves-per-brick core (rounding only)
-    ctx.set_option("cg_x2", 1)
-    for it in (60, 61):
-        res.append(ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=it, check_every=7)[0])
-    ctx.set_option("cg_x2", 0)
-    res.append(ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=61, check_every=7)[0])
-    ctx.set_option("brick_variant", 8)
-    res.append(ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=60, check_every=7)[0])
-    ctx.set_option("brick_variant", 0)
     np.save(os.path.join(out_dir, f"ov{rank}.npy"), np.stack(res))
     ctx.close()
     dist.destroy_process_group()
@@ -249,9 +239,6 @@ def test_gpu_overlapped_exchange_bitwise(tmp_path, world):
         assert np.isfinite(x).all() and np.abs(x[0]).max() > 0
         np.testing.assert_array_equal(x[0], x[1])
         np.testing.assert_array_equal(x[0], x[2])
-        np.testing.assert_array_equal(x[3], x[0])                   # cg_x2, 60 iterations
-        np.testing.assert_array_equal(x[4], x[5])                   # cg_x2 vs default, 61
-        assert np.linalg.norm(x[6] - x[0]) <= 1e-12 * np.linalg.norm(x[0])   # brick_variant 8
 
 
 # ---------------------------------------------------------------------------------------------

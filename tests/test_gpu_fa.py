@@ -322,30 +322,3 @@ def test_fa_reordered_space_solves(gpu_ctx, order):
             assert np.abs(new[k] - base[k]).max() <= 1e-12 * np.abs(base[k]).max(), k
     finally:
         gpu_ctx.set_option("sell_order", 3)
-
-
-@pytest.mark.parametrize("n", [16, 9])
-def test_fa_spmv_xcd_sort_bitwise(gpu_ctx, n):
-    """set_option("spmv_xcd_sort"): the global SELL layout sorted by length inside 8 contiguous row
-    ranges (one per XCD) instead of over the whole matrix.  Every row keeps its CSR entry order, so
-    Mult, the constrained Mult and GMRES(30) iterates are bitwise the default layout's; the CG
-    (whose den partials follow the slice placement) agrees to rounding."""
-    gm = cdfem.kuhn_mesh(3, n, 2, perturb=0.1)
-    rng = np.random.default_rng(17)
-    x = rng.uniform(-1, 1, gm.nl)
-    b = rng.uniform(-1, 1, gm.nl)
-    res = {}
-    try:
-        for flag in (0, 1):
-            gpu_ctx.set_option("spmv_xcd_sort", flag)
-            gpu_ctx.upload_mesh(gm)
-            gpu_ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
-            _, B = gpu_ctx.form_linear_system(np.zeros(gm.nl), b)
-            X, _ = gpu_ctx.solve(B, method="gmres", restart=30, rel_tol=0.0, abs_tol=0.0, max_iter=40)
-            Xc, _ = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=30)
-            res[flag] = (gpu_ctx.mult(x), gpu_ctx.mult(x, constrained=True), X, Xc)
-    finally:
-        gpu_ctx.set_option("spmv_xcd_sort", 0)
-    for a, c in zip(res[1][:3], res[0][:3]):
-        np.testing.assert_array_equal(a, c)
-    assert np.linalg.norm(res[1][3] - res[0][3]) <= 1e-12 * np.linalg.norm(res[0][3])

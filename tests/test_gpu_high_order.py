@@ -268,34 +268,3 @@ def test_ho_mfma_fused_cg_parity(gpu_ctx, n, p, mf):
         gpu_ctx.set_option("ho_mfma", 0)
     assert io["iterations"] == ig["iterations"] == 50
     assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
-
-
-@pytest.mark.parametrize("shape,p", [((3, 3, 3), 4), ((4, 3, 5), 3)])
-def test_ho_cg_dfold_matches_direction_pass(gpu_ctx, shape, p):
-    """cg_dfold = 1: the fused CG forms d = z + beta d in the apply's gather (owner elements
-    write it) instead of a separate direction pass.  Same formula, so the iterates agree with the
-    direction-pass path to rounding (1e-14) and with the oracle (1e-11)."""
-    nx, ny, nz = shape
-    om = O.BoxMesh(3, (nx, ny, nz), p, perturb=0.1)
-    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(5))
-    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
-    rng = np.random.default_rng(15)
-    u = np.zeros(om.nl)
-    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
-    b = rng.uniform(-1, 1, om.nl)
-    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
-    xo, io = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
-    out = {}
-    try:
-        for df in (0, 1):
-            gpu_ctx.set_option("cg_dfold", df)
-            gpu_ctx.upload_mesh(gm).set_structured(nx, ny, nz)
-            gpu_ctx.pa_setup(kinds=5, kappa=0.1, mass=1.0)
-            _, B = gpu_ctx.form_linear_system(u, b)
-            out[df] = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=9)
-    finally:
-        gpu_ctx.set_option("cg_dfold", 0)
-    for df, (xg, ig) in out.items():
-        assert ig["iterations"] == 40
-        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), df
-    assert np.abs(out[1][0] - out[0][0]).max() <= 1e-14 * np.abs(out[0][0]).max()

@@ -218,24 +218,14 @@ def test_mms_solution_error_matches_oracle(gpu_ctx):
 
 
 def test_variable_coefficients(gpu_ctx):
-    """kappa(x), s(x), c(x) sampled at quadrature points (host Coefficient::Eval) vs constant ones
-    scaled: a constant field passed per point must equal the constant path bitwise when the
-    constant path stores the mass weight (set_option mass_from_d 0, the default), and to rounding
-    when it derives it from the diffusion block (mass_from_d 1: M = s det(D) / (W^2 kappa^3))."""
+    """kappa(x), s(x), c(x) sampled at quadrature points (host Coefficient::Eval) vs constant ones:
+    a constant field passed per point equals the constant path bitwise."""
     om, gm = _mesh_pair(3, 3, 2, 0.1)
     ctx = gpu_ctx.upload_mesh(gm)
     nq = ctx.rule_size(cdfem.RULE_OPERATOR)
     x = np.random.default_rng(2).uniform(-1, 1, om.nl)
-    try:
-        ctx.set_option("mass_from_d", 0)
-        ctx.pa_setup(kinds=7, kappa=0.3, alpha=1.0, conv=C3, mass=2.0)
-        y_const = ctx.mult(x)
-        ctx.set_option("mass_from_d", 1)
-        ctx.pa_setup(kinds=7, kappa=0.3, alpha=1.0, conv=C3, mass=2.0)
-        y_derived = ctx.mult(x)
-    finally:
-        ctx.set_option("mass_from_d", 0)
-    assert np.abs(y_derived - y_const).max() <= 1e-14 * np.abs(y_const).max()
+    ctx.pa_setup(kinds=7, kappa=0.3, alpha=1.0, conv=C3, mass=2.0)
+    y_const = ctx.mult(x)
     ctx.pa_setup(kinds=7, kappa=0.0, alpha=1.0, conv=(0, 0, 0), mass=0.0,
                  kappa_q=np.full(om.ne * nq, 0.3), conv_q=np.tile(C3, om.ne * nq),
                  mass_q=np.full(om.ne * nq, 2.0))
@@ -369,13 +359,6 @@ def test_brick_cg_parity(gpu_ctx):
     xn, inn = gpu_ctx.solve(B, method="cg", pc="none", rel_tol=1e-12, max_iter=2000)
     xon, ion = O.cg(Ac, Bo, dinv=None, rel_tol=1e-12, max_iter=2000)
     assert inn["converged"] and np.linalg.norm(xn - xon) <= 1e-10 * np.linalg.norm(xon)
-    # every element-core variant of the CG kernel gives the same iterates (to rounding)
-    x50, _ = O.cg(Ac, Bo, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=50)
-    for v in (0, 1, 2):
-        gpu_ctx.set_option("brick_variant", v)
-        xv, iv = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=50)
-        assert np.linalg.norm(xv - x50) <= 1e-11 * np.linalg.norm(x50), v
-    gpu_ctx.set_option("brick_variant", 0)
 
 
 @pytest.mark.parametrize("n,p", [(8, 2), (9, 1)])
@@ -399,35 +382,6 @@ def test_brick_cg_bench_operator_parity(gpu_ctx, n, p):
     assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
     xg2, _ = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30)
     np.testing.assert_array_equal(xg, xg2)
-
-
-@pytest.mark.parametrize("max_iter,rel_tol,check", [(30, 0.0, 16), (31, 0.0, 7), (2000, 1e-10, 16), (1, 0.0, 16),
-                                                     (0, 0.0, 16)])
-def test_brick_cg_xfold_bitwise(gpu_ctx, max_iter, rel_tol, check):
-    """set_option("cg_xfold"): iteration k's x += alpha_k d_k moves into apply k + 1 and the last one
-    into the flush after the loop.  Same arithmetic on the same operands: the solution is bitwise
-    the unfolded one, whether the loop stops at max_iter (even / odd counts), on convergence, or
-    before the first update (max_iter 0 / 1); with essential values set (d on ess rows)."""
-    n, p = 8, 2
-    om = O.BoxMesh(3, n, p, perturb=0.1)
-    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
-    gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
-    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
-    rng = np.random.default_rng(77)
-    u = np.zeros(om.nl)
-    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
-    _, B = gpu_ctx.form_linear_system(u, rng.uniform(-1, 1, om.nl))
-    out = {}
-    try:
-        for fold in (0, 1):
-            gpu_ctx.set_option("cg_xfold", fold)
-            out[fold] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=rel_tol, abs_tol=0.0,
-                                      max_iter=max_iter, check_every=check)
-    finally:
-        gpu_ctx.set_option("cg_xfold", 0)
-    (x0, i0), (x1, i1) = out[0], out[1]
-    assert i0["iterations"] == i1["iterations"] and i0["converged"] == i1["converged"]
-    np.testing.assert_array_equal(x1, x0)
 
 
 def test_brick_full_size_matches_generic(gpu_ctx):
@@ -479,11 +433,9 @@ def test_config_c1_reference_case(gpu_ctx):
 
 
 @pytest.mark.parametrize("shape,kinds", [((8, 8, 8), 7), ((8, 8, 8), 5), ((9, 6, 7), 7), ((4, 4, 12), 1)])
-def test_brick_cg4_parity(gpu_ctx, shape, kinds):
-    """brick_variant 8 (k_brick_cg4: four waves per brick, one quadrature plane per lane, butterfly
-    plane sum, parity-class E->L) and 7 (qdata issued under the patch gather): fixed Jacobi-CG
-    iterates with essential values against the oracle (1e-11) and against variant 0 (1e-12), on
-    cubes, partial bricks and every kinds mask it serves; bitwise repeatable."""
+def test_brick_cg_partial_bricks_parity(gpu_ctx, shape, kinds):
+    """The brick CG kernel on cubes and on boxes with partial bricks, for several kinds masks: fixed
+    Jacobi-CG iterates with essential values against the oracle (1e-11); bitwise repeatable."""
     nx, ny, nz = shape
     p = 2
     om = O.BoxMesh(3, shape, p, perturb=0.1)
@@ -499,46 +451,8 @@ def test_brick_cg4_parity(gpu_ctx, shape, kinds):
     Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
     _, B = gpu_ctx.form_linear_system(u, b)
     xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
-    out = {}
-    try:
-        for v in (0, 7, 8, 9, 10):
-            gpu_ctx.set_option("brick_variant", v)
-            out[v] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40,
-                                   check_every=11)
-        x8b, _ = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=11)
-    finally:
-        gpu_ctx.set_option("brick_variant", 0)
-    for v, (xg, ig) in out.items():
-        assert ig["iterations"] == 40, v
-        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), v
-        assert np.linalg.norm(xg - out[0][0]) <= 1e-12 * np.linalg.norm(xo), v
-    np.testing.assert_array_equal(x8b, out[8][0])
-
-
-@pytest.mark.parametrize("max_iter,rel_tol,check", [(30, 0.0, 16), (31, 0.0, 7), (2000, 1e-10, 16), (2000, 1e-9, 5),
-                                                     (1, 0.0, 16), (2, 0.0, 16), (0, 0.0, 16)])
-def test_brick_cg_x2_bitwise(gpu_ctx, max_iter, rel_tol, check):
-    """set_option("cg_x2"): odd iterations leave x alone, even ones add both pending terms
-    (x + a_{i-1} d_{i-1} + a_i d_i, in that order), and an odd last iteration is flushed after the
-    loop.  The same adds in the same order: bitwise the per-iteration update, for even and odd
-    stopping points, on convergence and before the first update; with essential values set."""
-    n, p = 8, 2
-    om = O.BoxMesh(3, n, p, perturb=0.1)
-    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
-    gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
-    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
-    rng = np.random.default_rng(78)
-    u = np.zeros(om.nl)
-    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
-    _, B = gpu_ctx.form_linear_system(u, rng.uniform(-1, 1, om.nl))
-    out = {}
-    try:
-        for x2 in (0, 1):
-            gpu_ctx.set_option("cg_x2", x2)
-            out[x2] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=rel_tol, abs_tol=0.0,
-                                    max_iter=max_iter, check_every=check)
-    finally:
-        gpu_ctx.set_option("cg_x2", 0)
-    (x0, i0), (x1, i1) = out[0], out[1]
-    assert i0["iterations"] == i1["iterations"] and i0["converged"] == i1["converged"]
-    np.testing.assert_array_equal(x1, x0)
+    xg, ig = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=11)
+    x2, _ = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=11)
+    assert ig["iterations"] == 40
+    assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
+    np.testing.assert_array_equal(x2, xg)
