@@ -28,6 +28,7 @@ namespace cdfem {
 
 constexpr int kGmEPT = 4;                         // L-vector entries per thread in the pass kernels
 constexpr int kGmBatch = 2;                       // projections per load batch in pass 1
+constexpr int kGmBatch2 = 4;                      // basis vectors per load batch in pass 2
 constexpr int kGmChunk = kRedThreads * kGmEPT;    // entries per block
 
 int gmres_blocks(int64_t n) { return (int)((n + kGmChunk - 1) / kGmChunk); }
@@ -227,28 +228,46 @@ k_gm_dots_fin_mb(const double *__restrict__ part, int nb, GmresState *__restrict
 }
 
 // ---- pass 2: V_{j+1} = w - sum_i H[i][j] s_i V_i, partials of |V_{j+1}|^2 ------------------------
+// Pass 1's treatment: the coefficients H[i][j] s_i are staged once per block in LDS (one global
+// load per i per block instead of one per i per wave), and the basis vectors are read BAT at a time
+// with every load unconditional (entry indices clamped to n - 1, basis indices clamped to j with a
+// zero coefficient), so BAT * kGmEPT loads per lane are in flight before the first FMA.  The
+// subtractions keep the ascending-i order of the one-at-a-time loop (bitwise the same V_{j+1}).
+template <int BAT>
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int64_t ldv, int64_t skip_lo,
            double *__restrict__ part, const GmresState *__restrict__ st)
 {
     __shared__ double sh[kRedThreads / 64];
+    __shared__ double coef[kGmMaxRestart + BAT];
     if (st->cycle_done) return;
     const int j = st->j;
+    for (int i = threadIdx.x; i < kGmMaxRestart + BAT; i += blockDim.x)
+        coef[i] = i <= j ? st->H[i * kGmMaxRestart + j] * st->s[i] : 0.0;
     const int64_t base = (int64_t)blockIdx.x * kGmChunk + threadIdx.x;
+    int64_t kc[kGmEPT];
     double acc[kGmEPT];
 #pragma unroll
     for (int e = 0; e < kGmEPT; ++e) {
         const int64_t k = base + (int64_t)e * kRedThreads;
-        acc[e] = k < n ? w[k] : 0.0;
+        kc[e] = k < n ? k : n - 1;
+        acc[e] = w[kc[e]];
     }
-#pragma unroll 4
-    for (int i = 0; i <= j; ++i) {
-        const double coef = st->H[i * kGmMaxRestart + j] * st->s[i];
-        const double *vi = V + (int64_t)i * ldv;
+    __syncthreads();
+#pragma unroll 1
+    for (int i0 = 0; i0 <= j; i0 += BAT) {
+        double vv[BAT][kGmEPT];
 #pragma unroll
-        for (int e = 0; e < kGmEPT; ++e) {
-            const int64_t k = base + (int64_t)e * kRedThreads;
-            if (k < n) acc[e] -= coef * vi[k];
+        for (int b = 0; b < BAT; ++b) {
+            const double *vi = V + (int64_t)(i0 + b <= j ? i0 + b : j) * ldv;
+#pragma unroll
+            for (int e = 0; e < kGmEPT; ++e) vv[b][e] = vi[kc[e]];
+        }
+#pragma unroll
+        for (int b = 0; b < BAT; ++b) {
+            const double cb = coef[i0 + b];  // 0 past j
+#pragma unroll
+            for (int e = 0; e < kGmEPT; ++e) acc[e] -= cb * vv[b][e];
         }
     }
     double *vn = V + (int64_t)(j + 1) * ldv;
@@ -464,7 +483,7 @@ hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V
         comm_allreduce(c, red_of(st), m + 1);
         hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2);
     }
-    hipLaunchKernelGGL(k_gm_pass2, dim3(nb), dim3(kRedThreads), 0, c->stream, w, V, n, ldv, owned_from(c), part, st);
+    hipLaunchKernelGGL((k_gm_pass2<kGmBatch2>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, V, n, ldv, owned_from(c), part, st);
     hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, mr ? 1 : 0,
                        mr ? nullptr : poll);
     if (mr) {
