@@ -135,6 +135,60 @@ def host_cores(args):
 CPU_SAMPLES = 5  # median of >= 5 timed samples after one warm-up
 
 
+def pick_cpus(n):
+    """n CPUs of this job's affinity mask for the CPU baseline: distinct physical cores of one
+    package (the package of the lowest allowed CPU first), so the threads neither share a core nor
+    straddle sockets.  Falls back to the lowest allowed CPUs when sysfs topology is unreadable."""
+    allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+
+    def topo(c, f):
+        try:
+            return int(open(f"/sys/devices/system/cpu/cpu{c}/topology/{f}").read())
+        except (OSError, ValueError):
+            return None
+    pkg0 = topo(allowed[0], "physical_package_id")
+    seen, out = set(), []
+    for pass_pkg in (True, False):
+        for c in allowed:
+            core = (topo(c, "physical_package_id"), topo(c, "core_id"))
+            if core in seen or (pass_pkg and core[0] != pkg0):
+                continue
+            seen.add(core)
+            out.append(c)
+            if len(out) == n:
+                return out
+    for c in allowed:  # fewer physical cores than threads: SMT siblings too
+        if c not in out:
+            out.append(c)
+        if len(out) == n:
+            break
+    return out
+
+
+class PinnedThreads:
+    """Pin the oracle's OpenMP threads to pick_cpus(n) for the CPU baseline (timing stability on
+    a shared host: the r02 unpinned samples varied 1.8x between runs) and restore the calling
+    thread's affinity afterwards (the GPU runtime's threads keep theirs)."""
+
+    def __init__(self, O, n):
+        self.O, self.n = O, n
+
+    def __enter__(self):
+        self.saved = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+        self.cpus = pick_cpus(self.n)
+        self.pinned = self.O.pin_threads(self.cpus)
+        return self
+
+    def __exit__(self, *exc):
+        if self.saved is not None:
+            os.sched_setaffinity(0, self.saved)
+        return False
+
+    def record(self):
+        return {"pinned_cpus": f"{len(self.cpus)} cores: {self.cpus[0]}..{self.cpus[-1]}",
+                "threads_pinned": self.pinned}
+
+
 def cpu_samples(run, dofs, seconds, max_it, min_it=10, calib_it=5):
     """Time an oracle solver leg: calibrate on calib_it iterations, one untimed warm-up sample, then
     CPU_SAMPLES timed samples of about seconds / CPU_SAMPLES each.  run(k) runs k iterations and
@@ -170,6 +224,13 @@ def cpu_baseline(args, n, p, kinds):
     from oracle import oracle as O
     threads, host = host_cores(args)
     O.set_threads(threads)
+    with PinnedThreads(O, threads) as pin:
+        out = _cpu_baseline_box(args, O, n, p, kinds, threads, host)
+    out.update(pin.record())
+    return out
+
+
+def _cpu_baseline_box(args, O, n, p, kinds, threads, host):
     if p >= 3:
         n = min(n, 12)
     m = O.BoxMesh(3, n, p)
@@ -209,6 +270,13 @@ def cpu_baseline_c4(args, n, p):
     from oracle import oracle as O
     threads, host = host_cores(args)
     O.set_threads(threads)
+    with PinnedThreads(O, threads) as pin:
+        out = _cpu_baseline_kuhn(args, O, n, p, threads, host)
+    out.update(pin.record())
+    return out
+
+
+def _cpu_baseline_kuhn(args, O, n, p, threads, host):
     m = O.KuhnMesh(3, n, p)
     t0 = time.perf_counter()
     A = O.fa_assemble_simplex(m, kappa=0.1, alpha=1.0, s=1.0, c=(1.0, -2.0, 0.5))

@@ -1467,6 +1467,10 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 5)
                 throw ArgError("sell_order must be 0..5 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric)");
             c->sell_mode = value;
+        } else if (k == "gm_ept") {
+            if (value != 0 && value != 4 && value != 5 && value != 6 && value != 8)
+                throw ArgError("gm_ept must be 0 (auto), 4, 5, 6 or 8");
+            c->gm_ept = value;
         } else if (k == "spmv_xcd") {
             if (value < 0 || value > 1) throw ArgError("spmv_xcd must be 0 or 1");
             c->spmv_xcd = value;

@@ -153,6 +153,9 @@ struct cdfem_ctx {
     double *d_ones = nullptr;           // all-ones vector (unpreconditioned brick CG)
     double *d_dalt = nullptr;           // second search-direction buffer (brick CG)
     int nface = 0;                      // F
+    int gm_ept = 0;                     // set_option "gm_ept": GMRES orthogonalisation entries per thread (0: auto, orth_ept)
+    int gm_ept_auto = 4;                // the automatic choice for vectors of gm_ept_n entries
+    int64_t gm_ept_n = -1;
     int brick_xcd = 1;                  // k_brick_cg brick order: 0 dispatch, 1 XCD-contiguous (default)
     int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)
     int zhi_shared = 0;                 // local gz=Lz-1 plane shared with the rank above

@@ -116,7 +116,7 @@ k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st,
 // dropped).  Each wave parks its wave sums in LDS, so the whole step needs ONE barrier before the
 // block sums.  Measured at C4 (orthogonalisation per step): one barrier per batch of 8, 93.9 us;
 // one barrier in all, batches of 8 / 4 / 2 / 1: 85.7 / 83.2 / 82.6 / 82.1 us.
-template <int BAT>
+template <int BAT, int EPT>
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double *__restrict__ V, int64_t n,
            int64_t ldv, int64_t skip_lo, double *__restrict__ part, int nb, const GmresState *__restrict__ st)
@@ -125,11 +125,11 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
     if (st->cycle_done) return;
     const int j = st->j;
     const double sj = st->s[j];
-    const int64_t base = (int64_t)blockIdx.x * kGmChunk + threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * (kRedThreads * EPT) + threadIdx.x;
     const int lane = threadIdx.x & 63, wv_id = threadIdx.x >> 6;
-    double wv[kGmEPT];
+    double wv[EPT];
 #pragma unroll
-    for (int e = 0; e < kGmEPT; ++e) {
+    for (int e = 0; e < EPT; ++e) {
         const int64_t k = base + (int64_t)e * kRedThreads;
         double v = 0.0;
         if (k < n) {
@@ -141,12 +141,12 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
     }
 #pragma unroll 1
     for (int i0 = 0; i0 <= j; i0 += BAT) {
-        double vv[BAT][kGmEPT];
+        double vv[BAT][EPT];
 #pragma unroll
         for (int b = 0; b < BAT; ++b) {
             const double *vi = V + (int64_t)(i0 + b <= j ? i0 + b : j) * ldv;
 #pragma unroll
-            for (int e = 0; e < kGmEPT; ++e) {
+            for (int e = 0; e < EPT; ++e) {
                 const int64_t k = base + (int64_t)e * kRedThreads;
                 vv[b][e] = k < n ? vi[k] : 0.0;
             }
@@ -155,7 +155,7 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
         for (int b = 0; b < BAT; ++b) {
             double a = 0.0;
 #pragma unroll
-            for (int e = 0; e < kGmEPT; ++e) a += wv[e] * vv[b][e];
+            for (int e = 0; e < EPT; ++e) a += wv[e] * vv[b][e];
             const double t = wave_sum(a);
             if (lane == 0 && i0 + b <= j) sh[i0 + b][wv_id] = t;
         }
@@ -233,7 +233,7 @@ k_gm_dots_fin_mb(const double *__restrict__ part, int nb, GmresState *__restrict
 // with every load unconditional (entry indices clamped to n - 1, basis indices clamped to j with a
 // zero coefficient), so BAT * kGmEPT loads per lane are in flight before the first FMA.  The
 // subtractions keep the ascending-i order of the one-at-a-time loop (bitwise the same V_{j+1}).
-template <int BAT>
+template <int BAT, int EPT>
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int64_t ldv, int64_t skip_lo,
            double *__restrict__ part, const GmresState *__restrict__ st)
@@ -244,11 +244,11 @@ k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int6
     const int j = st->j;
     for (int i = threadIdx.x; i < kGmMaxRestart + BAT; i += blockDim.x)
         coef[i] = i <= j ? st->H[i * kGmMaxRestart + j] * st->s[i] : 0.0;
-    const int64_t base = (int64_t)blockIdx.x * kGmChunk + threadIdx.x;
-    int64_t kc[kGmEPT];
-    double acc[kGmEPT];
+    const int64_t base = (int64_t)blockIdx.x * (kRedThreads * EPT) + threadIdx.x;
+    int64_t kc[EPT];
+    double acc[EPT];
 #pragma unroll
-    for (int e = 0; e < kGmEPT; ++e) {
+    for (int e = 0; e < EPT; ++e) {
         const int64_t k = base + (int64_t)e * kRedThreads;
         kc[e] = k < n ? k : n - 1;
         acc[e] = w[kc[e]];
@@ -256,24 +256,24 @@ k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int6
     __syncthreads();
 #pragma unroll 1
     for (int i0 = 0; i0 <= j; i0 += BAT) {
-        double vv[BAT][kGmEPT];
+        double vv[BAT][EPT];
 #pragma unroll
         for (int b = 0; b < BAT; ++b) {
             const double *vi = V + (int64_t)(i0 + b <= j ? i0 + b : j) * ldv;
 #pragma unroll
-            for (int e = 0; e < kGmEPT; ++e) vv[b][e] = vi[kc[e]];
+            for (int e = 0; e < EPT; ++e) vv[b][e] = vi[kc[e]];
         }
 #pragma unroll
         for (int b = 0; b < BAT; ++b) {
             const double cb = coef[i0 + b];  // 0 past j
 #pragma unroll
-            for (int e = 0; e < kGmEPT; ++e) acc[e] -= cb * vv[b][e];
+            for (int e = 0; e < EPT; ++e) acc[e] -= cb * vv[b][e];
         }
     }
     double *vn = V + (int64_t)(j + 1) * ldv;
     double nrm = 0.0;
 #pragma unroll
-    for (int e = 0; e < kGmEPT; ++e) {
+    for (int e = 0; e < EPT; ++e) {
         const int64_t k = base + (int64_t)e * kRedThreads;
         if (k < n) {
             vn[k] = acc[e];
@@ -470,25 +470,61 @@ hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, c
     return hipGetLastError();
 }
 
-hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m, GmresState *poll)
+// Entries per thread of the two orthogonalisation passes: the smallest of 4, 5, 6, 8 whose grid is
+// resident in one round (blocks <= CUs x resident blocks per CU), so no tail of a few blocks runs
+// a second round alone (C2: 2097 blocks of 1024 entries against 2048 resident slots at EPT 4).
+static int orth_ept(cdfem_ctx *c)
 {
-    const int nb = gmres_blocks(c->nl);
+    if (c->gm_ept) return c->gm_ept;                  // set_option("gm_ept")
+    if (c->gm_ept_n == c->nl) return c->gm_ept_auto;  // chosen for this size already
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gm_pass1<kGmBatch, 4>, kRedThreads, 0);
+    const int64_t cap = (int64_t)std::max(cus, 1) * std::max(per, 1);
+    int ept = 8;
+    for (int e : {4, 5, 6, 8})
+        if ((c->nl + (int64_t)kRedThreads * e - 1) / ((int64_t)kRedThreads * e) <= cap) {
+            ept = e;
+            break;
+        }
+    c->gm_ept_auto = ept;
+    c->gm_ept_n = c->nl;
+    return ept;
+}
+
+template <int EPT>
+static void orth_passes(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
+                        GmresState *st, int m, GmresState *poll)
+{
+    const int nb = (int)((c->nl + (int64_t)kRedThreads * EPT - 1) / ((int64_t)kRedThreads * EPT));
     const int64_t n = c->nl;
     const bool mr = multi_rank(c);
-    hipLaunchKernelGGL((k_gm_pass1<kGmBatch>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv,
+    hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv,
                        owned_from(c), part, nb, st);
     hipLaunchKernelGGL(k_gm_dots_fin_mb, dim3(m + 1), dim3(kRedThreads), 0, c->stream, part, nb, st, mr ? 1 : 0);
     if (mr) {
         comm_allreduce(c, red_of(st), m + 1);
         hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2);
     }
-    hipLaunchKernelGGL((k_gm_pass2<kGmBatch2>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, V, n, ldv, owned_from(c), part, st);
+    hipLaunchKernelGGL((k_gm_pass2<kGmBatch2, EPT>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, V, n, ldv,
+                       owned_from(c), part, st);
     hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, mr ? 1 : 0,
                        mr ? nullptr : poll);
     if (mr) {
         comm_allreduce(c, red_of(st), 1);
         hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2, poll);
+    }
+}
+
+hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
+                          GmresState *st, int m, GmresState *poll)
+{
+    switch (orth_ept(c)) {
+    case 5: orth_passes<5>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    case 6: orth_passes<6>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    case 8: orth_passes<8>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    default: orth_passes<4>(c, w, dinv, V, ldv, part, st, m, poll); break;
     }
     return hipGetLastError();
 }

@@ -518,6 +518,126 @@ k_diag_sf(const double *__restrict__ qd, const int32_t *__restrict__ perm, int n
     for (int i3 = 0; i3 < D1; ++i3) out(i3, acc[i3]);
 }
 
+// PA diagonal on the element-major high-order layout (3D, qlay 1: p = 3, 4), sum-factorised in three
+// stages with LDS between them, so every qdata value is read from HBM exactly once, by one thread:
+//   1. thread (e, qx, qy) loads its point column (all qz, all components: the tile apply's 16-byte
+//      loads) and contracts z: A_g(qx, qy, dz) = sum_{t in g} mult_t sum_qz F_z^t(qz, dz) qd_t(q);
+//      terms are grouped by their (x, y) factor types g = (tx, ty) (at most 6 groups for D+C+M)
+//   2. per group, through LDS, thread (e, qx, dz) contracts y into S_tx(qx, dy, dz)
+//   3. thread (e, dy, dz) contracts x: diag(dx, dy, dz) = sum_tx sum_qx F_x^tx(qx, dx) S_tx.
+// Term list, sizes and factor types are compile-time (DiagTerms); ~4 KB of LDS per element.
+template <unsigned K>
+__host__ __device__ constexpr bool diag_slot_used(int slot)
+{
+    for (int t = 0; t < DiagTerms<3, K>::n; ++t)
+        if (3 * DiagTerms<3, K>::type(t, 0) + DiagTerms<3, K>::type(t, 1) == slot) return true;
+    return false;
+}
+
+template <int D1, int Q1, unsigned K>
+__global__ void __launch_bounds__(256)
+k_diag_ho(const double *__restrict__ qd, int ne, const HoLayout ho, const Tab<D1, Q1> T, double *__restrict__ Ye)
+{
+    using TT = DiagTerms<3, K>;
+    constexpr int NC = QLayout<K, 3>::nc, NP = NC / 2, QQ = Q1 * Q1;
+    constexpr int PS = qd_ho_plane(NC, Q1);
+    constexpr int EPB = 256 / QQ;
+    __shared__ double sA[EPB][D1][QQ];            // one group's z-contracted column sums
+    __shared__ double sS[3][EPB][D1][D1][Q1];     // y-contracted sums per x factor type
+    const int tid = threadIdx.x;
+    // ---- stage 1: thread (le, qx + Q1 qy)
+    const int le1 = tid / QQ, t1 = tid - le1 * QQ;
+    const int e1 = blockIdx.x * EPB + le1;
+    const bool v1 = le1 < EPB && e1 < ne;
+    double qv[Q1][NC];
+    {
+        const double *qe = qd + (size_t)(v1 ? e1 : ne - 1) * Q1 * PS;
+        const int tc = v1 ? t1 : 0;
+#pragma unroll
+        for (int qz = 0; qz < Q1; ++qz) {
+            const double *qp = qe + qz * PS;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const v2d_t w = __builtin_nontemporal_load(reinterpret_cast<const v2d_t *>(qp + p * 2 * QQ) + tc);
+                qv[qz][2 * p] = w.x;
+                qv[qz][2 * p + 1] = w.y;
+            }
+            if constexpr (NC & 1) qv[qz][NC - 1] = __builtin_nontemporal_load(qp + 2 * NP * QQ + tc);
+        }
+    }
+    double A[9][D1];
+#pragma unroll
+    for (int g = 0; g < 9; ++g)
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) A[g][dz] = 0.0;
+#pragma unroll
+    for (int t = 0; t < TT::n; ++t) {
+        const int g = 3 * TT::type(t, 0) + TT::type(t, 1), tz = TT::type(t, 2);
+#pragma unroll
+        for (int qz = 0; qz < Q1; ++qz) {
+            const double v = TT::mult(t) * qv[qz][TT::comp(t)];
+#pragma unroll
+            for (int dz = 0; dz < D1; ++dz) A[g][dz] += diag_factor(T, tz, qz, dz) * v;
+        }
+    }
+    // ---- stage 2, group by group: thread (le, qx, dz)
+    const int le2 = tid / (Q1 * D1), r2 = tid - le2 * (Q1 * D1);
+    const int qx2 = r2 % Q1, dz2 = r2 / Q1;
+    const bool v2 = le2 < EPB;
+    double S[3][D1];
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy) S[x][dy] = 0.0;
+#pragma unroll
+    for (int g = 0; g < 9; ++g) {
+        if (!diag_slot_used<K>(g)) continue;  // compile-time after unrolling
+        if (le1 < EPB)
+#pragma unroll
+            for (int dz = 0; dz < D1; ++dz) sA[le1][dz][t1] = A[g][dz];
+        __syncthreads();
+        if (v2) {
+            const int tx = g / 3, ty = g % 3;
+#pragma unroll
+            for (int qy = 0; qy < Q1; ++qy) {
+                const double a = sA[le2][dz2][qx2 + Q1 * qy];
+#pragma unroll
+                for (int dy = 0; dy < D1; ++dy) S[tx][dy] += diag_factor(T, ty, qy, dy) * a;
+            }
+        }
+        __syncthreads();
+    }
+    if (v2)
+#pragma unroll
+        for (int x = 0; x < 3; ++x)
+#pragma unroll
+            for (int dy = 0; dy < D1; ++dy) sS[x][le2][dz2][dy][qx2] = S[x][dy];
+    __syncthreads();
+    // ---- stage 3: thread (le, dy, dz)
+    const int le3 = tid / (D1 * D1), r3 = tid - le3 * (D1 * D1);
+    const int dy3 = r3 % D1, dz3 = r3 / D1;
+    const int e3 = blockIdx.x * EPB + le3;
+    if (le3 >= EPB || e3 >= ne) return;
+    double out[D1];
+#pragma unroll
+    for (int dx = 0; dx < D1; ++dx) out[dx] = 0.0;
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+        bool used = false;
+#pragma unroll
+        for (int y = 0; y < 3; ++y) used = used || diag_slot_used<K>(3 * x + y);
+        if (!used) continue;
+#pragma unroll
+        for (int qx = 0; qx < Q1; ++qx) {
+            const double sv = sS[x][le3][dz3][dy3][qx];
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) out[dx] += diag_factor(T, x, qx, dx) * sv;
+        }
+    }
+#pragma unroll
+    for (int dx = 0; dx < D1; ++dx) Ye[ho_eidx(ho, (uint32_t)e3, dx + D1 * (dy3 + D1 * dz3))] = out[dx];
+}
+
 // linear form, element part: be_l = sum_q W detJ f_q phi_l; thread per (block, l, lane)
 template <int DIM>
 __global__ void __launch_bounds__(256)
@@ -590,6 +710,27 @@ hipError_t launch_quad_points(cdfem_ctx *c, const Rule1D &r, double *xyz)
     return hipGetLastError();
 }
 
+template <int D1, int Q1>
+static bool diag_ho_kinds(cdfem_ctx *c, double *Ye)
+{
+    constexpr int EPB = 256 / (Q1 * Q1);
+    const dim3 g((unsigned)((c->ne + EPB - 1) / EPB)), bs(256);
+    const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
+#define CDFEM_DHO(K_)                                                                                    \
+    hipLaunchKernelGGL((k_diag_ho<D1, Q1, K_>), g, bs, 0, c->stream, c->d_qd, c->ne, ho_layout(c), T, Ye)
+    switch (c->kinds) {
+    case 1: CDFEM_DHO(1); return true;
+    case 2: CDFEM_DHO(2); return true;
+    case 3: CDFEM_DHO(3); return true;
+    case 4: CDFEM_DHO(4); return true;
+    case 5: CDFEM_DHO(5); return true;
+    case 6: CDFEM_DHO(6); return true;
+    case 7: CDFEM_DHO(7); return true;
+    default: return false;
+    }
+#undef CDFEM_DHO
+}
+
 template <int DIM, int D1, int Q1>
 static bool diag_sf_kinds(cdfem_ctx *c, double *Ye)
 {
@@ -621,8 +762,8 @@ hipError_t launch_diag_elem(cdfem_ctx *c, double *Ye)
         if (c->dim == 3) {
             if (d1 == 2) done = diag_sf_kinds<3, 2, 3>(c, Ye);
             else if (d1 == 3) done = diag_sf_kinds<3, 3, 4>(c, Ye);
-            else if (d1 == 4) done = diag_sf_kinds<3, 4, 5>(c, Ye);
-            else if (d1 == 5) done = diag_sf_kinds<3, 5, 6>(c, Ye);
+            else if (d1 == 4) done = c->qlay == 1 ? diag_ho_kinds<4, 5>(c, Ye) : diag_sf_kinds<3, 4, 5>(c, Ye);
+            else if (d1 == 5) done = c->qlay == 1 ? diag_ho_kinds<5, 6>(c, Ye) : diag_sf_kinds<3, 5, 6>(c, Ye);
         } else {
             if (d1 == 2) done = diag_sf_kinds<2, 2, 3>(c, Ye);
             else if (d1 == 3) done = diag_sf_kinds<2, 3, 4>(c, Ye);

@@ -239,6 +239,8 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan).  A permuted order runs the
  *               Krylov solve in that order (Mult to rounding, iterates to 1e-12).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
+ * "gm_ept": 0 (default, auto) — entries per thread of the GMRES orthogonalisation passes (4, 5, 6
+ *           or 8); auto takes the smallest whose grid is resident in one round (same results).
  * Variants measured slower and removed in round 3 (their records stay under profiles/r02_ab_*):
  * brick element cores 1-10 and the four-waves-per-brick kernel, x-fold / paired x updates, the
  * folded high-order direction, the derived mass weight, per-XCD SpMV sort, SpMV stream offsets and

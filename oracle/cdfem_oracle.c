@@ -41,6 +41,8 @@
  * algebraic identities (mass = volume, K*1 = 0, C*1 = 0, symmetry).  Bit-level parity with an
  * actual MFEM run is UNPINNED (no MFEM in this image).
  */
+#define _GNU_SOURCE
+#include <sched.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -1129,6 +1131,29 @@ ORC_API void orc_set_num_threads(int n)
     if (n > 0) omp_set_num_threads(n);
 #else
     (void)n;
+#endif
+}
+
+/* Pin the n OpenMP threads of the next parallel regions: thread t runs on cpus[t] only (the CPU
+ * baseline's timing stability on a shared host; the calling thread is pinned too, and the caller
+ * restores its own mask afterwards).  Returns the number of threads pinned. */
+ORC_API int orc_pin_threads(const int *cpus, int n)
+{
+#ifdef _OPENMP
+    int pinned = 0;
+    omp_set_num_threads(n);
+    #pragma omp parallel num_threads(n) reduction(+ : pinned)
+    {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(cpus[omp_get_thread_num()], &set);
+        pinned += sched_setaffinity(0, sizeof set, &set) == 0;
+    }
+    return pinned;
+#else
+    (void)cpus;
+    (void)n;
+    return 0;
 #endif
 }
 

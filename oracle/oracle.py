@@ -94,6 +94,8 @@ def lib():
         L.orc_dof_coords_simplex.argtypes = [C.c_int, C.c_int, C.c_int, dp, ip, dp]
         L.orc_num_threads.restype = C.c_int
         L.orc_set_num_threads.argtypes = [C.c_int]
+        L.orc_pin_threads.argtypes = [C.POINTER(C.c_int), C.c_int]
+        L.orc_pin_threads.restype = C.c_int
         _lib = L
     return _lib
 
@@ -481,6 +483,12 @@ def solve_mms(mesh: BoxMesh, prm, kappa, s, c, alpha=1.0, solver="gmres", tol=1e
 
 def set_threads(n):
     lib().orc_set_num_threads(int(n))
+
+
+def pin_threads(cpus):
+    """Pin OpenMP thread t to cpus[t] (and the calling thread to cpus[0]); returns threads pinned."""
+    a = np.ascontiguousarray(cpus, dtype=np.int32)
+    return lib().orc_pin_threads(a.ctypes.data_as(C.POINTER(C.c_int)), len(a))
 
 
 def num_threads():

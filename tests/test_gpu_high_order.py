@@ -52,6 +52,21 @@ def test_ho_diagonal_and_lf(gpu_ctx, n, p):
     assert np.abs(b - bo).max() <= 1e-12 * np.abs(bo).max()
 
 
+@pytest.mark.parametrize("n,p,pert,structured", [(2, 3, 0.1, False), (3, 4, 0.1, False), (3, 3, 0.0, True),
+                                                 (4, 4, 0.0, True)])
+@pytest.mark.parametrize("kinds", [1, 2, 3, 4, 5, 6, 7])
+def test_ho_diagonal_every_kinds(gpu_ctx, n, p, pert, structured, kinds):
+    """The staged sum-factorised diagonal (k_diag_ho: z contraction per point column, y and x through
+    LDS; compile-time term groups per kinds mask) against the oracle's assembled diagonal, 1e-13,
+    for every integrator combination, generic and structured (pencil E-vector) layouts."""
+    om, A = _pair(gpu_ctx, n, p, pert, kinds)
+    if structured:
+        gpu_ctx.set_structured(n, n, n)
+        gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    d, do = gpu_ctx.diagonal(), A.diag()
+    assert np.abs(d - do).max() <= 1e-13 * np.abs(do).max()
+
+
 @pytest.mark.parametrize("n,p", [(3, 3), (4, 4)])
 def test_ho_structured_e2l_bitwise(gpu_ctx, n, p):
     """cdfem_mesh_set_structured at p >= 3 switches to the lattice E->L (k_e2l_box): same sums,

@@ -21,7 +21,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--iters", type=int, default=60)
 ap.add_argument("--n", type=int, default=64)
-ap.add_argument("--variants", default="brick_waves=1,brick_waves=2")
+ap.add_argument("--variants", default="gm_ept=4,gm_ept=5")
 args = ap.parse_args()
 
 n = args.n
