@@ -418,8 +418,9 @@ def main():
     if world > 1:
         if args.comm == "rccl":
             # RCCL communicator over xGMI; the id travels over the gloo control group.  Every rank
-            # reports whether its init succeeded; if any failed, all ranks fall back to the
-            # host-callback communicator (same results, slower exchange) and the JSON line says so
+            # reports whether its init succeeded; if any failed, every rank exits non-zero: a
+            # scaling number is never measured on a silent host fallback (the host-callback
+            # communicator is opt-in, --comm host, for rehearsals with several ranks on one GPU)
             obj = [cdfem.comm_unique_id() if rank == 0 else None]
             pg.broadcast_object_list(obj, src=0)
             err = None
@@ -428,14 +429,23 @@ def main():
             except cdfem.CdfemError as e:
                 err = str(e)
             if allmax(pg, 1.0 if err else 0.0) > 0.0:
-                print(f"rank {rank}: RCCL communicator unavailable ({err or 'failed on another rank'}); "
-                      "falling back to host callbacks", file=sys.stderr, flush=True)
-                ctx.comm_init_torch()
-                args.comm = "host (RCCL init failed)"
+                print(f"rank {rank}: RCCL communicator unavailable ({err or 'failed on another rank'}) on "
+                      f"device {local % ndev} of {ndev}; refusing to run the N>1 bench on the host "
+                      "fallback (use --comm host to rehearse with several ranks on one GPU)",
+                      file=sys.stderr, flush=True)
+                ctx.close()
+                pg.destroy_process_group()
+                raise SystemExit(3)
         else:
             ctx.comm_init_torch()
         ctx.set_slab(rank > 0, rank < world - 1)
     comm_lib = cdfem.comm_info(ctx)
+    comm_ranks = None
+    if world > 1:
+        # per rank: its device and the communicator library it bound (gathered to rank 0)
+        mine = {"rank": rank, "device": local % ndev, "comm": comm_lib}
+        comm_ranks = [None] * world
+        pg.all_gather_object(comm_ranks, mine)
     c = (1.0, -2.0, 0.5)
     ctx.pa_setup(kinds=args.kinds, kappa=0.1, alpha=1.0, conv=c, mass=1.0)
 
@@ -607,7 +617,7 @@ def main():
                        "series": "strong: fixed n^3 split into z-slabs" if args.config == "c5"
                                  else "weak: an n x n x n/8 slab per rank (SURVEY 8e)" if args.config == "c5w"
                                  else "weak: an n^3 slab per rank",
-                       **({"comm": args.comm, "comm_lib": comm_lib} if world > 1 else {})},
+                       **({"comm": args.comm, "comm_lib": comm_lib, "comm_ranks": comm_ranks} if world > 1 else {})},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if gm is not None:

@@ -2097,6 +2097,35 @@ inline void MFEMInitializePetsc(int * = nullptr, char *** = nullptr, const char 
 }
 inline void MFEMFinalizePetsc() {}
 
+// The drivers' options-file choice (not MFEM API; the drivers' "-opts" argument):
+//  * an options file that exists is read (MFEMInitializePetsc);
+//  * an explicitly given file that does not exist: the reference's warning ("PETSc options file not
+//    found: ... Proceeding without options file.", linear_convection_diffusion_1D.cpp:310-324) and
+//    PETSc's defaults;
+//  * no -opts and no Input/petsc.opts in the working directory (the reference's default path, which
+//    exists beside the reference drivers): the values of the reference's Input/petsc.opts:2-6
+//    (gmres, rtol 1e-10, atol 1e-12, max_it 500, jacobi), so a run from any directory solves as the
+//    reference's default run does.
+// Returns the file to pass to MFEMInitializePetsc (nullptr: none).
+inline const char *DriverPetscOptionsFile(const std::string &given, const char *default_path = "Input/petsc.opts")
+{
+    static std::string chosen;
+    if (!given.empty()) {
+        if (std::ifstream(given).good()) return (chosen = given).c_str();
+        if (Mpi::Root())
+            std::cerr << "PETSc options file not found: " << given << ". Proceeding without options file." << std::endl;
+        return nullptr;
+    }
+    if (std::ifstream(default_path).good()) return (chosen = default_path).c_str();
+    auto &o = PetscOptions().kv;
+    o.emplace("-ksp_type", "gmres");
+    o.emplace("-ksp_rtol", "1.0e-10");
+    o.emplace("-ksp_atol", "1.0e-12");
+    o.emplace("-ksp_max_it", "500");
+    o.emplace("-pc_type", "jacobi");
+    return nullptr;
+}
+
 class PetscParMatrix : public Operator {
 public:
     // PetscParMatrix(MPI_COMM_WORLD, A_true, Operator::PETSC_MATAIJ)  (:367)

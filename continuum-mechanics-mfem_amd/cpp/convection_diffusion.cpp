@@ -32,22 +32,11 @@ using namespace mfem;
 
 namespace {
 
-// the reference's Input/petsc.opts:2-6 (its default options file), used when no file is found
-void default_petsc_options()
-{
-    auto &o = PetscOptions().kv;
-    o.emplace("-ksp_type", "gmres");
-    o.emplace("-ksp_rtol", "1.0e-10");
-    o.emplace("-ksp_atol", "1.0e-12");
-    o.emplace("-ksp_max_it", "500");
-    o.emplace("-pc_type", "jacobi");
-}
-
 struct Params {
     int dim = 2, n = 16, order = 2, rs = 0, rp = 0, print_level = 0;
     double kappa = 0.1, reaction = 1.0, c[3] = {1.0, -2.0, 0.5};
     int modes[3] = {3, 3, 3};
-    string opts = "Input/petsc.opts", mesh, cstr, mstr, mms = "sin";
+    string opts, mesh, cstr, mstr, mms = "sin";
 };
 
 // the circle variant's radial MMS, linear_convection_diffusion_2D_circle.cpp:140-215:
@@ -190,9 +179,7 @@ int main(int argc, char *argv[])
     if (!prm.mstr.empty()) std::sscanf(prm.mstr.c_str(), "%d,%d,%d", &prm.modes[0], &prm.modes[1], &prm.modes[2]);
 
     // :268-282, options file (the reference's default path; its values when the file is absent)
-    const char *petsc_file_to_use = nullptr;
-    if (!prm.opts.empty() && ifstream(prm.opts).good()) petsc_file_to_use = prm.opts.c_str();
-    else default_petsc_options();
+    const char *petsc_file_to_use = DriverPetscOptionsFile(prm.opts);
     MFEMInitializePetsc(&argc, &argv, petsc_file_to_use, NULL);
 
     int exit_code = 0;

@@ -32,15 +32,6 @@ using namespace mfem;
 
 namespace {
 
-void default_petsc_options()  // the reference's Input/petsc.opts:2-6
-{
-    auto &o = PetscOptions().kv;
-    o.emplace("-ksp_type", "gmres");
-    o.emplace("-ksp_rtol", "1.0e-10");
-    o.emplace("-ksp_atol", "1.0e-12");
-    o.emplace("-ksp_max_it", "500");
-    o.emplace("-pc_type", "jacobi");
-}
 
 // exp(a) erfc(b) without inf * 0 for large b (:128-144): the asymptotic erfc series past b = 26
 double ExpTimesErfc(const double a, const double b)
@@ -145,7 +136,7 @@ int main(int argc, char *argv[])
     Hypre::Init();
     const int myid = Mpi::WorldRank();
 
-    string mesh_file, opts = "Input/petsc.opts", csv;
+    string mesh_file, opts, csv;
     int n = 32, order = 3, rs = 0, rp = 0;
     double dt = 1.0e-3, t_final = 1.0;  // Input/input.yaml
     array<double, 3> peclet = {1.0, 10.0, 100.0};
@@ -171,9 +162,7 @@ int main(int argc, char *argv[])
         if (myid == 0) cerr << "Error: order >= 1, dt > 0, t_final >= 0 and Peclet > 0 required (:103-125)" << endl;
         return 2;
     }
-    const char *petsc_file_to_use = nullptr;
-    if (!opts.empty() && ifstream(opts).good()) petsc_file_to_use = opts.c_str();
-    else default_petsc_options();
+    const char *petsc_file_to_use = DriverPetscOptionsFile(opts);
     MFEMInitializePetsc(&argc, &argv, petsc_file_to_use, NULL);
 
     int exit_code = 0;

@@ -30,15 +30,6 @@ using namespace mfem;
 
 namespace {
 
-void default_petsc_options()  // the reference's Input/petsc.opts:2-6
-{
-    auto &o = PetscOptions().kv;
-    o.emplace("-ksp_type", "gmres");
-    o.emplace("-ksp_rtol", "1.0e-10");
-    o.emplace("-ksp_atol", "1.0e-12");
-    o.emplace("-ksp_max_it", "500");
-    o.emplace("-pc_type", "jacobi");
-}
 
 class ExactCoefficient : public Coefficient {
 public:
@@ -77,7 +68,7 @@ int main(int argc, char *argv[])
     Hypre::Init();
     const int myid = Mpi::WorldRank();
 
-    string mesh_file, opts = "Input/petsc.opts";
+    string mesh_file, opts;
     int n = 16, order = 1, rs = 0, rp = 0;
     double alpha = 0.1, dt = 0.05, t_final = 2.0;  // Input/input_diffusion_mms.yaml
     OptionsParser args(argc, argv);
@@ -95,9 +86,7 @@ int main(int argc, char *argv[])
         if (myid == 0) args.PrintUsage(cerr);
         return 1;
     }
-    const char *petsc_file_to_use = nullptr;
-    if (!opts.empty() && ifstream(opts).good()) petsc_file_to_use = opts.c_str();
-    else default_petsc_options();
+    const char *petsc_file_to_use = DriverPetscOptionsFile(opts);
     MFEMInitializePetsc(&argc, &argv, petsc_file_to_use, NULL);
 
     int exit_code = 0;

@@ -439,7 +439,8 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     double *red = c->d_state->red;  // device scalars awaiting the all-reduce (multi-rank)
     // high order on a structured box, one rank: den from the apply's E-vector, E->L fused into the
     // update (ho_kernels.hip k_apply3d_tile<DEN>, vec_kernels.hip k_e2l_box<UPD>)
-    const bool fused = !mr && !c->fa_ready && c->cg_fused && tile_den_ok(c) && e2l_box_ok(c);
+    const bool fused = !mr && !c->fa_ready && c->cg_fused && tile_den_ok(c) && e2l_box_ok(c) &&
+                       c->nl < ((int64_t)1 << 31);  // the flat update's fast division is exact below 2^31
     if (fused && !c->d_tpart) c->d_tpart = dalloc<double>(tile_den_blocks(c));
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();

@@ -82,25 +82,18 @@ __device__ __forceinline__ int axis_pairs(uint32_t g, uint32_t n, int *el, int *
     return k;
 }
 
-// UPD (CG mode with the den already known from the apply, k_apply3d_tile<DEN>): the E->L sum
-// q_i is consumed in place by the CG update instead of being stored:
-//   x_i += alpha d_i, r_i -= alpha q_i, y_i = z_i = M^-1 r_i, partial (r, z)
-// (x here is d; xs, r, dinv are the solution, residual and Jacobi inverse).
-template <bool CON, bool CG, int P, bool UPD = false>
+template <bool CON, bool CG, int P>
 __global__ void __launch_bounds__(kRedThreads)
 k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__restrict__ Ye,
           const double *__restrict__ x, double *__restrict__ y, int64_t nl, double *__restrict__ part,
-          KrylovState *__restrict__ st, double *__restrict__ xs = nullptr, double *__restrict__ res = nullptr,
-          const double *__restrict__ dinv = nullptr)
+          KrylovState *__restrict__ st)
 {
-    static_assert(!UPD || (CON && CG), "the fused update is the constrained CG mode");
     // one wave per x-row (gy, gz) of the dof lattice (grid-stride over rows): the y / z element
     // pairs are uniform across the wave, lanes run along x, and the row's contributions are one
     // contiguous run of the pencil E-vector (entries gx + ex - 1 and gx + ex, ex = gx / P)
     constexpr int D1 = P + 1;
     __shared__ double sh[kRedThreads / 64];
     if (CG && st->done) return;
-    const double alpha = UPD ? st->alpha : 0.0;
     double acc = 0.0;
     const int lane = threadIdx.x & 63;
     const uint32_t rows = bx.Ly * (uint32_t)(nl / ((int64_t)bx.Lx * bx.Ly));
@@ -136,12 +129,6 @@ k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__rest
             }
             const bool is_ess = CON && ess[i];
             const double xi = (CON || CG) ? x[i] : 0.0;
-            double si = 0.0, ri = 0.0, mi = 1.0;
-            if constexpr (UPD) {
-                si = xs[i];
-                ri = res[i];
-                if (dinv) mi = dinv[i];
-            }
             double v = 0.0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -151,20 +138,87 @@ k_e2l_box(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__rest
                 }
             }
             if (is_ess) v = xi;
-            if constexpr (UPD) {  // outputs streamed out: next read after a full apply
+            y[i] = v;
+            if (CG) acc += v * xi;
+        }
+    }
+    if (!CG) return;
+    store_partial(block_sum(acc, sh), part);
+}
+
+// The fused E->L + CG update (CG mode with the den already known from the apply,
+// k_apply3d_tile<DEN>): the E->L sum q_i is consumed in place instead of being stored,
+//   x_i += alpha d_i, r_i -= alpha q_i, z_i = M^-1 r_i, partial (r, z).
+// The dofs are taken in flat lattice order: a wave covers 64 * kFlatU consecutive dofs (row-
+// crossing) and every lane derives its own (gx, gy, gz) and element pairs, so no lane idles at the
+// end of an x-row (one wave per 513-dof row used 8.02 of its 9 passes: 1948 -> 1837 us per update
+// at C3, profiles/r03/ab_c3_e2l_flat.txt).  Pairs visited as in k_e2l_box (bitwise the same sums).
+constexpr int kFlatU = 2;
+template <int P>
+__global__ void __launch_bounds__(kRedThreads)
+k_e2l_update_flat(const BoxE2L bx, const uint8_t *__restrict__ ess, const double *__restrict__ Ye,
+                  const double *__restrict__ d, double *__restrict__ z, int64_t nl, double *__restrict__ part,
+                  const KrylovState *__restrict__ st, double *__restrict__ xs, double *__restrict__ res,
+                  const double *__restrict__ dinv)
+{
+    constexpr int D1 = P + 1;
+    __shared__ double sh[kRedThreads / 64];
+    if (st->done) return;
+    const double alpha = st->alpha;
+    const uint32_t ew = bx.nx * D1, Lxy = bx.Lx * bx.Ly;
+    double acc = 0.0;
+    const int64_t per_block = (int64_t)kRedThreads * kFlatU;
+    for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < nl; b0 += (int64_t)gridDim.x * per_block) {
+        const int64_t w0 = b0 + (int64_t)(threadIdx.x >> 6) * 64 * kFlatU + (threadIdx.x & 63);
+#pragma unroll
+        for (int u = 0; u < kFlatU; ++u) {
+            const int64_t i0 = w0 + 64 * u;
+            const bool in = i0 < nl;
+            const uint32_t i = (uint32_t)(in ? i0 : nl - 1);
+            const uint32_t gz = fdiv(i, bx.fLxy), rem = i - gz * Lxy;
+            const uint32_t gy = fdiv(rem, bx.fLx), gx = rem - gy * bx.Lx;
+            int ey[2], ly[2], ez[2], lz[2];
+            const int nyp = axis_pairs<P>(gy, bx.ny, ey, ly);
+            const int nzp = axis_pairs<P>(gz, bx.nz, ez, lz);
+            int64_t erow[4];
+            int ne_rows = 0;
+            for (int a = 0; a < nzp; ++a)
+                for (int b = 0; b < nyp; ++b)
+                    erow[ne_rows++] = (((int64_t)(ez[a] * D1 + lz[a]) * bx.ny + ey[b]) * D1 + ly[b]) * ew;
+            for (int k = ne_rows; k < 4; ++k) erow[k] = erow[0];
+            const uint32_t ex = gx / P, lx = gx - ex * P;
+            const bool left = lx == 0 && ex > 0, right = lx != 0 || ex < bx.nx;
+            const int64_t cl = left ? -1 : 0, cr = right ? 0 : -1;
+            double el[4], er[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const double *e0 = Ye + erow[k] + gx + ex;
+                el[k] = e0[cl];
+                er[k] = e0[cr];
+            }
+            const bool is_ess = ess[i];
+            const double xi = d[i], si = xs[i];
+            double ri = res[i];
+            const double mi = dinv ? dinv[i] : 1.0;
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k < ne_rows) {
+                    if (left) v += el[k];
+                    if (right) v += er[k];
+                }
+            }
+            if (is_ess) v = xi;
+            if (in) {
                 __builtin_nontemporal_store(si + alpha * xi, &xs[i]);
                 ri -= alpha * v;
                 __builtin_nontemporal_store(ri, &res[i]);
                 const double zi = mi * ri;
-                __builtin_nontemporal_store(zi, &y[i]);
+                __builtin_nontemporal_store(zi, &z[i]);
                 acc += ri * zi;
-            } else {
-                y[i] = v;
-                if (CG) acc += v * xi;
             }
         }
     }
-    if (!CG) return;
     store_partial(block_sum(acc, sh), part);
 }
 
@@ -472,8 +526,11 @@ template <int P>
 static hipError_t launch_e2l_update_p(cdfem_ctx *c, const double *Ye, const double *d, double *x, double *r,
                                       double *z, const double *dinv)
 {
-    const dim3 g = box_grid(c), b(kRedThreads);
-    hipLaunchKernelGGL((k_e2l_box<true, true, P, true>), g, b, 0, c->stream, box_e2l(c), c->d_ess, Ye, d, z, c->nl,
+    dim3 g;
+    const dim3 b(kRedThreads);
+    const int64_t per_block = (int64_t)kRedThreads * kFlatU;
+    g = dim3((unsigned)std::min<int64_t>((c->nl + per_block - 1) / per_block, 65536));
+    hipLaunchKernelGGL((k_e2l_update_flat<P>), g, b, 0, c->stream, box_e2l(c), c->d_ess, Ye, d, z, c->nl,
                        c->d_part, c->d_state, x, r, dinv);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

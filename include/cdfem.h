@@ -244,7 +244,8 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * Variants measured slower and removed in round 3 (their records stay under profiles/r02_ab_*):
  * brick element cores 1-10 and the four-waves-per-brick kernel, x-fold / paired x updates, the
  * folded high-order direction, the derived mass weight, per-XCD SpMV sort, SpMV stream offsets and
- * the software-pipelined SpMV loop, the two-waves-per-SIMD structured Mult.                      */
+ * the software-pipelined SpMV loop, the two-waves-per-SIMD structured Mult, 2 / 4 lanes per SpMV row
+ * (profiles/r03/ab_c4_spmv_lanes_per_row.txt).                      */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
 
 /* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */

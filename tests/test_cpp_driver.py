@@ -260,6 +260,23 @@ def test_driver_default_options_are_the_references(exe, tmp_path):
     assert abs(out["l2_abs"] - l2) <= 1e-6 * l2
 
 
+@pytest.mark.gpu
+def test_driver_missing_options_file_uses_petsc_defaults(exe, tmp_path):
+    """An explicitly given options file that does not exist: the reference's warning
+    (linear_convection_diffusion_1D.cpp:310-324) and PETSc's defaults (GMRES(30), rtol 1e-5,
+    atol 1e-50; Jacobi on the matrix-free operator, with a note)."""
+    from oracle import oracle as O
+    r = subprocess.run([exe, "-d", "2", "-n", "8", "-p", "2", "-opts", str(tmp_path / "missing.opts")],
+                       capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    assert "PETSc options file not found" in r.stderr
+    out = _parse(r.stdout)
+    mesh = O.BoxMesh(2, 8, 2)
+    prm = O.mms_params(O.MMS_SIN, 2, kappa=0.1, s=1.0, c=(1.0, -2.0), p=2)
+    _, info, _ = O.solve_mms(mesh, prm, kappa=0.1, s=1.0, c=(1.0, -2.0), solver="gmres", tol=1e-5, atol=1e-50)
+    assert abs(out["iterations"] - info["iterations"]) <= 1
+
+
 # ---- MPI: the reference's ParMesh(MPI_COMM_WORLD, *mesh) path, 2 and 3 ranks sharing the box's GPU
 # (host communicator over MPI).  The partitioned solve must reproduce the one-rank run: the same
 # global dof count, iteration count within 2, L2 error to 1e-7 relative (both stop at rtol 1e-10).

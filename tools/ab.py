@@ -21,7 +21,7 @@ ap.add_argument("--iters", type=int, default=100)
 ap.add_argument("--n", type=int, default=64)
 ap.add_argument("--p", type=int, default=2)
 ap.add_argument("--kinds", type=int, default=7)
-ap.add_argument("--variants", default="brick_waves=1,brick_waves=2")
+ap.add_argument("--variants", default="e2l_flat=0,e2l_flat=1")
 ap.add_argument("--no-events", action="store_true", help="time whole solves only (no per-kernel events)")
 args = ap.parse_args()
 
