@@ -1558,13 +1558,19 @@ private:
         unsigned kinds = 0;
         double kappa = 0.0, mass = 0.0, alpha = 1.0, conv[3] = {0, 0, 0};
         std::vector<double> kq, kmq, mq, cq;
-        int nq = 0;
-        std::vector<double> xyz;
-        auto points = [&]() -> const std::vector<double> & {
-            if (xyz.empty()) xyz = dev_->Points(CDFEM_RULE_OPERATOR, dim, ne, nq);
-            return xyz;
+        // every integrator samples its coefficient at the points of its own rule (on simplices
+        // MFEM's GetRule differs per integrator; on quads / hexes the three rules coincide)
+        std::map<int, std::pair<std::vector<double>, int>> pts;
+        auto points = [&](int rule) -> const std::pair<std::vector<double>, int> & {
+            auto it = pts.find(rule);
+            if (it == pts.end()) {
+                int n = 0;
+                std::vector<double> x = dev_->Points(rule, dim, ne, n);
+                it = pts.emplace(rule, std::make_pair(std::move(x), n)).first;
+            }
+            return it->second;
         };
-        auto accumulate = [&](Coefficient *q, double &cst, std::vector<double> &arr) {
+        auto accumulate = [&](Coefficient *q, double &cst, std::vector<double> &arr, int rule) {
             if (!q) {
                 cst += 1.0;  // MassIntegrator() / DiffusionIntegrator(): coefficient 1
                 if (!arr.empty())
@@ -1577,7 +1583,8 @@ private:
                     for (double &v : arr) v += c->constant;
                 return;
             }
-            std::vector<double> s = Sample(*q, points(), dim, nq);
+            const auto &P = points(rule);
+            std::vector<double> s = Sample(*q, P.first, dim, P.second);
             if (arr.empty()) arr.assign(s.size(), cst);
             for (size_t i = 0; i < s.size(); ++i) arr[i] += s[i];
         };
@@ -1585,11 +1592,12 @@ private:
             kinds |= bi->Kind();
             if (auto *d = dynamic_cast<DiffusionIntegrator *>(bi.get())) {
                 if (!d->MQ_) {
-                    accumulate(d->Q_, kappa, kq);
+                    accumulate(d->Q_, kappa, kq, CDFEM_RULE_DIFFUSION);
                     continue;
                 }
                 // MatrixCoefficient: symmetric tensor per point, xx,xy,(xz),yy,(yz),zz
-                const std::vector<double> &P = points();
+                const std::vector<double> &P = points(CDFEM_RULE_DIFFUSION).first;
+                const int nq = points(CDFEM_RULE_DIFFUSION).second;
                 if (kmq.empty()) kmq.assign(P.size() / dim * ns, 0.0);
                 ElementTransformation T;
                 IntegrationPoint ip;
@@ -1609,12 +1617,13 @@ private:
                         }
                 }
             } else if (auto *m = dynamic_cast<MassIntegrator *>(bi.get())) {
-                accumulate(m->Q_, mass, mq);
+                accumulate(m->Q_, mass, mq, CDFEM_RULE_MASS);
             } else if (auto *c = dynamic_cast<ConvectionIntegrator *>(bi.get())) {
                 if (auto *vc = dynamic_cast<VectorConstantCoefficient *>(c->Q_); vc && cq.empty()) {
                     for (int k = 0; k < dim; ++k) conv[k] += c->alpha * vc->GetVec()[k];
                 } else {
-                    const std::vector<double> &P = points();
+                    const std::vector<double> &P = points(CDFEM_RULE_CONVECTION).first;
+                    const int nq = points(CDFEM_RULE_CONVECTION).second;
                     if (cq.empty()) {
                         cq.resize(P.size());
                         for (size_t i = 0; i < P.size(); ++i) cq[i] = conv[i % dim];

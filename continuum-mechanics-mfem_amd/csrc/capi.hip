@@ -109,7 +109,8 @@ void free_mesh(cdfem_ctx *c)
     c->fa_ready = false;
     c->nnz = 0;
     c->h_verts.clear();
-    c->h_sxi.clear();
+    c->h_sxi_d.clear();
+    c->h_sxi_cm.clear();
     c->h_sxi_lf.clear();
     c->zlo_shared = c->zhi_shared = 0;
     c->gm_cap = 0;
@@ -954,18 +955,37 @@ int cdfem_prolongate(cdfem_ctx *c, const double *X, double *x, int where)
     });
 }
 
+// simplex meshes: points of a rule (and its reference coordinates); the operator's integrators have
+// rules of their own (CDFEM_RULE_DIFFUSION / CONVECTION / MASS), so CDFEM_RULE_OPERATOR is refused
+static int simplex_rule_pts(const cdfem_ctx *c, int rule, const std::vector<double> **sxi)
+{
+    const std::vector<double> *x = nullptr;
+    int nq = 0;
+    switch (rule) {
+    case CDFEM_RULE_DIFFUSION: x = &c->h_sxi_d; nq = c->nq_sd; break;
+    case CDFEM_RULE_CONVECTION:
+    case CDFEM_RULE_MASS: x = &c->h_sxi_cm; nq = c->nq_scm; break;
+    case CDFEM_RULE_LINEARFORM: x = &c->h_sxi_lf; nq = c->nq_lf; break;
+    case CDFEM_RULE_OPERATOR:
+        throw UnsupportedError("simplex meshes: each integrator has its own rule (CDFEM_RULE_DIFFUSION, "
+                               "CDFEM_RULE_CONVECTION, CDFEM_RULE_MASS)");
+    default: throw UnsupportedError("simplex meshes: no such rule (the L2-error rule is host-side)");
+    }
+    if (sxi) *sxi = x;
+    return nq;
+}
+
 int cdfem_rule_size(cdfem_ctx *c, int rule, int *nq)
 {
     return guarded(c, [&] {
         require_mesh(c);
         if (!nq) throw ArgError("nq is null");
         if (c->geom != 0) {
-            if (rule == CDFEM_RULE_ERROR) throw UnsupportedError("simplex meshes: operator / linear-form rules");
-            *nq = rule == CDFEM_RULE_OPERATOR ? c->nq_simplex : c->nq_lf;
+            *nq = simplex_rule_pts(c, rule, nullptr);
             return CDFEM_OK;
         }
-        const Rule1D &r = rule == CDFEM_RULE_OPERATOR ? c->rule_op
-                        : rule == CDFEM_RULE_LINEARFORM ? c->rule_lf : c->rule_err;
+        const Rule1D &r = rule == CDFEM_RULE_LINEARFORM ? c->rule_lf : rule == CDFEM_RULE_ERROR ? c->rule_err
+                                                                                                 : c->rule_op;
         *nq = nq_of(c, r);
         return CDFEM_OK;
     });
@@ -977,9 +997,10 @@ int cdfem_quadrature_points(cdfem_ctx *c, int rule, double *xyz, int where)
         require_mesh(c);
         if (!xyz) throw ArgError("xyz is null");
         if (c->geom != 0) {  // affine simplices: x = v0 + J xi, evaluated on the host
-            if (rule == CDFEM_RULE_ERROR) throw UnsupportedError("simplex meshes: operator / linear-form rules");
-            const std::vector<double> &sxi = rule == CDFEM_RULE_OPERATOR ? c->h_sxi : c->h_sxi_lf;
-            const int dim = c->dim, nv = dim + 1, nq = rule == CDFEM_RULE_OPERATOR ? c->nq_simplex : c->nq_lf;
+            const std::vector<double> *psxi = nullptr;
+            const int nq = simplex_rule_pts(c, rule, &psxi);
+            const std::vector<double> &sxi = *psxi;
+            const int dim = c->dim, nv = dim + 1;
             std::vector<double> out((size_t)c->ne * nq * dim);
             for (int e = 0; e < c->ne; ++e) {
                 const double *V = &c->h_verts[(size_t)e * nv * dim];
@@ -998,8 +1019,8 @@ int cdfem_quadrature_points(cdfem_ctx *c, int rule, double *xyz, int where)
             }
             return CDFEM_OK;
         }
-        const Rule1D &r = rule == CDFEM_RULE_OPERATOR ? c->rule_op
-                        : rule == CDFEM_RULE_LINEARFORM ? c->rule_lf : c->rule_err;
+        const Rule1D &r = rule == CDFEM_RULE_LINEARFORM ? c->rule_lf : rule == CDFEM_RULE_ERROR ? c->rule_err
+                                                                                                 : c->rule_op;
         const size_t n = (size_t)c->ne * nq_of(c, r) * c->dim;
         double *d = where == CDFEM_DEVICE ? xyz : dalloc<double>(n);
         HIPCHK(launch_quad_points(c, r, d));
@@ -1112,19 +1133,26 @@ int cdfem_mesh_upload_simplex(cdfem_ctx *c, int dim, int order, int ne, const do
         for (int64_t i = 0; i < nldofs; ++i)
             if (c->h_ess[i]) ess_list.push_back((int32_t)i);
         c->n_ess = (int)ess_list.size();
-        // operator rule (collapsed Gauss, n = p + 2) and its basis tables
-        std::vector<double> w;
-        c->nq_simplex = simplex_rule(dim, order + 2, c->h_sxi, w);
-        const int nq = c->nq_simplex;
-        std::vector<double> tab((size_t)nq * nd * (dim + 1) + nq);
-        for (int q = 0; q < nq; ++q) {
-            double phi[10], dphi[30];
-            simplex_basis(dim, order, &c->h_sxi[(size_t)q * dim], phi, dphi);
-            for (int i = 0; i < nd; ++i) {
-                tab[(size_t)q * nd + i] = phi[i];
-                for (int k = 0; k < dim; ++k) tab[(size_t)nq * nd + ((size_t)q * nd + i) * dim + k] = dphi[i * dim + k];
+        // the integrators' rules (MFEM's GetRule on affine simplices, tabulated rules): diffusion of
+        // order 2p - 2, convection and mass of order 2p; basis tables of both, diffusion first
+        std::vector<double> wd, wcm, tab;
+        c->nq_sd = simplex_rule_for_order(dim, std::max(2 * order - 2, 0), c->h_sxi_d, wd);
+        c->nq_scm = simplex_rule_for_order(dim, 2 * order, c->h_sxi_cm, wcm);
+        for (int r = 0; r < 2; ++r) {
+            const std::vector<double> &xi = r == 0 ? c->h_sxi_d : c->h_sxi_cm, &w = r == 0 ? wd : wcm;
+            const int nq = r == 0 ? c->nq_sd : c->nq_scm;
+            const size_t o = tab.size();
+            tab.resize(o + (size_t)nq * nd * (dim + 1) + nq);
+            for (int q = 0; q < nq; ++q) {
+                double phi[10], dphi[30];
+                simplex_basis(dim, order, &xi[(size_t)q * dim], phi, dphi);
+                for (int i = 0; i < nd; ++i) {
+                    tab[o + (size_t)q * nd + i] = phi[i];
+                    for (int k = 0; k < dim; ++k)
+                        tab[o + (size_t)nq * nd + ((size_t)q * nd + i) * dim + k] = dphi[i * dim + k];
+                }
+                tab[o + (size_t)nq * nd * (dim + 1) + q] = w[q];
             }
-            tab[(size_t)nq * nd * (dim + 1) + q] = w[q];
         }
         // linear-form rule: DomainLFIntegrator's default order 2p, MFEM's tabulated simplex rule
         std::vector<double> wl;
@@ -1226,9 +1254,10 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             }
             HIPCHK(hipStreamSynchronize(c->stream));  // P's host buffers die at scope exit
         }
-        const size_t neq = (size_t)c->ne * c->nq_simplex;
-        double *dk = upload_opt(c, f->kappa_q, neq), *dkm = upload_opt(c, f->kappa_mat_q, neq * c->dim * (c->dim + 1) / 2);
-        double *dc = upload_opt(c, f->conv_q, neq * c->dim), *dm = upload_opt(c, f->mass_q, neq);
+        // per-point coefficients at the rule of their integrator
+        const size_t nqd = (size_t)c->ne * c->nq_sd, nqc = (size_t)c->ne * c->nq_scm;
+        double *dk = upload_opt(c, f->kappa_q, nqd), *dkm = upload_opt(c, f->kappa_mat_q, nqd * c->dim * (c->dim + 1) / 2);
+        double *dc = upload_opt(c, f->conv_q, nqc * c->dim), *dm = upload_opt(c, f->mass_q, nqc);
         c->kinds = kinds;
         HIPCHK(launch_simplex_elem(c, dk, dkm, f->kappa, f->alpha, f->conv, dc, dm, f->mass));
         HIPCHK(launch_fa_assemble(c));

@@ -185,10 +185,13 @@ struct cdfem_ctx {
 
     // geometry family: 0 tensor (quad/hex: PA), 1 simplex (tri/tet: FA, cdfem_mesh_upload_simplex)
     int geom = 0;
-    int nq_simplex = 0;                 // points of the simplex operator rule
-    double *d_stab = nullptr;           // simplex rule tables: phi [nq][nd], dphi [nq][nd][dim], w [nq]
+    // simplex integrator rules (MFEM's GetRule on affine simplices): diffusion order 2p - 2,
+    // convection and mass order 2p, each on MFEM's tabulated rule (simplex_rule_for_order)
+    int nq_sd = 0, nq_scm = 0;          // points of the diffusion / convection + mass rules
+    double *d_stab = nullptr;           // rule tables, diffusion rule first then the convection + mass
+                                        // rule, each phi [nq][nd], dphi [nq][nd][dim], w [nq]
     std::vector<double> h_verts;        // simplex host geometry (quadrature points for coefficients)
-    std::vector<double> h_sxi;          // simplex rule points (reference coordinates)
+    std::vector<double> h_sxi_d, h_sxi_cm;  // the two rules' points (reference coordinates)
     int nq_lf = 0;                      // simplex LINEARFORM rule (collapsed Gauss, n = p + 3)
     std::vector<double> h_sxi_lf;
     double *d_stab_lf = nullptr;        // phi [nq_lf][nd], w [nq_lf]

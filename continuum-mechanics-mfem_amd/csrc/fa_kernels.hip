@@ -141,7 +141,7 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
 // ---- element matrices on affine simplices ----------------------------------------------------------
 template <int DIM, int P>
 __global__ void __launch_bounds__(64)
-k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *__restrict__ stab, unsigned kinds,
+k_simplex_elem(const double *__restrict__ verts, int ne, int nqd, int nqc, const double *__restrict__ stab, unsigned kinds,
                double kappa, const double *__restrict__ kq, const double *__restrict__ kmq, double alpha, double c0,
                double c1, double c2,
                const double *__restrict__ cq, double mass, const double *__restrict__ mq, double *__restrict__ Ee)
@@ -179,12 +179,21 @@ k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *_
     for (int i = 0; i < ND; ++i)
 #pragma unroll
         for (int j = 0; j < ND; ++j) M[i][j] = 0.0;
-    const double *phi_t = stab, *dphi_t = stab + (size_t)nq * ND, *w_t = stab + (size_t)nq * ND * (DIM + 1);
     const double cc[3] = {c0, c1, c2};
+    // two rules (MFEM's GetRule): r = 0 the diffusion rule (order 2p - 2) with the diffusion term,
+    // r = 1 the convection + mass rule (order 2p) with those terms; per-point coefficient arrays
+    // are indexed in the point order of their own rule
+    for (int r = 0; r < 2; ++r) {
+        const bool dif = r == 0 && (kinds & CDFEM_DIFFUSION), con = r == 1 && (kinds & CDFEM_CONVECTION),
+                   mas = r == 1 && (kinds & CDFEM_MASS);
+        if (!dif && !con && !mas) continue;
+        const int nq = r == 0 ? nqd : nqc;
+        const double *tab = r == 0 ? stab : stab + (size_t)nqd * (ND * (DIM + 1) + 1);
+        const double *phi_t = tab, *dphi_t = tab + (size_t)nq * ND, *w_t = tab + (size_t)nq * ND * (DIM + 1);
     for (int q = 0; q < nq; ++q) {
         const double W = w_t[q];
         double D[DIM][DIM] = {}, Cv[DIM] = {}, Ms = 0.0;
-        if (kinds & CDFEM_DIFFUSION) {
+        if (dif) {
             const double kap = kq ? kq[(size_t)e * nq + q] : kappa;
             if (kmq) {  // MatrixCoefficient: W adj(J) K adj(J)^T / det J with K = kap I + K_q
                 constexpr int NS = DIM * (DIM + 1) / 2;
@@ -221,7 +230,7 @@ k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *_
                     }
             }
         }
-        if (kinds & CDFEM_CONVECTION) {
+        if (con) {
 #pragma unroll
             for (int a = 0; a < DIM; ++a) {
                 double s = 0.0;
@@ -231,7 +240,7 @@ k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *_
                 Cv[a] = W * alpha * s;
             }
         }
-        if (kinds & CDFEM_MASS) Ms = W * (mq ? mq[(size_t)e * nq + q] : mass) * det;
+        if (mas) Ms = W * (mq ? mq[(size_t)e * nq + q] : mass) * det;
         double ph[ND], dph[ND][DIM];
 #pragma unroll
         for (int i = 0; i < ND; ++i) {
@@ -257,6 +266,7 @@ k_simplex_elem(const double *__restrict__ verts, int ne, int nq, const double *_
                 M[i][j] += v;
             }
         }
+    }
     }
     const int64_t base = (int64_t)(e / kLanes) * ND * ND * kLanes + e % kLanes;
 #pragma unroll
@@ -492,7 +502,7 @@ hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq
     const dim3 g((c->ne + 63) / 64), b(64);
     const double c0 = conv ? conv[0] : 0.0, c1 = conv ? conv[1] : 0.0, c2 = (conv && c->dim == 3) ? conv[2] : 0.0;
 #define CDFEM_SIMPLEX(D, P)                                                                              \
-    hipLaunchKernelGGL((k_simplex_elem<D, P>), g, b, 0, c->stream, c->d_verts, c->ne, c->nq_simplex,     \
+    hipLaunchKernelGGL((k_simplex_elem<D, P>), g, b, 0, c->stream, c->d_verts, c->ne, c->nq_sd, c->nq_scm, \
                        c->d_stab, c->kinds, kappa, kq, kmq, alpha, c0, c1, c2, cq, mass, mq, c->d_Ee)
     if (c->dim == 3 && c->p == 1) CDFEM_SIMPLEX(3, 1);
     else if (c->dim == 3 && c->p == 2) CDFEM_SIMPLEX(3, 2);

@@ -29,7 +29,7 @@ HOST, DEVICE = 0, 1
 CG, GMRES = 0, 1
 PC_NONE, PC_JACOBI, PC_ILU = 0, 1, 2
 _PCS = {"none": PC_NONE, "jacobi": PC_JACOBI, "ilu": PC_ILU}
-RULE_OPERATOR, RULE_LINEARFORM, RULE_ERROR = 0, 1, 2
+RULE_OPERATOR, RULE_LINEARFORM, RULE_ERROR, RULE_DIFFUSION, RULE_CONVECTION, RULE_MASS = 0, 1, 2, 3, 4, 5
 K_APPLY, K_E2L, K_UPDATE, K_DIRECTION, K_ORTH = 0, 1, 2, 3, 4
 
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_UNSUPPORTED, ERR_NOT_CONVERGED, ERR_COMM = range(7)

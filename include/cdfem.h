@@ -51,8 +51,12 @@ enum { CDFEM_HOST = 0, CDFEM_DEVICE = 1 };
 /* Krylov methods and preconditioners */
 enum { CDFEM_CG = 0, CDFEM_GMRES = 1 };
 enum { CDFEM_PC_NONE = 0, CDFEM_PC_JACOBI = 1, CDFEM_PC_ILU = 2 };
-/* quadrature rules whose points the host may need for coefficient evaluation */
-enum { CDFEM_RULE_OPERATOR = 0, CDFEM_RULE_LINEARFORM = 1, CDFEM_RULE_ERROR = 2 };
+/* quadrature rules whose points the host may need for coefficient evaluation.  Quads / hexes: one
+ * operator rule (Gauss n = p + 2, shared by the three integrators; DIFFUSION / CONVECTION / MASS
+ * name it too).  Simplices: each integrator its own rule, MFEM's GetRule on affine simplices on
+ * MFEM's tabulated rules: DIFFUSION order 2p - 2, CONVECTION and MASS order 2p (OPERATOR refused). */
+enum { CDFEM_RULE_OPERATOR = 0, CDFEM_RULE_LINEARFORM = 1, CDFEM_RULE_ERROR = 2, CDFEM_RULE_DIFFUSION = 3,
+       CDFEM_RULE_CONVECTION = 4, CDFEM_RULE_MASS = 5 };
 /* kernel ids for cdfem_profile_read */
 enum { CDFEM_K_APPLY = 0, CDFEM_K_E2L = 1, CDFEM_K_UPDATE = 2, CDFEM_K_DIRECTION = 3, CDFEM_K_ORTH = 4,
        CDFEM_K_COUNT = 8 };
@@ -101,7 +105,8 @@ int cdfem_quadrature_points(cdfem_ctx *ctx, int rule, double *xyz, int where);
  *           a.Assemble()                                                   :339
  * with MFEM partial-assembly semantics: per-quadrature-point data
  *   D = W kappa adj(J) adj(J)^T / det J,  C = W alpha adj(J) c,  M = W s det J.
- * *_q arrays (ne*nq of the OPERATOR rule; conv_q ne*nq*dim) override the constants when
+ * *_q arrays (ne*nq of the OPERATOR rule = the DIFFUSION / CONVECTION / MASS rules on quads and hexes;
+ * conv_q ne*nq*dim) override the constants when
  * non-NULL (host pointers): a variable Coefficient / VectorCoefficient sampled on the host.     */
 int cdfem_pa_setup(cdfem_ctx *ctx, unsigned kinds, double kappa, const double *kappa_q,
                    double alpha, const double *conv, const double *conv_q, double mass,
@@ -136,9 +141,11 @@ int cdfem_pa_setup_form(cdfem_ctx *ctx, const cdfem_form_coeffs *form);
  * local order: vertices, then edge nodes along a->b for edges (0,1),(0,2),(0,3),(1,2),(1,3),(2,3)
  * [2D: (0,1),(0,2),(1,2)], then the P3 centroid; det J > 0 required.  cdfem_lf_assemble works on
  * simplex meshes with f sampled at the CDFEM_RULE_LINEARFORM points (MFEM's tabulated rule of order
- * 2p, cdfem_simplex_rule_order).  The operator rule is collapsed Gauss with n = p + 2 (exact for the
- * constant-coefficient integrands; see DESIGN.md §1 for variable coefficients).
- * cdfem_fa_setup: same coefficients as cdfem_pa_setup (per-point arrays on the OPERATOR rule);
+ * 2p, cdfem_simplex_rule_order).  Each integrator has MFEM's rule (GetRule on affine simplices):
+ * diffusion order 2p - 2, convection and mass order 2p, on MFEM's tabulated rules.
+ * cdfem_fa_setup: same coefficients as cdfem_pa_setup, per-point arrays on the rule of their
+ * integrator: kappa_q / kappa_mat_q on CDFEM_RULE_DIFFUSION, conv_q on CDFEM_RULE_CONVECTION,
+ * mass_q on CDFEM_RULE_MASS (cdfem_rule_size / cdfem_quadrature_points);
  * assembles A (CSR, columns sorted) and the eliminated matrix of FormLinearSystem on the GPU.
  * Afterwards cdfem_pa_mult / cdfem_pa_diagonal / cdfem_form_linear_system / cdfem_solve run on the
  * CSR operator.  cdfem_fa_csr exports it (rowptr n+1, cols/vals nnz; pass NULLs to query nnz).   */

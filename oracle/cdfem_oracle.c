@@ -1427,9 +1427,8 @@ static void simplex_element_matrix(int dim, int p, const double *V, const orc_co
     for (int k = 0; k < dim; k++)
         for (int m = 0; m < dim; m++) J[k][m] = V[(m + 1) * dim + k] - V[k];
     const double detJ = adjugate(dim, J, A);
-    memset(Ae, 0, sizeof(double) * nd * nd);
     double phi[10], dphi[30];
-    for (int q = 0; q < nq; q++) {
+    for (int q = 0; q < nq; q++) {  /* accumulates into Ae */
         const double W = wq[q];
         double D[3][3] = {{0}}, Cv[3] = {0}, M = 0.0;
         point_coef(dim, cf, q, W, detJ, A, D, Cv, &M);
@@ -1450,7 +1449,21 @@ static void simplex_element_matrix(int dim, int p, const double *V, const orc_co
     }
 }
 
-/* FA CSR of the convection-diffusion-reaction form on P1/P2 simplices (rule: n = p + 2). */
+/* Integration orders of the simplex integrators [MFEM-ext fem/bilininteg.cpp GetRule, affine
+ * simplices: Trans.OrderW() = 0, Trans.Order() = 1, Trans.OrderGrad(Pk) = p - 1]:
+ *   DiffusionIntegrator   trial + test - 2          = 2p - 2  (FunctionSpace::Pk)
+ *   ConvectionIntegrator  OrderGrad + Order + test  = 2p
+ *   MassIntegrator        trial + test + OrderW     = 2p
+ * each on MFEM's tabulated rule of that order (orc_simplex_rule_order). */
+ORC_API int orc_simplex_integrator_order(int p, int kind)
+{
+    return kind == 1 ? (2 * p - 2 > 0 ? 2 * p - 2 : 0) : 2 * p;
+}
+
+/* FA CSR of the convection-diffusion-reaction form on P1-P3 simplices: the diffusion part on its
+ * rule (order 2p - 2), convection and mass on theirs (order 2p); per-point coefficient arrays are
+ * element-major in the point order of the rule of the integrator they belong to (kq, kmq: diffusion;
+ * cq: convection; sq: mass). */
 ORC_API orc_csr *orc_fa_assemble_simplex_q(int dim, int p, int ne, const double *verts, const int *dofmap,
                                            int64_t nl, double kappa, const double *kq, const double *kmq,
                                            double alpha, const double *c, const double *cq, double s,
@@ -1459,17 +1472,26 @@ ORC_API orc_csr *orc_fa_assemble_simplex_q(int dim, int p, int ne, const double 
     p3_init();
     const int nd = orc_simplex_nd(dim, p);
     if (nd < 0 || (dim != 2 && dim != 3)) return NULL;
-    orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
-                   (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0, kq, kmq, cq, sq};
-    const int n1 = p + 2;
-    double xi[16 * 16 * 16 * 3 / 16], wq[16 * 16 * 16 / 16];  /* n1 <= 4: 64 points */
-    const int nq = orc_simplex_rule(dim, n1, xi, wq);
-    double *Ae = (double *)malloc(sizeof(double) * (size_t)ne * nd * nd);
+    const orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, (c && dim == 3) ? c[2] : 0},
+                         (kinds & 1) != 0, (kinds & 2) != 0, (kinds & 4) != 0, kq, kmq, cq, sq};
+    orc_coef cd = cf, ccm = cf;  /* diffusion part / convection + mass part */
+    cd.use_conv = cd.use_mass = 0;
+    ccm.use_diff = 0;
+    double xd[64 * 3], wd[64], xc[64 * 3], wc[64];
+    const int nqd = orc_simplex_rule_order(dim, orc_simplex_integrator_order(p, 1), xd, wd);
+    const int nqc = orc_simplex_rule_order(dim, orc_simplex_integrator_order(p, 4), xc, wc);
+    double *Ae = (double *)calloc((size_t)ne * nd * nd, sizeof(double));
     #pragma omp parallel for schedule(static)
     for (int e = 0; e < ne; e++) {
-        const orc_coef ce = coef_of(&cf, dim, e, nq);
-        simplex_element_matrix(dim, p, verts + (size_t)e * (dim + 1) * dim, &ce, nq, xi, wq,
-                               Ae + (size_t)e * nd * nd);
+        const double *V = verts + (size_t)e * (dim + 1) * dim;
+        if (cd.use_diff) {
+            const orc_coef ce = coef_of(&cd, dim, e, nqd);
+            simplex_element_matrix(dim, p, V, &ce, nqd, xd, wd, Ae + (size_t)e * nd * nd);
+        }
+        if (ccm.use_conv || ccm.use_mass) {
+            const orc_coef ce = coef_of(&ccm, dim, e, nqc);
+            simplex_element_matrix(dim, p, V, &ce, nqc, xc, wc, Ae + (size_t)e * nd * nd);
+        }
     }
     orc_csr *A = csr_from_elements(nd, ne, dofmap, nl, Ae);
     free(Ae);

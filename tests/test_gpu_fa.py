@@ -140,11 +140,16 @@ def test_fa_reproducible_and_coefficient_arrays(gpu_ctx):
     gpu_ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
     _, _, v2 = gpu_ctx.fa_csr()
     np.testing.assert_array_equal(v1, v2)
-    nq = gpu_ctx.rule_size(cdfem.RULE_OPERATOR)
-    xyz = gpu_ctx.quadrature_points(cdfem.RULE_OPERATOR)
-    assert xyz.shape == (gm.ne, nq, 3)
-    gpu_ctx.fa_setup(kinds=7, kappa=0.0, kappa_q=np.full(gm.ne * nq, 0.1), alpha=1.0,
-                     conv_q=np.tile(np.array(C3), gm.ne * nq), mass=0.0, mass_q=np.full(gm.ne * nq, 1.0))
+    # MFEM's per-integrator rules on P2 tets: diffusion order 2 (4 points), convection / mass order 4
+    # (11 points); the operator rule of the tensor elements does not exist here
+    nqd, nqc, nqm = (gpu_ctx.rule_size(r) for r in (cdfem.RULE_DIFFUSION, cdfem.RULE_CONVECTION, cdfem.RULE_MASS))
+    assert (nqd, nqc, nqm) == (4, 11, 11)
+    with pytest.raises(cdfem.CdfemError):
+        gpu_ctx.rule_size(cdfem.RULE_OPERATOR)
+    xyz = gpu_ctx.quadrature_points(cdfem.RULE_DIFFUSION)
+    assert xyz.shape == (gm.ne, nqd, 3)
+    gpu_ctx.fa_setup(kinds=7, kappa=0.0, kappa_q=np.full(gm.ne * nqd, 0.1), alpha=1.0,
+                     conv_q=np.tile(np.array(C3), gm.ne * nqc), mass=0.0, mass_q=np.full(gm.ne * nqm, 1.0))
     _, _, v3 = gpu_ctx.fa_csr()
     assert np.abs(v3 - v1).max() <= 1e-14 * np.abs(v1).max()
     # a variable kappa(x) = 1 + x: x^T K 1 = 0 still (constants in the kernel), K symmetric

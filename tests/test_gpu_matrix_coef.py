@@ -23,10 +23,11 @@ def _spd_tensors(rng, n, dim):
 
 
 def _coeffs(ctx, m, rng):
-    nq = ctx.rule_size(cdfem.RULE_OPERATOR)
-    n = m.ne * nq
-    return dict(kappa=0.05, kappa_q=rng.uniform(0.01, 0.2, n), kmat_q=_spd_tensors(rng, n, m.dim),
-                conv_q=rng.uniform(-1, 1, n * m.dim), mass_q=rng.uniform(0.5, 2.0, n), alpha=0.7)
+    """random per-point coefficients, each at the points of its integrator's rule (on simplices MFEM's
+    GetRule: diffusion 2p - 2, convection and mass 2p; on quads / hexes one shared rule)"""
+    nd, nc, nm = (m.ne * ctx.rule_size(r) for r in (cdfem.RULE_DIFFUSION, cdfem.RULE_CONVECTION, cdfem.RULE_MASS))
+    return dict(kappa=0.05, kappa_q=rng.uniform(0.01, 0.2, nd), kmat_q=_spd_tensors(rng, nd, m.dim),
+                conv_q=rng.uniform(-1, 1, nc * m.dim), mass_q=rng.uniform(0.5, 2.0, nm), alpha=0.7)
 
 
 TENSOR = [(2, 6, 2, 0.15, False), (3, 4, 2, 0.1, False), (3, 4, 2, 0.0, True), (3, 3, 4, 0.1, False),
@@ -82,8 +83,12 @@ def test_ale_operator(gpu_ctx, kind, mesh):
         om = O.KuhnMesh(2, 8, 2, perturb=0.1)
         gm = cdfem.Mesh(2, 2, om.verts, om.dofmap, om.nl, om.ess, simplex=True)
     gpu_ctx.upload_mesh(gm)
-    xy = gpu_ctx.quadrature_points(cdfem.RULE_OPERATOR).reshape(-1, 2)
-    J, metric, phi, div = O.ale_coefficients(kind, xy, t0, t1, alpha, dt)
+    # every coefficient at its integrator's rule (the three coincide on quads)
+    pts = {r: gpu_ctx.quadrature_points(r).reshape(-1, 2)
+           for r in (cdfem.RULE_DIFFUSION, cdfem.RULE_CONVECTION, cdfem.RULE_MASS)}
+    metric = O.ale_coefficients(kind, pts[cdfem.RULE_DIFFUSION], t0, t1, alpha, dt)[1]
+    phi = O.ale_coefficients(kind, pts[cdfem.RULE_CONVECTION], t0, t1, alpha, dt)[2]
+    J, _, _, div = O.ale_coefficients(kind, pts[cdfem.RULE_MASS], t0, t1, alpha, dt)
     setup = gpu_ctx.fa_setup if gm.simplex else gpu_ctx.pa_setup
     # Mass(J) + Mass(-div phi) -> one mass coefficient; Convection(phi, -1) -> alpha = -1
     setup(kinds=7, kappa=0.0, kmat_q=metric, alpha=-1.0, conv_q=phi.ravel(), mass=0.0, mass_q=J - div)

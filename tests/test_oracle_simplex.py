@@ -239,3 +239,57 @@ def test_mfem_simplex_rules_exact_and_shared(dim, orders):
                     continue
                 exact = math.prod(math.factorial(k) for k in e) / math.factorial(dim + tot)
                 assert abs(np.sum(wo * np.prod(xo ** np.array(e), axis=1)) - exact) <= 1e-15
+
+
+@pytest.mark.parametrize("dim,p", [(2, 1), (2, 2), (2, 3), (3, 1), (3, 2)])
+def test_per_integrator_rules_are_mfems(dim, p):
+    """MFEM's GetRule on affine simplices: diffusion on the tabulated rule of order 2p - 2,
+    convection and mass on order 2p.  With per-point coefficients (the quantities that make the rule
+    matter), one element's diffusion, convection and mass matrices from the oracle equal a direct
+    restatement here: sum over those rules' points of w_q k_q (A grad phi_i).(A grad phi_j) / det J,
+    w_q phi_i (c_q . A grad phi_j), w_q s_q det J phi_i phi_j, with the product's host basis and rules
+    (cdfem_simplex_basis / cdfem_simplex_rule_order)."""
+    import ctypes as C
+    import cdfem
+    L = cdfem.lib()
+    dp = C.POINTER(C.c_double)
+    L.cdfem_simplex_rule_order.argtypes = [C.c_int, C.c_int, dp, dp]
+    L.cdfem_simplex_basis.argtypes = [C.c_int, C.c_int, C.c_int, dp, dp, dp]
+
+    def rule(order):
+        n = L.cdfem_simplex_rule_order(dim, order, None, None)
+        xi, w = np.zeros(n * dim), np.zeros(n)
+        L.cdfem_simplex_rule_order(dim, order, xi.ctypes.data_as(dp), w.ctypes.data_as(dp))
+        return xi.reshape(n, dim), w
+    nd = {(2, 1): 3, (2, 2): 6, (2, 3): 10, (3, 1): 4, (3, 2): 10}[(dim, p)]
+
+    def basis(xi):
+        phi, dphi = np.zeros(len(xi) * nd), np.zeros(len(xi) * nd * dim)
+        L.cdfem_simplex_basis(dim, p, len(xi), np.ascontiguousarray(xi).ctypes.data_as(dp), phi.ctypes.data_as(dp),
+                              dphi.ctypes.data_as(dp))
+        return phi.reshape(len(xi), nd), dphi.reshape(len(xi), nd, dim)
+    rng = np.random.default_rng(3)
+    V = np.eye(dim + 1, dim, -1) * 1.0 + rng.uniform(-0.1, 0.1, (dim + 1, dim))   # a perturbed reference simplex
+    J = (V[1:] - V[0]).T
+    det = np.linalg.det(J)
+    A = np.linalg.inv(J).T * det                                                     # adj(J)^T
+    xd, wd = rule(max(2 * p - 2, 0))
+    xc, wc = rule(2 * p)
+    assert (len(wd), len(wc)) == {2: {1: (1, 3), 2: (3, 6), 3: (6, 12)}, 3: {1: (1, 4), 2: (4, 11)}}[dim][p]
+    kq, cq, sq = rng.uniform(0.5, 2, len(wd)), rng.uniform(-1, 1, (len(wc), dim)), rng.uniform(0.5, 2, len(wc))
+    pd, gd = basis(xd)
+    pc, gc = basis(xc)
+    Kd = np.einsum("q,qia,qja->ij", wd * kq / det, gd @ A.T, gd @ A.T)
+    Cc = np.einsum("q,qi,qj->ij", wc, pc, np.einsum("qa,qja->qj", cq, gc @ A.T))
+    Mm = np.einsum("q,qi,qj->ij", wc * sq * det, pc, pc)
+
+    class M1:
+        pass
+    m = M1()
+    m.dim, m.p, m.ne, m.nl = dim, p, 1, nd
+    m.verts = V[None].copy()
+    m.dofmap = np.arange(nd, dtype=np.int32)[None]
+    for kinds, want, kw in ((O.DIFFUSION, Kd, dict(kappa_q=kq)), (O.CONVECTION, Cc, dict(c_q=cq.ravel())),
+                            (O.MASS, Mm, dict(s_q=sq))):
+        got = O.fa_assemble_q(m, kinds=kinds, simplex=True, **kw).to_scipy().toarray()
+        assert np.abs(got - want).max() <= 1e-13 * np.abs(want).max(), kinds
