@@ -555,9 +555,6 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     }
     double *x = c->d_w[2], *w = c->d_w[4], *V = c->d_gm, *part = c->d_gm_part;
     GmresState *st = c->d_gmst, *poll = c->h_gmpoll;
-    // structured brick operator on one rank: the Arnoldi step's face rows are formed by pass 1 from
-    // the brick face partials (no separate face pass; bitwise the same w)
-    const bool fuse_faces = use_brick(c) && !c->fa_ready && !multi_rank(c) && !ilu && n < ((int64_t)1 << 31);
     // the step's last scalar kernel has written poll[slot] (post_poll in gmres.hip); the event
     // marks its completion for the host
     auto post = [&](int slot) { HIPCHK(hipEventRecord(c->gm_ev[slot], c->stream)); };
@@ -585,18 +582,10 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
         post(0);
         if (wait(0).done) break;
         for (int j = 0; j < m; ++j) {
-            const double *vj = V + (int64_t)j * ldv;
-            if (fuse_faces) {  // brick interiors here, the face rows inside pass 1
-                prof_mark(c, CDFEM_K_APPLY, true);
-                HIPCHK(launch_brick_mult(c, vj, w, true, 1));
-                prof_mark(c, CDFEM_K_APPLY, false);
-            } else {
-                op_apply_global(c, vj, w, true);
-            }
+            op_apply_global(c, V + (int64_t)j * ldv, w, true);
             if (ilu) HIPCHK(ilu_apply(c));  // w <- (LU)^{-1} A v_j, in ilu.z
             prof_mark(c, CDFEM_K_ORTH, true);
-            HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, ldv, part, st, m, &poll[j & 1],
-                                  fuse_faces ? vj : nullptr));
+            HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, ldv, part, st, m, &poll[j & 1]));
             prof_mark(c, CDFEM_K_ORTH, false);
             post(j & 1);
             if (j > 0 && wait((j - 1) & 1).cycle_done) break;

@@ -407,10 +407,8 @@ hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it);
 // poll: pinned host slot the step's last scalar kernel writes the state head into (solve_gmres)
 hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
                               double *part, GmresState *st, bool first, double rtol, double atol, GmresState *poll);
-// faces_x != nullptr (structured brick operator, one rank): w holds only the brick-interior rows of
-// A_c V_j (launch_brick_mult which = 1) and pass 1 forms the face rows itself (faces_x = V_j)
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m, GmresState *poll, const double *faces_x = nullptr);
+                          GmresState *st, int m, GmresState *poll);
 hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st, GmresState *poll);
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 // ILU(0) (ilu_kernels.hip): factor + capture once per operator; apply: ilu.z = (LU)^{-1} d_w[4]

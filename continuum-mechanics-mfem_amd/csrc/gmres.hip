@@ -21,9 +21,7 @@
 
 #include <algorithm>
 
-#include "brick_common.hpp"
 #include "cdfem_internal.hpp"
-#include "pa_core.hpp"
 #include "reduce.hpp"
 
 namespace cdfem {
@@ -118,23 +116,10 @@ k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st,
 // dropped).  Each wave parks its wave sums in LDS, so the whole step needs ONE barrier before the
 // block sums.  Measured at C4 (orthogonalisation per step): one barrier per batch of 8, 93.9 us;
 // one barrier in all, batches of 8 / 4 / 2 / 1: 85.7 / 83.2 / 82.6 / 82.1 us.
-// S > 0 (structured brick operator, brick patch size S): w holds only the brick-interior rows of
-// A_c V_j (k_brick3d, which = 1); the rows on brick faces are formed here from the face partials,
-// A_c x = x on essential rows, exactly as k_brick_faces would (same sum order: bitwise the same w),
-// so the face pass and its y round trip disappear from the GMRES step.
-struct GmFaces {
-    const double *x;      // V_j (the operator's input)
-    const uint8_t *ess;
-    const double *face;   // brick face partials
-    FastDiv fLx, fLxy;
-    int Lx, Lxy, nbx, nby, nbz;
-};
-
-template <int BAT, int EPT, int S>
+template <int BAT, int EPT>
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double *__restrict__ V, int64_t n,
-           int64_t ldv, int64_t skip_lo, double *__restrict__ part, int nb, const GmresState *__restrict__ st,
-           const GmFaces fc)
+           int64_t ldv, int64_t skip_lo, double *__restrict__ part, int nb, const GmresState *__restrict__ st)
 {
     __shared__ double sh[kGmMaxRestart + 1][kRedThreads / 64];
     if (st->cycle_done) return;
@@ -148,15 +133,7 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
         const int64_t k = base + (int64_t)e * kRedThreads;
         double v = 0.0;
         if (k < n) {
-            double y = w[k];
-            if constexpr (S > 0) {
-                constexpr int s1 = S - 1;
-                const uint32_t gz = fdiv((uint32_t)k, fc.fLxy), rem = (uint32_t)k - gz * (uint32_t)fc.Lxy;
-                const uint32_t gy = fdiv(rem, fc.fLx), gx = rem - gy * (uint32_t)fc.Lx;
-                if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0)
-                    y = fc.ess[k] ? fc.x[k] : brick_face_sum<S>(fc.face, (int)gx, (int)gy, (int)gz, fc.nbx, fc.nby, fc.nbz);
-            }
-            v = sj * y;
+            v = sj * w[k];
             if (dinv) v *= dinv[k];
             w[k] = v;
         }
@@ -503,7 +480,7 @@ static int orth_ept(cdfem_ctx *c)
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gm_pass1<kGmBatch, 4, 0>, kRedThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gm_pass1<kGmBatch, 4>, kRedThreads, 0);
     const int64_t cap = (int64_t)std::max(cus, 1) * std::max(per, 1);
     int ept = 8;
     for (int e : {4, 5, 6, 8})
@@ -518,33 +495,13 @@ static int orth_ept(cdfem_ctx *c)
 
 template <int EPT>
 static void orth_passes(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                        GmresState *st, int m, GmresState *poll, const double *faces_x)
+                        GmresState *st, int m, GmresState *poll)
 {
     const int nb = (int)((c->nl + (int64_t)kRedThreads * EPT - 1) / ((int64_t)kRedThreads * EPT));
     const int64_t n = c->nl;
     const bool mr = multi_rank(c);
-    GmFaces fc{};
-    if (faces_x) {
-        fc.x = faces_x;
-        fc.ess = c->d_ess;
-        fc.face = c->d_face;
-        fc.Lx = (int)c->Lx;
-        fc.Lxy = (int)(c->Lx * c->Ly);
-        fc.fLx = make_fastdiv((uint32_t)c->Lx);
-        fc.fLxy = make_fastdiv((uint32_t)(c->Lx * c->Ly));
-        fc.nbx = c->nbx;
-        fc.nby = c->nby;
-        fc.nbz = c->nbz;
-    }
-    if (faces_x && c->p == 2)
-        hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT, kBrick * 2 + 1>), dim3(nb), dim3(kRedThreads), 0, c->stream, w,
-                           dinv, V, n, ldv, owned_from(c), part, nb, st, fc);
-    else if (faces_x && c->p == 1)
-        hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT, kBrick * 1 + 1>), dim3(nb), dim3(kRedThreads), 0, c->stream, w,
-                           dinv, V, n, ldv, owned_from(c), part, nb, st, fc);
-    else
-        hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT, 0>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n,
-                           ldv, owned_from(c), part, nb, st, fc);
+    hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv,
+                       owned_from(c), part, nb, st);
     hipLaunchKernelGGL(k_gm_dots_fin_mb, dim3(m + 1), dim3(kRedThreads), 0, c->stream, part, nb, st, mr ? 1 : 0);
     if (mr) {
         comm_allreduce(c, red_of(st), m + 1);
@@ -561,13 +518,13 @@ static void orth_passes(cdfem_ctx *c, double *w, const double *dinv, double *V, 
 }
 
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m, GmresState *poll, const double *faces_x)
+                          GmresState *st, int m, GmresState *poll)
 {
     switch (orth_ept(c)) {
-    case 5: orth_passes<5>(c, w, dinv, V, ldv, part, st, m, poll, faces_x); break;
-    case 6: orth_passes<6>(c, w, dinv, V, ldv, part, st, m, poll, faces_x); break;
-    case 8: orth_passes<8>(c, w, dinv, V, ldv, part, st, m, poll, faces_x); break;
-    default: orth_passes<4>(c, w, dinv, V, ldv, part, st, m, poll, faces_x); break;
+    case 5: orth_passes<5>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    case 6: orth_passes<6>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    case 8: orth_passes<8>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    default: orth_passes<4>(c, w, dinv, V, ldv, part, st, m, poll); break;
     }
     return hipGetLastError();
 }
