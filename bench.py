@@ -135,10 +135,30 @@ def host_cores(args):
 CPU_SAMPLES = 5  # median of >= 5 timed samples after one warm-up
 
 
+def _cpu_idle(window=0.5):
+    """Idle fraction of every CPU over a short window (/proc/stat), {} when unreadable."""
+    def snap():
+        out = {}
+        for line in open("/proc/stat"):
+            if line.startswith("cpu") and line[3].isdigit():
+                f = line.split()
+                vals = [int(v) for v in f[1:]]
+                out[int(f[0][3:])] = (vals[3] + (vals[4] if len(vals) > 4 else 0), sum(vals))
+        return out
+    try:
+        a = snap()
+        time.sleep(window)
+        b = snap()
+    except (OSError, ValueError, IndexError):
+        return {}
+    return {c: (b[c][0] - a[c][0]) / max(b[c][1] - a[c][1], 1) for c in b if c in a}
+
+
 def pick_cpus(n):
-    """n CPUs of this job's affinity mask for the CPU baseline: distinct physical cores of one
-    package (the package of the lowest allowed CPU first), so the threads neither share a core nor
-    straddle sockets.  Falls back to the lowest allowed CPUs when sysfs topology is unreadable."""
+    """n CPUs of this job's affinity mask for the CPU baseline, one per physical core, on one
+    package: the package with the most idle time, and in it the most idle cores over a 0.5 s
+    window (other jobs share the host's cores).  Falls back to the lowest allowed CPUs when the
+    topology is unreadable."""
     allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
 
     def topo(c, f):
@@ -146,22 +166,22 @@ def pick_cpus(n):
             return int(open(f"/sys/devices/system/cpu/cpu{c}/topology/{f}").read())
         except (OSError, ValueError):
             return None
-    pkg0 = topo(allowed[0], "physical_package_id")
-    seen, out = set(), []
-    for pass_pkg in (True, False):
-        for c in allowed:
-            core = (topo(c, "physical_package_id"), topo(c, "core_id"))
-            if core in seen or (pass_pkg and core[0] != pkg0):
-                continue
-            seen.add(core)
-            out.append(c)
-            if len(out) == n:
-                return out
+    idle = _cpu_idle()
+    cores = {}  # (package, core) -> [cpus]
+    for c in allowed:
+        cores.setdefault((topo(c, "physical_package_id"), topo(c, "core_id")), []).append(c)
+    # a core's idleness: its least idle hardware thread (a busy sibling slows the core)
+    score = {k: min(idle.get(c, 1.0) for c in v) for k, v in cores.items()}
+    pkgs = {}
+    for k, sc in score.items():
+        pkgs[k[0]] = pkgs.get(k[0], 0.0) + sc
+    order = sorted(cores, key=lambda k: (-pkgs[k[0]], k[0], -score[k], cores[k][0]))
+    out = [cores[k][0] for k in order][:n]
     for c in allowed:  # fewer physical cores than threads: SMT siblings too
+        if len(out) >= n:
+            break
         if c not in out:
             out.append(c)
-        if len(out) == n:
-            break
     return out
 
 
@@ -185,7 +205,7 @@ class PinnedThreads:
         return False
 
     def record(self):
-        return {"pinned_cpus": f"{len(self.cpus)} cores: {self.cpus[0]}..{self.cpus[-1]}",
+        return {"pinned_cpus": f"{len(self.cpus)} cores: " + ",".join(str(c) for c in sorted(self.cpus)),
                 "threads_pinned": self.pinned}
 
 
