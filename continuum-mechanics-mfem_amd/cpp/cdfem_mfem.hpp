@@ -292,71 +292,274 @@ public:
 };
 
 // ---- containers ---------------------------------------------------------------------------------
+namespace detail {
+// Device memory behind Vectors: one allocation/copy context per process, a free list per size (the
+// reference's time loop builds a ParLinearForm, a PetscParMatrix and a solver every step,
+// diffusion_mms.cpp:428-456), never handed back (process lifetime).  CDFEM_SHIM_STATS=1 prints the
+// host<->device traffic of the Vectors at exit (tests/test_cpp_driver.py counts it per time step).
+struct DeviceMemory {
+    cdfem_ctx *ctx = nullptr;
+    std::map<size_t, std::vector<double *>> free_;
+    unsigned long long h2d = 0, d2h = 0, h2d_calls = 0, d2h_calls = 0;
+};
+inline void print_shim_stats();
+inline DeviceMemory &devmem()
+{
+    static DeviceMemory *m = [] {
+        auto *d = new DeviceMemory();  // leaked on purpose: Vectors may outlive every static
+        if (const char *e = std::getenv("CDFEM_SHIM_STATS"); e && *e && *e != '0') std::atexit(print_shim_stats);
+        return d;
+    }();
+    return *m;
+}
+inline void print_shim_stats()
+{
+    const DeviceMemory &m = devmem();
+    std::fprintf(stderr, "shim_transfers rank %d h2d_bytes %llu h2d_calls %llu d2h_bytes %llu d2h_calls %llu\n",
+                 Mpi::WorldRank(), m.h2d, m.h2d_calls, m.d2h, m.d2h_calls);
+}
+inline cdfem_ctx *mem_ctx()
+{
+    DeviceMemory &m = devmem();
+    if (!m.ctx) check(cdfem_create(device_id(), &m.ctx), nullptr, "cdfem_create (no GPU? there is no CPU path)");
+    return m.ctx;
+}
+inline double *dev_alloc(size_t n)
+{
+    DeviceMemory &m = devmem();
+    auto it = m.free_.find(n);
+    if (it != m.free_.end() && !it->second.empty()) {
+        double *p = it->second.back();
+        it->second.pop_back();
+        return p;
+    }
+    void *p = nullptr;
+    check(cdfem_alloc(mem_ctx(), n * sizeof(double), &p), mem_ctx(), "cdfem_alloc");
+    return static_cast<double *>(p);
+}
+inline void dev_release(double *p, size_t n)
+{
+    if (p) devmem().free_[n].push_back(p);
+}
+inline void dev_copy(void *dst, int dw, const void *src, int sw, size_t n)
+{
+    if (n == 0) return;
+    DeviceMemory &m = devmem();
+    if (dw == CDFEM_DEVICE && sw == CDFEM_HOST) m.h2d += n * sizeof(double), ++m.h2d_calls;
+    if (dw == CDFEM_HOST && sw == CDFEM_DEVICE) m.d2h += n * sizeof(double), ++m.d2h_calls;
+    check(cdfem_memcpy(mem_ctx(), dst, dw, src, sw, n * sizeof(double)), mem_ctx(), "cdfem_memcpy");
+}
+}  // namespace detail
+
+// MFEM's Vector with its Memory<double> semantics (UseDevice): a host array and a device copy with
+// validity flags.  Host access (GetData, operator[], HostRead / HostWrite / HostReadWrite) copies the
+// device data back when only the device copy is current; the forms, FormLinearSystem, the solvers
+// and RecoverFEMSolution work on the device copy (Read / Write / ReadWrite), so a time loop's vectors
+// stay in HBM between those calls and cross PCIe only where the host touches them (coefficient
+// projection, error norms).
 class Vector {
 public:
     Vector() = default;
     explicit Vector(int n) : d_((size_t)n, 0.0) {}
     Vector(const double *p, int n) : d_(p, p + n) {}
-    virtual ~Vector() = default;
+    Vector(const Vector &o) { assign(o); }
+    Vector(Vector &&o) noexcept { steal(o); }
+    Vector &operator=(const Vector &o)
+    {
+        if (this != &o) assign(o);
+        return *this;
+    }
+    Vector &operator=(Vector &&o) noexcept
+    {
+        if (this != &o) {
+            detail::dev_release(dev_, d_.size());
+            steal(o);
+        }
+        return *this;
+    }
+    virtual ~Vector() { detail::dev_release(dev_, d_.size()); }
     int Size() const { return (int)d_.size(); }
-    void SetSize(int n) { d_.resize((size_t)n, 0.0); }
-    double *GetData() { return d_.data(); }
-    const double *GetData() const { return d_.data(); }
-    double &operator[](int i) { return d_[(size_t)i]; }
-    double operator[](int i) const { return d_[(size_t)i]; }
-    double &operator()(int i) { return d_[(size_t)i]; }
-    double operator()(int i) const { return d_[(size_t)i]; }
+    void SetSize(int n)
+    {
+        if ((size_t)n == d_.size()) return;
+        sync_host();
+        detail::dev_release(dev_, d_.size());
+        dev_ = nullptr;
+        dev_ok_ = false;
+        d_.resize((size_t)n, 0.0);
+    }
+    // host access
+    const double *HostRead() const
+    {
+        sync_host();
+        return d_.data();
+    }
+    double *HostReadWrite()
+    {
+        sync_host();
+        dev_ok_ = false;
+        return d_.data();
+    }
+    double *HostWrite()
+    {
+        host_ok_ = true;
+        dev_ok_ = false;
+        return d_.data();
+    }
+    // device access (HBM pointers for the C-ABI's CDFEM_DEVICE calls)
+    const double *Read() const
+    {
+        if (!dev_) dev_ = detail::dev_alloc(d_.size());
+        if (!dev_ok_) {
+            detail::dev_copy(dev_, CDFEM_DEVICE, d_.data(), CDFEM_HOST, d_.size());
+            dev_ok_ = true;
+        }
+        return dev_;
+    }
+    double *Write()
+    {
+        if (!dev_) dev_ = detail::dev_alloc(d_.size());
+        dev_ok_ = true;
+        host_ok_ = false;
+        return dev_;
+    }
+    double *ReadWrite()
+    {
+        Read();
+        host_ok_ = false;
+        return dev_;
+    }
+    bool DeviceIsValid() const { return dev_ok_; }
+    bool HostIsValid() const { return host_ok_; }
+
+    double *GetData() { return HostReadWrite(); }
+    const double *GetData() const { return HostRead(); }
+    double &operator[](int i) { return HostReadWrite()[(size_t)i]; }
+    double operator[](int i) const { return HostRead()[(size_t)i]; }
+    double &operator()(int i) { return HostReadWrite()[(size_t)i]; }
+    double operator()(int i) const { return HostRead()[(size_t)i]; }
     Vector &operator=(double v)
     {
         std::fill(d_.begin(), d_.end(), v);
+        HostWrite();
         return *this;
     }
     Vector &operator*=(double a)
     {
-        for (double &v : d_) v *= a;
+        for (double *p = HostReadWrite(), *e = p + d_.size(); p != e; ++p) *p *= a;
         return *this;
     }
     Vector &operator+=(const Vector &o)
     {
-        for (size_t i = 0; i < d_.size(); ++i) d_[i] += o.d_[i];
+        const double *q = o.HostRead();
+        double *p = HostReadWrite();
+        for (size_t i = 0; i < d_.size(); ++i) p[i] += q[i];
         return *this;
     }
     Vector &operator-=(const Vector &o)
     {
-        for (size_t i = 0; i < d_.size(); ++i) d_[i] -= o.d_[i];
+        const double *q = o.HostRead();
+        double *p = HostReadWrite();
+        for (size_t i = 0; i < d_.size(); ++i) p[i] -= q[i];
         return *this;
     }
     double operator*(const Vector &o) const
     {
+        const double *p = HostRead(), *q = o.HostRead();
         double s = 0.0;
-        for (size_t i = 0; i < d_.size(); ++i) s += d_[i] * o.d_[i];
+        for (size_t i = 0; i < d_.size(); ++i) s += p[i] * q[i];
         return s;
     }
     double Norml2() const { return std::sqrt((*this) * (*this)); }
     double Normlinf() const
     {
+        const double *p = HostRead();
         double m = 0.0;
-        for (double v : d_) m = std::max(m, std::fabs(v));
+        for (size_t i = 0; i < d_.size(); ++i) m = std::max(m, std::fabs(p[i]));
         return m;
     }
-    double Sum() const { return std::accumulate(d_.begin(), d_.end(), 0.0); }
+    double Sum() const
+    {
+        const double *p = HostRead();
+        return std::accumulate(p, p + d_.size(), 0.0);
+    }
+    // this += a x: on the device when both device copies are current and one side has no current
+    // host copy (rhs.Add(dt, f) of diffusion_mms.cpp:433: M u_old and the linear form, both fresh
+    // from the GPU), else on the host
     void Add(double a, const Vector &x)
     {
-        for (size_t i = 0; i < d_.size(); ++i) d_[i] += a * x.d_[i];
+        if (x.Size() != Size()) throw std::invalid_argument("Vector::Add: size");
+        if (dev_ok_ && x.dev_ok_ && !(host_ok_ && x.host_ok_) && !d_.empty()) {
+            check(cdfem_vec_axpby(detail::mem_ctx(), (int64_t)d_.size(), a, x.Read(), 1.0, ReadWrite()),
+                  detail::mem_ctx(), "cdfem_vec_axpby");
+            return;
+        }
+        const double *q = x.HostRead();
+        double *p = HostReadWrite();
+        for (size_t i = 0; i < d_.size(); ++i) p[i] += a * q[i];
     }
     void Neg()
     {
-        for (double &v : d_) v = -v;
+        for (double *p = HostReadWrite(), *e = p + d_.size(); p != e; ++p) *p = -*p;
+    }
+    // this = src[off, off + n) without a host round trip when src lives on the device
+    void SetSubVectorOf(const Vector &src, int off, int n)
+    {
+        if (off < 0 || n < 0 || off + n > src.Size()) throw std::invalid_argument("SetSubVectorOf: range");
+        SetSize(n);
+        if (src.dev_ok_ && !src.host_ok_) {
+            if (n) detail::dev_copy(Write(), CDFEM_DEVICE, src.dev_ + off, CDFEM_DEVICE, (size_t)n);
+            else Write();
+            return;
+        }
+        const double *q = src.HostRead() + off;
+        std::copy(q, q + n, HostWrite());
     }
 
 private:
-    std::vector<double> d_;
+    void sync_host() const
+    {
+        if (host_ok_) return;
+        detail::dev_copy(d_.data(), CDFEM_HOST, dev_, CDFEM_DEVICE, d_.size());
+        host_ok_ = true;
+    }
+    void assign(const Vector &o)
+    {
+        if (o.d_.size() != d_.size()) {
+            detail::dev_release(dev_, d_.size());
+            dev_ = nullptr;
+            d_.assign(o.d_.size(), 0.0);
+        }
+        if (o.dev_ok_ && !o.host_ok_) {  // device-only source: copy in HBM
+            if (!d_.empty()) detail::dev_copy(Write(), CDFEM_DEVICE, o.dev_, CDFEM_DEVICE, d_.size());
+            else Write();
+            return;
+        }
+        std::copy(o.d_.begin(), o.d_.end(), d_.begin());
+        HostWrite();
+    }
+    void steal(Vector &o)
+    {
+        d_ = std::move(o.d_);
+        dev_ = o.dev_;
+        host_ok_ = o.host_ok_;
+        dev_ok_ = o.dev_ok_;
+        o.d_.clear();
+        o.dev_ = nullptr;
+        o.host_ok_ = true;
+        o.dev_ok_ = false;
+    }
+    mutable std::vector<double> d_;  // mutable: a const read refreshes the host copy
+    mutable double *dev_ = nullptr;
+    mutable bool host_ok_ = true, dev_ok_ = false;
 };
 
 inline void subtract(const Vector &a, const Vector &b, Vector &c)
 {
     c.SetSize(a.Size());
-    for (int i = 0; i < a.Size(); ++i) c[i] = a[i] - b[i];
+    const double *p = a.HostRead(), *q = b.HostRead();
+    double *r = c.HostWrite();
+    for (int i = 0; i < a.Size(); ++i) r[i] = p[i] - q[i];
 }
 
 template <class T>
@@ -1325,6 +1528,7 @@ public:
         Mesh *m = fes.GetMesh();
         const int dim = m->Dimension();
         simplex_ = fes.Simplex();
+        points_.clear();
         auto up = simplex_ ? cdfem_mesh_upload_simplex : cdfem_mesh_upload;
         check(up(ctx_, dim, fes.GetOrder(), fes.GetNE(), fes.ElementVertices().data(), fes.GetVSize(),
                  fes.ElementDofs().data(), (int)ess.size(), ess.data()),
@@ -1348,24 +1552,37 @@ public:
     cdfem_ctx *ctx() const { return ctx_; }
     const std::vector<int32_t> &Ess() const { return ess_; }
     bool Simplex() const { return simplex_; }
-    // physical coordinates of a rule's points, element-major
-    std::vector<double> Points(int rule, int dim, int ne, int &nq) const
+    // physical coordinates of a rule's points, element-major; kept per rule (a time loop's linear
+    // form samples its coefficient at the same points every step)
+    const std::vector<double> &Points(int rule, int dim, int ne, int &nq) const
     {
-        check(cdfem_rule_size(ctx_, rule, &nq), ctx_, "cdfem_rule_size");
-        std::vector<double> xyz((size_t)ne * nq * dim);
-        check(cdfem_quadrature_points(ctx_, rule, xyz.data(), CDFEM_HOST), ctx_, "cdfem_quadrature_points");
-        return xyz;
+        auto it = points_.find(rule);
+        if (it == points_.end()) {
+            int n = 0;
+            check(cdfem_rule_size(ctx_, rule, &n), ctx_, "cdfem_rule_size");
+            std::vector<double> xyz((size_t)ne * n * dim);
+            check(cdfem_quadrature_points(ctx_, rule, xyz.data(), CDFEM_HOST), ctx_, "cdfem_quadrature_points");
+            it = points_.emplace(rule, std::make_pair(n, std::move(xyz))).first;
+        }
+        nq = it->second.first;
+        return it->second.second;
     }
-    // x (L) = P X (true dofs)
+    // x (L) = P X (true dofs), host arrays
     void Prolongate(const double *X, double *x) const
     {
         check(cdfem_prolongate(ctx_, X, x, CDFEM_HOST), ctx_, "cdfem_prolongate");
+    }
+    // the same on device vectors
+    void Prolongate(const Vector &X, Vector &x) const
+    {
+        check(cdfem_prolongate(ctx_, X.Read(), x.Write(), CDFEM_DEVICE), ctx_, "cdfem_prolongate");
     }
 
 private:
     cdfem_ctx *ctx_ = nullptr;
     std::vector<int32_t> ess_;
     bool simplex_ = false;
+    mutable std::map<int, std::pair<int, std::vector<double>>> points_;
 };
 
 inline DeviceSpace &FiniteElementSpace::Space() const
@@ -1496,7 +1713,8 @@ public:
     {
         Require(x.Size() == height, "Mult: size");
         y.SetSize(height);
-        check(cdfem_pa_mult(ctx(), x.GetData(), y.GetData(), 2, CDFEM_HOST), ctx(), "cdfem_pa_mult");
+        check(cdfem_pa_mult(ctx(), x.Read(), y.Write(), 2, CDFEM_DEVICE), ctx(), "cdfem_pa_mult");
+        check(cdfem_synchronize(ctx()), ctx(), "cdfem_synchronize");
     }
 
     // FormLinearSystem (:349-351): X = R x, B = P^T (b - A x_e) with B_ess = x_ess, both true-dof
@@ -1511,12 +1729,20 @@ public:
             dev_->Upload(*fes_, ess);
             Setup();
         }
-        Vector XL(height), BL(height);
-        check(cdfem_form_linear_system(ctx(), x.GetData(), b.GetData(), XL.GetData(), BL.GetData(), CDFEM_HOST), ctx(),
-              "cdfem_form_linear_system");
         const int nt = fes_->GetTrueVSize(), off = (int)fes_->FirstOwned();
-        X = Vector(XL.GetData() + off, nt);
-        B = Vector(BL.GetData() + off, nt);
+        if (off == 0 && nt == height) {  // one rank: the true dofs are the L-dofs
+            X.SetSize(nt);
+            B.SetSize(nt);
+            check(cdfem_form_linear_system(ctx(), x.Read(), b.Read(), X.Write(), B.Write(), CDFEM_DEVICE), ctx(),
+                  "cdfem_form_linear_system");
+        } else {
+            XL_.SetSize(height);
+            BL_.SetSize(height);
+            check(cdfem_form_linear_system(ctx(), x.Read(), b.Read(), XL_.Write(), BL_.Write(), CDFEM_DEVICE), ctx(),
+                  "cdfem_form_linear_system");
+            X.SetSubVectorOf(XL_, off, nt);
+            B.SetSubVectorOf(BL_, off, nt);
+        }
         cop_ = std::make_unique<ConstrainedPAOperator>(this, nt);
         A.Reset(cop_.get());
     }
@@ -1526,7 +1752,7 @@ public:
     {
         Require(X.Size() == fes_->GetTrueVSize(), "RecoverFEMSolution: size");
         x.SetSize(height);
-        dev_->Prolongate(X.GetData(), x.GetData());
+        dev_->Prolongate(X, x);
     }
 
     cdfem_ctx *ctx() const { return dev_->ctx(); }
@@ -1565,7 +1791,7 @@ private:
             auto it = pts.find(rule);
             if (it == pts.end()) {
                 int n = 0;
-                std::vector<double> x = dev_->Points(rule, dim, ne, n);
+                std::vector<double> x = dev_->Points(rule, dim, ne, n);  // a copy: Upload() may follow
                 it = pts.emplace(rule, std::make_pair(std::move(x), n)).first;
             }
             return it->second;
@@ -1651,6 +1877,7 @@ private:
     std::vector<std::unique_ptr<BilinearFormIntegrator>> integs_;
     std::unique_ptr<DeviceSpace> dev_;
     std::unique_ptr<ConstrainedPAOperator> cop_;
+    Vector XL_, BL_;  // FormLinearSystem's L-vectors, in HBM
 };
 using ParBilinearForm = BilinearForm;
 
@@ -1658,10 +1885,17 @@ inline void ConstrainedPAOperator::Mult(const Vector &x, Vector &y) const
 {
     if (x.Size() != height) throw std::invalid_argument("HypreParMatrix::Mult: size");
     const int nl = a_->FESpace()->GetVSize(), off = (int)a_->FESpace()->FirstOwned();
-    std::vector<double> xl((size_t)nl), yl((size_t)nl);
-    a_->DeviceCtx().Prolongate(x.GetData(), xl.data());
-    check(cdfem_pa_mult(a_->ctx(), xl.data(), yl.data(), 1, CDFEM_HOST), a_->ctx(), "cdfem_pa_mult");
-    y = Vector(yl.data() + off, height);
+    if (off == 0 && nl == height) {  // one rank: P is the identity
+        y.SetSize(height);
+        check(cdfem_pa_mult(a_->ctx(), x.Read(), y.Write(), 1, CDFEM_DEVICE), a_->ctx(), "cdfem_pa_mult");
+        check(cdfem_synchronize(a_->ctx()), a_->ctx(), "cdfem_synchronize");
+        return;
+    }
+    Vector xl(nl), yl(nl);
+    a_->DeviceCtx().Prolongate(x, xl);
+    check(cdfem_pa_mult(a_->ctx(), xl.Read(), yl.Write(), 1, CDFEM_DEVICE), a_->ctx(), "cdfem_pa_mult");
+    check(cdfem_synchronize(a_->ctx()), a_->ctx(), "cdfem_synchronize");
+    y.SetSubVectorOf(yl, off, height);
 }
 
 // ---- linear form ----------------------------------------------------------------------------------
@@ -1685,15 +1919,18 @@ public:
         DeviceSpace &dev = fes_->Space();
         const int dim = fes_->GetMesh()->Dimension();
         int nq = 0;
-        const std::vector<double> xyz = dev.Points(CDFEM_RULE_LINEARFORM, dim, fes_->GetNE(), nq);
-        std::vector<double> fq(xyz.size() / dim, 0.0);
+        const std::vector<double> &xyz = dev.Points(CDFEM_RULE_LINEARFORM, dim, fes_->GetNE(), nq);
+        Vector fq((int)(xyz.size() / dim));
+        double *f = fq.HostWrite();
+        std::fill(f, f + fq.Size(), 0.0);
         for (auto &li : integs_) {
             auto *d = dynamic_cast<DomainLFIntegrator *>(li.get());
             if (!d) throw std::invalid_argument("LinearForm: only DomainLFIntegrator is supported");
             const std::vector<double> s = Sample(*d->Q, xyz, dim, nq);
-            for (size_t i = 0; i < s.size(); ++i) fq[i] += s[i];
+            for (size_t i = 0; i < s.size(); ++i) f[i] += s[i];
         }
-        check(cdfem_lf_assemble(dev.ctx(), fq.data(), GetData(), CDFEM_HOST), dev.ctx(), "cdfem_lf_assemble");
+        // the point values cross PCIe (host Coefficient::Eval); the assembled vector stays in HBM
+        check(cdfem_lf_assemble(dev.ctx(), fq.Read(), Write(), CDFEM_DEVICE), dev.ctx(), "cdfem_lf_assemble");
     }
 
 private:
@@ -1785,10 +2022,9 @@ public:
     // MFEM ParGridFunction::GetTrueDofs / SetFromTrueDofs (R and P)
     void GetTrueDofs(Vector &tv) const
     {
-        const int off = (int)fes_->FirstOwned();
-        tv = Vector(GetData() + off, fes_->GetTrueVSize());
+        tv.SetSubVectorOf(*this, (int)fes_->FirstOwned(), fes_->GetTrueVSize());
     }
-    void SetFromTrueDofs(const Vector &tv) { fes_->Space().Prolongate(tv.GetData(), GetData()); }
+    void SetFromTrueDofs(const Vector &tv) { fes_->Space().Prolongate(tv, *this); }
 
     // ||u_h - u||_L2 over all ranks; tensor elements: Gauss rule of order max(2, 2p+3) or irs[geom]
     double ComputeL2Error(Coefficient &exact, const IntegrationRule *irs[] = nullptr) const
@@ -2020,12 +2256,19 @@ protected:
         cdfem_solver_result res{};
         const BilinearForm *a = oper->Form();
         const int nl = a->FESpace()->GetVSize(), off = (int)a->FESpace()->FirstOwned();
-        std::vector<double> bl((size_t)nl), xl((size_t)nl);
-        a->DeviceCtx().Prolongate(b.GetData(), bl.data());
         cdfem_ctx *c = a->ctx();
-        const int rc = cdfem_solve(c, &prm, bl.data(), xl.data(), CDFEM_HOST, &res);
+        int rc;
+        if (off == 0 && nl == height && &b != &x) {  // one rank: P is the identity
+            x.SetSize(height);
+            rc = cdfem_solve(c, &prm, b.Read(), x.Write(), CDFEM_DEVICE, &res);
+        } else {
+            bl_.SetSize(nl);
+            xl_.SetSize(nl);
+            a->DeviceCtx().Prolongate(b, bl_);
+            rc = cdfem_solve(c, &prm, bl_.Read(), xl_.Write(), CDFEM_DEVICE, &res);
+            if (rc == CDFEM_OK || rc == CDFEM_ERR_NOT_CONVERGED) x.SetSubVectorOf(xl_, off, height);
+        }
         if (rc != CDFEM_OK && rc != CDFEM_ERR_NOT_CONVERGED) check(rc, c, "cdfem_solve");
-        x = Vector(xl.data() + off, height);
         converged = res.converged != 0;
         final_iter = res.iterations;
         final_norm = res.final_norm;
@@ -2035,6 +2278,7 @@ protected:
                         res.initial_norm, converged ? "converged" : "NOT converged");
     }
     const ConstrainedPAOperator *oper = nullptr;
+    mutable Vector bl_, xl_;  // the solve's L-vectors, in HBM
     double rel_tol = 0.0, abs_tol = 0.0;
     int max_iter = 10, print_level = -1;
     int pc_kind = CDFEM_PC_NONE;

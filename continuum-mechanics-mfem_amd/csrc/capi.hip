@@ -101,6 +101,8 @@ void free_mesh(cdfem_ctx *c)
     c->d_rperm = nullptr; c->d_pv[0] = c->d_pv[1] = nullptr; c->d_dinv_p = nullptr;
     dfree(c->d_svals_c);
     c->d_svals_c = nullptr;
+    dfree(c->d_lfq);
+    c->lfq_cap = 0;
     ilu_free(c);
     partition_free(c);
     c->nslices = c->nstored = 0;
@@ -556,7 +558,9 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     double *x = c->d_w[2], *w = c->d_w[4], *V = c->d_gm, *part = c->d_gm_part;
     GmresState *st = c->d_gmst, *poll = c->h_gmpoll;
     // the step's last scalar kernel has written poll[slot] (post_poll in gmres.hip); the event
-    // marks its completion for the host
+    // marks its completion for the host.  (Measured alternatives, profiles/r03/ab_c2_gmres_poll.txt:
+    // spinning on a stamp in pinned memory, 392.2 / 392.0 against 392.3 us per C2 step; polling every
+    // 2 / 4 / 30 steps, 390.3 / 388.4 / 388.0 against 391.5: the host wait is not on the critical path.)
     auto post = [&](int slot) { HIPCHK(hipEventRecord(c->gm_ev[slot], c->stream)); };
     auto wait = [&](int slot) -> const GmresState & {
         HIPCHK(hipEventSynchronize(c->gm_ev[slot]));
@@ -701,6 +705,18 @@ int cdfem_memcpy(cdfem_ctx *c, void *dst, int dw, const void *src, int sw, size_
                                              : (sw == CDFEM_DEVICE ? hipMemcpyDeviceToHost
                                                                    : hipMemcpyHostToHost);
         HIPCHK(hipMemcpyAsync(dst, src, bytes, k, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_vec_axpby(cdfem_ctx *c, int64_t n, double a, const double *x, double b, double *y)
+{
+    return guarded(c, [&] {
+        if (n < 0) throw ArgError("n < 0");
+        if (n == 0) return CDFEM_OK;
+        if (!x || !y) throw ArgError("null vector");
+        HIPCHK(launch_axpby_n(c, n, a, x, b, y));
         HIPCHK(hipStreamSynchronize(c->stream));
         return CDFEM_OK;
     });
@@ -1326,7 +1342,12 @@ int cdfem_lf_assemble(cdfem_ctx *c, const double *f_q, double *b, int where)
         require_mesh(c);
         if (!f_q || !b) throw ArgError("null vector");
         const size_t n = (size_t)c->ne * (c->geom != 0 ? c->nq_lf : nq_of(c, c->rule_lf));
-        double *dfq = dalloc<double>(n);
+        if (c->lfq_cap < n) {  // kept: a time loop assembles a linear form every step
+            dfree(c->d_lfq);
+            c->d_lfq = dalloc<double>(n);
+            c->lfq_cap = n;
+        }
+        double *dfq = c->d_lfq;
         HIPCHK(hipMemcpyAsync(dfq, f_q, n * 8, where == CDFEM_DEVICE ? hipMemcpyDeviceToDevice
                                                                      : hipMemcpyHostToDevice, c->stream));
         double *db = where == CDFEM_DEVICE ? b : c->d_w[1];
@@ -1335,7 +1356,6 @@ int cdfem_lf_assemble(cdfem_ctx *c, const double *f_q, double *b, int where)
         HIPCHK(launch_e2l(c, c->d_Ye, nullptr, db, false, 0));
         dev_out(c, b, where, db, c->nl);
         HIPCHK(hipStreamSynchronize(c->stream));
-        dfree(dfq);
         return CDFEM_OK;
     });
 }

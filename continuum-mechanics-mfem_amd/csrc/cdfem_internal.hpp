@@ -241,6 +241,8 @@ struct cdfem_ctx {
     double *d_gm = nullptr;             // GMRES basis (restart+1) * nl
     int gm_cap = 0;
     double *d_gm_part = nullptr;        // GMRES partials [(restart+1) * blocks]
+    double *d_lfq = nullptr;            // cdfem_lf_assemble: the point values (kept across calls)
+    size_t lfq_cap = 0;
     cdfem::GmresState *d_gmst = nullptr;   // device GMRES state
     cdfem::GmresState *h_gmpoll = nullptr; // pinned, 2 poll slots of kGmPollBytes
     hipEvent_t gm_ev[2] = {};
@@ -298,6 +300,7 @@ hipError_t launch_e2l(cdfem_ctx *c, const double *Ye, const double *x, double *y
 hipError_t launch_set_ess(cdfem_ctx *c, double *y, const double *x);          // y[ess] = x[ess]
 hipError_t launch_mask_ess(cdfem_ctx *c, const double *x, double *y);        // y = x, y[ess] = 0
 hipError_t launch_axpby(cdfem_ctx *c, double a, const double *x, double b, double *y);  // y = a x + b y
+hipError_t launch_axpby_n(cdfem_ctx *c, int64_t n, double a, const double *x, double b, double *y);  // n entries
 hipError_t launch_dinv(cdfem_ctx *c, const double *diag, double *dinv);      // 1/diag, ess -> 1
 // CG pieces (MFEM CGSolver semantics)
 hipError_t launch_cg_init(cdfem_ctx *c, const double *B, double *x, double *r, double *z, double *d,

@@ -613,6 +613,12 @@ hipError_t launch_axpby(cdfem_ctx *c, double a, const double *x, double b, doubl
     return hipGetLastError();
 }
 
+hipError_t launch_axpby_n(cdfem_ctx *c, int64_t n, double a, const double *x, double b, double *y)
+{
+    hipLaunchKernelGGL(k_axpby, dim3(red_grid(c, n)), dim3(kRedThreads), 0, c->stream, a, x, b, y, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_dinv(cdfem_ctx *c, const double *diag, double *dinv)
 {
     hipLaunchKernelGGL(k_dinv, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, c->d_ess,

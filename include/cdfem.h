@@ -76,6 +76,10 @@ int cdfem_device_count(void);
 int cdfem_alloc(cdfem_ctx *ctx, size_t bytes, void **dptr);
 int cdfem_free(cdfem_ctx *ctx, void *dptr);
 int cdfem_memcpy(cdfem_ctx *ctx, void *dst, int dst_where, const void *src, int src_where, size_t bytes);
+/* y = a x + b y on n doubles of device memory, synchronous.  replaces: Vector::Add(a, x) on device
+ * vectors (MFEM's forall kernel; diffusion_mms.cpp:433 rhs.Add(dt, f), linear_convection_diffusion_1D.cpp
+ * the same rhs update), so the shim's time loop keeps rhs in HBM.                                  */
+int cdfem_vec_axpby(cdfem_ctx *ctx, int64_t n, double a, const double *x, double b, double *y);
 
 /* ---- mesh + H1 space -------------------------------------------------------------------------
  * replaces: ParMesh + H1_FECollection(order, dim) + ParFiniteElementSpace + GetEssentialTrueDofs
@@ -252,7 +256,8 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * brick element cores 1-10 and the four-waves-per-brick kernel, x-fold / paired x updates, the
  * folded high-order direction, the derived mass weight, per-XCD SpMV sort, SpMV stream offsets and
  * the software-pipelined SpMV loop, the two-waves-per-SIMD structured Mult, 2 / 4 lanes per SpMV row
- * (profiles/r03/ab_c4_spmv_lanes_per_row.txt).                      */
+ * (profiles/r03/ab_c4_spmv_lanes_per_row.txt), a spinning / less frequent GMRES host poll
+ * (profiles/r03/ab_c2_gmres_poll.txt).                               */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
 
 /* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */

@@ -247,6 +247,34 @@ def test_diffusion_mms_time_loop(tmp_path, kind, order):
 
 
 @pytest.mark.gpu
+def test_diffusion_mms_vectors_stay_in_hbm(tmp_path):
+    """The time loop's vectors live on the device between the hot calls (Vector's host/device
+    mirror in cdfem_mfem.hpp): per backward-Euler step only u crosses PCIe, down for the host's
+    boundary projection and Linf error and up again, plus the linear form's coefficient samples.
+    Measured from the shim's own transfer counters (CDFEM_SHIM_STATS) as the difference between a
+    10-step and a 5-step run, so set-up traffic cancels."""
+    exe = os.path.join(ROOT, "continuum-mechanics-mfem_amd", "lib", "diffusion_mms")
+    opts = tmp_path / "petsc.opts"
+    opts.write_text(PETSC_OPTS)
+    n, p = 32, 2
+    stats = {}
+    for T in ("0.25", "0.5"):
+        r = subprocess.run([exe, "-n", str(n), "-p", str(p), "-dt", "0.05", "-T", T, "-opts", str(opts)],
+                           capture_output=True, text=True, timeout=300, env={**os.environ, "CDFEM_SHIM_STATS": "1"})
+        assert r.returncode == 0, r.stderr
+        line = [ln for ln in r.stderr.splitlines() if ln.startswith("shim_transfers")][-1].split()
+        stats[T] = {line[i]: int(line[i + 1]) for i in range(3, len(line), 2)}
+    per = {k: (stats["0.5"][k] - stats["0.25"][k]) / 5 for k in stats["0.5"]}
+    nl, ne = (2 * n + 1) ** 2, n * n
+    vec = 8 * nl
+    lf_samples = 8 * ne * (p + 3) ** 2  # at most (p + 3)^2 linear-form points per quad
+    print("per step:", per, "vector bytes", vec)
+    assert per["d2h_bytes"] <= vec + 1024, per      # u, once (host projection + Linf error)
+    assert per["h2d_bytes"] <= vec + lf_samples + 1024, per  # u back, and f at the points
+    assert per["h2d_calls"] <= 3 and per["d2h_calls"] <= 2, per
+
+
+@pytest.mark.gpu
 def test_driver_default_options_are_the_references(exe, tmp_path):
     """Without -opts and without Input/petsc.opts in the working directory the driver uses the
     reference's Input/petsc.opts values (gmres, rtol 1e-10, atol 1e-12, max_it 500, jacobi)."""

@@ -22,6 +22,7 @@ ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--iters", type=int, default=60)
 ap.add_argument("--n", type=int, default=64)
 ap.add_argument("--variants", default="gm_ept=4,gm_ept=5")
+ap.add_argument("--no-prof", action="store_true", help="no HIP events around the kernels: wall time only")
 args = ap.parse_args()
 
 n = args.n
@@ -39,7 +40,7 @@ for rnd in range(args.rounds + 1):
     for k, v in variants:
         ctx.set_option(k, int(v))
         ctx.set_option("profile_mask", (1 << cdfem.K_APPLY) | (1 << cdfem.K_ORTH))
-        ctx.profile(True)
+        ctx.profile(not args.no_prof)
         ctx.synchronize()
         t0 = time.perf_counter()
         info = ctx.solve_device(dB, dX, method="gmres", pc="jacobi", rel_tol=0.0, abs_tol=0.0,
