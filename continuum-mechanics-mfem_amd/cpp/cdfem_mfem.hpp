@@ -1730,7 +1730,7 @@ public:
             Setup();
         }
         const int nt = fes_->GetTrueVSize(), off = (int)fes_->FirstOwned();
-        if (off == 0 && nt == height) {  // one rank: the true dofs are the L-dofs
+        if (fes_->NRanks() == 1) {  // one rank: the true dofs are the L-dofs (P = I)
             X.SetSize(nt);
             B.SetSize(nt);
             check(cdfem_form_linear_system(ctx(), x.Read(), b.Read(), X.Write(), B.Write(), CDFEM_DEVICE), ctx(),
@@ -1885,7 +1885,9 @@ inline void ConstrainedPAOperator::Mult(const Vector &x, Vector &y) const
 {
     if (x.Size() != height) throw std::invalid_argument("HypreParMatrix::Mult: size");
     const int nl = a_->FESpace()->GetVSize(), off = (int)a_->FESpace()->FirstOwned();
-    if (off == 0 && nl == height) {  // one rank: P is the identity
+    // one rank: P is the identity (on several ranks P is an exchange every rank joins, even one that
+    // owns all its dofs)
+    if (a_->FESpace()->NRanks() == 1) {
         y.SetSize(height);
         check(cdfem_pa_mult(a_->ctx(), x.Read(), y.Write(), 1, CDFEM_DEVICE), a_->ctx(), "cdfem_pa_mult");
         check(cdfem_synchronize(a_->ctx()), a_->ctx(), "cdfem_synchronize");
@@ -2258,7 +2260,7 @@ protected:
         const int nl = a->FESpace()->GetVSize(), off = (int)a->FESpace()->FirstOwned();
         cdfem_ctx *c = a->ctx();
         int rc;
-        if (off == 0 && nl == height && &b != &x) {  // one rank: P is the identity
+        if (a->FESpace()->NRanks() == 1 && &b != &x) {  // one rank: P is the identity (see ConstrainedPAOperator::Mult)
             x.SetSize(height);
             rc = cdfem_solve(c, &prm, b.Read(), x.Write(), CDFEM_DEVICE, &res);
         } else {
