@@ -75,6 +75,16 @@ struct KrylovState {
     int iter, done, converged, final_iter, max_iter, first_den;
 };
 
+// In-launch grid sums (reduce.hpp ticket_sum): per reduction site, 8 group counters, a top
+// counter and the 8 group sums.  Zeroed at allocation; each counter is reset by its last arriver.
+struct GridTicket {
+    unsigned grp[8];
+    unsigned top;
+    unsigned pad[7];
+    double gsum[8];
+};
+enum { kTkDen = 0, kTkUpdate = 1, kTkGmNorm = 2, kTkCount = 4 };
+
 // Device-side GMRES(m) state (gmres.hip).  The first 32 bytes are what the host polls.
 constexpr int kGmMaxRestart = 64;
 struct GmresState {
@@ -238,6 +248,9 @@ struct cdfem_ctx {
     int red_blocks = 1024;
     cdfem::KrylovState *d_state = nullptr;
     cdfem::KrylovState *h_state = nullptr;  // pinned
+    cdfem::GridTicket *d_tk = nullptr;  // [kTkCount] in-launch grid sums (reduce.hpp ticket_sum)
+    int grid_fin = 1;                   // set_option "grid_fin": one-rank CG / GMRES sums finished in-launch
+    int gm_faces = 1;                   // set_option "gm_faces": one-rank brick GMRES forms the face dofs in pass 1
     double *d_gm = nullptr;             // GMRES basis (restart+1) * nl
     int gm_cap = 0;
     double *d_gm_part = nullptr;        // GMRES partials [(restart+1) * blocks]
@@ -340,6 +353,12 @@ void comm_exchange_nbr_buf(cdfem_ctx *c, const std::vector<int64_t> &off, const 
                            hipStream_t s = nullptr);
 void partition_free(cdfem_ctx *c);
 inline bool multi_rank(const cdfem_ctx *c) { return c->nranks > 1; }
+// the ticket of an in-launch grid sum (reduce.hpp ticket_sum): one rank only (several ranks
+// all-reduce the rank-local sums between kernels); nullptr = partials + one-block finalizer
+inline GridTicket *grid_fin_ticket(cdfem_ctx *c, int slot)
+{
+    return (c->grid_fin && !multi_rank(c)) ? c->d_tk + slot : nullptr;
+}
 // split CG finalizers for the multi-rank path: local sum -> all-reduce -> step
 hipError_t launch_fin_sum(cdfem_ctx *c, int nparts, int slot);
 hipError_t launch_den_step(cdfem_ctx *c);
@@ -410,8 +429,10 @@ hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it);
 // poll: pinned host slot the step's last scalar kernel writes the state head into (solve_gmres)
 hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
                               double *part, GmresState *st, bool first, double rtol, double atol, GmresState *poll);
+// faces_x: non-null when w came from the brick apply without its face kernel (the operator's
+// input, V_j); pass 1 then forms the brick-face dofs of w itself
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m, GmresState *poll);
+                          GmresState *st, int m, GmresState *poll, const double *faces_x = nullptr);
 hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st, GmresState *poll);
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 // ILU(0) (ilu_kernels.hip): factor + capture once per operator; apply: ilu.z = (LU)^{-1} d_w[4]
