@@ -20,11 +20,17 @@
 #include <type_traits>
 
 #include "cdfem_internal.hpp"
-#include "brick_geom.hpp"
 #include "pa_core.hpp"
 #include "reduce.hpp"
 
 namespace cdfem {
+
+struct BrickGeom {
+    int nbx, nby, nbz;  // bricks per axis
+    int Lx, Ly, Lz;     // dof lattice per axis
+    int xcd;            // 1: XCD-contiguous brick order (default; set_option "brick_xcd")
+    int bz0, bzs;       // k_brick_cg: the launch covers brick layers bz0, bz0 + bzs, ... (all: 0, 1)
+};
 
 // workgroup b runs on XCD b % 8; with xcd = 1 each XCD takes a contiguous range of bricks, so a
 // brick's neighbours (which re-read its patch faces) are mostly on the same L2.  Measured in
@@ -36,6 +42,22 @@ __device__ __forceinline__ int brick_id(const BrickGeom &g)
     const unsigned G = gridDim.x, b = blockIdx.x, x = b % 8, k = b / 8, q = G / 8, r = G % 8;
     return (int)(x * q + (x < r ? x : r) + k);
 }
+
+// index of boundary position (a, b, c) of an S^3 patch in lexicographic order of the boundary set
+template <int S>
+__device__ __forceinline__ int face_index(int a, int b, int c)
+{
+    constexpr int ring = 4 * S - 4;
+    if (c == 0) return a + S * b;
+    if (c == S - 1) return S * S + (S - 2) * ring + a + S * b;
+    const int base = S * S + (c - 1) * ring;
+    if (b == 0) return base + a;
+    if (b == S - 1) return base + S + 2 * (S - 2) + a;
+    return base + S + 2 * (b - 1) + (a == S - 1 ? 1 : 0);
+}
+
+template <int S>
+constexpr int face_count() { return 2 * S * S + (S - 2) * (4 * S - 4); }
 
 // MODE 0: y = A x;  MODE 1: y = A_c x (ConstrainedOperator);  MODE 2: CG-fused (x := r)
 // One wave per SIMD, unconstrained registers: 241.5 vs 272.2 us per C2 apply in the GMRES leg
@@ -156,6 +178,7 @@ k_brick_faces(const double *__restrict__ x, const double *__restrict__ dinv, dou
               double *__restrict__ y, const double *__restrict__ face, const uint8_t *__restrict__ ess,
               const BrickGeom g, double *__restrict__ part, const KrylovState *__restrict__ st)
 {
+    constexpr int F = face_count<S>();
     constexpr int s1 = S - 1;
     __shared__ double sh[kRedThreads / 64];
     double beta = 0.0;
@@ -169,6 +192,14 @@ k_brick_faces(const double *__restrict__ x, const double *__restrict__ dinv, dou
     const int nfx = (Lx - 1) / s1 + 1, nfy = (Ly - 1) / s1 + 1;
     const int per = Lx + (s1 - 1) * nfx;                     // dofs per s1-line period (sparse plane)
     const int count = fz ? Lx * Ly : nfy * Lx + (Ly - nfy) * nfx;
+    int bzs[2], pzs[2], nzc = 0;
+    {
+        const int qz = gz / s1;
+        if (fz) {
+            if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
+            if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
+        } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
+    }
     double acc = 0.0;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < count; k += gridDim.x * blockDim.x) {
         int gx, gy;
@@ -179,7 +210,25 @@ k_brick_faces(const double *__restrict__ x, const double *__restrict__ dinv, dou
             if (rem < Lx) { gy = s1 * pi; gx = rem; }
             else { const int j = rem - Lx, jl = j / nfx; gy = s1 * pi + 1 + jl; gx = (j - jl * nfx) * s1; }
         }
-        const double sum = brick_face_sum<S>(gx, gy, gz, g, face);
+        int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0;
+        {
+            const int qx = gx / s1, qy = gy / s1;
+            if (gx - qx * s1 == 0) {
+                if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
+                if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
+            } else { bxs[0] = qx; pxs[0] = gx - qx * s1; nxc = 1; }
+            if (gy - qy * s1 == 0) {
+                if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
+                if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
+            } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
+        }
+        double sum = 0.0;
+        for (int kz = 0; kz < nzc; ++kz)
+            for (int ky = 0; ky < nyc; ++ky)
+                for (int kx = 0; kx < nxc; ++kx) {
+                    const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
+                    sum += face[(size_t)bb * F + face_index<S>(pxs[kx], pys[ky], pzs[kz])];
+                }
         const int64_t gid = gx + (int64_t)Lx * (gy + (int64_t)Ly * gz);
         if constexpr (MODE == 0) {
             y[gid] = sum;
@@ -298,7 +347,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
            const Tab<D1, Q1> T, const BrickGeom g, int zlo_shared, double *__restrict__ part,
-           KrylovState *__restrict__ st, GridTicket *__restrict__ tk)
+           const KrylovState *__restrict__ st)
 {
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
@@ -308,8 +357,6 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     constexpr int NQ = Q1 * Q1 * Q1;
     __shared__ double s_in[S3];
     __shared__ double s_out[S3];
-    __shared__ double s_red[1];
-    __shared__ int s_flag;
     if (st->done) return;
     const double beta = st->beta;
     const int t = threadIdx.x;
@@ -400,12 +447,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         q[gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz)] = v;  // ess rows: replaced by d in the update
     }
     den = wave_sum(den);
-    if (tk) {  // one rank: den summed in-launch, the MFEM den step by the block that completes it
-        double total;
-        if (ticket_sum(den, part, tk, s_red, &s_flag, &total) && t == 0) cg_den_step(st, total);
-    } else if (t == 0) {
-        part[b] = den;
-    }
+    if (t == 0) part[b] = den;
 }
 
 template <int S>
@@ -415,11 +457,11 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
                   const double *__restrict__ face, const uint8_t *__restrict__ ess, const BrickGeom g,
                   const FastDiv fdx, const FastDiv fdxy, int zlo_shared,
                   const double *__restrict__ remote_lo, const double *__restrict__ remote_hi,
-                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step,
-                  GridTicket *__restrict__ tk)
+                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step)
 {
+    constexpr int F = face_count<S>();
+    constexpr int s1 = S - 1;
     __shared__ double sh[kRedThreads / 64];
-    __shared__ int s_flag;
     if (st->done) return;
     double alpha;
     if (den_step) {
@@ -449,8 +491,28 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         const double di = d[gid], xi = x[gid];
         const double rold = r[gid], mi = dinv[gid];
         double qi;
-        if (on_brick_face<S>(gx, gy, gz)) {
-            qi = brick_face_sum<S>(gx, gy, gz, g, face);
+        if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
+            int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
+            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
+            if (gx - qx * s1 == 0) {
+                if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
+                if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
+            } else { bxs[0] = qx; pxs[0] = gx - qx * s1; nxc = 1; }
+            if (gy - qy * s1 == 0) {
+                if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
+                if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
+            } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
+            if (gz - qz * s1 == 0) {
+                if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
+                if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
+            } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
+            qi = 0.0;
+            for (int kz = 0; kz < nzc; ++kz)
+                for (int ky = 0; ky < nyc; ++ky)
+                    for (int kx = 0; kx < nxc; ++kx) {
+                        const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
+                        qi += face[(size_t)bb * F + face_index<S>(pxs[kx], pys[ky], pzs[kz])];
+                    }
         } else {
             qi = q[gid];
         }
@@ -464,12 +526,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
     }
     const double bs = block_sum(acc, sh);
-    if (tk) {  // one rank: betanom summed in-launch, MFEM's convergence test and beta by the last block
-        double total;
-        if (ticket_sum(bs, part, tk, sh, &s_flag, &total) && threadIdx.x == 0) cg_update_logic(st, total);
-    } else if (threadIdx.x == 0) {
-        part[blockIdx.x] = bs;
-    }
+    if (threadIdx.x == 0) part[blockIdx.x] = bs;
 }
 
 // one launch of k_brick_cg over brick layers bz0, bz0 + bzs, ... (nlay of them) on stream s;
@@ -491,10 +548,10 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
     if (whole)
         CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K>), grid, block, 0, r, dinv, d_old, d_new, q, c->d_face, c->d_qd,
-                     c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, grid_fin_ticket(c, kTkDen));
+                     c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);
     else
         hipLaunchKernelGGL((k_brick_cg<D1, Q1, K>), grid, block, 0, run.s, r, dinv, d_old, d_new, q, c->d_face,
-                           c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, nullptr);
+                           c->d_qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);
     return hipGetLastError();
 }
 
@@ -549,8 +606,7 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
 #define CDFEM_UPD(S_)                                                                                       \
     hipLaunchKernelGGL((k_cg_update_faces<S_>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, q, d, dinv, \
                        c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, c->d_part,     \
-                       c->d_state, (int)den_step, tk)
-    GridTicket *tk = grid_fin_ticket(c, kTkUpdate);
+                       c->d_state, (int)den_step)
     if (c->p == 1)
         CDFEM_UPD(kBrick * 1 + 1);
     else if (c->p == 2)
@@ -561,7 +617,6 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (multi_rank(c)) return launch_fin_sum(c, (int)grid, 1);
-    if (tk) return hipSuccess;
     return launch_update_fin(c, (int)grid);
 }
 
@@ -573,6 +628,8 @@ k_pack_qplanes(const double *__restrict__ q, const double *__restrict__ face, co
                int lo, int hi, double *__restrict__ out_lo, double *__restrict__ out_hi,
                const KrylovState *__restrict__ st)
 {
+    constexpr int F = face_count<S>();
+    constexpr int s1 = S - 1;
     if (st->done) return;
     const int n = g.Lx * g.Ly;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -582,8 +639,28 @@ k_pack_qplanes(const double *__restrict__ q, const double *__restrict__ face, co
         if (side == 0 ? !lo : !hi) continue;
         const int gz = side == 0 ? 0 : g.Lz - 1;
         double v;
-        if (on_brick_face<S>(gx, gy, gz)) {
-            v = brick_face_sum<S>(gx, gy, gz, g, face);
+        if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
+            int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
+            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
+            if (gx - qx * s1 == 0) {
+                if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
+                if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
+            } else { bxs[0] = qx; pxs[0] = gx - qx * s1; nxc = 1; }
+            if (gy - qy * s1 == 0) {
+                if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
+                if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
+            } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
+            if (gz - qz * s1 == 0) {
+                if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
+                if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
+            } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
+            v = 0.0;
+            for (int kz = 0; kz < nzc; ++kz)
+                for (int ky = 0; ky < nyc; ++ky)
+                    for (int kx = 0; kx < nxc; ++kx) {
+                        const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
+                        v += face[(size_t)bb * F + face_index<S>(pxs[kx], pys[ky], pzs[kz])];
+                    }
         } else {
             v = q[gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz)];
         }

@@ -394,7 +394,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], c->Lx * c->Ly);
             HIPCHK(launch_fin_sum(c, c->nblk, 0));
             comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
-        } else if (!grid_fin_ticket(c, kTkDen)) {
+        } else {
             HIPCHK(launch_den_fin(c, c->nblk));
         }
         prof_mark(c, CDFEM_K_E2L, false);
@@ -557,8 +557,6 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     }
     double *x = c->d_w[2], *w = c->d_w[4], *V = c->d_gm, *part = c->d_gm_part;
     GmresState *st = c->d_gmst, *poll = c->h_gmpoll;
-    const bool faces = c->gm_faces && !ilu && !multi_rank(c) && !c->fa_ready && use_brick(c) &&
-                       c->nl < ((int64_t)1 << 31);  // pass 1's fast division is exact below 2^31
     // the step's last scalar kernel has written poll[slot] (post_poll in gmres.hip); the event
     // marks its completion for the host.  (Measured alternatives, profiles/r03/ab_c2_gmres_poll.txt:
     // spinning on a stamp in pinned memory, 392.2 / 392.0 against 392.3 us per C2 step; polling every
@@ -588,18 +586,10 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
         post(0);
         if (wait(0).done) break;
         for (int j = 0; j < m; ++j) {
-            const double *vj = V + (int64_t)j * ldv;
-            if (faces) {  // the brick apply without its face kernel: pass 1 sums the face partials
-                prof_mark(c, CDFEM_K_APPLY, true);
-                HIPCHK(launch_brick_mult(c, vj, w, true, 1));
-                prof_mark(c, CDFEM_K_APPLY, false);
-            } else {
-                op_apply_global(c, vj, w, true);
-            }
+            op_apply_global(c, V + (int64_t)j * ldv, w, true);
             if (ilu) HIPCHK(ilu_apply(c));  // w <- (LU)^{-1} A v_j, in ilu.z
             prof_mark(c, CDFEM_K_ORTH, true);
-            HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, ldv, part, st, m, &poll[j & 1],
-                                  faces ? vj : nullptr));
+            HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, ldv, part, st, m, &poll[j & 1]));
             prof_mark(c, CDFEM_K_ORTH, false);
             post(j & 1);
             if (j > 0 && wait((j - 1) & 1).cycle_done) break;
@@ -650,8 +640,6 @@ int cdfem_create(int device, cdfem_ctx **out)
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_state, sizeof(KrylovState)) != hipSuccess ||
         hipMemset(c->d_state, 0, sizeof(KrylovState)) != hipSuccess ||
-        hipMalloc(&c->d_tk, kTkCount * sizeof(GridTicket)) != hipSuccess ||
-        hipMemset(c->d_tk, 0, kTkCount * sizeof(GridTicket)) != hipSuccess ||
         hipHostMalloc(&c->h_state, sizeof(KrylovState), hipHostMallocDefault) != hipSuccess) {
         cdfem_destroy(c);
         return CDFEM_ERR_HIP;
@@ -668,7 +656,6 @@ void cdfem_destroy(cdfem_ctx *c)
     free_mesh(c);
     comm_destroy(c);
     if (c->d_state) (void)hipFree(c->d_state);
-    if (c->d_tk) (void)hipFree(c->d_tk);
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->d_gmst) (void)hipFree(c->d_gmst);
     if (c->h_gmpoll) (void)hipHostFree(c->h_gmpoll);
@@ -1242,8 +1229,9 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
                 xyz = simplex_dof_coords(c->dim, c->p, c->ne, c->nd, c->nl, c->h_verts, c->h_dofs);
             FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl,
                                            multi_rank(c) ? 0 : c->sell_mode, c->dim,
-                                           xyz.empty() ? nullptr : xyz.data());
+                                           xyz.empty() ? nullptr : xyz.data(), c->spmv_chunk);
             c->nnz = P.nnz;
+            c->sell_chunk = P.chunk;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
             c->d_cols = dalloc<int32_t>(P.cols.size());
             c->d_diagpos = dalloc<int32_t>(P.diagpos.size());
@@ -1540,12 +1528,12 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "spmv_index16") {
             if (value < 0 || value > 1) throw ArgError("spmv_index16 must be 0 or 1");
             c->spmv_index16 = value;
-        } else if (k == "gm_faces") {
-            if (value < 0 || value > 1) throw ArgError("gm_faces must be 0 or 1");
-            c->gm_faces = value;
-        } else if (k == "grid_fin") {
-            if (value < 0 || value > 1) throw ArgError("grid_fin must be 0 or 1");
-            c->grid_fin = value;
+        } else if (k == "spmv_chunk") {  // read when the FA pattern is built (once per mesh)
+            if (value != 1 && value != 2 && value != 4) throw ArgError("spmv_chunk must be 1, 2 or 4");
+            c->spmv_chunk = value;
+        } else if (k == "spmv_u") {
+            if (value != 4 && value != 8) throw ArgError("spmv_u must be 4 or 8");
+            c->spmv_u = value;
         } else if (k == "profile_mask") {
             c->prof_mask = (unsigned)value;
         } else {

@@ -75,16 +75,6 @@ struct KrylovState {
     int iter, done, converged, final_iter, max_iter, first_den;
 };
 
-// In-launch grid sums (reduce.hpp ticket_sum): per reduction site, 8 group counters, a top
-// counter and the 8 group sums.  Zeroed at allocation; each counter is reset by its last arriver.
-struct GridTicket {
-    unsigned grp[8];
-    unsigned top;
-    unsigned pad[7];
-    double gsum[8];
-};
-enum { kTkDen = 0, kTkUpdate = 1, kTkGmNorm = 2, kTkCount = 4 };
-
 // Device-side GMRES(m) state (gmres.hip).  The first 32 bytes are what the host polls.
 constexpr int kGmMaxRestart = 64;
 struct GmresState {
@@ -224,6 +214,9 @@ struct cdfem_ctx {
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
+    int spmv_chunk = 1;                 // set_option "spmv_chunk" (read when the FA pattern is built)
+    int sell_chunk = 1;                 // the chunk the current SELL copy was built with
+    int spmv_u = 4;                     // set_option "spmv_u": entries in flight per lane (chunk 2: 4 or 8)
     int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD (windowed layout)
     int32_t *d_rperm = nullptr;         // SpMV space order: space row -> mesh row (null: mesh order)
     bool sell_windowed = false;         // slices cut from the space order (kernel row = slice * 64 + lane)
@@ -248,9 +241,6 @@ struct cdfem_ctx {
     int red_blocks = 1024;
     cdfem::KrylovState *d_state = nullptr;
     cdfem::KrylovState *h_state = nullptr;  // pinned
-    cdfem::GridTicket *d_tk = nullptr;  // [kTkCount] in-launch grid sums (reduce.hpp ticket_sum)
-    int grid_fin = 1;                   // set_option "grid_fin": one-rank CG / GMRES sums finished in-launch
-    int gm_faces = 1;                   // set_option "gm_faces": one-rank brick GMRES forms the face dofs in pass 1
     double *d_gm = nullptr;             // GMRES basis (restart+1) * nl
     int gm_cap = 0;
     double *d_gm_part = nullptr;        // GMRES partials [(restart+1) * blocks]
@@ -353,12 +343,6 @@ void comm_exchange_nbr_buf(cdfem_ctx *c, const std::vector<int64_t> &off, const 
                            hipStream_t s = nullptr);
 void partition_free(cdfem_ctx *c);
 inline bool multi_rank(const cdfem_ctx *c) { return c->nranks > 1; }
-// the ticket of an in-launch grid sum (reduce.hpp ticket_sum): one rank only (several ranks
-// all-reduce the rank-local sums between kernels); nullptr = partials + one-block finalizer
-inline GridTicket *grid_fin_ticket(cdfem_ctx *c, int slot)
-{
-    return (c->grid_fin && !multi_rank(c)) ? c->d_tk + slot : nullptr;
-}
 // split CG finalizers for the multi-rank path: local sum -> all-reduce -> step
 hipError_t launch_fin_sum(cdfem_ctx *c, int nparts, int slot);
 hipError_t launch_den_step(cdfem_ctx *c);
@@ -380,7 +364,8 @@ struct FaPattern {
     // SELL-64 (sigma = global sort by row length) copy of the pattern for the SpMV
     std::vector<int32_t> sptr;   // [nslices + 1] first stored entry of each 64-row slice
     std::vector<int32_t> srows;  // [nslices * 64] original row of (slice, lane), -1 = padding
-    std::vector<int32_t> scols;  // [stored] column, slice-major then entry-major then lane
+    std::vector<int32_t> scols;  // [stored] column, slice-major, then chunk of `chunk` entries, lane, entry
+    int chunk = 1;               // consecutive entries of one lane stored together (1, 2 or 4)
     std::vector<int32_t> smap;   // [stored] CSR index of the stored entry, -1 = padding
     std::vector<int16_t> sdel;   // [stored] column - row when every |column - row| < 2^15, else empty
     std::vector<int32_t> perm;   // SpMV space order (sell_plan.cpp): space row -> mesh row; empty = mesh order
@@ -393,6 +378,7 @@ struct SellPlan {
     bool windowed = false;
     int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0, bw_geometric = 0;
     std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
+    int chunk = 1;               // entries per lane stored together (set_option "spmv_chunk")
 };
 std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
 SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim = 0,
@@ -402,7 +388,7 @@ std::vector<double> simplex_dof_coords(int dim, int p, int ne, int nd, int64_t n
                                        const std::vector<int32_t> &dofs);
 void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl);
 FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl, int sell_mode,
-                           int dim = 0, const double *dof_xyz = nullptr);
+                           int dim = 0, const double *dof_xyz = nullptr, int chunk = 1);
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq, double kappa, double alpha,
                                const double *conv, const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);
@@ -429,10 +415,8 @@ hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it);
 // poll: pinned host slot the step's last scalar kernel writes the state head into (solve_gmres)
 hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
                               double *part, GmresState *st, bool first, double rtol, double atol, GmresState *poll);
-// faces_x: non-null when w came from the brick apply without its face kernel (the operator's
-// input, V_j); pass 1 then forms the brick-face dofs of w itself
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m, GmresState *poll, const double *faces_x = nullptr);
+                          GmresState *st, int m, GmresState *poll);
 hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st, GmresState *poll);
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 // ILU(0) (ilu_kernels.hip): factor + capture once per operator; apply: ilu.z = (LU)^{-1} d_w[4]

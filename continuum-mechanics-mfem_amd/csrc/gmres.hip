@@ -21,7 +21,6 @@
 
 #include <algorithm>
 
-#include "brick_geom.hpp"
 #include "cdfem_internal.hpp"
 #include "reduce.hpp"
 
@@ -117,14 +116,10 @@ k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st,
 // dropped).  Each wave parks its wave sums in LDS, so the whole step needs ONE barrier before the
 // block sums.  Measured at C4 (orthogonalisation per step): one barrier per batch of 8, 93.9 us;
 // one barrier in all, batches of 8 / 4 / 2 / 1: 85.7 / 83.2 / 82.6 / 82.1 us.
-// S > 0 (structured box, one rank): the apply was k_brick3d alone, so the brick-face dofs of w
-// hold no value yet; pass 1 forms them from the face partials (k_brick_faces' sum, same order) as
-// it reads w, which removes the face kernel and its pass over w from every GMRES step.
-template <int BAT, int EPT, int S>
+template <int BAT, int EPT>
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double *__restrict__ V, int64_t n,
-           int64_t ldv, int64_t skip_lo, double *__restrict__ part, int nb, const GmresState *__restrict__ st,
-           const GmFaces fc)
+           int64_t ldv, int64_t skip_lo, double *__restrict__ part, int nb, const GmresState *__restrict__ st)
 {
     __shared__ double sh[kGmMaxRestart + 1][kRedThreads / 64];
     if (st->cycle_done) return;
@@ -138,15 +133,7 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
         const int64_t k = base + (int64_t)e * kRedThreads;
         double v = 0.0;
         if (k < n) {
-            double wk = w[k];
-            if constexpr (S > 0) {
-                const uint32_t i = (uint32_t)k, Lx = (uint32_t)fc.g.Lx;
-                const uint32_t gz = fdiv(i, fc.fdxy), rem = i - gz * Lx * (uint32_t)fc.g.Ly;
-                const uint32_t gy = fdiv(rem, fc.fdx), gx = rem - gy * Lx;
-                if (on_brick_face<S>((int)gx, (int)gy, (int)gz))  // ConstrainedOperator: x on ess rows
-                    wk = fc.ess[k] ? fc.x[k] : brick_face_sum<S>((int)gx, (int)gy, (int)gz, fc.g, fc.face);
-            }
-            v = sj * wk;
+            v = sj * w[k];
             if (dinv) v *= dinv[k];
             w[k] = v;
         }
@@ -240,52 +227,6 @@ k_gm_dots_fin_mb(const double *__restrict__ part, int nb, GmresState *__restrict
     else st->H[i * kGmMaxRestart + j] = st->s[i] * v;
 }
 
-// the Hessenberg column and the rotations so far, loaded in parallel into LDS (threads <= j): the
-// serial rotation sequence of gm_norm_step then runs on LDS instead of dependent global loads
-__device__ inline void gm_stage_column(const GmresState *st, int j, double *hc, double *cs, double *sn)
-{
-    constexpr int LD = kGmMaxRestart;
-    for (int i = threadIdx.x; i <= j; i += blockDim.x) {
-        hc[i] = st->H[i * LD + j];
-        if (i < j) {
-            cs[i] = st->cs[i];
-            sn[i] = st->sn[i];
-        }
-    }
-}
-
-// one thread: |V_{j+1}|^2 = sum -> h_{j+1,j}, the rotations, the new one, residual, cycle control
-__device__ inline void gm_norm_step(GmresState *st, int j, double sum, double *hc, const double *cs,
-                                    const double *sn, GmresState *poll)
-{
-    constexpr int LD = kGmMaxRestart;
-    const double hn = sqrt(sum);
-    hc[j + 1] = hn;
-    for (int i = 0; i < j; ++i) {
-        const double a = hc[i], c2 = hc[i + 1];
-        hc[i] = cs[i] * a + sn[i] * c2;
-        hc[i + 1] = -sn[i] * a + cs[i] * c2;
-    }
-    const double a = hc[j], c2 = hc[j + 1];
-    const double rr = sqrt(a * a + c2 * c2);
-    const double cj = (rr == 0.0) ? 1.0 : a / rr, sj = (rr == 0.0) ? 0.0 : c2 / rr;
-    st->cs[j] = cj;
-    st->sn[j] = sj;
-    hc[j] = rr;
-    hc[j + 1] = 0.0;
-    for (int i = 0; i <= j + 1; ++i) st->H[i * LD + j] = hc[i];
-    const double gj = st->g[j];
-    st->g[j + 1] = -sj * gj;
-    st->g[j] = cj * gj;
-    st->res = fabs(-sj * gj);
-    st->kk = j + 1;
-    st->its += 1;
-    st->s[j + 1] = (hn != 0.0) ? 1.0 / hn : 0.0;
-    st->j = j + 1;
-    if (hn == 0.0 || st->res <= st->ttol || j + 1 == st->m || st->its >= st->max_it) st->cycle_done = 1;
-    post_poll(st, poll);
-}
-
 // ---- pass 2: V_{j+1} = w - sum_i H[i][j] s_i V_i, partials of |V_{j+1}|^2 ------------------------
 // Pass 1's treatment: the coefficients H[i][j] s_i are staged once per block in LDS (one global
 // load per i per block instead of one per i per wave), and the basis vectors are read BAT at a time
@@ -295,17 +236,11 @@ __device__ inline void gm_norm_step(GmresState *st, int j, double sum, double *h
 template <int BAT, int EPT>
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int64_t ldv, int64_t skip_lo,
-           double *__restrict__ part, GmresState *__restrict__ st, GridTicket *__restrict__ tk,
-           GmresState *__restrict__ poll)
+           double *__restrict__ part, const GmresState *__restrict__ st)
 {
     __shared__ double sh[kRedThreads / 64];
-    __shared__ double coef[3 * kGmMaxRestart + 1 > kGmMaxRestart + BAT ? 3 * kGmMaxRestart + 1 : kGmMaxRestart + BAT];
-    __shared__ int s_flag;
-    if (st->cycle_done) {
-        // in-launch finish (tk): k_gm_norm_fin's post for a step queued past the cycle's end
-        if (tk && blockIdx.x == 0 && threadIdx.x == 0) post_poll(st, poll);
-        return;
-    }
+    __shared__ double coef[kGmMaxRestart + BAT];
+    if (st->cycle_done) return;
     const int j = st->j;
     for (int i = threadIdx.x; i < kGmMaxRestart + BAT; i += blockDim.x)
         coef[i] = i <= j ? st->H[i * kGmMaxRestart + j] * st->s[i] : 0.0;
@@ -345,19 +280,7 @@ k_gm_pass2(const double *__restrict__ w, double *__restrict__ V, int64_t n, int6
             if (k >= skip_lo) nrm += acc[e] * acc[e];
         }
     }
-    const double bs = block_sum(nrm, sh);
-    if (!tk) {
-        store_partial(bs, part);
-        return;
-    }
-    // one rank: |V_{j+1}|^2 summed in-launch; the block that completes it runs k_gm_norm_fin's step
-    double total;
-    if (!ticket_sum(bs, part, tk, sh, &s_flag, &total)) return;
-    double *hc = coef, *cs = coef + kGmMaxRestart + 1, *sn = cs + kGmMaxRestart;
-    __syncthreads();  // coef is reused for the Hessenberg column and the rotations
-    gm_stage_column(st, j, hc, cs, sn);
-    __syncthreads();
-    if (threadIdx.x == 0) gm_norm_step(st, j, total, hc, cs, sn, poll);
+    store_partial(block_sum(nrm, sh), part);
 }
 
 // ---- h_{j+1,j}, Givens rotations, residual estimate, cycle control ------------------------------
@@ -365,6 +288,7 @@ __global__ void __launch_bounds__(1024)
 k_gm_norm_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ st, int mode,
               GmresState *__restrict__ poll)
 {
+    constexpr int LD = kGmMaxRestart;
     __shared__ double sh[1024 / 64];
     __shared__ double hc[kGmMaxRestart + 1], cs[kGmMaxRestart], sn[kGmMaxRestart];
     if (st->cycle_done) {  // uniform: every thread reads the same flag before the reduction
@@ -372,7 +296,13 @@ k_gm_norm_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ 
         return;
     }
     const int j = st->j;
-    gm_stage_column(st, j, hc, cs, sn);
+    // the Hessenberg column and the rotations so far, loaded in parallel into LDS: the serial
+    // rotation sequence below then runs on LDS instead of dependent global loads
+    if ((int)threadIdx.x <= j) hc[threadIdx.x] = st->H[threadIdx.x * LD + j];
+    if ((int)threadIdx.x < j) {
+        cs[threadIdx.x] = st->cs[threadIdx.x];
+        sn[threadIdx.x] = st->sn[threadIdx.x];
+    }
     const double sum = mode == 2 ? st->red[0] : sum_partials(part, nb, sh);  // (contains a barrier)
     if (mode == 2) __syncthreads();
     if (threadIdx.x != 0) return;
@@ -380,7 +310,31 @@ k_gm_norm_fin(const double *__restrict__ part, int nb, GmresState *__restrict__ 
         st->red[0] = sum;
         return;
     }
-    gm_norm_step(st, j, sum, hc, cs, sn, poll);
+    const double hn = sqrt(sum);
+    hc[j + 1] = hn;
+    for (int i = 0; i < j; ++i) {
+        const double a = hc[i], c2 = hc[i + 1];
+        hc[i] = cs[i] * a + sn[i] * c2;
+        hc[i + 1] = -sn[i] * a + cs[i] * c2;
+    }
+    const double a = hc[j], c2 = hc[j + 1];
+    const double rr = sqrt(a * a + c2 * c2);
+    const double cj = (rr == 0.0) ? 1.0 : a / rr, sj = (rr == 0.0) ? 0.0 : c2 / rr;
+    st->cs[j] = cj;
+    st->sn[j] = sj;
+    hc[j] = rr;
+    hc[j + 1] = 0.0;
+    for (int i = 0; i <= j + 1; ++i) st->H[i * LD + j] = hc[i];
+    const double gj = st->g[j];
+    st->g[j + 1] = -sj * gj;
+    st->g[j] = cj * gj;
+    st->res = fabs(-sj * gj);
+    st->kk = j + 1;
+    st->its += 1;
+    st->s[j + 1] = (hn != 0.0) ? 1.0 / hn : 0.0;
+    st->j = j + 1;
+    if (hn == 0.0 || st->res <= st->ttol || j + 1 == st->m || st->its >= st->max_it) st->cycle_done = 1;
+    post_poll(st, poll);
 }
 
 // ---- end of cycle: y = H_k^{-1} g_k (every block, redundantly: k <= 64), x += sum_i y_i s_i V_i --
@@ -526,7 +480,7 @@ static int orth_ept(cdfem_ctx *c)
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gm_pass1<kGmBatch, 4, 0>, kRedThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gm_pass1<kGmBatch, 4>, kRedThreads, 0);
     const int64_t cap = (int64_t)std::max(cus, 1) * std::max(per, 1);
     int ept = 8;
     for (int e : {4, 5, 6, 8})
@@ -541,32 +495,22 @@ static int orth_ept(cdfem_ctx *c)
 
 template <int EPT>
 static void orth_passes(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                        GmresState *st, int m, GmresState *poll, const GmFaces *fc)
+                        GmresState *st, int m, GmresState *poll)
 {
     const int nb = (int)((c->nl + (int64_t)kRedThreads * EPT - 1) / ((int64_t)kRedThreads * EPT));
     const int64_t n = c->nl;
     const bool mr = multi_rank(c);
-    const GmFaces f0 = fc ? *fc : GmFaces{};
-    if (!fc)
-        hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT, 0>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n,
-                           ldv, owned_from(c), part, nb, st, f0);
-    else if (fc->s == kBrick * 1 + 1)
-        hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT, kBrick * 1 + 1>), dim3(nb), dim3(kRedThreads), 0, c->stream, w,
-                           dinv, V, n, ldv, owned_from(c), part, nb, st, f0);
-    else
-        hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT, kBrick * 2 + 1>), dim3(nb), dim3(kRedThreads), 0, c->stream, w,
-                           dinv, V, n, ldv, owned_from(c), part, nb, st, f0);
+    hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv,
+                       owned_from(c), part, nb, st);
     hipLaunchKernelGGL(k_gm_dots_fin_mb, dim3(m + 1), dim3(kRedThreads), 0, c->stream, part, nb, st, mr ? 1 : 0);
     if (mr) {
         comm_allreduce(c, red_of(st), m + 1);
         hipLaunchKernelGGL(k_gm_dots_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2);
     }
-    GridTicket *tk = grid_fin_ticket(c, kTkGmNorm);
     hipLaunchKernelGGL((k_gm_pass2<kGmBatch2, EPT>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, V, n, ldv,
-                       owned_from(c), part, st, tk, poll);
-    if (!tk)
-        hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, mr ? 1 : 0,
-                           mr ? nullptr : poll);
+                       owned_from(c), part, st);
+    hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, mr ? 1 : 0,
+                       mr ? nullptr : poll);
     if (mr) {
         comm_allreduce(c, red_of(st), 1);
         hipLaunchKernelGGL(k_gm_norm_fin, dim3(1), dim3(1024), 0, c->stream, part, nb, st, 2, poll);
@@ -574,24 +518,13 @@ static void orth_passes(cdfem_ctx *c, double *w, const double *dinv, double *V, 
 }
 
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m, GmresState *poll, const double *faces_x)
+                          GmresState *st, int m, GmresState *poll)
 {
-    GmFaces fc{};
-    if (faces_x) {  // w came from k_brick3d<MODE 1> alone (gm_faces_fused)
-        fc.face = c->d_face;
-        fc.ess = c->d_ess;
-        fc.x = faces_x;
-        fc.g = BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1};
-        fc.fdx = make_fastdiv((uint32_t)c->Lx);
-        fc.fdxy = make_fastdiv((uint32_t)(c->Lx * c->Ly));
-        fc.s = kBrick * c->p + 1;
-    }
-    const GmFaces *f = faces_x ? &fc : nullptr;
     switch (orth_ept(c)) {
-    case 5: orth_passes<5>(c, w, dinv, V, ldv, part, st, m, poll, f); break;
-    case 6: orth_passes<6>(c, w, dinv, V, ldv, part, st, m, poll, f); break;
-    case 8: orth_passes<8>(c, w, dinv, V, ldv, part, st, m, poll, f); break;
-    default: orth_passes<4>(c, w, dinv, V, ldv, part, st, m, poll, f); break;
+    case 5: orth_passes<5>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    case 6: orth_passes<6>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    case 8: orth_passes<8>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    default: orth_passes<4>(c, w, dinv, V, ldv, part, st, m, poll); break;
     }
     return hipGetLastError();
 }

@@ -250,14 +250,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan).  A permuted order runs the
  *               Krylov solve in that order (Mult to rounding, iterates to 1e-12).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
- * "grid_fin": 1 (default) — one rank: the structured CG's (d, A d) and (r, z) sums and the GMRES
- *             norm finish inside the launch that produces their partials (the block that completes
- *             the sum runs MFEM's / PETSc's scalar step), instead of a one-block finalize kernel
- *             after it; 0 = finalize kernels (the same fixed-order sums per group, results agree to
- *             rounding).
- * "gm_faces": 1 (default) — one-rank GMRES on a structured box (p <= 2): the brick apply's face
- *             dofs are summed by the orthogonalisation's first pass as it reads A v_j, not by a
- *             face kernel of their own (same sums, same order: bitwise the same basis).
+ * "spmv_chunk": 1 (default), 2 or 4 — read when the FA pattern is built: a lane's CH consecutive
+ *             SELL entries stored together, so one 16-byte load brings two values and one load CH
+ *             column deltas (rows padded to whole chunks; bitwise the chunk-1 sums).
+ * "spmv_u": 4 (default) or 8 — SELL entries in flight per lane (8 only with spmv_chunk 2).
  * "gm_ept": 0 (default, auto) — entries per thread of the GMRES orthogonalisation passes (4, 5, 6
  *           or 8); auto takes the smallest whose grid is resident in one round (same results).
  * Variants measured slower and removed in round 3 (their records stay under profiles/r02_ab_*):
