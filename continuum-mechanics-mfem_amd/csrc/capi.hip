@@ -1229,9 +1229,8 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
                 xyz = simplex_dof_coords(c->dim, c->p, c->ne, c->nd, c->nl, c->h_verts, c->h_dofs);
             FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl,
                                            multi_rank(c) ? 0 : c->sell_mode, c->dim,
-                                           xyz.empty() ? nullptr : xyz.data(), c->spmv_chunk);
+                                           xyz.empty() ? nullptr : xyz.data());
             c->nnz = P.nnz;
-            c->sell_chunk = P.chunk;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
             c->d_cols = dalloc<int32_t>(P.cols.size());
             c->d_diagpos = dalloc<int32_t>(P.diagpos.size());
@@ -1528,12 +1527,6 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "spmv_index16") {
             if (value < 0 || value > 1) throw ArgError("spmv_index16 must be 0 or 1");
             c->spmv_index16 = value;
-        } else if (k == "spmv_chunk") {  // read when the FA pattern is built (once per mesh)
-            if (value != 1 && value != 2 && value != 4) throw ArgError("spmv_chunk must be 1, 2 or 4");
-            c->spmv_chunk = value;
-        } else if (k == "spmv_u") {
-            if (value != 4 && value != 8) throw ArgError("spmv_u must be 4 or 8");
-            c->spmv_u = value;
         } else if (k == "profile_mask") {
             c->prof_mask = (unsigned)value;
         } else {

@@ -214,9 +214,6 @@ struct cdfem_ctx {
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
-    int spmv_chunk = 1;                 // set_option "spmv_chunk" (read when the FA pattern is built)
-    int sell_chunk = 1;                 // the chunk the current SELL copy was built with
-    int spmv_u = 4;                     // set_option "spmv_u": entries in flight per lane (chunk 2: 4 or 8)
     int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD (windowed layout)
     int32_t *d_rperm = nullptr;         // SpMV space order: space row -> mesh row (null: mesh order)
     bool sell_windowed = false;         // slices cut from the space order (kernel row = slice * 64 + lane)
@@ -364,8 +361,7 @@ struct FaPattern {
     // SELL-64 (sigma = global sort by row length) copy of the pattern for the SpMV
     std::vector<int32_t> sptr;   // [nslices + 1] first stored entry of each 64-row slice
     std::vector<int32_t> srows;  // [nslices * 64] original row of (slice, lane), -1 = padding
-    std::vector<int32_t> scols;  // [stored] column, slice-major, then chunk of `chunk` entries, lane, entry
-    int chunk = 1;               // consecutive entries of one lane stored together (1, 2 or 4)
+    std::vector<int32_t> scols;  // [stored] column, slice-major then entry-major then lane
     std::vector<int32_t> smap;   // [stored] CSR index of the stored entry, -1 = padding
     std::vector<int16_t> sdel;   // [stored] column - row when every |column - row| < 2^15, else empty
     std::vector<int32_t> perm;   // SpMV space order (sell_plan.cpp): space row -> mesh row; empty = mesh order
@@ -378,7 +374,6 @@ struct SellPlan {
     bool windowed = false;
     int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0, bw_geometric = 0;
     std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
-    int chunk = 1;               // entries per lane stored together (set_option "spmv_chunk")
 };
 std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
 SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim = 0,
@@ -388,7 +383,7 @@ std::vector<double> simplex_dof_coords(int dim, int p, int ne, int nd, int64_t n
                                        const std::vector<int32_t> &dofs);
 void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl);
 FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl, int sell_mode,
-                           int dim = 0, const double *dof_xyz = nullptr, int chunk = 1);
+                           int dim = 0, const double *dof_xyz = nullptr);
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq, double kappa, double alpha,
                                const double *conv, const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);

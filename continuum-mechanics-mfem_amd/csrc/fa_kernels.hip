@@ -49,7 +49,7 @@ static inline int64_t ee_index(int e, int i, int j, int nd)
 }
 
 FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int64_t nl, int sell_mode, int dim,
-                           const double *dof_xyz, int chunk)
+                           const double *dof_xyz)
 {
     // dof -> incidences (e * nd + l), ascending
     std::vector<int64_t> cnt(nl + 1, 0);
@@ -133,7 +133,6 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     // SpMV layout: SELL-64 over the rows in the plan's order (sell_plan.cpp)
     P.rowptr = std::move(rowptr);
     SellPlan pl = sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode, dim, dof_xyz);
-    pl.chunk = chunk;
     sell_build(P, nl, pl);
     return P;
 }
@@ -437,89 +436,6 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ sptr, c
     return a0;
 }
 
-// Chunked slice (sell_build with chunk CH = 2 or 4): a lane's CH consecutive entries are adjacent,
-// so one 16-byte load brings 2 values and one 4 / 8-byte load CH column deltas; UC chunks in flight
-// per lane.  The row sum keeps the entry order j = 0, 1, ... (bitwise the CH = 1 sum).
-typedef double cd_d2 __attribute__((ext_vector_type(2)));
-typedef int16_t cd_s2 __attribute__((ext_vector_type(2)));
-typedef int16_t cd_s4 __attribute__((ext_vector_type(4)));
-typedef int32_t cd_i2 __attribute__((ext_vector_type(2)));
-typedef int32_t cd_i4 __attribute__((ext_vector_type(4)));
-
-template <int CH, typename CI, bool NT>
-__device__ __forceinline__ void chunk_cols(const CI *p, int32_t *out)
-{
-    if constexpr (CH == 2 && sizeof(CI) == 2) {
-        const cd_s2 v = stream_load<NT>((const cd_s2 *)p);
-        out[0] = v.x; out[1] = v.y;
-    } else if constexpr (CH == 4 && sizeof(CI) == 2) {
-        const cd_s4 v = stream_load<NT>((const cd_s4 *)p);
-        out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
-    } else if constexpr (CH == 2) {
-        const cd_i2 v = stream_load<NT>((const cd_i2 *)p);
-        out[0] = v.x; out[1] = v.y;
-    } else {
-        const cd_i4 v = stream_load<NT>((const cd_i4 *)p);
-        out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
-    }
-}
-
-template <int CH, bool NT>
-__device__ __forceinline__ void chunk_vals(const double *p, double *out)
-{
-#pragma unroll
-    for (int h = 0; h < CH / 2; ++h) {
-        const cd_d2 v = stream_load<NT>((const cd_d2 *)p + h);
-        out[2 * h] = v.x; out[2 * h + 1] = v.y;
-    }
-}
-
-template <typename CI, bool PERM, int CH, int UC, bool NT>
-__device__ __forceinline__ double sell_slice_ch(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows,
-                                                const CI *__restrict__ scols, const double *__restrict__ svals,
-                                                const double *__restrict__ x, int64_t n, int64_t sl, int lane,
-                                                int64_t &row, bool &valid)
-{
-    constexpr bool DELTA = sizeof(CI) == 2;
-    const int32_t b = sptr[sl], nch = (sptr[sl + 1] - b) / (64 * CH);
-    int64_t base;
-    if (PERM) {
-        row = sl * 64 + lane;
-        base = row < n ? row : n - 1;
-    } else {
-        row = srows[sl * 64 + lane];
-        base = row >= 0 ? row : 0;
-    }
-    valid = PERM ? row < n : row >= 0;
-    const double *xr = DELTA ? x + base : x;
-    const double *v = svals + b + lane * CH;
-    const CI *cidx = scols + b + lane * CH;
-    double a0 = 0.0;
-    int c = 0;
-    for (; c + UC <= nch; c += UC) {
-        double vv[UC][CH];
-        int32_t cc[UC][CH];
-#pragma unroll
-        for (int u = 0; u < UC; ++u) {
-            chunk_cols<CH, CI, NT>(cidx + (c + u) * 64 * CH, cc[u]);
-            chunk_vals<CH, NT>(v + (c + u) * 64 * CH, vv[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < UC; ++u)
-#pragma unroll
-            for (int k = 0; k < CH; ++k) a0 = fma(vv[u][k], xr[cc[u][k]], a0);
-    }
-    for (; c < nch; ++c) {
-        double vv[CH];
-        int32_t cc[CH];
-        chunk_cols<CH, CI, NT>(cidx + c * 64 * CH, cc);
-        chunk_vals<CH, NT>(v + c * 64 * CH, vv);
-#pragma unroll
-        for (int k = 0; k < CH; ++k) a0 = fma(vv[k], xr[cc[k]], a0);
-    }
-    return a0;
-}
-
 // y = A x on the SELL-64 layout: one wave per 64-row slice, one lane per row, entries of a row
 // summed in CSR order; every value/column load is one coalesced wave access.  CI = int32_t:
 // absolute columns; CI = int16_t: column = lane base + delta (10 instead of 12 streamed bytes per
@@ -529,7 +445,7 @@ __device__ __forceinline__ double sell_slice_ch(const int32_t *__restrict__ sptr
 // [(b mod 8) * xcd_per, + xcd_per), so its L2 sees each x line once (the loop runs once per block
 // with the launchers' grids; it keeps any smaller grid correct).
 // CG mode: partials of (x, y) and early exit once the Krylov state is done.
-template <bool CG, typename CI, bool PERM, int U, bool PIPE, bool NT, int CH = 1>
+template <bool CG, typename CI, bool PERM, int U, bool PIPE, bool NT>
 __global__ void __launch_bounds__(256)
 k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows, const CI *__restrict__ scols,
             const double *__restrict__ svals, const double *__restrict__ x, double *__restrict__ y, int64_t nslices,
@@ -555,11 +471,7 @@ k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows,
         if (sl >= nslices) continue;
         int64_t row;
         bool valid;
-        double acc;
-        if constexpr (CH == 1)
-            acc = sell_slice<CI, PERM, U, PIPE, NT>(sptr, srows, scols, svals, x, n, sl, lane, row, valid);
-        else
-            acc = sell_slice_ch<CI, PERM, CH, (U + CH - 1) / CH, NT>(sptr, srows, scols, svals, x, n, sl, lane, row, valid);
+        const double acc = sell_slice<CI, PERM, U, PIPE, NT>(sptr, srows, scols, svals, x, n, sl, lane, row, valid);
         if (valid) {
             y[row] = acc;
             if (CG) dd += acc * x[row];
@@ -665,17 +577,10 @@ static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, doubl
     const dim3 g(sell_grid(c)), b(256);
     const int per = sell_xcd_per(c);
     const bool perm = c->sell_windowed;
-#define CDFEM_SPMV_CH(CI, PM, CH, U)                                                                             \
-    CDFEM_LAUNCH(c, (k_sell_spmv<CG, CI, PM, U, false, true, CH>), g, b, 0, c->d_sptr, c->d_srows,                 \
+#define CDFEM_SPMV(CI, PM)                                                                                       \
+    CDFEM_LAUNCH(c, (k_sell_spmv<CG, CI, PM, 4, false, true>), g, b, 0, c->d_sptr, c->d_srows,                     \
                  (const CI *)(sizeof(CI) == 2 ? (const void *)c->d_sdel : (const void *)c->d_scols), vals, x, y,  \
                  c->nslices, (int64_t)c->nl, per, part, st)
-#define CDFEM_SPMV(CI, PM)                                                                                       \
-    do {                                                                                                         \
-        if (c->sell_chunk == 2 && c->spmv_u == 8) CDFEM_SPMV_CH(CI, PM, 2, 8);                                   \
-        else if (c->sell_chunk == 2) CDFEM_SPMV_CH(CI, PM, 2, 4);                                                \
-        else if (c->sell_chunk == 4) CDFEM_SPMV_CH(CI, PM, 4, 4);                                                \
-        else CDFEM_SPMV_CH(CI, PM, 1, 4);                                                                        \
-    } while (0)
     if (spmv_delta(c)) {
         if (perm) CDFEM_SPMV(int16_t, true);
         else CDFEM_SPMV(int16_t, false);
@@ -684,7 +589,6 @@ static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, doubl
         else CDFEM_SPMV(int32_t, false);
     }
 #undef CDFEM_SPMV
-#undef CDFEM_SPMV_CH
 }
 
 // y = A x in the mesh's dof order.  Permuted layout: inside a permuted-order solve (perm_space)

@@ -363,15 +363,6 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
     auto by_len = [&](int32_t a, int32_t b) { return rlen(a) > rlen(b); };
     if (!pl.windowed) std::stable_sort(order.begin(), order.end(), by_len);
     const bool permuted = pl.windowed;  // kernel row = slice position (no srows)
-    // chunked storage: entry j of lane l at (j / CH) * 64 CH + l CH + j % CH inside its slice, so a
-    // lane's CH consecutive entries are one wide load (the sums keep the order j = 0, 1, ...)
-    const int CH = pl.chunk;
-    if (CH != 1 && CH != 2 && CH != 4) throw std::runtime_error("SELL chunk must be 1, 2 or 4");
-    P.chunk = CH;
-    auto pos = [&](int64_t sl, int j, int l) -> int64_t {
-        return P.sptr[sl] + (int64_t)(j / CH) * kLanes * CH + (int64_t)l * CH + j % CH;
-    };
-    auto lane_of = [&](int64_t off) -> int { return (int)((off / CH) % kLanes); };
     P.sptr.assign(ns + 1, 0);
     if (!permuted) P.srows.assign(ns * kLanes, -1);
     int64_t stored = 0;
@@ -382,7 +373,6 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
             if (!permuted) P.srows[sl * kLanes + l] = q;
             len = std::max(len, rlen(q));
         }
-        len = (len + CH - 1) / CH * CH;  // whole chunks
         stored += (int64_t)len * kLanes;
         if (stored >= ((int64_t)1 << 31)) throw std::runtime_error("SELL storage exceeds int32 indexing");
         P.sptr[sl + 1] = (int32_t)stored;
@@ -413,7 +403,7 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
                 if (!inv.empty())
                     std::sort(ent.begin(), ent.end(), [&](int32_t a, int32_t b) { return inv[cols[a]] < inv[cols[b]]; });
                 for (int j = 0; j < len; ++j) {
-                    const int64_t t = pos(sl, j, l);
+                    const int64_t t = P.sptr[sl] + (int64_t)j * kLanes + l;
                     if (r >= 0 && j < (int)ent.size()) {
                         const int32_t c = cols[ent[j]];
                         P.scols[t] = inv.empty() ? c : inv[c];
@@ -429,14 +419,14 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
     bool fits = true;
     for (int64_t sl = 0; sl < ns && fits; ++sl)
         for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t) {
-            const int64_t d = (int64_t)P.scols[t] - lane_base(sl, lane_of(t - P.sptr[sl]));
+            const int64_t d = (int64_t)P.scols[t] - lane_base(sl, (t - P.sptr[sl]) % kLanes);
             if (d < -32768 || d > 32767) { fits = false; break; }
         }
     if (fits) {
         P.sdel.resize(stored);
         for (int64_t sl = 0; sl < ns; ++sl)
             for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t)
-                P.sdel[t] = (int16_t)(P.scols[t] - lane_base(sl, lane_of(t - P.sptr[sl])));
+                P.sdel[t] = (int16_t)(P.scols[t] - lane_base(sl, (t - P.sptr[sl]) % kLanes));
     }
 }
 

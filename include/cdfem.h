@@ -250,10 +250,6 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan).  A permuted order runs the
  *               Krylov solve in that order (Mult to rounding, iterates to 1e-12).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
- * "spmv_chunk": 1 (default), 2 or 4 — read when the FA pattern is built: a lane's CH consecutive
- *             SELL entries stored together, so one 16-byte load brings two values and one load CH
- *             column deltas (rows padded to whole chunks; bitwise the chunk-1 sums).
- * "spmv_u": 4 (default) or 8 — SELL entries in flight per lane (8 only with spmv_chunk 2).
  * "gm_ept": 0 (default, auto) — entries per thread of the GMRES orthogonalisation passes (4, 5, 6
  *           or 8); auto takes the smallest whose grid is resident in one round (same results).
  * Variants measured slower and removed in round 3 (their records stay under profiles/r02_ab_*):
@@ -261,7 +257,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * folded high-order direction, the derived mass weight, per-XCD SpMV sort, SpMV stream offsets and
  * the software-pipelined SpMV loop, the two-waves-per-SIMD structured Mult, 2 / 4 lanes per SpMV row
  * (profiles/r03/ab_c4_spmv_lanes_per_row.txt), a spinning / less frequent GMRES host poll
- * (profiles/r03/ab_c2_gmres_poll.txt).                               */
+ * (profiles/r03/ab_c2_gmres_poll.txt), in-launch grid sums for the CG / GMRES scalars
+ * (profiles/r03/ab_c2_grid_fin.txt), brick-face sums in GMRES pass 1
+ * (profiles/r03/ab_c2_gmres_faces_pass1.txt), chunked SELL storage with wide loads
+ * (profiles/r03/ab_c4_spmv_chunk.txt).                                                         */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
 
 /* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */

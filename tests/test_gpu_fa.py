@@ -195,36 +195,6 @@ def test_fa_c4_full_size_properties(gpu_ctx):
     assert info["final_norm"] <= 1e-3 * info["initial_norm"]
 
 
-def test_fa_spmv_chunk_bitwise():
-    """Chunked SELL storage (set_option "spmv_chunk" 2 / 4: a lane's consecutive entries stored
-    together, one wide load for several entries) sums every row in the same entry order as the
-    default layout: Mult, the constrained Mult, GMRES iterates and an FA CG solve are bitwise those of
-    chunk 1, for 16- and 32-bit columns and for the global and windowed layouts."""
-    gm = cdfem.kuhn_mesh(3, 12, 2, perturb=0.1)
-    rng = np.random.default_rng(21)
-    x = rng.uniform(-1, 1, gm.nl)
-    b = rng.uniform(-1, 1, gm.nl)
-    for order in (0, 1):
-        for idx16 in (1, 0):
-            res = {}
-            for chunk in (1, 2, 4):
-                with cdfem.Context(0) as ctx:
-                    ctx.set_option("sell_order", order)
-                    ctx.set_option("spmv_index16", idx16)
-                    ctx.set_option("spmv_chunk", chunk)
-                    ctx.upload_mesh(gm)
-                    ctx.fa_setup(kinds=5, kappa=0.1, mass=1.0)
-                    _, Bs = ctx.form_linear_system(np.zeros(gm.nl), b)
-                    Xc, _ = ctx.solve(Bs, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=30)
-                    ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
-                    _, B = ctx.form_linear_system(np.zeros(gm.nl), b)
-                    X, _ = ctx.solve(B, method="gmres", restart=30, rel_tol=0.0, abs_tol=0.0, max_iter=40)
-                    res[chunk] = (ctx.mult(x), ctx.mult(x, constrained=True), X, Xc)
-            for chunk in (2, 4):
-                for a, c in zip(res[1], res[chunk]):
-                    np.testing.assert_array_equal(a, c)
-
-
 def test_fa_spmv_index16_matches_int32(gpu_ctx):
     """The SpMV's 16-bit column deltas (set_option "spmv_index16", the default) give the same bits
     as 32-bit columns, for Mult, the constrained Mult and a CG solve.  A random DoF numbering
