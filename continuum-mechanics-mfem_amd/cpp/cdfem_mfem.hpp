@@ -1454,6 +1454,7 @@ public:
     const std::vector<int32_t> &NbrRanks() const { return nbr_ranks_; }
     const std::vector<int64_t> &NbrOff() const { return nbr_off_; }
     const std::vector<int32_t> &NbrIdx() const { return nbr_idx_; }
+    const std::vector<int64_t> &L2G() const { return l2g_; }  // global id of each local dof
     // the space's device context (mesh + communicator, no operator), created on first use
     DeviceSpace &Space() const;
 
@@ -1491,6 +1492,7 @@ private:
         ne_ = neloc;
         nl_ = (int)nlloc;
         n_not_owned_ = nno;
+        l2g_.swap(l2g);
         structured_ = false;
     }
 
@@ -1501,6 +1503,7 @@ private:
     int vdim_ = 1, nranks_ = 1, rank_ = 0;
     int ne_ = 0, nl_ = 0, nv_ = 0, nd_ = 0, sz_ = 1;
     int64_t n_not_owned_ = 0;
+    std::vector<int64_t> l2g_;  // general partition: global id of each local dof
     bool simplex_ = false, structured_ = false, slab_lo_ = false, slab_hi_ = false;
     std::vector<double> verts_, xyz_;
     std::vector<int32_t> dofs_, bmask_;
@@ -1545,6 +1548,7 @@ public:
                 const auto &ix = fes.NbrIdx();
                 check(cdfem_set_shared(ctx_, (int)r.size(), r.data(), o.data(), ix.empty() ? nullptr : ix.data()), ctx_,
                       "cdfem_set_shared");
+                check(cdfem_check_shared(ctx_, fes.L2G().data()), ctx_, "cdfem_check_shared");
             }
         }
         ess_ = ess;

@@ -943,6 +943,39 @@ int cdfem_set_shared(cdfem_ctx *c, int n_nbr, const int32_t *nbr_ranks, const in
     });
 }
 
+// every shared entry's global id against the neighbour's entry at the same position: the shared
+// sums pair slot j of a neighbour list with local dof idx[j] on both sides, so the lists must agree
+// entry for entry (ascending global id); a mismatch fails on both ranks of the pair
+int cdfem_check_shared(cdfem_ctx *c, const int64_t *l2g)
+{
+    return guarded(c, [&] {
+        require_mesh(c);
+        if (c->part_mode != 2) throw StateError("declare the partition first (cdfem_set_shared)");
+        if (!l2g) throw ArgError("l2g is null");
+        const int nn = (int)c->nbr_rank.size();
+        const int64_t ntot = nn ? c->nbr_off[nn] : 0;
+        if (ntot == 0) return CDFEM_OK;
+        std::vector<double> send((size_t)ntot), recv((size_t)ntot);
+        for (int64_t j = 0; j < ntot; ++j) {
+            const int64_t g = l2g[c->h_sh_idx[j]];
+            if (g < 0 || g >= ((int64_t)1 << 53)) throw ArgError("global dof id out of range");
+            send[j] = (double)g;  // exact below 2^53
+        }
+        HIPCHK(hipMemcpyAsync(c->d_sh_send, send.data(), ntot * 8, hipMemcpyHostToDevice, c->stream));
+        comm_exchange_nbr_buf(c, c->nbr_off, c->d_sh_send, c->d_sh_recv, c->stream);
+        HIPCHK(hipMemcpyAsync(recv.data(), c->d_sh_recv, ntot * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (int k = 0; k < nn; ++k)
+            for (int64_t j = c->nbr_off[k]; j < c->nbr_off[k + 1]; ++j)
+                if (recv[j] != send[j])
+                    throw ArgError("shared-dof list with rank " + std::to_string(c->nbr_rank[k]) + " differs at entry " +
+                                   std::to_string(j - c->nbr_off[k]) + ": global id " +
+                                   std::to_string((int64_t)send[j]) + " here, " + std::to_string((int64_t)recv[j]) +
+                                   " there (both sides must list the shared dofs in ascending global id)");
+        return CDFEM_OK;
+    });
+}
+
 int cdfem_true_size(cdfem_ctx *c, int64_t *ntrue, int64_t *first_owned)
 {
     return guarded(c, [&] {

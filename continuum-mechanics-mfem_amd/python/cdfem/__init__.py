@@ -112,6 +112,7 @@ def _declare(L):
         "cdfem_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, ALLREDUCE_FN, EXCHANGE_FN, vp]),
         "cdfem_set_slab": (C.c_int, [vp, C.c_int, C.c_int]),
         "cdfem_set_shared": (C.c_int, [vp, C.c_int, _ip, C.POINTER(i64), _ip]),
+        "cdfem_check_shared": (C.c_int, [vp, C.POINTER(i64)]),
         "cdfem_comm_set_host_nbr_exchange": (C.c_int, [vp, NBR_EXCHANGE_FN, vp]),
         "cdfem_true_size": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i64)]),
         "cdfem_prolongate": (C.c_int, [vp, vp, vp, C.c_int]),
@@ -553,13 +554,21 @@ class Context:
     def set_slab(self, zlo_shared, zhi_shared):
         self._chk(self.L.cdfem_set_slab(self.h, int(bool(zlo_shared)), int(bool(zhi_shared))))
 
-    def set_shared(self, ls: LocalSpace):
-        """General partition: the shared-dof lists of this rank's LocalSpace."""
+    def set_shared(self, ls: LocalSpace, check=True):
+        """General partition: the shared-dof lists of this rank's LocalSpace (checked against the
+        neighbours' lists by global id unless check=False; the check is collective)."""
         nr, no, ni = _i32(ls.nbr_ranks), np.ascontiguousarray(ls.nbr_off, dtype=np.int64), _i32(ls.nbr_idx)
         if len(ni) == 0:
             ni = np.zeros(1, dtype=np.int32)
         self._chk(self.L.cdfem_set_shared(self.h, len(nr), nr.ctypes.data_as(_ip),
                                           no.ctypes.data_as(C.POINTER(C.c_int64)), ni.ctypes.data_as(_ip)))
+        if check:  # collective with the neighbours: the lists must pair entries by global id
+            self.check_shared(ls.l2g)
+
+    def check_shared(self, l2g):
+        """cdfem_check_shared: every shared entry's global id equals the neighbour's at its position."""
+        g = np.ascontiguousarray(l2g, dtype=np.int64)
+        self._chk(self.L.cdfem_check_shared(self.h, g.ctypes.data_as(C.POINTER(C.c_int64))))
 
     def true_size(self):
         """(number of true dofs, first owned L-dof): the T-vector is the L-vector suffix."""

@@ -298,6 +298,11 @@ int cdfem_set_slab(cdfem_ctx *ctx, int zlo_shared, int zhi_shared);
  * nbr_off: n_nbr + 1 offsets into nbr_idx (n_nbr = 0: a rank that shares nothing).                 */
 int cdfem_set_shared(cdfem_ctx *ctx, int n_nbr, const int32_t *nbr_ranks, const int64_t *nbr_off,
                      const int32_t *nbr_idx);
+/* Collective between neighbours, after cdfem_set_shared: sends the global id (l2g, nl entries) of
+ * every shared entry and checks that each neighbour's list holds the same id at the same position
+ * (the shared sums pair entries by position).  CDFEM_ERR_ARG on a mismatch, on both ranks of the
+ * pair, naming the neighbour and the first differing entry.                                     */
+int cdfem_check_shared(cdfem_ctx *ctx, const int64_t *l2g);
 /* Host backend of the general partition: send[nbr_off[k] .. nbr_off[k+1]) goes to nbr_ranks[k] and
  * recv[same range] receives from it (MPI_Isend/Irecv, gloo, ...).  RCCL contexts need none.      */
 typedef int (*cdfem_nbr_exchange_fn)(int n_nbr, const int32_t *nbr_ranks, const int64_t *nbr_off,

@@ -352,6 +352,52 @@ def test_gpu_partition_state_errors(gpu_ctx):
     ctx._chk(ctx.L.cdfem_comm_init_host(ctx.h, 0, 1, cbs[0], cbs[1], None))
 
 
+def _check_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    import cdfem
+    dist = _init(rank, world, port)
+    ctx = cdfem.Context(0)
+    m = _case_mesh("tri")
+    part = cdfem.partition_rcb(m, world)
+    ls = cdfem.local_space(m, part, rank)
+    ctx.upload_mesh(ls.mesh)
+    ctx.comm_init_torch()
+    ctx.set_shared(ls)                          # consistent lists: the check passes on both ranks
+    res = {"good": "ok"}
+    idx = ls.nbr_idx.copy()
+    if rank == 1:                               # rank 1 lists two shared dofs in swapped order
+        o = int(ls.nbr_off[0])
+        idx[o], idx[o + 1] = idx[o + 1], idx[o]
+    bad = cdfem.LocalSpace(ls.mesh, ls.elems, ls.l2g, ls.nbr_ranks, ls.nbr_off, idx, ls.n_not_owned)
+    ctx.set_shared(bad, check=False)            # accepted locally: the pairing is not visible from one rank
+    try:
+        ctx.check_shared(ls.l2g)
+        res["bad"] = "accepted"
+    except cdfem.CdfemError as e:
+        res["bad"] = str(e)
+    with open(os.path.join(out_dir, f"check_{rank}.txt"), "w") as f:
+        f.write(res["good"] + "\n" + res["bad"] + "\n")
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_check_shared_detects_misordered_lists(tmp_path):
+    """cdfem_check_shared (called by set_shared): the shared sums pair neighbour-list entries by
+    position, so two ranks whose lists disagree on the order would sum the wrong partials without
+    any local symptom.  Consistent lists pass; a swapped pair on one rank fails on BOTH ranks with a
+    message naming the neighbour and the entry."""
+    world = 2
+    mp.start_processes(_check_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    for r in range(world):
+        good, bad = (tmp_path / f"check_{r}.txt").read_text().splitlines()
+        assert good == "ok"
+        assert "differs at entry 0" in bad and f"rank {1 - r}" in bad, bad
+
+
 # ---- block-Jacobi ILU(0) on several ranks (Input/petsc_circle.opts:6-8 under mpirun -np N) ---------
 CIRCLE = dict(kappa=1.0, alpha=1.0, conv=(1.0, 1.0), mass=1.0)   # Input/input_2d_circle.yaml:7-10
 
