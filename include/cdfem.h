@@ -260,7 +260,8 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * (profiles/r03/ab_c2_gmres_poll.txt), in-launch grid sums for the CG / GMRES scalars
  * (profiles/r03/ab_c2_grid_fin.txt), brick-face sums in GMRES pass 1
  * (profiles/r03/ab_c2_gmres_faces_pass1.txt), chunked SELL storage with wide loads
- * (profiles/r03/ab_c4_spmv_chunk.txt).                                                         */
+ * (profiles/r03/ab_c4_spmv_chunk.txt), XCD-ordered blocks of the p >= 3 tile apply
+ * (profiles/r03/ab_c3_tile_xcd_order.txt).                                                         */
 int cdfem_set_option(cdfem_ctx *ctx, const char *key, int value);
 
 /* ---- profiling (live HIP-event timing of the hot kernels, on the context's stream) ------------ */
