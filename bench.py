@@ -57,13 +57,16 @@ def parse():
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--path", choices=["brick", "generic"], default=None,
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c4s", "c5", "c5w"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c4s", "c4u", "c5", "c5w"], default="c2",
                     help="c2: 64^3 hex p=2 PA + CG (BASELINE metric config; N>1: weak scaling, a 64^3 slab "
                          "per rank); c3: 128^3 hex p=4 PA + CG (configs[2]); c4: Kuhn 55^3 x 6 tets P2, FA CSR "
-                         "+ GMRES(30)/Jacobi (configs[3]); c5: 256^3 hex p=2 PA + CG split into N z-slabs "
+                         "+ GMRES(30)/Jacobi (configs[3]); c4u: the same on a Delaunay mesh of random points "
+                         "(~1M tets, unstructured connectivity); c5: 256^3 hex p=2 PA + CG split into N z-slabs "
                          "(configs[4] at N=8: 256 x 256 x 32 per rank); c5w: SURVEY 8e's weak series, a "
                          "256 x 256 x 32 slab per rank (N=8: the C5 mesh)")
     ap.add_argument("--tet-n", type=int, default=55, help="c4: cubes per direction (6 tets each)")
+    ap.add_argument("--tet-points", type=int, default=170000,
+                    help="c4u: Delaunay points (about 6 tets per point: 170000 -> ~1.03M tets)")
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N>1 data-path communicator: rccl (production, one GPU per rank) or host "
                          "(gloo callbacks; rehearses the N>1 flow with several ranks on one GPU)")
@@ -283,21 +286,31 @@ def _cpu_baseline_box(args, O, n, p, kinds, threads, host):
             **host}
 
 
-def cpu_baseline_c4(args, n, p):
-    """Oracle FA-CSR GMRES(30)/Jacobi on the same Kuhn mesh (bounded sample, median of
-    CPU_SAMPLES samples after a warm-up)."""
+def cpu_baseline_c4(args, n, p, mesh=None):
+    """Oracle FA-CSR GMRES(30)/Jacobi on the same Kuhn mesh, or on `mesh` (c4u: the same Delaunay
+    mesh; bounded sample, median of CPU_SAMPLES samples after a warm-up)."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     threads, host = host_cores(args)
     O.set_threads(threads)
     with PinnedThreads(O, threads) as pin:
-        out = _cpu_baseline_kuhn(args, O, n, p, threads, host)
+        out = _cpu_baseline_kuhn(args, O, n, p, threads, host, mesh)
     out.update(pin.record())
     return out
 
 
-def _cpu_baseline_kuhn(args, O, n, p, threads, host):
-    m = O.KuhnMesh(3, n, p)
+class _OracleMesh:
+    """The oracle's mesh container for a product simplex Mesh (verts, dofmap, boundary marker)."""
+
+    def __init__(self, m):
+        self.dim, self.p, self.ne, self.nl = m.dim, m.order, m.ne, m.nl
+        self.verts, self.dofmap, self.ess = m.verts, m.dofmap, m.ess
+        self.bdr = np.zeros(m.nl, dtype=np.int32)
+        self.bdr[m.ess] = 1
+
+
+def _cpu_baseline_kuhn(args, O, n, p, threads, host, mesh=None):
+    m = O.KuhnMesh(3, n, p) if mesh is None else _OracleMesh(mesh)
     t0 = time.perf_counter()
     A = O.fa_assemble_simplex(m, kappa=0.1, alpha=1.0, s=1.0, c=(1.0, -2.0, 0.5))
     b = np.random.default_rng(20261015).uniform(-1, 1, m.nl)
@@ -309,8 +322,9 @@ def _cpu_baseline_kuhn(args, O, n, p, threads, host):
     def gmres(k):
         return O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=k)[1]["iterations"]
     v, rec, its, dt = cpu_samples(gmres, m.nl, args.cpu_seconds, 3000)
+    what = f"Kuhn {n}^3x6 tets" if mesh is None else f"the same Delaunay mesh ({m.ne} tets)"
     return {"value": v, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
-            "sample": f"oracle FA-CSR GMRES(30)/Jacobi, Kuhn {n}^3x6 tets P{p} ({m.nl} DoFs, nnz={Ac.nnz}): median "
+            "sample": f"oracle FA-CSR GMRES(30)/Jacobi, {what} P{p} ({m.nl} DoFs, nnz={Ac.nnz}): median "
                       f"of {CPU_SAMPLES} samples of {rec['iterations_per_sample']} iterations after a warm-up "
                       f"({its} iterations, {dt:.2f} s timed); assembly+FormLinearSystem {t_asm:.1f} s untimed",
             **rec, **host}
@@ -320,7 +334,15 @@ def main_c4(args):
     """BASELINE configs[3]: unstructured-path tets, FA CSR SpMV + GMRES(30)/Jacobi on 1 GPU."""
     import cdfem
     n, p = args.tet_n, 2
-    mesh = cdfem.kuhn_mesh(3, n, p, with_coords=False)
+    unstructured = args.config == "c4u"
+    t_mesh = 0.0
+    if unstructured:
+        # c4u: unstructured connectivity (Delaunay of random points, scipy/Qhull on the host, untimed)
+        t0 = time.perf_counter()
+        mesh = cdfem.simplex_space(*cdfem.delaunay_cube(args.tet_points, seed=20261017), p)
+        t_mesh = time.perf_counter() - t0
+    else:
+        mesh = cdfem.kuhn_mesh(3, n, p, with_coords=False)
     shuffled = args.config == "c4s"
     if shuffled:
         # c4s: the same mesh with a random dof numbering (what a gmsh file without bandwidth
@@ -371,7 +393,7 @@ def main_c4(args):
             traffic = None
             if os.path.exists(args.traffic_json):
                 try:
-                    key = f"{'c4s' if shuffled else 'c4'}_n{n}_p{p}"
+                    key = f"{args.config}_n{n}_p{p}" if not unstructured else f"c4u_pts{args.tet_points}_p{p}"
                     traffic = json.load(open(args.traffic_json)).get(key, {}).get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
@@ -391,16 +413,19 @@ def main_c4(args):
     cpu = None
     if not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline_c4(args, n, p)
+            cpu = cpu_baseline_c4(args, n, p, mesh if unstructured else None)
         except Exception as e:
             cpu = {"error": repr(e)}
     out = {"metric": "DoF-iter/s (CG, 3D p=2 hex convection-diffusion) + achieved HBM GB/s",
            "value": mesh.nl * iters / dt, "unit": "DoF-iter/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-           "config": {"workload": f"{'C4s' if shuffled else 'C4'}: Kuhn {n}^3x6 tets P2"
-                                  f"{', shuffled dof numbering (RCM SpMV order)' if shuffled else ''}, FA CSR "
-                                  f"(GPU-assembled) + GMRES(30)/Jacobi {iters_per_step} it/step",
+           "config": {"workload": (f"C4u: Delaunay tets of {args.tet_points} random points in the unit cube "
+                                   f"({mesh.ne} tets) P2" if unstructured else
+                                   f"{'C4s' if shuffled else 'C4'}: Kuhn {n}^3x6 tets P2"
+                                   f"{', shuffled dof numbering (RCM SpMV order)' if shuffled else ''}")
+                                  + f", FA CSR (GPU-assembled) + GMRES(30)/Jacobi {iters_per_step} it/step",
+                      **({"mesh_generation_s": round(t_mesh, 1)} if unstructured else {}),
                       "dofs": mesh.nl, "elements": mesh.ne, "nnz": nnz,
                       "fa_setup_s": round(t_setup, 3), "parallelism": "single"},
            "roofline": roof, "cpu_baseline": cpu}
@@ -412,7 +437,7 @@ def main_c4(args):
 
 def main():
     args = parse()
-    if args.config in ("c4", "c4s"):
+    if args.config in ("c4", "c4s", "c4u"):
         return main_c4(args)
     world, rank, local, pg = dist_setup(args)
     import cdfem

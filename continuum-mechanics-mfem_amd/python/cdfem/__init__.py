@@ -248,6 +248,78 @@ def kuhn_mesh(dim, n, order, perturb=0.0, with_coords=True) -> Mesh:
     return Mesh(dim, order, verts, dofmap, nl.value, ess, xyz, simplex=True)
 
 
+def simplex_space(vxyz, elem_v, bdr_v, bdr_attr, order) -> Mesh:
+    """H1 space of the given order on a simplex topology (cdfem_simplex_space): vertex coordinates
+    (nv, dim), elements (ne, dim + 1) and boundary facets (nbe, dim) with their attributes; essential
+    dofs on every boundary attribute."""
+    L = lib()
+    vx = np.ascontiguousarray(vxyz, dtype=np.float64)
+    dim = vx.shape[1]
+    ev, bv, ba = _i32(elem_v), _i32(bdr_v), _i32(bdr_attr)
+    nl = C.c_int64()
+    rc = L.cdfem_simplex_space_sizes(dim, len(vx), _p(vx), len(ev), ev.ctypes.data_as(_ip), order, C.byref(nl))
+    if rc:
+        raise CdfemError(rc, "bad simplex topology")
+    nd = dim + 1 if order == 1 else (dim + 1) * (dim + 2) // 2 if order == 2 else 10
+    verts = np.zeros((len(ev), dim + 1, dim))
+    dofmap = np.zeros((len(ev), nd), dtype=np.int32)
+    mask = np.zeros(nl.value, dtype=np.int32)
+    xyz = np.zeros((nl.value, dim))
+    rc = L.cdfem_simplex_space(dim, len(vx), _p(vx), len(ev), ev.ctypes.data_as(_ip), len(bv), bv.ctypes.data_as(_ip),
+                               ba.ctypes.data_as(_ip), order, _p(verts), dofmap.ctypes.data_as(_ip),
+                               mask.ctypes.data_as(_ip), _p(xyz))
+    if rc:
+        raise CdfemError(rc, "simplex space construction failed")
+    m = Mesh(dim, order, verts, dofmap, nl.value, np.nonzero(mask)[0].astype(np.int32), xyz, simplex=True)
+    m.bdr_mask = mask
+    return m
+
+
+def delaunay_cube(npts, seed=0):
+    """A genuinely unstructured tetrahedral mesh of [0,1]^3 (BASELINE configs[3], "unstructured tet
+    mesh"): the Delaunay tetrahedralisation (scipy.spatial, Qhull) of about npts random points — the 8
+    corners, uniform points on the 12 edges and the 6 faces (k - 2, (k - 2)^2 each, k = npts^(1/3))
+    and uniform interior points — so that no four points are coplanar except on a cube face.  The flat
+    tetrahedra Qhull returns for coplanar points of one face (volume exactly 0, all four vertices in
+    the face plane) are dropped, which leaves the mesh conforming; the boundary facets are the faces
+    held by one tetrahedron (attribute 1).  Returns (vxyz, tets, facets, attrs) in Qhull's point
+    order (unbanded: the FA setup chooses the SpMV order)."""
+    from scipy.spatial import Delaunay  # host-side mesh generation only
+    rng = np.random.default_rng(seed)
+    k = max(3, int(round(npts ** (1.0 / 3.0))))
+    parts = [np.array([[i, j, l] for i in (0.0, 1.0) for j in (0.0, 1.0) for l in (0.0, 1.0)])]
+    for a in range(3):  # 4 edges along axis a
+        for b0 in (0.0, 1.0):
+            for b1 in (0.0, 1.0):
+                e = np.empty((k - 2, 3))
+                e[:, a] = rng.uniform(0.0, 1.0, k - 2)
+                e[:, (a + 1) % 3], e[:, (a + 2) % 3] = b0, b1
+                parts.append(e)
+    for a in range(3):  # 2 faces normal to axis a
+        for c in (0.0, 1.0):
+            f = rng.uniform(0.0, 1.0, ((k - 2) ** 2, 3))
+            f[:, a] = c
+            parts.append(f)
+    nb = sum(len(q) for q in parts)
+    parts.append(rng.uniform(0.0, 1.0, (max(npts - nb, 1), 3)))
+    pts = np.concatenate(parts)
+    tets = Delaunay(pts).simplices.astype(np.int32)
+    v = pts[tets]
+    vol = np.einsum("ij,ij->i", np.cross(v[:, 1] - v[:, 0], v[:, 2] - v[:, 0]), v[:, 3] - v[:, 0])
+    flat = np.abs(vol) <= 1e-14 * max(np.abs(vol).max(), 1e-300)
+    on_face = np.zeros(len(tets), dtype=bool)
+    for a in range(3):
+        for c in (0.0, 1.0):
+            on_face |= np.all(v[:, :, a] == c, axis=1)
+    if np.any(flat & ~on_face):
+        raise RuntimeError("Delaunay returned a flat tetrahedron off the cube faces (degenerate input)")
+    tets = tets[~flat]
+    faces = np.sort(np.concatenate([tets[:, [1, 2, 3]], tets[:, [0, 2, 3]], tets[:, [0, 1, 3]], tets[:, [0, 1, 2]]]), 1)
+    uniq, cnt = np.unique(faces, axis=0, return_counts=True)
+    facets = uniq[cnt == 1].astype(np.int32)
+    return pts, tets, facets, np.ones(len(facets), dtype=np.int32)
+
+
 def gmsh_mesh(path, order, ess_attrs=None) -> Mesh:
     """A gmsh v2.2 simplex mesh (e.g. the reference's Mesh/unit_square.msh) with an H1 space of the
     given order; essential dofs on the boundary attributes ess_attrs (None: all)."""

@@ -98,6 +98,63 @@ def test_fa_gmres_parity(gpu_ctx, dim, n, p, pert):
     assert np.linalg.norm(xg - xo) <= 1e-8 * np.linalg.norm(xo)
 
 
+class _DelaunayOM:
+    """Oracle container for a product simplex Mesh (the Delaunay mesh of cdfem.delaunay_cube)."""
+
+    def __init__(self, m):
+        self.dim, self.p, self.ne, self.nl = m.dim, m.order, m.ne, m.nl
+        self.verts, self.dofmap, self.ess = m.verts, m.dofmap, m.ess
+        self.bdr = np.zeros(m.nl, dtype=np.int32)
+        self.bdr[m.ess] = 1
+
+
+@pytest.mark.parametrize("order", [1, 2])
+def test_fa_delaunay_parity(order):
+    """BASELINE configs[3] on genuinely unstructured connectivity (the c4u bench mesh family): a
+    Delaunay tetrahedralisation of random points in the unit cube (cdfem.delaunay_cube, 3000 points,
+    ~16.6 K tets), in Qhull's unbanded point order, so the FA setup picks the geometric SpMV order
+    and the Krylov solve runs permuted.  Against the oracle: the CSR pattern exact, values and the
+    constrained Mult to 1e-13, 25 fixed GMRES(7) iterates to 1e-11, the reference's GMRES settings
+    (iterations +-1, solutions to 1e-8) and both solved to rtol 1e-13 to 1e-10."""
+    gm = cdfem.simplex_space(*cdfem.delaunay_cube(3000, seed=5), order)
+    om = _DelaunayOM(gm)
+    A = O.fa_assemble_simplex(om, kappa=0.1, alpha=1.0, s=1.0, c=C3)
+    with cdfem.Context(0) as ctx:
+        ctx.upload_mesh(gm)
+        ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+        rp, cols, vals = ctx.fa_csr()
+        orp, ocol, oval = A.export()
+        np.testing.assert_array_equal(rp, orp)
+        np.testing.assert_array_equal(cols, ocol)
+        assert np.abs(vals - oval).max() <= 1e-13 * np.abs(oval).max()
+        rng = np.random.default_rng(9)
+        x = rng.uniform(-1, 1, om.nl)
+        xz = x.copy()
+        xz[om.ess] = 0.0
+        yc = A.mult(xz)
+        yc[om.ess] = x[om.ess]
+        assert np.abs(ctx.mult(x, constrained=True) - yc).max() <= 1e-13 * np.abs(yc).max()
+        u = np.zeros(om.nl)
+        u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+        b = rng.uniform(-1, 1, om.nl)
+        Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+        _, B = ctx.form_linear_system(u, b)
+        assert np.abs(B - Bo).max() <= 1e-13 * np.abs(Bo).max()
+        dinv = 1.0 / Ac.diag()
+        xo, io = O.gmres(Ac, Bo, dinv=dinv, restart=7, rtol=0.0, atol=0.0, max_it=25)
+        xg, ig = ctx.solve(B, method="gmres", restart=7, rel_tol=0.0, abs_tol=0.0, max_iter=25)
+        assert io["iterations"] == ig["iterations"] == 25
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
+        xo, io = O.gmres(Ac, Bo, dinv=dinv, restart=30, rtol=1e-10, atol=1e-12, max_it=2000)
+        xg, ig = ctx.solve(B, method="gmres", restart=30, rel_tol=1e-10, abs_tol=1e-12, max_iter=2000)
+        assert io["converged"] and ig["converged"] and abs(io["iterations"] - ig["iterations"]) <= 1
+        assert np.linalg.norm(xg - xo) <= 1e-8 * np.linalg.norm(xo)
+        xo, io = O.gmres(Ac, Bo, dinv=dinv, restart=30, rtol=1e-13, atol=0.0, max_it=4000)
+        xg, ig = ctx.solve(B, method="gmres", restart=30, rel_tol=1e-13, abs_tol=0.0, max_iter=4000)
+        assert io["converged"] and ig["converged"]
+        assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
+
+
 def test_fa_cg_parity(gpu_ctx):
     gm, om, A = _setup(gpu_ctx, 3, 4, 2, 0.1, kinds=5)   # kappa K + s M: SPD
     rng = np.random.default_rng(4)

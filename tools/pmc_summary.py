@@ -78,7 +78,9 @@ def main():
     p = os.path.join(prof, "pmc_traffic.json")
     tj = json.load(open(p)) if os.path.exists(p) else {}
     wl = cfg["workload"]
-    if wl.startswith("C4"):
+    if wl.startswith("C4u"):
+        key = f"c4u_pts{int(wl.split('Delaunay tets of ')[1].split(' ')[0])}_p2"
+    elif wl.startswith("C4"):
         key = f"{wl.split(':')[0].lower()}_n{int(wl.split('Kuhn ')[1].split('^')[0])}_p2"
     else:
         n = int(wl.split("x")[0])

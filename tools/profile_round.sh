@@ -2,7 +2,7 @@
 # Round profile of one bench configuration:
 #   bench line (with CPU baseline), rocprofv3 kernel stats of the same bench command, and
 #   PMC HBM traffic passes (FETCH_SIZE, WRITE_SIZE) plus the stream-probe calibration pass.
-# usage: bash tools/profile_round.sh TAG [c2|c3|c4|c4s]
+# usage: bash tools/profile_round.sh TAG [c2|c3|c4|c4s|c4u]
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -13,7 +13,7 @@ mkdir -p $OUT
 case $CFG in
   c2) SHORT="--cg-iters 20 --spd-steps 0";;
   c3) SHORT="--cg-iters 4 --gmres-iters 0 --spd-steps 0";;
-  c4|c4s) SHORT="--gmres-iters 30";;
+  c4|c4s|c4u) SHORT="--gmres-iters 30";;
   c5) SHORT="--cg-iters 10 --gmres-iters 0 --spd-steps 0";;
 esac
 timeout -k 10 900 python bench.py --config $CFG --steps 5 --warmup 1 > $OUT/bench.json 2> $OUT/bench.err || exit $?
