@@ -96,7 +96,10 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_stab); dfree(c->d_stab_lf); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);
     dfree(c->d_cpos); dfree(c->d_vals); dfree(c->d_vals_c); dfree(c->d_Ee);
     dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_sdel); dfree(c->d_svals);
+    dfree(c->d_swide);
     c->d_sdel = nullptr;
+    c->d_swide = nullptr;
+    c->sell_nnz_wide = 0;
     dfree(c->d_rperm); dfree(c->d_pv[0]); dfree(c->d_pv[1]); dfree(c->d_dinv_p);
     c->d_rperm = nullptr; c->d_pv[0] = c->d_pv[1] = nullptr; c->d_dinv_p = nullptr;
     dfree(c->d_svals_c);
@@ -1258,11 +1261,11 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             // a multi-rank partition keeps the mesh order (its shared-dof exchange indexes L-vectors)
             // dof coordinates for the geometric SpMV order (simplex geometry is on the host)
             std::vector<double> xyz;
-            if (!multi_rank(c) && (c->sell_mode == 3 || c->sell_mode == 5) && !c->h_verts.empty())
+            if (!multi_rank(c) && (c->sell_mode == 3 || c->sell_mode >= 5) && !c->h_verts.empty())
                 xyz = simplex_dof_coords(c->dim, c->p, c->ne, c->nd, c->nl, c->h_verts, c->h_dofs);
             FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl,
                                            multi_rank(c) ? 0 : c->sell_mode, c->dim,
-                                           xyz.empty() ? nullptr : xyz.data());
+                                           xyz.empty() ? nullptr : xyz.data(), c->sell_window);
             c->nnz = P.nnz;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
             c->d_cols = dalloc<int32_t>(P.cols.size());
@@ -1300,6 +1303,11 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             if (!P.sdel.empty()) {
                 c->d_sdel = dalloc<int16_t>(P.sdel.size());
                 HIPCHK(hipMemcpyAsync(c->d_sdel, P.sdel.data(), P.sdel.size() * 2, hipMemcpyHostToDevice, c->stream));
+            }
+            if (!P.swide.empty()) {  // mixed layout: the slices beyond 16 bits stream d_scols
+                c->d_swide = dalloc<uint8_t>(P.swide.size());
+                HIPCHK(hipMemcpyAsync(c->d_swide, P.swide.data(), P.swide.size(), hipMemcpyHostToDevice, c->stream));
+                c->sell_nnz_wide = P.nnz_wide;
             }
             HIPCHK(hipStreamSynchronize(c->stream));  // P's host buffers die at scope exit
         }
@@ -1547,9 +1555,13 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;
         } else if (k == "sell_order") {  // read when the FA pattern is built (once per mesh)
-            if (value < 0 || value > 5)
-                throw ArgError("sell_order must be 0..5 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric)");
+            if (value < 0 || value > 7)
+                throw ArgError("sell_order must be 0..7 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton)");
             c->sell_mode = value;
+        } else if (k == "sell_window") {  // read when the FA pattern is built (once per mesh)
+            if (value < 0 || (value > 0 && (value % 64 != 0 || value > (1 << 20))))
+                throw ArgError("sell_window must be 0 (auto) or a multiple of 64 up to 2^20");
+            c->sell_window = value;
         } else if (k == "gm_ept") {
             if (value != 0 && value != 4 && value != 5 && value != 6 && value != 8)
                 throw ArgError("gm_ept must be 0 (auto), 4, 5, 6 or 8");
@@ -1608,7 +1620,10 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
         if (c->fa_ready) {  // CSR SpMV: values + columns + row pointers + x + y
             if (k != CDFEM_K_APPLY) throw ArgError("FA operators report the SpMV (CDFEM_K_APPLY) only");
             // (SELL adds < 1 % padding; 16-bit column deltas when the bandwidth fits)
-            *bytes = (spmv_delta(c) ? 10.0 : 12.0) * (double)c->nnz + 4.0 * (nl + 1) + 16.0 * nl;
+            // 8 B value + 2 B delta per entry (4 B column in the 32-bit slices of a mixed layout)
+            *bytes = spmv_delta(c) ? 10.0 * (double)c->nnz + 2.0 * (double)c->sell_nnz_wide + 4.0 * (nl + 1) + 16.0 * nl +
+                                         (c->d_swide ? (double)c->nslices : 0.0)
+                                   : 12.0 * (double)c->nnz + 4.0 * (nl + 1) + 16.0 * nl;
             return CDFEM_OK;
         }
         const double nq = nq_of(c, c->rule_op);

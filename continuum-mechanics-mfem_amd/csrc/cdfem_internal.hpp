@@ -207,6 +207,8 @@ struct cdfem_ctx {
     int32_t *d_sptr = nullptr, *d_srows = nullptr, *d_scols = nullptr, *d_smap = nullptr;
     double *d_tpart = nullptr;          // den partials of the fused high-order CG apply (one per tile block)
     int16_t *d_sdel = nullptr;          // 16-bit column deltas (null when the bandwidth does not fit)
+    uint8_t *d_swide = nullptr;         // per slice: 1 = streams 32-bit columns (mixed layout; null: none)
+    int64_t sell_nnz_wide = 0;          // real entries in the 32-bit slices of a mixed layout
     int mr_overlap = 1;                 // set_option "mr_overlap": slab CG exchange overlapped with interior bricks
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
@@ -214,6 +216,7 @@ struct cdfem_ctx {
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
+    int sell_window = 0;                // set_option "sell_window": rows per window of a windowed order (0 auto)
     int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD (windowed layout)
     int32_t *d_rperm = nullptr;         // SpMV space order: space row -> mesh row (null: mesh order)
     bool sell_windowed = false;         // slices cut from the space order (kernel row = slice * 64 + lane)
@@ -363,27 +366,30 @@ struct FaPattern {
     std::vector<int32_t> srows;  // [nslices * 64] original row of (slice, lane), -1 = padding
     std::vector<int32_t> scols;  // [stored] column, slice-major then entry-major then lane
     std::vector<int32_t> smap;   // [stored] CSR index of the stored entry, -1 = padding
-    std::vector<int16_t> sdel;   // [stored] column - row when every |column - row| < 2^15, else empty
+    std::vector<int16_t> sdel;   // [stored] column - lane row where it fits 16 bits (see swide), else empty
+    std::vector<uint8_t> swide;  // [nslices] 1: this slice has a delta beyond 16 bits and streams scols
+                                 // (empty: every slice fits); nnz_wide = real entries in such slices
+    int64_t nnz_wide = 0;
     std::vector<int32_t> perm;   // SpMV space order (sell_plan.cpp): space row -> mesh row; empty = mesh order
     bool windowed = false;       // slices cut from the space order directly (no srows)
 };
 // SpMV order (sell_plan.cpp): 0 natural + global sort, 1 natural + windows, 2 RCM + windows,
 // 3 auto (mode 0, geometric or RCM + global), 4 RCM + global, 5 geometric + global
 struct SellPlan {
-    int mode = 0, base = 1;  // base: 1 natural, 2 RCM, 3 geometric
+    int mode = 0, base = 1;  // base: 1 natural, 2 RCM, 3 geometric, 4 Morton
     bool windowed = false;
     int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0, bw_geometric = 0;
     std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
 };
 std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
 SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim = 0,
-                   const double *xyz = nullptr);
+                   const double *xyz = nullptr, int64_t window = 0);
 // dof coordinates of a simplex space (P1, P2, triangle P3 nodes; element-affine map), nl * dim
 std::vector<double> simplex_dof_coords(int dim, int p, int ne, int nd, int64_t nl, const std::vector<double> &verts,
                                        const std::vector<int32_t> &dofs);
 void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl);
 FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl, int sell_mode,
-                           int dim = 0, const double *dof_xyz = nullptr);
+                           int dim = 0, const double *dof_xyz = nullptr, int64_t sell_window = 0);
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq, double kappa, double alpha,
                                const double *conv, const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);

@@ -49,7 +49,7 @@ static inline int64_t ee_index(int e, int i, int j, int nd)
 }
 
 FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int64_t nl, int sell_mode, int dim,
-                           const double *dof_xyz)
+                           const double *dof_xyz, int64_t sell_window)
 {
     // dof -> incidences (e * nd + l), ascending
     std::vector<int64_t> cnt(nl + 1, 0);
@@ -132,7 +132,7 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     });
     // SpMV layout: SELL-64 over the rows in the plan's order (sell_plan.cpp)
     P.rowptr = std::move(rowptr);
-    SellPlan pl = sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode, dim, dof_xyz);
+    SellPlan pl = sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode, dim, dof_xyz, sell_window);
     sell_build(P, nl, pl);
     return P;
 }
@@ -445,11 +445,14 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ sptr, c
 // [(b mod 8) * xcd_per, + xcd_per), so its L2 sees each x line once (the loop runs once per block
 // with the launchers' grids; it keeps any smaller grid correct).
 // CG mode: partials of (x, y) and early exit once the Krylov state is done.
-template <bool CG, typename CI, bool PERM, int U, bool PIPE, bool NT>
+// MIX (CI = int16_t): mixed layout, a slice flagged in swide holds a column beyond 16 bits of its
+// lane row and streams its 32-bit columns (cols32) instead (the flag is wave-uniform).
+template <bool CG, typename CI, bool PERM, int U, bool PIPE, bool NT, bool MIX = false>
 __global__ void __launch_bounds__(256)
 k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows, const CI *__restrict__ scols,
             const double *__restrict__ svals, const double *__restrict__ x, double *__restrict__ y, int64_t nslices,
-            int64_t n, int xcd_per, double *__restrict__ part, const KrylovState *__restrict__ st)
+            int64_t n, int xcd_per, double *__restrict__ part, const KrylovState *__restrict__ st,
+            const int32_t *__restrict__ cols32, const uint8_t *__restrict__ swide)
 {
     __shared__ double sh[256 / 64];
     if (CG && st->done) return;
@@ -471,7 +474,11 @@ k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows,
         if (sl >= nslices) continue;
         int64_t row;
         bool valid;
-        const double acc = sell_slice<CI, PERM, U, PIPE, NT>(sptr, srows, scols, svals, x, n, sl, lane, row, valid);
+        double acc;
+        if (MIX && swide[sl])
+            acc = sell_slice<int32_t, PERM, U, PIPE, NT>(sptr, srows, cols32, svals, x, n, sl, lane, row, valid);
+        else
+            acc = sell_slice<CI, PERM, U, PIPE, NT>(sptr, srows, scols, svals, x, n, sl, lane, row, valid);
         if (valid) {
             y[row] = acc;
             if (CG) dd += acc * x[row];
@@ -580,8 +587,14 @@ static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, doubl
 #define CDFEM_SPMV(CI, PM)                                                                                       \
     CDFEM_LAUNCH(c, (k_sell_spmv<CG, CI, PM, 4, false, true>), g, b, 0, c->d_sptr, c->d_srows,                     \
                  (const CI *)(sizeof(CI) == 2 ? (const void *)c->d_sdel : (const void *)c->d_scols), vals, x, y,  \
-                 c->nslices, (int64_t)c->nl, per, part, st)
-    if (spmv_delta(c)) {
+                 c->nslices, (int64_t)c->nl, per, part, st, (const int32_t *)nullptr, (const uint8_t *)nullptr)
+#define CDFEM_SPMV_MIX(PM)                                                                                       \
+    CDFEM_LAUNCH(c, (k_sell_spmv<CG, int16_t, PM, 4, false, true, true>), g, b, 0, c->d_sptr, c->d_srows,          \
+                 c->d_sdel, vals, x, y, c->nslices, (int64_t)c->nl, per, part, st, c->d_scols, c->d_swide)
+    if (spmv_delta(c) && c->d_swide) {
+        if (perm) CDFEM_SPMV_MIX(true);
+        else CDFEM_SPMV_MIX(false);
+    } else if (spmv_delta(c)) {
         if (perm) CDFEM_SPMV(int16_t, true);
         else CDFEM_SPMV(int16_t, false);
     } else {
@@ -589,6 +602,7 @@ static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, doubl
         else CDFEM_SPMV(int32_t, false);
     }
 #undef CDFEM_SPMV
+#undef CDFEM_SPMV_MIX
 }
 
 // y = A x in the mesh's dof order.  Permuted layout: inside a permuted-order solve (perm_space)

@@ -24,7 +24,8 @@
 //             2 = RCM + windows, 3 = auto (mode 0 when the mesh order is banded: 16-bit deltas and
 //             bandwidth under nl / 8; else the geometric order when coordinates are given and it
 //             is banded that way; else RCM + global when its bandwidth is under half the natural
-//             one), 4 = RCM + global, 5 = geometric + global.
+//             one), 4 = RCM + global, 5 = geometric + global, 6 = Morton + windows, 7 = Morton +
+//             global (morton_order).
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -223,17 +224,67 @@ std::vector<int32_t> geometric_order(int64_t nl, int dim, const double *xyz)
     return order;
 }
 
-SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim, const double *xyz)
+// Morton (Z-curve) order of the dof coordinates: each axis quantised to 2^21 cells of the bounding
+// box, bits interleaved (x lowest), ties by mesh index.  A space-filling curve keeps every run of
+// consecutive positions spatially compact on any mesh (unlike the slab order of geometric_order, whose
+// bandwidth on an unstructured mesh is the long edges' reach across z cells).
+std::vector<int32_t> morton_order(int64_t nl, int dim, const double *xyz)
+{
+    double lo[3] = {0, 0, 0}, hi[3] = {1, 1, 1};
+    for (int k = 0; k < dim; ++k) {
+        lo[k] = hi[k] = xyz[k];
+        for (int64_t i = 1; i < nl; ++i) {
+            lo[k] = std::min(lo[k], xyz[i * dim + k]);
+            hi[k] = std::max(hi[k], xyz[i * dim + k]);
+        }
+    }
+    const int bits = dim == 3 ? 21 : 31;
+    const double cells = (double)((1u << bits) - 1);
+    std::vector<uint64_t> key(nl);
+    par_for(nl, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            uint64_t q[3] = {0, 0, 0};
+            for (int k = 0; k < dim; ++k) {
+                const double t = (xyz[i * dim + k] - lo[k]) / std::max(hi[k] - lo[k], 1e-300);
+                q[k] = (uint64_t)std::llround(std::min(std::max(t, 0.0), 1.0) * cells);
+            }
+            uint64_t m = 0;
+            for (int bit = bits - 1; bit >= 0; --bit)
+                for (int k = dim - 1; k >= 0; --k) m = (m << 1) | ((q[k] >> bit) & 1u);
+            key[i] = m;
+        }
+    });
+    std::vector<int32_t> order(nl);
+    for (int64_t i = 0; i < nl; ++i) order[i] = (int32_t)i;
+    std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key[a] != key[b] ? key[a] < key[b] : a < b; });
+    return order;
+}
+
+SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim, const double *xyz,
+                   int64_t window)
 {
     SellPlan pl;
     pl.mode = mode;
     pl.base = 1;
-    if (mode < 0 || mode > 5) throw std::runtime_error("sell_plan: bad mode");
-    if (mode == 5 && !xyz) throw std::runtime_error("sell_plan: the geometric order needs dof coordinates");
+    if (mode < 0 || mode > 7) throw std::runtime_error("sell_plan: bad mode");
+    if ((mode == 5 || mode >= 6) && !xyz) throw std::runtime_error("sell_plan: the geometric / Morton order needs dof coordinates");
     if (mode == 0 || nl == 0) return pl;
     // base order
     std::vector<int32_t> bo, bp;  // base position -> row, row -> base position (empty: identity)
     pl.bw_natural = bandwidth(nl, rowptr, cols, {});
+    if (mode >= 6) {  // Morton base order: 6 + windows, 7 + global length sort
+        bo = morton_order(nl, dim, xyz);
+        bp.resize(nl);
+        for (int64_t k = 0; k < nl; ++k) bp[bo[k]] = (int32_t)k;
+        pl.base = 4;
+        pl.bw_geometric = bandwidth(nl, rowptr, cols, bp);
+        if (mode == 7) {
+            pl.windowed = false;
+            pl.max_delta = pl.bw_geometric;
+            pl.perm = std::move(bo);
+            return pl;
+        }
+    }
     auto banded = [&](int64_t bw) { return bw <= 32767 && bw * 8 <= nl; };
     if ((mode == 3 || mode == 5) && xyz && dim >= 1 && dim <= 3 && !(mode == 3 && banded(pl.bw_natural))) {
         std::vector<int32_t> go = geometric_order(nl, dim, xyz), gp(nl);
@@ -248,9 +299,10 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
         }
     }
     bool rcm = mode == 2 || mode == 4;
+    const bool morton = mode == 6;
     // the mesh order is banded (16-bit deltas, bandwidth under nl / 8): mode 0 without the RCM pass
     if (mode == 3 && banded(pl.bw_natural)) return pl;
-    if (mode >= 2) {
+    if (mode >= 2 && !morton) {
         bo = rcm_order(nl, rowptr, cols);
         bp.resize(nl);
         for (int64_t k = 0; k < nl; ++k) bp[bo[k]] = (int32_t)k;
@@ -261,8 +313,8 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
             bp.clear();
         }
     }
-    pl.base = rcm ? 2 : 1;
-    if (mode >= 3) {  // global length sort over the base order: the space order is the base order
+    pl.base = morton ? 4 : rcm ? 2 : 1;
+    if (mode >= 3 && !morton) {  // global length sort over the base order: the space order is the base order
         pl.windowed = false;
         pl.max_delta = rcm ? pl.bw_rcm : pl.bw_natural;
         pl.perm = std::move(bo);
@@ -323,9 +375,15 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
         for (int64_t k = 0; k < nl; ++k) inv[perm[k]] = (int32_t)k;
         return bandwidth(nl, rowptr, cols, inv);
     };
-    // the largest window whose deltas fit 16 bits; 4096 with 32-bit columns when none does
+    // the largest window whose deltas fit 16 bits; 4096 with 32-bit columns when none does (a given
+    // window: that one, the slices beyond 16 bits streaming 32-bit columns)
     int64_t chosen = 0;
+    if (window > 0) {
+        chosen = window;
+        pl.max_delta = build(window);
+    }
     for (int64_t W : {32768, 16384, 8192, 4096, 2048, 1024, 512}) {
+        if (chosen) break;
         const int64_t d = build(W);
         if (d <= 32767) {
             chosen = W;
@@ -415,18 +473,30 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
             }
         }
     });
-    // column - lane base in 16 bits when every delta fits (10 instead of 12 streamed bytes/entry)
-    bool fits = true;
-    for (int64_t sl = 0; sl < ns && fits; ++sl)
+    // column - lane base in 16 bits where it fits (10 instead of 12 streamed bytes per entry).  A
+    // slice holding a delta beyond 16 bits (an unstructured mesh's far neighbours) keeps streaming
+    // its 32-bit columns and is flagged in swide; the 16-bit stream is built when at least half of
+    // the stored entries lie in slices that fit (every slice of a lattice numbering does)
+    std::vector<uint8_t> wide((size_t)ns, 0);
+    int64_t stored_wide = 0;
+    for (int64_t sl = 0; sl < ns; ++sl) {
         for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t) {
             const int64_t d = (int64_t)P.scols[t] - lane_base(sl, (t - P.sptr[sl]) % kLanes);
-            if (d < -32768 || d > 32767) { fits = false; break; }
+            if (d < -32768 || d > 32767) { wide[sl] = 1; break; }
         }
-    if (fits) {
-        P.sdel.resize(stored);
-        for (int64_t sl = 0; sl < ns; ++sl)
+        if (wide[sl]) stored_wide += P.sptr[sl + 1] - P.sptr[sl];
+    }
+    if (2 * stored_wide <= stored) {
+        P.sdel.assign(stored, 0);
+        for (int64_t sl = 0; sl < ns; ++sl) {
+            if (wide[sl]) {
+                for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t) P.nnz_wide += P.smap[t] >= 0;
+                continue;
+            }
             for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t)
                 P.sdel[t] = (int16_t)(P.scols[t] - lane_base(sl, (t - P.sptr[sl]) % kLanes));
+        }
+        if (stored_wide) P.swide = std::move(wide);
     }
 }
 

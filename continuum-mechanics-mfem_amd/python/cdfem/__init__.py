@@ -354,7 +354,8 @@ def partition_rcb(mesh: Mesh, nranks) -> np.ndarray:
     return part
 
 
-SELL_ORDER = {"legacy": 0, "natural": 1, "rcm": 2, "auto": 3, "rcm_global": 4, "geometric": 5}
+SELL_ORDER = {"legacy": 0, "natural": 1, "rcm": 2, "auto": 3, "rcm_global": 4, "geometric": 5, "morton": 6,
+              "morton_global": 7}
 
 
 def sell_plan(rowptr, cols, mode="auto", xyz=None):

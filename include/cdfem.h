@@ -244,11 +244,16 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).
- * "spmv_index16": 1 (default) — the assembled-operator SpMV streams 16-bit column deltas when
- *                 every |column - row| < 2^15; 0 = 32-bit columns.
- * "sell_order": 0..5, default 3 (auto) — the FA SpMV's order, read when the pattern is built
- *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan).  A permuted order runs the
- *               Krylov solve in that order (Mult to rounding, iterates to 1e-12).
+ * "spmv_index16": 1 (default) — the assembled-operator SpMV streams 16-bit column deltas
+ *                 (column - lane row); a 64-row slice with a delta beyond 2^15 streams its 32-bit
+ *                 columns instead (mixed layout, when at least half the entries fit); 0 = 32-bit
+ *                 columns everywhere.
+ * "sell_order": 0..7, default 3 (auto) — the FA SpMV's order, read when the pattern is built
+ *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan): 0 natural, 1 natural +
+ *               windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton.
+ *               A permuted order runs the Krylov solve in that order (Mult to rounding, iterates to
+ *               1e-12).
+ * "sell_window": 0 (default, auto) or a multiple of 64 — rows per window of the windowed orders.
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
  * "gm_ept": 0 (default, auto) — entries per thread of the GMRES orthogonalisation passes (4, 5, 6
  *           or 8); auto takes the smallest whose grid is resident in one round (same results).

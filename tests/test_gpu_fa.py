@@ -252,6 +252,38 @@ def test_fa_c4_full_size_properties(gpu_ctx):
     assert info["final_norm"] <= 1e-3 * info["initial_norm"]
 
 
+def test_fa_spmv_mixed_columns_bitwise():
+    """Mixed SELL columns: slices whose rows reach a column beyond 16 bits of their own row (an
+    unstructured mesh's far neighbours) stream 32-bit columns, the rest 16-bit deltas.  A Kuhn P2
+    numbering with 3 far-apart dof pairs swapped (69 K dofs, natural SpMV order) makes a few slices
+    wide: Mult, the constrained Mult and 40 GMRES iterates are bitwise the all-32-bit ones, and the
+    SpMV's byte count lies strictly between the all-16-bit and all-32-bit counts."""
+    gm = cdfem.kuhn_mesh(3, 20, 2, perturb=0.05)
+    rng = np.random.default_rng(12)
+    lab = np.arange(gm.nl, dtype=np.int32)
+    for _ in range(3):
+        i = int(rng.integers(0, gm.nl // 4))
+        j = int(rng.integers(3 * gm.nl // 4, gm.nl))
+        lab[i], lab[j] = lab[j], lab[i]
+    m = cdfem.Mesh(gm.dim, gm.order, gm.verts, lab[gm.dofmap], gm.nl, np.sort(lab[gm.ess]), None, simplex=True)
+    x = rng.uniform(-1, 1, m.nl)
+    b = rng.uniform(-1, 1, m.nl)
+    res = {}
+    for idx16 in (1, 0):
+        with cdfem.Context(0) as ctx:
+            ctx.set_option("sell_order", 0)          # natural order: the swapped labels stay far
+            ctx.set_option("spmv_index16", idx16)
+            ctx.upload_mesh(m)
+            ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+            X, _ = ctx.solve(B, method="gmres", restart=30, rel_tol=0.0, abs_tol=0.0, max_iter=40)
+            nnz = len(ctx.fa_csr()[1])
+            res[idx16] = (ctx.mult(x), ctx.mult(x, constrained=True), X, ctx.kernel_bytes(cdfem.K_APPLY))
+    for a, c in zip(res[1][:3], res[0][:3]):
+        np.testing.assert_array_equal(a, c)
+    assert res[0][3] - 2.0 * nnz < res[1][3] < res[0][3]
+
+
 def test_fa_spmv_index16_matches_int32(gpu_ctx):
     """The SpMV's 16-bit column deltas (set_option "spmv_index16", the default) give the same bits
     as 32-bit columns, for Mult, the constrained Mult and a CG solve.  A random DoF numbering
@@ -276,7 +308,7 @@ def test_fa_spmv_index16_matches_int32(gpu_ctx):
             np.testing.assert_array_equal(a, c)
         nnz = len(gpu_ctx.fa_csr()[1])
         assert res[0][3] - res[1][3] == 2.0 * nnz       # 10 instead of 12 bytes per entry
-        # random numbering: deltas overflow 16 bits, the 32-bit path runs even with the option on
+        # random numbering
         gpu_ctx.set_option("spmv_index16", 1)
         perm = rng.permutation(gm.nl).astype(np.int32)
         xyzp = np.empty_like(gm.dof_xyz)
@@ -286,13 +318,18 @@ def test_fa_spmv_index16_matches_int32(gpu_ctx):
         xp = np.empty_like(x)
         xp[perm] = x
         y = res[1][0]
-        # natural base order: the shuffled bandwidth overflows 16 bits -> 32-bit columns;
-        # auto (default): the reverse Cuthill-McKee base order brings the deltas back into 16 bits
-        for order, nbytes in ((1, res[0][3]), (3, res[1][3])):
+        # natural base order: the shuffled numbering puts some columns beyond 16 bits of their row ->
+        # those slices stream 32-bit columns (mixed layout: between the two byte counts); auto
+        # (default): the reverse Cuthill-McKee base order brings every delta back into 16 bits
+        for order in (1, 3):
             gpu_ctx.set_option("sell_order", order)
             gpu_ctx.upload_mesh(gp)
             gpu_ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
-            assert gpu_ctx.kernel_bytes(cdfem.K_APPLY) == nbytes
+            nb = gpu_ctx.kernel_bytes(cdfem.K_APPLY)
+            if order == 1:
+                assert res[1][3] < nb < res[0][3]
+            else:
+                assert nb == res[1][3]
             yp = gpu_ctx.mult(xp)
             assert np.abs(yp[perm] - y).max() <= 1e-13 * np.abs(y).max()
     finally:

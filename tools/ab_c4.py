@@ -26,11 +26,15 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=60)
 ap.add_argument("--n", type=int, default=55)
+ap.add_argument("--points", type=int, default=170000, help="delaunay: random points (cdfem.delaunay_cube)")
 ap.add_argument("--variants", default="legacy:natural:sell_order=0+spmv_xcd=0,auto:natural:sell_order=3,"
                                       "shuf_legacy:shuffled:sell_order=0+spmv_xcd=0,shuf_auto:shuffled:sell_order=3")
 args = ap.parse_args()
 
 base = cdfem.kuhn_mesh(3, args.n, 2, with_coords=False)
+delaunay = None
+if "delaunay" in args.variants:
+    delaunay = cdfem.simplex_space(*cdfem.delaunay_cube(args.points, seed=20261017), 2)
 g = np.random.default_rng(7).permutation(base.nl).astype(np.int32)   # shuffled label of mesh dof i
 shuffled = cdfem.Mesh(base.dim, base.order, base.verts, g[base.dofmap], base.nl, np.sort(g[base.ess]),
                       None, simplex=True)
@@ -41,7 +45,7 @@ b_shuf[g] = b_nat
 variants = []
 for spec in args.variants.split(","):
     label, mesh, opts = spec.split(":")
-    m = base if mesh == "natural" else shuffled
+    m = {"natural": base, "shuffled": shuffled, "delaunay": delaunay}[mesh]
     ctx = cdfem.Context(0)
     for kv in filter(None, opts.split("+")):
         k, val = kv.split("=")
@@ -50,13 +54,14 @@ for spec in args.variants.split(","):
     ctx.upload_mesh(m)
     ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=(1.0, -2.0, 0.5), mass=1.0)
     setup_s = time.perf_counter() - t0
-    b = b_nat if mesh == "natural" else b_shuf
+    b = b_shuf if mesh == "shuffled" else b_nat if mesh == "natural" else \
+        np.random.default_rng(20261015).uniform(-1, 1, m.nl)
     _, B = ctx.form_linear_system(np.zeros(m.nl), b)
     variants.append(dict(label=label, mesh=mesh, ctx=ctx, dB=ctx.to_device(B), dX=ctx.alloc(8 * m.nl),
                          spmv_us=[], orth_us=[], solve_ms=[], setup_s=setup_s))
     print(f"# {label}: setup {setup_s:.2f} s", flush=True)
 
-ref = None
+refs = {}
 for rnd in range(args.rounds + 1):
     for v in variants:
         ctx = v["ctx"]
@@ -71,11 +76,14 @@ for rnd in range(args.rounds + 1):
         a = ctx.profile_read(cdfem.K_APPLY)
         o = ctx.profile_read(cdfem.K_ORTH)
         ctx.profile(False)
-        x = ctx.from_device(v["dX"], base.nl)
+        nl_v = delaunay.nl if v["mesh"] == "delaunay" else base.nl
+        x = ctx.from_device(v["dX"], nl_v)
         if v["mesh"] == "shuffled":
             x = x[g]                          # back to the natural labels
-        if ref is None:
-            ref = x
+        key = "delaunay" if v["mesh"] == "delaunay" else "kuhn"
+        if key not in refs:
+            refs[key] = x
+        ref = refs[key]
         err = float(np.abs(x - ref).max() / np.abs(ref).max())
         assert err <= 1e-9, (v["label"], err)
         if rnd == 0:
