@@ -100,6 +100,11 @@ void free_mesh(cdfem_ctx *c)
     c->d_sdel = nullptr;
     c->d_swide = nullptr;
     c->sell_nnz_wide = 0;
+    dfree(c->d_hptr); dfree(c->d_hidx); dfree(c->d_sloc);
+    c->d_hptr = c->d_hidx = nullptr;
+    c->d_sloc = nullptr;
+    c->lds_rows = 0;
+    c->lds_max = 0;
     dfree(c->d_rperm); dfree(c->d_pv[0]); dfree(c->d_pv[1]); dfree(c->d_dinv_p);
     c->d_rperm = nullptr; c->d_pv[0] = c->d_pv[1] = nullptr; c->d_dinv_p = nullptr;
     dfree(c->d_svals_c);
@@ -1265,7 +1270,7 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
                 xyz = simplex_dof_coords(c->dim, c->p, c->ne, c->nd, c->nl, c->h_verts, c->h_dofs);
             FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl,
                                            multi_rank(c) ? 0 : c->sell_mode, c->dim,
-                                           xyz.empty() ? nullptr : xyz.data(), c->sell_window);
+                                           xyz.empty() ? nullptr : xyz.data(), c->sell_window, c->spmv_lds);
             c->nnz = P.nnz;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
             c->d_cols = dalloc<int32_t>(P.cols.size());
@@ -1303,6 +1308,17 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
             if (!P.sdel.empty()) {
                 c->d_sdel = dalloc<int16_t>(P.sdel.size());
                 HIPCHK(hipMemcpyAsync(c->d_sdel, P.sdel.data(), P.sdel.size() * 2, hipMemcpyHostToDevice, c->stream));
+            }
+            if (P.lds_rows > 0) {  // LDS-staged windows (sell_plan.cpp)
+                c->d_hptr = dalloc<int32_t>(P.hptr.size());
+                c->d_hidx = dalloc<int32_t>(std::max<size_t>(P.hidx.size(), 1));
+                c->d_sloc = dalloc<uint16_t>(P.sloc.size());
+                HIPCHK(hipMemcpyAsync(c->d_hptr, P.hptr.data(), P.hptr.size() * 4, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(hipMemcpyAsync(c->d_hidx, P.hidx.data(), P.hidx.size() * 4, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(hipMemcpyAsync(c->d_sloc, P.sloc.data(), P.sloc.size() * 2, hipMemcpyHostToDevice, c->stream));
+                c->lds_rows = P.lds_rows;
+                c->lds_max = P.lds_max;
+                c->lds_halo = (int64_t)P.hidx.size();
             }
             if (!P.swide.empty()) {  // mixed layout: the slices beyond 16 bits stream d_scols
                 c->d_swide = dalloc<uint8_t>(P.swide.size());
@@ -1558,6 +1574,10 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 7)
                 throw ArgError("sell_order must be 0..7 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton)");
             c->sell_mode = value;
+        } else if (k == "spmv_lds") {  // read when the FA pattern is built (once per mesh)
+            if (value < 0 || value % 64 != 0 || value > 65536)
+                throw ArgError("spmv_lds must be 0 (off) or rows per window, a multiple of 64 up to 65536");
+            c->spmv_lds = value;
         } else if (k == "sell_window") {  // read when the FA pattern is built (once per mesh)
             if (value < 0 || (value > 0 && (value % 64 != 0 || value > (1 << 20))))
                 throw ArgError("sell_window must be 0 (auto) or a multiple of 64 up to 2^20");
@@ -1620,8 +1640,13 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
         if (c->fa_ready) {  // CSR SpMV: values + columns + row pointers + x + y
             if (k != CDFEM_K_APPLY) throw ArgError("FA operators report the SpMV (CDFEM_K_APPLY) only");
             // (SELL adds < 1 % padding; 16-bit column deltas when the bandwidth fits)
-            // 8 B value + 2 B delta per entry (4 B column in the 32-bit slices of a mixed layout)
-            *bytes = spmv_delta(c) ? 10.0 * (double)c->nnz + 2.0 * (double)c->sell_nnz_wide + 4.0 * (nl + 1) + 16.0 * nl +
+            // 8 B value + 2 B delta per entry (4 B column in the 32-bit slices of a mixed layout); LDS
+            // windows: 8 B value + 2 B window position per entry, 4 B per staged column (the x values
+            // themselves: 8 B per row, each window's halo beyond its own rows from L2)
+            if (c->lds_rows > 0)
+                *bytes = 10.0 * (double)c->nnz + 4.0 * (double)c->lds_halo + 4.0 * (double)(c->nslices + 1) +
+                         16.0 * nl;
+            else *bytes = spmv_delta(c) ? 10.0 * (double)c->nnz + 2.0 * (double)c->sell_nnz_wide + 4.0 * (nl + 1) + 16.0 * nl +
                                          (c->d_swide ? (double)c->nslices : 0.0)
                                    : 12.0 * (double)c->nnz + 4.0 * (nl + 1) + 16.0 * nl;
             return CDFEM_OK;

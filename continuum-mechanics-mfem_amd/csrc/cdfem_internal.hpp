@@ -217,6 +217,12 @@ struct cdfem_ctx {
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
     int sell_window = 0;                // set_option "sell_window": rows per window of a windowed order (0 auto)
+    int spmv_lds = 0;                   // set_option "spmv_lds": rows per LDS-staged SpMV window (0 off)
+    int32_t *d_hptr = nullptr, *d_hidx = nullptr;  // LDS-staged windows (FaPattern::hptr / hidx / sloc)
+    uint16_t *d_sloc = nullptr;
+    int64_t lds_rows = 0;               // rows per window of the current LDS layout (0: none)
+    int32_t lds_max = 0;                // largest window halo (doubles)
+    int64_t lds_halo = 0;               // staged columns over all windows
     int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD (windowed layout)
     int32_t *d_rperm = nullptr;         // SpMV space order: space row -> mesh row (null: mesh order)
     bool sell_windowed = false;         // slices cut from the space order (kernel row = slice * 64 + lane)
@@ -358,6 +364,7 @@ hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *d
 // ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
 // full assembly on simplices (fa_kernels.hip)
 constexpr int kSpmvMaxBlocks = 65536;  // partial slots reserved for the SpMV-CG den
+constexpr int kLdsHaloMax = 7936;      // doubles of x one LDS-staged SpMV window may stage (62 KiB)
 struct FaPattern {
     int64_t nnz = 0;
     std::vector<int32_t> rowptr, cols, diagpos, coff, cpos;
@@ -370,6 +377,13 @@ struct FaPattern {
     std::vector<uint8_t> swide;  // [nslices] 1: this slice has a delta beyond 16 bits and streams scols
                                  // (empty: every slice fits); nnz_wide = real entries in such slices
     int64_t nnz_wide = 0;
+    // LDS-staged windows (windowed layouts, sell_build with lds_rows > 0): window w = slices
+    // [w S, (w + 1) S), S = lds_rows / 64; its distinct columns hidx[hptr[w] .. hptr[w + 1]) (ascending)
+    // are staged in LDS and every stored entry addresses them by sloc (16-bit position in the window)
+    int64_t lds_rows = 0;
+    int32_t lds_max = 0;          // largest window halo (doubles of LDS)
+    std::vector<int32_t> hptr, hidx;
+    std::vector<uint16_t> sloc;
     std::vector<int32_t> perm;   // SpMV space order (sell_plan.cpp): space row -> mesh row; empty = mesh order
     bool windowed = false;       // slices cut from the space order directly (no srows)
 };
@@ -380,6 +394,7 @@ struct SellPlan {
     bool windowed = false;
     int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0, bw_geometric = 0;
     std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
+    int64_t lds_rows = 0;        // windowed: rows per LDS-staged window (set_option "spmv_lds"; 0 off)
 };
 std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
 SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim = 0,
@@ -389,7 +404,8 @@ std::vector<double> simplex_dof_coords(int dim, int p, int ne, int nd, int64_t n
                                        const std::vector<int32_t> &dofs);
 void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl);
 FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl, int sell_mode,
-                           int dim = 0, const double *dof_xyz = nullptr, int64_t sell_window = 0);
+                           int dim = 0, const double *dof_xyz = nullptr, int64_t sell_window = 0,
+                           int64_t lds_rows = 0);
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq, double kappa, double alpha,
                                const double *conv, const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);

@@ -49,7 +49,7 @@ static inline int64_t ee_index(int e, int i, int j, int nd)
 }
 
 FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int64_t nl, int sell_mode, int dim,
-                           const double *dof_xyz, int64_t sell_window)
+                           const double *dof_xyz, int64_t sell_window, int64_t lds_rows)
 {
     // dof -> incidences (e * nd + l), ascending
     std::vector<int64_t> cnt(nl + 1, 0);
@@ -133,6 +133,7 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     // SpMV layout: SELL-64 over the rows in the plan's order (sell_plan.cpp)
     P.rowptr = std::move(rowptr);
     SellPlan pl = sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode, dim, dof_xyz, sell_window);
+    pl.lds_rows = pl.windowed ? lds_rows : 0;
     sell_build(P, nl, pl);
     return P;
 }
@@ -487,6 +488,59 @@ k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows,
     if (CG) store_partial(block_sum(dd, sh), part);
 }
 
+// LDS-staged windows (windowed layouts, sell_plan.cpp): workgroup = one window of S slices.  The
+// window's distinct columns (hidx, ascending) are loaded into LDS once, then every entry reads its x
+// value from LDS through its 16-bit window position (sloc): no divergent global gathers, and x leaves
+// HBM / L2 once per window.  Each row sums its entries in the stored order (bitwise the windowed
+// layout's sums).  Windows run in XCD-contiguous ranges (xcd_per > 0), so neighbouring windows, whose
+// halos overlap, share an L2.  CG mode: partials of (x, y) and early exit once the Krylov state is done.
+template <bool CG>
+__global__ void __launch_bounds__(256)
+k_sell_spmv_lds(const int32_t *__restrict__ sptr, const uint16_t *__restrict__ sloc, const double *__restrict__ svals,
+                const int32_t *__restrict__ hptr, const int32_t *__restrict__ hidx, const double *__restrict__ x,
+                double *__restrict__ y, int64_t nslices, int64_t n, int spw, int nwin, int xcd_per,
+                double *__restrict__ part, const KrylovState *__restrict__ st)
+{
+    extern __shared__ double xs[];
+    __shared__ double sh[256 / 64];
+    if (CG && st->done) return;
+    const int w = xcd_per > 0 ? (int)((blockIdx.x & 7) * xcd_per + (blockIdx.x >> 3)) : (int)blockIdx.x;
+    double dd = 0.0;
+    if (w < nwin) {
+        const int h0 = hptr[w], H = hptr[w + 1] - h0;
+        for (int i = threadIdx.x; i < H; i += 256) xs[i] = x[hidx[h0 + i]];
+        __syncthreads();
+        const int lane = threadIdx.x & 63;
+        for (int s = threadIdx.x >> 6; s < spw; s += 4) {
+            const int64_t sl = (int64_t)w * spw + s;
+            if (sl >= nslices) break;
+            const int32_t b = sptr[sl], len = (sptr[sl + 1] - b) >> 6;
+            const double *v = svals + b + lane;
+            const uint16_t *ci = sloc + b + lane;
+            double a0 = 0.0;
+            int j = 0;
+            for (; j + 4 <= len; j += 4) {
+                double vv[4];
+                uint16_t cc[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    vv[k] = __builtin_nontemporal_load(v + (j + k) * 64);
+                    cc[k] = __builtin_nontemporal_load(ci + (j + k) * 64);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) a0 = fma(vv[k], xs[cc[k]], a0);
+            }
+            for (; j < len; ++j) a0 = fma(__builtin_nontemporal_load(v + j * 64), xs[__builtin_nontemporal_load(ci + j * 64)], a0);
+            const int64_t row = sl * 64 + lane;
+            if (row < n) {
+                y[row] = a0;
+                if (CG) dd += a0 * x[row];
+            }
+        }
+    }
+    if (CG) store_partial(block_sum(dd, sh), part);
+}
+
 // permuted layout: xp[i] = x[perm[i]] into the SpMV order, y[perm[i]] = yp[i] back to mesh order
 __global__ void __launch_bounds__(256)
 k_perm_gather(const int32_t *__restrict__ perm, const double *__restrict__ x, double *__restrict__ xp, int64_t n)
@@ -572,15 +626,33 @@ static int sell_xcd_per(const cdfem_ctx *c)
 }
 unsigned sell_grid(const cdfem_ctx *c)
 {
+    if (c->lds_rows > 0) {
+        const int64_t spw = c->lds_rows / 64, nwin = (c->nslices + spw - 1) / spw;
+        return c->spmv_xcd ? 8u * (unsigned)((nwin + 7) / 8) : (unsigned)nwin;
+    }
     return sell_xcd_per(c) ? 8u * (unsigned)sell_xcd_per(c) : sell_blocks(c);
 }
 
 bool spmv_delta(const cdfem_ctx *c) { return c->d_sdel && c->spmv_index16; }
 
+static int lds_windows(const cdfem_ctx *c)
+{
+    const int64_t spw = c->lds_rows / 64;
+    return (int)((c->nslices + spw - 1) / spw);
+}
+
 template <bool CG>
 static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, double *y, double *part,
                         const KrylovState *st)
 {
+    if (c->lds_rows > 0) {
+        const int nwin = lds_windows(c), per = c->spmv_xcd ? (nwin + 7) / 8 : 0;
+        const dim3 g(per ? 8u * (unsigned)per : (unsigned)nwin), b(256);
+        CDFEM_LAUNCH(c, (k_sell_spmv_lds<CG>), g, b, (size_t)c->lds_max * sizeof(double), c->d_sptr, c->d_sloc, vals,
+                     c->d_hptr, c->d_hidx, x, y, c->nslices, (int64_t)c->nl, (int)(c->lds_rows / 64), nwin, per, part,
+                     st);
+        return;
+    }
     const dim3 g(sell_grid(c)), b(256);
     const int per = sell_xcd_per(c);
     const bool perm = c->sell_windowed;

@@ -498,6 +498,46 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
         }
         if (stored_wide) P.swide = std::move(wide);
     }
+    // LDS-staged windows: every window of S consecutive slices stages its distinct columns, ascending
+    // (the x values it reads), and the entries address them by 16-bit window positions.  Windows
+    // halve (down to one slice) until every halo fits kLdsHaloMax doubles.
+    if (pl.lds_rows > 0 && permuted) {
+        int64_t S = std::max<int64_t>(1, pl.lds_rows / kLanes);
+        for (;; S = std::max<int64_t>(1, S / 2)) {
+            const int64_t nw = (ns + S - 1) / S;
+            std::vector<std::vector<int32_t>> halo((size_t)nw);
+            std::vector<int32_t> hmax(16, 0);
+            par_for(nw, [&](int64_t w0, int64_t w1) {
+                for (int64_t w = w0; w < w1; ++w) {
+                    auto &h = halo[(size_t)w];
+                    const int64_t s0 = w * S, s1 = std::min(ns, s0 + S);
+                    h.assign(P.scols.begin() + P.sptr[s0], P.scols.begin() + P.sptr[s1]);
+                    std::sort(h.begin(), h.end());
+                    h.erase(std::unique(h.begin(), h.end()), h.end());
+                }
+            });
+            int64_t big = 0;
+            for (auto &h : halo) big = std::max<int64_t>(big, (int64_t)h.size());
+            if (big > kLdsHaloMax && S > 1) continue;
+            if (big > kLdsHaloMax) break;  // one slice does not fit: no LDS layout
+            P.lds_rows = S * kLanes;
+            P.lds_max = (int32_t)big;
+            P.hptr.assign((size_t)nw + 1, 0);
+            for (int64_t w = 0; w < nw; ++w) P.hptr[w + 1] = P.hptr[w] + (int32_t)halo[(size_t)w].size();
+            P.hidx.resize((size_t)P.hptr[nw]);
+            P.sloc.resize((size_t)stored);
+            par_for(nw, [&](int64_t w0, int64_t w1) {
+                for (int64_t w = w0; w < w1; ++w) {
+                    const auto &h = halo[(size_t)w];
+                    std::copy(h.begin(), h.end(), P.hidx.begin() + P.hptr[w]);
+                    const int64_t s0 = w * S, s1 = std::min(ns, s0 + S);
+                    for (int32_t t = P.sptr[s0]; t < P.sptr[s1]; ++t)
+                        P.sloc[t] = (uint16_t)(std::lower_bound(h.begin(), h.end(), P.scols[t]) - h.begin());
+                }
+            });
+            break;
+        }
+    }
 }
 
 }  // namespace cdfem

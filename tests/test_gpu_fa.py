@@ -284,6 +284,41 @@ def test_fa_spmv_mixed_columns_bitwise():
     assert res[0][3] - 2.0 * nnz < res[1][3] < res[0][3]
 
 
+@pytest.mark.parametrize("mesh,order", [("kuhn", 1), ("delaunay", 2), ("delaunay", 6)])
+def test_fa_spmv_lds_windows_bitwise(mesh, order):
+    """LDS-staged SpMV windows (set_option "spmv_lds": each workgroup stages its window's distinct
+    columns in LDS and the entries read x there through 16-bit window positions) give the windowed
+    layout's row sums bit for bit: Mult, the constrained Mult and 40 GMRES iterates are bitwise those
+    of the same windowed layout without LDS, on the Kuhn lattice (natural windows) and on an
+    unstructured Delaunay mesh (RCM and Morton windows), at two window sizes.  The FA CG's den sums
+    its per-workgroup partials, whose grouping follows the launch, so its 30 iterates agree to 1e-12."""
+    if mesh == "kuhn":
+        m = cdfem.kuhn_mesh(3, 14, 2, perturb=0.1)
+    else:
+        m = cdfem.simplex_space(*cdfem.delaunay_cube(6000, seed=4), 2)
+    rng = np.random.default_rng(17)
+    x = rng.uniform(-1, 1, m.nl)
+    b = rng.uniform(-1, 1, m.nl)
+    for win in (512, 1024):
+        res = {}
+        for lds in (0, win):
+            with cdfem.Context(0) as ctx:
+                ctx.set_option("sell_order", order)
+                ctx.set_option("sell_window", win)
+                ctx.set_option("spmv_lds", lds)
+                ctx.upload_mesh(m)
+                ctx.fa_setup(kinds=5, kappa=0.1, mass=1.0)
+                _, Bs = ctx.form_linear_system(np.zeros(m.nl), b)
+                Xc, _ = ctx.solve(Bs, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=30)
+                ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+                _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+                X, _ = ctx.solve(B, method="gmres", restart=30, rel_tol=0.0, abs_tol=0.0, max_iter=40)
+                res[lds] = (ctx.mult(x), ctx.mult(x, constrained=True), X, Xc)
+        for k, name in enumerate(("mult", "constrained mult", "gmres")):
+            np.testing.assert_array_equal(res[0][k], res[win][k], err_msg=name)
+        assert np.linalg.norm(res[win][3] - res[0][3]) <= 1e-12 * np.linalg.norm(res[0][3])
+
+
 def test_fa_spmv_index16_matches_int32(gpu_ctx):
     """The SpMV's 16-bit column deltas (set_option "spmv_index16", the default) give the same bits
     as 32-bit columns, for Mult, the constrained Mult and a CG solve.  A random DoF numbering
