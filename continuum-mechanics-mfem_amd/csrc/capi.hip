@@ -1575,8 +1575,8 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
                 throw ArgError("sell_order must be 0..7 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton)");
             c->sell_mode = value;
         } else if (k == "spmv_lds") {  // read when the FA pattern is built (once per mesh)
-            if (value < 0 || value % 64 != 0 || value > 65536)
-                throw ArgError("spmv_lds must be 0 (off) or rows per window, a multiple of 64 up to 65536");
+            if (value < -1 || (value > 0 && (value % 64 != 0 || value > 65536)))
+                throw ArgError("spmv_lds must be -1 (auto), 0 (off) or rows per window, a multiple of 64 up to 65536");
             c->spmv_lds = value;
         } else if (k == "sell_window") {  // read when the FA pattern is built (once per mesh)
             if (value < 0 || (value > 0 && (value % 64 != 0 || value > (1 << 20))))

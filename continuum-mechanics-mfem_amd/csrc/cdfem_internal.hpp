@@ -217,7 +217,7 @@ struct cdfem_ctx {
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
     int sell_window = 0;                // set_option "sell_window": rows per window of a windowed order (0 auto)
-    int spmv_lds = 0;                   // set_option "spmv_lds": rows per LDS-staged SpMV window (0 off)
+    int spmv_lds = -1;                  // set_option "spmv_lds": rows per LDS-staged SpMV window (0 off, -1 auto)
     int32_t *d_hptr = nullptr, *d_hidx = nullptr;  // LDS-staged windows (FaPattern::hptr / hidx / sloc)
     uint16_t *d_sloc = nullptr;
     int64_t lds_rows = 0;               // rows per window of the current LDS layout (0: none)
@@ -395,7 +395,9 @@ struct SellPlan {
     int64_t window = 0, max_delta = 0, bw_natural = 0, bw_rcm = 0, bw_geometric = 0;
     std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
     int64_t lds_rows = 0;        // windowed: rows per LDS-staged window (set_option "spmv_lds"; 0 off)
+    bool auto_lds = false;       // the auto mode chose a windowed unstructured order: LDS windows
 };
+constexpr int64_t kAutoLdsRows = 512;  // rows per window of the auto unstructured orders
 std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
 SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim = 0,
                    const double *xyz = nullptr, int64_t window = 0);

@@ -133,7 +133,9 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     // SpMV layout: SELL-64 over the rows in the plan's order (sell_plan.cpp)
     P.rowptr = std::move(rowptr);
     SellPlan pl = sell_plan(nl, P.rowptr.data(), P.cols.data(), sell_mode, dim, dof_xyz, sell_window);
-    pl.lds_rows = pl.windowed ? lds_rows : 0;
+    // spmv_lds: > 0 rows per window; -1 (auto): the plan's window when the auto mode chose an
+    // unstructured windowed order
+    pl.lds_rows = !pl.windowed ? 0 : lds_rows > 0 ? lds_rows : (lds_rows < 0 && pl.auto_lds) ? pl.window : 0;
     sell_build(P, nl, pl);
     return P;
 }

@@ -24,8 +24,9 @@
 //             2 = RCM + windows, 3 = auto (mode 0 when the mesh order is banded: 16-bit deltas and
 //             bandwidth under nl / 8; else the geometric order when coordinates are given and it
 //             is banded that way; else RCM + global when its bandwidth is under half the natural
-//             one), 4 = RCM + global, 5 = geometric + global, 6 = Morton + windows, 7 = Morton +
-//             global (morton_order).
+//             one; when no order is banded — an unstructured mesh — Morton windows with coordinates,
+//             else RCM windows, both LDS-staged, spmv_lds auto), 4 = RCM + global, 5 = geometric +
+//             global, 6 = Morton + windows, 7 = Morton + global (morton_order).
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -272,19 +273,6 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
     // base order
     std::vector<int32_t> bo, bp;  // base position -> row, row -> base position (empty: identity)
     pl.bw_natural = bandwidth(nl, rowptr, cols, {});
-    if (mode >= 6) {  // Morton base order: 6 + windows, 7 + global length sort
-        bo = morton_order(nl, dim, xyz);
-        bp.resize(nl);
-        for (int64_t k = 0; k < nl; ++k) bp[bo[k]] = (int32_t)k;
-        pl.base = 4;
-        pl.bw_geometric = bandwidth(nl, rowptr, cols, bp);
-        if (mode == 7) {
-            pl.windowed = false;
-            pl.max_delta = pl.bw_geometric;
-            pl.perm = std::move(bo);
-            return pl;
-        }
-    }
     auto banded = [&](int64_t bw) { return bw <= 32767 && bw * 8 <= nl; };
     if ((mode == 3 || mode == 5) && xyz && dim >= 1 && dim <= 3 && !(mode == 3 && banded(pl.bw_natural))) {
         std::vector<int32_t> go = geometric_order(nl, dim, xyz), gp(nl);
@@ -295,6 +283,23 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
             pl.windowed = false;
             pl.max_delta = pl.bw_geometric;
             pl.perm = std::move(go);
+            return pl;
+        }
+        // an unstructured mesh (no banded order exists): Morton windows, staged in LDS
+        mode = 6;
+        pl.auto_lds = true;
+        if (window <= 0) window = kAutoLdsRows;
+    }
+    if (mode >= 6) {  // Morton base order: 6 + windows, 7 + global length sort (auto: an unstructured mesh)
+        bo = morton_order(nl, dim, xyz);
+        bp.resize(nl);
+        for (int64_t k = 0; k < nl; ++k) bp[bo[k]] = (int32_t)k;
+        pl.base = 4;
+        pl.bw_geometric = bandwidth(nl, rowptr, cols, bp);
+        if (mode == 7) {
+            pl.windowed = false;
+            pl.max_delta = pl.bw_geometric;
+            pl.perm = std::move(bo);
             return pl;
         }
     }
@@ -308,6 +313,12 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
         for (int64_t k = 0; k < nl; ++k) bp[bo[k]] = (int32_t)k;
         pl.bw_rcm = bandwidth(nl, rowptr, cols, bp);
         if (mode == 3) rcm = 2 * pl.bw_rcm < pl.bw_natural;
+        if (mode == 3 && rcm && !banded(pl.bw_rcm)) {
+            // no coordinates and no banded order: RCM windows, staged in LDS
+            mode = 2;
+            pl.auto_lds = true;
+            if (window <= 0) window = kAutoLdsRows;
+        }
         if (!rcm) {
             bo.clear();
             bp.clear();

@@ -361,7 +361,7 @@ SELL_ORDER = {"legacy": 0, "natural": 1, "rcm": 2, "auto": 3, "rcm_global": 4, "
 def sell_plan(rowptr, cols, mode="auto", xyz=None):
     """Order of the FA SpMV (host only; sell_plan.cpp): returns (perm, info) with perm[space row] =
     mesh row and info = {base (1 natural, 2 RCM, 3 geometric), window (0: global length sort),
-    max_delta, bw_natural, bw_rcm, padding, bw_geometric}; xyz = (nl, dim) dof coordinates or None."""
+    max_delta, bw_natural, bw_rcm, padding, bw_geometric} (base 4: Morton); xyz = (nl, dim) dof coordinates or None."""
     rp, cl = _i32(rowptr), _i32(cols)
     nl = len(rp) - 1
     perm = np.zeros(nl, dtype=np.int32)

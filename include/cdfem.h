@@ -254,6 +254,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               A permuted order runs the Krylov solve in that order (Mult to rounding, iterates to
  *               1e-12).
  * "sell_window": 0 (default, auto) or a multiple of 64 — rows per window of the windowed orders.
+ * "spmv_lds": -1 (default, auto), 0 or rows per window — LDS-staged SpMV windows for the windowed
+ *             orders: each workgroup stages its window's distinct columns in LDS and the entries
+ *             address them by 16-bit window positions (bitwise the windowed sums); auto = on for the
+ *             unstructured orders sell_order 3 picks (Morton / RCM windows of 512 rows).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
  * "gm_ept": 0 (default, auto) — entries per thread of the GMRES orthogonalisation passes (4, 5, 6
  *           or 8); auto takes the smallest whose grid is resident in one round (same results).
