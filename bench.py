@@ -399,7 +399,8 @@ def main_c4(args):
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(bytes_ / per / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(bytes_ / per / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "k_sell_spmv (SELL-64 SpMV on the eliminated FA matrix)",
+                    "kernel": (f"{ctx.kernel_name(cdfem.K_APPLY)} (SELL-64 SpMV on the eliminated FA matrix"
+                               f"{', LDS-staged windows' if ctx.kernel_name(cdfem.K_APPLY).endswith('_lds') else ''})"),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2), "launches": cnt,
                     "other_kernels_avg_us": {"gmres_orth": round(o_ms / max(o_cnt, 1) * 1e3, 2)}}
     rp, _, _ = ctx.fa_csr()

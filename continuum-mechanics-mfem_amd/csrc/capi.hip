@@ -1631,6 +1631,20 @@ int cdfem_profile_read(cdfem_ctx *c, int k, double *total_ms, int64_t *count)
     });
 }
 
+// name of the HIP kernel that kernel id runs as in the current configuration (rocprof's kernel
+// name without its template arguments); the assembled-operator apply only (the PA applies are named
+// by the bench from their path)
+int cdfem_kernel_name(cdfem_ctx *c, int k, char *buf, size_t n)
+{
+    return guarded(c, [&] {
+        require_pa(c);
+        if (!buf || n == 0) throw ArgError("buffer is null");
+        if (k != CDFEM_K_APPLY || !c->fa_ready) throw UnsupportedError("kernel names: the assembled-operator apply only");
+        std::snprintf(buf, n, "%s", c->lds_rows > 0 ? "k_sell_spmv_lds" : "k_sell_spmv");
+        return CDFEM_OK;
+    });
+}
+
 int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
 {
     return guarded(c, [&] {

@@ -107,6 +107,7 @@ def _declare(L):
         "cdfem_profile_reset": (C.c_int, [vp]),
         "cdfem_profile_read": (C.c_int, [vp, C.c_int, _dp, C.POINTER(i64)]),
         "cdfem_kernel_bytes": (C.c_int, [vp, C.c_int, _dp]),
+        "cdfem_kernel_name": (C.c_int, [vp, C.c_int, C.c_char_p, C.c_size_t]),
         "cdfem_comm_unique_id": (C.c_int, [C.c_char_p]),
         "cdfem_comm_init_rccl": (C.c_int, [vp, C.c_int, C.c_int, C.c_char_p]),
         "cdfem_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, ALLREDUCE_FN, EXCHANGE_FN, vp]),
@@ -717,6 +718,12 @@ class Context:
         ms, n = C.c_double(), C.c_int64()
         self._chk(self.L.cdfem_profile_read(self.h, kernel, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def kernel_name(self, kernel):
+        """HIP kernel name of kernel id in the current configuration (assembled-operator apply)."""
+        buf = C.create_string_buffer(128)
+        self._chk(self.L.cdfem_kernel_name(self.h, kernel, buf, 128))
+        return buf.value.decode()
 
     def kernel_bytes(self, kernel):
         b = C.c_double()

@@ -280,6 +280,9 @@ int cdfem_profile_reset(cdfem_ctx *ctx);
 int cdfem_profile_read(cdfem_ctx *ctx, int kernel, double *total_ms, int64_t *count);
 /* algorithmic bytes moved by one launch of kernel id (see DESIGN.md for the per-unit figures) */
 int cdfem_kernel_bytes(cdfem_ctx *ctx, int kernel, double *bytes);
+/* the HIP kernel name (without template arguments) kernel id runs as in the current configuration,
+ * as rocprof reports it: the assembled-operator apply (CDFEM_K_APPLY after cdfem_fa_setup) only   */
+int cdfem_kernel_name(cdfem_ctx *ctx, int kernel, char *buf, size_t n);
 
 /* ---- multi-GPU (element-partitioned z-slabs, one context per GPU / rank) ----------------------
  * replaces: MPI_COMM_WORLD + ParMesh partition (linear_convection_diffusion_2D.cpp:300) and the MPI
