@@ -10,7 +10,6 @@ GPU (marked gpu): the same with the HIP kernels — 2 processes on ONE device, c
 callbacks over gloo (RCCL refuses two ranks per GPU) — against a single-context solve.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -21,16 +20,18 @@ KAPPA, S = 0.1, 1.0
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A fresh rendezvous file for one multi-process test (file store: no TCP port that another
+    process of the same run can take between choosing it and binding it)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="cdfem_rdv_")
+    os.close(fd)
+    os.unlink(path)  # the file store creates it
+    return path
 
 
 def _init(rank, world, port):
     import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     return dist
 
 

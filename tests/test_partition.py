@@ -12,7 +12,6 @@ converged GMRES / CG, bitwise-equal shared copies, P X (prolongation) of the tru
 block-Jacobi ILU(0) (one block per rank) against the oracle's restatement on the reference circle.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -22,16 +21,18 @@ CONV = (1.0, -2.0, 0.5)
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A fresh rendezvous file for one multi-process test (file store: no TCP port that another
+    process of the same run can take between choosing it and binding it)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="cdfem_rdv_")
+    os.close(fd)
+    os.unlink(path)  # the file store creates it
+    return path
 
 
 def _init(rank, world, port):
     import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     return dist
 
 
