@@ -105,6 +105,7 @@ void free_mesh(cdfem_ctx *c)
     c->d_sloc = nullptr;
     c->lds_rows = 0;
     c->lds_max = 0;
+    c->sell_lpr = 1;
     dfree(c->d_rperm); dfree(c->d_pv[0]); dfree(c->d_pv[1]); dfree(c->d_dinv_p);
     c->d_rperm = nullptr; c->d_pv[0] = c->d_pv[1] = nullptr; c->d_dinv_p = nullptr;
     dfree(c->d_svals_c);
@@ -1270,7 +1271,8 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
                 xyz = simplex_dof_coords(c->dim, c->p, c->ne, c->nd, c->nl, c->h_verts, c->h_dofs);
             FaPattern P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl,
                                            multi_rank(c) ? 0 : c->sell_mode, c->dim,
-                                           xyz.empty() ? nullptr : xyz.data(), c->sell_window, c->spmv_lds);
+                                           xyz.empty() ? nullptr : xyz.data(), c->sell_window, c->spmv_lds,
+                                           c->spmv_lpr);
             c->nnz = P.nnz;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
             c->d_cols = dalloc<int32_t>(P.cols.size());
@@ -1317,6 +1319,7 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
                 HIPCHK(hipMemcpyAsync(c->d_hidx, P.hidx.data(), P.hidx.size() * 4, hipMemcpyHostToDevice, c->stream));
                 HIPCHK(hipMemcpyAsync(c->d_sloc, P.sloc.data(), P.sloc.size() * 2, hipMemcpyHostToDevice, c->stream));
                 c->lds_rows = P.lds_rows;
+                c->sell_lpr = P.lpr;
                 c->lds_max = P.lds_max;
                 c->lds_halo = (int64_t)P.hidx.size();
             }
@@ -1574,6 +1577,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 7)
                 throw ArgError("sell_order must be 0..7 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton)");
             c->sell_mode = value;
+        } else if (k == "spmv_lpr") {  // read when the FA pattern is built (once per mesh)
+            if (value != 1 && value != 2 && value != 4) throw ArgError("spmv_lpr must be 1, 2 or 4");
+            c->spmv_lpr = value;
         } else if (k == "spmv_lds") {  // read when the FA pattern is built (once per mesh)
             if (value < -1 || (value > 0 && (value % 64 != 0 || value > 65536)))
                 throw ArgError("spmv_lds must be -1 (auto), 0 (off) or rows per window, a multiple of 64 up to 65536");

@@ -223,6 +223,8 @@ struct cdfem_ctx {
     int64_t lds_rows = 0;               // rows per window of the current LDS layout (0: none)
     int32_t lds_max = 0;                // largest window halo (doubles)
     int64_t lds_halo = 0;               // staged columns over all windows
+    int spmv_lpr = 1;                   // set_option "spmv_lpr": lanes per row of the LDS layouts (1, 2, 4)
+    int sell_lpr = 1;                   // lanes per row of the current SELL copy
     int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD (windowed layout)
     int32_t *d_rperm = nullptr;         // SpMV space order: space row -> mesh row (null: mesh order)
     bool sell_windowed = false;         // slices cut from the space order (kernel row = slice * 64 + lane)
@@ -381,6 +383,7 @@ struct FaPattern {
     // [w S, (w + 1) S), S = lds_rows / 64; its distinct columns hidx[hptr[w] .. hptr[w + 1]) (ascending)
     // are staged in LDS and every stored entry addresses them by sloc (16-bit position in the window)
     int64_t lds_rows = 0;
+    int lpr = 1;                  // lanes per row (R = 64 / lpr rows per slice; LDS layouts only)
     int32_t lds_max = 0;          // largest window halo (doubles of LDS)
     std::vector<int32_t> hptr, hidx;
     std::vector<uint16_t> sloc;
@@ -396,6 +399,7 @@ struct SellPlan {
     std::vector<int32_t> perm;   // space row -> mesh row (empty: mesh order)
     int64_t lds_rows = 0;        // windowed: rows per LDS-staged window (set_option "spmv_lds"; 0 off)
     bool auto_lds = false;       // the auto mode chose a windowed unstructured order: LDS windows
+    int lpr = 1;                 // LDS layouts: lanes per row (set_option "spmv_lpr")
 };
 constexpr int64_t kAutoLdsRows = 512;  // rows per window of the auto unstructured orders
 std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
@@ -407,7 +411,7 @@ std::vector<double> simplex_dof_coords(int dim, int p, int ne, int nd, int64_t n
 void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl);
 FaPattern fa_build_pattern(const std::vector<int32_t> &elem_dofs, int ne, int nd, int64_t nl, int sell_mode,
                            int dim = 0, const double *dof_xyz = nullptr, int64_t sell_window = 0,
-                           int64_t lds_rows = 0);
+                           int64_t lds_rows = 0, int lpr = 1);
 hipError_t launch_simplex_elem(cdfem_ctx *c, const double *kq, const double *kmq, double kappa, double alpha,
                                const double *conv, const double *cq, const double *mq, double mass);
 hipError_t launch_fa_assemble(cdfem_ctx *c);

@@ -49,7 +49,7 @@ static inline int64_t ee_index(int e, int i, int j, int nd)
 }
 
 FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int64_t nl, int sell_mode, int dim,
-                           const double *dof_xyz, int64_t sell_window, int64_t lds_rows)
+                           const double *dof_xyz, int64_t sell_window, int64_t lds_rows, int lpr)
 {
     // dof -> incidences (e * nd + l), ascending
     std::vector<int64_t> cnt(nl + 1, 0);
@@ -136,7 +136,17 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     // spmv_lds: > 0 rows per window; -1 (auto): the plan's window when the auto mode chose an
     // unstructured windowed order
     pl.lds_rows = !pl.windowed ? 0 : lds_rows > 0 ? lds_rows : (lds_rows < 0 && pl.auto_lds) ? pl.window : 0;
-    sell_build(P, nl, pl);
+    pl.lpr = pl.lds_rows > 0 ? lpr : 1;
+    try {
+        sell_build(P, nl, pl);
+    } catch (const std::runtime_error &) {
+        if (pl.lpr == 1) throw;
+        pl.lpr = 1;  // a multi-lane slice's halo exceeds the LDS budget: one lane per row
+        P.sptr.clear(); P.srows.clear(); P.scols.clear(); P.smap.clear(); P.sdel.clear(); P.swide.clear();
+        P.hptr.clear(); P.hidx.clear(); P.sloc.clear();
+        P.nnz_wide = 0; P.lds_rows = 0; P.lds_max = 0;
+        sell_build(P, nl, pl);
+    }
     return P;
 }
 
@@ -496,7 +506,10 @@ k_sell_spmv(const int32_t *__restrict__ sptr, const int32_t *__restrict__ srows,
 // HBM / L2 once per window.  Each row sums its entries in the stored order (bitwise the windowed
 // layout's sums).  Windows run in XCD-contiguous ranges (xcd_per > 0), so neighbouring windows, whose
 // halos overlap, share an L2.  CG mode: partials of (x, y) and early exit once the Krylov state is done.
-template <bool CG>
+// LPR lanes per row (R = 64 / LPR rows per slice): lane l sums the (l / R)-th contiguous part of row
+// l % R's entries, and the parts are combined by a fixed butterfly ((p0 + p1) + (p2 + p3)), so every
+// lane of the row holds the same total.
+template <bool CG, int LPR>
 __global__ void __launch_bounds__(256)
 k_sell_spmv_lds(const int32_t *__restrict__ sptr, const uint16_t *__restrict__ sloc, const double *__restrict__ svals,
                 const int32_t *__restrict__ hptr, const int32_t *__restrict__ hidx, const double *__restrict__ x,
@@ -533,8 +546,11 @@ k_sell_spmv_lds(const int32_t *__restrict__ sptr, const uint16_t *__restrict__ s
                 for (int k = 0; k < 4; ++k) a0 = fma(vv[k], xs[cc[k]], a0);
             }
             for (; j < len; ++j) a0 = fma(__builtin_nontemporal_load(v + j * 64), xs[__builtin_nontemporal_load(ci + j * 64)], a0);
-            const int64_t row = sl * 64 + lane;
-            if (row < n) {
+            constexpr int R = 64 / LPR;
+#pragma unroll
+            for (int o = R; o < 64; o <<= 1) a0 += __shfl_xor(a0, o, 64);
+            const int64_t row = sl * R + (lane % R);
+            if (lane < R && row < n) {
                 y[row] = a0;
                 if (CG) dd += a0 * x[row];
             }
@@ -629,7 +645,7 @@ static int sell_xcd_per(const cdfem_ctx *c)
 unsigned sell_grid(const cdfem_ctx *c)
 {
     if (c->lds_rows > 0) {
-        const int64_t spw = c->lds_rows / 64, nwin = (c->nslices + spw - 1) / spw;
+        const int64_t spw = c->lds_rows / (64 / c->sell_lpr), nwin = (c->nslices + spw - 1) / spw;
         return c->spmv_xcd ? 8u * (unsigned)((nwin + 7) / 8) : (unsigned)nwin;
     }
     return sell_xcd_per(c) ? 8u * (unsigned)sell_xcd_per(c) : sell_blocks(c);
@@ -639,7 +655,7 @@ bool spmv_delta(const cdfem_ctx *c) { return c->d_sdel && c->spmv_index16; }
 
 static int lds_windows(const cdfem_ctx *c)
 {
-    const int64_t spw = c->lds_rows / 64;
+    const int64_t spw = c->lds_rows / (64 / c->sell_lpr);
     return (int)((c->nslices + spw - 1) / spw);
 }
 
@@ -650,9 +666,14 @@ static void spmv_launch(cdfem_ctx *c, const double *vals, const double *x, doubl
     if (c->lds_rows > 0) {
         const int nwin = lds_windows(c), per = c->spmv_xcd ? (nwin + 7) / 8 : 0;
         const dim3 g(per ? 8u * (unsigned)per : (unsigned)nwin), b(256);
-        CDFEM_LAUNCH(c, (k_sell_spmv_lds<CG>), g, b, (size_t)c->lds_max * sizeof(double), c->d_sptr, c->d_sloc, vals,
-                     c->d_hptr, c->d_hidx, x, y, c->nslices, (int64_t)c->nl, (int)(c->lds_rows / 64), nwin, per, part,
-                     st);
+        const int spw = (int)(c->lds_rows / (64 / c->sell_lpr));
+#define CDFEM_SPMV_LDS(L)                                                                                       \
+    CDFEM_LAUNCH(c, (k_sell_spmv_lds<CG, L>), g, b, (size_t)c->lds_max * sizeof(double), c->d_sptr, c->d_sloc, vals, \
+                 c->d_hptr, c->d_hidx, x, y, c->nslices, (int64_t)c->nl, spw, nwin, per, part, st)
+        if (c->sell_lpr == 4) CDFEM_SPMV_LDS(4);
+        else if (c->sell_lpr == 2) CDFEM_SPMV_LDS(2);
+        else CDFEM_SPMV_LDS(1);
+#undef CDFEM_SPMV_LDS
         return;
     }
     const dim3 g(sell_grid(c)), b(256);

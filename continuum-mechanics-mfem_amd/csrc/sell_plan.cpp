@@ -416,7 +416,14 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
 void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
 {
     const std::vector<int32_t> &rowptr = P.rowptr, &cols = P.cols;
-    const int64_t ns = (nl + kLanes - 1) / kLanes;
+    // LDS-staged windowed layouts may give each row LPR lanes (R = 64 / LPR rows per slice, lane l
+    // holding the (l / R)-th contiguous part of row l % R's entries): less padding on meshes whose row
+    // lengths vary (the partial sums are combined in a fixed order by the kernel, k_sell_spmv_lds)
+    const int LPR = (pl.windowed && pl.lds_rows > 0) ? std::max(1, pl.lpr) : 1;
+    if (LPR != 1 && LPR != 2 && LPR != 4) throw std::runtime_error("sell_build: lanes per row must be 1, 2 or 4");
+    const int R = kLanes / LPR;
+    const int64_t ns = (nl + R - 1) / R;
+    P.lpr = LPR;
     const std::vector<int32_t> &sp = pl.perm;  // space row -> mesh row
     std::vector<int32_t> inv;                   // mesh row -> space row
     if (!sp.empty()) {
@@ -436,11 +443,11 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
     if (!permuted) P.srows.assign(ns * kLanes, -1);
     int64_t stored = 0;
     for (int64_t sl = 0; sl < ns; ++sl) {
-        int len = 0;
-        for (int l = 0; l < kLanes && sl * kLanes + l < nl; ++l) {
-            const int32_t q = order[sl * kLanes + l];
+        int len = 0;  // entries per lane
+        for (int l = 0; l < R && sl * R + l < nl; ++l) {
+            const int32_t q = order[sl * R + l];
             if (!permuted) P.srows[sl * kLanes + l] = q;
-            len = std::max(len, rlen(q));
+            len = std::max(len, (rlen(q) + LPR - 1) / LPR);
         }
         stored += (int64_t)len * kLanes;
         if (stored >= ((int64_t)1 << 31)) throw std::runtime_error("SELL storage exceeds int32 indexing");
@@ -451,9 +458,9 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
     // lane's own index in the space order (the base of its column deltas): its srows entry (global
     // layout) or its slice position (windowed); padding lanes take max(row, 0) / nl - 1
     auto lane_base = [&](int64_t sl, int l) -> int64_t {
-        const int64_t k = sl * kLanes + l;
+        const int64_t k = sl * R + l % R;
         if (permuted) return std::min<int64_t>(k, nl - 1);
-        const int32_t r = P.srows[k];
+        const int32_t r = P.srows[sl * kLanes + l];
         return r >= 0 ? r : 0;
     };
     par_for(ns, [&](int64_t s0, int64_t s1) {
@@ -461,8 +468,9 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
         for (int64_t sl = s0; sl < s1; ++sl) {
             const int len = (P.sptr[sl + 1] - P.sptr[sl]) / kLanes;
             for (int l = 0; l < kLanes; ++l) {
-                const int64_t k = sl * kLanes + l;
-                const int32_t r = k < nl ? mrow(order[k]) : -1;  // mesh row
+                const int64_t k = sl * R + l % R;
+                const int part = l / R;
+                const int32_t r = (k < nl && (permuted || l < R)) ? mrow(order[k]) : -1;  // mesh row
                 // a row's entries in ascending space column: in a permuted space the j-th entries
                 // of a slice's rows are then the same stencil neighbour (one short contiguous run
                 // of x per gather); the mesh order keeps its CSR order (bitwise the CSR sums)
@@ -471,12 +479,14 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
                     for (int32_t q = rowptr[r]; q < rowptr[r + 1]; ++q) ent.push_back(q);
                 if (!inv.empty())
                     std::sort(ent.begin(), ent.end(), [&](int32_t a, int32_t b) { return inv[cols[a]] < inv[cols[b]]; });
+                const int h = ((int)ent.size() + LPR - 1) / LPR;  // this row's entries per lane
                 for (int j = 0; j < len; ++j) {
                     const int64_t t = P.sptr[sl] + (int64_t)j * kLanes + l;
-                    if (r >= 0 && j < (int)ent.size()) {
-                        const int32_t c = cols[ent[j]];
+                    const int e = part * h + j;
+                    if (r >= 0 && j < h && e < (int)ent.size()) {
+                        const int32_t c = cols[ent[e]];
                         P.scols[t] = inv.empty() ? c : inv[c];
-                        P.smap[t] = ent[j];
+                        P.smap[t] = ent[e];
                     } else {
                         P.scols[t] = (int32_t)lane_base(sl, l);  // padding: a valid column, value 0
                     }
@@ -489,8 +499,9 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
     // its 32-bit columns and is flagged in swide; the 16-bit stream is built when at least half of
     // the stored entries lie in slices that fit (every slice of a lattice numbering does)
     std::vector<uint8_t> wide((size_t)ns, 0);
-    int64_t stored_wide = 0;
-    for (int64_t sl = 0; sl < ns; ++sl) {
+    int64_t stored_wide = LPR > 1 ? stored : 0;  // multi-lane rows: LDS positions only, no deltas
+    for (int64_t sl = 0; sl < ns && LPR > 1; ++sl) wide[sl] = 1;
+    for (int64_t sl = 0; sl < ns && LPR == 1; ++sl) {
         for (int32_t t = P.sptr[sl]; t < P.sptr[sl + 1]; ++t) {
             const int64_t d = (int64_t)P.scols[t] - lane_base(sl, (t - P.sptr[sl]) % kLanes);
             if (d < -32768 || d > 32767) { wide[sl] = 1; break; }
@@ -513,7 +524,7 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
     // (the x values it reads), and the entries address them by 16-bit window positions.  Windows
     // halve (down to one slice) until every halo fits kLdsHaloMax doubles.
     if (pl.lds_rows > 0 && permuted) {
-        int64_t S = std::max<int64_t>(1, pl.lds_rows / kLanes);
+        int64_t S = std::max<int64_t>(1, pl.lds_rows / R);  // slices per window
         for (;; S = std::max<int64_t>(1, S / 2)) {
             const int64_t nw = (ns + S - 1) / S;
             std::vector<std::vector<int32_t>> halo((size_t)nw);
@@ -530,8 +541,11 @@ void sell_build(FaPattern &P, int64_t nl, const SellPlan &pl)
             int64_t big = 0;
             for (auto &h : halo) big = std::max<int64_t>(big, (int64_t)h.size());
             if (big > kLdsHaloMax && S > 1) continue;
-            if (big > kLdsHaloMax) break;  // one slice does not fit: no LDS layout
-            P.lds_rows = S * kLanes;
+            if (big > kLdsHaloMax) {  // one slice does not fit: no LDS layout
+                if (LPR > 1) throw std::runtime_error("sell_build: a multi-lane SELL slice exceeds the LDS halo budget");
+                break;
+            }
+            P.lds_rows = S * R;
             P.lds_max = (int32_t)big;
             P.hptr.assign((size_t)nw + 1, 0);
             for (int64_t w = 0; w < nw; ++w) P.hptr[w + 1] = P.hptr[w] + (int32_t)halo[(size_t)w].size();
