@@ -1578,7 +1578,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
                 throw ArgError("sell_order must be 0..7 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton)");
             c->sell_mode = value;
         } else if (k == "spmv_lpr") {  // read when the FA pattern is built (once per mesh)
-            if (value != 1 && value != 2 && value != 4) throw ArgError("spmv_lpr must be 1, 2 or 4");
+            if (value != 0 && value != 1 && value != 2 && value != 4) throw ArgError("spmv_lpr must be 0 (auto), 1, 2 or 4");
             c->spmv_lpr = value;
         } else if (k == "spmv_lds") {  // read when the FA pattern is built (once per mesh)
             if (value < -1 || (value > 0 && (value % 64 != 0 || value > 65536)))

@@ -223,7 +223,7 @@ struct cdfem_ctx {
     int64_t lds_rows = 0;               // rows per window of the current LDS layout (0: none)
     int32_t lds_max = 0;                // largest window halo (doubles)
     int64_t lds_halo = 0;               // staged columns over all windows
-    int spmv_lpr = 1;                   // set_option "spmv_lpr": lanes per row of the LDS layouts (1, 2, 4)
+    int spmv_lpr = 0;                   // set_option "spmv_lpr": lanes per row of the LDS layouts (0 auto, 1, 2, 4)
     int sell_lpr = 1;                   // lanes per row of the current SELL copy
     int spmv_xcd = 1;                   // set_option "spmv_xcd": contiguous slice range per XCD (windowed layout)
     int32_t *d_rperm = nullptr;         // SpMV space order: space row -> mesh row (null: mesh order)

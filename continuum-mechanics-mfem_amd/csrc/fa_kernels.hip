@@ -136,7 +136,9 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     // spmv_lds: > 0 rows per window; -1 (auto): the plan's window when the auto mode chose an
     // unstructured windowed order
     pl.lds_rows = !pl.windowed ? 0 : lds_rows > 0 ? lds_rows : (lds_rows < 0 && pl.auto_lds) ? pl.window : 0;
-    pl.lpr = pl.lds_rows > 0 ? lpr : 1;
+    // spmv_lpr: 1, 2 or 4 lanes per row; 0 (auto): 4 on the auto mode's unstructured LDS layouts
+    // (c4u SpMV 103.3 -> 91.2 us, profiles/r03/ab_c4u_spmv_lanes_per_row.txt), else 1
+    pl.lpr = pl.lds_rows <= 0 ? 1 : lpr > 0 ? lpr : (pl.auto_lds ? 4 : 1);
     try {
         sell_build(P, nl, pl);
     } catch (const std::runtime_error &) {

@@ -254,9 +254,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *               A permuted order runs the Krylov solve in that order (Mult to rounding, iterates to
  *               1e-12).
  * "sell_window": 0 (default, auto) or a multiple of 64 — rows per window of the windowed orders.
- * "spmv_lpr": 1 (default), 2 or 4 — lanes per row of the LDS-staged layouts (read when the pattern
- *             is built): each lane sums a contiguous part of its row and the parts are combined in a
- *             fixed order (less padding where row lengths vary; results to rounding).
+ * "spmv_lpr": 0 (default, auto), 1, 2 or 4 — lanes per row of the LDS-staged layouts (read when
+ *             the pattern is built): each lane sums a contiguous part of its row and the parts are
+ *             combined in a fixed order (less padding where row lengths vary; results to rounding);
+ *             auto = 4 on the auto mode's unstructured layouts, else 1.
  * "spmv_lds": -1 (default, auto), 0 or rows per window — LDS-staged SpMV windows for the windowed
  *             orders: each workgroup stages its window's distinct columns in LDS and the entries
  *             address them by 16-bit window positions (bitwise the windowed sums); auto = on for the
