@@ -1574,8 +1574,8 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;
         } else if (k == "sell_order") {  // read when the FA pattern is built (once per mesh)
-            if (value < 0 || value > 7)
-                throw ArgError("sell_order must be 0..7 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton)");
+            if (value < 0 || value > 8)
+                throw ArgError("sell_order must be 0..8 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton, 8 Morton LDS windows / auto)");
             c->sell_mode = value;
         } else if (k == "spmv_lpr") {  // read when the FA pattern is built (once per mesh)
             if (value != 0 && value != 1 && value != 2 && value != 4) throw ArgError("spmv_lpr must be 0 (auto), 1, 2 or 4");

@@ -215,7 +215,7 @@ struct cdfem_ctx {
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
-    int sell_mode = 3;                  // set_option "sell_order" (read when the FA pattern is built)
+    int sell_mode = 8;                  // set_option "sell_order" (read when the FA pattern is built)
     int sell_window = 0;                // set_option "sell_window": rows per window of a windowed order (0 auto)
     int spmv_lds = -1;                  // set_option "spmv_lds": rows per LDS-staged SpMV window (0 off, -1 auto)
     int32_t *d_hptr = nullptr, *d_hidx = nullptr;  // LDS-staged windows (FaPattern::hptr / hidx / sloc)

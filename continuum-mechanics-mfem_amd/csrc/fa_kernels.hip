@@ -138,7 +138,23 @@ FaPattern fa_build_pattern(const std::vector<int32_t> &dof, int ne, int nd, int6
     pl.lds_rows = !pl.windowed ? 0 : lds_rows > 0 ? lds_rows : (lds_rows < 0 && pl.auto_lds) ? pl.window : 0;
     // spmv_lpr: 1, 2 or 4 lanes per row; 0 (auto): 4 on the auto mode's unstructured LDS layouts
     // (c4u SpMV 103.3 -> 91.2 us, profiles/r03/ab_c4u_spmv_lanes_per_row.txt), else 1
-    pl.lpr = pl.lds_rows <= 0 ? 1 : lpr > 0 ? lpr : (pl.auto_lds ? 4 : 1);
+    if (pl.lds_rows > 0 && lpr <= 0 && pl.auto_lds) {
+        // one lane per row pads each 64-row slice to its longest row: where that costs more than 15 %
+        // (unstructured meshes' vertex rows) 4 lanes per row, else 2 (measured best on the lattice)
+        int64_t st = 0, real = 0;
+        for (int64_t k0 = 0; k0 < nl; k0 += kLanes) {
+            int32_t mx = 0;
+            for (int64_t k = k0; k < std::min<int64_t>(nl, k0 + kLanes); ++k) {
+                const int32_t r = pl.perm.empty() ? (int32_t)k : pl.perm[k];
+                const int32_t len = P.rowptr[r + 1] - P.rowptr[r];
+                mx = std::max(mx, len);
+                real += len;
+            }
+            st += (int64_t)mx * kLanes;
+        }
+        lpr = st > real + real * 15 / 100 ? 4 : 2;
+    }
+    pl.lpr = pl.lds_rows <= 0 ? 1 : lpr > 0 ? lpr : 1;
     try {
         sell_build(P, nl, pl);
     } catch (const std::runtime_error &) {

@@ -26,7 +26,8 @@
 //             is banded that way; else RCM + global when its bandwidth is under half the natural
 //             one; when no order is banded — an unstructured mesh — Morton windows with coordinates,
 //             else RCM windows, both LDS-staged, spmv_lds auto), 4 = RCM + global, 5 = geometric +
-//             global, 6 = Morton + windows, 7 = Morton + global (morton_order).
+//             global, 6 = Morton + windows, 7 = Morton + global (morton_order), 8 = Morton windows
+//             staged in LDS when coordinates are known, else 3 (cdfem_fa_setup's default).
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -267,7 +268,19 @@ SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int m
     SellPlan pl;
     pl.mode = mode;
     pl.base = 1;
-    if (mode < 0 || mode > 7) throw std::runtime_error("sell_plan: bad mode");
+    if (mode < 0 || mode > 8) throw std::runtime_error("sell_plan: bad mode");
+    // 8 (the FA setup's default): Morton windows staged in LDS whenever the dof coordinates are known
+    // (lattice or unstructured alike), else the auto mode 3
+    if (mode == 8) {
+        if (xyz && dim >= 1 && dim <= 3) {
+            mode = 6;
+            pl.auto_lds = true;
+            if (window <= 0) window = kAutoLdsRows;
+        } else {
+            mode = 3;
+        }
+        pl.mode = mode;
+    }
     if ((mode == 5 || mode >= 6) && !xyz) throw std::runtime_error("sell_plan: the geometric / Morton order needs dof coordinates");
     if (mode == 0 || nl == 0) return pl;
     // base order

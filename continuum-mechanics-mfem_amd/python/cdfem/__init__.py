@@ -356,7 +356,7 @@ def partition_rcb(mesh: Mesh, nranks) -> np.ndarray:
 
 
 SELL_ORDER = {"legacy": 0, "natural": 1, "rcm": 2, "auto": 3, "rcm_global": 4, "geometric": 5, "morton": 6,
-              "morton_global": 7}
+              "morton_global": 7, "morton_lds": 8}
 
 
 def sell_plan(rowptr, cols, mode="auto", xyz=None):

@@ -248,16 +248,19 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *                 (column - lane row); a 64-row slice with a delta beyond 2^15 streams its 32-bit
  *                 columns instead (mixed layout, when at least half the entries fit); 0 = 32-bit
  *                 columns everywhere.
- * "sell_order": 0..7, default 3 (auto) — the FA SpMV's order, read when the pattern is built
+ * "sell_order": 0..8, default 8 — the FA SpMV's order, read when the pattern is built
  *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan): 0 natural, 1 natural +
- *               windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton.
+ *               windows, 2 RCM + windows, 3 auto (banded mesh order, geometric, RCM), 4 RCM, 5
+ *               geometric, 6 Morton + windows, 7 Morton, 8 Morton windows of 512 rows staged in LDS
+ *               (2 or 4 lanes per row by the padding) when the dof coordinates are known, else 3.
  *               A permuted order runs the Krylov solve in that order (Mult to rounding, iterates to
  *               1e-12).
  * "sell_window": 0 (default, auto) or a multiple of 64 — rows per window of the windowed orders.
  * "spmv_lpr": 0 (default, auto), 1, 2 or 4 — lanes per row of the LDS-staged layouts (read when
  *             the pattern is built): each lane sums a contiguous part of its row and the parts are
  *             combined in a fixed order (less padding where row lengths vary; results to rounding);
- *             auto = 4 on the auto mode's unstructured layouts, else 1.
+ *             auto = 4 where one lane per row would pad slices by more than 15 %, else 2, on the
+ *             auto modes' LDS layouts; 1 elsewhere.
  * "spmv_lds": -1 (default, auto), 0 or rows per window — LDS-staged SpMV windows for the windowed
  *             orders: each workgroup stages its window's distinct columns in LDS and the entries
  *             address them by 16-bit window positions (bitwise the windowed sums); auto = on for the
