@@ -360,12 +360,13 @@ def test_fa_spmv_index16_matches_int32(gpu_ctx):
     as 32-bit columns, for Mult, the constrained Mult and a CG solve.  A random DoF numbering
     (bandwidth > 2^15) falls back to 32-bit columns when the SpMV keeps the mesh's base order
     (sell_order 1) and is brought back into 16 bits by the reverse Cuthill-McKee order (sell_order 3,
-    the default); both give the permuted result."""
+    the auto order without LDS staging); both give the permuted result."""
     gm = cdfem.kuhn_mesh(3, 16, 2, perturb=0.1)      # 35,937 DoFs, lattice bandwidth 2,180
     rng = np.random.default_rng(16)
     x = rng.uniform(-1, 1, gm.nl)
     b = rng.uniform(-1, 1, gm.nl)
     res = {}
+    gpu_ctx.set_option("sell_order", 3)              # the SELL paths that stream column deltas
     try:
         for flag in (1, 0):
             gpu_ctx.set_option("spmv_index16", flag)
@@ -405,7 +406,7 @@ def test_fa_spmv_index16_matches_int32(gpu_ctx):
             assert np.abs(yp[perm] - y).max() <= 1e-13 * np.abs(y).max()
     finally:
         gpu_ctx.set_option("spmv_index16", 1)
-        gpu_ctx.set_option("sell_order", 3)
+        gpu_ctx.set_option("sell_order", 8)
 
 
 @pytest.mark.parametrize("dim,n,p,pert", [(2, 8, 2, 0.15), (3, 4, 2, 0.1), (2, 10, 1, 0.1)])
@@ -448,10 +449,11 @@ def test_ilu_rejected_for_cg_and_pa(gpu_ctx):
         gpu_ctx.solve(np.ones(m.nl), method="gmres", pc="ilu")
 
 
-@pytest.mark.parametrize("order", [2, 3, 4, 5, 1])
+@pytest.mark.parametrize("order", [2, 3, 4, 5, 1, 6, 8])
 def test_fa_reordered_space_solves(gpu_ctx, order):
     """The SpMV order (sell_order: 1 natural + windows, 2 RCM + windows, 3 auto = geometric + global
-    on a shuffled numbering, 4 RCM + global, 5 geometric + global) on a randomly relabelled Kuhn P2
+    on a shuffled numbering, 4 RCM + global, 5 geometric + global, 6 Morton + windows, 8 = the
+    default, Morton windows staged in LDS with 2 lanes per row) on a randomly relabelled Kuhn P2
     mesh: Krylov solves run in
     the permuted space (B in / X out permuted once per solve).  Against the mesh-order SpMV
     (sell_order 0) on the same shuffled mesh: Mult and constrained Mult to 1e-14 (a row sums its
@@ -491,4 +493,4 @@ def test_fa_reordered_space_solves(gpu_ctx, order):
         for k in (2, 3, 4, 5):
             assert np.abs(new[k] - base[k]).max() <= 1e-12 * np.abs(base[k]).max(), k
     finally:
-        gpu_ctx.set_option("sell_order", 3)
+        gpu_ctx.set_option("sell_order", 8)
