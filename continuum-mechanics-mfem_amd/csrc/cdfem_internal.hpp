@@ -401,7 +401,7 @@ struct SellPlan {
     bool auto_lds = false;       // the auto mode chose a windowed unstructured order: LDS windows
     int lpr = 1;                 // LDS layouts: lanes per row (set_option "spmv_lpr")
 };
-constexpr int64_t kAutoLdsRows = 512;  // rows per window of the auto unstructured orders
+constexpr int64_t kAutoLdsRows = 768;  // rows per window of the auto LDS orders (profiles/r03/ab_c4_lds_windows.txt)
 std::vector<int32_t> rcm_order(int64_t nl, const int32_t *rowptr, const int32_t *cols);
 SellPlan sell_plan(int64_t nl, const int32_t *rowptr, const int32_t *cols, int mode, int dim = 0,
                    const double *xyz = nullptr, int64_t window = 0);

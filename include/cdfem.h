@@ -251,7 +251,7 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "sell_order": 0..8, default 8 — the FA SpMV's order, read when the pattern is built
  *               (cdfem_fa_setup on a new mesh; see cdfem_sell_plan): 0 natural, 1 natural +
  *               windows, 2 RCM + windows, 3 auto (banded mesh order, geometric, RCM), 4 RCM, 5
- *               geometric, 6 Morton + windows, 7 Morton, 8 Morton windows of 512 rows staged in LDS
+ *               geometric, 6 Morton + windows, 7 Morton, 8 Morton windows of 768 rows staged in LDS
  *               (2 or 4 lanes per row by the padding) when the dof coordinates are known, else 3.
  *               A permuted order runs the Krylov solve in that order (Mult to rounding, iterates to
  *               1e-12).
@@ -264,7 +264,8 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "spmv_lds": -1 (default, auto), 0 or rows per window — LDS-staged SpMV windows for the windowed
  *             orders: each workgroup stages its window's distinct columns in LDS and the entries
  *             address them by 16-bit window positions (bitwise the windowed sums); auto = on for the
- *             unstructured orders sell_order 3 picks (Morton / RCM windows of 512 rows).
+ *             auto orders (sell_order 8, and the RCM windows sell_order 3 picks on unstructured meshes
+ *             without coordinates: 768 rows).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
  * "gm_ept": 0 (default, auto) — entries per thread of the GMRES orthogonalisation passes (4, 5, 6
  *           or 8); auto takes the smallest whose grid is resident in one round (same results).
