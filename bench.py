@@ -32,6 +32,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "continuum-mechanics-mfem_amd", "python"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# MI355X dense f64 peak, the same on the VALU (v_fma_f64) and the matrix cores (v_mfma_f64): 78.6
+# TFLOP/s spec; measured here 62.8 / 75.0 (profiles/r01c_fp64_probe.json)
+F64_PEAK_TFLOPS = 78.6
 
 
 def parse():
@@ -494,6 +497,11 @@ def main():
         pg.all_gather_object(comm_ranks, mine)
     c = (1.0, -2.0, 0.5)
     ctx.pa_setup(kinds=args.kinds, kappa=0.1, alpha=1.0, conv=c, mass=1.0)
+    # pa_affine (default): on this parallelepiped mesh the brick kernels form the point data from
+    # per-element factors; the byte count tells which form the context took
+    nq = (p + 2) ** 3
+    ncomp = (6 if args.kinds & 1 else 0) + (3 if args.kinds & 2 else 0) + (1 if args.kinds & 4 else 0)
+    affine = ctx.kernel_bytes(cdfem.K_APPLY) < 8.0 * ncomp * nq * mesh.ne
 
     # synthetic RHS resident in HBM: B = FormLinearSystem(u_bc = 0, b ~ U[-1,1))
     rng = np.random.default_rng(20261015 + rank)
@@ -551,13 +559,28 @@ def main():
             if os.path.exists(args.traffic_json):
                 try:
                     tj = json.load(open(args.traffic_json))
-                    key = f"n{n}_p{p}_k{args.kinds}"
+                    key = f"n{n}_p{p}_k{args.kinds}" + ("_aff" if affine else "")
                     traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": ("k_brick_cg (brick patch gather + D/C/M PA apply + in-LDS E->L + d.Ad)" if args.path == "brick"
+            if affine:
+                # affine factors: the apply reads ~110 MB and is bound by its f64 arithmetic
+                flops = ctx.kernel_flops(cdfem.K_APPLY)
+                tf = flops / per / 1e12
+                roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(tf / F64_PEAK_TFLOPS, 4), "traffic": traffic,
+                        "compute_unit": "VALU v_fma_f64 (the f64 dense peak is the same on the VALU and the "
+                                        "matrix cores)",
+                        "algorithmic_flops_per_launch": flops,
+                        "hbm_view": {"achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(achieved / HBM_PEAK_GBS, 4)}}
+            else:
+                roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+            roof.update({
+                    "kernel": (("k_brick_cg (brick patch gather + D/C/M PA apply" +
+                                (", point data from affine factors" if affine else "") +
+                                " + in-LDS E->L + d.Ad)") if args.path == "brick"
                                else "k_apply3d_tile (Q1 x Q1 thread tile per element, z planes in registers)" if args.order >= 3
                                else "k_apply3d (fused L->E gather + D/C/M PA apply)"),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
@@ -565,7 +588,7 @@ def main():
                     "other_kernels_avg_us": {
                         "e2l": round(e_ms / max(e_cnt, 1) * 1e3, 2),
                         "cg_update": round(u_ms / max(u_cnt, 1) * 1e3, 2),
-                        "cg_direction": round(d_ms / max(d_cnt, 1) * 1e3, 2)}}
+                        "cg_direction": round(d_ms / max(d_cnt, 1) * 1e3, 2)}})
 
     # host-boundary (PCIe-inclusive) rate: one solve with B and X in host memory (not `value`)
     host_rate = None
@@ -660,6 +683,9 @@ def main():
                                         "fixed-iteration Jacobi-CG on a symmetric operator",
                        "dofs": total_dofs, "elements": n * n * nz, "cg_iters_per_step": args.cg_iters,
                        "parallelism": f"slab{world}" if world > 1 else "single", "path": args.path,
+                       "qdata": ("affine: 10 factors per element, point data W_q g_e formed in the kernel "
+                                 "(pa_affine 1; the operator equals the per-point form bit for bit)" if affine
+                                 else "per-point stream (MFEM's PA layout)"),
                        "series": "strong: fixed n^3 split into z-slabs" if args.config == "c5"
                                  else "weak: an n x n x n/8 slab per rank (SURVEY 8e)" if args.config == "c5w"
                                  else "weak: an n^3 slab per rank",

@@ -85,10 +85,36 @@ T *dalloc(size_t n)
 
 int nq_of(const cdfem_ctx *c, const Rule1D &r) { return c->dim == 3 ? r.q1 * r.q1 * r.q1 : r.q1 * r.q1; }
 
+// every element a parallelepiped: each vertex v (lexicographic, bit k = axis k) equals
+// v0 + sum_k bit_k (v_{2^k} - v0) to 1e-13 of the element's coordinate scale.  Then the multilinear
+// map is affine and its Jacobian is the edge matrix at every point (the PA setup's pa_affine form).
+static bool mesh_is_affine(int dim, int64_t ne, const double *V)
+{
+    const int nv = 1 << dim;
+    for (int64_t e = 0; e < ne; ++e) {
+        const double *X = V + (size_t)e * nv * dim;
+        double h = 0.0;  // scale: edge lengths and coordinate magnitudes (rounding of the sums)
+        for (int v = 0; v < nv; ++v)
+            for (int i = 0; i < dim; ++i) h = std::max(h, std::fabs(X[v * dim + i]));
+        for (int k = 0; k < dim; ++k)
+            for (int i = 0; i < dim; ++i) h = std::max(h, std::fabs(X[(1 << k) * dim + i] - X[i]));
+        for (int v = 3; v < nv; ++v) {
+            if ((v & (v - 1)) == 0) continue;  // the edge vertices themselves
+            for (int i = 0; i < dim; ++i) {
+                double p = X[i];
+                for (int k = 0; k < dim; ++k)
+                    if (v >> k & 1) p += X[(1 << k) * dim + i] - X[i];
+                if (std::fabs(p - X[v * dim + i]) > 1e-13 * h) return false;
+            }
+        }
+    }
+    return true;
+}
+
 void free_mesh(cdfem_ctx *c)
 {
     dfree(c->d_verts); dfree(c->d_map); dfree(c->d_e2l_off); dfree(c->d_e2l_pos);
-    dfree(c->d_ess); dfree(c->d_ess_list); dfree(c->d_qd); dfree(c->d_Ye); dfree(c->d_dinv);
+    dfree(c->d_ess); dfree(c->d_ess_list); dfree(c->d_qd); dfree(c->d_qaff); dfree(c->d_Ye); dfree(c->d_dinv);
     for (auto &w : c->d_w) dfree(w);
     dfree(c->d_part); dfree(c->d_tpart); dfree(c->d_gm); dfree(c->d_gm_part);
     dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones); dfree(c->d_dalt);
@@ -770,6 +796,7 @@ int cdfem_mesh_upload(cdfem_ctx *c, int dim, int order, int ne, const double *el
             if (c->h_ess[i]) ess_list.push_back((int32_t)i);
         c->n_ess = (int)ess_list.size();
 
+        c->mesh_affine = mesh_is_affine(dim, ne, elem_verts);
         c->d_verts = dalloc<double>((size_t)ne * c->nv * dim);
         c->d_ess = dalloc<uint8_t>(nldofs);
         c->d_ess_list = dalloc<int32_t>(ess_list.size());
@@ -1126,6 +1153,10 @@ static int pa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
         c->d_qd = c->qlay == 1 ? dalloc<double>((size_t)c->ne * c->rule_op.q1 * qd_ho_plane(c->ncomp, c->rule_op.q1))
                                : dalloc<double>((size_t)c->nblk * nq * c->ncomp * kLanes);
         const size_t neq = (size_t)c->ne * nq;
+        dfree(c->d_qaff);
+        if (c->pa_affine && c->mesh_affine && c->qlay == 0 && !f->kappa_q && !f->kappa_mat_q && !f->conv_q &&
+            !f->mass_q)
+            c->d_qaff = dalloc<double>((size_t)c->nblk * c->ncomp * kLanes);
         double *dk = upload_opt(c, f->kappa_q, neq), *dkm = upload_opt(c, f->kappa_mat_q, neq * c->dim * (c->dim + 1) / 2);
         double *dc = upload_opt(c, f->conv_q, neq * c->dim), *dm = upload_opt(c, f->mass_q, neq);
         HIPCHK(launch_setup_qdata(c, dk, dkm, f->kappa, f->alpha, f->conv, dc, dm, f->mass));
@@ -1577,6 +1608,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 8)
                 throw ArgError("sell_order must be 0..8 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton, 8 Morton LDS windows / auto)");
             c->sell_mode = value;
+        } else if (k == "pa_affine") {  // read by cdfem_pa_setup
+            if (value != 0 && value != 1) throw ArgError("pa_affine must be 0 or 1");
+            c->pa_affine = value;
         } else if (k == "spmv_lpr") {  // read when the FA pattern is built (once per mesh)
             if (value != 0 && value != 1 && value != 2 && value != 4) throw ArgError("spmv_lpr must be 0 (auto), 1, 2 or 4");
             c->spmv_lpr = value;
@@ -1651,6 +1685,34 @@ int cdfem_kernel_name(cdfem_ctx *c, int k, char *buf, size_t n)
     });
 }
 
+int cdfem_kernel_flops(cdfem_ctx *c, int k, double *flops)
+{
+    return guarded(c, [&] {
+        require_pa(c);
+        if (!flops) throw ArgError("flops is null");
+        if (k != CDFEM_K_APPLY || c->fa_ready || c->dim != 3)
+            throw UnsupportedError("kernel flops: the 3D partial-assembly apply only");
+        // sum factorization, one element (pa_core.hpp elem_apply3d): per z plane the z contraction
+        // (D^3 FMA per field), per (z, y) the y contraction, per point the x contraction, the
+        // point operator and the transposed x contraction, then the transposed y and z contractions.
+        // Fields: value, plus the three reference derivatives when diffusion or convection is on.
+        const int D = c->d1, Q = c->rule_op.q1;
+        const bool kD = c->kinds & CDFEM_DIFFUSION, kC = c->kinds & CDFEM_CONVECTION, kM = c->kinds & CDFEM_MASS;
+        const int g = (kD || kC) ? 1 : 0;
+        double pt_fma = D * (1 + 3 * g) + D * (kD ? 4 : 1), pt_mul = 0.0;  // x contraction, transposed x
+        if (kD) { pt_fma += 6; pt_mul += 3; }
+        if (kC) { pt_fma += 2; pt_mul += 1; }
+        if (kM) { if (kC) pt_fma += 1; else pt_mul += 1; }
+        if (c->d_qaff) pt_mul += c->ncomp + 2;  // point data W_q * g_k, W_q = (w_x w_y) w_z
+        const double fma = Q * ((double)D * D * D * (1 + g) + Q * ((double)D * D * (1 + 2 * g) + Q * pt_fma +
+                                                                   (double)D * D * (kD ? 3 : 1)) +
+                                (double)D * D * D * (kD ? 2 : 1));
+        const double mul = (double)Q * Q * Q * pt_mul;
+        *flops = (2.0 * fma + mul) * (double)c->ne;
+        return CDFEM_OK;
+    });
+}
+
 int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
 {
     return guarded(c, [&] {
@@ -1684,8 +1746,9 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
             const double nf = (double)nface_dofs, nown = nl - nf;
             const double partials = 8.0 * c->nface * (double)c->nblk;
             switch (k) {
-            case CDFEM_K_APPLY:   // qdata + gathered r, M^-1, d + ess flags + owned d, q + face partials
-                *bytes = 8.0 * c->ncomp * nq * ne + 24.0 * nl + 1.0 * nl + 16.0 * nown + partials;
+            case CDFEM_K_APPLY:   // qdata (or per-element affine factors) + gathered r, M^-1, d + ess
+                                  // flags + owned d, q + face partials
+                *bytes = 8.0 * c->ncomp * (c->d_qaff ? 1.0 : nq) * ne + 24.0 * nl + 1.0 * nl + 16.0 * nown + partials;
                 return CDFEM_OK;
             case CDFEM_K_E2L:     // face partials + r, M^-1, d, ess of face dofs + d, q of face dofs
                 *bytes = partials + 25.0 * nf + 16.0 * nf;

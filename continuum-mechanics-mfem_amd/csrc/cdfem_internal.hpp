@@ -239,6 +239,9 @@ struct cdfem_ctx {
     int ncomp = 0;
     bool pa_ready = false;
     double *d_qd = nullptr;             // [nblk][nq][nc][64]
+    double *d_qaff = nullptr;           // [nblk][nc][64] per-element factors of an affine mesh (qd = W_q * g)
+    bool mesh_affine = false;           // every element a parallelepiped (checked at upload)
+    int pa_affine = 1;                  // set_option "pa_affine": 1 use the factors when the mesh allows
     double *d_Ye = nullptr;             // [nblk][nd][64]
     double *d_dinv = nullptr;           // Jacobi (constrained: ess -> 1)
     bool dinv_ready = false;

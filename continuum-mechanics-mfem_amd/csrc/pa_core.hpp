@@ -12,6 +12,7 @@ template <int D1, int Q1>
 struct Tab {
     double B[Q1][D1];
     double G[Q1][D1];
+    double w[Q1];  // 1D rule weights (the affine-geometry apply forms W_q = (w_x w_y) w_z)
 };
 
 template <int D1, int Q1>
@@ -23,6 +24,7 @@ static Tab<D1, Q1> make_tab(const Rule1D &r)
             t.B[q][d] = r.B[q][d];
             t.G[q][d] = r.G[q][d];
         }
+    for (int q = 0; q < Q1; ++q) t.w[q] = r.wts[q];
     return t;
 }
 
@@ -80,12 +82,20 @@ __device__ __forceinline__ void load_qp(const double *__restrict__ qp, int lane,
 // plane's worth of it live in registers.  QZU = unroll factor of the quadrature-plane loop
 // (Q1: straight-line code, the compiler hoists qdata loads across planes; 1: one plane's loads
 // in flight, ~250 VGPRs at p = 2, two waves per SIMD).
-template <int D1, int Q1, unsigned K, typename XL, int QZU = Q1>
+// AFF (affine elements, constant coefficients): q0 points at the block's per-element factors
+// [NC][kLanes] instead, and the point data is formed as W_q * G_k, the same product the setup
+// stores (k_setup_qdata, aff), so both forms apply the same operator bit for bit.
+template <int D1, int Q1, unsigned K, typename XL, int QZU = Q1, bool AFF = false>
 __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restrict__ q0, int lane,
                                              const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
 {
     using L = QLayout<K, 3>;
     constexpr int NC = L::nc;
+    double ga[NC];
+    if constexpr (AFF) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) ga[k] = q0[k * kLanes + lane];
+    }
 #pragma unroll
     for (int dz = 0; dz < D1; ++dz)
 #pragma unroll
@@ -147,9 +157,15 @@ __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restr
                     uy += T.B[qx][dx] * ay[dx];
                     uz += T.B[qx][dx] * az[dx];
                 }
-                const int q = qx + Q1 * (qy + Q1 * qz);
                 double qv[NC];
-                load_qp<NC, true>(q0 + (size_t)q * NC * kLanes, lane, qv);
+                if constexpr (AFF) {
+                    const double W = T.w[qx] * T.w[qy] * T.w[qz];
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) qv[k] = W * ga[k];
+                } else {
+                    const int q = qx + Q1 * (qy + Q1 * qz);
+                    load_qp<NC, true>(q0 + (size_t)q * NC * kLanes, lane, qv);
+                }
                 double vv = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
                 if constexpr (L::kD) {
                     gx = qv[0] * ux + qv[1] * uy + qv[2] * uz;

@@ -244,7 +244,7 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
               const Rule1D r, unsigned kinds,
               int nc, double kappa, const double *__restrict__ kappa_q, const double *__restrict__ kmat_q,
               double alpha, double c0, double c1, double c2, const double *__restrict__ conv_q, double mass,
-              const double *__restrict__ mass_q, double *__restrict__ qd)
+              const double *__restrict__ mass_q, double *__restrict__ qd, double *__restrict__ gaff)
 {
     const int q1 = r.q1;
     const int nq = DIM == 3 ? q1 * q1 * q1 : q1 * q1;
@@ -260,15 +260,51 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
         if (qlay == 1) qd[qd_ho_index(e, k, q, nc, q1)] = v;
         else out[qd_offset(k, lane, nc)] = v;
     };
+    // affine elements (gaff != nullptr, constant coefficients, block layout): J from the edge vectors
+    // (the multilinear map's Jacobian, constant on a parallelepiped) and every stored point value
+    // is W_q * g_k, with the per-element factor g_k also kept in gaff[b][k][lane] for the kernels
+    // that form the point data themselves (elem_apply3d<..., AFF>)
+    auto put_g = [&](int k, double W, double gk) {
+        out[qd_offset(k, lane, nc)] = W * gk;
+        if (q == 0) gaff[((size_t)b * nc + k) * kLanes + lane] = gk;
+    };
     if (e < 0 || e >= ne) {
         if (qlay == 0)
             for (int k = 0; k < nc; ++k) out[qd_offset(k, lane, nc)] = 0.0;
+        if (gaff && q == 0)
+            for (int k = 0; k < nc; ++k) gaff[((size_t)b * nc + k) * kLanes + lane] = 0.0;
         return;
     }
     double xi[3], W;
     qpoint(q, q1, DIM, r, xi, W);
     double x[3], J[3][3], A[3][3];
-    q1_map<DIM>(verts + (size_t)e * (1 << DIM) * DIM, xi, x, J);
+    const double *V = verts + (size_t)e * (1 << DIM) * DIM;
+    if (gaff) {
+        for (int i = 0; i < DIM; ++i)
+            for (int k = 0; k < DIM; ++k) J[i][k] = V[(1 << k) * DIM + i] - V[i];
+        const double det = adjugate<DIM>(J, A);
+        int o = 0;
+        if (kinds & CDFEM_DIFFUSION) {
+            const double s = kappa / det;
+            for (int i = 0; i < DIM; ++i)
+                for (int j = i; j < DIM; ++j) {
+                    double acc = 0.0;
+                    for (int k = 0; k < DIM; ++k) acc += A[i][k] * A[j][k];
+                    put_g(o++, W, s * acc);
+                }
+        }
+        if (kinds & CDFEM_CONVECTION) {
+            const double cv[3] = {c0, c1, c2};
+            for (int i = 0; i < DIM; ++i) {
+                double acc = 0.0;
+                for (int k = 0; k < DIM; ++k) acc += A[i][k] * cv[k];
+                put_g(o++, W, alpha * acc);
+            }
+        }
+        if (kinds & CDFEM_MASS) put_g(o++, W, mass * det);
+        return;
+    }
+    q1_map<DIM>(V, xi, x, J);
     const double det = adjugate<DIM>(J, A);
     const size_t eq = (size_t)e * nq + q;
     int o = 0;
@@ -689,11 +725,11 @@ hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, const doubl
     if (c->dim == 3)
         hipLaunchKernelGGL(k_setup_qdata<3>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
                            c->d_verts, c->d_perm, c->ne, c->nblk, c->qlay, c->rule_op, c->kinds, c->ncomp, kappa,
-                           d_kappa_q, d_kmat_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
+                           d_kappa_q, d_kmat_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd, c->d_qaff);
     else
         hipLaunchKernelGGL(k_setup_qdata<2>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream,
                            c->d_verts, c->d_perm, c->ne, c->nblk, c->qlay, c->rule_op, c->kinds, c->ncomp, kappa,
-                           d_kappa_q, d_kmat_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd);
+                           d_kappa_q, d_kmat_q, alpha, c0, c1, c2, d_conv_q, mass, d_mass_q, c->d_qd, c->d_qaff);
     return hipGetLastError();
 }
 

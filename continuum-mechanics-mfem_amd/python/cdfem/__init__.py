@@ -107,6 +107,7 @@ def _declare(L):
         "cdfem_profile_reset": (C.c_int, [vp]),
         "cdfem_profile_read": (C.c_int, [vp, C.c_int, _dp, C.POINTER(i64)]),
         "cdfem_kernel_bytes": (C.c_int, [vp, C.c_int, _dp]),
+        "cdfem_kernel_flops": (C.c_int, [vp, C.c_int, _dp]),
         "cdfem_kernel_name": (C.c_int, [vp, C.c_int, C.c_char_p, C.c_size_t]),
         "cdfem_comm_unique_id": (C.c_int, [C.c_char_p]),
         "cdfem_comm_init_rccl": (C.c_int, [vp, C.c_int, C.c_int, C.c_char_p]),
@@ -724,6 +725,12 @@ class Context:
         buf = C.create_string_buffer(128)
         self._chk(self.L.cdfem_kernel_name(self.h, kernel, buf, 128))
         return buf.value.decode()
+
+    def kernel_flops(self, kernel):
+        """Algorithmic f64 flops of one launch of the 3D PA apply (FMA = 2)."""
+        f = C.c_double()
+        self._chk(self.L.cdfem_kernel_flops(self.h, kernel, C.byref(f)))
+        return f.value
 
     def kernel_bytes(self, kernel):
         b = C.c_double()

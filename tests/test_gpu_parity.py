@@ -384,6 +384,48 @@ def test_brick_cg_bench_operator_parity(gpu_ctx, n, p):
     np.testing.assert_array_equal(xg, xg2)
 
 
+@pytest.mark.parametrize("n,p,kinds", [(8, 2, 7), (6, 2, 3), (9, 1, 7), (5, 2, 4)])
+def test_brick_affine_factors(gpu_ctx, n, p, kinds):
+    """Affine box (pa_affine, default): the brick kernels form each point's data as W_q * g_e from
+    one factor set per element instead of streaming the per-point qdata.  Against the oracle at the
+    generic bar, against the per-point form (pa_affine 0) to rounding, and the byte count shows the
+    factor form is in use (a perturbed mesh keeps the per-point stream)."""
+    om = O.BoxMesh(3, n, p)
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_to_oracle(kinds))
+    x = np.random.default_rng(31).uniform(-1, 1, om.nl)
+    b = np.random.default_rng(32).uniform(-1, 1, om.nl)
+    u = np.zeros(om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    out = {}
+    try:
+        for aff in (1, 0):
+            gpu_ctx.set_option("pa_affine", aff)
+            gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+            gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            out[aff] = dict(y=gpu_ctx.mult(x), yc=gpu_ctx.mult(x, constrained=True), dg=gpu_ctx.diagonal(),
+                            bytes=gpu_ctx.kernel_bytes(cdfem.K_APPLY))
+            _, B = gpu_ctx.form_linear_system(u, b)
+            out[aff]["x"], info = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0,
+                                                max_iter=30)
+            assert info["iterations"] == 30
+    finally:
+        gpu_ctx.set_option("pa_affine", 1)
+    assert out[1]["bytes"] < out[0]["bytes"]
+    assert _relmax(out[1]["y"], A.mult(x)) <= MULT_TOL
+    assert _relmax(out[1]["dg"], A.diag()) <= MULT_TOL
+    assert np.linalg.norm(out[1]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
+    for k in ("y", "yc", "dg"):
+        assert _relmax(out[1][k], out[0][k]) <= 1e-13
+    assert np.linalg.norm(out[1]["x"] - out[0]["x"]) <= 1e-12 * np.linalg.norm(out[0]["x"])
+    # a perturbed mesh is not affine: the per-point stream stays
+    om2 = O.BoxMesh(3, n, p, perturb=0.1)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om2.verts, om2.dofmap, om2.nl, om2.ess)).set_structured(n, n, n)
+    gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    assert gpu_ctx.kernel_bytes(cdfem.K_APPLY) == out[0]["bytes"]
+
+
 def test_brick_full_size_matches_generic(gpu_ctx):
     """64^3 p=2: brick and generic paths agree (different E->L summation order only)."""
     gm = cdfem.box_mesh(3, 64, 2, with_coords=False)

@@ -3,7 +3,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-OUT=gpurun_out/r03l
+OUT=gpurun_out/${OUT_TAG:-r03l}
 mkdir -p $OUT
 T=900 bash tools/gpu_suite.sh; rc=$?
 cp gpurun_out/suite.log $OUT/suite.log

@@ -7,7 +7,7 @@ writes profiles/<tag>_kernel_stats.csv   (rocprofv3 --kernel-trace --stats of th
        profiles/<tag>_bench.json         (the bench line of the same round)
        profiles/<tag>_pmc.json           (per-kernel HBM bytes per launch, corrected)
        profiles/pmc_traffic.json         (the roofline kernel's entry, read by bench.py -> roofline.traffic;
-                                          key n{n}_p{p}_k{kinds} for the hex configs, c4_n{n}_p2 for C4)
+                                          key n{n}_p{p}_k{kinds}[_aff] for the hex configs, c4_n{n}_p2 for C4)
 
 Correction (MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE reports 1/2 of the bytes actually read.  The factor is not assumed but
@@ -86,7 +86,7 @@ def main():
         n = int(wl.split("x")[0])
         order = int(wl.split("p=")[1].split(",")[0])
         kinds = int(wl.split("kinds=")[1].split(")")[0])
-        key = f"n{n}_p{order}_k{kinds}"
+        key = f"n{n}_p{order}_k{kinds}" + ("_aff" if cfg.get("qdata", "").startswith("affine") else "")
     tj[key] = {"hbm_bytes_per_launch": apply["hbm_bytes_per_launch"], "round": tag,
                                      "kernel": kname, "source": f"profiles/{tag}_pmc.json"}
     json.dump(tj, open(p, "w"), indent=1)
