@@ -1154,8 +1154,7 @@ static int pa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
                                : dalloc<double>((size_t)c->nblk * nq * c->ncomp * kLanes);
         const size_t neq = (size_t)c->ne * nq;
         dfree(c->d_qaff);
-        if (c->pa_affine && c->mesh_affine && c->qlay == 0 && !f->kappa_q && !f->kappa_mat_q && !f->conv_q &&
-            !f->mass_q)
+        if (c->pa_affine && c->mesh_affine && !f->kappa_q && !f->kappa_mat_q && !f->conv_q && !f->mass_q)
             c->d_qaff = dalloc<double>((size_t)c->nblk * c->ncomp * kLanes);
         double *dk = upload_opt(c, f->kappa_q, neq), *dkm = upload_opt(c, f->kappa_mat_q, neq * c->dim * (c->dim + 1) / 2);
         double *dc = upload_opt(c, f->conv_q, neq * c->dim), *dm = upload_opt(c, f->mass_q, neq);
@@ -1759,12 +1758,14 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
             default: throw ArgError("kernel not launched on the brick path");
             }
         }
+        // the high-order tile apply on affine factors reads one factor set per element
+        const double nqs = (c->qlay == 1 && tile_affine(c)) ? 1.0 : nq;
         switch (k) {
         case CDFEM_K_APPLY:
             if (c->epencil)  // lattice gather: x + ess flags (each L-dof once) + qdata + E-vector write
-                *bytes = 9.0 * nl + 8.0 * c->ncomp * nq * ne + 8.0 * nd * ne;
+                *bytes = 9.0 * nl + 8.0 * c->ncomp * nqs * ne + 8.0 * nd * ne;
             else             // x gather (each L-dof once) + qdata stream + element map + E-vector write
-                *bytes = 8.0 * nl + 8.0 * c->ncomp * nq * ne + 4.0 * nd * ne + 8.0 * nd * ne;
+                *bytes = 8.0 * nl + 8.0 * c->ncomp * nqs * ne + 4.0 * nd * ne + 8.0 * nd * ne;
             break;
         case CDFEM_K_E2L:
             if (c->epencil)  // E-vector read + ess flags + y write + x read (constraint / dot)

@@ -286,6 +286,9 @@ struct cdfem_ctx {
 
 namespace cdfem {
 
+// the high-order tile apply forms the point data from the affine factors (ho_mfma keeps the stream)
+inline bool tile_affine(const cdfem_ctx *c) { return c->d_qaff != nullptr && c->ho_mfma == 0; }
+
 // ---- kernel launchers (pa_kernels.hip) -------------------------------------------------------
 hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, const double *d_kmat_q, double kappa, double alpha,
                               const double *conv, const double *d_conv_q, const double *d_mass_q,

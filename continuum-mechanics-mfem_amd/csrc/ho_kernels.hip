@@ -106,7 +106,7 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     constexpr int SA = 3 * D1 * QQ;          // X, then W0 / Wx / Wy [dz][qy][qx]
     constexpr int SB = 2 * D1 * D1 * Q1;     // BX / GX, then ZB / ZG [dz][dy][qx]
     static_assert(SA >= ND, "LDS buffer sizes");
-    __shared__ double sBt[Q1 * D1], sGt[Q1 * D1];
+    __shared__ double sBt[Q1 * D1], sGt[Q1 * D1], sW[Q1];
     __shared__ double bufA[EPB][SA];
     __shared__ double bufB[EPB][SB];
 
@@ -118,6 +118,7 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
         const int q = threadIdx.x / D1, d = threadIdx.x % D1;
         sBt[threadIdx.x] = T.B[q][d];
         sGt[threadIdx.x] = T.G[q][d];
+        if (d == 0) sW[q] = T.w[q];
     }
     double *A = bufA[le < EPB ? le : 0], *Bf = bufB[le < EPB ? le : 0];
 
@@ -158,7 +159,12 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     // gather loads ahead of the stream in issue order)
     __builtin_amdgcn_sched_barrier(0);
     double qv[Q1][NC];
-    {
+    if constexpr ((MF & 16) != 0) {
+        // affine factors (pa_affine): qd holds g[e][NC]; the point data W_q g_k with W_q = (w_x w_y) w_z,
+        // the product the setup stores (k_setup_qdata), formed after the table barrier below
+#pragma unroll
+        for (int k = 0; k < NC; ++k) qv[0][k] = qd[(size_t)ec * NC + k];
+    } else {
         const double *qe = qd + (size_t)ec * Q1 * PS;
 #pragma unroll
         for (int qz = 0; qz < Q1; ++qz) {
@@ -181,6 +187,18 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
         A[gthr ? (dz * D1 + ty) * D1 + tx : ND + t * D1 + dz] = zero ? 0.0 : xr[dz];
     }
     __syncthreads();
+    if constexpr ((MF & 16) != 0) {
+        double g[NC];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) g[k] = qv[0][k];
+        const double wxy = sW[tx < Q1 ? tx : 0] * sW[ty < Q1 ? ty : 0];
+#pragma unroll
+        for (int qz = 0; qz < Q1; ++qz) {
+            const double W = wxy * T.w[qz];
+#pragma unroll
+            for (int k = 0; k < NC; ++k) qv[qz][k] = W * g[k];
+        }
+    }
     // stage x: threads (qx = tx, dy = ty), or the matrix cores (MF & 1)
     constexpr int DD = D1 * D1, DQ = D1 * Q1;
     if constexpr ((MF & 1) != 0) {
@@ -436,24 +454,25 @@ static hipError_t tile_kinds_mf(cdfem_ctx *c, const double *x, double *Ye, bool 
     geo.Ly = (uint32_t)c->Ly;
     geo.nz = c->epencil ? (uint32_t)(c->ne / ((int64_t)geo.ho.nx * geo.ho.ny)) : 0;
     geo.ess = c->d_ess;
+    const double *qd = (MF & 16) ? c->d_qaff : c->d_qd;
     if (den_part) {
         if (!c->epencil || !con) return hipErrorInvalidValue;
-        CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true, MF>), grid, block, 0, c->d_map, x, c->d_qd,
+        CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, true, MF>), grid, block, 0, c->d_map, x, qd,
                      Ye, T, c->ne, geo, st, den_part);
     } else if (c->epencil) {
         if (con)
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, true, false, MF>), grid, block, 0, c->d_map, x, qd,
                          Ye, T, c->ne, geo, st, (double *)nullptr);
         else
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, true, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, true, false, MF>), grid, block, 0, c->d_map, x, qd,
                          Ye, T, c->ne, geo, st, (double *)nullptr);
     } else {
         if (con)
-            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, false, false, MF>), grid, block, 0, c->d_map, x, c->d_qd,
+            CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, true, false, false, MF>), grid, block, 0, c->d_map, x, qd,
                          Ye, T, c->ne, geo, st, (double *)nullptr);
         else
             CDFEM_LAUNCH(c, (k_apply3d_tile<D1, Q1, K, false, false, false, MF>), grid, block, 0, c->d_map, x,
-                         c->d_qd, Ye, T, c->ne, geo, st, (double *)nullptr);
+                         qd, Ye, T, c->ne, geo, st, (double *)nullptr);
     }
     return hipGetLastError();
 }
@@ -462,6 +481,7 @@ template <int D1, int Q1, unsigned K>
 static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
                              double *den_part)
 {
+    if (tile_affine(c)) return tile_kinds_mf<D1, Q1, K, 16>(c, x, Ye, con, st, den_part);
     switch (c->ho_mfma) {
     case 1: return tile_kinds_mf<D1, Q1, K, 1>(c, x, Ye, con, st, den_part);
     case 3: return tile_kinds_mf<D1, Q1, K, 3>(c, x, Ye, con, st, den_part);

@@ -262,16 +262,17 @@ k_setup_qdata(const double *__restrict__ verts, const int32_t *__restrict__ perm
     };
     // affine elements (gaff != nullptr, constant coefficients, block layout): J from the edge vectors
     // (the multilinear map's Jacobian, constant on a parallelepiped) and every stored point value
-    // is W_q * g_k, with the per-element factor g_k also kept in gaff[b][k][lane] for the kernels
-    // that form the point data themselves (elem_apply3d<..., AFF>)
+    // is W_q * g_k, with the per-element factor g_k also kept in gaff ([b][k][lane] on the block
+    // layout, [e][k] on the high-order layout) for the kernels that form the point data themselves
+    // (elem_apply3d<..., AFF>, k_apply3d_tile<..., MF & 16>)
     auto put_g = [&](int k, double W, double gk) {
-        out[qd_offset(k, lane, nc)] = W * gk;
-        if (q == 0) gaff[((size_t)b * nc + k) * kLanes + lane] = gk;
+        put(k, W * gk);
+        if (q == 0) gaff[qlay == 1 ? (size_t)e * nc + k : ((size_t)b * nc + k) * kLanes + lane] = gk;
     };
     if (e < 0 || e >= ne) {
         if (qlay == 0)
             for (int k = 0; k < nc; ++k) out[qd_offset(k, lane, nc)] = 0.0;
-        if (gaff && q == 0)
+        if (gaff && q == 0 && qlay == 0)
             for (int k = 0; k < nc; ++k) gaff[((size_t)b * nc + k) * kLanes + lane] = 0.0;
         return;
     }

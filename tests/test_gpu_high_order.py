@@ -283,3 +283,45 @@ def test_ho_mfma_fused_cg_parity(gpu_ctx, n, p, mf):
         gpu_ctx.set_option("ho_mfma", 0)
     assert io["iterations"] == ig["iterations"] == 50
     assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
+
+
+@pytest.mark.parametrize("n,p,structured,kinds", [(3, 4, True, 7), (4, 3, True, 5), (3, 4, False, 7),
+                                                  (5, 4, True, 6)])
+def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
+    """pa_affine (default) on an affine box: the tile apply forms each point's data as W_q * g_e from
+    one factor set per element (the product the setup stores, so the per-point values are the
+    same bits).  Mult, constrained Mult, diagonal against the oracle (1e-13) and the per-point
+    multilinear-map setup (pa_affine 0, rounding: 1e-13); 50 fused CG iterates against the oracle
+    (1e-11); the byte count drops by the stream."""
+    om = O.BoxMesh(3, n, p)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(kinds))
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    x = np.random.default_rng(41).uniform(-1, 1, om.nl)
+    rng = np.random.default_rng(42)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=50)
+    out = {}
+    try:
+        for aff in (1, 0):
+            gpu_ctx.set_option("pa_affine", aff)
+            gpu_ctx.upload_mesh(gm)
+            if structured:
+                gpu_ctx.set_structured(n, n, n)
+            gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            _, B = gpu_ctx.form_linear_system(u, b)
+            xg, ig = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=50, check_every=7)
+            out[aff] = dict(y=gpu_ctx.mult(x), yc=gpu_ctx.mult(x, constrained=True), dg=gpu_ctx.diagonal(),
+                            bytes=gpu_ctx.kernel_bytes(cdfem.K_APPLY), x=xg, it=ig["iterations"])
+    finally:
+        gpu_ctx.set_option("pa_affine", 1)
+    yo = A.mult(x)
+    assert out[1]["bytes"] < out[0]["bytes"]
+    assert np.abs(out[1]["y"] - yo).max() <= 1e-13 * np.abs(yo).max()
+    assert np.abs(out[1]["dg"] - A.diag()).max() <= 1e-13 * np.abs(A.diag()).max()
+    for k in ("y", "yc", "dg"):
+        assert np.abs(out[1][k] - out[0][k]).max() <= 1e-13 * np.abs(out[0][k]).max()
+    assert out[1]["it"] == 50
+    assert np.linalg.norm(out[1]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
