@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spd-steps", type=int, default=2,
                     help="informational CG line on the symmetric kK+sM operator (steps of 200 it); 0 = skip")
+    ap.add_argument("--per-point-steps", type=int, default=2,
+                    help="informational: the CG line with the per-point qdata stream (pa_affine 0); 0 = skip")
     ap.add_argument("--gmres-iters", type=int, default=60,
                     help="informational GMRES(30)+Jacobi line (the reference's solver); 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
@@ -652,8 +654,47 @@ def main():
         s_us = a_ms / max(a_cnt, 1) * 1e3
         spd = {"value": mesh.nl * sits / sdt, "unit": "DoF-iter/s", "operator": "kK+sM (kinds=5, c=0)",
                "cg_iters_per_step": 200, "steps": args.spd_steps, "apply_avg_us": round(s_us, 2),
-               "apply_frac": round(sb / (s_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if a_cnt else None}
+               "apply_frac": (round(ctx.kernel_flops(cdfem.K_APPLY) / (s_us * 1e-6) / 1e12 / F64_PEAK_TFLOPS, 4)
+                              if affine else round(sb / (s_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)) if a_cnt else None,
+               "apply_frac_of": "f64 78.6 TFLOP/s" if affine else "HBM 8 TB/s"}
         ctx.free(dB5)
+
+    # informational: the same CG steps with MFEM's per-point qdata stream (pa_affine 0), so the line
+    # shows both forms of the operator on one box
+    per_point = None
+    if world == 1 and affine and args.per_point_steps > 0 and args.config in ("c2", "c3"):
+        c2 = cdfem.Context(local % ndev)
+        c2.set_option("pa_affine", 0)
+        c2.upload_mesh(mesh)
+        if args.path == "brick" or p >= 3:
+            c2.set_structured(n, n, nzr)
+        c2.pa_setup(kinds=args.kinds, kappa=0.1, alpha=1.0, conv=c, mass=1.0)
+        dB2, dX2 = c2.to_device(B), c2.alloc(8 * mesh.nl)
+
+        def pstep():
+            return c2.solve_device(dB2, dX2, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0,
+                                   max_iter=args.cg_iters, check_every=args.cg_iters)
+        pstep()
+        c2.synchronize()
+        t0 = time.perf_counter()
+        pits = sum(pstep()["iterations"] for _ in range(args.per_point_steps))
+        c2.synchronize()
+        pdt = time.perf_counter() - t0
+        c2.set_option("profile_mask", 1 << cdfem.K_APPLY)
+        c2.profile(True)
+        pstep()
+        c2.synchronize()
+        a_ms, a_cnt = c2.profile_read(cdfem.K_APPLY)
+        c2.profile(False)
+        p_us = a_ms / max(a_cnt, 1) * 1e3
+        pb = c2.kernel_bytes(cdfem.K_APPLY)
+        per_point = {"value": mesh.nl * pits / pdt, "unit": "DoF-iter/s", "steps": args.per_point_steps,
+                     "qdata": "per-point stream (pa_affine 0, MFEM's PA layout)", "apply_avg_us": round(p_us, 2),
+                     "apply_hbm_frac": round(pb / (p_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if a_cnt else None,
+                     "algorithmic_bytes_per_launch": pb}
+        c2.free(dB2)
+        c2.free(dX2)
+        c2.close()
 
     ntrue = mesh.nl  # per rank (slab L-vector); interface planes counted once below
     total_dofs = (p * n + 1) ** 2 * (p * nz + 1) if world > 1 else ntrue
@@ -696,6 +737,8 @@ def main():
             out["gmres"] = gm
         if spd is not None:
             out["spd_cg"] = spd
+        if per_point is not None:
+            out["per_point_qdata"] = per_point
         if host_rate is not None:
             out["host_boundary_rate"] = {"value": host_rate, "unit": "DoF-iter/s",
                                          "note": "one solve with B/X in host memory (PCIe copies included)"}
