@@ -1702,7 +1702,8 @@ int cdfem_kernel_flops(cdfem_ctx *c, int k, double *flops)
         if (kD) { pt_fma += 6; pt_mul += 3; }
         if (kC) { pt_fma += 2; pt_mul += 1; }
         if (kM) { if (kC) pt_fma += 1; else pt_mul += 1; }
-        if (c->d_qaff) pt_mul += c->ncomp + 2;  // point data W_q * g_k, W_q = (w_x w_y) w_z
+        if (c->qlay == 1 ? tile_affine(c) : c->d_qaff != nullptr)
+            pt_mul += c->ncomp + 2;  // point data W_q * g_k, W_q = (w_x w_y) w_z
         const double fma = Q * ((double)D * D * D * (1 + g) + Q * ((double)D * D * (1 + 2 * g) + Q * pt_fma +
                                                                    (double)D * D * (kD ? 3 : 1)) +
                                 (double)D * D * D * (kD ? 2 : 1));
@@ -1758,8 +1759,8 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
             default: throw ArgError("kernel not launched on the brick path");
             }
         }
-        // the high-order tile apply on affine factors reads one factor set per element
-        const double nqs = (c->qlay == 1 && tile_affine(c)) ? 1.0 : nq;
+        // the 3D applies on affine factors read one factor set per element (the 2D apply streams)
+        const double nqs = (c->qlay == 1 ? tile_affine(c) : (c->dim == 3 && c->d_qaff != nullptr)) ? 1.0 : nq;
         switch (k) {
         case CDFEM_K_APPLY:
             if (c->epencil)  // lattice gather: x + ess flags (each L-dof once) + qdata + E-vector write
