@@ -63,8 +63,8 @@ constexpr int face_count() { return 2 * S * S + (S - 2) * (4 * S - 4); }
 // One wave per SIMD, unconstrained registers: 241.5 vs 272.2 us per C2 apply in the GMRES leg
 // against a two-waves-per-SIMD build (<= 256 registers, 124 B/lane of spills; tools/ab_gmres.py,
 // profiles/r02_ab_c2_gmres_brick_waves.txt).
-template <int D1, int Q1, unsigned K, int MODE, bool AFF>
-__global__ void __launch_bounds__(64, 1)
+template <int D1, int Q1, unsigned K, int MODE, int AF>
+__global__ void __launch_bounds__(64, AF == 2 ? 2 : 1)
 k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double *__restrict__ d,
           double *__restrict__ y, double *__restrict__ face, const double *__restrict__ qd,
           const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g,
@@ -120,7 +120,7 @@ k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double 
     const int o0 = P * ez * S2 + P * ey * S + P * ex;
     double Y[D1][D1][D1];
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
-    elem_apply3d<D1, Q1, K, decltype(xl), Q1, AFF>(xl, qd + (size_t)b * (AFF ? 1 : NQ) * NC * kLanes, t, T, Y);
+    elem_apply3d_af<D1, Q1, K, AF>(xl, qd + (size_t)b * (AF ? 1 : NQ) * NC * kLanes, t, T, Y);
 
     // 3. deterministic E->L inside the brick: one local dof per step, all lanes distinct targets
 #pragma unroll
@@ -272,11 +272,14 @@ static hipError_t brick_launch(cdfem_ctx *c, const double *x, const double *dinv
     const BrickGeom g = geom_of(c);
     if (which & 1) {
         const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
-        if (c->d_qaff)
-            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, true>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv, d,
+        if (pa_af(c) == 2)
+            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 2>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv, d,
+                               y, c->d_face, c->d_qaff, c->d_ess, T, g, c->d_part, c->d_state);
+        else if (pa_af(c) == 1)
+            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 1>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv, d,
                                y, c->d_face, c->d_qaff, c->d_ess, T, g, c->d_part, c->d_state);
         else
-            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, false>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv, d,
+            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 0>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv, d,
                                y, c->d_face, c->d_qd, c->d_ess, T, g, c->d_part, c->d_state);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -345,8 +348,8 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // below, which owns it for the dot products (remote_lo / remote_hi carry the neighbours' partial
 // sums of the interface planes; nullptr on a single GPU).
 // ================================================================================================
-template <int D1, int Q1, unsigned K, bool AFF>
-__global__ void __launch_bounds__(64, 1)
+template <int D1, int Q1, unsigned K, int AF>
+__global__ void __launch_bounds__(64, AF == 2 ? 2 : 1)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
@@ -371,7 +374,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const int bx = b % g.nbx, by = (b / g.nbx) % g.nby;
     const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
     const bool lastx = bx == g.nbx - 1, lasty = by == g.nby - 1, lastz = bz == g.nbz - 1;
-    const double *q0 = qd + (size_t)b * (AFF ? 1 : NQ) * NC * kLanes;  // AFF: per-element factors
+    const double *q0 = qd + (size_t)b * (AF ? 1 : NQ) * NC * kLanes;  // AF: per-element factors
     double den = 0.0;
     // patch gather: every load of the patch is issued before any is consumed (clamped indices,
     // no branches between them): one memory latency per brick instead of one per patch row.
@@ -421,7 +424,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const int o0 = P * ez * S2 + P * ey * S + P * ex;
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
     double Y[D1][D1][D1];
-    elem_apply3d<D1, Q1, K, decltype(xl), Q1, AFF>(xl, q0, t, T, Y);
+    elem_apply3d_af<D1, Q1, K, AF>(xl, q0, t, T, Y);
 
     // element-wise den contribution d0_e . (A_e d0_e) and deterministic in-LDS E->L
 #pragma unroll
@@ -558,7 +561,7 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     else                                                                                                     \
         hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_>), grid, block, 0, run.s, r, dinv, d_old, d_new, q,    \
                            c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state)
-    if (c->d_qaff) { CDFEM_BCG(true); } else { CDFEM_BCG(false); }
+    if (pa_af(c) == 2) { CDFEM_BCG(2); } else if (pa_af(c) == 1) { CDFEM_BCG(1); } else { CDFEM_BCG(0); }
 #undef CDFEM_BCG
     return hipGetLastError();
 }

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -86,25 +87,36 @@ T *dalloc(size_t n)
 int nq_of(const cdfem_ctx *c, const Rule1D &r) { return c->dim == 3 ? r.q1 * r.q1 * r.q1 : r.q1 * r.q1; }
 
 // every element a parallelepiped: each vertex v (lexicographic, bit k = axis k) equals
-// v0 + sum_k bit_k (v_{2^k} - v0) to 1e-13 of the element's coordinate scale.  Then the multilinear
-// map is affine and its Jacobian is the edge matrix at every point (the PA setup's pa_affine form).
+// v0 + sum_k bit_k (v_{2^k} - v0) up to the rounding of those coordinates (32 ulp of the largest
+// coordinate magnitude) plus 1e-12 of the element's longest edge.  Then the multilinear map is
+// affine and its Jacobian is the edge matrix at every point (the PA setup's pa_affine form) to a
+// relative 1e-12 of the element (the tolerance was 1e-13 of max(|x|, edge), which for
+// small elements far from the origin admitted defects far larger than the element's own scale).
 static bool mesh_is_affine(int dim, int64_t ne, const double *V)
 {
     const int nv = 1 << dim;
+    const double eps = std::numeric_limits<double>::epsilon();
     for (int64_t e = 0; e < ne; ++e) {
         const double *X = V + (size_t)e * nv * dim;
-        double h = 0.0;  // scale: edge lengths and coordinate magnitudes (rounding of the sums)
+        double xmax = 0.0, hmax = 0.0;
         for (int v = 0; v < nv; ++v)
-            for (int i = 0; i < dim; ++i) h = std::max(h, std::fabs(X[v * dim + i]));
-        for (int k = 0; k < dim; ++k)
-            for (int i = 0; i < dim; ++i) h = std::max(h, std::fabs(X[(1 << k) * dim + i] - X[i]));
+            for (int i = 0; i < dim; ++i) xmax = std::max(xmax, std::fabs(X[v * dim + i]));
+        for (int k = 0; k < dim; ++k) {
+            double h2 = 0.0;
+            for (int i = 0; i < dim; ++i) {
+                const double d = X[(1 << k) * dim + i] - X[i];
+                h2 += d * d;
+            }
+            hmax = std::max(hmax, std::sqrt(h2));
+        }
+        const double tol = 32.0 * eps * xmax + 1e-12 * hmax;
         for (int v = 3; v < nv; ++v) {
             if ((v & (v - 1)) == 0) continue;  // the edge vertices themselves
             for (int i = 0; i < dim; ++i) {
                 double p = X[i];
                 for (int k = 0; k < dim; ++k)
                     if (v >> k & 1) p += X[(1 << k) * dim + i] - X[i];
-                if (std::fabs(p - X[v * dim + i]) > 1e-13 * h) return false;
+                if (std::fabs(p - X[v * dim + i]) > tol) return false;
             }
         }
     }
@@ -990,17 +1002,43 @@ int cdfem_check_shared(cdfem_ctx *c, const int64_t *l2g)
         if (!l2g) throw ArgError("l2g is null");
         const int nn = (int)c->nbr_rank.size();
         const int64_t ntot = nn ? c->nbr_off[nn] : 0;
-        if (ntot == 0) return CDFEM_OK;
+        if (nn == 0) return CDFEM_OK;
+        // 1. list lengths first: mismatched send / recv counts would hang RCCL or misread
+        //    the host buffers, so both ranks of a pair compare them before any id moves
+        std::vector<int64_t> off1(nn + 1);
+        std::vector<double> cs(nn), cr(nn);
+        for (int k = 0; k <= nn; ++k) off1[k] = k;
+        for (int k = 0; k < nn; ++k) cs[k] = (double)(c->nbr_off[k + 1] - c->nbr_off[k]);
+        double *d_a = nullptr, *d_b = nullptr;
+        HIPCHK(hipMalloc(&d_a, nn * sizeof(double)));
+        HIPCHK(hipMalloc(&d_b, nn * sizeof(double)));
+        HIPCHK(hipMemcpyAsync(d_a, cs.data(), nn * 8, hipMemcpyHostToDevice, c->stream));
+        comm_exchange_nbr_buf(c, off1, d_a, d_b, c->stream);
+        HIPCHK(hipMemcpyAsync(cr.data(), d_b, nn * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        (void)hipFree(d_a);
+        (void)hipFree(d_b);
+        for (int k = 0; k < nn; ++k)
+            if (cr[k] != cs[k])
+                throw ArgError("shared-dof list with rank " + std::to_string(c->nbr_rank[k]) + " has " +
+                               std::to_string((int64_t)cs[k]) + " entries here, " + std::to_string((int64_t)cr[k]) +
+                               " there");
+        // 2. the ids; an out-of-range id is reported after the exchange, so every rank stays in step
         std::vector<double> send((size_t)ntot), recv((size_t)ntot);
+        int64_t bad = -1;
         for (int64_t j = 0; j < ntot; ++j) {
             const int64_t g = l2g[c->h_sh_idx[j]];
-            if (g < 0 || g >= ((int64_t)1 << 53)) throw ArgError("global dof id out of range");
-            send[j] = (double)g;  // exact below 2^53
+            const bool ok = g >= 0 && g < ((int64_t)1 << 53);
+            if (!ok && bad < 0) bad = j;
+            send[j] = ok ? (double)g : -1.0;  // exact below 2^53
         }
         HIPCHK(hipMemcpyAsync(c->d_sh_send, send.data(), ntot * 8, hipMemcpyHostToDevice, c->stream));
         comm_exchange_nbr_buf(c, c->nbr_off, c->d_sh_send, c->d_sh_recv, c->stream);
         HIPCHK(hipMemcpyAsync(recv.data(), c->d_sh_recv, ntot * 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        if (bad >= 0)
+            throw ArgError("global dof id out of range: " + std::to_string(l2g[c->h_sh_idx[bad]]) +
+                           " (local dof " + std::to_string(c->h_sh_idx[bad]) + ")");
         for (int k = 0; k < nn; ++k)
             for (int64_t j = c->nbr_off[k]; j < c->nbr_off[k + 1]; ++j)
                 if (recv[j] != send[j])
@@ -1303,6 +1341,22 @@ static int fa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
                                            multi_rank(c) ? 0 : c->sell_mode, c->dim,
                                            xyz.empty() ? nullptr : xyz.data(), c->sell_window, c->spmv_lds,
                                            c->spmv_lpr);
+            if (P.lds_rows > 0) {
+                // the LDS-staged SpMV launches one block per window (rounded up to whole XCD ranges)
+                // and its CG form writes one partial per block: the grid must fit the partial slots
+                // (ADVICE r03).  Windows halve below their nominal size when halos are large, so the
+                // automatic choice falls back to the layout without LDS; an explicit one is refused.
+                const int64_t spw = P.lds_rows / (kLanes / std::max(1, P.lpr));
+                const int64_t nwin = ((int64_t)P.sptr.size() - 1 + spw - 1) / spw;
+                if (8 * ((nwin + 7) / 8) > kSpmvMaxBlocks) {
+                    if (c->spmv_lds >= 0)
+                        throw UnsupportedError("spmv_lds " + std::to_string(c->spmv_lds) + ": " +
+                                               std::to_string(nwin) + " LDS windows exceed the SpMV grid (" +
+                                               std::to_string(kSpmvMaxBlocks) + " blocks); use larger windows or 0");
+                    P = fa_build_pattern(c->h_dofs, c->ne, c->nd, c->nl, multi_rank(c) ? 0 : c->sell_mode,
+                                         c->dim, xyz.empty() ? nullptr : xyz.data(), c->sell_window, 0, 1);
+                }
+            }
             c->nnz = P.nnz;
             c->d_rowptr = dalloc<int32_t>(P.rowptr.size());
             c->d_cols = dalloc<int32_t>(P.cols.size());
@@ -1608,7 +1662,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
                 throw ArgError("sell_order must be 0..8 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton, 8 Morton LDS windows / auto)");
             c->sell_mode = value;
         } else if (k == "pa_affine") {  // read by cdfem_pa_setup
-            if (value != 0 && value != 1) throw ArgError("pa_affine must be 0 or 1");
+            if (value < 0 || value > 2) throw ArgError("pa_affine must be 0, 1 or 2");
             c->pa_affine = value;
         } else if (k == "spmv_lpr") {  // read when the FA pattern is built (once per mesh)
             if (value != 0 && value != 1 && value != 2 && value != 4) throw ArgError("spmv_lpr must be 0 (auto), 1, 2 or 4");
@@ -1697,6 +1751,18 @@ int cdfem_kernel_flops(cdfem_ctx *c, int k, double *flops)
         // Fields: value, plus the three reference derivatives when diffusion or convection is on.
         const int D = c->d1, Q = c->rule_op.q1;
         const bool kD = c->kinds & CDFEM_DIFFUSION, kC = c->kinds & CDFEM_CONVECTION, kM = c->kinds & CDFEM_MASS;
+        if (c->qlay == 0 && pa_af(c) == 2) {
+            // Kronecker form (pa_core.hpp elem_apply3d_kron), per input z plane: a length-n linear
+            // combination counts 2n - 1 flops, an accumulation into Y 2 per term
+            const bool kG = kD || kC;
+            auto lc = [](int n) { return n > 0 ? 2.0 * n - 1.0 : 0.0; };
+            const double x_row = lc(D) * (1 + 2 * kD + kG) + lc(kM + kD + kC) + 2 * lc(kD + kC);
+            double y_pt = lc(D) + (kG ? 2 * lc(D) + 1 : 0.0);
+            if (kD) y_pt += 6 * lc(D) + 2 + 2 + 1 + 2 + 3;
+            const double z_pt = 2.0 * (1 + 2 * kD + kG) * D;
+            *flops = (double)D * ((double)D * D * x_row + (double)D * D * (y_pt + z_pt)) * (double)c->ne;
+            return CDFEM_OK;
+        }
         const int g = (kD || kC) ? 1 : 0;
         double pt_fma = D * (1 + 3 * g) + D * (kD ? 4 : 1), pt_mul = 0.0;  // x contraction, transposed x
         if (kD) { pt_fma += 6; pt_mul += 3; }

@@ -241,7 +241,9 @@ struct cdfem_ctx {
     double *d_qd = nullptr;             // [nblk][nq][nc][64]
     double *d_qaff = nullptr;           // [nblk][nc][64] per-element factors of an affine mesh (qd = W_q * g)
     bool mesh_affine = false;           // every element a parallelepiped (checked at upload)
-    int pa_affine = 1;                  // set_option "pa_affine": 1 use the factors when the mesh allows
+    int pa_affine = 2;                  // set_option "pa_affine": when the mesh allows, 1 form the point data
+                                        // from the affine factors, 2 the Kronecker form of the same factors
+                                        // (3D p <= 2 applies; the p >= 3 tile apply takes 2 as 1); 0 stream
     double *d_Ye = nullptr;             // [nblk][nd][64]
     double *d_dinv = nullptr;           // Jacobi (constrained: ess -> 1)
     bool dinv_ready = false;
@@ -288,6 +290,9 @@ namespace cdfem {
 
 // the high-order tile apply forms the point data from the affine factors (ho_mfma keeps the stream)
 inline bool tile_affine(const cdfem_ctx *c) { return c->d_qaff != nullptr && c->ho_mfma == 0; }
+// the element core of the 3D p <= 2 applies (pa_core.hpp elem_apply3d_af): 0 per-point stream,
+// 1 point data from the affine factors, 2 Kronecker form of the factors
+inline int pa_af(const cdfem_ctx *c) { return c->d_qaff == nullptr ? 0 : (c->pa_affine == 2 ? 2 : 1); }
 
 // ---- kernel launchers (pa_kernels.hip) -------------------------------------------------------
 hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, const double *d_kmat_q, double kappa, double alpha,

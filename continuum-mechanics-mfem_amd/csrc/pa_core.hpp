@@ -13,6 +13,12 @@ struct Tab {
     double B[Q1][D1];
     double G[Q1][D1];
     double w[Q1];  // 1D rule weights (the affine-geometry apply forms W_q = (w_x w_y) w_z)
+    // the rule's 1D element matrices (the Kronecker form of the affine operator, elem_apply3d_kron):
+    // M1[i][j] = sum_q w_q B_qi B_qj, K1 = sum_q w_q G_qi G_qj, C1[i][j] = sum_q w_q B_qi G_qj
+    // (test value i, trial derivative j; its transpose is the test-derivative / trial-value factor)
+    double M1[D1][D1];
+    double K1[D1][D1];
+    double C1[D1][D1];
 };
 
 template <int D1, int Q1>
@@ -25,6 +31,18 @@ static Tab<D1, Q1> make_tab(const Rule1D &r)
             t.G[q][d] = r.G[q][d];
         }
     for (int q = 0; q < Q1; ++q) t.w[q] = r.wts[q];
+    for (int i = 0; i < D1; ++i)
+        for (int j = 0; j < D1; ++j) {
+            double m = 0.0, k = 0.0, c = 0.0;
+            for (int q = 0; q < Q1; ++q) {
+                m += r.wts[q] * r.B[q][i] * r.B[q][j];
+                k += r.wts[q] * r.G[q][i] * r.G[q][j];
+                c += r.wts[q] * r.B[q][i] * r.G[q][j];
+            }
+            t.M1[i][j] = m;
+            t.K1[i][j] = k;
+            t.C1[i][j] = c;
+        }
     return t;
 }
 
@@ -213,6 +231,144 @@ __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restr
                 }
     }
 
+}
+
+// Y = A_e X for one affine element with constant coefficients in its Kronecker form.  With the
+// Jacobian constant on the element the point data factor as W_q g_k (g = the 10 per-element factors
+// k_setup_qdata keeps, pa_affine), and the tensor rule's W_q = w_x w_y w_z separates, so every term
+// of the quadrature sum is a Kronecker product of the rule's 1D matrices (Tab::M1, K1, C1):
+//     term                 (z, y, x) factors           coefficient
+//     mass                 (M, M, M)                    s detJ
+//     D_aa                 K in axis a, M elsewhere     D_aa
+//     D_ab (a != b)        Ct in a, C in b, M else      D_ab (both orderings)
+//     convection c_b       C in axis b, M elsewhere     c_b
+// (C: trial derivative, test value; Ct = C^T: test derivative, trial value; K both; M neither).
+// A_e = sum_t g_t Fz (x) Fy (x) Fx is the same operator as the quadrature form to rounding (an
+// algebraic identity for any tensor rule, not an exactness argument).  Evaluated per input z plane
+// jz: x stage (M, K, C, Ct on the plane's rows), the per-element combinations, y stage into the four
+// z groups (M, K, C, Ct), z stage into Y.  At p = 2: 1.73 K FMA-class operations per element against
+// 4.3 K for the quadrature form (elem_apply3d<..., AFF>), 45 + 27 live doubles.
+template <int D1, int Q1, unsigned K, typename XL>
+__device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__restrict__ q0, int lane,
+                                                  const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
+{
+    using L = QLayout<K, 3>;
+    constexpr int NC = L::nc;
+    constexpr bool kD = L::kD, kC = L::kC, kM = L::kM, kG = L::kD || L::kC;
+    double g[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) g[k] = q0[k * kLanes + lane];
+    // D = [[g0 g1 g2] [g1 g3 g4] [g2 g4 g5]], c = g[oC..oC+2], s = g[oM]
+#pragma unroll
+    for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < D1; ++dx) Y[dz][dy][dx] = 0.0;
+
+#pragma unroll
+    for (int jz = 0; jz < D1; ++jz) {
+        // x stage of this input plane and the per-element combinations:
+        //   u1 = s M + D_xx K + c_x C,  u3 = D_xy Ct + c_y M,  u5 = D_xz Ct + c_z M  (applied along x)
+        double xm[D1][D1], xc[D1][D1], u1[D1][D1], u3[D1][D1], u5[D1][D1];
+#pragma unroll
+        for (int jy = 0; jy < D1; ++jy) {
+            double r[D1];
+#pragma unroll
+            for (int jx = 0; jx < D1; ++jx) r[jx] = xl(jz, jy, jx);
+#pragma unroll
+            for (int ix = 0; ix < D1; ++ix) {
+                double m = 0.0, k = 0.0, c = 0.0, ct = 0.0;
+#pragma unroll
+                for (int jx = 0; jx < D1; ++jx) {
+                    m += T.M1[ix][jx] * r[jx];
+                    if constexpr (kD) {
+                        k += T.K1[ix][jx] * r[jx];
+                        ct += T.C1[jx][ix] * r[jx];
+                    }
+                    if constexpr (kG) c += T.C1[ix][jx] * r[jx];
+                }
+                xm[jy][ix] = m;
+                xc[jy][ix] = c;
+                double a = 0.0;
+                if constexpr (kM) a = g[L::oM] * m;
+                if constexpr (kD) a += g[0] * k;
+                if constexpr (kC) a += g[L::oC] * c;
+                u1[jy][ix] = a;
+                if constexpr (kD && kC) {
+                    u3[jy][ix] = g[1] * ct + g[L::oC + 1] * m;
+                    u5[jy][ix] = g[2] * ct + g[L::oC + 2] * m;
+                } else if constexpr (kD) {
+                    u3[jy][ix] = g[1] * ct;
+                    u5[jy][ix] = g[2] * ct;
+                } else if constexpr (kC) {
+                    u3[jy][ix] = g[L::oC + 1] * m;
+                    u5[jy][ix] = g[L::oC + 2] * m;
+                }
+            }
+        }
+        // y stage into the z groups, then the z stage
+#pragma unroll
+        for (int iy = 0; iy < D1; ++iy)
+#pragma unroll
+            for (int ix = 0; ix < D1; ++ix) {
+                double pm = 0.0, pk = 0.0, pc = 0.0, pct = 0.0;
+                {
+                    double s1 = 0.0;
+#pragma unroll
+                    for (int jy = 0; jy < D1; ++jy) s1 += T.M1[iy][jy] * u1[jy][ix];
+                    pm = s1;
+                }
+                if constexpr (kG) {
+                    double s3 = 0.0, s5 = 0.0;
+#pragma unroll
+                    for (int jy = 0; jy < D1; ++jy) {
+                        s3 += T.C1[iy][jy] * u3[jy][ix];
+                        s5 += T.M1[iy][jy] * u5[jy][ix];
+                    }
+                    pm += s3;
+                    pc = s5;
+                }
+                if constexpr (kD) {
+                    double kym = 0.0, ctyc = 0.0, mym = 0.0, ctym = 0.0, myc = 0.0, cym = 0.0;
+#pragma unroll
+                    for (int jy = 0; jy < D1; ++jy) {
+                        kym += T.K1[iy][jy] * xm[jy][ix];
+                        ctyc += T.C1[jy][iy] * xc[jy][ix];
+                        mym += T.M1[iy][jy] * xm[jy][ix];
+                        ctym += T.C1[jy][iy] * xm[jy][ix];
+                        myc += T.M1[iy][jy] * xc[jy][ix];
+                        cym += T.C1[iy][jy] * xm[jy][ix];
+                    }
+                    pm += g[3] * kym;
+                    pm += g[1] * ctyc;
+                    pk = g[5] * mym;
+                    pc += g[4] * ctym;
+                    pct = g[2] * myc + g[4] * cym;
+                }
+#pragma unroll
+                for (int iz = 0; iz < D1; ++iz) {
+                    double y = Y[iz][iy][ix];
+                    y += T.M1[iz][jz] * pm;
+                    if constexpr (kD) {
+                        y += T.K1[iz][jz] * pk;
+                        y += T.C1[jz][iz] * pct;
+                    }
+                    if constexpr (kG) y += T.C1[iz][jz] * pc;
+                    Y[iz][iy][ix] = y;
+                }
+            }
+    }
+}
+
+// the element core of the apply kernels by affine form: AF 0 per-point stream, 1 point data formed
+// from the affine factors (elem_apply3d<..., AFF>), 2 the Kronecker form of the same factors
+template <int D1, int Q1, unsigned K, int AF, typename XL>
+__device__ __forceinline__ void elem_apply3d_af(const XL &xl, const double *__restrict__ q0, int lane,
+                                                const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
+{
+    if constexpr (AF == 2) elem_apply3d_kron<D1, Q1, K>(xl, q0, lane, T, Y);
+    else elem_apply3d<D1, Q1, K, XL, Q1, AF == 1>(xl, q0, lane, T, Y);
 }
 
 // exact unsigned division by a run-time divisor: n / d == (n * m) >> k for n < 2^31

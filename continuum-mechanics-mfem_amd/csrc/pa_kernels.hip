@@ -22,7 +22,7 @@ namespace cdfem {
 // ------------------------------------------------------------------------------------------------
 // 3D apply: Ye = A_e x_e for every element (thread per element)
 // ------------------------------------------------------------------------------------------------
-template <int D1, int Q1, unsigned K, bool CON, bool AFF>
+template <int D1, int Q1, unsigned K, bool CON, int AF>
 __global__ void __launch_bounds__(256)
 k_apply3d(const int32_t *__restrict__ map, const double *__restrict__ x,
           const double *__restrict__ qd, double *__restrict__ Ye, const Tab<D1, Q1> T,
@@ -56,10 +56,10 @@ k_apply3d(const int32_t *__restrict__ map, const double *__restrict__ x,
             }
 
     double Y[D1][D1][D1];
-    // AFF: qd holds the block's affine factors [NC][kLanes] (pa_affine), else the per-point stream
-    const double *q0 = qd + (size_t)b * (AFF ? 1 : NQ) * NC * kLanes;
+    // AF: qd holds the block's affine factors [NC][kLanes] (pa_affine), else the per-point stream
+    const double *q0 = qd + (size_t)b * (AF ? 1 : NQ) * NC * kLanes;
     auto xl = [&](int dz, int dy, int dx) { return X[dz][dy][dx]; };
-    elem_apply3d<D1, Q1, K, decltype(xl), Q1, AFF>(xl, q0, lane, T, Y);
+    elem_apply3d_af<D1, Q1, K, AF>(xl, q0, lane, T, Y);
 
     double *yp = Ye + (size_t)b * ND * kLanes + lane;
 #pragma unroll
@@ -841,20 +841,17 @@ static hipError_t apply_kinds(cdfem_ctx *c, const double *x, double *Ye, bool co
     const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
     const dim3 grid(grid_for(c->nblk, 4)), block(256);
     if constexpr (DIM == 3) {
-        const bool aff = c->d_qaff != nullptr;
-        const double *qd = aff ? c->d_qaff : c->d_qd;
-        if (con && aff)
-            hipLaunchKernelGGL((k_apply3d<D1, Q1, K, true, true>), grid, block, 0, c->stream, c->d_map, x,
-                               qd, Ye, T, c->nblk, st);
-        else if (con)
-            hipLaunchKernelGGL((k_apply3d<D1, Q1, K, true, false>), grid, block, 0, c->stream, c->d_map, x,
-                               qd, Ye, T, c->nblk, st);
-        else if (aff)
-            hipLaunchKernelGGL((k_apply3d<D1, Q1, K, false, true>), grid, block, 0, c->stream, c->d_map,
-                               x, qd, Ye, T, c->nblk, st);
-        else
-            hipLaunchKernelGGL((k_apply3d<D1, Q1, K, false, false>), grid, block, 0, c->stream, c->d_map,
-                               x, qd, Ye, T, c->nblk, st);
+        const int af = pa_af(c);
+        const double *qd = af ? c->d_qaff : c->d_qd;
+#define CDFEM_A3(CON_, AF_)                                                                                  \
+    hipLaunchKernelGGL((k_apply3d<D1, Q1, K, CON_, AF_>), grid, block, 0, c->stream, c->d_map, x, qd, Ye, T, \
+                       c->nblk, st)
+        if (con) {
+            if (af == 2) CDFEM_A3(true, 2); else if (af == 1) CDFEM_A3(true, 1); else CDFEM_A3(true, 0);
+        } else {
+            if (af == 2) CDFEM_A3(false, 2); else if (af == 1) CDFEM_A3(false, 1); else CDFEM_A3(false, 0);
+        }
+#undef CDFEM_A3
     } else {
         if (con)
             hipLaunchKernelGGL((k_apply2d<D1, Q1, K, true>), grid, block, 0, c->stream, c->d_map, x,

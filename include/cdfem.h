@@ -241,13 +241,21 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *            v_mfma_f64_16x16x4_f64, bit 0 = stage x, 1 = y, 2 = y^T, 3 = x^T; the masks 1, 3, 8, 9
  *            and 15 are built (results agree to rounding; the north star's MFMA alternative,
  *            measured even to slower).
- * "pa_affine": 1 (default) — read by cdfem_pa_setup: on a mesh whose elements are all
- *              parallelepipeds (checked at upload) with constant coefficients and the block layout
- *              (p <= 2), the Jacobian is the element's edge matrix, every point value is stored as
- *              W_q * g_e, and the structured brick kernels form it from the 10 per-element factors
- *              g_e instead of streaming the per-point data (the same operator bit for bit between the
- *              two forms; against the per-point multilinear-map setup, to rounding); 0 = the
- *              per-point map and stream everywhere.
+ * "pa_affine": 2 (default) — read by cdfem_pa_setup: on a mesh whose elements are all
+ *              parallelepipeds (checked at upload: every vertex within 32 ulp of the coordinates plus
+ *              1e-12 of the element's longest edge of v0 + sum of the edge vectors) with constant
+ *              coefficients, the Jacobian is the element's edge matrix, the per-point data are stored
+ *              as W_q * g_e (so the diagonal and the 2D / FA paths see the same operator), and the
+ *              3D applies read the 10 per-element factors g_e instead of the per-point stream:
+ *                2 — the structured brick kernels (p <= 2, CG and Mult) and the generic 3D
+ *                    element-block apply (p <= 2) apply the factors in their Kronecker form
+ *                    (1D rule matrices M, K, C per axis, pa_core.hpp elem_apply3d_kron);
+ *                1 — the same applies form each point's data W_q * g_e from the factors;
+ *                the p >= 3 tile apply forms the point data from the factors under 1 and 2 (and
+ *                streams them when "ho_mfma" is non-zero).  The 2D applies always stream the per-point
+ *                data.  All forms apply the operator of the per-point multilinear-map setup to rounding
+ *                (the Kronecker form is an algebraic identity of the tensor rule, not an exactness
+ *                argument); 0 = the per-point map and stream everywhere.
  * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).
@@ -296,7 +304,8 @@ int cdfem_profile_read(cdfem_ctx *ctx, int kernel, double *total_ms, int64_t *co
 /* algorithmic bytes moved by one launch of kernel id (see DESIGN.md for the per-unit figures) */
 int cdfem_kernel_bytes(cdfem_ctx *ctx, int kernel, double *bytes);
 /* algorithmic f64 flops of one launch of the 3D partial-assembly apply (CDFEM_K_APPLY; FMA = 2):
- * the sum-factorized element apply, plus the point data W_q * g_e under pa_affine */
+ * the sum-factorized element apply (plus the point data W_q * g_e under pa_affine 1), or the
+ * Kronecker-form element apply under pa_affine 2                                 */
 int cdfem_kernel_flops(cdfem_ctx *ctx, int kernel, double *flops);
 /* the HIP kernel name (without template arguments) kernel id runs as in the current configuration,
  * as rocprof reports it: the assembled-operator apply (CDFEM_K_APPLY after cdfem_fa_setup) only   */

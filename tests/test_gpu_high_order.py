@@ -316,7 +316,7 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
             out[aff] = dict(y=gpu_ctx.mult(x), yc=gpu_ctx.mult(x, constrained=True), dg=gpu_ctx.diagonal(),
                             bytes=gpu_ctx.kernel_bytes(cdfem.K_APPLY), x=xg, it=ig["iterations"])
     finally:
-        gpu_ctx.set_option("pa_affine", 1)
+        gpu_ctx.set_option("pa_affine", 2)
     yo = A.mult(x)
     assert out[1]["bytes"] < out[0]["bytes"]
     assert np.abs(out[1]["y"] - yo).max() <= 1e-13 * np.abs(yo).max()

@@ -411,7 +411,7 @@ def test_brick_affine_factors(gpu_ctx, n, p, kinds):
                                                 max_iter=30)
             assert info["iterations"] == 30
     finally:
-        gpu_ctx.set_option("pa_affine", 1)
+        gpu_ctx.set_option("pa_affine", 2)
     assert out[1]["bytes"] < out[0]["bytes"]
     assert _relmax(out[1]["y"], A.mult(x)) <= MULT_TOL
     assert _relmax(out[1]["dg"], A.diag()) <= MULT_TOL
@@ -519,7 +519,7 @@ def test_generic_affine_factors(gpu_ctx, n, p, kinds):
             out[aff] = dict(y=gpu_ctx.mult(x), yc=gpu_ctx.mult(x, constrained=True), x=xg,
                             bytes=gpu_ctx.kernel_bytes(cdfem.K_APPLY))
     finally:
-        gpu_ctx.set_option("pa_affine", 1)
+        gpu_ctx.set_option("pa_affine", 2)
     assert out[1]["bytes"] < out[0]["bytes"]
     assert _relmax(out[1]["y"], A.mult(x)) <= MULT_TOL
     for k in ("y", "yc"):

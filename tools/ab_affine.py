@@ -1,11 +1,12 @@
-"""Interleaved in-process A/B of the affine-factor brick apply (pa_affine 1) against the per-point
-qdata stream (pa_affine 0) on the C2 workload (64^3 hex p = 2, D + C + M), GPU box only.
+"""Interleaved in-process A/B of the affine-factor brick applies (pa_affine 2 Kronecker form, 1 point
+data from the factors) against the per-point qdata stream (pa_affine 0) on the C2 workload (64^3
+hex p = 2, D + C + M), GPU box only.
 
 Two contexts (pa_affine is read by pa_setup); per round each runs a fixed Jacobi-CG solve (apply
 launch time from the profiling events) and a fixed GMRES(30) solve.  Prints medians and the
 relative difference of the two contexts' iterates.
 
-    python tools/ab_affine.py [--rounds 5] [--iters 100] [--n 64]
+    python tools/ab_affine.py [--rounds 5] [--iters 100] [--n 64] [--forms 2,1,0]
 """
 import argparse
 import json
@@ -25,13 +26,14 @@ ap.add_argument("--iters", type=int, default=100)
 ap.add_argument("--gmres-iters", type=int, default=60)
 ap.add_argument("--n", type=int, default=64)
 ap.add_argument("--p", type=int, default=2)
+ap.add_argument("--forms", default="2,1,0")
 args = ap.parse_args()
 
 n = args.n
 mesh = cdfem.box_mesh(3, n, args.p, with_coords=False)
 b = np.random.default_rng(1).uniform(-1, 1, mesh.nl)
 runs = []
-for aff in (1, 0):
+for aff in [int(f) for f in args.forms.split(",")]:
     ctx = cdfem.Context(0)
     ctx.set_option("pa_affine", aff)
     ctx.upload_mesh(mesh).set_structured(n, n, n)
@@ -72,7 +74,8 @@ def rel(a, c):
 
 
 out = {"dofs": mesh.nl, "cg_iters": args.iters, "gmres_iters": args.gmres_iters,
-       "rel_diff_cg": rel(runs[0]["x_cg"], runs[1]["x_cg"]), "rel_diff_gmres": rel(runs[0]["x_gm"], runs[1]["x_gm"])}
+       "rel_diff_cg_vs_last": [rel(r["x_cg"], runs[-1]["x_cg"]) for r in runs],
+       "rel_diff_gmres_vs_last": [rel(r["x_gm"], runs[-1]["x_gm"]) for r in runs]}
 for r in runs:
     med = {k: float(np.median(r[k])) for k in ("cg_us", "apply_us", "upd_us", "gm_us")}
     med["apply_bytes"] = r["bytes"]
