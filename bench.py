@@ -519,6 +519,10 @@ def main():
     for _ in range(args.warmup):
         step()
     ctx.synchronize()
+    host_comm = world > 1 and args.comm == "host"
+    if host_comm:  # rehearsal: host seconds inside the communicator callbacks over the timed steps
+        for k in ctx.comm_stats:
+            ctx.comm_stats[k] = 0 if k.endswith("calls") else 0.0
     # timed region: the production path, no instrumentation
     barrier(pg)
     ctx.synchronize()
@@ -531,6 +535,17 @@ def main():
     barrier(pg)
     dt = time.perf_counter() - t0
     dt_max = allmax(pg, dt)
+    comm_timing = None
+    if host_comm:
+        cs = dict(ctx.comm_stats)
+        mine = {"rank": rank, "s_total": dt, "iters": iters,
+                "allreduce_us_per_iter": cs["allreduce_s"] / max(iters, 1) * 1e6,
+                "allreduce_calls_per_iter": cs["allreduce_calls"] / max(iters, 1),
+                "exchange_us_per_iter": cs["exchange_s"] / max(iters, 1) * 1e6,
+                "exchange_calls_per_iter": cs["exchange_calls"] / max(iters, 1),
+                "comm_share": (cs["allreduce_s"] + cs["exchange_s"]) / dt}
+        comm_timing = [None] * world
+        pg.all_gather_object(comm_timing, mine)
 
     # roofline of the dominant kernel (fused PA apply): a profiled pass of the same steps with HIP
     # events at the kernel's dispatch start / end on the library stream.  Event-bracketed launches
@@ -730,7 +745,8 @@ def main():
                        "series": "strong: fixed n^3 split into z-slabs" if args.config == "c5"
                                  else "weak: an n x n x n/8 slab per rank (SURVEY 8e)" if args.config == "c5w"
                                  else "weak: an n^3 slab per rank",
-                       **({"comm": args.comm, "comm_lib": comm_lib, "comm_ranks": comm_ranks} if world > 1 else {})},
+                       **({"comm": args.comm, "comm_lib": comm_lib, "comm_ranks": comm_ranks} if world > 1 else {}),
+                       **({"comm_host_timing": comm_timing} if comm_timing else {})},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if gm is not None:

@@ -43,32 +43,84 @@ __device__ __forceinline__ int brick_id(const BrickGeom &g)
     return (int)(x * q + (x < r ? x : r) + k);
 }
 
-// index of boundary position (a, b, c) of an S^3 patch in lexicographic order of the boundary set
+// index of boundary position (a, b, c) of an S^3 patch in lexicographic order of the boundary set;
+// selects instead of branches (the callers run it for every lane, faces or not)
 template <int S>
 __device__ __forceinline__ int face_index(int a, int b, int c)
 {
     constexpr int ring = 4 * S - 4;
-    if (c == 0) return a + S * b;
-    if (c == S - 1) return S * S + (S - 2) * ring + a + S * b;
-    const int base = S * S + (c - 1) * ring;
-    if (b == 0) return base + a;
-    if (b == S - 1) return base + S + 2 * (S - 2) + a;
-    return base + S + 2 * (b - 1) + (a == S - 1 ? 1 : 0);
+    const int cap = a + S * b;                                  // c == 0 / c == S - 1 plane
+    const int base = S * S + (c - 1) * ring;                    // ring plane c
+    const int mid = b == 0 ? a : b == S - 1 ? S + 2 * (S - 2) + a : S + 2 * (b - 1) + (a == S - 1 ? 1 : 0);
+    return c == 0 ? cap : c == S - 1 ? S * S + (S - 2) * ring + cap : base + mid;
 }
 
 template <int S>
 constexpr int face_count() { return 2 * S * S + (S - 2) * (4 * S - 4); }
 
-// MODE 0: y = A x;  MODE 1: y = A_c x (ConstrainedOperator);  MODE 2: CG-fused (x := r)
-// One wave per SIMD, unconstrained registers: 241.5 vs 272.2 us per C2 apply in the GMRES leg
-// against a two-waves-per-SIMD build (<= 256 registers, 124 B/lane of spills; tools/ab_gmres.py,
-// profiles/r02_ab_c2_gmres_brick_waves.txt).
+// v unchanged, but opaque to the optimiser: index arithmetic that depends on it cannot be hoisted
+// above this point (LLVM otherwise computes a later phase's per-position indices at kernel entry
+// and spills them across the element apply)
+__device__ __forceinline__ int opaque(int v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// In-LDS E->L schedule.  At P = 2 an element's local dof d lands on patch position 2e + d per axis,
+// so two (element, local dof) pairs meet on one position only if their local dofs agree mod 2: the
+// 27 local dofs split into 8 parity classes (dx & 1, dy & 1, dz & 1) of 8, 4, 4, 2, 4, 2, 2, 1 dofs
+// that never collide with each other, and round r adds member r of every class (8 rounds instead of
+// one dof per step, 27).  Member r of class cls (members in lexicographic order), -1 past the end.
+__host__ __device__ constexpr int e2l_member(int cls, int r)
+{
+    const int a = cls & 1, b = (cls >> 1) & 1, c = (cls >> 2) & 1;
+    const int nx = a ? 1 : 2, ny = b ? 1 : 2, nz = c ? 1 : 2;
+    if (r >= nx * ny * nz) return -1;
+    const int ix = r % nx, iy = (r / nx) % ny, iz = r / (nx * ny);
+    const int dx = a ? 1 : 2 * ix, dy = b ? 1 : 2 * iy, dz = c ? 1 : 2 * iz;
+    return dx + 3 * (dy + 3 * dz);
+}
+
+// s_out[o0 + patch offset of local dof] += Y for the 64 elements of a brick, deterministic order
+template <int D1, int S>
+__device__ __forceinline__ void brick_e2l(double *s_out, int o0, const double (&Y)[D1][D1][D1])
+{
+    constexpr int S2 = S * S;
+    if constexpr (D1 == 3) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+#pragma unroll
+            for (int cls = 0; cls < 8; ++cls) {
+                const int l = e2l_member(cls, r);
+                if (l < 0) continue;
+                const int dz = l / 9, dy = (l / 3) % 3, dx = l % 3;
+                s_out[o0 + dz * S2 + dy * S + dx] += Y[dz][dy][dx];
+            }
+            __syncthreads();
+        }
+    } else {
+        // P = 1: every pair of local dofs can meet (positions e + d), one dof per step
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+            for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < D1; ++dx) {
+                    s_out[o0 + dz * S2 + dy * S + dx] += Y[dz][dy][dx];
+                    __syncthreads();
+                }
+    }
+}
+
+// MODE 0: y = A x;  MODE 1: y = A_c x (ConstrainedOperator).  (The CG loop runs k_brick_cg.)
+// One wave per SIMD with the per-point stream, unconstrained registers: 241.5 vs 272.2 us per C2
+// apply in the GMRES leg against a two-waves-per-SIMD build (<= 256 registers, 124 B/lane of
+// spills; tools/ab_gmres.py, profiles/r02_ab_c2_gmres_brick_waves.txt); two with the Kronecker form.
 template <int D1, int Q1, unsigned K, int MODE, int AF>
 __global__ void __launch_bounds__(64, AF == 2 ? 2 : 1)
-k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double *__restrict__ d,
-          double *__restrict__ y, double *__restrict__ face, const double *__restrict__ qd,
-          const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g,
-          double *__restrict__ part, const KrylovState *__restrict__ st)
+k_brick3d(const double *__restrict__ x, double *__restrict__ y, double *__restrict__ face,
+          const double *__restrict__ qd, const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g)
 {
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
@@ -76,41 +128,36 @@ k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double 
     constexpr int F = face_count<S>();
     constexpr int NC = QLayout<K, 3>::nc;
     constexpr int NQ = Q1 * Q1 * Q1;
+    constexpr int NI = (S3 + 63) / 64;
     __shared__ double s_in[S3];
     __shared__ double s_out[S3];
 
-    double beta = 0.0;
-    if constexpr (MODE == 2) {
-        if (st->done) return;
-        beta = st->beta;
-    }
     const int t = threadIdx.x;
     const int b = blockIdx.x;
     const int bx = b % g.nbx, by = (b / g.nbx) % g.nby, bz = b / (g.nbx * g.nby);
     const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
+    const int Lx = g.Lx, Lxy = g.Lx * g.Ly;
 
     // 1. gather the input patch (zero outside the lattice and, when constrained, on ess dofs);
-    //    fully unrolled so all of a thread's loads are in flight together
+    //    every load issued before any is consumed
+    double xv[NI];
+    uint8_t ev[NI];
+    bool inv[NI];
 #pragma unroll
-    for (int k = 0; k < (S3 + 63) / 64; ++k) {
-        const int i = t + 64 * k;
-        if (i >= S3) break;
-        const int px = i % S, py = (i / S) % S, pz = i / S2;
+    for (int k = 0; k < NI; ++k) {
+        const unsigned i = t + 64 * k;
+        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
         const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-        double v = 0.0;
-        if (gx < g.Lx && gy < g.Ly && gz < g.Lz) {
-            const int64_t gid = gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz);
-            if constexpr (MODE == 2) {
-                const double dn = dinv[gid] * x[gid] + beta * d[gid];
-                const bool owned = px > 0 && px < S - 1 && py > 0 && py < S - 1 && pz > 0 && pz < S - 1;
-                if (owned) d[gid] = dn;  // no other brick's patch contains this dof
-                v = ess[gid] ? 0.0 : dn;
-            } else {
-                v = x[gid];
-                if (MODE == 1 && ess[gid]) v = 0.0;
-            }
-        }
-        s_in[i] = v;
+        inv[k] = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
+        const int gid = inv[k] ? gx + Lx * gy + Lxy * gz : 0;
+        xv[k] = x[gid];
+        ev[k] = MODE == 1 ? ess[gid] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const unsigned i = t + 64 * k;
+        if (k == NI - 1 && i >= S3) break;
+        s_in[i] = (inv[k] && !ev[k]) ? xv[k] : 0.0;
         s_out[i] = 0.0;
     }
     __syncthreads();
@@ -122,49 +169,32 @@ k_brick3d(const double *__restrict__ x, const double *__restrict__ dinv, double 
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
     elem_apply3d_af<D1, Q1, K, AF>(xl, qd + (size_t)b * (AF ? 1 : NQ) * NC * kLanes, t, T, Y);
 
-    // 3. deterministic E->L inside the brick: one local dof per step, all lanes distinct targets
-#pragma unroll
-    for (int dz = 0; dz < D1; ++dz)
-#pragma unroll
-        for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < D1; ++dx) {
-                const int o = o0 + dz * S2 + dy * S + dx;
-                s_out[o] += Y[dz][dy][dx];
-                __syncthreads();
-            }
+    // 3. deterministic E->L inside the brick (brick_e2l: all lanes of a step write distinct targets)
+    brick_e2l<D1, S>(s_out, o0, Y);
 
-    // 4. owned dofs -> y, face dofs -> partial buffer
-    double acc = 0.0;
+    // 4. owned dofs -> y (constrained: y = x on ess rows), face dofs -> this brick's partials
+    double *const fb = face + (size_t)b * F;
+    const unsigned to = (unsigned)opaque(t);
 #pragma unroll
-    for (int k = 0; k < (S3 + 63) / 64; ++k) {
-        const int i = t + 64 * k;
-        if (i >= S3) break;
-        const int px = i % S, py = (i / S) % S, pz = i / S2;
-        const double v = s_out[i];
+    for (int k = 0; k < NI; ++k) {
+        const unsigned i = to + 64 * k;
+        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
         const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
-        if (onface) {
-            face[(size_t)b * F + face_index<S>(px, py, pz)] = v;
-            continue;
-        }
         const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-        if (gx >= g.Lx || gy >= g.Ly || gz >= g.Lz) continue;
-        const int64_t gid = gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz);
-        if constexpr (MODE == 0) {
-            y[gid] = v;
-        } else if constexpr (MODE == 1) {
-            y[gid] = ess[gid] ? x[gid] : v;
-        } else {
-            const bool e = ess[gid] != 0;
-            const double dn = e ? d[gid] : s_in[i];  // this thread wrote d[gid] in step 1
-            const double q = e ? dn : v;
-            y[gid] = q;
-            acc += dn * q;
+        const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
+        if (in && !onface) {
+            const int gid = gx + Lx * gy + Lxy * gz;
+            const double v = s_out[i];
+            if constexpr (MODE == 0) y[gid] = v;
+            else y[gid] = ess[gid] ? x[gid] : v;
         }
     }
-    if constexpr (MODE == 2) {
-        acc = wave_sum(acc);
-        if (t == 0) part[b] = acc;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const unsigned i = to + 64 * k;
+        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
+        const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
+        if (i < S3 && onface) fb[face_index<S>(px, py, pz)] = s_out[i];
     }
 }
 
@@ -272,15 +302,13 @@ static hipError_t brick_launch(cdfem_ctx *c, const double *x, const double *dinv
     const BrickGeom g = geom_of(c);
     if (which & 1) {
         const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
-        if (pa_af(c) == 2)
-            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 2>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv, d,
-                               y, c->d_face, c->d_qaff, c->d_ess, T, g, c->d_part, c->d_state);
-        else if (pa_af(c) == 1)
-            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 1>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv, d,
-                               y, c->d_face, c->d_qaff, c->d_ess, T, g, c->d_part, c->d_state);
-        else
-            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 0>), dim3(c->nblk), dim3(64), 0, c->stream, x, dinv, d,
-                               y, c->d_face, c->d_qd, c->d_ess, T, g, c->d_part, c->d_state);
+#define CDFEM_B3(AF_, QD_)                                                                                    \
+    hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, AF_>), dim3(c->nblk), dim3(64), 0, c->stream, x, y, c->d_face, \
+                       QD_, c->d_ess, T, g)
+        if (pa_af(c) == 2) CDFEM_B3(2, c->d_qaff);
+        else if (pa_af(c) == 1) CDFEM_B3(1, c->d_qaff);
+        else CDFEM_B3(0, c->d_qd);
+#undef CDFEM_B3
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -354,7 +382,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
            const Tab<D1, Q1> T, const BrickGeom g, int zlo_shared, double *__restrict__ part,
-           const KrylovState *__restrict__ st)
+           const KrylovState *__restrict__ st, double *__restrict__ x)
 {
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
@@ -366,6 +394,10 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     __shared__ double s_out[S3];
     if (st->done) return;
     const double beta = st->beta;
+    // x-fold (x != nullptr, set_option "cg_xfold"): the previous iteration's x += alpha d_old, for
+    // the dofs this brick writes d_new for (each dof has exactly one writer brick); the update
+    // kernel then leaves x alone.  Bitwise the unfolded update (same fma on the same values).
+    const double alpha_prev = x ? st->alpha : 0.0;
     const int t = threadIdx.x;
     // launch-local brick -> global brick (a launch covers every g.bzs-th layer from g.bz0)
     const int bl = brick_id(g), nxy = g.nbx * g.nby;
@@ -380,42 +412,42 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     // no branches between them): one memory latency per brick instead of one per patch row.
     // Measured (tools/ab.py, in process): 241.1 vs 242.4 us per launch for the per-row form; the
     // other waves of the CU hide most of that latency.
+    // (the lattice index fits 32 bits: N_L < 2^31 on one context)
     constexpr int NI = (S3 + 63) / 64;
-    double rv[NI], mv[NI], ov[NI];
+    double rv[NI], mv[NI], ov[NI], xv[NI];
     uint8_t ev[NI];
-    int64_t gidv[NI];
+    int gidv[NI];
+    const int Lx = g.Lx, Lxy = g.Lx * g.Ly;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
-        const int i = t + 64 * k;
-        const int px = i % S, py = (i / S) % S, pz = i / S2;
+        const unsigned i = t + 64 * k;
+        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
         const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
         const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
-        const int64_t gid = in ? gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz) : 0;
+        const int gid = in ? gx + Lx * gy + Lxy * gz : 0;
         gidv[k] = in ? gid : -1;
         rv[k] = r[gid];
         mv[k] = dinv[gid];
         ov[k] = d_old[gid];
         ev[k] = ess[gid];
+        const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
+        xv[k] = (x && writer) ? x[gid] : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
-        const int i = t + 64 * k;
-        if (i >= S3) break;
-        const int px = i % S, py = (i / S) % S, pz = i / S2;
+        const unsigned i = t + 64 * k;
+        if (k == NI - 1 && i >= S3) break;
+        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
         const int gz = gz0 + pz;
-        double v = 0.0;
-        if (gidv[k] >= 0) {
-            const int64_t gid = gidv[k];
-            const double dn = mv[k] * rv[k] + beta * ov[k];
-            const bool e = ev[k] != 0;
-            const bool writer = (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
-            if (writer) {
-                d_new[gid] = dn;
-                if (e && !(zlo_shared && gz == 0)) den += dn * dn;  // (A_c d)_i = d_i on ess dofs
-            }
-            v = e ? 0.0 : dn;
-        }
-        s_in[i] = v;
+        const bool in = gidv[k] >= 0;
+        const double dn = mv[k] * rv[k] + beta * ov[k];
+        const bool e = ev[k] != 0;
+        const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
+        if (writer) d_new[gidv[k]] = dn;
+        if (x && writer) x[gidv[k]] = xv[k] + alpha_prev * ov[k];
+        // (A_c d)_i = d_i on ess dofs
+        den += (writer && e && !(zlo_shared && gz == 0)) ? dn * dn : 0.0;
+        s_in[i] = (in && !e) ? dn : 0.0;
         s_out[i] = 0.0;
     }
     __syncthreads();
@@ -432,32 +464,40 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
 #pragma unroll
         for (int dy = 0; dy < D1; ++dy)
 #pragma unroll
-            for (int dx = 0; dx < D1; ++dx) {
-                const int o = o0 + dz * S2 + dy * S + dx;
-                den += s_in[o] * Y[dz][dy][dx];
-                s_out[o] += Y[dz][dy][dx];
-                __syncthreads();
-            }
+            for (int dx = 0; dx < D1; ++dx) den += s_in[o0 + dz * S2 + dy * S + dx] * Y[dz][dy][dx];
+    brick_e2l<D1, S>(s_out, o0, Y);
 
+    // owned (patch-interior) rows -> q, face rows -> this brick's face partials; one store per
+    // position through a selected pointer (no divergent branches: the masks cost scalar registers)
+    double *const fb = face + (size_t)b * F;
+    const unsigned to = (unsigned)opaque(t);
+    double vv[NI];
 #pragma unroll
-    for (int k = 0; k < (S3 + 63) / 64; ++k) {
-        const int i = t + 64 * k;
-        if (i >= S3) break;
-        const int px = i % S, py = (i / S) % S, pz = i / S2;
-        const double v = s_out[i];
-        if (px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1) {
-            face[(size_t)b * F + face_index<S>(px, py, pz)] = v;
-            continue;
-        }
+    for (int k = 0; k < NI; ++k) vv[k] = (k < NI - 1 || to + 64 * k < S3) ? s_out[to + 64 * k] : 0.0;
+    // two predicated stores per position (patch-interior rows -> q, face rows -> this brick's face
+    // partials) instead of an if / else, which the compiler structurises into divergent branches
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const unsigned i = to + 64 * k;
+        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
+        const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
+        // the lattice index again (cheaper than keeping the gather's indices live through the apply)
         const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-        if (gx >= g.Lx || gy >= g.Ly || gz >= g.Lz) continue;
-        q[gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz)] = v;  // ess rows: replaced by d in the update
+        const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
+        if (in && !onface) q[gx + Lx * gy + Lxy * gz] = vv[k];  // ess rows: replaced by d in the update
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const unsigned i = to + 64 * k;
+        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
+        const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
+        if (i < S3 && onface) fb[face_index<S>(px, py, pz)] = vv[k];
     }
     den = wave_sum(den);
     if (t == 0) part[b] = den;
 }
 
-template <int S>
+template <int S, bool XF>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ q,
                   const double *__restrict__ d, const double *__restrict__ dinv,
@@ -495,7 +535,8 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         // every load is issued before any is consumed: which of q / the face partials holds this
         // dof's row sum depends on its lattice position only, and the essential flag selects last
         const bool is_ess = ess[gid] != 0;
-        const double di = d[gid], xi = x[gid];
+        // XF: x was advanced by the apply (x-fold); d is then needed on essential rows only
+        const double di = (!XF || is_ess) ? d[gid] : 0.0, xi = XF ? 0.0 : x[gid];
         const double rold = r[gid], mi = dinv[gid];
         double qi;
         if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
@@ -527,7 +568,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         if (remote_lo && gz == 0) qi += remote_lo[rem];
         if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
         if (is_ess) qi = di;
-        __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
+        if constexpr (!XF) __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
         const double ri = rold - alpha * qi;
         __builtin_nontemporal_store(ri, &r[gid]);
         if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
@@ -545,7 +586,7 @@ struct BrickRun {
 
 template <int D1, int Q1, unsigned K>
 static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *dinv,
-                                   const double *d_old, double *d_new, double *q, const BrickRun &run)
+                                   const double *d_old, double *d_new, double *q, const BrickRun &run, double *x)
 {
     const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
     BrickGeom g = geom_of(c);
@@ -557,28 +598,28 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
 #define CDFEM_BCG(AFF_)                                                                                      \
     if (whole)                                                                                               \
         CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_>), grid, block, 0, r, dinv, d_old, d_new, q, c->d_face, qd, \
-                     c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state);                                  \
+                     c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x);                               \
     else                                                                                                     \
         hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_>), grid, block, 0, run.s, r, dinv, d_old, d_new, q,    \
-                           c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state)
+                           c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x)
     if (pa_af(c) == 2) { CDFEM_BCG(2); } else if (pa_af(c) == 1) { CDFEM_BCG(1); } else { CDFEM_BCG(0); }
 #undef CDFEM_BCG
     return hipGetLastError();
 }
 
 static hipError_t brick_cg2_run(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                                double *d_new, double *q, const BrickRun &run)
+                                double *d_new, double *q, const BrickRun &run, double *x)
 {
     const int q1 = c->rule_op.q1;
 #define CDFEM_K(D1_, Q1_)                                                                           \
     switch (c->kinds) {                                                                             \
-    case 1: return brick_cg2_launch<D1_, Q1_, 1>(c, r, dinv, d_old, d_new, q, run);                 \
-    case 2: return brick_cg2_launch<D1_, Q1_, 2>(c, r, dinv, d_old, d_new, q, run);                 \
-    case 3: return brick_cg2_launch<D1_, Q1_, 3>(c, r, dinv, d_old, d_new, q, run);                 \
-    case 4: return brick_cg2_launch<D1_, Q1_, 4>(c, r, dinv, d_old, d_new, q, run);                 \
-    case 5: return brick_cg2_launch<D1_, Q1_, 5>(c, r, dinv, d_old, d_new, q, run);                 \
-    case 6: return brick_cg2_launch<D1_, Q1_, 6>(c, r, dinv, d_old, d_new, q, run);                 \
-    case 7: return brick_cg2_launch<D1_, Q1_, 7>(c, r, dinv, d_old, d_new, q, run);                 \
+    case 1: return brick_cg2_launch<D1_, Q1_, 1>(c, r, dinv, d_old, d_new, q, run, x);                 \
+    case 2: return brick_cg2_launch<D1_, Q1_, 2>(c, r, dinv, d_old, d_new, q, run, x);                 \
+    case 3: return brick_cg2_launch<D1_, Q1_, 3>(c, r, dinv, d_old, d_new, q, run, x);                 \
+    case 4: return brick_cg2_launch<D1_, Q1_, 4>(c, r, dinv, d_old, d_new, q, run, x);                 \
+    case 5: return brick_cg2_launch<D1_, Q1_, 5>(c, r, dinv, d_old, d_new, q, run, x);                 \
+    case 6: return brick_cg2_launch<D1_, Q1_, 6>(c, r, dinv, d_old, d_new, q, run, x);                 \
+    case 7: return brick_cg2_launch<D1_, Q1_, 7>(c, r, dinv, d_old, d_new, q, run, x);                 \
     default: return hipErrorInvalidValue;                                                           \
     }
     if (c->p == 1 && q1 == 3) { CDFEM_K(2, 3) }
@@ -588,25 +629,25 @@ static hipError_t brick_cg2_run(cdfem_ctx *c, const double *r, const double *din
 }
 
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                            double *d_new, double *q)
+                            double *d_new, double *q, double *x)
 {
-    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, 1, c->nbz, c->stream});
+    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, 1, c->nbz, c->stream}, x);
 }
 
 // the first and last brick layers (the shared planes' partial sums) on stream s, the interior
 // layers on the context stream; nbz >= 3
 hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                                  double *d_new, double *q, hipStream_t s)
+                                  double *d_new, double *q, hipStream_t s, double *x)
 {
     if (c->nbz < 3) return hipErrorInvalidValue;
-    const hipError_t e = brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, c->nbz - 1, 2, s});
+    const hipError_t e = brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, c->nbz - 1, 2, s}, x);
     if (e != hipSuccess) return e;
-    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{1, 1, c->nbz - 2, c->stream});
+    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{1, 1, c->nbz - 2, c->stream}, x);
 }
 
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
                                   const double *dinv, const double *remote_lo, const double *remote_hi,
-                                  bool den_step)
+                                  bool den_step, bool xfold)
 {
     const BrickGeom g = geom_of(c);
     const FastDiv fdx = make_fastdiv((uint32_t)c->Lx), fdxy = make_fastdiv((uint32_t)(c->Lx * c->Ly));
@@ -615,15 +656,21 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
     const unsigned grid = (unsigned)(need < 16384 ? need : 16384);
 #define CDFEM_UPD(S_)                                                                                       \
-    hipLaunchKernelGGL((k_cg_update_faces<S_>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, q, d, dinv, \
-                       c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, c->d_part,     \
-                       c->d_state, (int)den_step)
-    if (c->p == 1)
+    if (xfold)                                                                                              \
+        hipLaunchKernelGGL((k_cg_update_faces<S_, true>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, q, \
+                           d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi,     \
+                           c->d_part, c->d_state, (int)den_step);                                           \
+    else                                                                                                    \
+        hipLaunchKernelGGL((k_cg_update_faces<S_, false>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, \
+                           q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, \
+                           c->d_part, c->d_state, (int)den_step)
+    if (c->p == 1) {
         CDFEM_UPD(kBrick * 1 + 1);
-    else if (c->p == 2)
+    } else if (c->p == 2) {
         CDFEM_UPD(kBrick * 2 + 1);
-    else
+    } else {
         return hipErrorInvalidValue;
+    }
 #undef CDFEM_UPD
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -416,13 +416,21 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
         HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
         for (auto &e : c->ov_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
+    // x-fold (set_option "cg_xfold", default): every apply after the first advances x by the previous
+    // iteration's alpha d (the update kernel then streams neither x nor d); k_cg_xflush adds the
+    // last update's term after the loop when the update logic stopped the solve
+    const bool xfold = c->cg_xfold != 0;
+    double *const dbuf0 = dcur, *const dbuf1 = dprev;  // apply j writes d_j into dbuf[(j - 1) & 1]
+    int napply = 0;
     auto apply = [&] {
+        double *xf = (xfold && napply > 0) ? x : nullptr;
+        ++napply;
         if (overlap) {
             HIPCHK(hipEventRecord(c->ov_ev[0], c->stream));
             HIPCHK(hipStreamWaitEvent(c->stream2, c->ov_ev[0], 0));
             // boundary layers on the side stream, interior layers queued on the main stream
             // before the (possibly host-blocking) exchange is issued
-            HIPCHK(launch_brick_cg2_split(c, r, dinv, dprev, dcur, q, c->stream2));
+            HIPCHK(launch_brick_cg2_split(c, r, dinv, dprev, dcur, q, c->stream2, xf));
             HIPCHK(launch_pack_qplanes(c, q, c->stream2));
             comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], c->Lx * c->Ly, c->stream2);
             HIPCHK(hipEventRecord(c->ov_ev[1], c->stream2));
@@ -432,7 +440,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             return;
         }
         prof_mark(c, CDFEM_K_APPLY, true);
-        HIPCHK(launch_brick_cg2(c, r, dinv, dprev, dcur, q));
+        HIPCHK(launch_brick_cg2(c, r, dinv, dprev, dcur, q, xf));
         prof_mark(c, CDFEM_K_APPLY, false);
         prof_mark(c, CDFEM_K_E2L, true);
         if (mr) {
@@ -453,7 +461,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             prof_mark(c, CDFEM_K_UPDATE, true);
             HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv,
                                           mr && c->zlo_shared ? c->d_if[1] : nullptr,
-                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr));
+                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr, xfold));
             if (mr) {
                 comm_allreduce(c, red + 1, 1);
                 HIPCHK(launch_update_step(c));
@@ -466,6 +474,10 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (c->h_state->done || launched >= p.max_iter) break;
+    }
+    if (xfold) {
+        HIPCHK(launch_cg_xflush(c, x, dbuf0, dbuf1));
+        HIPCHK(hipStreamSynchronize(c->stream));
     }
     const auto t1 = std::chrono::steady_clock::now();
     prof_collect(c);
@@ -1654,6 +1666,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value != 0 && value != 1 && value != 3 && value != 8 && value != 9 && value != 15)
                 throw ArgError("ho_mfma must be 0, 1, 3, 8, 9 or 15");
             c->ho_mfma = value;
+        } else if (k == "cg_xfold") {
+            if (value != 0 && value != 1) throw ArgError("cg_xfold must be 0 or 1");
+            c->cg_xfold = value;
         } else if (k == "cg_fused") {
             if (value < 0 || value > 1) throw ArgError("cg_fused must be 0 or 1");
             c->cg_fused = value;

@@ -73,6 +73,8 @@ struct KrylovState {
     double nom, nom0, den, alpha, beta, betanom, r0;
     double red[4];  // rank-local reductions awaiting the all-reduce (0 den, 1 betanom, 2 nom)
     int iter, done, converged, final_iter, max_iter, first_den;
+    int xflush;     // x-fold CG (cg_xfold): the last update's x += alpha d is still pending (stopped by
+                    // the update logic, so no further apply folded it): k_cg_xflush applies it
 };
 
 // Device-side GMRES(m) state (gmres.hip).  The first 32 bytes are what the host polls.
@@ -214,6 +216,7 @@ struct cdfem_ctx {
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
+    int cg_xfold = 1;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 8;                  // set_option "sell_order" (read when the FA pattern is built)
     int sell_window = 0;                // set_option "sell_window": rows per window of a windowed order (0 auto)
@@ -339,11 +342,14 @@ hipError_t launch_den_fin(cdfem_ctx *c, int nparts);
 hipError_t launch_update_fin(cdfem_ctx *c, int nparts);
 // brick CG v2 (brick_kernels.hip): d_new = M^{-1} r + beta d_old, q/face partials, den partials
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                            double *d_new, double *q);
+                            double *d_new, double *q, double *x = nullptr);
+// x-fold CG after the loop: x += alpha d_m when the last update's x term is still pending
+// (d_m in dbuf[(m - 1) & 1], m = the final iteration)
+hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *d0, const double *d1);
 // q from interior/face partials (+ remote interface sums), x += alpha d, r -= alpha q, betanom
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
                                   const double *dinv, const double *remote_lo, const double *remote_hi,
-                                  bool den_step = false);
+                                  bool den_step = false, bool xfold = false);
 // generic deterministic dot into host-visible scalar via state (used by GMRES / tests)
 hipError_t launch_dot(cdfem_ctx *c, const double *a, const double *b, double *d_out);
 // multi-rank CG: rank-local (d, q) over owned entries into the state's den slot (all-reduce next)
@@ -372,7 +378,7 @@ hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double
 // pack the local partial sums of q on the shared interface planes into d_if[0] / d_if[2]
 hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q, hipStream_t s = nullptr);
 hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                                  double *d_new, double *q, hipStream_t s);
+                                  double *d_new, double *q, hipStream_t s, double *x = nullptr);
 
 // ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
 // full assembly on simplices (fa_kernels.hip)

@@ -21,6 +21,28 @@ struct Tab {
     double C1[D1][D1];
 };
 
+// Symmetry of the 1D matrices: the rule's points and weights and the GLL nodes are symmetric about
+// the centre, so B[Q-1-q][D-1-i] = B[q][i] and G[Q-1-q][D-1-i] = -G[q][i]; M and K are then symmetric
+// and centro-symmetric, C is centro-antisymmetric (C[D-1-i][D-1-j] = -C[i][j], its centre entry 0).
+// make_tab averages each orbit into its canonical entry and the Kronecker core reads only those, so
+// only the distinct values (4 + 4 + 4 at p = 2) occupy scalar registers.
+__host__ __device__ constexpr int sym_can(int D, int i, int j)
+{
+    const int a = i * D + j, b = j * D + i, c = (D - 1 - i) * D + (D - 1 - j), d = (D - 1 - j) * D + (D - 1 - i);
+    const int m1 = a < b ? a : b, m2 = c < d ? c : d;
+    return m1 < m2 ? m1 : m2;
+}
+__host__ __device__ constexpr int anti_can(int D, int i, int j)
+{
+    const int a = i * D + j, c = (D - 1 - i) * D + (D - 1 - j);
+    return a < c ? a : c;
+}
+__host__ __device__ constexpr int anti_sign(int D, int i, int j)
+{
+    const int a = i * D + j, c = (D - 1 - i) * D + (D - 1 - j);
+    return a == c ? 0 : (a < c ? 1 : -1);
+}
+
 template <int D1, int Q1>
 static Tab<D1, Q1> make_tab(const Rule1D &r)
 {
@@ -43,7 +65,38 @@ static Tab<D1, Q1> make_tab(const Rule1D &r)
             t.K1[i][j] = k;
             t.C1[i][j] = c;
         }
-    return t;
+    // the orbit averages (the canonical entries the Kronecker core reads)
+    Tab<D1, Q1> u = t;
+    for (int i = 0; i < D1; ++i)
+        for (int j = 0; j < D1; ++j) {
+            const int a = D1 - 1 - i, b = D1 - 1 - j;
+            u.M1[i][j] = 0.25 * ((t.M1[i][j] + t.M1[j][i]) + (t.M1[a][b] + t.M1[b][a]));
+            u.K1[i][j] = 0.25 * ((t.K1[i][j] + t.K1[j][i]) + (t.K1[a][b] + t.K1[b][a]));
+            u.C1[i][j] = 0.5 * (t.C1[i][j] - t.C1[a][b]);
+        }
+    return u;
+}
+
+// the canonical entries of the 1D matrices (compile-time indices after unrolling)
+template <int D1, int Q1>
+__device__ __forceinline__ double tM(const Tab<D1, Q1> &T, int i, int j)
+{
+    const int k = sym_can(D1, i, j);
+    return T.M1[k / D1][k % D1];
+}
+template <int D1, int Q1>
+__device__ __forceinline__ double tK(const Tab<D1, Q1> &T, int i, int j)
+{
+    const int k = sym_can(D1, i, j);
+    return T.K1[k / D1][k % D1];
+}
+// acc + C[i][j] x (the centre entry is structurally zero and adds nothing)
+template <int D1, int Q1>
+__device__ __forceinline__ double tCacc(const Tab<D1, Q1> &T, int i, int j, double x, double acc)
+{
+    const int s = anti_sign(D1, i, j), k = anti_can(D1, i, j);
+    if (s == 0) return acc;
+    return s > 0 ? acc + T.C1[k / D1][k % D1] * x : acc - T.C1[k / D1][k % D1] * x;
 }
 
 // qdata component layout for a kinds mask: [D (sym) | C (dim) | M]
@@ -281,12 +334,12 @@ __device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__
                 double m = 0.0, k = 0.0, c = 0.0, ct = 0.0;
 #pragma unroll
                 for (int jx = 0; jx < D1; ++jx) {
-                    m += T.M1[ix][jx] * r[jx];
+                    m += tM(T, ix, jx) * r[jx];
                     if constexpr (kD) {
-                        k += T.K1[ix][jx] * r[jx];
-                        ct += T.C1[jx][ix] * r[jx];
+                        k += tK(T, ix, jx) * r[jx];
+                        ct = tCacc(T, jx, ix, r[jx], ct);
                     }
-                    if constexpr (kG) c += T.C1[ix][jx] * r[jx];
+                    if constexpr (kG) c = tCacc(T, ix, jx, r[jx], c);
                 }
                 xm[jy][ix] = m;
                 xc[jy][ix] = c;
@@ -316,15 +369,15 @@ __device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__
                 {
                     double s1 = 0.0;
 #pragma unroll
-                    for (int jy = 0; jy < D1; ++jy) s1 += T.M1[iy][jy] * u1[jy][ix];
+                    for (int jy = 0; jy < D1; ++jy) s1 += tM(T, iy, jy) * u1[jy][ix];
                     pm = s1;
                 }
                 if constexpr (kG) {
                     double s3 = 0.0, s5 = 0.0;
 #pragma unroll
                     for (int jy = 0; jy < D1; ++jy) {
-                        s3 += T.C1[iy][jy] * u3[jy][ix];
-                        s5 += T.M1[iy][jy] * u5[jy][ix];
+                        s3 = tCacc(T, iy, jy, u3[jy][ix], s3);
+                        s5 += tM(T, iy, jy) * u5[jy][ix];
                     }
                     pm += s3;
                     pc = s5;
@@ -333,12 +386,12 @@ __device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__
                     double kym = 0.0, ctyc = 0.0, mym = 0.0, ctym = 0.0, myc = 0.0, cym = 0.0;
 #pragma unroll
                     for (int jy = 0; jy < D1; ++jy) {
-                        kym += T.K1[iy][jy] * xm[jy][ix];
-                        ctyc += T.C1[jy][iy] * xc[jy][ix];
-                        mym += T.M1[iy][jy] * xm[jy][ix];
-                        ctym += T.C1[jy][iy] * xm[jy][ix];
-                        myc += T.M1[iy][jy] * xc[jy][ix];
-                        cym += T.C1[iy][jy] * xm[jy][ix];
+                        kym += tK(T, iy, jy) * xm[jy][ix];
+                        ctyc = tCacc(T, jy, iy, xc[jy][ix], ctyc);
+                        mym += tM(T, iy, jy) * xm[jy][ix];
+                        ctym = tCacc(T, jy, iy, xm[jy][ix], ctym);
+                        myc += tM(T, iy, jy) * xc[jy][ix];
+                        cym = tCacc(T, iy, jy, xm[jy][ix], cym);
                     }
                     pm += g[3] * kym;
                     pm += g[1] * ctyc;
@@ -349,12 +402,12 @@ __device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__
 #pragma unroll
                 for (int iz = 0; iz < D1; ++iz) {
                     double y = Y[iz][iy][ix];
-                    y += T.M1[iz][jz] * pm;
+                    y += tM(T, iz, jz) * pm;
                     if constexpr (kD) {
-                        y += T.K1[iz][jz] * pk;
-                        y += T.C1[jz][iz] * pct;
+                        y += tK(T, iz, jz) * pk;
+                        y = tCacc(T, jz, iz, pct, y);
                     }
-                    if constexpr (kG) y += T.C1[iz][jz] * pc;
+                    if constexpr (kG) y = tCacc(T, iz, jz, pc, y);
                     Y[iz][iy][ix] = y;
                 }
             }

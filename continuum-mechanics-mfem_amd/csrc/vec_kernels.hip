@@ -259,6 +259,7 @@ __device__ inline void cg_init_logic(KrylovState *st, double nom, double rel_tol
     st->done = 0;
     st->first_den = 1;  // next den is the initial one
     st->beta = 0.0;
+    st->xflush = 0;
     if (nom < 0.0) {             // preconditioner not positive definite
         st->done = 1;
         st->final_iter = 0;
@@ -275,11 +276,11 @@ __device__ inline void cg_update_logic(KrylovState *st, double betanom)
     st->betanom = betanom;
     const int i = st->iter;
     if (betanom < 0.0) {
-        st->done = 1; st->converged = 0; st->final_iter = i;
+        st->done = 1; st->converged = 0; st->final_iter = i; st->xflush = 1;
     } else if (betanom <= st->r0) {
-        st->done = 1; st->converged = 1; st->final_iter = i;
+        st->done = 1; st->converged = 1; st->final_iter = i; st->xflush = 1;
     } else if (i + 1 > st->max_iter) {
-        st->done = 1; st->converged = 0; st->final_iter = st->max_iter;
+        st->done = 1; st->converged = 0; st->final_iter = st->max_iter; st->xflush = 1;
     } else {
         st->beta = betanom / st->nom;
         st->iter = i + 1;
@@ -383,6 +384,18 @@ k_cg_update_fin(const double *__restrict__ part, int n, KrylovState *__restrict_
     if (threadIdx.x == 0) cg_update_logic(st, betanom);
 }
 
+// x-fold CG, after the loop: the last executed update's x += alpha_m d_m (no apply folded it)
+__global__ void __launch_bounds__(kRedThreads)
+k_cg_xflush(double *__restrict__ x, const double *__restrict__ d0, const double *__restrict__ d1, int64_t n,
+            const KrylovState *__restrict__ st)
+{
+    if (!st->xflush) return;
+    const double *__restrict__ d = ((st->final_iter - 1) & 1) ? d1 : d0;
+    const double alpha = st->alpha;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] += alpha * d[i];
+}
+
 // d = z + beta d
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_direction(const double *__restrict__ z, double *__restrict__ d, int64_t n,
@@ -469,6 +482,13 @@ static inline unsigned red_grid(cdfem_ctx *c, int64_t n)
 hipError_t launch_den_fin(cdfem_ctx *c, int nparts)
 {
     hipLaunchKernelGGL(k_cg_den_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, nparts, c->d_state);
+    return hipGetLastError();
+}
+
+hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *d0, const double *d1)
+{
+    hipLaunchKernelGGL(k_cg_xflush, dim3(red_grid(c, c->nl)), dim3(kRedThreads), 0, c->stream, x, d0, d1, c->nl,
+                       c->d_state);
     return hipGetLastError();
 }
 

@@ -567,9 +567,14 @@ class Context:
         """Host-callback communicator over torch.distributed (any backend, e.g. gloo)."""
         import torch
         import torch.distributed as dist
+        import time
         rank, world = dist.get_rank(group), dist.get_world_size(group)
+        # host seconds spent inside the callbacks (rehearsal timing: bench.py --comm host)
+        self.comm_stats = {"allreduce_s": 0.0, "allreduce_calls": 0, "exchange_s": 0.0, "exchange_calls": 0}
+        st = self.comm_stats
 
         def allreduce(buf, n, _user):
+            t0 = time.perf_counter()
             try:
                 a = np.ctypeslib.as_array(buf, shape=(n,))
                 t = torch.from_numpy(a.copy())
@@ -578,8 +583,12 @@ class Context:
                 return 0
             except Exception:  # errors must not unwind through C
                 return 1
+            finally:
+                st["allreduce_s"] += time.perf_counter() - t0
+                st["allreduce_calls"] += 1
 
         def exchange(send_lo, recv_lo, send_hi, recv_hi, n, _user):
+            t0 = time.perf_counter()
             try:
                 reqs, outs = [], []
                 if bool(send_lo):
@@ -601,6 +610,9 @@ class Context:
                 return 0
             except Exception:
                 return 1
+            finally:
+                st["exchange_s"] += time.perf_counter() - t0
+                st["exchange_calls"] += 1
 
         def nbr_exchange(n_nbr, ranks, off, send, recv, _user):
             try:

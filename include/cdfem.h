@@ -256,6 +256,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *                data.  All forms apply the operator of the per-point multilinear-map setup to rounding
  *                (the Kronecker form is an algebraic identity of the tensor rule, not an exactness
  *                argument); 0 = the per-point map and stream everywhere.
+ * "cg_xfold": 1 (default) — structured brick CG (p <= 2): each apply after the first advances x by
+ *             the previous iteration's alpha d on the dofs it writes the new direction for, so the
+ *             update kernel streams neither x nor d (bitwise the same iterates); 0 = x in the update.
  * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).

@@ -342,10 +342,14 @@ def _cpu_gmres_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def _gathered_rhs(tmp_path, plane):
-    b0, b1 = np.load(tmp_path / "b0.npy"), np.load(tmp_path / "b1.npy")
-    bfull = np.concatenate([b0, np.zeros(len(b1) - plane)])
-    bfull[len(b0) - plane:] += b1
+def _gathered_rhs(tmp_path, plane, world=2):
+    """The global right-hand side of per-rank slab partials (shared planes summed)."""
+    bs = [np.load(tmp_path / f"b{r}.npy") for r in range(world)]
+    bfull = np.zeros(len(bs[0]) + sum(len(b) - plane for b in bs[1:]))
+    off = 0
+    for b in bs:
+        bfull[off:off + len(b)] += b
+        off += len(b) - plane
     return bfull
 
 
@@ -519,16 +523,18 @@ def _gpu_c5_worker(rank, world, port, out_dir):
 
 
 @pytest.mark.gpu
-def test_gpu_c5_per_rank_slabs(tmp_path):
+@pytest.mark.parametrize("world", [2, 8])
+def test_gpu_c5_per_rank_slabs(tmp_path, world):
     """C5's per-GPU slab (256 x 256 x 32, p = 2, D+C+M) through the multi-rank brick CG: 20 fixed
-    Jacobi-CG iterates on 2 ranks == one context on 256 x 256 x 64 (1e-12), and the shared plane
-    is bitwise the same on both ranks."""
+    Jacobi-CG iterates on `world` ranks == one context on 256 x 256 x (32 world) (1e-12), and every
+    shared plane is bitwise the same on both of its ranks.  world = 8 is C5's actual 8-way partition
+    of the 256^3 mesh (six interior ranks with two neighbours), here on one GPU with the host
+    communicator (RCCL refuses two ranks on one device)."""
     import cdfem
-    world = 2
     mp.start_processes(_gpu_c5_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
                        start_method="spawn", join=True)
     plane = (P * C5_N + 1) ** 2
-    bfull = _gathered_rhs(tmp_path, plane)
+    bfull = _gathered_rhs(tmp_path, plane, world)
     m = cdfem.box_mesh(3, (C5_N, C5_N, C5_PER * world), P, with_coords=False)
     with cdfem.Context(0) as ctx:
         ctx.upload_mesh(m).set_structured(C5_N, C5_N, C5_PER * world)
@@ -536,8 +542,10 @@ def test_gpu_c5_per_rank_slabs(tmp_path):
         _, B = ctx.form_linear_system(np.zeros(m.nl), bfull)
         xs, info = ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=C5_ITERS,
                              check_every=C5_ITERS)
-    x0, x1 = np.load(tmp_path / "x0.npy"), np.load(tmp_path / "x1.npy")
-    assert int(np.load(tmp_path / "its0.npy")[0]) == info["iterations"] == C5_ITERS
-    np.testing.assert_array_equal(x1[:plane], x0[-plane:])
-    xg = np.concatenate([x0, x1[plane:]])
+    xr = [np.load(tmp_path / f"x{r}.npy") for r in range(world)]
+    for r in range(world):
+        assert int(np.load(tmp_path / f"its{r}.npy")[0]) == info["iterations"] == C5_ITERS
+    for r in range(world - 1):
+        np.testing.assert_array_equal(xr[r + 1][:plane], xr[r][-plane:])
+    xg = np.concatenate([xr[0]] + [x[plane:] for x in xr[1:]])
     assert np.linalg.norm(xg - xs) <= 1e-12 * np.linalg.norm(xs)

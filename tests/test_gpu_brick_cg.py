@@ -1,0 +1,43 @@
+"""Brick CG (the BASELINE metric's loop) options that must not change the iterates.
+
+cg_xfold (default 1) moves x += alpha d of iteration k into the apply of iteration k + 1 (the dofs a
+brick writes the new direction for), with k_cg_xflush adding the last update's term after the loop
+when the update logic stopped the solve.  Against cg_xfold 0 the solution must be bitwise equal for
+every way a solve ends: fixed iteration counts (max_iter, including 0, 1 and 2), convergence inside a
+host-poll batch (check_every), and on partial bricks with essential values.  MFEM CGSolver semantics
+(mesh_recession_handler.cpp:270-276) are pinned against the oracle elsewhere (test_gpu_parity.py)."""
+import numpy as np
+import pytest
+
+import cdfem
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+C3 = (1.0, -2.0, 0.5)
+
+
+def _solve(gpu_ctx, om, shape, kinds, xfold, B, **kw):
+    gpu_ctx.set_option("cg_xfold", xfold)
+    try:
+        return gpu_ctx.solve(B, method="cg", pc="jacobi", **kw)
+    finally:
+        gpu_ctx.set_option("cg_xfold", 1)
+
+
+@pytest.mark.parametrize("shape,p,kinds,pert", [((8, 8, 8), 2, 7, 0.0), ((9, 6, 7), 2, 5, 0.1), ((6, 5, 7), 1, 7, 0.0)])
+def test_xfold_bitwise(gpu_ctx, shape, p, kinds, pert):
+    om = O.BoxMesh(3, shape, p, perturb=pert)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(*shape)
+    gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    rng = np.random.default_rng(5)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    _, B = gpu_ctx.form_linear_system(u, rng.uniform(-1, 1, om.nl))
+    cases = [dict(rel_tol=0.0, abs_tol=0.0, max_iter=m, check_every=ce) for m, ce in ((0, 16), (1, 16), (2, 1), (30, 7))]
+    if kinds == 5:  # SPD: a converged stop inside a poll batch
+        cases.append(dict(rel_tol=1e-8, max_iter=2000, check_every=7))
+    for kw in cases:
+        x0, i0 = _solve(gpu_ctx, om, shape, kinds, 0, B, **kw)
+        x1, i1 = _solve(gpu_ctx, om, shape, kinds, 1, B, **kw)
+        assert i0["iterations"] == i1["iterations"] and i0["converged"] == i1["converged"], kw
+        np.testing.assert_array_equal(x1, x0)
