@@ -376,8 +376,10 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // below, which owns it for the dot products (remote_lo / remote_hi carry the neighbours' partial
 // sums of the interface planes; nullptr on a single GPU).
 // ================================================================================================
-template <int D1, int Q1, unsigned K, int AF>
-__global__ void __launch_bounds__(64, AF == 2 ? 2 : 1)
+// W: waves per SIMD the register allocation targets (set_option "brick_cg_waves"; the Kronecker
+// form fits 2 without spills, 3 with a few spilled scalars; the point-data forms take 1)
+template <int D1, int Q1, unsigned K, int AF, int W = 1>
+__global__ void __launch_bounds__(64, W)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
@@ -595,14 +597,20 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const dim3 grid((unsigned)(c->nbx * c->nby * run.nlay)), block(64);
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
     const double *qd = c->d_qaff ? c->d_qaff : c->d_qd;
-#define CDFEM_BCG(AFF_)                                                                                      \
+#define CDFEM_BCG(AFF_, W_)                                                                                  \
     if (whole)                                                                                               \
-        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_>), grid, block, 0, r, dinv, d_old, d_new, q, c->d_face, qd, \
-                     c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x);                               \
+        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_>), grid, block, 0, r, dinv, d_old, d_new, q, c->d_face, \
+                     qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x);                           \
     else                                                                                                     \
-        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_>), grid, block, 0, run.s, r, dinv, d_old, d_new, q,    \
+        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_>), grid, block, 0, run.s, r, dinv, d_old, d_new, q, \
                            c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x)
-    if (pa_af(c) == 2) { CDFEM_BCG(2); } else if (pa_af(c) == 1) { CDFEM_BCG(1); } else { CDFEM_BCG(0); }
+    if (pa_af(c) == 2) {
+        if (c->brick_cg_waves == 3) { CDFEM_BCG(2, 3); } else { CDFEM_BCG(2, 2); }
+    } else if (pa_af(c) == 1) {
+        CDFEM_BCG(1, 1);
+    } else {
+        CDFEM_BCG(0, 1);
+    }
 #undef CDFEM_BCG
     return hipGetLastError();
 }

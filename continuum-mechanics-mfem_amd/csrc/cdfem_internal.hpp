@@ -159,6 +159,7 @@ struct cdfem_ctx {
     int gm_ept_auto = 4;                // the automatic choice for vectors of gm_ept_n entries
     int64_t gm_ept_n = -1;
     int brick_xcd = 1;                  // k_brick_cg brick order: 0 dispatch, 1 XCD-contiguous (default)
+    int brick_cg_waves = 2;             // set_option "brick_cg_waves": waves per SIMD of the Kronecker k_brick_cg (2, 3)
     int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)
     int zhi_shared = 0;                 // local gz=Lz-1 plane shared with the rank above
     cdfem::Comm *comm = nullptr;        // rank communicator (comm.hip), nullptr on one GPU
@@ -216,7 +217,7 @@ struct cdfem_ctx {
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
-    int cg_xfold = 1;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply
+    int cg_xfold = 0;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 8;                  // set_option "sell_order" (read when the FA pattern is built)
     int sell_window = 0;                // set_option "sell_window": rows per window of a windowed order (0 auto)
@@ -291,8 +292,14 @@ struct cdfem_ctx {
 
 namespace cdfem {
 
-// the high-order tile apply forms the point data from the affine factors (ho_mfma keeps the stream)
-inline bool tile_affine(const cdfem_ctx *c) { return c->d_qaff != nullptr && c->ho_mfma == 0; }
+// the high-order tile apply forms the point data from the affine factors; with MFMA stages
+// (ho_mfma) only on the full operator (kinds 7) and the masks 1, 8, 9, else ho_mfma keeps the stream
+inline bool tile_affine(const cdfem_ctx *c)
+{
+    if (c->d_qaff == nullptr) return false;
+    if (c->ho_mfma == 0) return true;
+    return c->kinds == 7 && (c->ho_mfma == 1 || c->ho_mfma == 8 || c->ho_mfma == 9);
+}
 // the element core of the 3D p <= 2 applies (pa_core.hpp elem_apply3d_af): 0 per-point stream,
 // 1 point data from the affine factors, 2 Kronecker form of the factors
 inline int pa_af(const cdfem_ctx *c) { return c->d_qaff == nullptr ? 0 : (c->pa_affine == 2 ? 2 : 1); }

@@ -481,7 +481,19 @@ template <int D1, int Q1, unsigned K>
 static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
                              double *den_part)
 {
-    if (tile_affine(c)) return tile_kinds_mf<D1, Q1, K, 16>(c, x, Ye, con, st, den_part);
+    if (tile_affine(c)) {
+        // affine factors; on the BASELINE operator (kinds 7) also with the x / x^T stages on the
+        // matrix cores (ho_mfma 1, 8, 9: VERDICT r03 item 4, the arithmetic-bound regime)
+        if constexpr (K == 7) {
+            switch (c->ho_mfma) {
+            case 1: return tile_kinds_mf<D1, Q1, K, 17>(c, x, Ye, con, st, den_part);
+            case 8: return tile_kinds_mf<D1, Q1, K, 24>(c, x, Ye, con, st, den_part);
+            case 9: return tile_kinds_mf<D1, Q1, K, 25>(c, x, Ye, con, st, den_part);
+            default: break;
+            }
+        }
+        return tile_kinds_mf<D1, Q1, K, 16>(c, x, Ye, con, st, den_part);
+    }
     switch (c->ho_mfma) {
     case 1: return tile_kinds_mf<D1, Q1, K, 1>(c, x, Ye, con, st, den_part);
     case 3: return tile_kinds_mf<D1, Q1, K, 3>(c, x, Ye, con, st, den_part);

@@ -321,63 +321,63 @@ __device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__
 
 #pragma unroll
     for (int jz = 0; jz < D1; ++jz) {
-        // x stage of this input plane and the per-element combinations:
+        double X[D1][D1];
+#pragma unroll
+        for (int jy = 0; jy < D1; ++jy)
+#pragma unroll
+            for (int jx = 0; jx < D1; ++jx) X[jy][jx] = xl(jz, jy, jx);
+        // one output column ix at a time (x stage of that column for every row jy, then the y and z
+        // stages of the column), so only one column's intermediates are live:
         //   u1 = s M + D_xx K + c_x C,  u3 = D_xy Ct + c_y M,  u5 = D_xz Ct + c_z M  (applied along x)
-        double xm[D1][D1], xc[D1][D1], u1[D1][D1], u3[D1][D1], u5[D1][D1];
 #pragma unroll
-        for (int jy = 0; jy < D1; ++jy) {
-            double r[D1];
+        for (int ix = 0; ix < D1; ++ix) {
+            double xm[D1], xc[D1], u1[D1], u3[D1], u5[D1];
 #pragma unroll
-            for (int jx = 0; jx < D1; ++jx) r[jx] = xl(jz, jy, jx);
-#pragma unroll
-            for (int ix = 0; ix < D1; ++ix) {
+            for (int jy = 0; jy < D1; ++jy) {
                 double m = 0.0, k = 0.0, c = 0.0, ct = 0.0;
 #pragma unroll
                 for (int jx = 0; jx < D1; ++jx) {
-                    m += tM(T, ix, jx) * r[jx];
+                    m += tM(T, ix, jx) * X[jy][jx];
                     if constexpr (kD) {
-                        k += tK(T, ix, jx) * r[jx];
-                        ct = tCacc(T, jx, ix, r[jx], ct);
+                        k += tK(T, ix, jx) * X[jy][jx];
+                        ct = tCacc(T, jx, ix, X[jy][jx], ct);
                     }
-                    if constexpr (kG) c = tCacc(T, ix, jx, r[jx], c);
+                    if constexpr (kG) c = tCacc(T, ix, jx, X[jy][jx], c);
                 }
-                xm[jy][ix] = m;
-                xc[jy][ix] = c;
+                xm[jy] = m;
+                xc[jy] = c;
                 double a = 0.0;
                 if constexpr (kM) a = g[L::oM] * m;
                 if constexpr (kD) a += g[0] * k;
                 if constexpr (kC) a += g[L::oC] * c;
-                u1[jy][ix] = a;
+                u1[jy] = a;
                 if constexpr (kD && kC) {
-                    u3[jy][ix] = g[1] * ct + g[L::oC + 1] * m;
-                    u5[jy][ix] = g[2] * ct + g[L::oC + 2] * m;
+                    u3[jy] = g[1] * ct + g[L::oC + 1] * m;
+                    u5[jy] = g[2] * ct + g[L::oC + 2] * m;
                 } else if constexpr (kD) {
-                    u3[jy][ix] = g[1] * ct;
-                    u5[jy][ix] = g[2] * ct;
+                    u3[jy] = g[1] * ct;
+                    u5[jy] = g[2] * ct;
                 } else if constexpr (kC) {
-                    u3[jy][ix] = g[L::oC + 1] * m;
-                    u5[jy][ix] = g[L::oC + 2] * m;
+                    u3[jy] = g[L::oC + 1] * m;
+                    u5[jy] = g[L::oC + 2] * m;
                 }
             }
-        }
-        // y stage into the z groups, then the z stage
+            // y stage into the z groups (M, K, C, Ct), then the z stage
 #pragma unroll
-        for (int iy = 0; iy < D1; ++iy)
-#pragma unroll
-            for (int ix = 0; ix < D1; ++ix) {
+            for (int iy = 0; iy < D1; ++iy) {
                 double pm = 0.0, pk = 0.0, pc = 0.0, pct = 0.0;
                 {
                     double s1 = 0.0;
 #pragma unroll
-                    for (int jy = 0; jy < D1; ++jy) s1 += tM(T, iy, jy) * u1[jy][ix];
+                    for (int jy = 0; jy < D1; ++jy) s1 += tM(T, iy, jy) * u1[jy];
                     pm = s1;
                 }
                 if constexpr (kG) {
                     double s3 = 0.0, s5 = 0.0;
 #pragma unroll
                     for (int jy = 0; jy < D1; ++jy) {
-                        s3 = tCacc(T, iy, jy, u3[jy][ix], s3);
-                        s5 += tM(T, iy, jy) * u5[jy][ix];
+                        s3 = tCacc(T, iy, jy, u3[jy], s3);
+                        s5 += tM(T, iy, jy) * u5[jy];
                     }
                     pm += s3;
                     pc = s5;
@@ -386,12 +386,12 @@ __device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__
                     double kym = 0.0, ctyc = 0.0, mym = 0.0, ctym = 0.0, myc = 0.0, cym = 0.0;
 #pragma unroll
                     for (int jy = 0; jy < D1; ++jy) {
-                        kym += tK(T, iy, jy) * xm[jy][ix];
-                        ctyc = tCacc(T, jy, iy, xc[jy][ix], ctyc);
-                        mym += tM(T, iy, jy) * xm[jy][ix];
-                        ctym = tCacc(T, jy, iy, xm[jy][ix], ctym);
-                        myc += tM(T, iy, jy) * xc[jy][ix];
-                        cym = tCacc(T, iy, jy, xm[jy][ix], cym);
+                        kym += tK(T, iy, jy) * xm[jy];
+                        ctyc = tCacc(T, jy, iy, xc[jy], ctyc);
+                        mym += tM(T, iy, jy) * xm[jy];
+                        ctym = tCacc(T, jy, iy, xm[jy], ctym);
+                        myc += tM(T, iy, jy) * xc[jy];
+                        cym = tCacc(T, iy, jy, xm[jy], cym);
                     }
                     pm += g[3] * kym;
                     pm += g[1] * ctyc;
@@ -411,6 +411,7 @@ __device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__
                     Y[iz][iy][ix] = y;
                 }
             }
+        }
     }
 }
 

@@ -232,6 +232,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
 /* ---- tuning knobs (performance only; results identical to rounding) --------------------------
  * "profile_mask": bit k set = kernel slot k (CDFEM_K_*) gets HIP events while profiling is on
  *                 (default all; events around every kernel cost ~1 us each on the stream).
+ * "brick_cg_waves": 2 (default) — waves per SIMD the Kronecker-form structured CG kernel is compiled
+ *                   for (register budget, spill-free); 3 = a tighter budget with a few spills (measured
+ *                   slower: 80.7 against 77.4 us per C2 iteration, profiles/r04/ab_c2_xfold_waves.json).
  * "brick_xcd": 1 (default) — XCD-contiguous brick order of the structured CG kernel; 0 = the
  *              dispatcher's round-robin order.
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
@@ -256,9 +259,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *                data.  All forms apply the operator of the per-point multilinear-map setup to rounding
  *                (the Kronecker form is an algebraic identity of the tensor rule, not an exactness
  *                argument); 0 = the per-point map and stream everywhere.
- * "cg_xfold": 1 (default) — structured brick CG (p <= 2): each apply after the first advances x by
- *             the previous iteration's alpha d on the dofs it writes the new direction for, so the
- *             update kernel streams neither x nor d (bitwise the same iterates); 0 = x in the update.
+ * "cg_xfold": 0 (default) — 1: structured brick CG (p <= 2), each apply after the first advances x
+ *             by the previous iteration's alpha d on the dofs it writes the new direction for, so the
+ *             update kernel streams neither x nor d (bitwise the same iterates; measured even at C2:
+ *             the apply gains what the update loses, profiles/r04/ab_c2_xfold_waves.json).
  * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).

@@ -129,6 +129,19 @@ def test_affine_map_tile(gpu_ctx, p, structured, kinds):
     _check(gpu_ctx, shape, p, kinds, structured=structured)
 
 
+@pytest.mark.parametrize("p,structured", [(4, True), (3, False)])
+@pytest.mark.parametrize("mf", [1, 9])
+def test_affine_map_tile_mfma(gpu_ctx, p, structured, mf):
+    """The affine-factor tile apply with its x / x^T stages on v_mfma_f64_16x16x4_f64 (ho_mfma 1, 9;
+    kinds 7, the BASELINE operator)."""
+    shape = (3, 4, 2) if p == 4 else (4, 3, 5)
+    gpu_ctx.set_option("ho_mfma", mf)
+    try:
+        _check(gpu_ctx, shape, p, 7, structured=structured)
+    finally:
+        gpu_ctx.set_option("ho_mfma", 0)
+
+
 def test_affine_tolerance_is_element_relative(gpu_ctx):
     """mesh_is_affine compares each vertex's parallelepiped defect with 32 ulp of the coordinates
     plus 1e-12 of the element's edge: small elements far from the origin (|x| ~ 100, edges 0.01) are
