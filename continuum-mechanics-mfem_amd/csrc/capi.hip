@@ -699,7 +699,8 @@ int cdfem_create(int device, cdfem_ctx **out)
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_state, sizeof(KrylovState)) != hipSuccess ||
         hipMemset(c->d_state, 0, sizeof(KrylovState)) != hipSuccess ||
-        hipHostMalloc(&c->h_state, sizeof(KrylovState), hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&c->h_state, sizeof(KrylovState), hipHostMallocDefault) != hipSuccess ||
+        hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
         cdfem_destroy(c);
         return CDFEM_ERR_HIP;
     }
@@ -1656,7 +1657,10 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
     return guarded(c, [&] {
         if (!key) throw ArgError("key is null");
         const std::string k(key);
-        if (k == "brick_cg_waves") {
+        if (k == "brick_cg_persist") {
+            if (value != 0 && value != 1) throw ArgError("brick_cg_persist must be 0 or 1");
+            c->brick_cg_persist = value;
+        } else if (k == "brick_cg_waves") {
             if (value != 2 && value != 3) throw ArgError("brick_cg_waves must be 2 or 3");
             c->brick_cg_waves = value;
         } else if (k == "brick_xcd") {

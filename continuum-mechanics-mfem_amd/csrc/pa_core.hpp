@@ -301,16 +301,13 @@ __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restr
 // jz: x stage (M, K, C, Ct on the plane's rows), the per-element combinations, y stage into the four
 // z groups (M, K, C, Ct), z stage into Y.  At p = 2: 1.73 K FMA-class operations per element against
 // 4.3 K for the quadrature form (elem_apply3d<..., AFF>), 45 + 27 live doubles.
+// g: the element's factors (QLayout<K, 3> order), loaded by the caller (kron_load_g)
 template <int D1, int Q1, unsigned K, typename XL>
-__device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__restrict__ q0, int lane,
-                                                  const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
+__device__ __forceinline__ void kron_core(const XL &xl, const double (&g)[QLayout<K, 3>::nc], const Tab<D1, Q1> &T,
+                                          double (&Y)[D1][D1][D1])
 {
     using L = QLayout<K, 3>;
-    constexpr int NC = L::nc;
     constexpr bool kD = L::kD, kC = L::kC, kM = L::kM, kG = L::kD || L::kC;
-    double g[NC];
-#pragma unroll
-    for (int k = 0; k < NC; ++k) g[k] = q0[k * kLanes + lane];
     // D = [[g0 g1 g2] [g1 g3 g4] [g2 g4 g5]], c = g[oC..oC+2], s = g[oM]
 #pragma unroll
     for (int dz = 0; dz < D1; ++dz)
@@ -413,6 +410,23 @@ __device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__
             }
         }
     }
+}
+
+// the factors of element `lane` of the block whose factors start at q0 ([NC][kLanes])
+template <unsigned K>
+__device__ __forceinline__ void kron_load_g(const double *__restrict__ q0, int lane, double (&g)[QLayout<K, 3>::nc])
+{
+#pragma unroll
+    for (int k = 0; k < QLayout<K, 3>::nc; ++k) g[k] = q0[k * kLanes + lane];
+}
+
+template <int D1, int Q1, unsigned K, typename XL>
+__device__ __forceinline__ void elem_apply3d_kron(const XL &xl, const double *__restrict__ q0, int lane,
+                                                  const Tab<D1, Q1> &T, double (&Y)[D1][D1][D1])
+{
+    double g[QLayout<K, 3>::nc];
+    kron_load_g<K>(q0, lane, g);
+    kron_core<D1, Q1, K>(xl, g, T, Y);
 }
 
 // the element core of the apply kernels by affine form: AF 0 per-point stream, 1 point data formed
