@@ -43,16 +43,41 @@ __device__ __forceinline__ int brick_id(const BrickGeom &g)
     return (int)(x * q + (x < r ? x : r) + k);
 }
 
-// index of boundary position (a, b, c) of an S^3 patch in lexicographic order of the boundary set;
-// selects instead of branches (the callers run it for every lane, faces or not)
+// Patch positions i = t, t + 64, t + 128, ... of an S^3 patch (x fastest), advanced incrementally:
+// 64 = dz S^2 + dy S + dx, so each step adds (dx, dy, dz) with carries (a few adds and selects
+// instead of two constant divisions per position)
+template <int S>
+struct PatchWalk {
+    int x, y, z;
+    __device__ __forceinline__ explicit PatchWalk(unsigned t) : x((int)(t % S)), y((int)((t / S) % S)), z((int)(t / (S * S))) {}
+    __device__ __forceinline__ void next()
+    {
+        constexpr int dx = 64 % S, dy = (64 / S) % S, dz = 64 / (S * S);
+        x += dx;
+        const int cx = x >= S ? 1 : 0;
+        x -= S & -cx;
+        y += dy + cx;
+        const int cy = y >= S ? 1 : 0;
+        y -= S & -cy;
+        z += dz + cy;
+    }
+};
+
+// index of boundary position (a, b, c) of an S^3 patch in lexicographic order of the boundary set.
+// Bit-mask selects, no ?: on expressions: the callers run it in every lane, and the compiler turns
+// conditional expressions into divergent branches.
+__device__ __forceinline__ int bsel(bool c, int a, int b)
+{
+    const int m = -(int)c;
+    return (a & m) | (b & ~m);
+}
 template <int S>
 __device__ __forceinline__ int face_index(int a, int b, int c)
 {
     constexpr int ring = 4 * S - 4;
-    const int cap = a + S * b;                                  // c == 0 / c == S - 1 plane
-    const int base = S * S + (c - 1) * ring;                    // ring plane c
-    const int mid = b == 0 ? a : b == S - 1 ? S + 2 * (S - 2) + a : S + 2 * (b - 1) + (a == S - 1 ? 1 : 0);
-    return c == 0 ? cap : c == S - 1 ? S * S + (S - 2) * ring + cap : base + mid;
+    const int cap = a + S * b;                                   // planes c == 0 and c == S - 1
+    const int mid = bsel(b == 0, a, bsel(b == S - 1, S + 2 * (S - 2) + a, S + 2 * (b - 1) + (int)(a == S - 1)));
+    return bsel(c == 0, cap, bsel(c == S - 1, S * S + (S - 2) * ring + cap, S * S + (c - 1) * ring + mid));
 }
 
 template <int S>
@@ -65,6 +90,24 @@ __device__ __forceinline__ int opaque(int v)
 {
     asm volatile("" : "+v"(v));
     return v;
+}
+
+// Raw buffer access (MI355X buffer resources): a 32-bit byte offset from a scalar base instead of a
+// 64-bit address per lane, and an offset past num_records (kOOB) reads 0 and drops a store, so the
+// brick kernels' out-of-lattice positions and predicated stores need neither branches nor clamps.
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+constexpr uint32_t kOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, double v)
+{
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, off, 0, 0);
 }
 
 // In-LDS E->L schedule.  At P = 2 an element's local dof d lands on patch position 2e + d per axis,
@@ -143,10 +186,12 @@ k_brick3d(const double *__restrict__ x, double *__restrict__ y, double *__restri
     double xv[NI];
     uint8_t ev[NI];
     bool inv[NI];
+    PatchWalk<S> pw0(t);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const unsigned i = t + 64 * k;
-        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
+        const int px = pw0.x, py = pw0.y, pz = pw0.z;
+        pw0.next();
         const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
         inv[k] = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
         const int gid = inv[k] ? gx + Lx * gy + Lxy * gz : 0;
@@ -175,10 +220,12 @@ k_brick3d(const double *__restrict__ x, double *__restrict__ y, double *__restri
     // 4. owned dofs -> y (constrained: y = x on ess rows), face dofs -> this brick's partials
     double *const fb = face + (size_t)b * F;
     const unsigned to = (unsigned)opaque(t);
+    PatchWalk<S> pw1(to);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const unsigned i = to + 64 * k;
-        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
+        const int px = pw1.x, py = pw1.y, pz = pw1.z;
+        pw1.next();
         const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
         const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
         const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
@@ -189,10 +236,12 @@ k_brick3d(const double *__restrict__ x, double *__restrict__ y, double *__restri
             else y[gid] = ess[gid] ? x[gid] : v;
         }
     }
+    PatchWalk<S> pw2(to);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const unsigned i = to + 64 * k;
-        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
+        const int px = pw2.x, py = pw2.y, pz = pw2.z;
+        pw2.next();
         const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
         if (i < S3 && onface) fb[face_index<S>(px, py, pz)] = s_out[i];
     }
@@ -378,7 +427,7 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // ================================================================================================
 // W: waves per SIMD the register allocation targets (set_option "brick_cg_waves"; the Kronecker
 // form fits 2 without spills, 3 with a few spilled scalars; the point-data forms take 1)
-template <int D1, int Q1, unsigned K, int AF, int W = 1>
+template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false>
 __global__ void __launch_bounds__(64, W)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
@@ -389,17 +438,17 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
     constexpr int S2 = S * S, S3 = S * S * S;
-    constexpr int F = face_count<S>();
     constexpr int NC = QLayout<K, 3>::nc;
     constexpr int NQ = Q1 * Q1 * Q1;
     __shared__ double s_in[S3];
     __shared__ double s_out[S3];
     if (st->done) return;
     const double beta = st->beta;
-    // x-fold (x != nullptr, set_option "cg_xfold"): the previous iteration's x += alpha d_old, for
-    // the dofs this brick writes d_new for (each dof has exactly one writer brick); the update
-    // kernel then leaves x alone.  Bitwise the unfolded update (same fma on the same values).
-    const double alpha_prev = x ? st->alpha : 0.0;
+    // x-fold (XF, set_option "cg_xfold"): the previous iteration's x += alpha d_old, for the dofs
+    // this brick writes d_new for (each dof has exactly one writer brick); the update kernel then
+    // leaves x alone.  Bitwise the unfolded update (same fma on the same values).  A template flag:
+    // a run-time one costs every position's writer mask a scalar register pair.
+    const double alpha_prev = XF ? st->alpha : 0.0;
     const int t = threadIdx.x;
     // launch-local brick -> global brick (a launch covers every g.bzs-th layer from g.bz0)
     const int bl = brick_id(g), nxy = g.nbx * g.nby;
@@ -414,42 +463,51 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     // no branches between them): one memory latency per brick instead of one per patch row.
     // Measured (tools/ab.py, in process): 241.1 vs 242.4 us per launch for the per-row form; the
     // other waves of the CU hide most of that latency.
-    // (the lattice index fits 32 bits: N_L < 2^31 on one context)
+    // Buffer access (brsrc): byte offsets fit 32 bits (8 N_L < 2^32 on one context: N_L <= 1.35e8,
+    // SURVEY 8a); out-of-lattice positions of partial bricks use kOOB (loads 0, stores dropped).
     constexpr int NI = (S3 + 63) / 64;
-    double rv[NI], mv[NI], ov[NI], xv[NI];
-    uint8_t ev[NI];
-    int gidv[NI];
     const int Lx = g.Lx, Lxy = g.Lx * g.Ly;
+    const uint32_t nl = (uint32_t)Lxy * (uint32_t)g.Lz;
+    const auto br = brsrc(r, 8u * nl), bm = brsrc(dinv, 8u * nl), bo = brsrc(d_old, 8u * nl);
+    const auto be = brsrc(ess, nl), bd = brsrc(d_new, 8u * nl), bxf = brsrc(x, XF ? 8u * nl : 0u);
+    double rv[NI], mv[NI], ov[NI], xv[NI];
+    uint32_t offv[NI];
+    uint8_t ev[NI];
+    PatchWalk<S> pw0(t);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const unsigned i = t + 64 * k;
-        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
+        const int px = pw0.x, py = pw0.y, pz = pw0.z;
+        pw0.next();
         const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
         const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
-        const int gid = in ? gx + Lx * gy + Lxy * gz : 0;
-        gidv[k] = in ? gid : -1;
-        rv[k] = r[gid];
-        mv[k] = dinv[gid];
-        ov[k] = d_old[gid];
-        ev[k] = ess[gid];
+        const uint32_t gid = (uint32_t)opaque(gx + Lx * gy + Lxy * gz);  // computed in every lane, selected
+        offv[k] = in ? 8u * gid : kOOB;
+        rv[k] = bload(br, offv[k]);
+        mv[k] = bload(bm, offv[k]);
+        ov[k] = bload(bo, offv[k]);
+        ev[k] = __builtin_amdgcn_raw_buffer_load_b8(be, in ? gid : kOOB, 0, 0);
         const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
-        xv[k] = (x && writer) ? x[gid] : 0.0;
+        if constexpr (XF) xv[k] = bload(bxf, writer ? offv[k] : kOOB);
     }
+    PatchWalk<S> pw1(t);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const unsigned i = t + 64 * k;
         if (k == NI - 1 && i >= S3) break;
-        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
+        const int px = pw1.x, py = pw1.y, pz = pw1.z;
+        pw1.next();
         const int gz = gz0 + pz;
-        const bool in = gidv[k] >= 0;
-        const double dn = mv[k] * rv[k] + beta * ov[k];
+        const bool in = offv[k] != kOOB;
+        const double dn = mv[k] * rv[k] + beta * ov[k];  // 0 outside the lattice
         const bool e = ev[k] != 0;
         const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
-        if (writer) d_new[gidv[k]] = dn;
-        if (x && writer) x[gidv[k]] = xv[k] + alpha_prev * ov[k];
+        const uint32_t woff = writer ? offv[k] : kOOB;
+        bstore(bd, woff, dn);
+        if constexpr (XF) bstore(bxf, woff, xv[k] + alpha_prev * ov[k]);
         // (A_c d)_i = d_i on ess dofs
         den += (writer && e && !(zlo_shared && gz == 0)) ? dn * dn : 0.0;
-        s_in[i] = (in && !e) ? dn : 0.0;
+        s_in[i] = e ? 0.0 : dn;
         s_out[i] = 0.0;
     }
     __syncthreads();
@@ -469,31 +527,14 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
             for (int dx = 0; dx < D1; ++dx) den += s_in[o0 + dz * S2 + dy * S + dx] * Y[dz][dy][dx];
     brick_e2l<D1, S>(s_out, o0, Y);
 
-    // owned (patch-interior) rows -> q, face rows -> this brick's face partials; one store per
-    // position through a selected pointer (no divergent branches: the masks cost scalar registers)
-    double *const fb = face + (size_t)b * F;
-    const unsigned to = (unsigned)opaque(t);
-    double vv[NI];
-#pragma unroll
-    for (int k = 0; k < NI; ++k) vv[k] = (k < NI - 1 || to + 64 * k < S3) ? s_out[to + 64 * k] : 0.0;
-    // two predicated stores per position (patch-interior rows -> q, face rows -> this brick's face
-    // partials) instead of an if / else, which the compiler structurises into divergent branches
+    // the brick's whole patch output (interior rows complete, face rows partial) -> its slot of the
+    // patch buffer: contiguous stores; k_cg_update_faces sums each dof's 1-8 patch entries
+    double *const pbo = face + (size_t)b * S3;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
-        const unsigned i = to + 64 * k;
-        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
-        const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
-        // the lattice index again (cheaper than keeping the gather's indices live through the apply)
-        const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-        const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
-        if (in && !onface) q[gx + Lx * gy + Lxy * gz] = vv[k];  // ess rows: replaced by d in the update
-    }
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const unsigned i = to + 64 * k;
-        const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
-        const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
-        if (i < S3 && onface) fb[face_index<S>(px, py, pz)] = vv[k];
+        const int i = t + 64 * k;
+        if (k == NI - 1 && i >= S3) break;
+        pbo[i] = s_out[i];
     }
     den = wave_sum(den);
     if (t == 0) part[b] = den;
@@ -518,7 +559,6 @@ k_brick_cgp(const double *__restrict__ r, const double *__restrict__ dinv,
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
     constexpr int S2 = S * S, S3 = S * S * S;
-    constexpr int F = face_count<S>();
     constexpr int NC = QLayout<K, 3>::nc;
     constexpr int NI = (S3 + 63) / 64;
     __shared__ double s_in[S3];
@@ -598,26 +638,12 @@ k_brick_cgp(const double *__restrict__ r, const double *__restrict__ dinv,
                 for (int dx = 0; dx < D1; ++dx) den += s_in[o0 + dz * S2 + dy * S + dx] * Y[dz][dy][dx];
         brick_e2l<D1, S>(s_out, o0, Y);
 
-        double *const fb = face + (size_t)b * F;
-        const unsigned to = (unsigned)opaque(t);
-        double vv[NI];
-#pragma unroll
-        for (int k = 0; k < NI; ++k) vv[k] = (k < NI - 1 || to + 64 * k < S3) ? s_out[to + 64 * k] : 0.0;
+        double *const pbo = face + (size_t)b * S3;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
-            const unsigned i = to + 64 * k;
-            const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
-            const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
-            const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-            const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
-            if (in && !onface) q[gx + Lx * gy + Lxy * gz] = vv[k];
-        }
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-            const unsigned i = to + 64 * k;
-            const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
-            const bool onface = px == 0 || px == S - 1 || py == 0 || py == S - 1 || pz == 0 || pz == S - 1;
-            if (i < S3 && onface) fb[face_index<S>(px, py, pz)] = vv[k];
+            const int i = t + 64 * k;
+            if (k == NI - 1 && i >= S3) break;
+            pbo[i] = s_out[i];
         }
         den = wave_sum(den);
         if (t == 0) part[b] = den;
@@ -627,14 +653,14 @@ k_brick_cgp(const double *__restrict__ r, const double *__restrict__ dinv,
 
 template <int S, bool XF>
 __global__ void __launch_bounds__(kRedThreads)
-k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ q,
-                  const double *__restrict__ d, const double *__restrict__ dinv,
-                  const double *__restrict__ face, const uint8_t *__restrict__ ess, const BrickGeom g,
+k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ d,
+                  const double *__restrict__ dinv, const double *__restrict__ pb,
+                  const uint8_t *__restrict__ ess, const BrickGeom g,
                   const FastDiv fdx, const FastDiv fdxy, int zlo_shared,
                   const double *__restrict__ remote_lo, const double *__restrict__ remote_hi,
                   double *__restrict__ part, KrylovState *__restrict__ st, int den_step)
 {
-    constexpr int F = face_count<S>();
+    constexpr int S3 = S * S * S;
     constexpr int s1 = S - 1;
     __shared__ double sh[kRedThreads / 64];
     if (st->done) return;
@@ -660,8 +686,8 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         const int rem = gid - gz * plane;
         const int gy = (int)fdiv((uint32_t)rem, fdx);
         const int gx = rem - gy * g.Lx;
-        // every load is issued before any is consumed: which of q / the face partials holds this
-        // dof's row sum depends on its lattice position only, and the essential flag selects last
+        // every load is issued before any is consumed: which bricks' patch outputs hold this dof's
+        // row sum depends on its lattice position only, and the essential flag selects last
         const bool is_ess = ess[gid] != 0;
         // XF: x was advanced by the apply (x-fold); d is then needed on essential rows only
         const double di = (!XF || is_ess) ? d[gid] : 0.0, xi = XF ? 0.0 : x[gid];
@@ -687,10 +713,11 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
                 for (int ky = 0; ky < nyc; ++ky)
                     for (int kx = 0; kx < nxc; ++kx) {
                         const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
-                        qi += face[(size_t)bb * F + face_index<S>(pxs[kx], pys[ky], pzs[kz])];
+                        qi += pb[(size_t)bb * S3 + pxs[kx] + S * (pys[ky] + S * pzs[kz])];
                     }
-        } else {
-            qi = q[gid];
+        } else {  // inside one brick's patch
+            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
+            qi = pb[(size_t)(qx + g.nbx * (qy + g.nby * qz)) * S3 + (gx - qx * s1) + S * ((gy - qy * s1) + S * (gz - qz * s1))];
         }
         // interface planes: add the neighbour rank's partial sums
         if (remote_lo && gz == 0) qi += remote_lo[rem];
@@ -723,13 +750,14 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const dim3 grid((unsigned)(c->nbx * c->nby * run.nlay)), block(64);
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
     const double *qd = c->d_qaff ? c->d_qaff : c->d_qd;
-#define CDFEM_BCG(AFF_, W_)                                                                                  \
+#define CDFEM_BCG3(AFF_, W_, XF_)                                                                           \
     if (whole)                                                                                               \
-        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_>), grid, block, 0, r, dinv, d_old, d_new, q, c->d_face, \
-                     qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x);                           \
+        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_>), grid, block, 0, r, dinv, d_old, d_new, q,       \
+                     c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x);                \
     else                                                                                                     \
-        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_>), grid, block, 0, run.s, r, dinv, d_old, d_new, q, \
-                           c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x)
+        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_>), grid, block, 0, run.s, r, dinv, d_old, d_new, \
+                           q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x)
+#define CDFEM_BCG(AFF_, W_) CDFEM_BCG3(AFF_, W_, false)
     if (pa_af(c) == 2 && c->brick_cg_persist && !x) {
         // persistent grid: two waves per SIMD of the device (a multiple of 8: XCD ranges), at most
         // one workgroup per brick
@@ -744,13 +772,16 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
             hipLaunchKernelGGL((k_brick_cgp<D1, Q1, K>), dim3((unsigned)G), block, 0, run.s, r, dinv, d_old, d_new, q,
                                c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, nb);
     } else if (pa_af(c) == 2) {
-        if (c->brick_cg_waves == 3) { CDFEM_BCG(2, 3); } else { CDFEM_BCG(2, 2); }
+        if (x) { CDFEM_BCG3(2, 2, true); }
+        else if (c->brick_cg_waves == 3) { CDFEM_BCG(2, 3); }
+        else { CDFEM_BCG(2, 2); }
     } else if (pa_af(c) == 1) {
         CDFEM_BCG(1, 1);
     } else {
         CDFEM_BCG(0, 1);
     }
 #undef CDFEM_BCG
+#undef CDFEM_BCG3
     return hipGetLastError();
 }
 
@@ -804,12 +835,12 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     const unsigned grid = (unsigned)(need < 16384 ? need : 16384);
 #define CDFEM_UPD(S_)                                                                                       \
     if (xfold)                                                                                              \
-        hipLaunchKernelGGL((k_cg_update_faces<S_, true>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, q, \
-                           d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi,     \
+        hipLaunchKernelGGL((k_cg_update_faces<S_, true>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, d, \
+                           dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi,        \
                            c->d_part, c->d_state, (int)den_step);                                           \
     else                                                                                                    \
         hipLaunchKernelGGL((k_cg_update_faces<S_, false>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, \
-                           q, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, \
+                           d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi,     \
                            c->d_part, c->d_state, (int)den_step)
     if (c->p == 1) {
         CDFEM_UPD(kBrick * 1 + 1);
@@ -833,7 +864,7 @@ k_pack_qplanes(const double *__restrict__ q, const double *__restrict__ face, co
                int lo, int hi, double *__restrict__ out_lo, double *__restrict__ out_hi,
                const KrylovState *__restrict__ st)
 {
-    constexpr int F = face_count<S>();
+    constexpr int S3 = S * S * S;
     constexpr int s1 = S - 1;
     if (st->done) return;
     const int n = g.Lx * g.Ly;
@@ -864,10 +895,11 @@ k_pack_qplanes(const double *__restrict__ q, const double *__restrict__ face, co
                 for (int ky = 0; ky < nyc; ++ky)
                     for (int kx = 0; kx < nxc; ++kx) {
                         const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
-                        v += face[(size_t)bb * F + face_index<S>(pxs[kx], pys[ky], pzs[kz])];
+                        v += face[(size_t)bb * S3 + pxs[kx] + S * (pys[ky] + S * pzs[kz])];
                     }
-        } else {
-            v = q[gx + (int64_t)g.Lx * (gy + (int64_t)g.Ly * gz)];
+        } else {  // inside one brick's patch
+            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
+            v = face[(size_t)(qx + g.nbx * (qy + g.nby * qz)) * S3 + (gx - qx * s1) + S * ((gy - qy * s1) + S * (gz - qz * s1))];
         }
         (side == 0 ? out_lo : out_hi)[k] = v;
     }

@@ -419,7 +419,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     // x-fold (set_option "cg_xfold", default): every apply after the first advances x by the previous
     // iteration's alpha d (the update kernel then streams neither x nor d); k_cg_xflush adds the
     // last update's term after the loop when the update logic stopped the solve
-    const bool xfold = c->cg_xfold != 0;
+    const bool xfold = c->cg_xfold != 0 && pa_af(c) == 2 && c->brick_cg_persist == 0;  // Kronecker kernel only
     double *const dbuf0 = dcur, *const dbuf1 = dprev;  // apply j writes d_j into dbuf[(j - 1) & 1]
     int napply = 0;
     auto apply = [&] {
@@ -890,7 +890,8 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
         const int S = kBrick * p + 1;
         c->nface = 2 * S * S + (S - 2) * (4 * S - 4);
         dfree(c->d_face);
-        c->d_face = dalloc<double>((size_t)c->nblk * c->nface);
+        // per brick: the Mult's face partials (nface) or the CG apply's whole patch output (S^3)
+        c->d_face = dalloc<double>((size_t)c->nblk * std::max(c->nface, S * S * S));
         dfree(c->d_qd);
         c->structured = true;
         c->pa_ready = false;
@@ -1831,18 +1832,19 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
                     if (z % s1 == 0 || y % s1 == 0) { nface_dofs += c->Lx; continue; }
                     nface_dofs += (c->Lx - 1) / s1 + 1;
                 }
-            const double nf = (double)nface_dofs, nown = nl - nf;
-            const double partials = 8.0 * c->nface * (double)c->nblk;
+            const double nf = (double)nface_dofs;
+            const double S = kBrick * c->p + 1.0;
+            const double patches = 8.0 * S * S * S * (double)c->nblk;  // the CG apply's patch outputs
             switch (k) {
             case CDFEM_K_APPLY:   // qdata (or per-element affine factors) + gathered r, M^-1, d + ess
-                                  // flags + owned d, q + face partials
-                *bytes = 8.0 * c->ncomp * (c->d_qaff ? 1.0 : nq) * ne + 24.0 * nl + 1.0 * nl + 16.0 * nown + partials;
+                                  // flags + d (each dof by its one writer brick) + patch outputs
+                *bytes = 8.0 * c->ncomp * (c->d_qaff ? 1.0 : nq) * ne + 24.0 * nl + 1.0 * nl + 8.0 * nl + patches;
                 return CDFEM_OK;
-            case CDFEM_K_E2L:     // face partials + r, M^-1, d, ess of face dofs + d, q of face dofs
-                *bytes = partials + 25.0 * nf + 16.0 * nf;
+            case CDFEM_K_E2L:     // (the Mult's face-partial sum) face partials + x, ess, y of face dofs
+                *bytes = 8.0 * c->nface * (double)c->nblk + 25.0 * nf;
                 return CDFEM_OK;
-            case CDFEM_K_UPDATE:  // x, d, r, q, M^-1 read; x, r write
-                *bytes = 56.0 * nl;
+            case CDFEM_K_UPDATE:  // x, d, r, M^-1 read, ess, x, r write + the patch outputs (each once)
+                *bytes = 49.0 * nl + patches;
                 return CDFEM_OK;
             default: throw ArgError("kernel not launched on the brick path");
             }
