@@ -83,6 +83,15 @@ __device__ __forceinline__ int face_index(int a, int b, int c)
 template <int S>
 constexpr int face_count() { return 2 * S * S + (S - 2) * (4 * S - 4); }
 
+// The CG apply's patch-output buffer, x rows of the brick lattice contiguous ([bz][pz][by][py][bx][px]):
+// a brick writes 81 runs of S, and the update kernel's wave over a lattice x row reads one contiguous
+// run (each dof's 1-8 entries: its own brick's, plus the neighbours' on brick faces)
+template <int S>
+__device__ __forceinline__ size_t patch_idx(const BrickGeom &g, int bx, int by, int bz, int px, int py, int pz)
+{
+    return ((((size_t)bz * S + pz) * g.nby + by) * S + py) * ((size_t)g.nbx * S) + (size_t)bx * S + px;
+}
+
 // v unchanged, but opaque to the optimiser: index arithmetic that depends on it cannot be hoisted
 // above this point (LLVM otherwise computes a later phase's per-position indices at kernel entry
 // and spills them across the element apply)
@@ -527,128 +536,21 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
             for (int dx = 0; dx < D1; ++dx) den += s_in[o0 + dz * S2 + dy * S + dx] * Y[dz][dy][dx];
     brick_e2l<D1, S>(s_out, o0, Y);
 
-    // the brick's whole patch output (interior rows complete, face rows partial) -> its slot of the
-    // patch buffer: contiguous stores; k_cg_update_faces sums each dof's 1-8 patch entries
-    double *const pbo = face + (size_t)b * S3;
+    // the brick's whole patch output (interior rows complete, face rows partial) -> the patch buffer
+    // (patch_idx); k_cg_update_faces sums each dof's 1-8 patch entries
+    {
+        const unsigned to = (unsigned)opaque(t);
+        PatchWalk<S> pw(to);
 #pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int i = t + 64 * k;
-        if (k == NI - 1 && i >= S3) break;
-        pbo[i] = s_out[i];
+        for (int k = 0; k < NI; ++k) {
+            const unsigned i = to + 64 * k;
+            if (k == NI - 1 && i >= S3) break;
+            face[patch_idx<S>(g, bx, by, bz, pw.x, pw.y, pw.z)] = s_out[i];
+            pw.next();
+        }
     }
     den = wave_sum(den);
     if (t == 0) part[b] = den;
-}
-
-// k_brick_cg as a persistent grid (Kronecker form, set_option "brick_cg_persist", default): a
-// workgroup runs bricks bl = blockIdx.x, + G, + 2G, ... (G = two waves per SIMD of the device,
-// a multiple of 8, so every brick of a workgroup stays on its XCD's contiguous range).  As soon as a
-// brick's patch is combined into LDS, the loads of the NEXT brick's patch (r, M^-1, d_old, ess) are
-// issued into the registers just consumed, behind the factor loads of the current one, so the
-// patch latency of every brick after the first runs under the element apply of the one before;
-// with one brick per wave every wave of the chip gathers at once and then computes at once.
-// Same arithmetic as k_brick_cg, bitwise.
-template <int D1, int Q1, unsigned K>
-__global__ void __launch_bounds__(64, 2)
-k_brick_cgp(const double *__restrict__ r, const double *__restrict__ dinv,
-            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
-            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
-            const Tab<D1, Q1> T, const BrickGeom g, int zlo_shared, double *__restrict__ part,
-            const KrylovState *__restrict__ st, int nb)
-{
-    constexpr int P = D1 - 1;
-    constexpr int S = kBrick * P + 1;
-    constexpr int S2 = S * S, S3 = S * S * S;
-    constexpr int NC = QLayout<K, 3>::nc;
-    constexpr int NI = (S3 + 63) / 64;
-    __shared__ double s_in[S3];
-    __shared__ double s_out[S3];
-    if (st->done) return;
-    const double beta = st->beta;
-    const int t = threadIdx.x;
-    const int G = gridDim.x, nxy = g.nbx * g.nby;
-    const int Lx = g.Lx, Lxy = g.Lx * g.Ly;
-    const unsigned nq8 = (unsigned)nb / 8, nr8 = (unsigned)nb % 8;
-    // launch-local brick bl -> global brick (contiguous range per XCD: XCD of bl = bl % 8)
-    auto brick_of = [&](int bl) {
-        const unsigned x8 = (unsigned)bl % 8, k8 = (unsigned)bl / 8;
-        const int lin = (int)(x8 * nq8 + (x8 < nr8 ? x8 : nr8) + k8);
-        const int bz = g.bz0 + (lin / nxy) * g.bzs;
-        return lin % nxy + nxy * bz;
-    };
-    double rv[NI], mv[NI], ov[NI];
-    uint8_t ev[NI];
-    auto issue = [&](int b) {
-        const int bx = b % g.nbx, by = (b / g.nbx) % g.nby, bz = b / nxy;
-        const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-            const unsigned i = t + 64 * k;
-            const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
-            const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-            const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
-            const int gid = in ? gx + Lx * gy + Lxy * gz : 0;
-            rv[k] = r[gid];
-            mv[k] = dinv[gid];
-            ov[k] = d_old[gid];
-            ev[k] = ess[gid];
-        }
-    };
-    int bl = blockIdx.x;
-    if (bl >= nb) return;
-    issue(brick_of(bl));
-    for (; bl < nb; bl += G) {
-        const int b = brick_of(bl);
-        const int bx = b % g.nbx, by = (b / g.nbx) % g.nby, bz = b / nxy;
-        const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
-        const bool lastx = bx == g.nbx - 1, lasty = by == g.nby - 1, lastz = bz == g.nbz - 1;
-        double den = 0.0;
-        // combine the patch (the loads issued one brick earlier) into LDS
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-            const unsigned i = t + 64 * k;
-            if (k == NI - 1 && i >= S3) break;
-            const int px = (int)(i % S), py = (int)((i / S) % S), pz = (int)(i / S2);
-            const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-            const bool in = gx < g.Lx && gy < g.Ly && gz < g.Lz;
-            const double dn = mv[k] * rv[k] + beta * ov[k];
-            const bool e = ev[k] != 0;
-            const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
-            if (writer) d_new[gx + Lx * gy + Lxy * gz] = dn;
-            den += (writer && e && !(zlo_shared && gz == 0)) ? dn * dn : 0.0;  // (A_c d)_i = d_i on ess dofs
-            s_in[i] = (in && !e) ? dn : 0.0;
-            s_out[i] = 0.0;
-        }
-        __syncthreads();
-        // this brick's factors first, then the next brick's patch: the apply waits for the factors only
-        double gf[NC];
-        kron_load_g<K>(qd + (size_t)b * NC * kLanes, t, gf);
-        if (bl + G < nb) issue(brick_of(bl + G));
-
-        const int ex = t & 3, ey = (t >> 2) & 3, ez = t >> 4;
-        const int o0 = P * ez * S2 + P * ey * S + P * ex;
-        auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
-        double Y[D1][D1][D1];
-        kron_core<D1, Q1, K>(xl, gf, T, Y);
-#pragma unroll
-        for (int dz = 0; dz < D1; ++dz)
-#pragma unroll
-            for (int dy = 0; dy < D1; ++dy)
-#pragma unroll
-                for (int dx = 0; dx < D1; ++dx) den += s_in[o0 + dz * S2 + dy * S + dx] * Y[dz][dy][dx];
-        brick_e2l<D1, S>(s_out, o0, Y);
-
-        double *const pbo = face + (size_t)b * S3;
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-            const int i = t + 64 * k;
-            if (k == NI - 1 && i >= S3) break;
-            pbo[i] = s_out[i];
-        }
-        den = wave_sum(den);
-        if (t == 0) part[b] = den;
-        __syncthreads();  // the next combine overwrites s_in / s_out
-    }
 }
 
 template <int S, bool XF>
@@ -660,7 +562,6 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
                   const double *__restrict__ remote_lo, const double *__restrict__ remote_hi,
                   double *__restrict__ part, KrylovState *__restrict__ st, int den_step)
 {
-    constexpr int S3 = S * S * S;
     constexpr int s1 = S - 1;
     __shared__ double sh[kRedThreads / 64];
     if (st->done) return;
@@ -712,12 +613,11 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
             for (int kz = 0; kz < nzc; ++kz)
                 for (int ky = 0; ky < nyc; ++ky)
                     for (int kx = 0; kx < nxc; ++kx) {
-                        const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
-                        qi += pb[(size_t)bb * S3 + pxs[kx] + S * (pys[ky] + S * pzs[kz])];
+                        qi += pb[patch_idx<S>(g, bxs[kx], bys[ky], bzs[kz], pxs[kx], pys[ky], pzs[kz])];
                     }
         } else {  // inside one brick's patch
             const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
-            qi = pb[(size_t)(qx + g.nbx * (qy + g.nby * qz)) * S3 + (gx - qx * s1) + S * ((gy - qy * s1) + S * (gz - qz * s1))];
+            qi = pb[patch_idx<S>(g, qx, qy, qz, gx - qx * s1, gy - qy * s1, gz - qz * s1)];
         }
         // interface planes: add the neighbour rank's partial sums
         if (remote_lo && gz == 0) qi += remote_lo[rem];
@@ -758,20 +658,7 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
         hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_>), grid, block, 0, run.s, r, dinv, d_old, d_new, \
                            q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x)
 #define CDFEM_BCG(AFF_, W_) CDFEM_BCG3(AFF_, W_, false)
-    if (pa_af(c) == 2 && c->brick_cg_persist && !x) {
-        // persistent grid: two waves per SIMD of the device (a multiple of 8: XCD ranges), at most
-        // one workgroup per brick
-        const int nb = (int)grid.x;
-        int G = 8 * c->ncu;
-        if (G <= 0) G = 2048;
-        if (G > ((nb + 7) / 8) * 8) G = ((nb + 7) / 8) * 8;
-        if (whole)
-            CDFEM_LAUNCH(c, (k_brick_cgp<D1, Q1, K>), dim3((unsigned)G), block, 0, r, dinv, d_old, d_new, q, c->d_face,
-                         qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, nb);
-        else
-            hipLaunchKernelGGL((k_brick_cgp<D1, Q1, K>), dim3((unsigned)G), block, 0, run.s, r, dinv, d_old, d_new, q,
-                               c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, nb);
-    } else if (pa_af(c) == 2) {
+    if (pa_af(c) == 2) {
         if (x) { CDFEM_BCG3(2, 2, true); }
         else if (c->brick_cg_waves == 3) { CDFEM_BCG(2, 3); }
         else { CDFEM_BCG(2, 2); }
@@ -864,7 +751,6 @@ k_pack_qplanes(const double *__restrict__ q, const double *__restrict__ face, co
                int lo, int hi, double *__restrict__ out_lo, double *__restrict__ out_hi,
                const KrylovState *__restrict__ st)
 {
-    constexpr int S3 = S * S * S;
     constexpr int s1 = S - 1;
     if (st->done) return;
     const int n = g.Lx * g.Ly;
@@ -894,12 +780,11 @@ k_pack_qplanes(const double *__restrict__ q, const double *__restrict__ face, co
             for (int kz = 0; kz < nzc; ++kz)
                 for (int ky = 0; ky < nyc; ++ky)
                     for (int kx = 0; kx < nxc; ++kx) {
-                        const int bb = bxs[kx] + g.nbx * (bys[ky] + g.nby * bzs[kz]);
-                        v += face[(size_t)bb * S3 + pxs[kx] + S * (pys[ky] + S * pzs[kz])];
+                        v += face[patch_idx<S>(g, bxs[kx], bys[ky], bzs[kz], pxs[kx], pys[ky], pzs[kz])];
                     }
         } else {  // inside one brick's patch
             const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
-            v = face[(size_t)(qx + g.nbx * (qy + g.nby * qz)) * S3 + (gx - qx * s1) + S * ((gy - qy * s1) + S * (gz - qz * s1))];
+            v = face[patch_idx<S>(g, qx, qy, qz, gx - qx * s1, gy - qy * s1, gz - qz * s1)];
         }
         (side == 0 ? out_lo : out_hi)[k] = v;
     }

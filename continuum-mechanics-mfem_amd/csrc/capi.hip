@@ -419,7 +419,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     // x-fold (set_option "cg_xfold", default): every apply after the first advances x by the previous
     // iteration's alpha d (the update kernel then streams neither x nor d); k_cg_xflush adds the
     // last update's term after the loop when the update logic stopped the solve
-    const bool xfold = c->cg_xfold != 0 && pa_af(c) == 2 && c->brick_cg_persist == 0;  // Kronecker kernel only
+    const bool xfold = c->cg_xfold != 0 && pa_af(c) == 2;  // Kronecker kernel only
     double *const dbuf0 = dcur, *const dbuf1 = dprev;  // apply j writes d_j into dbuf[(j - 1) & 1]
     int napply = 0;
     auto apply = [&] {
@@ -1658,10 +1658,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
     return guarded(c, [&] {
         if (!key) throw ArgError("key is null");
         const std::string k(key);
-        if (k == "brick_cg_persist") {
-            if (value != 0 && value != 1) throw ArgError("brick_cg_persist must be 0 or 1");
-            c->brick_cg_persist = value;
-        } else if (k == "brick_cg_waves") {
+        if (k == "brick_cg_waves") {
             if (value != 2 && value != 3) throw ArgError("brick_cg_waves must be 2 or 3");
             c->brick_cg_waves = value;
         } else if (k == "brick_xcd") {
