@@ -79,4 +79,35 @@ __device__ inline void cg_den_step(KrylovState *st, double den)
     }
 }
 
+// MFEM CGSolver after betanom = (r, z): convergence test, iteration bound, beta
+__device__ inline void cg_update_logic(KrylovState *st, double betanom)
+{
+    st->betanom = betanom;
+    const int i = st->iter;
+    if (betanom < 0.0) {
+        st->done = 1; st->converged = 0; st->final_iter = i; st->xflush = 1;
+    } else if (betanom <= st->r0) {
+        st->done = 1; st->converged = 1; st->final_iter = i; st->xflush = 1;
+    } else if (i + 1 > st->max_iter) {
+        st->done = 1; st->converged = 0; st->final_iter = st->max_iter; st->xflush = 1;
+    } else {
+        st->beta = betanom / st->nom;
+        st->iter = i + 1;
+    }
+}
+
+// every block's copy of sum(part[0..n)), in one fixed order (so all blocks hold the same bits):
+// thread t adds part[t], part[t + bd], ... (loads issued kB at a time), then the block tree;
+// the result is returned in every thread (sh: >= blockDim / 64 + 1 doubles)
+__device__ inline double sum_partials_all(const double *part, int n, double *sh)
+{
+    const double v = sum_partials(part, n, sh);
+    __syncthreads();
+    if (threadIdx.x == 0) sh[0] = v;
+    __syncthreads();
+    const double r = sh[0];
+    __syncthreads();
+    return r;
+}
+
 }  // namespace cdfem

@@ -270,22 +270,6 @@ __device__ inline void cg_init_logic(KrylovState *st, double nom, double rel_tol
     }
 }
 
-// MFEM CGSolver after betanom = (r, z): convergence test, iteration bound, beta
-__device__ inline void cg_update_logic(KrylovState *st, double betanom)
-{
-    st->betanom = betanom;
-    const int i = st->iter;
-    if (betanom < 0.0) {
-        st->done = 1; st->converged = 0; st->final_iter = i; st->xflush = 1;
-    } else if (betanom <= st->r0) {
-        st->done = 1; st->converged = 1; st->final_iter = i; st->xflush = 1;
-    } else if (i + 1 > st->max_iter) {
-        st->done = 1; st->converged = 0; st->final_iter = st->max_iter; st->xflush = 1;
-    } else {
-        st->beta = betanom / st->nom;
-        st->iter = i + 1;
-    }
-}
 
 // one block: nom = sum of the init partials; MFEM CGSolver initial convergence test
 __global__ void __launch_bounds__(1024)
