@@ -553,15 +553,19 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     brick_e2l<D1, S>(s_out, o0, Y);
 
     // the brick's whole patch output (interior rows complete, face rows partial) -> the patch buffer
-    // (patch_idx); k_cg_update_faces sums each dof's 1-8 patch entries
+    // (patch_idx, here in 32-bit arithmetic with the brick's part uniform: index = base + pz A + py R
+    // + px); k_cg_update_faces sums each dof's 1-8 patch entries
     {
+        const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
+        const uint32_t base = (uint32_t)bz * S * A + (uint32_t)by * S * R + (uint32_t)bx * S;
+        const auto bp = brsrc(face, 8u * (uint32_t)g.nbx * g.nby * g.nbz * S3);
         const unsigned to = (unsigned)opaque(t);
         PatchWalk<S> pw(to);
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             const unsigned i = to + 64 * k;
             if (k == NI - 1 && i >= S3) break;
-            face[patch_idx<S>(g, bx, by, bz, pw.x, pw.y, pw.z)] = s_out[i];
+            bstore(bp, 8u * (base + (uint32_t)pw.z * A + (uint32_t)pw.y * R + (uint32_t)pw.x), s_out[i]);
             pw.next();
         }
     }

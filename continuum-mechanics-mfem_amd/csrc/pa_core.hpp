@@ -301,21 +301,114 @@ __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restr
 // jz: x stage (M, K, C, Ct on the plane's rows), the per-element combinations, y stage into the four
 // z groups (M, K, C, Ct), z stage into Y.  At p = 2: 1.73 K FMA-class operations per element against
 // 4.3 K for the quadrature form (elem_apply3d<..., AFF>), 45 + 27 live doubles.
+// The two halves of the Kronecker form, shared by the thread-per-element core (kron_core) and the
+// high-order tile kernel (ho_kernels.hip k_apply3d_ktile).
+// x stage of one input row X[jz][jy][*] for output column ix: the five x-applied quantities
+//   v[0] = (M X)_ix, v[1] = (C X)_ix, v[2] = u1 = s M + D_xx K + c_x C, v[3] = u3 = D_xy Ct + c_y M,
+//   v[4] = u5 = D_xz Ct + c_z M   (applied along x)
+template <int D1, int Q1, unsigned K>
+__device__ __forceinline__ void kron_xrow(const Tab<D1, Q1> &T, const double (&g)[QLayout<K, 3>::nc],
+                                          const double (&X)[D1], int ix, double (&v)[5])
+{
+    using L = QLayout<K, 3>;
+    constexpr bool kD = L::kD, kC = L::kC, kM = L::kM, kG = L::kD || L::kC;
+    double m = 0.0, k = 0.0, c = 0.0, ct = 0.0;
+#pragma unroll
+    for (int jx = 0; jx < D1; ++jx) {
+        m += tM(T, ix, jx) * X[jx];
+        if constexpr (kD) {
+            k += tK(T, ix, jx) * X[jx];
+            ct = tCacc(T, jx, ix, X[jx], ct);
+        }
+        if constexpr (kG) c = tCacc(T, ix, jx, X[jx], c);
+    }
+    v[0] = m;
+    v[1] = c;
+    double a = 0.0;
+    if constexpr (kM) a = g[L::oM] * m;
+    if constexpr (kD) a += g[0] * k;
+    if constexpr (kC) a += g[L::oC] * c;
+    v[2] = a;
+    v[3] = v[4] = 0.0;
+    if constexpr (kD && kC) {
+        v[3] = g[1] * ct + g[L::oC + 1] * m;
+        v[4] = g[2] * ct + g[L::oC + 2] * m;
+    } else if constexpr (kD) {
+        v[3] = g[1] * ct;
+        v[4] = g[2] * ct;
+    } else if constexpr (kC) {
+        v[3] = g[L::oC + 1] * m;
+        v[4] = g[L::oC + 2] * m;
+    }
+}
+
+// y stage of one output column (the x-stage quantities col(q, jy) of kron_xrow, q = 0..4, for every
+// input row jy of plane jz) into the four z groups, then the z stage into Yz[iz] (this (iy, ix))
+template <int D1, int Q1, unsigned K, typename COL>
+__device__ __forceinline__ void kron_yz(const Tab<D1, Q1> &T, const double (&g)[QLayout<K, 3>::nc], const COL &col,
+                                        int iy, int jz, double (&Yz)[D1])
+{
+    using L = QLayout<K, 3>;
+    constexpr bool kD = L::kD, kG = L::kD || L::kC;
+    double pm = 0.0, pk = 0.0, pc = 0.0, pct = 0.0;
+    {
+        double s1 = 0.0;
+#pragma unroll
+        for (int jy = 0; jy < D1; ++jy) s1 += tM(T, iy, jy) * col(2, jy);
+        pm = s1;
+    }
+    if constexpr (kG) {
+        double s3 = 0.0, s5 = 0.0;
+#pragma unroll
+        for (int jy = 0; jy < D1; ++jy) {
+            s3 = tCacc(T, iy, jy, col(3, jy), s3);
+            s5 += tM(T, iy, jy) * col(4, jy);
+        }
+        pm += s3;
+        pc = s5;
+    }
+    if constexpr (kD) {
+        double kym = 0.0, ctyc = 0.0, mym = 0.0, ctym = 0.0, myc = 0.0, cym = 0.0;
+#pragma unroll
+        for (int jy = 0; jy < D1; ++jy) {
+            const double xm = col(0, jy), xc = col(1, jy);
+            kym += tK(T, iy, jy) * xm;
+            ctyc = tCacc(T, jy, iy, xc, ctyc);
+            mym += tM(T, iy, jy) * xm;
+            ctym = tCacc(T, jy, iy, xm, ctym);
+            myc += tM(T, iy, jy) * xc;
+            cym = tCacc(T, iy, jy, xm, cym);
+        }
+        pm += g[3] * kym;
+        pm += g[1] * ctyc;
+        pk = g[5] * mym;
+        pc += g[4] * ctym;
+        pct = g[2] * myc + g[4] * cym;
+    }
+#pragma unroll
+    for (int iz = 0; iz < D1; ++iz) {
+        double y = Yz[iz];
+        y += tM(T, iz, jz) * pm;
+        if constexpr (kD) {
+            y += tK(T, iz, jz) * pk;
+            y = tCacc(T, jz, iz, pct, y);
+        }
+        if constexpr (kG) y = tCacc(T, iz, jz, pc, y);
+        Yz[iz] = y;
+    }
+}
+
 // g: the element's factors (QLayout<K, 3> order), loaded by the caller (kron_load_g)
 template <int D1, int Q1, unsigned K, typename XL>
 __device__ __forceinline__ void kron_core(const XL &xl, const double (&g)[QLayout<K, 3>::nc], const Tab<D1, Q1> &T,
                                           double (&Y)[D1][D1][D1])
 {
-    using L = QLayout<K, 3>;
-    constexpr bool kD = L::kD, kC = L::kC, kM = L::kM, kG = L::kD || L::kC;
-    // D = [[g0 g1 g2] [g1 g3 g4] [g2 g4 g5]], c = g[oC..oC+2], s = g[oM]
 #pragma unroll
     for (int dz = 0; dz < D1; ++dz)
 #pragma unroll
         for (int dy = 0; dy < D1; ++dy)
 #pragma unroll
             for (int dx = 0; dx < D1; ++dx) Y[dz][dy][dx] = 0.0;
-
 #pragma unroll
     for (int jz = 0; jz < D1; ++jz) {
         double X[D1][D1];
@@ -324,89 +417,21 @@ __device__ __forceinline__ void kron_core(const XL &xl, const double (&g)[QLayou
 #pragma unroll
             for (int jx = 0; jx < D1; ++jx) X[jy][jx] = xl(jz, jy, jx);
         // one output column ix at a time (x stage of that column for every row jy, then the y and z
-        // stages of the column), so only one column's intermediates are live:
-        //   u1 = s M + D_xx K + c_x C,  u3 = D_xy Ct + c_y M,  u5 = D_xz Ct + c_z M  (applied along x)
+        // stages of the column), so only one column's intermediates are live
 #pragma unroll
         for (int ix = 0; ix < D1; ++ix) {
-            double xm[D1], xc[D1], u1[D1], u3[D1], u5[D1];
+            double v[D1][5];
 #pragma unroll
-            for (int jy = 0; jy < D1; ++jy) {
-                double m = 0.0, k = 0.0, c = 0.0, ct = 0.0;
-#pragma unroll
-                for (int jx = 0; jx < D1; ++jx) {
-                    m += tM(T, ix, jx) * X[jy][jx];
-                    if constexpr (kD) {
-                        k += tK(T, ix, jx) * X[jy][jx];
-                        ct = tCacc(T, jx, ix, X[jy][jx], ct);
-                    }
-                    if constexpr (kG) c = tCacc(T, ix, jx, X[jy][jx], c);
-                }
-                xm[jy] = m;
-                xc[jy] = c;
-                double a = 0.0;
-                if constexpr (kM) a = g[L::oM] * m;
-                if constexpr (kD) a += g[0] * k;
-                if constexpr (kC) a += g[L::oC] * c;
-                u1[jy] = a;
-                if constexpr (kD && kC) {
-                    u3[jy] = g[1] * ct + g[L::oC + 1] * m;
-                    u5[jy] = g[2] * ct + g[L::oC + 2] * m;
-                } else if constexpr (kD) {
-                    u3[jy] = g[1] * ct;
-                    u5[jy] = g[2] * ct;
-                } else if constexpr (kC) {
-                    u3[jy] = g[L::oC + 1] * m;
-                    u5[jy] = g[L::oC + 2] * m;
-                }
-            }
-            // y stage into the z groups (M, K, C, Ct), then the z stage
+            for (int jy = 0; jy < D1; ++jy) kron_xrow<D1, Q1, K>(T, g, X[jy], ix, v[jy]);
+            auto col = [&](int q, int jy) { return v[jy][q]; };
 #pragma unroll
             for (int iy = 0; iy < D1; ++iy) {
-                double pm = 0.0, pk = 0.0, pc = 0.0, pct = 0.0;
-                {
-                    double s1 = 0.0;
+                double Yz[D1];
 #pragma unroll
-                    for (int jy = 0; jy < D1; ++jy) s1 += tM(T, iy, jy) * u1[jy];
-                    pm = s1;
-                }
-                if constexpr (kG) {
-                    double s3 = 0.0, s5 = 0.0;
+                for (int iz = 0; iz < D1; ++iz) Yz[iz] = Y[iz][iy][ix];
+                kron_yz<D1, Q1, K>(T, g, col, iy, jz, Yz);
 #pragma unroll
-                    for (int jy = 0; jy < D1; ++jy) {
-                        s3 = tCacc(T, iy, jy, u3[jy], s3);
-                        s5 += tM(T, iy, jy) * u5[jy];
-                    }
-                    pm += s3;
-                    pc = s5;
-                }
-                if constexpr (kD) {
-                    double kym = 0.0, ctyc = 0.0, mym = 0.0, ctym = 0.0, myc = 0.0, cym = 0.0;
-#pragma unroll
-                    for (int jy = 0; jy < D1; ++jy) {
-                        kym += tK(T, iy, jy) * xm[jy];
-                        ctyc = tCacc(T, jy, iy, xc[jy], ctyc);
-                        mym += tM(T, iy, jy) * xm[jy];
-                        ctym = tCacc(T, jy, iy, xm[jy], ctym);
-                        myc += tM(T, iy, jy) * xc[jy];
-                        cym = tCacc(T, iy, jy, xm[jy], cym);
-                    }
-                    pm += g[3] * kym;
-                    pm += g[1] * ctyc;
-                    pk = g[5] * mym;
-                    pc += g[4] * ctym;
-                    pct = g[2] * myc + g[4] * cym;
-                }
-#pragma unroll
-                for (int iz = 0; iz < D1; ++iz) {
-                    double y = Y[iz][iy][ix];
-                    y += tM(T, iz, jz) * pm;
-                    if constexpr (kD) {
-                        y += tK(T, iz, jz) * pk;
-                        y = tCacc(T, jz, iz, pct, y);
-                    }
-                    if constexpr (kG) y = tCacc(T, iz, jz, pc, y);
-                    Y[iz][iy][ix] = y;
-                }
+                for (int iz = 0; iz < D1; ++iz) Y[iz][iy][ix] = Yz[iz];
             }
         }
     }

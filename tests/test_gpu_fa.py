@@ -494,3 +494,27 @@ def test_fa_reordered_space_solves(gpu_ctx, order):
             assert np.abs(new[k] - base[k]).max() <= 1e-12 * np.abs(base[k]).max(), k
     finally:
         gpu_ctx.set_option("sell_order", 8)
+
+
+def test_lds_spmv_grid_bound(gpu_ctx):
+    """the LDS-staged SpMV launches one workgroup per window and its CG form writes one
+    partial per workgroup, so the window count must fit the partial slots (kSpmvMaxBlocks = 65536).
+    With 64-row windows (spmv_lds 64, one lane per row) a P2 Kuhn mesh of 82^3 cubes has
+    165^3 = 4.49 M rows = 70.2 K windows: an explicit choice is refused with a message (no write past
+    the partial buffer), and the automatic layout on the same mesh sets up and applies normally."""
+    m = cdfem.kuhn_mesh(3, 82, 2, with_coords=True)
+    assert m.nl > 64 * 65536
+    try:
+        gpu_ctx.set_option("spmv_lds", 64)
+        gpu_ctx.set_option("spmv_lpr", 1)
+        gpu_ctx.upload_mesh(m)
+        with pytest.raises(cdfem.CdfemError, match="exceed the SpMV grid"):
+            gpu_ctx.fa_setup(kinds=cdfem.DIFFUSION | cdfem.MASS, kappa=0.1, mass=1.0)
+    finally:
+        gpu_ctx.set_option("spmv_lds", -1)
+        gpu_ctx.set_option("spmv_lpr", 0)
+    gpu_ctx.upload_mesh(m)
+    gpu_ctx.fa_setup(kinds=cdfem.DIFFUSION | cdfem.MASS, kappa=0.1, mass=1.0)
+    x = np.ones(m.nl)
+    y = gpu_ctx.mult(x)
+    assert np.isfinite(y).all()
