@@ -436,18 +436,13 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // ================================================================================================
 // W: waves per SIMD the register allocation targets (set_option "brick_cg_waves"; the Kronecker
 // form fits 2 without spills, 3 with a few spilled scalars; the point-data forms take 1)
-// FF (fused finalizers, set_option "cg_fused_fin", one rank): the betanom step of the previous
-// iteration runs here instead of in a one-block kernel: every workgroup sums the update kernel's
-// nupart partials (upart) in one fixed order and takes MFEM's decision (cg_update_logic) itself;
-// workgroup 0 records it in the state.  kk = the number of updates so far (0: the first apply).
-template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false, bool FF = false>
+template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false>
 __global__ void __launch_bounds__(64, W)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
            const Tab<D1, Q1> T, const BrickGeom g, int zlo_shared, double *__restrict__ part,
-           KrylovState *__restrict__ st, double *__restrict__ x, const double *__restrict__ upart,
-           int nupart, int kk)
+           const KrylovState *__restrict__ st, double *__restrict__ x)
 {
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
@@ -457,18 +452,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     __shared__ double s_in[S3];
     __shared__ double s_out[S3];
     if (st->done) return;
-    double beta = st->beta;
-    if constexpr (FF) {
-        if (kk > 0) {
-            __shared__ double sh_ff[2];
-            const double B = sum_partials_all(upart, nupart, sh_ff);
-            // cg_update_logic's decision, taken identically by every workgroup
-            const bool stop = B < 0.0 || B <= st->r0 || kk + 1 > st->max_iter;
-            if (blockIdx.x == 0 && threadIdx.x == 0) cg_update_logic(st, B);
-            if (stop) return;
-            beta = B / st->nom;
-        }
-    }
+    const double beta = st->beta;
     // x-fold (XF, set_option "cg_xfold"): the previous iteration's x += alpha d_old, for the dofs
     // this brick writes d_new for (each dof has exactly one writer brick); the update kernel then
     // leaves x alone.  Bitwise the unfolded update (same fma on the same values).  A template flag:
@@ -652,87 +636,12 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
     if (threadIdx.x == 0) part[blockIdx.x] = bs;
 }
 
-// The update with the den step folded in (set_option "cg_fused_fin", one rank): every workgroup sums
-// the apply's napart den partials (apart) in one fixed order, takes MFEM's den step itself
-// (workgroup 0 records it, cg_den_step) and covers the lattice with a grid-stride loop, so a grid of
-// a few thousand workgroups keeps the redundant partial sums small; its own partials go to part.
-template <int S, bool XF>
-__global__ void __launch_bounds__(kRedThreads)
-k_cg_update_ff(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ d,
-               const double *__restrict__ dinv, const double *__restrict__ pb,
-               const uint8_t *__restrict__ ess, const BrickGeom g,
-               const FastDiv fdx, const FastDiv fdxy, int zlo_shared,
-               const double *__restrict__ apart, int napart, double *__restrict__ part,
-               KrylovState *__restrict__ st)
-{
-    constexpr int s1 = S - 1;
-    __shared__ double sh[kRedThreads / 64 + 1];
-    if (st->done) return;
-    const double den = sum_partials_all(apart, napart, sh);
-    if (blockIdx.x == 0 && threadIdx.x == 0) cg_den_step(st, den);
-    if (den == 0.0) return;
-    const double alpha = st->betanom / den;  // = cg_den_step's nom / den
-    const double *remote_lo = nullptr, *remote_hi = nullptr;
-    const int n = g.Lx * g.Ly * g.Lz;
-    const int plane = g.Lx * g.Ly;
-    double acc = 0.0;
-#pragma unroll 2
-    for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += gridDim.x * blockDim.x) {
-        const int gz = (int)fdiv((uint32_t)gid, fdxy);
-        const int rem = gid - gz * plane;
-        const int gy = (int)fdiv((uint32_t)rem, fdx);
-        const int gx = rem - gy * g.Lx;
-        // every load is issued before any is consumed: which bricks' patch outputs hold this dof's
-        // row sum depends on its lattice position only, and the essential flag selects last
-        const bool is_ess = ess[gid] != 0;
-        // XF: x was advanced by the apply (x-fold); d is then needed on essential rows only
-        const double di = (!XF || is_ess) ? d[gid] : 0.0, xi = XF ? 0.0 : x[gid];
-        const double rold = r[gid], mi = dinv[gid];
-        double qi;
-        if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
-            int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
-            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
-            if (gx - qx * s1 == 0) {
-                if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
-                if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
-            } else { bxs[0] = qx; pxs[0] = gx - qx * s1; nxc = 1; }
-            if (gy - qy * s1 == 0) {
-                if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
-                if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
-            } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
-            if (gz - qz * s1 == 0) {
-                if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
-                if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
-            } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
-            qi = 0.0;
-            for (int kz = 0; kz < nzc; ++kz)
-                for (int ky = 0; ky < nyc; ++ky)
-                    for (int kx = 0; kx < nxc; ++kx) {
-                        qi += pb[patch_idx<S>(g, bxs[kx], bys[ky], bzs[kz], pxs[kx], pys[ky], pzs[kz])];
-                    }
-        } else {  // inside one brick's patch
-            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
-            qi = pb[patch_idx<S>(g, qx, qy, qz, gx - qx * s1, gy - qy * s1, gz - qz * s1)];
-        }
-        // interface planes: add the neighbour rank's partial sums
-        if (remote_lo && gz == 0) qi += remote_lo[rem];
-        if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
-        if (is_ess) qi = di;
-        if constexpr (!XF) __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
-        const double ri = rold - alpha * qi;
-        __builtin_nontemporal_store(ri, &r[gid]);
-        if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
-    }
-    const double bs = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = bs;
-}
 
 // one launch of k_brick_cg over brick layers bz0, bz0 + bzs, ... (nlay of them) on stream s;
 // the whole slab (0, 1, nbz) on the context stream goes through CDFEM_LAUNCH (profiling events)
 struct BrickRun {
     int bz0, bzs, nlay;
     hipStream_t s;
-    int ffkk = -1;  // >= 0: the fused-finalizer apply (k_brick_cg<..., FF>) after ffkk updates
 };
 
 template <int D1, int Q1, unsigned K>
@@ -746,21 +655,15 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const dim3 grid((unsigned)(c->nbx * c->nby * run.nlay)), block(64);
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
     const double *qd = c->d_qaff ? c->d_qaff : c->d_qd;
-    const double *upart = c->d_part + c->nblk;  // the fused update's partials (k_cg_update_ff)
-    const int nup = cg_ff_grid(c), kk = run.ffkk < 0 ? 0 : run.ffkk;
-#define CDFEM_BCG4(AFF_, W_, XF_, FF_)                                                                      \
+#define CDFEM_BCG3(AFF_, W_, XF_)                                                                           \
     if (whole)                                                                                               \
-        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_, FF_>), grid, block, 0, r, dinv, d_old, d_new, q,  \
-                     c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x, upart, nup, kk); \
+        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_>), grid, block, 0, r, dinv, d_old, d_new, q,       \
+                     c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x);                \
     else                                                                                                     \
-        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_, FF_>), grid, block, 0, run.s, r, dinv, d_old,   \
-                           d_new, q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x,  \
-                           upart, nup, kk)
-#define CDFEM_BCG3(AFF_, W_, XF_) CDFEM_BCG4(AFF_, W_, XF_, false)
+        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_>), grid, block, 0, run.s, r, dinv, d_old, d_new, \
+                           q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x)
 #define CDFEM_BCG(AFF_, W_) CDFEM_BCG3(AFF_, W_, false)
-    if (pa_af(c) == 2 && run.ffkk >= 0) {
-        if (x) { CDFEM_BCG4(2, 2, true, true); } else { CDFEM_BCG4(2, 2, false, true); }
-    } else if (pa_af(c) == 2) {
+    if (pa_af(c) == 2) {
         if (x) { CDFEM_BCG3(2, 2, true); }
         else if (c->brick_cg_waves == 3) { CDFEM_BCG(2, 3); }
         else { CDFEM_BCG(2, 2); }
@@ -771,7 +674,6 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     }
 #undef CDFEM_BCG
 #undef CDFEM_BCG3
-#undef CDFEM_BCG4
     return hipGetLastError();
 }
 
@@ -797,39 +699,9 @@ static hipError_t brick_cg2_run(cdfem_ctx *c, const double *r, const double *din
 }
 
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                            double *d_new, double *q, double *x, int ffkk)
+                            double *d_new, double *q, double *x)
 {
-    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, 1, c->nbz, c->stream, ffkk}, x);
-}
-
-// workgroups of the fused-finalizer update (k_cg_update_ff): a grid-stride loop over the lattice;
-// every workgroup sums the nblk den partials and every apply workgroup the update's partials
-int cg_ff_grid(const cdfem_ctx *c)
-{
-    const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
-    const int64_t cap = c->cg_ff_blocks > 0 ? c->cg_ff_blocks : 2048;
-    return (int)(need < cap ? need : cap);
-}
-
-hipError_t launch_cg_update_ff(cdfem_ctx *c, double *x, double *r, const double *d, const double *dinv,
-                               bool xfold)
-{
-    const BrickGeom g = geom_of(c);
-    const FastDiv fdx = make_fastdiv((uint32_t)c->Lx), fdxy = make_fastdiv((uint32_t)(c->Lx * c->Ly));
-    const unsigned grid = (unsigned)cg_ff_grid(c);
-    double *upart = c->d_part + c->nblk;
-#define CDFEM_UFF(S_, XF_)                                                                                   \
-    hipLaunchKernelGGL((k_cg_update_ff<S_, XF_>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, d, dinv,   \
-                       c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, c->d_part, c->nblk, upart, c->d_state)
-    if (c->p == 1) {
-        if (xfold) { CDFEM_UFF(kBrick * 1 + 1, true); } else { CDFEM_UFF(kBrick * 1 + 1, false); }
-    } else if (c->p == 2) {
-        if (xfold) { CDFEM_UFF(kBrick * 2 + 1, true); } else { CDFEM_UFF(kBrick * 2 + 1, false); }
-    } else {
-        return hipErrorInvalidValue;
-    }
-#undef CDFEM_UFF
-    return hipGetLastError();
+    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, 1, c->nbz, c->stream}, x);
 }
 
 // the first and last brick layers (the shared planes' partial sums) on stream s, the interior

@@ -422,11 +422,6 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     const bool xfold = c->cg_xfold != 0 && pa_af(c) == 2;  // Kronecker kernel only
     double *const dbuf0 = dcur, *const dbuf1 = dprev;  // apply j writes d_j into dbuf[(j - 1) & 1]
     int napply = 0;
-    // fused finalizers (set_option "cg_fused_fin", one rank, Kronecker kernel): the apply takes the
-    // betanom step and the update the den step (every workgroup from the other kernel's partials),
-    // so an iteration is two launches instead of four
-    const bool ff = !mr && c->cg_fused_fin != 0 && pa_af(c) == 2;
-    int nupd = 0;
     auto apply = [&] {
         double *xf = (xfold && napply > 0) ? x : nullptr;
         ++napply;
@@ -445,9 +440,8 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             return;
         }
         prof_mark(c, CDFEM_K_APPLY, true);
-        HIPCHK(launch_brick_cg2(c, r, dinv, dprev, dcur, q, xf, ff ? nupd : -1));
+        HIPCHK(launch_brick_cg2(c, r, dinv, dprev, dcur, q, xf));
         prof_mark(c, CDFEM_K_APPLY, false);
-        if (ff) return;
         prof_mark(c, CDFEM_K_E2L, true);
         if (mr) {
             // neighbours' partial sums of q on the shared planes (added by the update kernel)
@@ -465,13 +459,9 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     for (;;) {
         for (int k = 0; k < check && launched < p.max_iter; ++k, ++launched) {
             prof_mark(c, CDFEM_K_UPDATE, true);
-            if (ff)
-                HIPCHK(launch_cg_update_ff(c, x, r, dcur, dinv, xfold));
-            else
-                HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv,
-                                              mr && c->zlo_shared ? c->d_if[1] : nullptr,
-                                              mr && c->zhi_shared ? c->d_if[3] : nullptr, mr, xfold));
-            ++nupd;
+            HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv,
+                                          mr && c->zlo_shared ? c->d_if[1] : nullptr,
+                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr, xfold));
             if (mr) {
                 comm_allreduce(c, red + 1, 1);
                 HIPCHK(launch_update_step(c));
@@ -1681,12 +1671,6 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value != 0 && value != 1 && value != 3 && value != 8 && value != 9 && value != 15)
                 throw ArgError("ho_mfma must be 0, 1, 3, 8, 9 or 15");
             c->ho_mfma = value;
-        } else if (k == "cg_fused_fin") {
-            if (value != 0 && value != 1) throw ArgError("cg_fused_fin must be 0 or 1");
-            c->cg_fused_fin = value;
-        } else if (k == "cg_ff_blocks") {
-            if (value < 0 || value > 65536) throw ArgError("cg_ff_blocks must be 0..65536");
-            c->cg_ff_blocks = value;
         } else if (k == "cg_xfold") {
             if (value != 0 && value != 1) throw ArgError("cg_xfold must be 0 or 1");
             c->cg_xfold = value;

@@ -218,8 +218,6 @@ struct cdfem_ctx {
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
-    int cg_fused_fin = 1;               // set_option "cg_fused_fin": brick CG without the one-block finalizers
-    int cg_ff_blocks = 0;               // set_option "cg_ff_blocks": workgroups of the fused update (0: 2048)
     int cg_xfold = 0;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 8;                  // set_option "sell_order" (read when the FA pattern is built)
@@ -352,11 +350,7 @@ hipError_t launch_den_fin(cdfem_ctx *c, int nparts);
 hipError_t launch_update_fin(cdfem_ctx *c, int nparts);
 // brick CG v2 (brick_kernels.hip): d_new = M^{-1} r + beta d_old, q/face partials, den partials
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                            double *d_new, double *q, double *x = nullptr, int ffkk = -1);
-// fused finalizers (cg_fused_fin, one rank): the update with the den step folded in
-int cg_ff_grid(const cdfem_ctx *c);
-hipError_t launch_cg_update_ff(cdfem_ctx *c, double *x, double *r, const double *d, const double *dinv,
-                               bool xfold);
+                            double *d_new, double *q, double *x = nullptr);
 // x-fold CG after the loop: x += alpha d_m when the last update's x term is still pending
 // (d_m in dbuf[(m - 1) & 1], m = the final iteration)
 hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *d0, const double *d1);

@@ -259,13 +259,6 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *                data.  All forms apply the operator of the per-point multilinear-map setup to rounding
  *                (the Kronecker form is an algebraic identity of the tensor rule, not an exactness
  *                argument); 0 = the per-point map and stream everywhere.
- * "cg_fused_fin": 1 (default) — structured brick CG (p <= 2, Kronecker form, one rank): the den and
- *                 betanom steps run inside the update and apply kernels (every workgroup sums the
- *                 other kernel's partials in one fixed order; workgroup 0 records the state), two
- *                 launches per iteration instead of four; MFEM's CG arithmetic, the partial sums in
- *                 another (fixed) grouping, so the iterates agree to rounding; 0 = the one-block
- *                 finalizer kernels.
- * "cg_ff_blocks": 0 (default: 2048) — workgroups of the fused update kernel (grid-stride loop).
  * "cg_xfold": 0 (default) — 1: structured brick CG (p <= 2), each apply after the first advances x
  *             by the previous iteration's alpha d on the dofs it writes the new direction for, so the
  *             update kernel streams neither x nor d (bitwise the same iterates; measured even at C2:
