@@ -602,7 +602,10 @@ def main():
                     "kernel": (("k_brick_cg (brick patch gather + fused CG direction + D/C/M PA apply" +
                                 (", Kronecker form of the affine factors" if affine else "") +
                                 " + in-LDS E->L + d.Ad)") if args.path == "brick"
-                               else "k_apply3d_tile (Q1 x Q1 thread tile per element, z planes in registers)" if args.order >= 3
+                               else ("k_apply3d_ktile (D1 x D1 thread tile per element, Kronecker form of the affine "
+                                     "factors)" if affine else
+                                     "k_apply3d_tile (Q1 x Q1 thread tile per element, z planes in registers)")
+                               if args.order >= 3
                                else "k_apply3d (fused L->E gather + D/C/M PA apply)"),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
                     "launches": cnt,

@@ -503,7 +503,11 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     // update (ho_kernels.hip k_apply3d_tile<DEN>, vec_kernels.hip k_e2l_box<UPD>)
     const bool fused = !mr && !c->fa_ready && c->cg_fused && tile_den_ok(c) && e2l_box_ok(c) &&
                        c->nl < ((int64_t)1 << 31);  // the flat update's fast division is exact below 2^31
-    if (fused && !c->d_tpart) c->d_tpart = dalloc<double>(tile_den_blocks(c));
+    if (fused && !c->d_tpart) c->d_tpart = dalloc<double>(tile_den_blocks(c, true));
+    // direction fold (ho_dfold): apply j forms d_j = z + beta d_{j-1} into the other direction buffer
+    const bool dfold = fused && tile_dfold_ok(c);
+    if (dfold && !c->d_dalt) c->d_dalt = dalloc<double>(c->nl);
+    double *dprev = d, *dcur = dfold ? c->d_dalt : d;
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     if (mr) {
@@ -517,7 +521,8 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     auto apply = [&] {
         prof_mark(c, CDFEM_K_APPLY, true);
         if (fused) {  // Ye = A_c d and den; q stays an E-vector until the update
-            HIPCHK(launch_apply_den(c, d, c->d_Ye, c->d_state, c->d_tpart));
+            if (dfold) HIPCHK(launch_apply_den_dfold(c, z, dprev, dcur, c->d_Ye, c->d_state, c->d_tpart));
+            else HIPCHK(launch_apply_den(c, d, c->d_Ye, c->d_state, c->d_tpart));
             prof_mark(c, CDFEM_K_APPLY, false);
             prof_mark(c, CDFEM_K_E2L, true);
             HIPCHK(launch_den_from_partials(c, c->d_tpart, tile_den_blocks(c)));
@@ -550,16 +555,20 @@ void solve_cg(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, doub
     for (;;) {
         for (int k = 0; k < check && launched < p.max_iter; ++k, ++launched) {
             prof_mark(c, CDFEM_K_UPDATE, true);
-            if (fused) HIPCHK(launch_e2l_cg_update(c, c->d_Ye, d, x, r, z, dinv));
+            if (fused) HIPCHK(launch_e2l_cg_update(c, c->d_Ye, dcur, x, r, z, dinv));
             else HIPCHK(launch_cg_update(c, x, r, z, d, dinv));
             if (mr) {
                 comm_allreduce(c, red + 1, 1);
                 HIPCHK(launch_update_step(c));
             }
             prof_mark(c, CDFEM_K_UPDATE, false);
-            prof_mark(c, CDFEM_K_DIRECTION, true);
-            HIPCHK(launch_cg_direction(c, z, d));
-            prof_mark(c, CDFEM_K_DIRECTION, false);
+            if (dfold) {
+                std::swap(dprev, dcur);
+            } else {
+                prof_mark(c, CDFEM_K_DIRECTION, true);
+                HIPCHK(launch_cg_direction(c, z, d));
+                prof_mark(c, CDFEM_K_DIRECTION, false);
+            }
             apply();
         }
         HIPCHK(hipMemcpyAsync(c->h_state, c->d_state, sizeof(KrylovState), hipMemcpyDeviceToHost,
@@ -1667,6 +1676,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "mr_overlap") {
             if (value < 0 || value > 1) throw ArgError("mr_overlap must be 0 or 1");
             c->mr_overlap = value;
+        } else if (k == "ho_dfold") {
+            if (value != 0 && value != 1) throw ArgError("ho_dfold must be 0 or 1");
+            c->ho_dfold = value;
         } else if (k == "ho_mfma") {
             if (value != 0 && value != 1 && value != 3 && value != 8 && value != 9 && value != 15)
                 throw ArgError("ho_mfma must be 0, 1, 3, 8, 9 or 15");
@@ -1771,9 +1783,10 @@ int cdfem_kernel_flops(cdfem_ctx *c, int k, double *flops)
         // Fields: value, plus the three reference derivatives when diffusion or convection is on.
         const int D = c->d1, Q = c->rule_op.q1;
         const bool kD = c->kinds & CDFEM_DIFFUSION, kC = c->kinds & CDFEM_CONVECTION, kM = c->kinds & CDFEM_MASS;
-        if (c->qlay == 0 && pa_af(c) == 2) {
-            // Kronecker form (pa_core.hpp elem_apply3d_kron), per input z plane: a length-n linear
-            // combination counts 2n - 1 flops, an accumulation into Y 2 per term
+        if ((c->qlay == 0 && pa_af(c) == 2) || (c->qlay == 1 && tile_kron(c))) {
+            // Kronecker form (pa_core.hpp elem_apply3d_kron; the tile kernel k_apply3d_ktile runs the
+            // same stages across threads), per input z plane: a length-n linear combination counts
+            // 2n - 1 flops, an accumulation into Y 2 per term
             const bool kG = kD || kC;
             auto lc = [](int n) { return n > 0 ? 2.0 * n - 1.0 : 0.0; };
             const double x_row = lc(D) * (1 + 2 * kD + kG) + lc(kM + kD + kC) + 2 * lc(kD + kC);

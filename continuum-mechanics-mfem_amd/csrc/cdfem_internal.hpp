@@ -216,6 +216,7 @@ struct cdfem_ctx {
     int mr_overlap = 1;                 // set_option "mr_overlap": slab CG exchange overlapped with interior bricks
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
+    int ho_dfold = 0;                   // set_option "ho_dfold": CG direction folded into the Kronecker tile apply
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
     int cg_xfold = 0;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply
@@ -301,6 +302,8 @@ inline bool tile_affine(const cdfem_ctx *c)
     if (c->ho_mfma == 0) return true;
     return c->kinds == 7 && (c->ho_mfma == 1 || c->ho_mfma == 8 || c->ho_mfma == 9);
 }
+// the high-order tile apply in the Kronecker form of the affine factors (k_apply3d_ktile)
+inline bool tile_kron(const cdfem_ctx *c) { return c->d_qaff != nullptr && c->ho_mfma == 0 && c->pa_affine == 2; }
 // the element core of the 3D p <= 2 applies (pa_core.hpp elem_apply3d_af): 0 per-point stream,
 // 1 point data from the affine factors, 2 Kronecker form of the factors
 inline int pa_af(const cdfem_ctx *c) { return c->d_qaff == nullptr ? 0 : (c->pa_affine == 2 ? 2 : 1); }
@@ -450,8 +453,12 @@ hipError_t launch_perm(cdfem_ctx *c, bool to_spmv_order, const double *src, doub
 bool spmv_delta(const cdfem_ctx *c);
 // fused high-order CG iteration (ho_kernels.hip / vec_kernels.hip)
 bool tile_den_ok(const cdfem_ctx *c);
-int tile_den_blocks(const cdfem_ctx *c);
+int tile_den_blocks(const cdfem_ctx *c, bool most = false);
 hipError_t launch_apply_den(cdfem_ctx *c, const double *d, double *Ye, const KrylovState *st, double *part);
+// the same with the CG direction folded in (ho_dfold, Kronecker tile): d_new = z + beta d_old
+bool tile_dfold_ok(const cdfem_ctx *c);
+hipError_t launch_apply_den_dfold(cdfem_ctx *c, const double *z, const double *dold, double *dnew, double *Ye,
+                                  const KrylovState *st, double *part);
 bool e2l_box_ok(const cdfem_ctx *c);
 hipError_t launch_den_from_partials(cdfem_ctx *c, const double *in, int64_t n);
 hipError_t launch_e2l_cg_update(cdfem_ctx *c, const double *Ye, const double *d, double *x, double *r, double *z,

@@ -441,6 +441,234 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
     }
 }
 
+// Kronecker-form tile apply (pa_affine 2: affine mesh, constant coefficients, ho_mfma 0).  The
+// element operator is sum_t g_t Fz (x) Fy (x) Fx with the rule's 1D matrices (pa_core.hpp
+// kron_xrow / kron_y / kron_z), so no stage runs over the Q1 quadrature points: one D1 x D1 thread
+// tile per element (25 threads at p = 4, 10 elements per 256-thread block; 16 at p = 3):
+//   gather   X[dz][dy][dx]                       threads (dx, dy), D1 loads each     -> LDS
+//   x + y    plane jz, output column ix          threads (ix, jz): the five x-applied rows of the
+//            plane (kron_xrow on this thread's rows of M, K, C, Ct, read from LDS), then for every
+//            output row iy the four z groups P[grp][jz][iy][ix] (kron_y, compile-time tables)   -> LDS
+//   z        output (ix, iy), all iz             threads (ix, iy): kron_z over the planes jz, then
+//            the E-vector store (and the den partials) exactly as k_apply3d_tile
+// Two barriers per element; 5 KB of LDS per element at p = 4, three blocks per CU.
+// DF (fused CG, set_option "ho_dfold"): x is z = M^-1 r; the gather also reads d_old and forms the
+// direction d = z + beta d_old (k_cg_direction's formula) in registers, and each dof's one owner
+// element (the DEN ownership rule) writes it to d_new, so the direction pass disappears.
+template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, bool DF = false>
+__global__ void __launch_bounds__(256, 3)
+k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qaff,
+                double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const TileGeo geo,
+                const KrylovState *__restrict__ st, double *__restrict__ part, const double *__restrict__ dold,
+                double *__restrict__ dnew)
+{
+    static_assert(!DEN || (CON && LAT), "den partials need the constrained lattice path");
+    static_assert(!DF || DEN, "the direction fold runs in the fused CG apply");
+    if (st != nullptr && st->done) return;
+    using L = QLayout<K, 3>;
+    constexpr int NC = L::nc, DD = D1 * D1, ND = DD * D1;
+    constexpr int EPB = 256 / DD;
+    __shared__ double sR[4][D1][D1];  // M, K, C rows and C^T rows (canonical entries)
+    __shared__ double sX[EPB][ND];
+    __shared__ double sP[EPB][4][ND];  // [grp][jz][iy][ix]
+
+    const int le = threadIdx.x / DD, t = threadIdx.x - le * DD;
+    const int a = t % D1, b = t / D1;
+    const int e = blockIdx.x * EPB + le;
+    const bool inb = le < EPB, valid = inb && e < ne;
+    const int ec = valid ? e : ne - 1;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < D1; ++i)
+#pragma unroll
+            for (int j = 0; j < D1; ++j) {
+                sR[0][i][j] = tM(T, i, j);
+                sR[1][i][j] = tK(T, i, j);
+                sR[2][i][j] = tCacc(T, i, j, 1.0, 0.0);
+                sR[3][i][j] = tCacc(T, j, i, 1.0, 0.0);
+            }
+    }
+    // gather X (threads dx = a, dy = b) and the element's factors
+    uint32_t ex = 0, ey = 0, ez = 0;
+    double xr[D1];
+    int32_t m[D1];  // LAT: ess flag; map path: map entry
+    if constexpr (LAT) {
+        const uint32_t r = fdiv((uint32_t)ec, geo.ho.fnx);
+        ex = (uint32_t)ec - r * geo.ho.nx;
+        ez = fdiv(r, geo.ho.fny);
+        ey = r - ez * geo.ho.ny;
+        constexpr int P = D1 - 1;
+        const size_t g0 = (size_t)(ex * P + a) + (size_t)geo.Lx * ((ey * P + b) + (size_t)geo.Ly * (ez * P));
+        const size_t sz = (size_t)geo.Lx * geo.Ly;
+        double ov[D1];
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            xr[dz] = x[g0 + dz * sz];
+            if constexpr (DF) ov[dz] = dold[g0 + dz * sz];
+            m[dz] = CON ? geo.ess[g0 + dz * sz] : 0;
+        }
+        if constexpr (DF) {
+            const double beta = st->beta;
+            const bool ownxy = inb && (a < P || ex == geo.ho.nx - 1) && (b < P || ey == geo.ho.ny - 1);
+#pragma unroll
+            for (int dz = 0; dz < D1; ++dz) {
+                xr[dz] = xr[dz] + beta * ov[dz];
+                if (valid && ownxy && (dz < P || ez == geo.nz - 1)) dnew[g0 + dz * sz] = xr[dz];
+            }
+        }
+    } else {
+        const int32_t *me = map + (size_t)ec * ND + b * D1 + a;
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) m[dz] = me[dz * DD];
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) xr[dz] = x[m[dz] < 0 ? -m[dz] - 1 : m[dz]];
+    }
+    double g[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) g[k] = qaff[(size_t)ec * NC + k];
+    if (inb) {
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            const bool zero = CON && (LAT ? m[dz] != 0 : m[dz] < 0);
+            sX[le][(dz * D1 + b) * D1 + a] = zero ? 0.0 : xr[dz];
+        }
+    }
+    __syncthreads();
+    // x + y stages: thread (ix = a, jz = b)
+    if (inb) {
+        double Mr[D1], Kr[D1], Cr[D1], Ctr[D1];
+#pragma unroll
+        for (int j = 0; j < D1; ++j) {
+            Mr[j] = sR[0][a][j];
+            Kr[j] = sR[1][a][j];
+            Cr[j] = sR[2][a][j];
+            Ctr[j] = sR[3][a][j];
+        }
+        double v[D1][5];
+#pragma unroll
+        for (int jy = 0; jy < D1; ++jy) {
+            const double *xrow = &sX[le][(b * D1 + jy) * D1];
+            double mm = 0.0, kk = 0.0, cc = 0.0, ct = 0.0;
+#pragma unroll
+            for (int jx = 0; jx < D1; ++jx) {
+                const double xv = xrow[jx];
+                mm += Mr[jx] * xv;
+                if constexpr (L::kD) {
+                    kk += Kr[jx] * xv;
+                    ct += Ctr[jx] * xv;
+                }
+                if constexpr (L::kD || L::kC) cc += Cr[jx] * xv;
+            }
+            kron_xcombine<K>(g, mm, kk, cc, ct, v[jy]);
+        }
+        auto col = [&](int q, int jy) { return v[jy][q]; };
+#pragma unroll
+        for (int iy = 0; iy < D1; ++iy) {
+            double P[4];
+            kron_y<D1, Q1, K>(T, g, col, iy, P);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sP[le][k][(b * D1 + iy) * D1 + a] = P[k];
+        }
+    }
+    __syncthreads();
+    // z stage and the E-vector: thread (ix = dx = a, iy = dy = b)
+    double dacc = 0.0;
+    if (valid) {
+        double Yz[D1];
+#pragma unroll
+        for (int iz = 0; iz < D1; ++iz) Yz[iz] = 0.0;
+#pragma unroll
+        for (int jz = 0; jz < D1; ++jz) {
+            double P[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) P[k] = sP[le][k][(jz * D1 + b) * D1 + a];
+            kron_z<D1, Q1, K>(T, P, jz, Yz);
+        }
+        double *ye;
+        size_t zs;  // stride between dz planes
+        if constexpr (LAT) {
+            const size_t row = (size_t)geo.ho.nx * D1;
+            ye = Ye + (((size_t)ez * D1 * geo.ho.ny + ey) * D1 + b) * row + (size_t)ex * D1 + a;
+            zs = (size_t)geo.ho.ny * D1 * row;
+        } else {
+            ye = Ye + (size_t)e * ND + b * D1 + a;
+            zs = DD;
+        }
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            __builtin_nontemporal_store(Yz[dz], &ye[dz * zs]);
+            if constexpr (DEN) {
+                constexpr int P = D1 - 1;
+                const bool own = (a < P || ex == geo.ho.nx - 1) && (b < P || ey == geo.ho.ny - 1) &&
+                                 (dz < P || ez == geo.nz - 1);
+                dacc += m[dz] != 0 ? (own ? xr[dz] * xr[dz] : 0.0) : xr[dz] * Yz[dz];
+            }
+        }
+    }
+    if constexpr (DEN) {
+        __shared__ double shd[256 / 64];
+        store_partial(block_sum(dacc, shd), part);
+    }
+}
+
+template <int D1, int Q1, unsigned K>
+static hipError_t ktile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
+                              double *den_part, const double *dold = nullptr, double *dnew = nullptr)
+{
+    const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
+    constexpr int EPB = 256 / (D1 * D1);
+    const dim3 grid((unsigned)((c->ne + EPB - 1) / EPB)), block(256);
+    TileGeo geo{};
+    geo.ho = ho_layout(c);
+    geo.Lx = (uint32_t)c->Lx;
+    geo.Ly = (uint32_t)c->Ly;
+    geo.nz = c->epencil ? (uint32_t)(c->ne / ((int64_t)geo.ho.nx * geo.ho.ny)) : 0;
+    geo.ess = c->d_ess;
+    const double *qa = c->d_qaff;
+    double *const np = nullptr;
+    if (den_part && dnew) {
+        if (!c->epencil || !con || !dold) return hipErrorInvalidValue;
+        CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye,
+                     T, c->ne, geo, st, den_part, dold, dnew);
+    } else if (den_part) {
+        if (!c->epencil || !con) return hipErrorInvalidValue;
+        CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye, T,
+                     c->ne, geo, st, den_part, np, np);
+    } else if (c->epencil) {
+        if (con)
+            CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, false>), grid, block, 0, c->d_map, x, qa, Ye,
+                         T, c->ne, geo, st, np, np, np);
+        else
+            CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, false, true, false>), grid, block, 0, c->d_map, x, qa, Ye,
+                         T, c->ne, geo, st, np, np, np);
+    } else {
+        if (con)
+            CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, false, false>), grid, block, 0, c->d_map, x, qa, Ye,
+                         T, c->ne, geo, st, np, np, np);
+        else
+            CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, false, false, false>), grid, block, 0, c->d_map, x, qa, Ye,
+                         T, c->ne, geo, st, np, np, np);
+    }
+    return hipGetLastError();
+}
+
+// the fused CG apply with the direction fold (ho_dfold): d_new = z + beta d_old, Ye = A_c d_new, den
+template <int D1, int Q1>
+static hipError_t ktile_dfold(cdfem_ctx *c, const double *z, const double *dold, double *dnew, double *Ye,
+                              const KrylovState *st, double *part)
+{
+    switch (c->kinds) {
+    case 1: return ktile_kinds<D1, Q1, 1>(c, z, Ye, true, st, part, dold, dnew);
+    case 2: return ktile_kinds<D1, Q1, 2>(c, z, Ye, true, st, part, dold, dnew);
+    case 3: return ktile_kinds<D1, Q1, 3>(c, z, Ye, true, st, part, dold, dnew);
+    case 4: return ktile_kinds<D1, Q1, 4>(c, z, Ye, true, st, part, dold, dnew);
+    case 5: return ktile_kinds<D1, Q1, 5>(c, z, Ye, true, st, part, dold, dnew);
+    case 6: return ktile_kinds<D1, Q1, 6>(c, z, Ye, true, st, part, dold, dnew);
+    case 7: return ktile_kinds<D1, Q1, 7>(c, z, Ye, true, st, part, dold, dnew);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 template <int D1, int Q1, unsigned K, int MF>
 static hipError_t tile_kinds_mf(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
                              double *den_part)
@@ -481,6 +709,7 @@ template <int D1, int Q1, unsigned K>
 static hipError_t tile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
                              double *den_part)
 {
+    if (tile_kron(c)) return ktile_kinds<D1, Q1, K>(c, x, Ye, con, st, den_part);
     if (tile_affine(c)) {
         // affine factors; on the BASELINE operator (kinds 7) also with the x / x^T stages on the
         // matrix cores (ho_mfma 1, 8, 9: VERDICT r03 item 4, the arithmetic-bound regime)
@@ -528,16 +757,30 @@ hipError_t launch_apply_wpe(cdfem_ctx *c, const double *x, double *Ye, bool con,
     return hipErrorInvalidValue;
 }
 
-int tile_den_blocks(const cdfem_ctx *c)
+// den partials of the CG-mode tile apply: one per block of the kernel the configuration launches, or
+// (most) the quadrature tile's count, which bounds both (D1 < Q1), for the allocation
+int tile_den_blocks(const cdfem_ctx *c, bool most)
 {
-    const int q1 = c->rule_op.q1;
-    return (int)((c->ne + 256 / (q1 * q1) - 1) / (256 / (q1 * q1)));
+    const int q1 = c->rule_op.q1, t = !most && tile_kron(c) ? c->d1 * c->d1 : q1 * q1;
+    return (int)((c->ne + 256 / t - 1) / (256 / t));
 }
 
 bool tile_den_ok(const cdfem_ctx *c)
 {
     const int q1 = c->rule_op.q1;
     return c->dim == 3 && c->epencil && c->structured && ((c->p == 3 && q1 == 5) || (c->p == 4 && q1 == 6));
+}
+
+bool tile_dfold_ok(const cdfem_ctx *c) { return c->ho_dfold != 0 && tile_kron(c) && tile_den_ok(c); }
+
+hipError_t launch_apply_den_dfold(cdfem_ctx *c, const double *z, const double *dold, double *dnew, double *Ye,
+                                  const KrylovState *st, double *part)
+{
+    if (!tile_dfold_ok(c)) return hipErrorInvalidValue;
+    const int q1 = c->rule_op.q1;
+    if (c->p == 3 && q1 == 5) return ktile_dfold<4, 5>(c, z, dold, dnew, Ye, st, part);
+    if (c->p == 4 && q1 == 6) return ktile_dfold<5, 6>(c, z, dold, dnew, Ye, st, part);
+    return hipErrorInvalidValue;
 }
 
 // CG mode: Ye = A_c d (E-vector) and the den partials (one per block) into part

@@ -306,12 +306,15 @@ __device__ __forceinline__ void elem_apply3d(const XL &xl, const double *__restr
 // x stage of one input row X[jz][jy][*] for output column ix: the five x-applied quantities
 //   v[0] = (M X)_ix, v[1] = (C X)_ix, v[2] = u1 = s M + D_xx K + c_x C, v[3] = u3 = D_xy Ct + c_y M,
 //   v[4] = u5 = D_xz Ct + c_z M   (applied along x)
+template <unsigned K>
+__device__ __forceinline__ void kron_xcombine(const double (&g)[QLayout<K, 3>::nc], double m, double k, double c,
+                                              double ct, double (&v)[5]);
 template <int D1, int Q1, unsigned K>
 __device__ __forceinline__ void kron_xrow(const Tab<D1, Q1> &T, const double (&g)[QLayout<K, 3>::nc],
                                           const double (&X)[D1], int ix, double (&v)[5])
 {
     using L = QLayout<K, 3>;
-    constexpr bool kD = L::kD, kC = L::kC, kM = L::kM, kG = L::kD || L::kC;
+    constexpr bool kD = L::kD, kG = L::kD || L::kC;
     double m = 0.0, k = 0.0, c = 0.0, ct = 0.0;
 #pragma unroll
     for (int jx = 0; jx < D1; ++jx) {
@@ -322,6 +325,16 @@ __device__ __forceinline__ void kron_xrow(const Tab<D1, Q1> &T, const double (&g
         }
         if constexpr (kG) c = tCacc(T, ix, jx, X[jx], c);
     }
+    kron_xcombine<K>(g, m, k, c, ct, v);
+}
+
+// the per-element combinations of one x-applied row: m, k, c, ct = (M X), (K X), (C X), (Ct X)
+template <unsigned K>
+__device__ __forceinline__ void kron_xcombine(const double (&g)[QLayout<K, 3>::nc], double m, double k, double c,
+                                              double ct, double (&v)[5])
+{
+    using L = QLayout<K, 3>;
+    constexpr bool kD = L::kD, kC = L::kC, kM = L::kM;
     v[0] = m;
     v[1] = c;
     double a = 0.0;
@@ -343,10 +356,10 @@ __device__ __forceinline__ void kron_xrow(const Tab<D1, Q1> &T, const double (&g
 }
 
 // y stage of one output column (the x-stage quantities col(q, jy) of kron_xrow, q = 0..4, for every
-// input row jy of plane jz) into the four z groups, then the z stage into Yz[iz] (this (iy, ix))
+// input row jy of plane jz) into the four z groups P = (pm, pk, pc, pct) of output row iy
 template <int D1, int Q1, unsigned K, typename COL>
-__device__ __forceinline__ void kron_yz(const Tab<D1, Q1> &T, const double (&g)[QLayout<K, 3>::nc], const COL &col,
-                                        int iy, int jz, double (&Yz)[D1])
+__device__ __forceinline__ void kron_y(const Tab<D1, Q1> &T, const double (&g)[QLayout<K, 3>::nc], const COL &col,
+                                       int iy, double (&P)[4])
 {
     using L = QLayout<K, 3>;
     constexpr bool kD = L::kD, kG = L::kD || L::kC;
@@ -385,6 +398,19 @@ __device__ __forceinline__ void kron_yz(const Tab<D1, Q1> &T, const double (&g)[
         pc += g[4] * ctym;
         pct = g[2] * myc + g[4] * cym;
     }
+    P[0] = pm;
+    P[1] = pk;
+    P[2] = pc;
+    P[3] = pct;
+}
+
+// z stage of input plane jz: Yz[iz] += the four groups P of one output (iy, ix) along z
+template <int D1, int Q1, unsigned K>
+__device__ __forceinline__ void kron_z(const Tab<D1, Q1> &T, const double (&P)[4], int jz, double (&Yz)[D1])
+{
+    using L = QLayout<K, 3>;
+    constexpr bool kD = L::kD, kG = L::kD || L::kC;
+    const double pm = P[0], pk = P[1], pc = P[2], pct = P[3];
 #pragma unroll
     for (int iz = 0; iz < D1; ++iz) {
         double y = Yz[iz];
@@ -396,6 +422,15 @@ __device__ __forceinline__ void kron_yz(const Tab<D1, Q1> &T, const double (&g)[
         if constexpr (kG) y = tCacc(T, iz, jz, pc, y);
         Yz[iz] = y;
     }
+}
+
+template <int D1, int Q1, unsigned K, typename COL>
+__device__ __forceinline__ void kron_yz(const Tab<D1, Q1> &T, const double (&g)[QLayout<K, 3>::nc], const COL &col,
+                                        int iy, int jz, double (&Yz)[D1])
+{
+    double P[4];
+    kron_y<D1, Q1, K>(T, g, col, iy, P);
+    kron_z<D1, Q1, K>(T, P, jz, Yz);
 }
 
 // g: the element's factors (QLayout<K, 3> order), loaded by the caller (kron_load_g)

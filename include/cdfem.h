@@ -240,6 +240,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
  *               interface pack and the exchange run on a side stream under the interior layers;
  *               0 = one launch, then the exchange (bitwise the same results).
+ * "ho_dfold": 0 (default) — read by the CG solve on structured boxes (one rank, fused high-order CG,
+ *              Kronecker tile: pa_affine 2, ho_mfma 0): 1 = the apply gathers z and the previous
+ *              direction, forms d = z + beta d_old itself (each dof's owner element stores it to a
+ *              second direction buffer), and the direction pass is skipped (same formula).
  * "ho_mfma": 0 (default) — the LDS stages of the high-order (3D p = 3, 4) tile apply as block GEMMs on
  *            v_mfma_f64_16x16x4_f64, bit 0 = stage x, 1 = y, 2 = y^T, 3 = x^T; the masks 1, 3, 8, 9
  *            and 15 are built (results agree to rounding; the north star's MFMA alternative,

@@ -162,6 +162,38 @@ def test_ho_fused_cg_box_shapes(gpu_ctx, shape, p):
     assert np.linalg.norm(x1 - x0) <= 1e-10 * np.linalg.norm(x0)
 
 
+@pytest.mark.parametrize("shape,p,kinds", [((3, 3, 3), 4, 7), ((4, 3, 5), 3, 5), ((3, 4, 2), 4, 3)])
+def test_ho_dfold_matches_direction_pass(gpu_ctx, shape, p, kinds):
+    """ho_dfold: the Kronecker tile's fused CG apply forms d = z + beta d_old itself (its owner element
+    writes it to the other direction buffer) and the direction pass is skipped.  Affine boxes with
+    non-zero essential values: 40 fixed iterates against the oracle (1e-11) and against the direction
+    pass (same formula: 1e-13), same residual norms to rounding."""
+    om = O.BoxMesh(3, shape, p)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(kinds))
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    rng = np.random.default_rng(17)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
+    out = {}
+    try:
+        for df in (1, 0):
+            gpu_ctx.set_option("ho_dfold", df)
+            gpu_ctx.upload_mesh(gm).set_structured(*shape)
+            gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            _, B = gpu_ctx.form_linear_system(u, b)
+            out[df] = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=7)
+    finally:
+        gpu_ctx.set_option("ho_dfold", 0)
+    for df, (xg, ig) in out.items():
+        assert ig["iterations"] == 40
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), df
+    assert np.linalg.norm(out[1][0] - out[0][0]) <= 1e-13 * np.linalg.norm(out[0][0])
+    assert abs(out[1][1]["final_norm"] - out[0][1]["final_norm"]) <= 1e-12 * out[0][1]["initial_norm"]
+
+
 def test_ho_mms_error_matches_oracle(gpu_ctx):
     n, p = 3, 4
     om = O.BoxMesh(3, n, p)
@@ -286,13 +318,14 @@ def test_ho_mfma_fused_cg_parity(gpu_ctx, n, p, mf):
 
 
 @pytest.mark.parametrize("n,p,structured,kinds", [(3, 4, True, 7), (4, 3, True, 5), (3, 4, False, 7),
-                                                  (5, 4, True, 6)])
+                                                  (5, 4, True, 6), (4, 3, False, 1), (3, 4, True, 2),
+                                                  (4, 3, True, 3), (3, 4, True, 4)])
 def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
-    """pa_affine (default) on an affine box: the tile apply forms each point's data as W_q * g_e from
-    one factor set per element (the product the setup stores, so the per-point values are the
-    same bits).  Mult, constrained Mult, diagonal against the oracle (1e-13) and the per-point
-    multilinear-map setup (pa_affine 0, rounding: 1e-13); 50 fused CG iterates against the oracle
-    (1e-11); the byte count drops by the stream."""
+    """pa_affine on an affine box: 2 (default) runs the Kronecker-form tile (k_apply3d_ktile, 1D rule
+    matrices, no quadrature-point stage), 1 the quadrature tile forming each point's data as
+    W_q * g_e from one factor set per element.  Mult, constrained Mult, diagonal against the oracle
+    (1e-13) and the per-point multilinear-map setup (pa_affine 0, rounding: 1e-13); 50 fused CG
+    iterates against the oracle (1e-11); the byte count drops by the stream."""
     om = O.BoxMesh(3, n, p)
     A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(kinds))
     gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
@@ -305,7 +338,7 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
     xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=50)
     out = {}
     try:
-        for aff in (1, 0):
+        for aff in (2, 1, 0):
             gpu_ctx.set_option("pa_affine", aff)
             gpu_ctx.upload_mesh(gm)
             if structured:
@@ -318,10 +351,12 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
     finally:
         gpu_ctx.set_option("pa_affine", 2)
     yo = A.mult(x)
-    assert out[1]["bytes"] < out[0]["bytes"]
-    assert np.abs(out[1]["y"] - yo).max() <= 1e-13 * np.abs(yo).max()
-    assert np.abs(out[1]["dg"] - A.diag()).max() <= 1e-13 * np.abs(A.diag()).max()
-    for k in ("y", "yc", "dg"):
-        assert np.abs(out[1][k] - out[0][k]).max() <= 1e-13 * np.abs(out[0][k]).max()
-    assert out[1]["it"] == 50
-    assert np.linalg.norm(out[1]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
+    for aff in (2, 1):
+        assert out[aff]["bytes"] < out[0]["bytes"]
+        assert np.abs(out[aff]["y"] - yo).max() <= 1e-13 * np.abs(yo).max()
+        assert np.abs(out[aff]["dg"] - A.diag()).max() <= 1e-13 * np.abs(A.diag()).max()
+        for k in ("y", "yc", "dg"):
+            assert np.abs(out[aff][k] - out[0][k]).max() <= 1e-13 * np.abs(out[0][k]).max()
+        assert out[aff]["it"] == 50
+        if kinds != 2:  # pure convection: Jacobi-CG breaks down (the oracle's iterates too)
+            assert np.linalg.norm(out[aff]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
