@@ -557,7 +557,11 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     if (t == 0) part[b] = den;
 }
 
-template <int S, bool XF>
+// PB (set_option "brick_upd_pb"): the 1-8 patch entries of every dof as eight unconditional buffer
+// loads at fixed offsets from its own brick's entry P (the lower brick's face entry along x / y / z
+// sits at P - 1 / P - R / P - A in the pencil layout), the missing ones at kOOB (read as 0), summed
+// in the branchy form's order (lower brick first per face axis, z outermost): bitwise the same q.
+template <int S, bool XF, bool PB = false>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ d,
                   const double *__restrict__ dinv, const double *__restrict__ pb,
@@ -598,7 +602,25 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         const double di = (!XF || is_ess) ? d[gid] : 0.0, xi = XF ? 0.0 : x[gid];
         const double rold = r[gid], mi = dinv[gid];
         double qi;
-        if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
+        if constexpr (PB) {
+            const int qx = min(gx / s1, g.nbx - 1), qy = min(gy / s1, g.nby - 1), qz = min(gz / s1, g.nbz - 1);
+            const int px = gx - qx * s1, py = gy - qy * s1, pz = gz - qz * s1;
+            const bool fx = px == 0 && qx > 0, fy = py == 0 && qy > 0, fz = pz == 0 && qz > 0;
+            const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
+            const uint32_t P = (((uint32_t)qz * S + pz) * g.nby + qy) * S * R + (uint32_t)py * R + (uint32_t)qx * S + px;
+            const auto bp = brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S));
+            double t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int sz = (k >> 2) & 1 ? 0 : 1, sy = (k >> 1) & 1 ? 0 : 1, sx = k & 1 ? 0 : 1;
+                const bool ok = (!sx || fx) && (!sy || fy) && (!sz || fz);
+                const uint32_t o = P - (uint32_t)sx - (uint32_t)sy * R - (uint32_t)sz * A;
+                t[k] = bload(bp, ok ? 8u * o : kOOB);
+            }
+            qi = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) qi += t[k];
+        } else if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
             int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
             const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
             if (gx - qx * s1 == 0) {
@@ -725,15 +747,19 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     // loads, so every dof's chain must be in flight at once
     const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
     const unsigned grid = (unsigned)(need < 16384 ? need : 16384);
+#define CDFEM_UPD2(S_, XF_, PB_)                                                                           \
+    hipLaunchKernelGGL((k_cg_update_faces<S_, XF_, PB_>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, d, \
+                       dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, c->d_part, \
+                       c->d_state, (int)den_step)
+    // predicated-load face sums: the patch buffer's byte offsets must fit 32 bits
+    const double s3 = std::pow(kBrick * c->p + 1.0, 3.0);
+    const bool pb = c->brick_upd_pb != 0 && 8.0 * (double)c->nblk * s3 < 4294967296.0;
 #define CDFEM_UPD(S_)                                                                                       \
-    if (xfold)                                                                                              \
-        hipLaunchKernelGGL((k_cg_update_faces<S_, true>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, d, \
-                           dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi,        \
-                           c->d_part, c->d_state, (int)den_step);                                           \
-    else                                                                                                    \
-        hipLaunchKernelGGL((k_cg_update_faces<S_, false>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, \
-                           d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi,     \
-                           c->d_part, c->d_state, (int)den_step)
+    if (xfold) {                                                                                            \
+        if (pb) { CDFEM_UPD2(S_, true, true); } else { CDFEM_UPD2(S_, true, false); }                       \
+    } else {                                                                                                \
+        if (pb) { CDFEM_UPD2(S_, false, true); } else { CDFEM_UPD2(S_, false, false); }                     \
+    }
     if (c->p == 1) {
         CDFEM_UPD(kBrick * 1 + 1);
     } else if (c->p == 2) {
@@ -742,6 +768,7 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
         return hipErrorInvalidValue;
     }
 #undef CDFEM_UPD
+#undef CDFEM_UPD2
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (multi_rank(c)) return launch_fin_sum(c, (int)grid, 1);

@@ -1676,6 +1676,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "mr_overlap") {
             if (value < 0 || value > 1) throw ArgError("mr_overlap must be 0 or 1");
             c->mr_overlap = value;
+        } else if (k == "brick_upd_pb") {
+            if (value != 0 && value != 1) throw ArgError("brick_upd_pb must be 0 or 1");
+            c->brick_upd_pb = value;
         } else if (k == "ho_dfold") {
             if (value != 0 && value != 1) throw ArgError("ho_dfold must be 0 or 1");
             c->ho_dfold = value;
@@ -1864,7 +1867,9 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
         switch (k) {
         case CDFEM_K_APPLY:
             if (c->epencil)  // lattice gather: x + ess flags (each L-dof once) + qdata + E-vector write
-                *bytes = 9.0 * nl + 8.0 * c->ncomp * nqs * ne + 8.0 * nd * ne;
+                *bytes = 9.0 * nl + 8.0 * c->ncomp * nqs * ne + 8.0 * nd * ne +
+                         (tile_dfold_ok(c) ? 16.0 * nl : 0.0);  // CG apply with the direction fold:
+                                                                // + d_old gather, + d store
             else             // x gather (each L-dof once) + qdata stream + element map + E-vector write
                 *bytes = 8.0 * nl + 8.0 * c->ncomp * nqs * ne + 4.0 * nd * ne + 8.0 * nd * ne;
             break;

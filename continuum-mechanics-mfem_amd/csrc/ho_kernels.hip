@@ -509,11 +509,11 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
         }
         if constexpr (DF) {
             const double beta = st->beta;
-            const bool ownxy = inb && (a < P || ex == geo.ho.nx - 1) && (b < P || ey == geo.ho.ny - 1);
+            const bool ownxy = valid && (a < P || ex == geo.ho.nx - 1) && (b < P || ey == geo.ho.ny - 1);
 #pragma unroll
             for (int dz = 0; dz < D1; ++dz) {
                 xr[dz] = xr[dz] + beta * ov[dz];
-                if (valid && ownxy && (dz < P || ez == geo.nz - 1)) dnew[g0 + dz * sz] = xr[dz];
+                if (ownxy && (dz < P || ez == geo.nz - 1)) dnew[g0 + dz * sz] = xr[dz];
             }
         }
     } else {

@@ -240,10 +240,14 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
  *               interface pack and the exchange run on a side stream under the interior layers;
  *               0 = one launch, then the exchange (bitwise the same results).
- * "ho_dfold": 0 (default) — read by the CG solve on structured boxes (one rank, fused high-order CG,
- *              Kronecker tile: pa_affine 2, ho_mfma 0): 1 = the apply gathers z and the previous
+ * "brick_upd_pb": 0 (default) — the brick CG update (k_cg_update_faces) reads each dof's 1-8 patch
+ *              entries as eight predicated buffer loads (absent ones out of range) instead of
+ *              branching on the face planes; bitwise the same sums.
+ * "ho_dfold": 1 (default) — read by the CG solve on structured boxes (one rank, fused high-order CG,
+ *              Kronecker tile: pa_affine 2, ho_mfma 0): the apply gathers z and the previous
  *              direction, forms d = z + beta d_old itself (each dof's owner element stores it to a
- *              second direction buffer), and the direction pass is skipped (same formula).
+ *              second direction buffer), and the direction pass is skipped (same formula); 0 = the
+ *              direction pass.
  * "ho_mfma": 0 (default) — the LDS stages of the high-order (3D p = 3, 4) tile apply as block GEMMs on
  *            v_mfma_f64_16x16x4_f64, bit 0 = stage x, 1 = y, 2 = y^T, 3 = x^T; the masks 1, 3, 8, 9
  *            and 15 are built (results agree to rounding; the north star's MFMA alternative,
@@ -312,7 +316,9 @@ int cdfem_profile_enable(cdfem_ctx *ctx, int on);
 int cdfem_profile_reset(cdfem_ctx *ctx);
 /* total milliseconds and launch count of kernel id (CDFEM_K_*) since the last reset */
 int cdfem_profile_read(cdfem_ctx *ctx, int kernel, double *total_ms, int64_t *count);
-/* algorithmic bytes moved by one launch of kernel id (see DESIGN.md for the per-unit figures) */
+/* algorithmic bytes moved by one launch of kernel id (see DESIGN.md for the per-unit figures); on
+ * structured boxes the figure is that of the kernel the CG solve launches (the brick CG kernels, the
+ * fused high-order apply with its direction fold)                                                 */
 int cdfem_kernel_bytes(cdfem_ctx *ctx, int kernel, double *bytes);
 /* algorithmic f64 flops of one launch of the 3D partial-assembly apply (CDFEM_K_APPLY; FMA = 2):
  * the sum-factorized element apply (plus the point data W_q * g_e under pa_affine 1), or the

@@ -42,3 +42,29 @@ def test_xfold_bitwise(gpu_ctx, shape, p, kinds, pert):
         assert i0["iterations"] == i1["iterations"] and i0["converged"] == i1["converged"], kw
         np.testing.assert_array_equal(x1, x0)
 
+
+
+@pytest.mark.parametrize("shape,p,kinds,xfold", [((8, 8, 8), 2, 7, 0), ((9, 6, 7), 2, 5, 1), ((6, 5, 7), 1, 7, 0),
+                                                 ((5, 9, 10), 2, 3, 0)])
+def test_brick_update_predicated_faces_bitwise(gpu_ctx, shape, p, kinds, xfold):
+    """brick_upd_pb: the update's face sums as eight predicated patch-buffer loads summed in the
+    branchy form's order: bitwise the same iterates (partial bricks in every direction, essential
+    values, with and without the x-fold)."""
+    om = O.BoxMesh(3, shape, p)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(*shape)
+    gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    rng = np.random.default_rng(11)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    _, B = gpu_ctx.form_linear_system(u, rng.uniform(-1, 1, om.nl))
+    out = {}
+    try:
+        gpu_ctx.set_option("cg_xfold", xfold)
+        for pb in (1, 0):
+            gpu_ctx.set_option("brick_upd_pb", pb)
+            out[pb] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=25, check_every=7)
+    finally:
+        gpu_ctx.set_option("brick_upd_pb", 0)
+        gpu_ctx.set_option("cg_xfold", 0)
+    assert out[1][1]["iterations"] == out[0][1]["iterations"] == 25
+    np.testing.assert_array_equal(out[1][0], out[0][0])

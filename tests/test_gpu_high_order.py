@@ -165,9 +165,10 @@ def test_ho_fused_cg_box_shapes(gpu_ctx, shape, p):
 @pytest.mark.parametrize("shape,p,kinds", [((3, 3, 3), 4, 7), ((4, 3, 5), 3, 5), ((3, 4, 2), 4, 3)])
 def test_ho_dfold_matches_direction_pass(gpu_ctx, shape, p, kinds):
     """ho_dfold: the Kronecker tile's fused CG apply forms d = z + beta d_old itself (its owner element
-    writes it to the other direction buffer) and the direction pass is skipped.  Affine boxes with
-    non-zero essential values: 40 fixed iterates against the oracle (1e-11) and against the direction
-    pass (same formula: 1e-13), same residual norms to rounding."""
+    writes it to the other direction buffer) and the direction pass is skipped (default).  Affine
+    boxes with non-zero essential values: 40 fixed iterates against the oracle (1e-11) and against
+    the direction pass (same formula: 1e-13), same residual norms to rounding; a converging solve
+    (stopped by the tolerance inside a check interval) gives the same iteration count and solution."""
     om = O.BoxMesh(3, shape, p)
     A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(kinds))
     gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
@@ -177,7 +178,7 @@ def test_ho_dfold_matches_direction_pass(gpu_ctx, shape, p, kinds):
     b = rng.uniform(-1, 1, om.nl)
     Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
     xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
-    out = {}
+    out, conv = {}, {}
     try:
         for df in (1, 0):
             gpu_ctx.set_option("ho_dfold", df)
@@ -185,13 +186,17 @@ def test_ho_dfold_matches_direction_pass(gpu_ctx, shape, p, kinds):
             gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
             _, B = gpu_ctx.form_linear_system(u, b)
             out[df] = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=7)
+            conv[df] = gpu_ctx.solve(B, method="cg", rel_tol=1e-6, abs_tol=0.0, max_iter=400, check_every=16)
     finally:
-        gpu_ctx.set_option("ho_dfold", 0)
+        gpu_ctx.set_option("ho_dfold", 1)
     for df, (xg, ig) in out.items():
         assert ig["iterations"] == 40
         assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), df
-    assert np.linalg.norm(out[1][0] - out[0][0]) <= 1e-13 * np.linalg.norm(out[0][0])
-    assert abs(out[1][1]["final_norm"] - out[0][1]["final_norm"]) <= 1e-12 * out[0][1]["initial_norm"]
+    for df in (1,):
+        assert np.linalg.norm(out[df][0] - out[0][0]) <= 1e-13 * np.linalg.norm(out[0][0]), df
+        assert abs(out[df][1]["final_norm"] - out[0][1]["final_norm"]) <= 1e-12 * out[0][1]["initial_norm"]
+        assert conv[df][1]["iterations"] == conv[0][1]["iterations"], df
+        assert np.linalg.norm(conv[df][0] - conv[0][0]) <= 1e-12 * np.linalg.norm(conv[0][0]), df
 
 
 def test_ho_mms_error_matches_oracle(gpu_ctx):
