@@ -128,7 +128,8 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_verts); dfree(c->d_map); dfree(c->d_e2l_off); dfree(c->d_e2l_pos);
     dfree(c->d_ess); dfree(c->d_ess_list); dfree(c->d_qd); dfree(c->d_qaff); dfree(c->d_Ye); dfree(c->d_dinv);
     for (auto &w : c->d_w) dfree(w);
-    dfree(c->d_part); dfree(c->d_tpart); dfree(c->d_gm); dfree(c->d_gm_part);
+    dfree(c->d_part); dfree(c->d_tpart); dfree(c->d_gm); dfree(c->d_gm_part); dfree(c->d_ktab);
+    c->ktab_key = -1;  // rebuilt (and reallocated) by the next k_apply3d_ktile launch
     dfree(c->d_perm); dfree(c->d_face); dfree(c->d_ones); dfree(c->d_dalt);
     for (auto &b : c->d_if) dfree(b);
     dfree(c->d_stab); dfree(c->d_stab_lf); dfree(c->d_rowptr); dfree(c->d_cols); dfree(c->d_diagpos); dfree(c->d_coff);

@@ -210,6 +210,9 @@ struct cdfem_ctx {
     int64_t nslices = 0, nstored = 0;   // SELL-64 copy (the SpMV layout)
     int32_t *d_sptr = nullptr, *d_srows = nullptr, *d_scols = nullptr, *d_smap = nullptr;
     double *d_tpart = nullptr;          // den partials of the fused high-order CG apply (one per tile block)
+    double *d_ktab = nullptr;           // k_apply3d_ktile's rows of M, K, C, C^T (canonical entries, [4][D1][D1])
+    double h_ktab[4 * 5 * 5] = {};      //   host copy (source of the async upload)
+    int ktab_key = -1;                  //   (p, rule) the table was built for
     int16_t *d_sdel = nullptr;          // 16-bit column deltas (null when the bandwidth does not fit)
     uint8_t *d_swide = nullptr;         // per slice: 1 = streams 32-bit columns (mixed layout; null: none)
     int64_t sell_nnz_wide = 0;          // real entries in the 32-bit slices of a mixed layout

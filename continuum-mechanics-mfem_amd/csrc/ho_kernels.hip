@@ -447,7 +447,8 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 // tile per element (25 threads at p = 4, 10 elements per 256-thread block; 16 at p = 3):
 //   gather   X[dz][dy][dx]                       threads (dx, dy), D1 loads each     -> LDS
 //   x + y    plane jz, output column ix          threads (ix, jz): the five x-applied rows of the
-//            plane (kron_xrow on this thread's rows of M, K, C, Ct, read from LDS), then for every
+//            plane (kron_xrow on this thread's rows of M, K, C, Ct, loaded from a 100-double device
+//            table, ktab: ix is a thread index, so these are the only run-time-indexed constants), then for every
 //            output row iy the four z groups P[grp][jz][iy][ix] (kron_y, compile-time tables)   -> LDS
 //   z        output (ix, iy), all iz             threads (ix, iy): kron_z over the planes jz, then
 //            the E-vector store (and the den partials) exactly as k_apply3d_tile
@@ -460,7 +461,7 @@ __global__ void __launch_bounds__(256, 3)
 k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qaff,
                 double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const TileGeo geo,
                 const KrylovState *__restrict__ st, double *__restrict__ part, const double *__restrict__ dold,
-                double *__restrict__ dnew)
+                double *__restrict__ dnew, const double *__restrict__ ktab)
 {
     static_assert(!DEN || (CON && LAT), "den partials need the constrained lattice path");
     static_assert(!DF || DEN, "the direction fold runs in the fused CG apply");
@@ -468,7 +469,6 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
     using L = QLayout<K, 3>;
     constexpr int NC = L::nc, DD = D1 * D1, ND = DD * D1;
     constexpr int EPB = 256 / DD;
-    __shared__ double sR[4][D1][D1];  // M, K, C rows and C^T rows (canonical entries)
     __shared__ double sX[EPB][ND];
     __shared__ double sP[EPB][4][ND];  // [grp][jz][iy][ix]
 
@@ -477,16 +477,14 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
     const int e = blockIdx.x * EPB + le;
     const bool inb = le < EPB, valid = inb && e < ne;
     const int ec = valid ? e : ne - 1;
-    if (threadIdx.x == 0) {
+    // this thread's x-stage rows (ix = a), in flight with the gather
+    double Mr[D1], Kr[D1], Cr[D1], Ctr[D1];
 #pragma unroll
-        for (int i = 0; i < D1; ++i)
-#pragma unroll
-            for (int j = 0; j < D1; ++j) {
-                sR[0][i][j] = tM(T, i, j);
-                sR[1][i][j] = tK(T, i, j);
-                sR[2][i][j] = tCacc(T, i, j, 1.0, 0.0);
-                sR[3][i][j] = tCacc(T, j, i, 1.0, 0.0);
-            }
+    for (int j = 0; j < D1; ++j) {
+        Mr[j] = ktab[(0 * D1 + a) * D1 + j];
+        Kr[j] = ktab[(1 * D1 + a) * D1 + j];
+        Cr[j] = ktab[(2 * D1 + a) * D1 + j];
+        Ctr[j] = ktab[(3 * D1 + a) * D1 + j];
     }
     // gather X (threads dx = a, dy = b) and the element's factors
     uint32_t ex = 0, ey = 0, ez = 0;
@@ -536,14 +534,6 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
     __syncthreads();
     // x + y stages: thread (ix = a, jz = b)
     if (inb) {
-        double Mr[D1], Kr[D1], Cr[D1], Ctr[D1];
-#pragma unroll
-        for (int j = 0; j < D1; ++j) {
-            Mr[j] = sR[0][a][j];
-            Kr[j] = sR[1][a][j];
-            Cr[j] = sR[2][a][j];
-            Ctr[j] = sR[3][a][j];
-        }
         double v[D1][5];
 #pragma unroll
         for (int jy = 0; jy < D1; ++jy) {
@@ -626,28 +616,54 @@ static hipError_t ktile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool co
     geo.ess = c->d_ess;
     const double *qa = c->d_qaff;
     double *const np = nullptr;
+    // the x-stage rows (canonical entries of make_tab's orbit averages, as tM / tK / tCacc read them)
+    const int key = c->p * 64 + c->rule_op.q1;
+    if (c->ktab_key != key) {
+        // (a rebuild follows a new setup: let any copy still reading h_ktab finish first)
+        const hipError_t es = hipStreamSynchronize(c->stream);
+        if (es != hipSuccess) return es;
+        if (!c->d_ktab) {
+            const hipError_t e = hipMalloc(&c->d_ktab, sizeof(c->h_ktab));
+            if (e != hipSuccess) return e;
+        }
+        for (int i = 0; i < D1; ++i)
+            for (int j = 0; j < D1; ++j) {
+                const int m = sym_can(D1, i, j), ca = anti_can(D1, i, j), sa = anti_sign(D1, i, j);
+                const int cb = anti_can(D1, j, i), sb = anti_sign(D1, j, i);
+                c->h_ktab[(0 * D1 + i) * D1 + j] = T.M1[m / D1][m % D1];
+                c->h_ktab[(1 * D1 + i) * D1 + j] = T.K1[m / D1][m % D1];
+                c->h_ktab[(2 * D1 + i) * D1 + j] = sa == 0 ? 0.0 : sa * T.C1[ca / D1][ca % D1];
+                c->h_ktab[(3 * D1 + i) * D1 + j] = sb == 0 ? 0.0 : sb * T.C1[cb / D1][cb % D1];
+            }
+        const hipError_t e = hipMemcpyAsync(c->d_ktab, c->h_ktab, sizeof(double) * 4 * D1 * D1,
+                                            hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) return e;
+        c->ktab_key = key;
+    }
+    const double *kt = c->d_ktab;
+    if (kt == nullptr) return hipErrorInvalidValue;
     if (den_part && dnew) {
         if (!c->epencil || !con || !dold) return hipErrorInvalidValue;
         CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye,
-                     T, c->ne, geo, st, den_part, dold, dnew);
+                     T, c->ne, geo, st, den_part, dold, dnew, kt);
     } else if (den_part) {
         if (!c->epencil || !con) return hipErrorInvalidValue;
         CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye, T,
-                     c->ne, geo, st, den_part, np, np);
+                     c->ne, geo, st, den_part, np, np, kt);
     } else if (c->epencil) {
         if (con)
             CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, false>), grid, block, 0, c->d_map, x, qa, Ye,
-                         T, c->ne, geo, st, np, np, np);
+                         T, c->ne, geo, st, np, np, np, kt);
         else
             CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, false, true, false>), grid, block, 0, c->d_map, x, qa, Ye,
-                         T, c->ne, geo, st, np, np, np);
+                         T, c->ne, geo, st, np, np, np, kt);
     } else {
         if (con)
             CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, false, false>), grid, block, 0, c->d_map, x, qa, Ye,
-                         T, c->ne, geo, st, np, np, np);
+                         T, c->ne, geo, st, np, np, np, kt);
         else
             CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, false, false, false>), grid, block, 0, c->d_map, x, qa, Ye,
-                         T, c->ne, geo, st, np, np, np);
+                         T, c->ne, geo, st, np, np, np, kt);
     }
     return hipGetLastError();
 }

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 4: the whole GPU suite and smoke(), the brick update's predicated face sums A/B at C2,
+# C2 and C3 bench lines.
+set -u
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/${TAG:-r04p}; mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread \
+    -p no:cacheprovider > $O/suite.log 2>&1 || { echo "suite rc=$?"; grep -E "^(FAILED|ERROR)|passed|failed" $O/suite.log | head -20; exit 1; }
+tail -2 $O/suite.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; tail $O/smoke.log; exit 1; }
+cat $O/smoke.log
+timeout -k 10 300 python -u tools/ab_opts.py --variant "brick_upd_pb=0" --variant "brick_upd_pb=1" --rounds 5 --iters 100 > $O/ab_c2_upd_pb.json 2> $O/ab_c2_upd_pb.err || { echo "ab rc=$?"; tail $O/ab_c2_upd_pb.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('$O/ab_c2_upd_pb.json'))
+for k,v in d.items():
+    if isinstance(v, dict): print(k, {a: (round(b,2) if isinstance(b,float) else b) for a,b in v.items() if a!='it_us_all'})
+"
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 2 > $O/bench_c2.json 2> $O/bench_c2.err || { echo "bench rc=$?"; tail $O/bench_c2.err; exit 1; }
+timeout -k 10 400 python -u bench.py --config c3 --steps 3 --warmup 1 > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench c3 rc=$?"; tail $O/bench_c3.err; exit 1; }
+for f in bench_c2 bench_c3; do python3 -c "
+import json
+d=json.loads(open('$O/$f.json').read().strip().splitlines()[-1])
+r=d['roofline']; print('$f', '%.3e'%d['value'], r['bound'], r['frac'], r['avg_launch_us'], r['other_kernels_avg_us'])"; done
