@@ -240,9 +240,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
  *               interface pack and the exchange run on a side stream under the interior layers;
  *               0 = one launch, then the exchange (bitwise the same results).
- * "brick_upd_pb": 0 (default) — the brick CG update (k_cg_update_faces) reads each dof's 1-8 patch
+ * "brick_upd_pb": 1 (default) — the brick CG update (k_cg_update_faces) reads each dof's 1-8 patch
  *              entries as eight predicated buffer loads (absent ones out of range) instead of
- *              branching on the face planes; bitwise the same sums.
+ *              branching on the face planes (0); bitwise the same sums.
  * "ho_dfold": 1 (default) — read by the CG solve on structured boxes (one rank, fused high-order CG,
  *              Kronecker tile: pa_affine 2, ho_mfma 0): the apply gathers z and the previous
  *              direction, forms d = z + beta d_old itself (each dof's owner element stores it to a

@@ -64,7 +64,7 @@ def test_brick_update_predicated_faces_bitwise(gpu_ctx, shape, p, kinds, xfold):
             gpu_ctx.set_option("brick_upd_pb", pb)
             out[pb] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=25, check_every=7)
     finally:
-        gpu_ctx.set_option("brick_upd_pb", 0)
+        gpu_ctx.set_option("brick_upd_pb", 1)
         gpu_ctx.set_option("cg_xfold", 0)
     assert out[1][1]["iterations"] == out[0][1]["iterations"] == 25
     np.testing.assert_array_equal(out[1][0], out[0][0])
