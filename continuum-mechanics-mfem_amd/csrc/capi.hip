@@ -1680,6 +1680,12 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "brick_upd_pb") {
             if (value != 0 && value != 1) throw ArgError("brick_upd_pb must be 0 or 1");
             c->brick_upd_pb = value;
+        } else if (k == "ho_xcd") {
+            if (value != 0 && value != 1) throw ArgError("ho_xcd must be 0 or 1");
+            c->ho_xcd = value;
+        } else if (k == "ho_ye_nt") {
+            if (value != 0 && value != 1) throw ArgError("ho_ye_nt must be 0 or 1");
+            c->ho_ye_nt = value;
         } else if (k == "ho_dfold") {
             if (value != 0 && value != 1) throw ArgError("ho_dfold must be 0 or 1");
             c->ho_dfold = value;
@@ -1849,16 +1855,21 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
             const double nf = (double)nface_dofs;
             const double S = kBrick * c->p + 1.0;
             const double patches = 8.0 * S * S * S * (double)c->nblk;  // the CG apply's patch outputs
+            // x-fold (cg_xfold, Kronecker form): x += alpha d moves from the update into the apply
+            const bool xf = c->cg_xfold != 0 && pa_af(c) == 2;
             switch (k) {
             case CDFEM_K_APPLY:   // qdata (or per-element affine factors) + gathered r, M^-1, d + ess
                                   // flags + d (each dof by its one writer brick) + patch outputs
-                *bytes = 8.0 * c->ncomp * (c->d_qaff ? 1.0 : nq) * ne + 24.0 * nl + 1.0 * nl + 8.0 * nl + patches;
+                                  // (+ x read and written by its writer brick under the x-fold)
+                *bytes = 8.0 * c->ncomp * (c->d_qaff ? 1.0 : nq) * ne + 24.0 * nl + 1.0 * nl + 8.0 * nl + patches +
+                         (xf ? 16.0 * nl : 0.0);
                 return CDFEM_OK;
             case CDFEM_K_E2L:     // (the Mult's face-partial sum) face partials + x, ess, y of face dofs
                 *bytes = 8.0 * c->nface * (double)c->nblk + 25.0 * nf;
                 return CDFEM_OK;
-            case CDFEM_K_UPDATE:  // x, d, r, M^-1 read, ess, x, r write + the patch outputs (each once)
-                *bytes = 49.0 * nl + patches;
+            case CDFEM_K_UPDATE:  // x, d, r, M^-1 read, ess, x, r write + the patch outputs (each once);
+                                  // x-fold: r, M^-1, ess and r write only
+                *bytes = (xf ? 25.0 : 49.0) * nl + patches;
                 return CDFEM_OK;
             default: throw ArgError("kernel not launched on the brick path");
             }

@@ -220,10 +220,12 @@ struct cdfem_ctx {
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int brick_upd_pb = 1;               // set_option "brick_upd_pb": predicated-load face sums in the brick CG update
+    int ho_xcd = 0;                     // set_option "ho_xcd": XCD-contiguous block order of the Kronecker tile
+    int ho_ye_nt = 1;                   // set_option "ho_ye_nt": streaming E-vector stores of the Kronecker tile
     int ho_dfold = 1;                   // set_option "ho_dfold": CG direction folded into the Kronecker tile apply
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
     int cg_fused = 1;                   // set_option "cg_fused": fused high-order CG iteration (p >= 3 boxes)
-    int cg_xfold = 0;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply
+    int cg_xfold = 1;                   // set_option "cg_xfold": brick CG folds x += alpha d into the next apply
     int spmv_index16 = 1;               // set_option "spmv_index16": SpMV streams d_sdel when present
     int sell_mode = 8;                  // set_option "sell_order" (read when the FA pattern is built)
     int sell_window = 0;                // set_option "sell_window": rows per window of a windowed order (0 auto)

@@ -44,6 +44,7 @@ struct TileGeo {
     HoLayout ho;
     uint32_t Lx, Ly, nz;
     const uint8_t *ess;
+    int xcd, ye_nt;  // k_apply3d_ktile: XCD-contiguous block order, streaming E-vector stores
 };
 
 // DEN (CG mode, structured box, constrained): the block also publishes its share of
@@ -453,6 +454,10 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 //   z        output (ix, iy), all iz             threads (ix, iy): kron_z over the planes jz, then
 //            the E-vector store (and the den partials) exactly as k_apply3d_tile
 // Two barriers per element; 5 KB of LDS per element at p = 4, three blocks per CU.
+// geo.xcd (set_option "ho_xcd"): workgroup b runs on XCD b mod 8, so consecutive blocks (x
+// neighbours) and the blocks one element row / plane away land in different L2s, and a dof shared by
+// up to 8 elements is fetched by several XCDs; with xcd the blocks dealt to one XCD take one
+// contiguous range of elements instead.  geo.ye_nt: streaming (non-temporal) E-vector stores.
 // DF (fused CG, set_option "ho_dfold"): x is z = M^-1 r; the gather also reads d_old and forms the
 // direction d = z + beta d_old (k_cg_direction's formula) in registers, and each dof's one owner
 // element (the DEN ownership rule) writes it to d_new, so the direction pass disappears.
@@ -474,7 +479,12 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
 
     const int le = threadIdx.x / DD, t = threadIdx.x - le * DD;
     const int a = t % D1, b = t / D1;
-    const int e = blockIdx.x * EPB + le;
+    int blk = blockIdx.x;
+    if (geo.xcd) {
+        const int nb = gridDim.x, q = nb >> 3, r = nb & 7, x = blk & 7;
+        blk = x * q + min(x, r) + (blk >> 3);
+    }
+    const int e = blk * EPB + le;
     const bool inb = le < EPB, valid = inb && e < ne;
     const int ec = valid ? e : ne - 1;
     // this thread's x-stage rows (ix = a), in flight with the gather
@@ -586,7 +596,8 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
         }
 #pragma unroll
         for (int dz = 0; dz < D1; ++dz) {
-            __builtin_nontemporal_store(Yz[dz], &ye[dz * zs]);
+            if (geo.ye_nt) __builtin_nontemporal_store(Yz[dz], &ye[dz * zs]);
+            else ye[dz * zs] = Yz[dz];
             if constexpr (DEN) {
                 constexpr int P = D1 - 1;
                 const bool own = (a < P || ex == geo.ho.nx - 1) && (b < P || ey == geo.ho.ny - 1) &&
@@ -614,6 +625,8 @@ static hipError_t ktile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool co
     geo.Ly = (uint32_t)c->Ly;
     geo.nz = c->epencil ? (uint32_t)(c->ne / ((int64_t)geo.ho.nx * geo.ho.ny)) : 0;
     geo.ess = c->d_ess;
+    geo.xcd = c->ho_xcd;
+    geo.ye_nt = c->ho_ye_nt;
     const double *qa = c->d_qaff;
     double *const np = nullptr;
     // the x-stage rows (canonical entries of make_tab's orbit averages, as tM / tK / tCacc read them)

@@ -243,6 +243,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "brick_upd_pb": 1 (default) — the brick CG update (k_cg_update_faces) reads each dof's 1-8 patch
  *              entries as eight predicated buffer loads (absent ones out of range) instead of
  *              branching on the face planes (0); bitwise the same sums.
+ * "ho_xcd": 0 (default) — the Kronecker tile apply deals its workgroups to the 8 XCDs as one
+ *              contiguous element range each (1) instead of in dispatch order (bitwise the same E-vector).
+ * "ho_ye_nt": 1 (default) — streaming (non-temporal) E-vector stores in the Kronecker tile apply; 0 =
+ *              ordinary stores (same values).
  * "ho_dfold": 1 (default) — read by the CG solve on structured boxes (one rank, fused high-order CG,
  *              Kronecker tile: pa_affine 2, ho_mfma 0): the apply gathers z and the previous
  *              direction, forms d = z + beta d_old itself (each dof's owner element stores it to a
@@ -267,10 +271,11 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *                data.  All forms apply the operator of the per-point multilinear-map setup to rounding
  *                (the Kronecker form is an algebraic identity of the tensor rule, not an exactness
  *                argument); 0 = the per-point map and stream everywhere.
- * "cg_xfold": 0 (default) — 1: structured brick CG (p <= 2), each apply after the first advances x
- *             by the previous iteration's alpha d on the dofs it writes the new direction for, so the
- *             update kernel streams neither x nor d (bitwise the same iterates; measured even at C2:
- *             the apply gains what the update loses, profiles/r04/ab_c2_xfold_waves.json).
+ * "cg_xfold": 1 (default) — structured brick CG (p <= 2, Kronecker form): each apply after the first
+ *             advances x by the previous iteration's alpha d on the dofs it writes the new direction
+ *             for, so the update kernel streams neither x nor d (bitwise the same iterates; 1 % faster
+ *             at C2 in two A/B runs, profiles/r04/ab_c2_patchbuf_xfold.json, ab_c2_xfold_pb.json);
+ *             0 = x += alpha d in the update.
  * "cg_fused": 1 (default) — high-order (p = 3, 4) CG on a structured box, one rank: (d, A d) from the
  *             apply's element outputs and the E->L sum fused into the CG update; 0 = separate
  *             E->L kernel (results agree to rounding).

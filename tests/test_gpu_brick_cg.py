@@ -1,6 +1,6 @@
 """Brick CG (the BASELINE metric's loop) options that must not change the iterates.
 
-cg_xfold (option, default 0) moves x += alpha d of iteration k into the apply of iteration k + 1 (the dofs a
+cg_xfold (option, default 1) moves x += alpha d of iteration k into the apply of iteration k + 1 (the dofs a
 brick writes the new direction for), with k_cg_xflush adding the last update's term after the loop
 when the update logic stopped the solve.  Against cg_xfold 0 the solution must be bitwise equal for
 every way a solve ends: fixed iteration counts (max_iter, including 0, 1 and 2), convergence inside a
@@ -21,7 +21,7 @@ def _solve(gpu_ctx, om, shape, kinds, xfold, B, **kw):
     try:
         return gpu_ctx.solve(B, method="cg", pc="jacobi", **kw)
     finally:
-        gpu_ctx.set_option("cg_xfold", 0)
+        gpu_ctx.set_option("cg_xfold", 1)
 
 
 @pytest.mark.parametrize("shape,p,kinds,pert", [((8, 8, 8), 2, 7, 0.0), ((9, 6, 7), 2, 5, 0.1), ((6, 5, 7), 1, 7, 0.0)])
@@ -65,6 +65,6 @@ def test_brick_update_predicated_faces_bitwise(gpu_ctx, shape, p, kinds, xfold):
             out[pb] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=25, check_every=7)
     finally:
         gpu_ctx.set_option("brick_upd_pb", 1)
-        gpu_ctx.set_option("cg_xfold", 0)
+        gpu_ctx.set_option("cg_xfold", 1)
     assert out[1][1]["iterations"] == out[0][1]["iterations"] == 25
     np.testing.assert_array_equal(out[1][0], out[0][0])
