@@ -44,7 +44,6 @@ struct TileGeo {
     HoLayout ho;
     uint32_t Lx, Ly, nz;
     const uint8_t *ess;
-    int xcd, ye_nt;  // k_apply3d_ktile: XCD-contiguous block order, streaming E-vector stores
 };
 
 // DEN (CG mode, structured box, constrained): the block also publishes its share of
@@ -454,15 +453,14 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 //   z        output (ix, iy), all iz             threads (ix, iy): kron_z over the planes jz, then
 //            the E-vector store (and the den partials) exactly as k_apply3d_tile
 // Two barriers per element; 5 KB of LDS per element at p = 4, three blocks per CU.
-// geo.xcd (set_option "ho_xcd"): workgroup b runs on XCD b mod 8, so consecutive blocks (x
-// neighbours) and the blocks one element row / plane away land in different L2s, and a dof shared by
-// up to 8 elements is fetched by several XCDs; with xcd the blocks dealt to one XCD take one
-// contiguous range of elements instead.  geo.ye_nt: streaming (non-temporal) E-vector stores.
 // DF (fused CG, set_option "ho_dfold"): x is z = M^-1 r; the gather also reads d_old and forms the
 // direction d = z + beta d_old (k_cg_direction's formula) in registers, and each dof's one owner
 // element (the DEN ownership rule) writes it to d_new, so the direction pass disappears.
-template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, bool DF = false>
-__global__ void __launch_bounds__(256, 3)
+// W (set_option "ho_ktile_waves"): waves per SIMD the register allocation targets.  X lives in the
+// first group of the element's P buffer (a barrier separates the x stage's reads from the y stage's
+// writes), so a block takes 40 KB of LDS and four blocks fit a CU.
+template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, bool DF = false, int W = 3>
+__global__ void __launch_bounds__(256, W)
 k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qaff,
                 double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const TileGeo geo,
                 const KrylovState *__restrict__ st, double *__restrict__ part, const double *__restrict__ dold,
@@ -474,17 +472,12 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
     using L = QLayout<K, 3>;
     constexpr int NC = L::nc, DD = D1 * D1, ND = DD * D1;
     constexpr int EPB = 256 / DD;
-    __shared__ double sX[EPB][ND];
-    __shared__ double sP[EPB][4][ND];  // [grp][jz][iy][ix]
+    __shared__ double sP[EPB][4][ND];  // [grp][jz][iy][ix]; X[dz][dy][dx] in group 0 until the y stage
+    auto sX = [&](int e, int i) -> double & { return sP[e][0][i]; };
 
     const int le = threadIdx.x / DD, t = threadIdx.x - le * DD;
     const int a = t % D1, b = t / D1;
-    int blk = blockIdx.x;
-    if (geo.xcd) {
-        const int nb = gridDim.x, q = nb >> 3, r = nb & 7, x = blk & 7;
-        blk = x * q + min(x, r) + (blk >> 3);
-    }
-    const int e = blk * EPB + le;
+    const int e = blockIdx.x * EPB + le;
     const bool inb = le < EPB, valid = inb && e < ne;
     const int ec = valid ? e : ne - 1;
     // this thread's x-stage rows (ix = a), in flight with the gather
@@ -538,16 +531,16 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
 #pragma unroll
         for (int dz = 0; dz < D1; ++dz) {
             const bool zero = CON && (LAT ? m[dz] != 0 : m[dz] < 0);
-            sX[le][(dz * D1 + b) * D1 + a] = zero ? 0.0 : xr[dz];
+            sX(le, (dz * D1 + b) * D1 + a) = zero ? 0.0 : xr[dz];
         }
     }
     __syncthreads();
     // x + y stages: thread (ix = a, jz = b)
+    double v[D1][5];
     if (inb) {
-        double v[D1][5];
 #pragma unroll
         for (int jy = 0; jy < D1; ++jy) {
-            const double *xrow = &sX[le][(b * D1 + jy) * D1];
+            const double *xrow = &sX(le, (b * D1 + jy) * D1);
             double mm = 0.0, kk = 0.0, cc = 0.0, ct = 0.0;
 #pragma unroll
             for (int jx = 0; jx < D1; ++jx) {
@@ -561,6 +554,9 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
             }
             kron_xcombine<K>(g, mm, kk, cc, ct, v[jy]);
         }
+    }
+    __syncthreads();  // X (group 0 of sP) read by every thread of the element before P overwrites it
+    if (inb) {
         auto col = [&](int q, int jy) { return v[jy][q]; };
 #pragma unroll
         for (int iy = 0; iy < D1; ++iy) {
@@ -596,8 +592,7 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
         }
 #pragma unroll
         for (int dz = 0; dz < D1; ++dz) {
-            if (geo.ye_nt) __builtin_nontemporal_store(Yz[dz], &ye[dz * zs]);
-            else ye[dz * zs] = Yz[dz];
+            __builtin_nontemporal_store(Yz[dz], &ye[dz * zs]);
             if constexpr (DEN) {
                 constexpr int P = D1 - 1;
                 const bool own = (a < P || ex == geo.ho.nx - 1) && (b < P || ey == geo.ho.ny - 1) &&
@@ -625,8 +620,6 @@ static hipError_t ktile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool co
     geo.Ly = (uint32_t)c->Ly;
     geo.nz = c->epencil ? (uint32_t)(c->ne / ((int64_t)geo.ho.nx * geo.ho.ny)) : 0;
     geo.ess = c->d_ess;
-    geo.xcd = c->ho_xcd;
-    geo.ye_nt = c->ho_ye_nt;
     const double *qa = c->d_qaff;
     double *const np = nullptr;
     // the x-stage rows (canonical entries of make_tab's orbit averages, as tM / tK / tCacc read them)
@@ -657,8 +650,12 @@ static hipError_t ktile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool co
     if (kt == nullptr) return hipErrorInvalidValue;
     if (den_part && dnew) {
         if (!c->epencil || !con || !dold) return hipErrorInvalidValue;
-        CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye,
-                     T, c->ne, geo, st, den_part, dold, dnew, kt);
+        if (c->ho_ktile_waves == 4)
+            CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true, true, 4>), grid, block, 0, c->d_map, x, qa,
+                         Ye, T, c->ne, geo, st, den_part, dold, dnew, kt);
+        else
+            CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye,
+                         T, c->ne, geo, st, den_part, dold, dnew, kt);
     } else if (den_part) {
         if (!c->epencil || !con) return hipErrorInvalidValue;
         CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye, T,

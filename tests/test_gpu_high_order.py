@@ -367,32 +367,29 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
             assert np.linalg.norm(out[aff]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
 
 
+
 @pytest.mark.parametrize("shape,p", [((5, 4, 3), 4), ((7, 3, 4), 3)])
-def test_ktile_block_order_and_store_policy(gpu_ctx, shape, p):
-    """ho_xcd (XCD-contiguous workgroup order) and ho_ye_nt (store policy of the E-vector) change
-    where and how the Kronecker tile's blocks run, not what they compute: Mult and constrained Mult
-    bitwise equal to the default, 30 fused CG iterates within 1e-12 (the den partials are summed in
-    another order)."""
+def test_ktile_waves_variant(gpu_ctx, shape, p):
+    """ho_ktile_waves 4 (the fused Kronecker tile compiled for four waves per SIMD) against the default
+    3: the same arithmetic, so 30 fused CG iterates agree bitwise and match the oracle to 1e-11."""
     om = O.BoxMesh(3, shape, p)
     gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(7))
     rng = np.random.default_rng(23)
-    x = rng.uniform(-1, 1, om.nl)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
     b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=30)
     out = {}
     try:
-        for xcd, nt in ((0, 1), (1, 1), (0, 0), (1, 0)):
-            gpu_ctx.set_option("ho_xcd", xcd)
-            gpu_ctx.set_option("ho_ye_nt", nt)
+        for w in (3, 4):
+            gpu_ctx.set_option("ho_ktile_waves", w)
             gpu_ctx.upload_mesh(gm).set_structured(*shape)
             gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
-            _, B = gpu_ctx.form_linear_system(np.zeros(om.nl), b)
-            xg, _ = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=30, check_every=30)
-            out[xcd, nt] = (gpu_ctx.mult(x), gpu_ctx.mult(x, constrained=True), xg)
+            _, B = gpu_ctx.form_linear_system(u, b)
+            out[w], _ = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=30, check_every=30)
     finally:
-        gpu_ctx.set_option("ho_xcd", 0)
-        gpu_ctx.set_option("ho_ye_nt", 1)
-    y0, yc0, x0 = out[0, 1]
-    for key, (y, yc, xg) in out.items():
-        np.testing.assert_array_equal(y, y0)
-        np.testing.assert_array_equal(yc, yc0)
-        assert np.linalg.norm(xg - x0) <= 1e-12 * np.linalg.norm(x0), key
+        gpu_ctx.set_option("ho_ktile_waves", 3)
+    np.testing.assert_array_equal(out[4], out[3])
+    assert np.linalg.norm(out[3] - xo) <= 1e-11 * np.linalg.norm(xo)
