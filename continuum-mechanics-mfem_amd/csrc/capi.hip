@@ -1680,9 +1680,6 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "brick_upd_pb") {
             if (value != 0 && value != 1) throw ArgError("brick_upd_pb must be 0 or 1");
             c->brick_upd_pb = value;
-        } else if (k == "ho_ktile_waves") {
-            if (value != 3 && value != 4) throw ArgError("ho_ktile_waves must be 3 or 4");
-            c->ho_ktile_waves = value;
         } else if (k == "ho_dfold") {
             if (value != 0 && value != 1) throw ArgError("ho_dfold must be 0 or 1");
             c->ho_dfold = value;

@@ -456,11 +456,8 @@ k_apply3d_tile(const int32_t *__restrict__ map, const double *__restrict__ x, co
 // DF (fused CG, set_option "ho_dfold"): x is z = M^-1 r; the gather also reads d_old and forms the
 // direction d = z + beta d_old (k_cg_direction's formula) in registers, and each dof's one owner
 // element (the DEN ownership rule) writes it to d_new, so the direction pass disappears.
-// W (set_option "ho_ktile_waves"): waves per SIMD the register allocation targets.  X lives in the
-// first group of the element's P buffer (a barrier separates the x stage's reads from the y stage's
-// writes), so a block takes 40 KB of LDS and four blocks fit a CU.
-template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, bool DF = false, int W = 3>
-__global__ void __launch_bounds__(256, W)
+template <int D1, int Q1, unsigned K, bool CON, bool LAT, bool DEN, bool DF = false>
+__global__ void __launch_bounds__(256, 3)
 k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, const double *__restrict__ qaff,
                 double *__restrict__ Ye, const Tab<D1, Q1> T, const int ne, const TileGeo geo,
                 const KrylovState *__restrict__ st, double *__restrict__ part, const double *__restrict__ dold,
@@ -472,8 +469,8 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
     using L = QLayout<K, 3>;
     constexpr int NC = L::nc, DD = D1 * D1, ND = DD * D1;
     constexpr int EPB = 256 / DD;
-    __shared__ double sP[EPB][4][ND];  // [grp][jz][iy][ix]; X[dz][dy][dx] in group 0 until the y stage
-    auto sX = [&](int e, int i) -> double & { return sP[e][0][i]; };
+    __shared__ double sX[EPB][ND];
+    __shared__ double sP[EPB][4][ND];  // [grp][jz][iy][ix]
 
     const int le = threadIdx.x / DD, t = threadIdx.x - le * DD;
     const int a = t % D1, b = t / D1;
@@ -531,16 +528,16 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
 #pragma unroll
         for (int dz = 0; dz < D1; ++dz) {
             const bool zero = CON && (LAT ? m[dz] != 0 : m[dz] < 0);
-            sX(le, (dz * D1 + b) * D1 + a) = zero ? 0.0 : xr[dz];
+            sX[le][(dz * D1 + b) * D1 + a] = zero ? 0.0 : xr[dz];
         }
     }
     __syncthreads();
     // x + y stages: thread (ix = a, jz = b)
-    double v[D1][5];
     if (inb) {
+        double v[D1][5];
 #pragma unroll
         for (int jy = 0; jy < D1; ++jy) {
-            const double *xrow = &sX(le, (b * D1 + jy) * D1);
+            const double *xrow = &sX[le][(b * D1 + jy) * D1];
             double mm = 0.0, kk = 0.0, cc = 0.0, ct = 0.0;
 #pragma unroll
             for (int jx = 0; jx < D1; ++jx) {
@@ -554,9 +551,6 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
             }
             kron_xcombine<K>(g, mm, kk, cc, ct, v[jy]);
         }
-    }
-    __syncthreads();  // X (group 0 of sP) read by every thread of the element before P overwrites it
-    if (inb) {
         auto col = [&](int q, int jy) { return v[jy][q]; };
 #pragma unroll
         for (int iy = 0; iy < D1; ++iy) {
@@ -650,12 +644,8 @@ static hipError_t ktile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool co
     if (kt == nullptr) return hipErrorInvalidValue;
     if (den_part && dnew) {
         if (!c->epencil || !con || !dold) return hipErrorInvalidValue;
-        if (c->ho_ktile_waves == 4)
-            CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true, true, 4>), grid, block, 0, c->d_map, x, qa,
-                         Ye, T, c->ne, geo, st, den_part, dold, dnew, kt);
-        else
-            CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye,
-                         T, c->ne, geo, st, den_part, dold, dnew, kt);
+        CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye,
+                     T, c->ne, geo, st, den_part, dold, dnew, kt);
     } else if (den_part) {
         if (!c->epencil || !con) return hipErrorInvalidValue;
         CDFEM_LAUNCH(c, (k_apply3d_ktile<D1, Q1, K, true, true, true>), grid, block, 0, c->d_map, x, qa, Ye, T,

@@ -243,8 +243,6 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "brick_upd_pb": 1 (default) — the brick CG update (k_cg_update_faces) reads each dof's 1-8 patch
  *              entries as eight predicated buffer loads (absent ones out of range) instead of
  *              branching on the face planes (0); bitwise the same sums.
- * "ho_ktile_waves": 3 (default) — register target of the fused CG Kronecker tile apply (waves per
- *              SIMD); 4 = fewer registers, four blocks per CU (same arithmetic).
  * "ho_dfold": 1 (default) — read by the CG solve on structured boxes (one rank, fused high-order CG,
  *              Kronecker tile: pa_affine 2, ho_mfma 0): the apply gathers z and the previous
  *              direction, forms d = z + beta d_old itself (each dof's owner element stores it to a

@@ -367,29 +367,3 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
             assert np.linalg.norm(out[aff]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
 
 
-
-@pytest.mark.parametrize("shape,p", [((5, 4, 3), 4), ((7, 3, 4), 3)])
-def test_ktile_waves_variant(gpu_ctx, shape, p):
-    """ho_ktile_waves 4 (the fused Kronecker tile compiled for four waves per SIMD) against the default
-    3: the same arithmetic, so 30 fused CG iterates agree bitwise and match the oracle to 1e-11."""
-    om = O.BoxMesh(3, shape, p)
-    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
-    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(7))
-    rng = np.random.default_rng(23)
-    u = np.zeros(om.nl)
-    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
-    b = rng.uniform(-1, 1, om.nl)
-    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
-    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=30)
-    out = {}
-    try:
-        for w in (3, 4):
-            gpu_ctx.set_option("ho_ktile_waves", w)
-            gpu_ctx.upload_mesh(gm).set_structured(*shape)
-            gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
-            _, B = gpu_ctx.form_linear_system(u, b)
-            out[w], _ = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=30, check_every=30)
-    finally:
-        gpu_ctx.set_option("ho_ktile_waves", 3)
-    np.testing.assert_array_equal(out[4], out[3])
-    assert np.linalg.norm(out[3] - xo) <= 1e-11 * np.linalg.norm(xo)
