@@ -561,20 +561,30 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
 // loads at fixed offsets from its own brick's entry P (the lower brick's face entry along x / y / z
 // sits at P - 1 / P - R / P - A in the pencil layout), the missing ones at kOOB (read as 0), summed
 // in the branchy form's order (lower brick first per face axis, z outermost): bitwise the same q.
-template <int S, bool XF, bool PB = false>
+// DS (set_option "cg_den_fold", one rank): every workgroup sums the apply's den partials (apart,
+// napart) in one fixed order and takes MFEM's den step itself (workgroup 0 records it), so the
+// one-block den finalizer and its launch go away; the grid is a few hundred to a few thousand
+// workgroups (grid-stride loop) to keep the redundant sums small, and its partials go to part.
+template <int S, bool XF, bool PB = false, bool DS = false>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ d,
                   const double *__restrict__ dinv, const double *__restrict__ pb,
                   const uint8_t *__restrict__ ess, const BrickGeom g,
                   const FastDiv fdx, const FastDiv fdxy, int zlo_shared,
                   const double *__restrict__ remote_lo, const double *__restrict__ remote_hi,
-                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step)
+                  double *__restrict__ part, KrylovState *__restrict__ st, int den_step,
+                  const double *__restrict__ apart, int napart)
 {
     constexpr int s1 = S - 1;
-    __shared__ double sh[kRedThreads / 64];
+    __shared__ double sh[kRedThreads / 64 + 1];
     if (st->done) return;
     double alpha;
-    if (den_step) {
+    if constexpr (DS) {
+        const double den = sum_partials_all(apart, napart, sh);
+        if (blockIdx.x == 0 && threadIdx.x == 0) cg_den_step(st, den);
+        if (den == 0.0) return;
+        alpha = st->betanom / den;  // = cg_den_step's nom / den (block 0 may not have stored it yet)
+    } else if (den_step) {
         // multi-rank: the MFEM den step on the all-reduced den, folded in (no one-thread kernel
         // between the all-reduce and the update).  Every block forms alpha = betanom / den as
         // cg_den_step does; block 0 alone writes the state (den, nom, alpha; done if den == 0).
@@ -747,10 +757,16 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     // loads, so every dof's chain must be in flight at once
     const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
     const unsigned grid = (unsigned)(need < 16384 ? need : 16384);
+    // den fold (one rank): a grid of cg_den_fold workgroups, partials after the apply's
+    const bool ds = !den_step && !multi_rank(c) && c->cg_den_fold != 0;
+    const unsigned ugrid = ds ? (unsigned)std::min<int64_t>(c->cg_den_fold, need) : grid;
+    double *const upart = ds ? c->d_part + c->nblk : c->d_part;
+#define CDFEM_UPD3(S_, XF_, PB_, DS_)                                                                      \
+    hipLaunchKernelGGL((k_cg_update_faces<S_, XF_, PB_, DS_>), dim3(ugrid), dim3(kRedThreads), 0, c->stream, x, r, \
+                       d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, upart,  \
+                       c->d_state, (int)den_step, c->d_part, c->nblk)
 #define CDFEM_UPD2(S_, XF_, PB_)                                                                           \
-    hipLaunchKernelGGL((k_cg_update_faces<S_, XF_, PB_>), dim3(grid), dim3(kRedThreads), 0, c->stream, x, r, d, \
-                       dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, c->d_part, \
-                       c->d_state, (int)den_step)
+    if (ds) { CDFEM_UPD3(S_, XF_, PB_, true); } else { CDFEM_UPD3(S_, XF_, PB_, false); }
     // predicated-load face sums: the patch buffer's byte offsets must fit 32 bits
     const double s3 = std::pow(kBrick * c->p + 1.0, 3.0);
     const bool pb = c->brick_upd_pb != 0 && 8.0 * (double)c->nblk * s3 < 4294967296.0;
@@ -769,10 +785,11 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     }
 #undef CDFEM_UPD
 #undef CDFEM_UPD2
+#undef CDFEM_UPD3
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (multi_rank(c)) return launch_fin_sum(c, (int)grid, 1);
-    return launch_update_fin(c, (int)grid);
+    return launch_update_fin(c, (int)ugrid, ds ? c->nblk : 0);
 }
 
 

@@ -450,8 +450,8 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], c->Lx * c->Ly);
             HIPCHK(launch_fin_sum(c, c->nblk, 0));
             comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
-        } else {
-            HIPCHK(launch_den_fin(c, c->nblk));
+        } else if (!c->cg_den_fold) {
+            HIPCHK(launch_den_fin(c, c->nblk));  // (cg_den_fold: the update kernel takes the den step)
         }
         prof_mark(c, CDFEM_K_E2L, false);
     };
@@ -1677,6 +1677,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "mr_overlap") {
             if (value < 0 || value > 1) throw ArgError("mr_overlap must be 0 or 1");
             c->mr_overlap = value;
+        } else if (k == "cg_den_fold") {
+            if (value != 0 && (value < 64 || value > 16384)) throw ArgError("cg_den_fold must be 0 or 64..16384");
+            c->cg_den_fold = value;
         } else if (k == "brick_upd_pb") {
             if (value != 0 && value != 1) throw ArgError("brick_upd_pb must be 0 or 1");
             c->brick_upd_pb = value;

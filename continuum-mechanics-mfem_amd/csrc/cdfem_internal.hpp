@@ -219,6 +219,7 @@ struct cdfem_ctx {
     int mr_overlap = 1;                 // set_option "mr_overlap": slab CG exchange overlapped with interior bricks
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
+    int cg_den_fold = 0;                // set_option "cg_den_fold": brick CG den step in the update (N workgroups; 0 off)
     int brick_upd_pb = 1;               // set_option "brick_upd_pb": predicated-load face sums in the brick CG update
     int ho_dfold = 1;                   // set_option "ho_dfold": CG direction folded into the Kronecker tile apply
     int ho_mfma = 0;                    // set_option "ho_mfma": bit 0 = stage x of the p >= 3 tile apply on MFMA
@@ -354,7 +355,7 @@ hipError_t launch_cg_update_noz(cdfem_ctx *c, double *x, double *r, const double
 hipError_t launch_zero(cdfem_ctx *c, double *y);
 // one-block finalizers: den = sum(d_part[0..nparts)) (MFEM CG den step); betanom (update step)
 hipError_t launch_den_fin(cdfem_ctx *c, int nparts);
-hipError_t launch_update_fin(cdfem_ctx *c, int nparts);
+hipError_t launch_update_fin(cdfem_ctx *c, int nparts, int64_t off = 0);
 // brick CG v2 (brick_kernels.hip): d_new = M^{-1} r + beta d_old, q/face partials, den partials
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
                             double *d_new, double *q, double *x = nullptr);

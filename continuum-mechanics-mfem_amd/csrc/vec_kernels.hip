@@ -476,9 +476,9 @@ hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *d0, const dou
     return hipGetLastError();
 }
 
-hipError_t launch_update_fin(cdfem_ctx *c, int nparts)
+hipError_t launch_update_fin(cdfem_ctx *c, int nparts, int64_t off)
 {
-    hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part, nparts, c->d_state);
+    hipLaunchKernelGGL(k_cg_update_fin, dim3(1), dim3(1024), 0, c->stream, c->d_part + off, nparts, c->d_state);
     return hipGetLastError();
 }
 

@@ -68,3 +68,40 @@ def test_brick_update_predicated_faces_bitwise(gpu_ctx, shape, p, kinds, xfold):
         gpu_ctx.set_option("cg_xfold", 1)
     assert out[1][1]["iterations"] == out[0][1]["iterations"] == 25
     np.testing.assert_array_equal(out[1][0], out[0][0])
+
+
+@pytest.mark.parametrize("shape,p,kinds,fold", [((8, 8, 8), 2, 7, 256), ((9, 6, 7), 2, 5, 1024), ((6, 5, 7), 1, 7, 64)])
+def test_den_fold_matches_den_finalizer(gpu_ctx, shape, p, kinds, fold):
+    """cg_den_fold N: the update kernel (N workgroups) sums the apply's den partials itself and takes
+    MFEM's den step, instead of the one-block finalizer (which sums them with 1024 threads, so den
+    differs by rounding): 30 fixed iterates within 1e-12 of the finalizer path and 1e-11 of the
+    oracle; on the SPD operator a converging solve stops on the same iteration."""
+    om = O.BoxMesh(3, shape, p)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3,
+                      kinds=(O.DIFFUSION if kinds & 1 else 0) | (O.CONVECTION if kinds & 2 else 0) |
+                      (O.MASS if kinds & 4 else 0))
+    rng = np.random.default_rng(31)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(*shape)
+    gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    out, conv = {}, {}
+    try:
+        for f in (fold, 0):
+            gpu_ctx.set_option("cg_den_fold", f)
+            out[f] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30, check_every=7)
+            if kinds == 5:
+                conv[f] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=1e-8, max_iter=2000, check_every=7)
+    finally:
+        gpu_ctx.set_option("cg_den_fold", 0)
+    for f, (xg, ig) in out.items():
+        assert ig["iterations"] == 30
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), f
+    assert np.linalg.norm(out[fold][0] - out[0][0]) <= 1e-12 * np.linalg.norm(out[0][0])
+    if conv:
+        assert conv[fold][1]["converged"] and conv[fold][1]["iterations"] == conv[0][1]["iterations"]
+        assert np.linalg.norm(conv[fold][0] - conv[0][0]) <= 1e-10 * np.linalg.norm(conv[0][0])
