@@ -240,9 +240,11 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
  *               interface pack and the exchange run on a side stream under the interior layers;
  *               0 = one launch, then the exchange (bitwise the same results).
- * "cg_den_fold": 0 (default) — N (64..16384): the one-rank brick CG takes MFEM's den step inside the
- *              update kernel, run as N workgroups that each sum the apply's den partials in one fixed
- *              order; the one-block den finalizer is not launched (iterates agree to rounding).
+ * "cg_den_fold": 1024 (default) — N (64..16384): the one-rank brick CG takes MFEM's den step inside
+ *              the update kernel, run as N workgroups that each sum the apply's den partials in one
+ *              fixed order; the one-block den finalizer is not launched (iterates agree with the
+ *              finalizer path, 0, to rounding; C2: 62.4 against 64.6 us per iteration,
+ *              profiles/r04/ab_c2_den_fold.json).
  * "brick_upd_pb": 1 (default) — the brick CG update (k_cg_update_faces) reads each dof's 1-8 patch
  *              entries as eight predicated buffer loads (absent ones out of range) instead of
  *              branching on the face planes (0); bitwise the same sums.

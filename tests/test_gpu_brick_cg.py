@@ -97,7 +97,7 @@ def test_den_fold_matches_den_finalizer(gpu_ctx, shape, p, kinds, fold):
             if kinds == 5:
                 conv[f] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=1e-8, max_iter=2000, check_every=7)
     finally:
-        gpu_ctx.set_option("cg_den_fold", 0)
+        gpu_ctx.set_option("cg_den_fold", 1024)
     for f, (xg, ig) in out.items():
         assert ig["iterations"] == 30
         assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), f
