@@ -1714,6 +1714,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || (value > 0 && (value % 64 != 0 || value > (1 << 20))))
                 throw ArgError("sell_window must be 0 (auto) or a multiple of 64 up to 2^20");
             c->sell_window = value;
+        } else if (k == "gm_dpp") {
+            if (value != 0 && value != 1) throw ArgError("gm_dpp must be 0 or 1");
+            c->gm_dpp = value;
         } else if (k == "gm_ept") {
             if (value != 0 && value != 4 && value != 5 && value != 6 && value != 8)
                 throw ArgError("gm_ept must be 0 (auto), 4, 5, 6 or 8");

@@ -155,6 +155,7 @@ struct cdfem_ctx {
     double *d_ones = nullptr;           // all-ones vector (unpreconditioned brick CG)
     double *d_dalt = nullptr;           // second search-direction buffer (brick CG)
     int nface = 0;                      // F
+    int gm_dpp = 1;                     // set_option "gm_dpp": DPP wave sums for the GMRES projections (pass 1)
     int gm_ept = 0;                     // set_option "gm_ept": GMRES orthogonalisation entries per thread (0: auto, orth_ept)
     int gm_ept_auto = 4;                // the automatic choice for vectors of gm_ept_n entries
     int64_t gm_ept_n = -1;

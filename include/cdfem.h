@@ -303,6 +303,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *             auto orders (sell_order 8, and the RCM windows sell_order 3 picks on unstructured meshes
  *             without coordinates: 768 rows).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
+ * "gm_dpp": 1 (default) — GMRES orthogonalisation pass 1 sums each projection across a wave with
+ *           four DPP row moves and two shuffles (0: six shuffles through the LDS crossbar); the
+ *           projections are summed in another fixed order, so iterates agree to rounding.
  * "gm_ept": 0 (default, auto) — entries per thread of the GMRES orthogonalisation passes (4, 5, 6
  *           or 8); auto takes the smallest whose grid is resident in one round (same results).
  * Variants measured slower and removed in round 3 (their records stay under profiles/r02_ab_*):
