@@ -434,8 +434,9 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // below, which owns it for the dot products (remote_lo / remote_hi carry the neighbours' partial
 // sums of the interface planes; nullptr on a single GPU).
 // ================================================================================================
-// W: waves per SIMD the register allocation targets (set_option "brick_cg_waves"; the Kronecker
-// form fits 2 without spills, 3 with a few spilled scalars; the point-data forms take 1)
+// W: waves per SIMD the register allocation targets (the Kronecker form fits 2 without spills; three
+// waves, 168 registers with a few spilled values, measured slower twice: profiles/r04/ab_c2_xfold_waves.json,
+// ab_c2_xfold_pb.json; the point-data forms take 1)
 template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false>
 __global__ void __launch_bounds__(64, W)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
@@ -697,7 +698,6 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
 #define CDFEM_BCG(AFF_, W_) CDFEM_BCG3(AFF_, W_, false)
     if (pa_af(c) == 2) {
         if (x) { CDFEM_BCG3(2, 2, true); }
-        else if (c->brick_cg_waves == 3) { CDFEM_BCG(2, 3); }
         else { CDFEM_BCG(2, 2); }
     } else if (pa_af(c) == 1) {
         CDFEM_BCG(1, 1);

@@ -1668,10 +1668,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
     return guarded(c, [&] {
         if (!key) throw ArgError("key is null");
         const std::string k(key);
-        if (k == "brick_cg_waves") {
-            if (value != 2 && value != 3) throw ArgError("brick_cg_waves must be 2 or 3");
-            c->brick_cg_waves = value;
-        } else if (k == "brick_xcd") {
+        if (k == "brick_xcd") {
             if (value < 0 || value > 1) throw ArgError("brick_xcd must be 0 or 1");
             c->brick_xcd = value;
         } else if (k == "mr_overlap") {

@@ -161,7 +161,6 @@ struct cdfem_ctx {
     int64_t gm_ept_n = -1;
     int brick_xcd = 1;                  // k_brick_cg brick order: 0 dispatch, 1 XCD-contiguous (default)
     int ncu = 0;                        // compute units of the device
-    int brick_cg_waves = 2;             // set_option "brick_cg_waves": waves per SIMD of the Kronecker k_brick_cg (2, 3)
     int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)
     int zhi_shared = 0;                 // local gz=Lz-1 plane shared with the rank above
     cdfem::Comm *comm = nullptr;        // rank communicator (comm.hip), nullptr on one GPU

@@ -232,9 +232,6 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
 /* ---- tuning knobs (performance only; results identical to rounding) --------------------------
  * "profile_mask": bit k set = kernel slot k (CDFEM_K_*) gets HIP events while profiling is on
  *                 (default all; events around every kernel cost ~1 us each on the stream).
- * "brick_cg_waves": 2 (default) — waves per SIMD the Kronecker-form structured CG kernel is compiled
- *                   for (register budget, spill-free); 3 = a tighter budget with a few spills (measured
- *                   slower: 80.7 against 77.4 us per C2 iteration, profiles/r04/ab_c2_xfold_waves.json).
  * "brick_xcd": 1 (default) — XCD-contiguous brick order of the structured CG kernel; 0 = the
  *              dispatcher's round-robin order.
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
