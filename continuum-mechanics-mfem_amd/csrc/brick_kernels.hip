@@ -165,11 +165,41 @@ __device__ __forceinline__ void brick_e2l(double *s_out, int o0, const double (&
     }
 }
 
+// The 1-8 patch-buffer entries of lattice dof (gx, gy, gz) summed in a fixed order (lower brick first
+// per face axis, z outermost): eight buffer loads at fixed offsets from its own brick's entry P (the
+// lower brick's face entry along x / y / z sits at P - 1 / P - R / P - A in the pencil layout of
+// patch_idx), the absent ones at kOOB (read as 0).
+template <int S>
+__device__ __forceinline__ double patch_sum8(__amdgpu_buffer_rsrc_t bp, const BrickGeom &g, int gx, int gy, int gz)
+{
+    constexpr int s1 = S - 1;
+    const int qx = min(gx / s1, g.nbx - 1), qy = min(gy / s1, g.nby - 1), qz = min(gz / s1, g.nbz - 1);
+    const int px = gx - qx * s1, py = gy - qy * s1, pz = gz - qz * s1;
+    const bool fx = px == 0 && qx > 0, fy = py == 0 && qy > 0, fz = pz == 0 && qz > 0;
+    const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
+    const uint32_t P = (((uint32_t)qz * S + pz) * g.nby + qy) * S * R + (uint32_t)py * R + (uint32_t)qx * S + px;
+    double t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int sz = (k >> 2) & 1 ? 0 : 1, sy = (k >> 1) & 1 ? 0 : 1, sx = k & 1 ? 0 : 1;
+        const bool ok = (!sx || fx) && (!sy || fy) && (!sz || fz);
+        const uint32_t o = P - (uint32_t)sx - (uint32_t)sy * R - (uint32_t)sz * A;
+        t[k] = bload(bp, ok ? 8u * o : kOOB);
+    }
+    double q = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q += t[k];
+    return q;
+}
+
 // MODE 0: y = A x;  MODE 1: y = A_c x (ConstrainedOperator).  (The CG loop runs k_brick_cg.)
+// PBO (set_option "brick_mult_pb"): the whole patch sum goes to the patch buffer (patch_idx, as the CG
+// kernel writes it) and k_brick_patch_sum forms y; otherwise owned dofs go to y, face dofs to the
+// brick's face partials (k_brick_faces).
 // One wave per SIMD with the per-point stream, unconstrained registers: 241.5 vs 272.2 us per C2
 // apply in the GMRES leg against a two-waves-per-SIMD build (<= 256 registers, 124 B/lane of
 // spills; tools/ab_gmres.py, profiles/r02_ab_c2_gmres_brick_waves.txt); two with the Kronecker form.
-template <int D1, int Q1, unsigned K, int MODE, int AF>
+template <int D1, int Q1, unsigned K, int MODE, int AF, bool PBO = false>
 __global__ void __launch_bounds__(64, AF == 2 ? 2 : 1)
 k_brick3d(const double *__restrict__ x, double *__restrict__ y, double *__restrict__ face,
           const double *__restrict__ qd, const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g)
@@ -226,6 +256,23 @@ k_brick3d(const double *__restrict__ x, double *__restrict__ y, double *__restri
     // 3. deterministic E->L inside the brick (brick_e2l: all lanes of a step write distinct targets)
     brick_e2l<D1, S>(s_out, o0, Y);
 
+    if constexpr (PBO) {
+        // 4'. the whole patch -> the patch buffer (32-bit index: base + pz A + py R + px)
+        const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
+        const int bxp = b % g.nbx, byp = (b / g.nbx) % g.nby, bzp = b / (g.nbx * g.nby);
+        const uint32_t base = (uint32_t)bzp * S * A + (uint32_t)byp * S * R + (uint32_t)bxp * S;
+        const auto bp = brsrc(face, 8u * (uint32_t)g.nbx * g.nby * g.nbz * S3);
+        const unsigned tp = (unsigned)opaque(t);
+        PatchWalk<S> pw(tp);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const unsigned i = tp + 64 * k;
+            if (k == NI - 1 && i >= S3) break;
+            bstore(bp, 8u * (base + (uint32_t)pw.z * A + (uint32_t)pw.y * R + (uint32_t)pw.x), s_out[i]);
+            pw.next();
+        }
+        return;
+    }
     // 4. owned dofs -> y (constrained: y = x on ess rows), face dofs -> this brick's partials
     double *const fb = face + (size_t)b * F;
     const unsigned to = (unsigned)opaque(t);
@@ -336,6 +383,29 @@ k_brick_faces(const double *__restrict__ x, const double *__restrict__ dinv, dou
     }
 }
 
+// The structured Mult's row sums from k_brick3d<..., PBO>'s patch buffer: y = the dof's 1-8 patch
+// entries (patch_sum8), constrained (MODE 1): y = x on essential rows.  Rank-local: the interface
+// planes of a slab get this rank's partial sums, as from k_brick_faces.
+template <int S, int MODE>
+__global__ void __launch_bounds__(kRedThreads)
+k_brick_patch_sum(const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ pb,
+                  const uint8_t *__restrict__ ess, const BrickGeom g, const FastDiv fdx, const FastDiv fdxy)
+{
+    const int n = g.Lx * g.Ly * g.Lz, plane = g.Lx * g.Ly;
+    const auto bp = brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S));
+    for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += gridDim.x * blockDim.x) {
+        const int gz = (int)fdiv((uint32_t)gid, fdxy);
+        const int rem = gid - gz * plane;
+        const int gy = (int)fdiv((uint32_t)rem, fdx);
+        const int gx = rem - gy * g.Lx;
+        double v = patch_sum8<S>(bp, g, gx, gy, gz);
+        if constexpr (MODE == 1) {
+            if (ess[gid]) v = x[gid];
+        }
+        __builtin_nontemporal_store(v, &y[gid]);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 bool brick_supported(int dim, int p) { return dim == 3 && (p == 1 || p == 2); }
 
@@ -358,17 +428,29 @@ static hipError_t brick_launch(cdfem_ctx *c, const double *x, const double *dinv
 {
     constexpr int S = kBrick * (D1 - 1) + 1;
     const BrickGeom g = geom_of(c);
+    // patch-buffer Mult (Kronecker form, byte offsets within 32 bits)
+    const bool mpb = c->brick_mult_pb != 0 && pa_af(c) == 2 && 8.0 * c->nblk * (double)(S * S * S) < 4294967296.0;
     if (which & 1) {
         const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
 #define CDFEM_B3(AF_, QD_)                                                                                    \
     hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, AF_>), dim3(c->nblk), dim3(64), 0, c->stream, x, y, c->d_face, \
                        QD_, c->d_ess, T, g)
-        if (pa_af(c) == 2) CDFEM_B3(2, c->d_qaff);
+        if (pa_af(c) == 2 && mpb)
+            hipLaunchKernelGGL((k_brick3d<D1, Q1, K, MODE, 2, true>), dim3(c->nblk), dim3(64), 0, c->stream, x, y,
+                               c->d_face, c->d_qaff, c->d_ess, T, g);
+        else if (pa_af(c) == 2) CDFEM_B3(2, c->d_qaff);
         else if (pa_af(c) == 1) CDFEM_B3(1, c->d_qaff);
         else CDFEM_B3(0, c->d_qd);
 #undef CDFEM_B3
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+    }
+    if ((which & 2) && mpb) {
+        const FastDiv fdx = make_fastdiv((uint32_t)c->Lx), fdxy = make_fastdiv((uint32_t)(c->Lx * c->Ly));
+        const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
+        hipLaunchKernelGGL((k_brick_patch_sum<S, MODE>), dim3((unsigned)std::min<int64_t>(need, 16384)),
+                           dim3(kRedThreads), 0, c->stream, x, y, c->d_face, c->d_ess, g, fdx, fdxy);
+        return hipGetLastError();
     }
     if (which & 2) {
         const dim3 fg = faces_grid(c);
@@ -614,23 +696,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         const double rold = r[gid], mi = dinv[gid];
         double qi;
         if constexpr (PB) {
-            const int qx = min(gx / s1, g.nbx - 1), qy = min(gy / s1, g.nby - 1), qz = min(gz / s1, g.nbz - 1);
-            const int px = gx - qx * s1, py = gy - qy * s1, pz = gz - qz * s1;
-            const bool fx = px == 0 && qx > 0, fy = py == 0 && qy > 0, fz = pz == 0 && qz > 0;
-            const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
-            const uint32_t P = (((uint32_t)qz * S + pz) * g.nby + qy) * S * R + (uint32_t)py * R + (uint32_t)qx * S + px;
-            const auto bp = brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S));
-            double t[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int sz = (k >> 2) & 1 ? 0 : 1, sy = (k >> 1) & 1 ? 0 : 1, sx = k & 1 ? 0 : 1;
-                const bool ok = (!sx || fx) && (!sy || fy) && (!sz || fz);
-                const uint32_t o = P - (uint32_t)sx - (uint32_t)sy * R - (uint32_t)sz * A;
-                t[k] = bload(bp, ok ? 8u * o : kOOB);
-            }
-            qi = 0.0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) qi += t[k];
+            qi = patch_sum8<S>(brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S)), g, gx, gy, gz);
         } else if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
             int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
             const int qx = gx / s1, qy = gy / s1, qz = gz / s1;

@@ -1674,6 +1674,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "mr_overlap") {
             if (value < 0 || value > 1) throw ArgError("mr_overlap must be 0 or 1");
             c->mr_overlap = value;
+        } else if (k == "brick_mult_pb") {
+            if (value != 0 && value != 1) throw ArgError("brick_mult_pb must be 0 or 1");
+            c->brick_mult_pb = value;
         } else if (k == "cg_den_fold") {
             if (value != 0 && (value < 64 || value > 16384)) throw ArgError("cg_den_fold must be 0 or 64..16384");
             c->cg_den_fold = value;

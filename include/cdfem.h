@@ -237,6 +237,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
  *               interface pack and the exchange run on a side stream under the interior layers;
  *               0 = one launch, then the exchange (bitwise the same results).
+ * "brick_mult_pb": 0 (default) — the structured Mult (GMRES, cdfem_pa_mult; Kronecker form) writes
+ *              each brick's whole patch sum to the patch buffer and a second pass forms every row from
+ *              its 1-8 entries (predicated loads), instead of owned rows + face partials + face sums.
+ *              Same sums in the same order.
  * "cg_den_fold": 1024 (default) — N (64..16384): the one-rank brick CG takes MFEM's den step inside
  *              the update kernel, run as N workgroups that each sum the apply's den partials in one
  *              fixed order; the one-block den finalizer is not launched (iterates agree with the

@@ -3,7 +3,7 @@ D+C+M; the reference's solver, Input/petsc.opts), GPU box only.  One context; op
 before each solve.  Prints per variant the median operator-apply and orthogonalisation times per
 inner step (HIP events) and the wall time per step.
 
-    python tools/ab_gmres.py [--rounds R] [--iters K] [--variants "brick_waves=1,brick_waves=2"]
+    python tools/ab_gmres.py [--rounds R] [--iters K] [--variants "gm_dpp=0/brick_mult_pb=0,gm_dpp=1/brick_mult_pb=0"]
 """
 import argparse
 import json
@@ -33,12 +33,15 @@ ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=(1.0, -2.0, 0.5), mass=1.0)
 b = np.random.default_rng(20261015).uniform(-1, 1, mesh.nl)
 _, B = ctx.form_linear_system(np.zeros(mesh.nl), b)
 dB, dX = ctx.to_device(B), ctx.alloc(8 * mesh.nl)
-variants = [v.split("=") for v in args.variants.split(",")]
-res = {f"{k}={v}": {"apply_us": [], "orth_us": [], "step_us": []} for k, v in variants}
+# a variant is one or more k=v settings joined by '/', all set before its solve (options persist on
+# the context, so every variant should name every key the list varies)
+variants = [(v, [kv.split("=") for kv in v.split("/")]) for v in args.variants.split(",")]
+res = {name: {"apply_us": [], "orth_us": [], "step_us": []} for name, _ in variants}
 ref = None
 for rnd in range(args.rounds + 1):
-    for k, v in variants:
-        ctx.set_option(k, int(v))
+    for name, kvs in variants:
+        for k, v in kvs:
+            ctx.set_option(k, int(v))
         ctx.set_option("profile_mask", (1 << cdfem.K_APPLY) | (1 << cdfem.K_ORTH))
         ctx.profile(not args.no_prof)
         ctx.synchronize()
@@ -56,7 +59,7 @@ for rnd in range(args.rounds + 1):
         assert np.abs(x - ref).max() <= 1e-9 * np.abs(ref).max()
         if rnd == 0:
             continue
-        r = res[f"{k}={v}"]
+        r = res[name]
         r["apply_us"].append(a[0] / max(a[1], 1) * 1e3)
         r["orth_us"].append(o[0] / max(o[1], 1) * 1e3)
         r["step_us"].append(dt / info["iterations"] * 1e6)
