@@ -600,10 +600,10 @@ def main():
                 roof = {"bound": "hbm", **hbm_view}
             roof.update({
                     "kernel": (("k_brick_cg (brick patch gather + fused CG direction + D/C/M PA apply" +
-                                (", Kronecker form of the affine factors" if affine else "") +
+                                (", Kronecker form of the affine factors, x += alpha d folded in" if affine else "") +
                                 " + in-LDS E->L + d.Ad)") if args.path == "brick"
                                else ("k_apply3d_ktile (D1 x D1 thread tile per element, Kronecker form of the affine "
-                                     "factors)" if affine else
+                                     "factors, CG direction folded in)" if affine else
                                      "k_apply3d_tile (Q1 x Q1 thread tile per element, z planes in registers)")
                                if args.order >= 3
                                else "k_apply3d (fused L->E gather + D/C/M PA apply)"),
