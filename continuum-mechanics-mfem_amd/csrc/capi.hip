@@ -1714,9 +1714,6 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || (value > 0 && (value % 64 != 0 || value > (1 << 20))))
                 throw ArgError("sell_window must be 0 (auto) or a multiple of 64 up to 2^20");
             c->sell_window = value;
-        } else if (k == "gm_dpp") {
-            if (value != 0 && value != 1) throw ArgError("gm_dpp must be 0 or 1");
-            c->gm_dpp = value;
         } else if (k == "gm_ept") {
             if (value != 0 && value != 4 && value != 5 && value != 6 && value != 8)
                 throw ArgError("gm_ept must be 0 (auto), 4, 5, 6 or 8");
@@ -1864,8 +1861,10 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
                 *bytes = 8.0 * c->ncomp * (c->d_qaff ? 1.0 : nq) * ne + 24.0 * nl + 1.0 * nl + 8.0 * nl + patches +
                          (xf ? 16.0 * nl : 0.0);
                 return CDFEM_OK;
-            case CDFEM_K_E2L:     // (the Mult's face-partial sum) face partials + x, ess, y of face dofs
-                *bytes = 8.0 * c->nface * (double)c->nblk + 25.0 * nf;
+            case CDFEM_K_E2L:     // the Mult's row sums: the patch buffer + ess flags + y (brick_mult_pb,
+                                  // Kronecker form), or face partials + x, ess, y of the face dofs
+                *bytes = (c->brick_mult_pb && pa_af(c) == 2) ? patches + 9.0 * nl
+                                                             : 8.0 * c->nface * (double)c->nblk + 25.0 * nf;
                 return CDFEM_OK;
             case CDFEM_K_UPDATE:  // x, d, r, M^-1 read, ess, x, r write + the patch outputs (each once);
                                   // x-fold: r, M^-1, ess and r write only

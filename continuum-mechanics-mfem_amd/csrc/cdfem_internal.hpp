@@ -155,7 +155,6 @@ struct cdfem_ctx {
     double *d_ones = nullptr;           // all-ones vector (unpreconditioned brick CG)
     double *d_dalt = nullptr;           // second search-direction buffer (brick CG)
     int nface = 0;                      // F
-    int gm_dpp = 1;                     // set_option "gm_dpp": DPP wave sums for the GMRES projections (pass 1)
     int gm_ept = 0;                     // set_option "gm_ept": GMRES orthogonalisation entries per thread (0: auto, orth_ept)
     int gm_ept_auto = 4;                // the automatic choice for vectors of gm_ept_n entries
     int64_t gm_ept_n = -1;
@@ -219,7 +218,7 @@ struct cdfem_ctx {
     int mr_overlap = 1;                 // set_option "mr_overlap": slab CG exchange overlapped with interior bricks
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
-    int brick_mult_pb = 0;              // set_option "brick_mult_pb": structured Mult through the patch buffer
+    int brick_mult_pb = 1;              // set_option "brick_mult_pb": structured Mult through the patch buffer
     int cg_den_fold = 1024;             // set_option "cg_den_fold": brick CG den step in the update (N workgroups; 0 off)
     int brick_upd_pb = 1;               // set_option "brick_upd_pb": predicated-load face sums in the brick CG update
     int ho_dfold = 1;                   // set_option "ho_dfold": CG direction folded into the Kronecker tile apply

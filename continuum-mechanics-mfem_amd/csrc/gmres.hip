@@ -26,8 +26,6 @@
 
 namespace cdfem {
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
 constexpr int kGmEPT = 4;                         // L-vector entries per thread in the pass kernels
 constexpr int kGmBatch = 2;                       // projections per load batch in pass 1
 constexpr int kGmBatch2 = 4;                      // basis vectors per load batch in pass 2
@@ -118,30 +116,7 @@ k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st,
 // dropped).  Each wave parks its wave sums in LDS, so the whole step needs ONE barrier before the
 // block sums.  Measured at C4 (orthogonalisation per step): one barrier per batch of 8, 93.9 us;
 // one barrier in all, batches of 8 / 4 / 2 / 1: 85.7 / 83.2 / 82.6 / 82.1 us.
-// wave sum for the projections of pass 1: the first four butterfly steps as DPP moves inside each
-// 16-lane row (quad_perm xor 1 / xor 2, row_ror 4 / 8: no LDS round trip), the last two as shuffles.
-// A fixed order, so every lane holds the same bits; not the order of reduce.hpp's wave_sum.
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v)
-{
-    const u32x2 p = __builtin_bit_cast(u32x2, v);
-    u32x2 q;
-    q.x = (unsigned)__builtin_amdgcn_mov_dpp((int)p.x, CTRL, 0xF, 0xF, false);
-    q.y = (unsigned)__builtin_amdgcn_mov_dpp((int)p.y, CTRL, 0xF, 0xF, false);
-    return __builtin_bit_cast(double, q);
-}
-__device__ __forceinline__ double wave_sum_dpp(double v)
-{
-    v += dpp_d<0xB1>(v);   // quad_perm [1, 0, 3, 2]
-    v += dpp_d<0x4E>(v);   // quad_perm [2, 3, 0, 1]
-    v += dpp_d<0x124>(v);  // row_ror 4
-    v += dpp_d<0x128>(v);  // row_ror 8
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    return v;
-}
-
-template <int BAT, int EPT, bool DPP = true>
+template <int BAT, int EPT>
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double *__restrict__ V, int64_t n,
            int64_t ldv, int64_t skip_lo, double *__restrict__ part, int nb, const GmresState *__restrict__ st)
@@ -181,7 +156,7 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
             double a = 0.0;
 #pragma unroll
             for (int e = 0; e < EPT; ++e) a += wv[e] * vv[b][e];
-            const double t = DPP ? wave_sum_dpp(a) : wave_sum(a);
+            const double t = wave_sum(a);
             if (lane == 0 && i0 + b <= j) sh[i0 + b][wv_id] = t;
         }
     }
@@ -525,12 +500,8 @@ static void orth_passes(cdfem_ctx *c, double *w, const double *dinv, double *V, 
     const int nb = (int)((c->nl + (int64_t)kRedThreads * EPT - 1) / ((int64_t)kRedThreads * EPT));
     const int64_t n = c->nl;
     const bool mr = multi_rank(c);
-    if (c->gm_dpp)
-        hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n,
-                           ldv, owned_from(c), part, nb, st);
-    else
-        hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT, false>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V,
-                           n, ldv, owned_from(c), part, nb, st);
+    hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv,
+                       owned_from(c), part, nb, st);
     hipLaunchKernelGGL(k_gm_dots_fin_mb, dim3(m + 1), dim3(kRedThreads), 0, c->stream, part, nb, st, mr ? 1 : 0);
     if (mr) {
         comm_allreduce(c, red_of(st), m + 1);

@@ -237,10 +237,11 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "mr_overlap": 1 (default) — slab (multi-rank) structured CG: the first/last brick layers, the
  *               interface pack and the exchange run on a side stream under the interior layers;
  *               0 = one launch, then the exchange (bitwise the same results).
- * "brick_mult_pb": 0 (default) — the structured Mult (GMRES, cdfem_pa_mult; Kronecker form) writes
+ * "brick_mult_pb": 1 (default) — the structured Mult (GMRES, cdfem_pa_mult; Kronecker form) writes
  *              each brick's whole patch sum to the patch buffer and a second pass forms every row from
- *              its 1-8 entries (predicated loads), instead of owned rows + face partials + face sums.
- *              Same sums in the same order.
+ *              its 1-8 entries (predicated loads); 0 = owned rows + face partials + face sums
+ *              (k_brick_faces).  Same sums in the same order (bitwise); C2 GMRES step 195.0 -> 189.4 us,
+ *              profiles/r04/ab_c2_gmres_dpp_multpb.json.
  * "cg_den_fold": 1024 (default) — N (64..16384): the one-rank brick CG takes MFEM's den step inside
  *              the update kernel, run as N workgroups that each sum the apply's den partials in one
  *              fixed order; the one-block den finalizer is not launched (iterates agree with the
@@ -304,9 +305,6 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *             auto orders (sell_order 8, and the RCM windows sell_order 3 picks on unstructured meshes
  *             without coordinates: 768 rows).
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
- * "gm_dpp": 1 (default) — GMRES orthogonalisation pass 1 sums each projection across a wave with
- *           four DPP row moves and two shuffles (0: six shuffles through the LDS crossbar); the
- *           projections are summed in another fixed order, so iterates agree to rounding.
  * "gm_ept": 0 (default, auto) — entries per thread of the GMRES orthogonalisation passes (4, 5, 6
  *           or 8); auto takes the smallest whose grid is resident in one round (same results).
  * Variants measured slower and removed in round 3 (their records stay under profiles/r02_ab_*):

@@ -131,7 +131,7 @@ def test_brick_mult_patch_buffer_bitwise(gpu_ctx, shape, p, kinds):
             xg, ig = gpu_ctx.solve(B, method="gmres", pc="jacobi", restart=30, rel_tol=0.0, abs_tol=0.0, max_iter=40)
             out[pb] = (gpu_ctx.mult(x), gpu_ctx.mult(x, constrained=True), xg, ig["iterations"])
     finally:
-        gpu_ctx.set_option("brick_mult_pb", 0)
+        gpu_ctx.set_option("brick_mult_pb", 1)
     for k in range(3):
         np.testing.assert_array_equal(out[1][k], out[0][k])
     assert out[1][3] == out[0][3] == 40
