@@ -663,7 +663,8 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
     if (st->done) return;
     double alpha;
     if constexpr (DS) {
-        const double den = sum_partials_all(apart, napart, sh);
+        // (16 loads per thread in flight at once: the apply's 4096 partials in one round trip)
+        const double den = sum_partials_all<16>(apart, napart, sh);
         if (blockIdx.x == 0 && threadIdx.x == 0) cg_den_step(st, den);
         if (den == 0.0) return;
         alpha = st->betanom / den;  // = cg_den_step's nom / den (block 0 may not have stored it yet)

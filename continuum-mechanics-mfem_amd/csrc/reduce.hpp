@@ -47,9 +47,9 @@ __device__ inline void store_partial(double block_total, double *part)
 // written by blocks on all 8 XCDs, so each load is a far round trip, and a load-add loop pays one
 // per partial per thread.  The adds keep the loop's order (out-of-range slots add +0.0, which
 // leaves every sum unchanged), so the result is bitwise the same.
+template <int kB = 8>
 __device__ inline double sum_partials(const double *part, int n, double *sh)
 {
-    constexpr int kB = 8;
     const int bd = blockDim.x;
     double v = 0.0;
     for (int i = threadIdx.x; i < n; i += kB * bd) {
@@ -99,9 +99,10 @@ __device__ inline void cg_update_logic(KrylovState *st, double betanom)
 // every block's copy of sum(part[0..n)), in one fixed order (so all blocks hold the same bits):
 // thread t adds part[t], part[t + bd], ... (loads issued kB at a time), then the block tree;
 // the result is returned in every thread (sh: >= blockDim / 64 + 1 doubles)
+template <int kB = 8>
 __device__ inline double sum_partials_all(const double *part, int n, double *sh)
 {
-    const double v = sum_partials(part, n, sh);
+    const double v = sum_partials<kB>(part, n, sh);
     __syncthreads();
     if (threadIdx.x == 0) sh[0] = v;
     __syncthreads();
