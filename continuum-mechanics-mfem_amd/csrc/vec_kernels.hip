@@ -364,7 +364,8 @@ k_cg_update_fin(const double *__restrict__ part, int n, KrylovState *__restrict_
 {
     __shared__ double sh[1024 / 64];
     if (st->done) return;
-    const double betanom = sum_partials(part, n, sh);
+    // (up to 32 loads per thread in flight: the C3 update leaves 65536 partials; same order as kB 8)
+    const double betanom = sum_partials<32>(part, n, sh);
     if (threadIdx.x == 0) cg_update_logic(st, betanom);
 }
 
