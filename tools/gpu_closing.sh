@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-4 last check after the finalizer load batching: the whole GPU suite, smoke(), the default
+# Closing check of a round: the whole GPU suite, smoke(), the default
 # bench line and the C3 line.
 set -u
-cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r04final3; mkdir -p $O
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/${TAG:-closing}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread \
     -p no:cacheprovider > $O/suite.log 2>&1 || { echo "suite rc=$?"; grep -E "^(FAILED|ERROR)|passed|failed" $O/suite.log | head -20; exit 1; }
 tail -2 $O/suite.log
