@@ -519,13 +519,19 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // W: waves per SIMD the register allocation targets (the Kronecker form fits 2 without spills; three
 // waves, 168 registers with a few spilled values, measured slower twice: profiles/r04/ab_c2_xfold_waves.json,
 // ab_c2_xfold_pb.json; the point-data forms take 1)
-template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false>
+// BF (set_option "cg_beta_fold", one rank, with the den fold): the betanom step of the previous
+// update runs here: every workgroup (one wave) loads the update's nupart <= 1024 partials together
+// with its patch gather, sums them in one fixed order, takes MFEM's decision (workgroup 0 records it,
+// cg_update_logic; kk = updates so far, from the host) and forms beta itself, so the one-block update
+// finalizer is not launched.
+template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false, bool BF = false>
 __global__ void __launch_bounds__(64, W)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
            const Tab<D1, Q1> T, const BrickGeom g, int zlo_shared, double *__restrict__ part,
-           const KrylovState *__restrict__ st, double *__restrict__ x)
+           KrylovState *__restrict__ st, double *__restrict__ x, const double *__restrict__ upart, int nupart,
+           int kk)
 {
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
@@ -535,7 +541,18 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     __shared__ double s_in[S3];
     __shared__ double s_out[S3];
     if (st->done) return;
-    const double beta = st->beta;
+    double beta = st->beta;
+    constexpr int NPL = 16;  // BF: partials per lane (nupart <= 64 NPL)
+    double pv[NPL];
+    if constexpr (BF) {
+        if (kk > 0) {
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) {
+                const int j = (int)threadIdx.x + 64 * i;
+                pv[i] = j < nupart ? upart[j] : 0.0;
+            }
+        }
+    }
     // x-fold (XF, set_option "cg_xfold"): the previous iteration's x += alpha d_old, for the dofs
     // this brick writes d_new for (each dof has exactly one writer brick); the update kernel then
     // leaves x alone.  Bitwise the unfolded update (same fma on the same values).  A template flag:
@@ -581,6 +598,19 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         ev[k] = __builtin_amdgcn_raw_buffer_load_b8(be, in ? gid : kOOB, 0, 0);
         const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
         if constexpr (XF) xv[k] = bload(bxf, writer ? offv[k] : kOOB);
+    }
+    if constexpr (BF) {
+        if (kk > 0) {
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) v += pv[i];
+            const double B = wave_sum(v);
+            // cg_update_logic's decision, taken identically by every workgroup
+            const bool stop = B < 0.0 || B <= st->r0 || kk + 1 > st->max_iter;
+            if (blockIdx.x == 0 && t == 0) cg_update_logic(st, B);
+            if (stop) return;
+            beta = B / st->nom;
+        }
     }
     PatchWalk<S> pw1(t);
 #pragma unroll
@@ -742,6 +772,8 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
 struct BrickRun {
     int bz0, bzs, nlay;
     hipStream_t s;
+    int kk = -1;      // >= 0: the betanom-fold apply (k_brick_cg<..., BF>) after kk updates
+    int nupart = 0;   //   with the update's partial count
 };
 
 template <int D1, int Q1, unsigned K>
@@ -755,15 +787,22 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const dim3 grid((unsigned)(c->nbx * c->nby * run.nlay)), block(64);
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
     const double *qd = c->d_qaff ? c->d_qaff : c->d_qd;
-#define CDFEM_BCG3(AFF_, W_, XF_)                                                                           \
+    const double *upart = c->d_part + c->nblk;  // the den-fold update's partials
+#define CDFEM_BCG4(AFF_, W_, XF_, BF_)                                                                      \
     if (whole)                                                                                               \
-        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_>), grid, block, 0, r, dinv, d_old, d_new, q,       \
-                     c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x);                \
+        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_>), grid, block, 0, r, dinv, d_old, d_new, q,  \
+                     c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x, upart, run.nupart, \
+                     run.kk);                                                                                \
     else                                                                                                     \
-        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_>), grid, block, 0, run.s, r, dinv, d_old, d_new, \
-                           q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x)
+        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_>), grid, block, 0, run.s, r, dinv, d_old,   \
+                           d_new, q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x, upart, \
+                           run.nupart, run.kk)
+#define CDFEM_BCG3(AFF_, W_, XF_) CDFEM_BCG4(AFF_, W_, XF_, false)
 #define CDFEM_BCG(AFF_, W_) CDFEM_BCG3(AFF_, W_, false)
-    if (pa_af(c) == 2) {
+    if (pa_af(c) == 2 && run.kk >= 0) {
+        if (x) { CDFEM_BCG4(2, 2, true, true); }
+        else { CDFEM_BCG4(2, 2, false, true); }
+    } else if (pa_af(c) == 2) {
         if (x) { CDFEM_BCG3(2, 2, true); }
         else { CDFEM_BCG(2, 2); }
     } else if (pa_af(c) == 1) {
@@ -773,6 +812,7 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     }
 #undef CDFEM_BCG
 #undef CDFEM_BCG3
+#undef CDFEM_BCG4
     return hipGetLastError();
 }
 
@@ -798,9 +838,28 @@ static hipError_t brick_cg2_run(cdfem_ctx *c, const double *r, const double *din
 }
 
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                            double *d_new, double *q, double *x)
+                            double *d_new, double *q, double *x, int bfkk)
 {
-    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, 1, c->nbz, c->stream}, x);
+    BrickRun run{0, 1, c->nbz, c->stream};
+    if (bfkk >= 0) {
+        run.kk = bfkk;
+        run.nupart = cg_den_fold_grid(c);
+    }
+    return brick_cg2_run(c, r, dinv, d_old, d_new, q, run, x);
+}
+
+// the den-fold update's workgroups (k_cg_update_faces<..., DS>), one per partial
+int cg_den_fold_grid(const cdfem_ctx *c)
+{
+    const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
+    return (int)std::min<int64_t>(c->cg_den_fold, need);
+}
+
+// the betanom step folded into the next apply (one rank, Kronecker form, den fold on, <= 1024 partials)
+bool cg_beta_fold_ok(const cdfem_ctx *c)
+{
+    return c->cg_beta_fold != 0 && c->cg_den_fold != 0 && !multi_rank(c) && pa_af(c) == 2 &&
+           cg_den_fold_grid(c) <= 1024;
 }
 
 // the first and last brick layers (the shared planes' partial sums) on stream s, the interior
@@ -826,7 +885,7 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     const unsigned grid = (unsigned)(need < 16384 ? need : 16384);
     // den fold (one rank): a grid of cg_den_fold workgroups, partials after the apply's
     const bool ds = !den_step && !multi_rank(c) && c->cg_den_fold != 0;
-    const unsigned ugrid = ds ? (unsigned)std::min<int64_t>(c->cg_den_fold, need) : grid;
+    const unsigned ugrid = ds ? (unsigned)cg_den_fold_grid(c) : grid;
     double *const upart = ds ? c->d_part + c->nblk : c->d_part;
 #define CDFEM_UPD3(S_, XF_, PB_, DS_)                                                                      \
     hipLaunchKernelGGL((k_cg_update_faces<S_, XF_, PB_, DS_>), dim3(ugrid), dim3(kRedThreads), 0, c->stream, x, r, \
@@ -856,6 +915,7 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (multi_rank(c)) return launch_fin_sum(c, (int)grid, 1);
+    if (ds && cg_beta_fold_ok(c)) return hipSuccess;  // the next apply takes the betanom step
     return launch_update_fin(c, (int)ugrid, ds ? c->nblk : 0);
 }
 

@@ -422,6 +422,10 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     // last update's term after the loop when the update logic stopped the solve
     const bool xfold = c->cg_xfold != 0 && pa_af(c) == 2;  // Kronecker kernel only
     double *const dbuf0 = dcur, *const dbuf1 = dprev;  // apply j writes d_j into dbuf[(j - 1) & 1]
+    // betanom fold (cg_beta_fold): apply j > 0 takes the betanom step of update j - 1 (nupd updates so
+    // far); the loop always ends with an apply, so every update's step runs
+    const bool bfold = !mr && cg_beta_fold_ok(c);
+    int nupd = 0;
     int napply = 0;
     auto apply = [&] {
         double *xf = (xfold && napply > 0) ? x : nullptr;
@@ -441,7 +445,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             return;
         }
         prof_mark(c, CDFEM_K_APPLY, true);
-        HIPCHK(launch_brick_cg2(c, r, dinv, dprev, dcur, q, xf));
+        HIPCHK(launch_brick_cg2(c, r, dinv, dprev, dcur, q, xf, bfold ? nupd : -1));
         prof_mark(c, CDFEM_K_APPLY, false);
         prof_mark(c, CDFEM_K_E2L, true);
         if (mr) {
@@ -468,6 +472,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
                 HIPCHK(launch_update_step(c));
             }
             prof_mark(c, CDFEM_K_UPDATE, false);
+            ++nupd;
             std::swap(dprev, dcur);
             apply();
         }
@@ -1677,6 +1682,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "brick_mult_pb") {
             if (value != 0 && value != 1) throw ArgError("brick_mult_pb must be 0 or 1");
             c->brick_mult_pb = value;
+        } else if (k == "cg_beta_fold") {
+            if (value != 0 && value != 1) throw ArgError("cg_beta_fold must be 0 or 1");
+            c->cg_beta_fold = value;
         } else if (k == "cg_den_fold") {
             if (value != 0 && (value < 64 || value > 16384)) throw ArgError("cg_den_fold must be 0 or 64..16384");
             c->cg_den_fold = value;

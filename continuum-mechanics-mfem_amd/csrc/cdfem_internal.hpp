@@ -219,6 +219,7 @@ struct cdfem_ctx {
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int brick_mult_pb = 1;              // set_option "brick_mult_pb": structured Mult through the patch buffer
+    int cg_beta_fold = 0;               // set_option "cg_beta_fold": brick CG betanom step in the next apply
     int cg_den_fold = 1024;             // set_option "cg_den_fold": brick CG den step in the update (N workgroups; 0 off)
     int brick_upd_pb = 1;               // set_option "brick_upd_pb": predicated-load face sums in the brick CG update
     int ho_dfold = 1;                   // set_option "ho_dfold": CG direction folded into the Kronecker tile apply
@@ -358,7 +359,9 @@ hipError_t launch_den_fin(cdfem_ctx *c, int nparts);
 hipError_t launch_update_fin(cdfem_ctx *c, int nparts, int64_t off = 0);
 // brick CG v2 (brick_kernels.hip): d_new = M^{-1} r + beta d_old, q/face partials, den partials
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                            double *d_new, double *q, double *x = nullptr);
+                            double *d_new, double *q, double *x = nullptr, int bfkk = -1);
+int cg_den_fold_grid(const cdfem_ctx *c);
+bool cg_beta_fold_ok(const cdfem_ctx *c);
 // x-fold CG after the loop: x += alpha d_m when the last update's x term is still pending
 // (d_m in dbuf[(m - 1) & 1], m = the final iteration)
 hipError_t launch_cg_xflush(cdfem_ctx *c, double *x, const double *d0, const double *d1);

@@ -137,3 +137,40 @@ def test_brick_mult_patch_buffer_bitwise(gpu_ctx, shape, p, kinds):
     assert out[1][3] == out[0][3] == 40
     yo = A.mult(x)
     assert np.abs(out[1][0] - yo).max() <= 1e-13 * np.abs(yo).max()
+
+
+@pytest.mark.parametrize("shape,p,kinds", [((8, 8, 8), 2, 7), ((9, 6, 7), 2, 5), ((6, 5, 7), 1, 7)])
+def test_beta_fold_matches_update_finalizer(gpu_ctx, shape, p, kinds):
+    """cg_beta_fold: the apply takes the betanom step of the previous update (every workgroup sums the
+    update's partials, workgroup 0 records MFEM's decision) instead of the one-block finalizer: fixed
+    iterate counts 0 / 1 / 2 / 30 within 1e-12 of the finalizer path and 1e-11 of the oracle, and on
+    the SPD operator a converging solve stops on the same iteration with the same flags."""
+    om = O.BoxMesh(3, shape, p)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3,
+                      kinds=(O.DIFFUSION if kinds & 1 else 0) | (O.CONVECTION if kinds & 2 else 0) |
+                      (O.MASS if kinds & 4 else 0))
+    rng = np.random.default_rng(37)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(*shape)
+    gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    cases = [dict(rel_tol=0.0, abs_tol=0.0, max_iter=m, check_every=ce) for m, ce in ((0, 16), (1, 16), (2, 1), (30, 7))]
+    if kinds == 5:
+        cases.append(dict(rel_tol=1e-8, max_iter=2000, check_every=7))
+    try:
+        for kw in cases:
+            res = {}
+            for bf in (1, 0):
+                gpu_ctx.set_option("cg_beta_fold", bf)
+                res[bf] = gpu_ctx.solve(B, method="cg", pc="jacobi", **kw)
+            (x1, i1), (x0, i0) = res[1], res[0]
+            assert i1["iterations"] == i0["iterations"] and i1["converged"] == i0["converged"], kw
+            assert np.linalg.norm(x1 - x0) <= 1e-12 * max(np.linalg.norm(x0), 1e-300), kw
+            if kw["max_iter"] == 30:
+                assert np.linalg.norm(x1 - xo) <= 1e-11 * np.linalg.norm(xo)
+    finally:
+        gpu_ctx.set_option("cg_beta_fold", 0)
