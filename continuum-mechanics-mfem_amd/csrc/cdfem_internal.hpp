@@ -219,7 +219,7 @@ struct cdfem_ctx {
     hipStream_t stream2 = nullptr;      // side stream of the overlapped exchange (created on first use)
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int brick_mult_pb = 1;              // set_option "brick_mult_pb": structured Mult through the patch buffer
-    int cg_beta_fold = 0;               // set_option "cg_beta_fold": brick CG betanom step in the next apply
+    int cg_beta_fold = 1;               // set_option "cg_beta_fold": brick CG betanom step in the next apply
     int cg_den_fold = 1024;             // set_option "cg_den_fold": brick CG den step in the update (N workgroups; 0 off)
     int brick_upd_pb = 1;               // set_option "brick_upd_pb": predicated-load face sums in the brick CG update
     int ho_dfold = 1;                   // set_option "ho_dfold": CG direction folded into the Kronecker tile apply

@@ -242,10 +242,11 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *              its 1-8 entries (predicated loads); 0 = owned rows + face partials + face sums
  *              (k_brick_faces).  Same sums in the same order (bitwise); C2 GMRES step 195.0 -> 189.4 us,
  *              profiles/r04/ab_c2_gmres_dpp_multpb.json.
- * "cg_beta_fold": 0 (default) — 1: with cg_den_fold (one rank, Kronecker form, <= 1024 update
+ * "cg_beta_fold": 1 (default) — with cg_den_fold (one rank, Kronecker form, <= 1024 update
  *              workgroups) the brick CG apply also takes MFEM's betanom step of the previous update:
  *              every workgroup sums the update's partials with its patch gather in flight, and the
- *              one-block update finalizer is not launched (iterates agree to rounding).
+ *              one-block update finalizer is not launched (iterates agree with 0 to rounding; C2:
+ *              60.8 against 62.6 us per iteration, profiles/r04/ab_c2_beta_fold.json).
  * "cg_den_fold": 1024 (default) — N (64..16384): the one-rank brick CG takes MFEM's den step inside
  *              the update kernel, run as N workgroups that each sum the apply's den partials in one
  *              fixed order; the one-block den finalizer is not launched (iterates agree with the

@@ -173,4 +173,4 @@ def test_beta_fold_matches_update_finalizer(gpu_ctx, shape, p, kinds):
             if kw["max_iter"] == 30:
                 assert np.linalg.norm(x1 - xo) <= 1e-11 * np.linalg.norm(xo)
     finally:
-        gpu_ctx.set_option("cg_beta_fold", 0)
+        gpu_ctx.set_option("cg_beta_fold", 1)
