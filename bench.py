@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes of the apply kernel from a rocprofv3 --pmc pass")
+    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "sq_counters.json"),
+                    help="SQ counter record of the apply kernel (tools/sq_record.py): roofline.limiter")
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--path", choices=["brick", "generic"], default=None,
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
@@ -272,6 +274,8 @@ def _cpu_baseline_box(args, O, n, p, kinds, threads, host):
     dinv = 1.0 / Ac.diag()
     t_asm = time.perf_counter() - t0
 
+    host_bw = host_bandwidth(O, Ac, m.nl)
+
     def cg(k):
         return O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=k)[1]["iterations"]
 
@@ -279,16 +283,51 @@ def _cpu_baseline_box(args, O, n, p, kinds, threads, host):
         return O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=k)[1]["iterations"]
     v, rec, its, dt = cpu_samples(cg, m.nl, args.cpu_seconds, 20000, calib_it=10)
     gv, grec, gits, gdt = cpu_samples(gmres, m.nl, 0.5 * args.cpu_seconds, 3000)
+    # SURVEY 8d's like-for-like leg: MFEM's host partial assembly (per-integrator point data, one
+    # sum-factorised element loop per integrator, L->E / E->L) under CGSolver, same matrix-free operator
+    t0 = time.perf_counter()
+    pa = O.PA(m, kappa=0.1, alpha=1.0, s=1.0, c=(1.0, -2.0, 0.5), kinds=ok)
+    t_pa = time.perf_counter() - t0
+
+    def pacg(k):
+        return pa.cg(B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=k)[1]["iterations"]
+    pv, prec, pits, pdt = cpu_samples(pacg, m.nl, 0.5 * args.cpu_seconds, 3000, calib_it=3)
+    del pa
     return {"value": v, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
             "sample": f"oracle FA-CSR Jacobi-CG, {n}^3 hex p={p} ({m.nl} DoFs, nnz={Ac.nnz}): median of "
                       f"{CPU_SAMPLES} samples of {rec['iterations_per_sample']} iterations after a warm-up "
                       f"({its} iterations, {dt:.2f} s timed); assembly+FormLinearSystem {t_asm:.1f} s untimed",
-            **rec,
+            **rec, **host_bw,
             "gmres": {"value": gv, "unit": "DoF-iter/s",
                       "sample": f"oracle FA-CSR GMRES(30)+Jacobi on the same matrix: median of {CPU_SAMPLES} "
                                 f"samples of {grec['iterations_per_sample']} inner steps ({gits} steps, "
                                 f"{gdt:.2f} s timed)", **grec},
+            "pa_cg": {"value": pv, "unit": "DoF-iter/s",
+                      "sample": f"oracle host PA (MFEM's AssemblyLevel::PARTIAL on the CPU: per-integrator point "
+                                f"data, sum-factorised element loops, L->E / E->L) + Jacobi-CG on the same mesh and "
+                                f"operator: median of {CPU_SAMPLES} samples of {prec['iterations_per_sample']} "
+                                f"iterations ({pits} iterations, {pdt:.2f} s timed); PA setup {t_pa:.1f} s untimed",
+                      **prec},
             **host}
+
+
+def host_bandwidth(O, A, nl, reps=10):
+    """What the CPU baseline's pinned cores get from memory: a STREAM triad (orc_stream_triad, 3 x 512 MB,
+    best of 5) and the oracle's CSR SpMV on the baseline's matrix (median of reps, SURVEY 8d bytes
+    12 nnz + 4 (n + 1) + 16 n).  A host-to-host swing of the baseline follows these numbers."""
+    triad = O.stream_triad_gbs(1 << 26, 5)
+    x = np.random.default_rng(5).uniform(-1, 1, nl)
+    A.mult(x)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        A.mult(x)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    sb = 12.0 * A.nnz + 4.0 * (nl + 1) + 16.0 * nl
+    return {"host_stream_gbs": round(triad, 1), "spmv_gbs": round(sb / t / 1e9, 1),
+            "spmv_frac_of_stream": round(sb / t / 1e9 / triad, 3) if triad > 0 else None,
+            "spmv_ms": round(t * 1e3, 2)}
 
 
 def cpu_baseline_c4(args, n, p, mesh=None):
@@ -326,13 +365,14 @@ def _cpu_baseline_kuhn(args, O, n, p, threads, host, mesh=None):
 
     def gmres(k):
         return O.gmres(Ac, B, dinv=dinv, restart=30, rtol=0.0, atol=0.0, max_it=k)[1]["iterations"]
+    host_bw = host_bandwidth(O, Ac, m.nl)
     v, rec, its, dt = cpu_samples(gmres, m.nl, args.cpu_seconds, 3000)
     what = f"Kuhn {n}^3x6 tets" if mesh is None else f"the same Delaunay mesh ({m.ne} tets)"
     return {"value": v, "unit": "DoF-iter/s", "cores": threads, "kind": "port",
             "sample": f"oracle FA-CSR GMRES(30)/Jacobi, {what} P{p} ({m.nl} DoFs, nnz={Ac.nnz}): median "
                       f"of {CPU_SAMPLES} samples of {rec['iterations_per_sample']} iterations after a warm-up "
                       f"({its} iterations, {dt:.2f} s timed); assembly+FormLinearSystem {t_asm:.1f} s untimed",
-            **rec, **host}
+            **rec, **host_bw, **host}
 
 
 def main_c4(args):
@@ -573,13 +613,19 @@ def main():
             bytes_ = ctx.kernel_bytes(cdfem.K_APPLY)
             achieved = bytes_ / per / 1e9
             traffic = None
+            key = f"n{n}_p{p}_k{args.kinds}" + ("_aff" if affine else "")
             if os.path.exists(args.traffic_json):
                 try:
                     tj = json.load(open(args.traffic_json))
-                    key = f"n{n}_p{p}_k{args.kinds}" + ("_aff" if affine else "")
                     traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
+            limiter = None
+            if os.path.exists(args.sq_json):
+                try:
+                    limiter = json.load(open(args.sq_json)).get(key)
+                except Exception:
+                    limiter = None
             hbm_view = {"achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
             if affine:
@@ -609,6 +655,11 @@ def main():
                                else "k_apply3d (fused L->E gather + D/C/M PA apply)"),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
                     "launches": cnt,
+                    # what binds the kernel per its SQ counters (issue / memory / LDS), beside the closer roofline
+                    "limiter": limiter["limiter"] if limiter else None,
+                    "limiter_counters": limiter,
+                    "events_note": "avg_launch_us is event-bracketed: the completion fences add a few percent per "
+                                   "kernel against the uninstrumented ms_per_step",
                     "other_kernels_avg_us": {
                         "e2l": round(e_ms / max(e_cnt, 1) * 1e3, 2),
                         "cg_update": round(u_ms / max(u_cnt, 1) * 1e3, 2),

@@ -409,6 +409,15 @@ k_brick_patch_sum(const double *__restrict__ x, double *__restrict__ y, const do
 // ------------------------------------------------------------------------------------------------
 bool brick_supported(int dim, int p) { return dim == 3 && (p == 1 || p == 2); }
 
+// kOOB = 2^31 is out of range only for buffers below 2^31 bytes: the lattice vectors (8 N_L) and the
+// patch buffer (8 S^3 per brick) must both fit, else an out-of-lattice load would read real data and a
+// dropped store would land inside the buffer
+bool brick_fits(const cdfem_ctx *c)
+{
+    const double S = kBrick * c->p + 1.0, lim = (double)c->brick_limit;
+    return 8.0 * (double)c->nl < lim && 8.0 * (double)c->nblk * S * S * S < lim;
+}
+
 static BrickGeom geom_of(const cdfem_ctx *c)
 {
     return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1};
@@ -429,7 +438,7 @@ static hipError_t brick_launch(cdfem_ctx *c, const double *x, const double *dinv
     constexpr int S = kBrick * (D1 - 1) + 1;
     const BrickGeom g = geom_of(c);
     // patch-buffer Mult (Kronecker form, byte offsets within 32 bits)
-    const bool mpb = c->brick_mult_pb != 0 && pa_af(c) == 2 && 8.0 * c->nblk * (double)(S * S * S) < 4294967296.0;
+    const bool mpb = c->brick_mult_pb != 0 && pa_af(c) == 2 && brick_fits(c);
     if (which & 1) {
         const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
 #define CDFEM_B3(AF_, QD_)                                                                                    \
@@ -605,9 +614,15 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
 #pragma unroll
             for (int i = 0; i < NPL; ++i) v += pv[i];
             const double B = wave_sum(v);
-            // cg_update_logic's decision, taken identically by every workgroup
-            const bool stop = B < 0.0 || B <= st->r0 || kk + 1 > st->max_iter;
-            if (blockIdx.x == 0 && t == 0) cg_update_logic(st, B);
+            // cg_update_logic's decision (cg_stop_kind), taken identically by every workgroup at the
+            // host's update count kk; workgroup 0 records it at the same kk
+            const bool stop = cg_stop_kind(st, B, kk) != kCgGoOn;
+            if (blockIdx.x == 0 && t == 0) {
+#ifdef CDFEM_DEBUG
+                assert(st->iter == kk);
+#endif
+                cg_update_logic_at(st, B, kk);
+            }
             if (stop) return;
             beta = B / st->nom;
         }
@@ -894,8 +909,7 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
 #define CDFEM_UPD2(S_, XF_, PB_)                                                                           \
     if (ds) { CDFEM_UPD3(S_, XF_, PB_, true); } else { CDFEM_UPD3(S_, XF_, PB_, false); }
     // predicated-load face sums: the patch buffer's byte offsets must fit 32 bits
-    const double s3 = std::pow(kBrick * c->p + 1.0, 3.0);
-    const bool pb = c->brick_upd_pb != 0 && 8.0 * (double)c->nblk * s3 < 4294967296.0;
+    const bool pb = c->brick_upd_pb != 0 && brick_fits(c);
 #define CDFEM_UPD(S_)                                                                                       \
     if (xfold) {                                                                                            \
         if (pb) { CDFEM_UPD2(S_, true, true); } else { CDFEM_UPD2(S_, true, false); }                       \

@@ -256,7 +256,7 @@ void build_layout(cdfem_ctx *c, const std::vector<int32_t> &perm)
     HIPCHK(hipStreamSynchronize(c->stream));
 }
 
-bool use_brick(const cdfem_ctx *c) { return c->structured && brick_supported(c->dim, c->p); }
+bool use_brick(const cdfem_ctx *c) { return c->structured && brick_supported(c->dim, c->p) && brick_fits(c); }
 
 const double *ones_vector(cdfem_ctx *c)
 {
@@ -1038,15 +1038,21 @@ int cdfem_check_shared(cdfem_ctx *c, const int64_t *l2g)
         std::vector<double> cs(nn), cr(nn);
         for (int k = 0; k <= nn; ++k) off1[k] = k;
         for (int k = 0; k < nn; ++k) cs[k] = (double)(c->nbr_off[k + 1] - c->nbr_off[k]);
-        double *d_a = nullptr, *d_b = nullptr;
-        HIPCHK(hipMalloc(&d_a, nn * sizeof(double)));
-        HIPCHK(hipMalloc(&d_b, nn * sizeof(double)));
+        // (the counts travel in the send / recv buffers of the shared sums when they hold nn slots,
+        //  else in scratch freed on every exit path, exceptions from the exchange included)
+        struct Scratch {
+            double *p = nullptr;
+            ~Scratch() { dfree(p); }
+        } sa, sb;
+        double *d_a = c->d_sh_send, *d_b = c->d_sh_recv;
+        if (ntot < nn) {
+            sa.p = d_a = dalloc<double>(nn);
+            sb.p = d_b = dalloc<double>(nn);
+        }
         HIPCHK(hipMemcpyAsync(d_a, cs.data(), nn * 8, hipMemcpyHostToDevice, c->stream));
         comm_exchange_nbr_buf(c, off1, d_a, d_b, c->stream);
         HIPCHK(hipMemcpyAsync(cr.data(), d_b, nn * 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        (void)hipFree(d_a);
-        (void)hipFree(d_b);
         for (int k = 0; k < nn; ++k)
             if (cr[k] != cs[k])
                 throw ArgError("shared-dof list with rank " + std::to_string(c->nbr_rank[k]) + " has " +
@@ -1676,6 +1682,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         if (k == "brick_xcd") {
             if (value < 0 || value > 1) throw ArgError("brick_xcd must be 0 or 1");
             c->brick_xcd = value;
+        } else if (k == "brick_byte_limit") {
+            if (value < 1) throw ArgError("brick_byte_limit must be 1..2^31-1");
+            c->brick_limit = value;
         } else if (k == "mr_overlap") {
             if (value < 0 || value > 1) throw ArgError("mr_overlap must be 0 or 1");
             c->mr_overlap = value;

@@ -159,6 +159,11 @@ struct cdfem_ctx {
     int gm_ept_auto = 4;                // the automatic choice for vectors of gm_ept_n entries
     int64_t gm_ept_n = -1;
     int brick_xcd = 1;                  // k_brick_cg brick order: 0 dispatch, 1 XCD-contiguous (default)
+    // the brick kernels address r, M^-1, d, x, ess and the patch buffer through buffer resources with
+    // 32-bit byte offsets and the out-of-range marker kOOB = 2^31, so every such buffer must stay below
+    // 2^31 bytes (8 N_L and 8 S^3 nblk); larger boxes take the generic 64-bit-indexed element kernels.
+    // set_option "brick_byte_limit" lowers the bound (tests force the fallback on small boxes).
+    int64_t brick_limit = (int64_t)1 << 31;
     int ncu = 0;                        // compute units of the device
     int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)
     int zhi_shared = 0;                 // local gz=Lz-1 plane shared with the rank above
@@ -330,6 +335,8 @@ bool apply_supported(int dim, int p);
 // ---- structured brick kernels (brick_kernels.hip) --------------------------------------------
 constexpr int kBrick = 4;               // elements per brick edge (4^3 = 64 = one wavefront)
 bool brick_supported(int dim, int p);
+// every buffer the brick kernels reach through a 32-bit buffer resource is below c->brick_limit bytes
+bool brick_fits(const cdfem_ctx *c);
 // y = A x (constrained: ess in -> 0, y[ess] = x[ess]); fused E->L through LDS + face partials
 hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool constrained, int which);
 

@@ -79,22 +79,32 @@ __device__ inline void cg_den_step(KrylovState *st, double den)
     }
 }
 
-// MFEM CGSolver after betanom = (r, z): convergence test, iteration bound, beta
-__device__ inline void cg_update_logic(KrylovState *st, double betanom)
+// MFEM CGSolver's decision after betanom = (r, z) at iteration i: 0 go on, 1 breakdown (betanom < 0),
+// 2 converged, 3 iteration bound.  The one definition of the stop test: cg_update_logic records it,
+// and the betanom-fold apply (k_brick_cg<..., BF>) takes it in every workgroup with i from the host.
+enum : int { kCgGoOn = 0, kCgBreakdown = 1, kCgConverged = 2, kCgMaxIter = 3 };
+__device__ inline int cg_stop_kind(const KrylovState *st, double betanom, int i)
+{
+    if (betanom < 0.0) return kCgBreakdown;
+    if (betanom <= st->r0) return kCgConverged;
+    if (i + 1 > st->max_iter) return kCgMaxIter;
+    return kCgGoOn;
+}
+
+// MFEM CGSolver after betanom = (r, z): convergence test, iteration bound, beta (at iteration i)
+__device__ inline void cg_update_logic_at(KrylovState *st, double betanom, int i)
 {
     st->betanom = betanom;
-    const int i = st->iter;
-    if (betanom < 0.0) {
-        st->done = 1; st->converged = 0; st->final_iter = i; st->xflush = 1;
-    } else if (betanom <= st->r0) {
-        st->done = 1; st->converged = 1; st->final_iter = i; st->xflush = 1;
-    } else if (i + 1 > st->max_iter) {
-        st->done = 1; st->converged = 0; st->final_iter = st->max_iter; st->xflush = 1;
-    } else {
+    switch (cg_stop_kind(st, betanom, i)) {
+    case kCgBreakdown: st->done = 1; st->converged = 0; st->final_iter = i; st->xflush = 1; break;
+    case kCgConverged: st->done = 1; st->converged = 1; st->final_iter = i; st->xflush = 1; break;
+    case kCgMaxIter: st->done = 1; st->converged = 0; st->final_iter = st->max_iter; st->xflush = 1; break;
+    default:
         st->beta = betanom / st->nom;
         st->iter = i + 1;
     }
 }
+__device__ inline void cg_update_logic(KrylovState *st, double betanom) { cg_update_logic_at(st, betanom, st->iter); }
 
 // every block's copy of sum(part[0..n)), in one fixed order (so all blocks hold the same bits):
 // thread t adds part[t], part[t + bd], ... (loads issued kB at a time), then the block tree;

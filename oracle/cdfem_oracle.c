@@ -47,6 +47,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -621,12 +622,26 @@ static double dot(int64_t n, const double *a, const double *b)
  * MFEM CGSolver::Mult semantics (iterative_mode = false), optional Jacobi preconditioner
  * z = dinv .* r (OperatorJacobiSmoother / HypreDiagScale).  Convergence when
  * (r, z) <= max(nom0 * rel_tol^2, abs_tol^2).  Pinned by use: mesh_recession_handler.cpp:270-276.
- * Returns 1 if converged; *iters = final_iter, *final_norm = sqrt(betanom).
+ * An indefinite preconditioner stops the solve unconverged, as CGSolver does [MFEM-ext]: nom0 < 0
+ * at iteration 0, betanom < 0 at iteration i (tested before the convergence test).
+ * Returns 1 if converged; *iters = final_iter, *final_norm = sqrt(|betanom|).
  */
+typedef void (*orc_op_fn)(const void *op, const double *x, double *y);
+static void csr_op(const void *op, const double *x, double *y) { orc_csr_spmv((const orc_csr *)op, x, y); }
+
+static int cg_core(orc_op_fn apply, const void *op, int64_t n, const double *dinv, const double *b, double *x,
+                   double rel_tol, double abs_tol, int max_iter, int *iters, double *final_norm);
+
 ORC_API int orc_cg(const orc_csr *A, const double *dinv, const double *b, double *x, double rel_tol,
                    double abs_tol, int max_iter, int *iters, double *final_norm)
 {
-    const int64_t n = A->n;
+    return cg_core(csr_op, A, A->n, dinv, b, x, rel_tol, abs_tol, max_iter, iters, final_norm);
+}
+
+/* the CGSolver loop on any operator y = op(x) */
+static int cg_core(orc_op_fn apply, const void *op, int64_t n, const double *dinv, const double *b, double *x,
+                   double rel_tol, double abs_tol, int max_iter, int *iters, double *final_norm)
+{
     double *r = (double *)malloc(sizeof(double) * n), *d = (double *)malloc(sizeof(double) * n);
     double *z = (double *)malloc(sizeof(double) * n);
     memcpy(r, b, sizeof(double) * n);
@@ -638,8 +653,9 @@ ORC_API int orc_cg(const orc_csr *A, const double *dinv, const double *b, double
     int converged = 0;
     double betanom = nom;
     *iters = 0;
+    if (nom < 0.0) { *final_norm = sqrt(-nom); free(r); free(d); free(z); return 0; }
     if (nom <= r0) { *final_norm = sqrt(nom); free(r); free(d); free(z); return 1; }
-    orc_csr_spmv(A, d, z);
+    apply(op, d, z);
     double den = dot(n, z, d);
     if (den == 0.0) { *final_norm = sqrt(nom); free(r); free(d); free(z); return 0; }
     int final_iter = max_iter;
@@ -652,13 +668,14 @@ ORC_API int orc_cg(const orc_csr *A, const double *dinv, const double *b, double
             for (int64_t k = 0; k < n; k++) z[k] = dinv[k] * r[k];
             betanom = dot(n, r, z);
         } else betanom = dot(n, r, r);
+        if (betanom < 0.0) { final_iter = i; break; }
         if (betanom <= r0) { converged = 1; final_iter = i; break; }
         if (++i > max_iter) break;
         double beta = betanom / nom;
         const double *src = dinv ? z : r;
         #pragma omp parallel for schedule(static)
         for (int64_t k = 0; k < n; k++) d[k] = src[k] + beta * d[k];
-        orc_csr_spmv(A, d, z);
+        apply(op, d, z);
         den = dot(n, d, z);
         if (den == 0.0) { final_iter = i; break; }
         nom = betanom;
@@ -1594,4 +1611,293 @@ ORC_API void orc_dof_coords_simplex(int dim, int p, int ne, const double *verts,
             for (int k = 0; k < dim; k++) xyz[(size_t)dofmap[(size_t)e * nd + l] * dim + k] = X[k];
         }
     }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* CPU partial assembly as MFEM runs it on the host: the like-for-like CPU baseline of the PA    */
+/* hot path (SURVEY.md 8d "CPU PA + CG"), timed by bench.py's cpu_baseline only.                 */
+/* ------------------------------------------------------------------------------------------ */
+
+/*
+ * [MFEM-ext] ParBilinearForm with AssemblyLevel::PARTIAL on a hex mesh, device "cpu":
+ *   - each integrator keeps its own point data (DiffusionIntegrator::AssemblePA: the 6 symmetric
+ *     components of W adj(J) K adj(J)^T / detJ; ConvectionIntegrator: W alpha adj(J) c, 3 per point;
+ *     MassIntegrator: W s detJ), layout [e][comp][q] as MFEM's Reshape(Q1D^3, comps, NE);
+ *   - Mult = ElementRestriction::Mult (L -> E gather), then every integrator's AddMultPA over the
+ *     E-vector with sum factorisation (PADiffusionApply3D, PAConvectionApply3D, PAMassApply3D: one
+ *     element loop each), then ElementRestriction::MultTranspose (E -> L through per-dof offsets);
+ *   - the ConstrainedOperator of FormLinearSystem: essential inputs zeroed, y_ess = x_ess;
+ *   - CGSolver (cg_core) with OperatorJacobiSmoother (the caller passes 1 / diag, ess -> 1).
+ * Stages written after MFEM's generic (non-shared-memory) 3D kernels: x, y, z contractions to the
+ * points, the point operator, and the transposed contractions, all in per-element scratch.
+ * Call sites: linear_convection_diffusion_2D.cpp:335-374 (forms, solver); the PA level is the
+ * north star's (BASELINE.json); mesh_recession_handler.cpp:270-276 (CGSolver semantics).
+ */
+typedef struct {
+    int p, d1, nq, ne, nd, q3;
+    int64_t nl;
+    int use_diff, use_conv, use_mass;
+    double B[64], G[64];            /* [q][d] */
+    double *qd_d, *qd_c, *qd_m;     /* [e][6][q3], [e][3][q3], [e][q3] */
+    int *dofmap;                    /* [e][nd] (copy) */
+    int64_t *off;                   /* E->L: offsets [nl + 1] into idx (element-major E-vector index) */
+    int64_t *idx;
+    double *xe, *ye;                /* E-vectors [e][nd] */
+    const int *ess;                 /* ess marker for the constrained operator (borrowed during a solve) */
+    double *xz;                     /* scratch: x with ess zeroed */
+} orc_pa;
+
+ORC_API orc_pa *orc_pa_setup(int p, int ne, const double *verts, const int *dofmap, int64_t nl, double kappa,
+                             double alpha, double s, const double *c, int kinds)
+{
+    const int d1 = p + 1, nq = orc_rule_npts(0, 3, p), nd = d1 * d1 * d1, q3 = nq * nq * nq;
+    if (d1 > 8 || nq > 8) return NULL;
+    orc_pa *pa = (orc_pa *)calloc(1, sizeof(orc_pa));
+    pa->p = p; pa->d1 = d1; pa->nq = nq; pa->ne = ne; pa->nd = nd; pa->q3 = q3; pa->nl = nl;
+    pa->use_diff = (kinds & 1) != 0; pa->use_conv = (kinds & 2) != 0; pa->use_mass = (kinds & 4) != 0;
+    double pts[8], wts[8];
+    tables(p, nq, pa->B, pa->G, pts, wts);
+    orc_coef cf = {kappa, alpha, s, {c ? c[0] : 0, c ? c[1] : 0, c ? c[2] : 0},
+                   pa->use_diff, pa->use_conv, pa->use_mass, NULL, NULL, NULL, NULL};
+    if (pa->use_diff) pa->qd_d = (double *)malloc(sizeof(double) * (size_t)ne * 6 * q3);
+    if (pa->use_conv) pa->qd_c = (double *)malloc(sizeof(double) * (size_t)ne * 3 * q3);
+    if (pa->use_mass) pa->qd_m = (double *)malloc(sizeof(double) * (size_t)ne * q3);
+    #pragma omp parallel for schedule(static)
+    for (int e = 0; e < ne; e++) {
+        const double *V = verts + (size_t)e * 8 * 3;
+        for (int qz = 0; qz < nq; qz++)
+        for (int qy = 0; qy < nq; qy++)
+        for (int qx = 0; qx < nq; qx++) {
+            const int q = qx + nq * (qy + nq * qz);
+            double xi[3] = {pts[qx], pts[qy], pts[qz]}, xx[3], J[3][3], A[3][3];
+            q1_map(3, V, xi, xx, J);
+            const double detJ = adjugate(3, J, A);
+            double D[3][3] = {{0}}, Cv[3] = {0}, M = 0.0;
+            point_coef(3, &cf, q, wts[qx] * wts[qy] * wts[qz], detJ, A, D, Cv, &M);
+            if (pa->use_diff) {
+                double *o = pa->qd_d + (size_t)e * 6 * q3 + q;
+                o[0 * q3] = D[0][0]; o[1 * q3] = D[0][1]; o[2 * q3] = D[0][2];
+                o[3 * q3] = D[1][1]; o[4 * q3] = D[1][2]; o[5 * q3] = D[2][2];
+            }
+            if (pa->use_conv)
+                for (int k = 0; k < 3; k++) pa->qd_c[(size_t)e * 3 * q3 + k * q3 + q] = Cv[k];
+            if (pa->use_mass) pa->qd_m[(size_t)e * q3 + q] = M;
+        }
+    }
+    pa->dofmap = (int *)malloc(sizeof(int) * (size_t)ne * nd);
+    memcpy(pa->dofmap, dofmap, sizeof(int) * (size_t)ne * nd);
+    /* ElementRestriction's transpose: for every L-dof its E-vector entries in ascending order */
+    pa->off = (int64_t *)calloc((size_t)nl + 1, sizeof(int64_t));
+    pa->idx = (int64_t *)malloc(sizeof(int64_t) * (size_t)ne * nd);
+    for (int64_t k = 0; k < (int64_t)ne * nd; k++) pa->off[dofmap[k] + 1]++;
+    for (int64_t i = 0; i < nl; i++) pa->off[i + 1] += pa->off[i];
+    int64_t *fill = (int64_t *)malloc(sizeof(int64_t) * (size_t)nl);
+    memcpy(fill, pa->off, sizeof(int64_t) * (size_t)nl);
+    for (int64_t k = 0; k < (int64_t)ne * nd; k++) pa->idx[fill[dofmap[k]]++] = k;
+    free(fill);
+    pa->xe = (double *)malloc(sizeof(double) * (size_t)ne * nd);
+    pa->ye = (double *)malloc(sizeof(double) * (size_t)ne * nd);
+    pa->xz = (double *)malloc(sizeof(double) * (size_t)nl);
+    return pa;
+}
+
+ORC_API void orc_pa_free(orc_pa *pa)
+{
+    if (!pa) return;
+    free(pa->qd_d); free(pa->qd_c); free(pa->qd_m); free(pa->dofmap); free(pa->off); free(pa->idx);
+    free(pa->xe); free(pa->ye); free(pa->xz); free(pa);
+}
+
+/* value (and reference gradient) of one element's E-vector at its Q1^3 points: u[q], g[q][3] */
+static void pa_interp(const orc_pa *pa, const double *X, double *u, double (*g)[3], int grad)
+{
+    const int D = pa->d1, Q = pa->nq;
+    const double *B = pa->B, *G = pa->G;
+    double tx[8][8][8][2];  /* [dz][dy][qx]: B x, G x along x */
+    for (int dz = 0; dz < D; dz++)
+        for (int dy = 0; dy < D; dy++)
+            for (int qx = 0; qx < Q; qx++) {
+                double a = 0.0, b = 0.0;
+                for (int dx = 0; dx < D; dx++) {
+                    const double v = X[dx + D * (dy + D * dz)];
+                    a += B[qx * D + dx] * v;
+                    b += G[qx * D + dx] * v;
+                }
+                tx[dz][dy][qx][0] = a; tx[dz][dy][qx][1] = b;
+            }
+    double ty[8][8][8][3];  /* [dz][qy][qx]: (Bx By), (Gx By), (Bx Gy) */
+    for (int dz = 0; dz < D; dz++)
+        for (int qy = 0; qy < Q; qy++)
+            for (int qx = 0; qx < Q; qx++) {
+                double a = 0.0, b = 0.0, c = 0.0;
+                for (int dy = 0; dy < D; dy++) {
+                    a += B[qy * D + dy] * tx[dz][dy][qx][0];
+                    b += B[qy * D + dy] * tx[dz][dy][qx][1];
+                    c += G[qy * D + dy] * tx[dz][dy][qx][0];
+                }
+                ty[dz][qy][qx][0] = a; ty[dz][qy][qx][1] = b; ty[dz][qy][qx][2] = c;
+            }
+    for (int qz = 0; qz < Q; qz++)
+        for (int qy = 0; qy < Q; qy++)
+            for (int qx = 0; qx < Q; qx++) {
+                double a = 0.0, gx = 0.0, gy = 0.0, gz = 0.0;
+                for (int dz = 0; dz < D; dz++) {
+                    const double bz = B[qz * D + dz], dzv = G[qz * D + dz];
+                    a += bz * ty[dz][qy][qx][0];
+                    gx += bz * ty[dz][qy][qx][1];
+                    gy += bz * ty[dz][qy][qx][2];
+                    gz += dzv * ty[dz][qy][qx][0];
+                }
+                const int q = qx + Q * (qy + Q * qz);
+                u[q] = a;
+                if (grad) { g[q][0] = gx; g[q][1] = gy; g[q][2] = gz; }
+            }
+}
+
+/* Y += sum_q (phi v[q] + grad phi . w[q]) over one element (w NULL: values only) */
+static void pa_test(const orc_pa *pa, const double *v, double (*w)[3], double *Y)
+{
+    const int D = pa->d1, Q = pa->nq;
+    const double *B = pa->B, *G = pa->G;
+    double sz[8][8][8][3];  /* [dz][qy][qx]: Bz (v, wx, wy) + Gz wz */
+    for (int dz = 0; dz < D; dz++)
+        for (int qy = 0; qy < Q; qy++)
+            for (int qx = 0; qx < Q; qx++) {
+                double a = 0.0, b = 0.0, c = 0.0;
+                for (int qz = 0; qz < Q; qz++) {
+                    const int q = qx + Q * (qy + Q * qz);
+                    const double bz = B[qz * D + dz], gz = G[qz * D + dz];
+                    a += bz * v[q] + (w ? gz * w[q][2] : 0.0);
+                    if (w) { b += bz * w[q][0]; c += bz * w[q][1]; }
+                }
+                sz[dz][qy][qx][0] = a; sz[dz][qy][qx][1] = b; sz[dz][qy][qx][2] = c;
+            }
+    double sy[8][8][8][2];  /* [dz][dy][qx]: By (a, b) + Gy c, i.e. the x-test value and x-test gradient parts */
+    for (int dz = 0; dz < D; dz++)
+        for (int dy = 0; dy < D; dy++)
+            for (int qx = 0; qx < Q; qx++) {
+                double a = 0.0, b = 0.0;
+                for (int qy = 0; qy < Q; qy++) {
+                    const double by = B[qy * D + dy], gy = G[qy * D + dy];
+                    a += by * sz[dz][qy][qx][0] + (w ? gy * sz[dz][qy][qx][2] : 0.0);
+                    if (w) b += by * sz[dz][qy][qx][1];
+                }
+                sy[dz][dy][qx][0] = a; sy[dz][dy][qx][1] = b;
+            }
+    for (int dz = 0; dz < D; dz++)
+        for (int dy = 0; dy < D; dy++)
+            for (int dx = 0; dx < D; dx++) {
+                double a = 0.0;
+                for (int qx = 0; qx < Q; qx++)
+                    a += B[qx * D + dx] * sy[dz][dy][qx][0] + (w ? G[qx * D + dx] * sy[dz][dy][qx][1] : 0.0);
+                Y[dx + D * (dy + D * dz)] += a;
+            }
+}
+
+/* y = A x on L-vectors (constrained: inputs on ess zeroed, y_ess = x_ess) */
+static void pa_apply(const orc_pa *pa, const double *x, double *y, int constrained)
+{
+    const int ne = pa->ne, nd = pa->nd, q3 = pa->q3;
+    const double *xs = x;
+    if (constrained) {
+        #pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < pa->nl; i++) pa->xz[i] = pa->ess[i] ? 0.0 : x[i];
+        xs = pa->xz;
+    }
+    /* ElementRestriction::Mult */
+    #pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < (int64_t)ne * nd; k++) { pa->xe[k] = xs[pa->dofmap[k]]; pa->ye[k] = 0.0; }
+    /* AddMultPA of each integrator: one element loop each */
+    if (pa->use_diff) {
+        #pragma omp parallel for schedule(static)
+        for (int e = 0; e < ne; e++) {
+            double u[512], g[512][3], v[512];
+            pa_interp(pa, pa->xe + (size_t)e * nd, u, g, 1);
+            const double *Dq = pa->qd_d + (size_t)e * 6 * q3;
+            for (int q = 0; q < q3; q++) {
+                const double a = g[q][0], b = g[q][1], c = g[q][2];
+                const double d00 = Dq[q], d01 = Dq[q3 + q], d02 = Dq[2 * q3 + q], d11 = Dq[3 * q3 + q],
+                             d12 = Dq[4 * q3 + q], d22 = Dq[5 * q3 + q];
+                g[q][0] = d00 * a + d01 * b + d02 * c;
+                g[q][1] = d01 * a + d11 * b + d12 * c;
+                g[q][2] = d02 * a + d12 * b + d22 * c;
+                v[q] = 0.0;
+            }
+            pa_test(pa, v, g, pa->ye + (size_t)e * nd);
+        }
+    }
+    if (pa->use_conv) {
+        #pragma omp parallel for schedule(static)
+        for (int e = 0; e < ne; e++) {
+            double u[512], g[512][3], v[512];
+            pa_interp(pa, pa->xe + (size_t)e * nd, u, g, 1);
+            const double *Cq = pa->qd_c + (size_t)e * 3 * q3;
+            for (int q = 0; q < q3; q++) v[q] = Cq[q] * g[q][0] + Cq[q3 + q] * g[q][1] + Cq[2 * q3 + q] * g[q][2];
+            pa_test(pa, v, NULL, pa->ye + (size_t)e * nd);
+        }
+    }
+    if (pa->use_mass) {
+        #pragma omp parallel for schedule(static)
+        for (int e = 0; e < ne; e++) {
+            double u[512], v[512];
+            pa_interp(pa, pa->xe + (size_t)e * nd, u, NULL, 0);
+            const double *Mq = pa->qd_m + (size_t)e * q3;
+            for (int q = 0; q < q3; q++) v[q] = Mq[q] * u[q];
+            pa_test(pa, v, NULL, pa->ye + (size_t)e * nd);
+        }
+    }
+    /* ElementRestriction::MultTranspose (+ the constraint) */
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < pa->nl; i++) {
+        double acc = 0.0;
+        for (int64_t k = pa->off[i]; k < pa->off[i + 1]; k++) acc += pa->ye[pa->idx[k]];
+        y[i] = (constrained && pa->ess[i]) ? x[i] : acc;
+    }
+}
+
+ORC_API void orc_pa_mult(orc_pa *pa, const int *ess_marker, const double *x, double *y)
+{
+    pa->ess = ess_marker;
+    pa_apply(pa, x, y, ess_marker != NULL);
+    pa->ess = NULL;
+}
+
+static void pa_con_op(const void *op, const double *x, double *y) { pa_apply((const orc_pa *)op, x, y, 1); }
+
+/* CGSolver on the ConstrainedOperator of the PA form (dinv: Jacobi, ess entries 1) */
+ORC_API int orc_pa_cg(orc_pa *pa, const int *ess_marker, const double *dinv, const double *b, double *x,
+                      double rel_tol, double abs_tol, int max_iter, int *iters, double *final_norm)
+{
+    pa->ess = ess_marker;
+    const int r = cg_core(pa_con_op, pa, pa->nl, dinv, b, x, rel_tol, abs_tol, max_iter, iters, final_norm);
+    pa->ess = NULL;
+    return r;
+}
+
+/* Host memory bandwidth probe (STREAM triad a = b + s c, 24 B per index counted, best of reps) on the
+ * current OpenMP threads (bench.py pins them to the CPU baseline's cores first): explains the CPU
+ * baseline's spread across hosts by the bandwidth its cores actually get. */
+ORC_API double orc_stream_triad(int64_t n, int reps)
+{
+    double *a = (double *)malloc(sizeof(double) * (size_t)n), *b = (double *)malloc(sizeof(double) * (size_t)n),
+           *c = (double *)malloc(sizeof(double) * (size_t)n);
+    if (!a || !b || !c) { free(a); free(b); free(c); return -1.0; }
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) { a[i] = 0.0; b[i] = 1.0; c[i] = 2.0; }
+    double best = 0.0;
+    for (int r = 0; r < reps; r++) {
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        const double s = 3.0 + r;
+        #pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < n; i++) a[i] = b[i] + s * c[i];
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        const double dt = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+        const double gbs = 24.0 * (double)n / dt / 1e9;
+        if (gbs > best) best = gbs;
+    }
+    volatile double sink = a[n / 2];
+    (void)sink;
+    free(a); free(b); free(c);
+    return best;
 }

@@ -70,6 +70,14 @@ def lib():
         L.orc_ilu_solve.argtypes = [C.c_void_p, dp, dp]
         L.orc_gmres_ilu.argtypes = [C.c_void_p, C.c_void_p, dp, dp, C.c_int, C.c_double, C.c_double, C.c_int,
                                     ip, dp]
+        L.orc_pa_setup.restype = C.c_void_p
+        L.orc_pa_setup.argtypes = [C.c_int, C.c_int, dp, ip, C.c_int64, C.c_double, C.c_double, C.c_double, dp,
+                                   C.c_int]
+        L.orc_pa_free.argtypes = [C.c_void_p]
+        L.orc_pa_mult.argtypes = [C.c_void_p, ip, dp, dp]
+        L.orc_pa_cg.argtypes = [C.c_void_p, ip, dp, dp, dp, C.c_double, C.c_double, C.c_int, ip, dp]
+        L.orc_stream_triad.argtypes = [C.c_int64, C.c_int]
+        L.orc_stream_triad.restype = C.c_double
         L.orc_mms_u.argtypes = [dp, dp]
         L.orc_mms_u.restype = C.c_double
         L.orc_mms_f.argtypes = [dp, dp]
@@ -330,6 +338,46 @@ def ebe_mult(mesh: BoxMesh, x, kappa=1.0, alpha=1.0, s=1.0, c=None, kinds=DIFFUS
     lib().orc_ebe_mult(mesh.dim, mesh.p, mesh.ne, _d(mesh.verts), _i(mesh.dofmap), mesh.nl, kappa,
                        alpha, s, _d(cc), kinds, _d(x), _d(y))
     return y
+
+
+class PA:
+    """MFEM's host partial assembly of the 3D hex operator (orc_pa_*: per-integrator point data, L->E,
+    one sum-factorised element loop per integrator, E->L): the CPU PA + CG baseline of bench.py."""
+
+    def __init__(self, mesh: BoxMesh, kappa=1.0, alpha=1.0, s=1.0, c=None, kinds=DIFFUSION | CONVECTION | MASS):
+        if mesh.dim != 3:
+            raise ValueError("PA restatement: 3D hexes")
+        self.nl, self.bdr = mesh.nl, np.ascontiguousarray(mesh.bdr, dtype=np.int32)
+        self.h = lib().orc_pa_setup(mesh.p, mesh.ne, _d(mesh.verts), _i(mesh.dofmap), mesh.nl, kappa, alpha, s,
+                                    _d(_conv(c, 3)), kinds)
+        if not self.h:
+            raise RuntimeError("orc_pa_setup: unsupported order")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_pa_free(self.h)
+            self.h = None
+
+    def mult(self, x, constrained=False):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.empty(self.nl)
+        lib().orc_pa_mult(self.h, _i(self.bdr) if constrained else None, _d(x), _d(y))
+        return y
+
+    def cg(self, b, dinv=None, rel_tol=1e-12, abs_tol=0.0, max_iter=500):
+        """CGSolver on the constrained operator (b: FormLinearSystem's B, dinv: 1 / diag with ess 1)."""
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        x = np.zeros(self.nl)
+        it, fn = C.c_int(0), C.c_double(0.0)
+        di = None if dinv is None else _d(np.ascontiguousarray(dinv, dtype=np.float64))
+        conv = lib().orc_pa_cg(self.h, _i(self.bdr), di, _d(b), _d(x), rel_tol, abs_tol, max_iter,
+                               C.byref(it), C.byref(fn))
+        return x, {"converged": bool(conv), "iterations": it.value, "final_norm": fn.value}
+
+
+def stream_triad_gbs(n=1 << 26, reps=5):
+    """Host STREAM triad GB/s (24 B per index) on the current OpenMP threads."""
+    return lib().orc_stream_triad(n, reps)
 
 
 def form_linear_system(A: CSR, ess_marker, X, b):

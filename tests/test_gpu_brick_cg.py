@@ -174,3 +174,93 @@ def test_beta_fold_matches_update_finalizer(gpu_ctx, shape, p, kinds):
                 assert np.linalg.norm(x1 - xo) <= 1e-11 * np.linalg.norm(xo)
     finally:
         gpu_ctx.set_option("cg_beta_fold", 1)
+
+
+def test_beta_fold_breakdown_paths(gpu_ctx):
+    """The two early exits the betanom fold must take exactly as the finalizer path does:
+    (a) an indefinite Jacobi preconditioner (kappa K + s M with s = -124 on a 6 x 5 x 7 p = 2 box: 210
+    negative diagonal entries), where MFEM's CGSolver stops on betanom < 0 at iteration 4 — the fold's
+    workgroups take that decision from the shared cg_stop_kind at the host's update count; (b) den == 0
+    at the first den step (a zero operator away from the boundary, zero boundary values, pc none), where
+    the den-fold update returns before any update.  Both: same iteration count and flags with
+    cg_beta_fold 0 and 1 and the oracle, x within 1e-12 of each other and 1e-11 of the oracle."""
+    shape, p = (6, 5, 7), 2
+    om = O.BoxMesh(3, shape, p)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(*shape)
+    rng = np.random.default_rng(3)
+    u, b = np.zeros(om.nl), rng.uniform(-1, 1, om.nl)
+    cases = []
+    # (a) betanom < 0 after four updates
+    A = O.fa_assemble(om, kappa=0.1, s=-124.0, kinds=O.DIFFUSION | O.MASS)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, io = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=1e-12, max_iter=200)
+    assert not io["converged"] and io["iterations"] == 4
+    cases.append((dict(kinds=5, kappa=0.1, mass=-124.0), "jacobi", xo, io))
+    # (b) den == 0 at the first den step: convection with c = 0 is the zero operator, the constrained
+    # operator is the identity on the (zero) boundary values only
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, c=(0.0, 0.0, 0.0), kinds=O.CONVECTION)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, io = O.cg(Ac, Bo, dinv=None, rel_tol=1e-12, max_iter=200)
+    assert not io["converged"] and io["iterations"] == 0
+    cases.append((dict(kinds=2, alpha=1.0, conv=(0.0, 0.0, 0.0)), "none", xo, io))
+    try:
+        for setup, pc, xo, io in cases:
+            gpu_ctx.pa_setup(**setup)
+            _, B = gpu_ctx.form_linear_system(u, b)
+            res = {}
+            for bf in (1, 0):
+                gpu_ctx.set_option("cg_beta_fold", bf)
+                res[bf] = gpu_ctx.solve(B, method="cg", pc=pc, rel_tol=1e-12, max_iter=200, check_every=3)
+            (x1, i1), (x0, i0) = res[1], res[0]
+            assert i1["iterations"] == i0["iterations"] == io["iterations"], setup
+            assert not i1["converged"] and not i0["converged"], setup
+            scale = max(np.linalg.norm(xo), 1e-300)
+            assert np.linalg.norm(x1 - x0) <= 1e-12 * scale, setup
+            assert np.linalg.norm(x1 - xo) <= 1e-11 * scale, setup
+    finally:
+        gpu_ctx.set_option("cg_beta_fold", 1)
+
+
+def test_brick_byte_limit_falls_back_to_generic(gpu_ctx):
+    """The brick kernels reach their vectors and patch buffer through buffer resources whose 32-bit
+    offsets use kOOB = 2^31 as the out-of-range marker, so the brick path is taken only when every such
+    buffer is below 2^31 bytes; a larger box runs the generic element kernels.  Forced
+    here on a small box with brick_byte_limit: the generic path takes over (its CG launches the
+    direction kernel, which the brick CG does not have) and gives the brick path's Mult (1e-13),
+    diagonal and CG iterates (1e-11 of the oracle)."""
+    shape, p = (8, 8, 8), 2
+    om = O.BoxMesh(3, shape, p)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3)
+    rng = np.random.default_rng(71)
+    x, b = rng.uniform(-1, 1, om.nl), rng.uniform(-1, 1, om.nl)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(*shape)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    out = {}
+    try:
+        for lim in (None, 4096):
+            if lim:
+                gpu_ctx.set_option("brick_byte_limit", lim)
+            gpu_ctx.set_option("profile_mask", -1)
+            gpu_ctx.profile(True)
+            xg, ig = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30)
+            _, ndir = gpu_ctx.profile_read(cdfem.K_DIRECTION)
+            gpu_ctx.profile(False)
+            out[lim] = dict(y=gpu_ctx.mult(x), yc=gpu_ctx.mult(x, constrained=True), x=xg, it=ig["iterations"],
+                            ndir=ndir)
+    finally:
+        gpu_ctx.set_option("brick_byte_limit", 2**31 - 1)
+        gpu_ctx.profile(False)
+    assert out[None]["ndir"] == 0 and out[4096]["ndir"] > 0
+    yo = A.mult(x)
+    for lim in (None, 4096):
+        assert np.abs(out[lim]["y"] - yo).max() <= 1e-13 * np.abs(yo).max()
+        assert out[lim]["it"] == 30
+        assert np.linalg.norm(out[lim]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
+    assert np.abs(out[4096]["yc"] - out[None]["yc"]).max() <= 1e-13 * np.abs(out[None]["yc"]).max()
+    with pytest.raises(cdfem.CdfemError):
+        gpu_ctx.set_option("brick_byte_limit", 0)

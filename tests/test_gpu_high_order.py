@@ -340,7 +340,9 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
     u[om.ess] = rng.uniform(-1, 1, len(om.ess))
     b = rng.uniform(-1, 1, om.nl)
     Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
-    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=50)
+    # pure convection (kinds 2): the Jacobi diagonal is zero off the boundary, so there is no oracle
+    # solve to compare with (the GPU iterates are only checked for the iteration count)
+    xo = None if kinds == 2 else O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=50)[0]
     out = {}
     try:
         for aff in (2, 1, 0):
@@ -363,7 +365,7 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
         for k in ("y", "yc", "dg"):
             assert np.abs(out[aff][k] - out[0][k]).max() <= 1e-13 * np.abs(out[0][k]).max()
         assert out[aff]["it"] == 50
-        if kinds != 2:  # pure convection: Jacobi-CG breaks down (the oracle's iterates too)
+        if xo is not None:
             assert np.linalg.norm(out[aff]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
 
 

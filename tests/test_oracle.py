@@ -167,3 +167,49 @@ def test_oracle_regression_vectors():
         np.testing.assert_allclose(A.diag(), g[f"{name}_diag"], rtol=0, atol=1e-15)
         prm = O.mms_params(O.MMS_SIN, dim, kappa=0.1, s=1.0, c=c, p=p)
         np.testing.assert_allclose(O.lf_assemble(m, prm), g[f"{name}_b"], rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("shape,p,pert,kinds", [((4, 3, 5), 2, 0.2, 7), ((3, 3, 3), 3, 0.1, 7), ((4, 4, 4), 1, 0.1, 5),
+                                                ((3, 4, 3), 4, 0.0, 3), ((3, 3, 3), 2, 0.1, 4)])
+def test_oracle_pa_matches_fa(shape, p, pert, kinds):
+    """The host partial-assembly restatement (O.PA: MFEM's per-integrator point data and sum-factorised
+    element loops, the CPU PA + CG baseline of bench.py) is the FA operator: Mult and the constrained
+    Mult to 1e-13 of the assembled CSR, and CGSolver on it gives the CSR solve's 30 iterates (1e-12)."""
+    om = O.BoxMesh(3, shape, p, perturb=pert)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=(1.0, -2.0, 0.5), kinds=kinds)
+    pa = O.PA(om, kappa=0.1, alpha=1.0, s=1.0, c=(1.0, -2.0, 0.5), kinds=kinds)
+    rng = np.random.default_rng(1)
+    x, b = rng.uniform(-1, 1, om.nl), rng.uniform(-1, 1, om.nl)
+    yo = A.mult(x)
+    assert np.abs(pa.mult(x) - yo).max() <= 1e-13 * np.abs(yo).max()
+    xz = x.copy()
+    xz[om.ess] = 0.0
+    yc = A.mult(xz)
+    yc[om.ess] = x[om.ess]
+    assert np.abs(pa.mult(x, constrained=True) - yc).max() <= 1e-13 * np.abs(yc).max()
+    Ac, B = O.form_linear_system(A, om.bdr, np.zeros(om.nl), b)
+    dinv = 1.0 / Ac.diag()
+    x1, i1 = O.cg(Ac, B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    x2, i2 = pa.cg(B, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    assert i1["iterations"] == i2["iterations"] == 30
+    assert np.linalg.norm(x2 - x1) <= 1e-12 * np.linalg.norm(x1)
+
+
+def test_oracle_cg_indefinite_preconditioner():
+    """MFEM CGSolver stops unconverged when (r, M^-1 r) < 0: at iteration 0 (nom0 < 0) or at the
+    iteration where betanom turns negative (kK + sM with s = -124: 210 negative Jacobi entries)."""
+    om = O.BoxMesh(3, (6, 5, 7), 2)
+    A = O.fa_assemble(om, kappa=0.1, s=-124.0, kinds=O.DIFFUSION | O.MASS)
+    b = np.random.default_rng(3).uniform(-1, 1, om.nl)
+    Ac, B = O.form_linear_system(A, om.bdr, np.zeros(om.nl), b)
+    dg = Ac.diag()
+    _, info = O.cg(Ac, B, dinv=1.0 / dg, rel_tol=1e-12, max_iter=200)
+    assert not info["converged"] and info["iterations"] == 4
+    Bn = np.where(dg < 0, B, 0.0)       # nom0 = sum B_i^2 / d_i over negative d_i < 0
+    _, info = O.cg(Ac, Bn, dinv=1.0 / dg, rel_tol=1e-12, max_iter=200)
+    assert not info["converged"] and info["iterations"] == 0
+
+
+def test_oracle_stream_triad_probe():
+    gbs = O.stream_triad_gbs(n=1 << 22, reps=2)
+    assert 0.5 < gbs < 1e5
