@@ -43,16 +43,16 @@ __device__ __forceinline__ int brick_id(const BrickGeom &g)
     return (int)(x * q + (x < r ? x : r) + k);
 }
 
-// Patch positions i = t, t + 64, t + 128, ... of an S^3 patch (x fastest), advanced incrementally:
-// 64 = dz S^2 + dy S + dx, so each step adds (dx, dy, dz) with carries (a few adds and selects
-// instead of two constant divisions per position)
-template <int S>
+// Patch positions i = t, t + STEP, t + 2 STEP, ... of an S^3 patch (x fastest), advanced incrementally:
+// STEP = dz S^2 + dy S + dx, so each step adds (dx, dy, dz) with carries (a few adds and selects
+// instead of two constant divisions per position; STEP < S^3)
+template <int S, int STEP = 64>
 struct PatchWalk {
     int x, y, z;
     __device__ __forceinline__ explicit PatchWalk(unsigned t) : x((int)(t % S)), y((int)((t / S) % S)), z((int)(t / (S * S))) {}
     __device__ __forceinline__ void next()
     {
-        constexpr int dx = 64 % S, dy = (64 / S) % S, dz = 64 / (S * S);
+        constexpr int dx = STEP % S, dy = (STEP / S) % S, dz = STEP / (S * S);
         x += dx;
         const int cx = x >= S ? 1 : 0;
         x -= S & -cx;
@@ -60,6 +60,32 @@ struct PatchWalk {
         const int cy = y >= S ? 1 : 0;
         y -= S & -cy;
         z += dz + cy;
+    }
+};
+
+// PatchWalk plus the lattice index gid = gx + Lx gy + Lxy gz of the position, advanced with the walk's
+// carries (no per-position 32-bit multiplies: v_mul_lo_u32 issues at a quarter of the VALU rate)
+template <int S, int STEP = 64>
+struct LatWalk {
+    int x, y, z;
+    uint32_t gid;
+    __device__ __forceinline__ LatWalk(unsigned t, uint32_t g0, uint32_t Lx, uint32_t Lxy)
+        : x((int)(t % S)), y((int)((t / S) % S)), z((int)(t / (S * S)))
+    {
+        gid = g0 + (uint32_t)x + Lx * (uint32_t)y + Lxy * (uint32_t)z;
+    }
+    __device__ __forceinline__ void next(uint32_t dgid, uint32_t cxd, uint32_t cyd)
+    {
+        constexpr int dx = STEP % S, dy = (STEP / S) % S, dz = STEP / (S * S);
+        x += dx;
+        const int cx = x >= S ? 1 : 0;
+        x -= S & -cx;
+        y += dy + cx;
+        const int cy = y >= S ? 1 : 0;
+        y -= S & -cy;
+        z += dz + cy;
+        // dgid = dx + dy Lx + dz Lxy; a carry out of x adds Lx - S, out of y Lxy - S Lx
+        gid += dgid + (cxd & (uint32_t)-cx) + (cyd & (uint32_t)-cy);
     }
 };
 
@@ -408,20 +434,27 @@ k_brick_patch_sum(const double *__restrict__ x, double *__restrict__ y, const do
 
 // ------------------------------------------------------------------------------------------------
 bool brick_supported(int dim, int p) { return dim == 3 && (p == 1 || p == 2); }
+int brick_count(const cdfem_ctx *c);
+int brick_patch_side(const cdfem_ctx *c);
 
 // kOOB = 2^31 is out of range only for buffers below 2^31 bytes: the lattice vectors (8 N_L) and the
 // patch buffer (8 S^3 per brick) must both fit, else an out-of-lattice load would read real data and a
 // dropped store would land inside the buffer
 bool brick_fits(const cdfem_ctx *c)
 {
-    const double S = kBrick * c->p + 1.0, lim = (double)c->brick_limit;
-    return 8.0 * (double)c->nl < lim && 8.0 * (double)c->nblk * S * S * S < lim;
+    const double S = brick_patch_side(c), lim = (double)c->brick_limit;
+    return 8.0 * (double)c->nl < lim && 8.0 * (double)brick_count(c) * S * S * S < lim;
 }
 
+// the brick lattice of the context: 4^3-element bricks at p <= 2, 2^3-element blocks at p = 3, 4 (ho_brick)
 static BrickGeom geom_of(const cdfem_ctx *c)
 {
+    if (c->p >= 3) return BrickGeom{c->hb_nbx, c->hb_nby, c->hb_nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1};
     return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1};
 }
+
+int brick_count(const cdfem_ctx *c) { return c->p >= 3 ? c->hb_nblk : c->nblk; }
+int brick_patch_side(const cdfem_ctx *c) { return c->p >= 3 ? kHoBrickEdge * c->p + 1 : kBrick * c->p + 1; }
 
 static dim3 faces_grid(const cdfem_ctx *c)
 {
@@ -533,7 +566,7 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // with its patch gather, sums them in one fixed order, takes MFEM's decision (workgroup 0 records it,
 // cg_update_logic; kk = updates so far, from the host) and forms beta itself, so the one-block update
 // finalizer is not launched.
-template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false, bool BF = false>
+template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false, bool BF = false, bool FULL = false>
 __global__ void __launch_bounds__(64, W)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
@@ -549,6 +582,11 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     constexpr int NQ = Q1 * Q1 * Q1;
     __shared__ double s_in[S3];
     __shared__ double s_out[S3];
+    // EP (the Kronecker form, AF 2): the essential rows' patch entries carry (A_c d)_i = d_i, the
+    // writer brick's d (0 where the den ownership bit is off: non-writers, and the slab plane the rank
+    // below owns), so the update's sum of a row's entries is its q with no essential flag or d read
+    constexpr bool EP = AF == 2;
+    __shared__ double s_d[EP ? S3 : 1];
     if (st->done) return;
     double beta = st->beta;
     constexpr int NPL = 16;  // BF: partials per lane (nupart <= 64 NPL)
@@ -588,25 +626,37 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const uint32_t nl = (uint32_t)Lxy * (uint32_t)g.Lz;
     const auto br = brsrc(r, 8u * nl), bm = brsrc(dinv, 8u * nl), bo = brsrc(d_old, 8u * nl);
     const auto be = brsrc(ess, nl), bd = brsrc(d_new, 8u * nl), bxf = brsrc(x, XF ? 8u * nl : 0u);
+    // per position: the writer's byte offset (kOOB where this brick does not write the dof) and one
+    // bit of dbits for "writer, and its d^2 counts in den" (not on a slab plane the rank below owns),
+    // formed once here: the second pass then needs neither the patch walk nor the lane masks (which
+    // the compiler kept in scalar registers and spilled to VGPR lanes across the loads)
     double rv[NI], mv[NI], ov[NI], xv[NI];
-    uint32_t offv[NI];
+    uint32_t woffv[NI];
+    uint32_t dbits = 0, ebits = 0;
     uint8_t ev[NI];
-    PatchWalk<S> pw0(t);
+    // FULL (every brick of the box has its whole patch inside the lattice: the element counts are
+    // multiples of 4): no lattice bound per position
+    const uint32_t uLx = (uint32_t)Lx, uLxy = (uint32_t)Lxy;
+    constexpr uint32_t wdx = 64 % S, wdy = (64 / S) % S, wdz = 64 / (S * S);
+    const uint32_t dgid = wdx + wdy * uLx + wdz * uLxy, cxd = uLx - S, cyd = uLxy - S * uLx;
+    LatWalk<S> pw0(t, (uint32_t)gx0 + uLx * (uint32_t)gy0 + uLxy * (uint32_t)gz0, uLx, uLxy);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const unsigned i = t + 64 * k;
         const int px = pw0.x, py = pw0.y, pz = pw0.z;
-        pw0.next();
-        const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
-        const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
-        const uint32_t gid = (uint32_t)opaque(gx + Lx * gy + Lxy * gz);  // computed in every lane, selected
-        offv[k] = in ? 8u * gid : kOOB;
-        rv[k] = bload(br, offv[k]);
-        mv[k] = bload(bm, offv[k]);
-        ov[k] = bload(bo, offv[k]);
+        const uint32_t gid = pw0.gid;
+        pw0.next(dgid, cxd, cyd);
+        const int gz = gz0 + pz;
+        const bool in = i < S3 && (FULL || (gx0 + px < g.Lx && gy0 + py < g.Ly && gz < g.Lz));
+        const uint32_t off = in ? 8u * gid : kOOB;
+        rv[k] = bload(br, off);
+        mv[k] = bload(bm, off);
+        ov[k] = bload(bo, off);
         ev[k] = __builtin_amdgcn_raw_buffer_load_b8(be, in ? gid : kOOB, 0, 0);
         const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
-        if constexpr (XF) xv[k] = bload(bxf, writer ? offv[k] : kOOB);
+        woffv[k] = writer ? off : kOOB;
+        dbits |= (uint32_t)(writer && !(zlo_shared && gz == 0)) << k;
+        if constexpr (XF) xv[k] = bload(bxf, woffv[k]);
     }
     if constexpr (BF) {
         if (kk > 0) {
@@ -617,7 +667,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
             // cg_update_logic's decision (cg_stop_kind), taken identically by every workgroup at the
             // host's update count kk; workgroup 0 records it at the same kk
             const bool stop = cg_stop_kind(st, B, kk) != kCgGoOn;
-            if (blockIdx.x == 0 && t == 0) {
+            if (b == 0 && t == 0) {  // (global brick 0: one launch records, also when a slab is split in two)
 #ifdef CDFEM_DEBUG
                 assert(st->iter == kk);
 #endif
@@ -627,25 +677,22 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
             beta = B / st->nom;
         }
     }
-    PatchWalk<S> pw1(t);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const unsigned i = t + 64 * k;
         if (k == NI - 1 && i >= S3) break;
-        const int px = pw1.x, py = pw1.y, pz = pw1.z;
-        pw1.next();
-        const int gz = gz0 + pz;
-        const bool in = offv[k] != kOOB;
         const double dn = mv[k] * rv[k] + beta * ov[k];  // 0 outside the lattice
         const bool e = ev[k] != 0;
-        const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
-        const uint32_t woff = writer ? offv[k] : kOOB;
-        bstore(bd, woff, dn);
-        if constexpr (XF) bstore(bxf, woff, xv[k] + alpha_prev * ov[k]);
+        bstore(bd, woffv[k], dn);
+        if constexpr (XF) bstore(bxf, woffv[k], xv[k] + alpha_prev * ov[k]);
         // (A_c d)_i = d_i on ess dofs
-        den += (writer && e && !(zlo_shared && gz == 0)) ? dn * dn : 0.0;
+        den += (e && ((dbits >> k) & 1u)) ? dn * dn : 0.0;
         s_in[i] = e ? 0.0 : dn;
         s_out[i] = 0.0;
+        if constexpr (EP) {  // (unconditional: a predicated LDS store compiles to a branch per position)
+            ebits |= (uint32_t)e << k;
+            s_d[i] = ((dbits >> k) & 1u) ? dn : 0.0;
+        }
     }
     __syncthreads();
 
@@ -677,7 +724,9 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         for (int k = 0; k < NI; ++k) {
             const unsigned i = to + 64 * k;
             if (k == NI - 1 && i >= S3) break;
-            bstore(bp, 8u * (base + (uint32_t)pw.z * A + (uint32_t)pw.y * R + (uint32_t)pw.x), s_out[i]);
+            double v = s_out[i];
+            if constexpr (EP) v = ((ebits >> k) & 1u) ? s_d[i] : v;
+            bstore(bp, 8u * (base + (uint32_t)pw.z * A + (uint32_t)pw.y * R + (uint32_t)pw.x), v);
             pw.next();
         }
     }
@@ -693,7 +742,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
 // napart) in one fixed order and takes MFEM's den step itself (workgroup 0 records it), so the
 // one-block den finalizer and its launch go away; the grid is a few hundred to a few thousand
 // workgroups (grid-stride loop) to keep the redundant sums small, and its partials go to part.
-template <int S, bool XF, bool PB = false, bool DS = false>
+template <int S, bool XF, bool PB = false, bool DS = false, bool EP = false>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ d,
                   const double *__restrict__ dinv, const double *__restrict__ pb,
@@ -729,58 +778,312 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
     const int n = g.Lx * g.Ly * g.Lz;
     const int plane = g.Lx * g.Ly;
     double acc = 0.0;
-    for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += gridDim.x * blockDim.x) {
-        const int gz = (int)fdiv((uint32_t)gid, fdxy);
-        const int rem = gid - gz * plane;
-        const int gy = (int)fdiv((uint32_t)rem, fdx);
-        const int gx = rem - gy * g.Lx;
-        // every load is issued before any is consumed: which bricks' patch outputs hold this dof's
-        // row sum depends on its lattice position only, and the essential flag selects last
-        const bool is_ess = ess[gid] != 0;
-        // XF: x was advanced by the apply (x-fold); d is then needed on essential rows only
-        const double di = (!XF || is_ess) ? d[gid] : 0.0, xi = XF ? 0.0 : x[gid];
-        const double rold = r[gid], mi = dinv[gid];
-        double qi;
-        if constexpr (PB) {
-            qi = patch_sum8<S>(brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S)), g, gx, gy, gz);
-        } else if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
-            int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
-            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
-            if (gx - qx * s1 == 0) {
-                if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
-                if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
-            } else { bxs[0] = qx; pxs[0] = gx - qx * s1; nxc = 1; }
-            if (gy - qy * s1 == 0) {
-                if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
-                if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
-            } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
-            if (gz - qz * s1 == 0) {
-                if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
-                if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
-            } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
-            qi = 0.0;
-            for (int kz = 0; kz < nzc; ++kz)
-                for (int ky = 0; ky < nyc; ++ky)
-                    for (int kx = 0; kx < nxc; ++kx) {
-                        qi += pb[patch_idx<S>(g, bxs[kx], bys[ky], bzs[kz], pxs[kx], pys[ky], pzs[kz])];
-                    }
-        } else {  // inside one brick's patch
-            const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
-            qi = pb[patch_idx<S>(g, qx, qy, qz, gx - qx * s1, gy - qy * s1, gz - qz * s1)];
+    if constexpr (EP) {
+        // the apply's essential-row patch entries (EP in k_brick_cg): q is the sum of the row's 1-8
+        // entries everywhere (with the neighbour's plane sums on a slab), so the loop reads r, M^-1 and
+        // the patch only, every load independent of the others (no essential flag, no d)
+        static_assert(PB, "EP reads the patch buffer with the predicated loads");
+        const auto bp = brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S));
+        for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += gridDim.x * blockDim.x) {
+            const int gz = (int)fdiv((uint32_t)gid, fdxy);
+            const int rem = gid - gz * plane;
+            const int gy = (int)fdiv((uint32_t)rem, fdx);
+            const int gx = rem - gy * g.Lx;
+            const double rold = r[gid], mi = dinv[gid];
+            const double xi = XF ? 0.0 : x[gid], di = XF ? 0.0 : d[gid];
+            double qi = patch_sum8<S>(bp, g, gx, gy, gz);
+            if (remote_lo && gz == 0) qi += remote_lo[rem];
+            if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
+            if constexpr (!XF) __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
+            const double ri = rold - alpha * qi;
+            __builtin_nontemporal_store(ri, &r[gid]);
+            if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
         }
-        // interface planes: add the neighbour rank's partial sums
-        if (remote_lo && gz == 0) qi += remote_lo[rem];
-        if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
-        if (is_ess) qi = di;
-        if constexpr (!XF) __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
-        const double ri = rold - alpha * qi;
-        __builtin_nontemporal_store(ri, &r[gid]);
-        if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
+    } else {
+        for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += gridDim.x * blockDim.x) {
+            const int gz = (int)fdiv((uint32_t)gid, fdxy);
+            const int rem = gid - gz * plane;
+            const int gy = (int)fdiv((uint32_t)rem, fdx);
+            const int gx = rem - gy * g.Lx;
+            // every load is issued before any is consumed: which bricks' patch outputs hold this dof's
+            // row sum depends on its lattice position only, and the essential flag selects last
+            const bool is_ess = ess[gid] != 0;
+            // XF: x was advanced by the apply (x-fold); d is then needed on essential rows only
+            const double di = (!XF || is_ess) ? d[gid] : 0.0, xi = XF ? 0.0 : x[gid];
+            const double rold = r[gid], mi = dinv[gid];
+            double qi;
+            if constexpr (PB) {
+                qi = patch_sum8<S>(brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S)), g, gx, gy, gz);
+            } else if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
+                int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
+                const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
+                if (gx - qx * s1 == 0) {
+                    if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
+                    if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
+                } else { bxs[0] = qx; pxs[0] = gx - qx * s1; nxc = 1; }
+                if (gy - qy * s1 == 0) {
+                    if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
+                    if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
+                } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
+                if (gz - qz * s1 == 0) {
+                    if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
+                    if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
+                } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
+                qi = 0.0;
+                for (int kz = 0; kz < nzc; ++kz)
+                    for (int ky = 0; ky < nyc; ++ky)
+                        for (int kx = 0; kx < nxc; ++kx) {
+                            qi += pb[patch_idx<S>(g, bxs[kx], bys[ky], bzs[kz], pxs[kx], pys[ky], pzs[kz])];
+                        }
+            } else {  // inside one brick's patch
+                const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
+                qi = pb[patch_idx<S>(g, qx, qy, qz, gx - qx * s1, gy - qy * s1, gz - qz * s1)];
+            }
+            // interface planes: add the neighbour rank's partial sums
+            if (remote_lo && gz == 0) qi += remote_lo[rem];
+            if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
+            if (is_ess) qi = di;
+            if constexpr (!XF) __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
+            const double ri = rold - alpha * qi;
+            __builtin_nontemporal_store(ri, &r[gid]);
+            if (!(zlo_shared && gz == 0)) acc += ri * (mi * ri);
+        }
     }
     const double bs = block_sum(acc, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = bs;
 }
 
+
+// ================================================================================================
+// High-order brick CG apply (3D p = 3, 4 on a structured affine box; set_option "ho_brick"): the brick
+// CG protocol of k_brick_cg on blocks of 2 x 2 x 2 elements (an S^3 patch, S = 2p + 1: 9^3 at p = 4),
+// with the Kronecker-form element core of k_apply3d_ktile (ho_kernels.hip) spread over one D1 x D1
+// thread tile per element.  Per block (8 D1^2 threads, 256 at p = 4):
+//   1. patch: d_new = M^-1 r + beta d_old on every position (the writer block stores it, and x +=
+//      alpha d_old under the x-fold), the essential entries zeroed in LDS, their d^2 into den;
+//   2. the eight elements' tiles: x + y stages (thread (ix, jz)) -> LDS groups, z stage (thread
+//      (ix, iy)) -> the element output Y in LDS, d~_e . Y_e into den;
+//   3. E->L inside the block: every patch position sums its 1-8 element entries in a fixed order
+//      and the whole patch goes to the patch buffer (patch_idx, the p = 2 brick's layout), so
+//      k_cg_update_faces (S = 2p + 1) forms q and updates r exactly as on the p = 2 brick.
+// This replaces the tile path's E-vector round trip (125 entries per element written, then read by
+// the flat E->L update) with 729 patch entries per 8 elements, and the update's x, d and z streams
+// with the brick CG's r, M^-1.
+// ================================================================================================
+constexpr int kHoBrick = kHoBrickEdge;  // elements per block edge (high order)
+
+// MF (set_option "ho_brick_mfma", kinds 7): the x stage of the eight elements as block GEMMs on
+// v_mfma_f64_16x16x4_f64 (block_mfma, pa_core.hpp): rows = the block's 8 x 25 element rows
+// (element, jz, jy), k = jx (5, padded to 8), columns = (matrix, ix) for M, K, C, C^T (20, as a
+// 16-column and a 4-column GEMM), staged through LDS (aliased on the y-stage groups) to the tile
+// threads, which form the element combinations and the y / z stages on the VALU as before.  The
+// north star's "MFMA for the per-element B^T D B contraction at high order", A/B'd against the VALU
+// x stage.
+template <int D1, int Q1, unsigned K, bool XF, bool MF = false>
+__global__ void __launch_bounds__(((kHoBrick * kHoBrick * kHoBrick * D1 * D1 + 63) / 64) * 64, 2)
+k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, const double *__restrict__ d_old,
+             double *__restrict__ d_new, double *__restrict__ face, const double *__restrict__ qaff,
+             const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g, int nex, int ney, int nez,
+             double *__restrict__ part, const KrylovState *__restrict__ st, double *__restrict__ x,
+             const double *__restrict__ ktab)
+{
+    using L = QLayout<K, 3>;
+    constexpr int P = D1 - 1, EB = kHoBrick, S = EB * P + 1, S2 = S * S, S3 = S * S * S;
+    constexpr int DD = D1 * D1, ND = DD * D1, NEB = EB * EB * EB, NC = L::nc;
+    constexpr int NT = ((NEB * DD + 63) / 64) * 64, NI = (S3 + NT - 1) / NT;
+    __shared__ double s_in[S3];
+    __shared__ double sP[NEB][4][ND];  // [element][grp][jz][iy][ix]
+    __shared__ double sE[NEB][ND];     // element outputs Y [dz][dy][dx]
+    __shared__ double shd[NT / 64];
+    if (st->done) return;
+    const double beta = st->beta;
+    const double alpha_prev = XF ? st->alpha : 0.0;
+    const int tid = threadIdx.x;
+    const int b = brick_id(g);
+    const int nxy = g.nbx * g.nby;
+    const int bz = b / nxy, by = (b - bz * nxy) / g.nbx, bx = b - bz * nxy - by * g.nbx;
+    const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
+    const bool lastx = bx == g.nbx - 1, lasty = by == g.nby - 1, lastz = bz == g.nbz - 1;
+    const int Lx = g.Lx, Lxy = g.Lx * g.Ly;
+    const uint32_t nl = (uint32_t)Lxy * (uint32_t)g.Lz;
+    const auto br = brsrc(r, 8u * nl), bm = brsrc(dinv, 8u * nl), bo = brsrc(d_old, 8u * nl);
+    const auto be = brsrc(ess, nl), bd = brsrc(d_new, 8u * nl), bxf = brsrc(x, XF ? 8u * nl : 0u);
+    // this thread's element tile and x-stage rows (ix = a), loaded with the patch
+    const int le = tid / DD, tt = tid - le * DD, a = tt % D1, bb = tt / D1;
+    const int lex = le & 1, ley = (le >> 1) & 1, lez = le >> 2;
+    const int ex = EB * bx + lex, ey = EB * by + ley, ez = EB * bz + lez;
+    const bool tile = le < NEB, valid = tile && ex < nex && ey < ney && ez < nez;
+    const int64_t ec = valid ? (int64_t)ex + (int64_t)nex * (ey + (int64_t)ney * ez) : 0;
+    double Mr[D1], Kr[D1], Cr[D1], Ctr[D1], gf[NC];
+#pragma unroll
+    for (int j = 0; j < D1; ++j) {
+        Mr[j] = ktab[(0 * D1 + a) * D1 + j];
+        Kr[j] = ktab[(1 * D1 + a) * D1 + j];
+        Cr[j] = ktab[(2 * D1 + a) * D1 + j];
+        Ctr[j] = ktab[(3 * D1 + a) * D1 + j];
+    }
+#pragma unroll
+    for (int k = 0; k < NC; ++k) gf[k] = qaff[ec * NC + k];
+    // 1. the patch: all loads issued before any is consumed (kOOB outside the lattice: 0)
+    double den = 0.0;
+    {
+        double rv[NI], mv[NI], ov[NI], xv[NI];
+        uint32_t offv[NI];
+        uint8_t ev[NI];
+        PatchWalk<S, NT> pw0(tid);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const unsigned i = tid + NT * k;
+            const int px = pw0.x, py = pw0.y, pz = pw0.z;
+            pw0.next();
+            const int gx = gx0 + px, gy = gy0 + py, gz = gz0 + pz;
+            const bool in = i < S3 && gx < g.Lx && gy < g.Ly && gz < g.Lz;
+            const uint32_t gid = (uint32_t)opaque(gx + Lx * gy + Lxy * gz);
+            offv[k] = in ? 8u * gid : kOOB;
+            rv[k] = bload(br, offv[k]);
+            mv[k] = bload(bm, offv[k]);
+            ov[k] = bload(bo, offv[k]);
+            ev[k] = __builtin_amdgcn_raw_buffer_load_b8(be, in ? gid : kOOB, 0, 0);
+            const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
+            if constexpr (XF) xv[k] = bload(bxf, writer ? offv[k] : kOOB);
+        }
+        PatchWalk<S, NT> pw1(tid);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const unsigned i = tid + NT * k;
+            const int px = pw1.x, py = pw1.y, pz = pw1.z;
+            pw1.next();
+            if (i >= S3) break;
+            const bool in = offv[k] != kOOB;
+            const double dn = mv[k] * rv[k] + beta * ov[k];  // 0 outside the lattice
+            const bool e = ev[k] != 0;
+            const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
+            const uint32_t woff = writer ? offv[k] : kOOB;
+            bstore(bd, woff, dn);
+            if constexpr (XF) bstore(bxf, woff, xv[k] + alpha_prev * ov[k]);
+            den += (writer && e) ? dn * dn : 0.0;  // (A_c d)_i = d_i on ess dofs
+            s_in[i] = e ? 0.0 : dn;
+        }
+    }
+    __syncthreads();
+    // 2. element tiles: x + y stages, thread (ix = a, jz = bb)
+    const int o0 = P * lez * S2 + P * ley * S + P * lex;
+    double xq[MF ? 4 : 1][MF ? D1 : 1];  // MF: this thread's (M, K, C, C^T) X rows, from the GEMM
+    if constexpr (MF) {
+        constexpr int NR = NEB * DD, NCOL = 4 * D1;
+        static_assert(NR * NCOL <= NEB * 4 * ND, "the x-stage output aliases the y-stage groups");
+        double *xs = &sP[0][0][0];
+        auto arow = [&](int row, int k) {
+            const int e8 = row / DD, rr = row - e8 * DD, jz = rr / D1, jy = rr - jz * D1;
+            const int ob = P * (e8 >> 2) * S2 + P * ((e8 >> 1) & 1) * S + P * (e8 & 1);
+            return k < D1 ? s_in[ob + jz * S2 + jy * S + k] : 0.0;
+        };
+        auto bcol = [&](int k, int col) { return (k < D1 && col < NCOL) ? ktab[col * D1 + k] : 0.0; };
+        block_mfma<NR, (D1 + 3) / 4>(arow, bcol, [&](int row, int col, double v) { xs[row * NCOL + col] = v; });
+        block_mfma<NR, (D1 + 3) / 4>(arow, [&](int k, int col) { return bcol(k, 16 + col); },
+                                     [&](int row, int col, double v) {
+                                         if (16 + col < NCOL) xs[row * NCOL + 16 + col] = v;
+                                     });
+        __syncthreads();
+        if (tile) {
+#pragma unroll
+            for (int jy = 0; jy < D1; ++jy) {
+                const int row = le * DD + bb * D1 + jy;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) xq[q][jy] = xs[row * NCOL + q * D1 + a];
+            }
+        }
+        __syncthreads();  // (the y stage's groups overwrite xs)
+    }
+    if (tile) {
+        double v[D1][5];
+#pragma unroll
+        for (int jy = 0; jy < D1; ++jy) {
+            double mm = 0.0, kk = 0.0, cc = 0.0, ct = 0.0;
+            if constexpr (MF) {
+                mm = xq[0][jy];
+                kk = xq[1][jy];
+                cc = xq[2][jy];
+                ct = xq[3][jy];
+            } else {
+                const double *xrow = &s_in[o0 + bb * S2 + jy * S];
+#pragma unroll
+                for (int jx = 0; jx < D1; ++jx) {
+                    const double xv = xrow[jx];
+                    mm += Mr[jx] * xv;
+                    if constexpr (L::kD) {
+                        kk += Kr[jx] * xv;
+                        ct += Ctr[jx] * xv;
+                    }
+                    if constexpr (L::kD || L::kC) cc += Cr[jx] * xv;
+                }
+            }
+            kron_xcombine<K>(gf, mm, kk, cc, ct, v[jy]);
+        }
+        auto col = [&](int q, int jy) { return v[jy][q]; };
+#pragma unroll
+        for (int iy = 0; iy < D1; ++iy) {
+            double Pg[4];
+            kron_y<D1, Q1, K>(T, gf, col, iy, Pg);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sP[le][k][(bb * D1 + iy) * D1 + a] = Pg[k];
+        }
+    }
+    __syncthreads();
+    // z stage, thread (ix = a, iy = bb): Y -> LDS and the element's d~ . A_e d~
+    if (tile) {
+        double Yz[D1];
+#pragma unroll
+        for (int iz = 0; iz < D1; ++iz) Yz[iz] = 0.0;
+#pragma unroll
+        for (int jz = 0; jz < D1; ++jz) {
+            double Pg[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Pg[k] = sP[le][k][(jz * D1 + bb) * D1 + a];
+            kron_z<D1, Q1, K>(T, Pg, jz, Yz);
+        }
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz) {
+            const double y = valid ? Yz[dz] : 0.0;
+            den += s_in[o0 + dz * S2 + bb * S + a] * y;
+            sE[le][(dz * D1 + bb) * D1 + a] = y;
+        }
+    }
+    __syncthreads();
+    // 3. E->L in the block: position (px, py, pz) takes the entries of the 1-8 elements holding it
+    //    (lower element first per axis, z outermost) -> the patch buffer
+    {
+        const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
+        const uint32_t base = (uint32_t)bz * S * A + (uint32_t)by * S * R + (uint32_t)bx * S;
+        const auto bp = brsrc(face, 8u * (uint32_t)g.nbx * g.nby * g.nbz * S3);
+        const unsigned to = (unsigned)opaque(tid);
+        PatchWalk<S, NT> pw(to);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const unsigned i = to + NT * k;
+            if (i >= S3) break;
+            const int px = pw.x, py = pw.y, pz = pw.z;
+            // per axis: element 0 holds positions 0..P, element 1 positions P..2P (local P + 0..P)
+            const int x0 = px < P ? px : P, y0 = py < P ? py : P, z0 = pz < P ? pz : P;
+            const bool hx1 = px >= P, hy1 = py >= P, hz1 = pz >= P;
+            const bool hx0 = px <= P, hy0 = py <= P, hz0 = pz <= P;
+            const int x1 = px - P, y1 = py - P, z1 = pz - P;
+            double sum = 0.0;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int cx = c & 1, cy = (c >> 1) & 1, cz = c >> 2;
+                const bool ok = (cx ? hx1 : hx0) && (cy ? hy1 : hy0) && (cz ? hz1 : hz0);
+                const int lx = cx ? x1 : x0, ly = cy ? y1 : y0, lz = cz ? z1 : z0;
+                const double t = sE[cx + 2 * cy + 4 * cz][ok ? (lz * D1 + ly) * D1 + lx : 0];
+                sum += ok ? t : 0.0;
+            }
+            bstore(bp, 8u * (base + (uint32_t)pw.z * A + (uint32_t)pw.y * R + (uint32_t)pw.x), sum);
+            pw.next();
+        }
+    }
+    const double bs = block_sum(den, shd);
+    if (tid == 0) part[b] = bs;
+}
 
 // one launch of k_brick_cg over brick layers bz0, bz0 + bzs, ... (nlay of them) on stream s;
 // the whole slab (0, 1, nbz) on the context stream goes through CDFEM_LAUNCH (profiling events)
@@ -803,23 +1106,27 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
     const double *qd = c->d_qaff ? c->d_qaff : c->d_qd;
     const double *upart = c->d_part + c->nblk;  // the den-fold update's partials
-#define CDFEM_BCG4(AFF_, W_, XF_, BF_)                                                                      \
+#define CDFEM_BCG5(AFF_, W_, XF_, BF_, FU_)                                                                 \
     if (whole)                                                                                               \
-        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_>), grid, block, 0, r, dinv, d_old, d_new, q,  \
+        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_>), grid, block, 0, r, dinv, d_old, d_new, q, \
                      c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x, upart, run.nupart, \
                      run.kk);                                                                                \
     else                                                                                                     \
-        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_>), grid, block, 0, run.s, r, dinv, d_old,   \
-                           d_new, q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x, upart, \
-                           run.nupart, run.kk)
-#define CDFEM_BCG3(AFF_, W_, XF_) CDFEM_BCG4(AFF_, W_, XF_, false)
+        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_>), grid, block, 0, run.s, r, dinv,     \
+                           d_old, d_new, q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x, \
+                           upart, run.nupart, run.kk)
+#define CDFEM_BCG4(AFF_, W_, XF_, BF_)                                                                      \
+    if (full) { CDFEM_BCG5(AFF_, W_, XF_, BF_, true); } else { CDFEM_BCG5(AFF_, W_, XF_, BF_, false); }
+#define CDFEM_BCG3(AFF_, W_, XF_) CDFEM_BCG5(AFF_, W_, XF_, false, false)
 #define CDFEM_BCG(AFF_, W_) CDFEM_BCG3(AFF_, W_, false)
+    // every brick's patch inside the lattice (element counts multiples of 4): no per-position bounds
+    const bool full = c->sx % kBrick == 0 && c->sy % kBrick == 0 && c->sz % kBrick == 0;
     if (pa_af(c) == 2 && run.kk >= 0) {
         if (x) { CDFEM_BCG4(2, 2, true, true); }
         else { CDFEM_BCG4(2, 2, false, true); }
     } else if (pa_af(c) == 2) {
-        if (x) { CDFEM_BCG3(2, 2, true); }
-        else { CDFEM_BCG(2, 2); }
+        if (x) { CDFEM_BCG4(2, 2, true, false); }
+        else { CDFEM_BCG4(2, 2, false, false); }
     } else if (pa_af(c) == 1) {
         CDFEM_BCG(1, 1);
     } else {
@@ -828,6 +1135,33 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
 #undef CDFEM_BCG
 #undef CDFEM_BCG3
 #undef CDFEM_BCG4
+#undef CDFEM_BCG5
+    return hipGetLastError();
+}
+
+template <int D1, int Q1, unsigned K>
+static hipError_t hobrick_launch(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old, double *d_new,
+                                 double *x)
+{
+    constexpr int NT = ((kHoBrick * kHoBrick * kHoBrick * D1 * D1 + 63) / 64) * 64;
+    const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
+    const double *kt = nullptr;
+    if (c->d_hbpart == nullptr) return hipErrorInvalidValue;
+    const hipError_t e = ho_ktab(c, &kt);
+    if (e != hipSuccess || kt == nullptr) return e != hipSuccess ? e : hipErrorInvalidValue;
+    const BrickGeom g = geom_of(c);
+    const dim3 grid((unsigned)c->hb_nblk), block(NT);
+#define CDFEM_HB(XF_, MF_)                                                                                     \
+    CDFEM_LAUNCH(c, (k_hobrick_cg<D1, Q1, K, XF_, MF_>), grid, block, 0, r, dinv, d_old, d_new, c->d_face, c->d_qaff, \
+                 c->d_ess, T, g, c->sx, c->sy, c->sz, c->d_hbpart, c->d_state, x, kt)
+    if constexpr (K == 7) {  // the MFMA x stage is built for the full operator only (ho_brick_mfma)
+        if (c->ho_brick_mfma) {
+            if (x) { CDFEM_HB(true, true); } else { CDFEM_HB(false, true); }
+            return hipGetLastError();
+        }
+    }
+    if (x) { CDFEM_HB(true, false); } else { CDFEM_HB(false, false); }
+#undef CDFEM_HB
     return hipGetLastError();
 }
 
@@ -835,6 +1169,24 @@ static hipError_t brick_cg2_run(cdfem_ctx *c, const double *r, const double *din
                                 double *d_new, double *q, const BrickRun &run, double *x)
 {
     const int q1 = c->rule_op.q1;
+    if (c->p >= 3) {  // 2^3-element blocks, one launch (one rank)
+        if (run.nlay != c->hb_nbz || run.kk >= 0) return hipErrorInvalidValue;
+#define CDFEM_HK(D1_, Q1_)                                                                          \
+    switch (c->kinds) {                                                                             \
+    case 1: return hobrick_launch<D1_, Q1_, 1>(c, r, dinv, d_old, d_new, x);                        \
+    case 2: return hobrick_launch<D1_, Q1_, 2>(c, r, dinv, d_old, d_new, x);                        \
+    case 3: return hobrick_launch<D1_, Q1_, 3>(c, r, dinv, d_old, d_new, x);                        \
+    case 4: return hobrick_launch<D1_, Q1_, 4>(c, r, dinv, d_old, d_new, x);                        \
+    case 5: return hobrick_launch<D1_, Q1_, 5>(c, r, dinv, d_old, d_new, x);                        \
+    case 6: return hobrick_launch<D1_, Q1_, 6>(c, r, dinv, d_old, d_new, x);                        \
+    case 7: return hobrick_launch<D1_, Q1_, 7>(c, r, dinv, d_old, d_new, x);                        \
+    default: return hipErrorInvalidValue;                                                           \
+    }
+        if (c->p == 3 && q1 == 5) { CDFEM_HK(4, 5) }
+        if (c->p == 4 && q1 == 6) { CDFEM_HK(5, 6) }
+#undef CDFEM_HK
+        return hipErrorInvalidValue;
+    }
 #define CDFEM_K(D1_, Q1_)                                                                           \
     switch (c->kinds) {                                                                             \
     case 1: return brick_cg2_launch<D1_, Q1_, 1>(c, r, dinv, d_old, d_new, q, run, x);                 \
@@ -855,7 +1207,7 @@ static hipError_t brick_cg2_run(cdfem_ctx *c, const double *r, const double *din
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
                             double *d_new, double *q, double *x, int bfkk)
 {
-    BrickRun run{0, 1, c->nbz, c->stream};
+    BrickRun run{0, 1, c->p >= 3 ? c->hb_nbz : c->nbz, c->stream};
     if (bfkk >= 0) {
         run.kk = bfkk;
         run.nupart = cg_den_fold_grid(c);
@@ -871,21 +1223,49 @@ int cg_den_fold_grid(const cdfem_ctx *c)
 }
 
 // the betanom step folded into the next apply (one rank, Kronecker form, den fold on, <= 1024 partials)
+// both scalar steps folded (den in the update, betanom in the next apply): p <= 2, Kronecker form, and
+// partial counts the kernels' fixed-order sums are sized for (the apply's 4,096 per 64^3 slab, the
+// update's <= 1024)
+static bool cg_folds_fit(const cdfem_ctx *c)
+{
+    return c->cg_den_fold != 0 && c->cg_beta_fold != 0 && c->p <= 2 && pa_af(c) == 2 && cg_den_fold_grid(c) <= 1024;
+}
+
+// several ranks (set_option "cg_mr_fold"): the ranks all-reduce the apply's den partials and the
+// update's betanom partials as vectors (element-wise sum over ranks: every rank then holds the same
+// partials and forms the same scalars in the same order), so the update and the next apply take the
+// den and betanom steps as on one rank; no sum / step kernels between them
+bool cg_mr_fold(const cdfem_ctx *c)
+{
+    return multi_rank(c) && c->cg_mr_fold != 0 && cg_folds_fit(c) && brick_count(c) <= kMrFoldMaxParts;
+}
+
 bool cg_beta_fold_ok(const cdfem_ctx *c)
 {
-    return c->cg_beta_fold != 0 && c->cg_den_fold != 0 && !multi_rank(c) && pa_af(c) == 2 &&
-           cg_den_fold_grid(c) <= 1024;
+    return cg_folds_fit(c) && (!multi_rank(c) || cg_mr_fold(c));
+}
+
+// den step inside the update (p <= 2: every update workgroup sums the apply's partials, one per
+// 64-element brick; the high-order blocks leave too many partials and keep the finalizer)
+bool cg_den_fold_on(const cdfem_ctx *c)
+{
+    return c->cg_den_fold != 0 && c->p <= 2 && (!multi_rank(c) || cg_mr_fold(c));
 }
 
 // the first and last brick layers (the shared planes' partial sums) on stream s, the interior
 // layers on the context stream; nbz >= 3
 hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                                  double *d_new, double *q, hipStream_t s, double *x)
+                                  double *d_new, double *q, hipStream_t s, double *x, int bfkk)
 {
     if (c->nbz < 3) return hipErrorInvalidValue;
-    const hipError_t e = brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{0, c->nbz - 1, 2, s}, x);
+    BrickRun edge{0, c->nbz - 1, 2, s}, inner{1, 1, c->nbz - 2, c->stream};
+    if (bfkk >= 0) {
+        edge.kk = inner.kk = bfkk;
+        edge.nupart = inner.nupart = cg_den_fold_grid(c);
+    }
+    const hipError_t e = brick_cg2_run(c, r, dinv, d_old, d_new, q, edge, x);
     if (e != hipSuccess) return e;
-    return brick_cg2_run(c, r, dinv, d_old, d_new, q, BrickRun{1, 1, c->nbz - 2, c->stream}, x);
+    return brick_cg2_run(c, r, dinv, d_old, d_new, q, inner, x);
 }
 
 hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const double *q, const double *d,
@@ -899,13 +1279,17 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     const int64_t need = (c->nl + kRedThreads - 1) / kRedThreads;
     const unsigned grid = (unsigned)(need < 16384 ? need : 16384);
     // den fold (one rank): a grid of cg_den_fold workgroups, partials after the apply's
-    const bool ds = !den_step && !multi_rank(c) && c->cg_den_fold != 0;
+    const bool ds = !den_step && cg_den_fold_on(c);
     const unsigned ugrid = ds ? (unsigned)cg_den_fold_grid(c) : grid;
     double *const upart = ds ? c->d_part + c->nblk : c->d_part;
-#define CDFEM_UPD3(S_, XF_, PB_, DS_)                                                                      \
-    hipLaunchKernelGGL((k_cg_update_faces<S_, XF_, PB_, DS_>), dim3(ugrid), dim3(kRedThreads), 0, c->stream, x, r, \
-                       d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, upart,  \
+#define CDFEM_UPD4(S_, XF_, PB_, DS_, EP_)                                                                 \
+    hipLaunchKernelGGL((k_cg_update_faces<S_, XF_, PB_, DS_, EP_>), dim3(ugrid), dim3(kRedThreads), 0, c->stream, x, \
+                       r, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, upart, \
                        c->d_state, (int)den_step, c->d_part, c->nblk)
+    // the apply's essential-row patch entries (k_brick_cg EP: the Kronecker form at p <= 2)
+    const bool ep = pa_af(c) == 2 && c->p <= 2;
+#define CDFEM_UPD3(S_, XF_, PB_, DS_)                                                                      \
+    if (ep && PB_) { CDFEM_UPD4(S_, XF_, PB_, DS_, PB_); } else { CDFEM_UPD4(S_, XF_, PB_, DS_, false); }
 #define CDFEM_UPD2(S_, XF_, PB_)                                                                           \
     if (ds) { CDFEM_UPD3(S_, XF_, PB_, true); } else { CDFEM_UPD3(S_, XF_, PB_, false); }
     // predicated-load face sums: the patch buffer's byte offsets must fit 32 bits
@@ -918,18 +1302,21 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     }
     if (c->p == 1) {
         CDFEM_UPD(kBrick * 1 + 1);
-    } else if (c->p == 2) {
+    } else if (c->p == 2 || c->p == 4) {  // (p = 4: 2^3-element blocks, the same 9^3 patch)
         CDFEM_UPD(kBrick * 2 + 1);
+    } else if (c->p == 3) {
+        CDFEM_UPD(kHoBrickEdge * 3 + 1);
     } else {
         return hipErrorInvalidValue;
     }
 #undef CDFEM_UPD
 #undef CDFEM_UPD2
 #undef CDFEM_UPD3
+#undef CDFEM_UPD4
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (multi_rank(c)) return launch_fin_sum(c, (int)grid, 1);
     if (ds && cg_beta_fold_ok(c)) return hipSuccess;  // the next apply takes the betanom step
+    if (multi_rank(c)) return launch_fin_sum(c, (int)grid, 1);
     return launch_update_fin(c, (int)ugrid, ds ? c->nblk : 0);
 }
 

@@ -167,6 +167,10 @@ void free_mesh(cdfem_ctx *c)
     c->mesh_ready = c->pa_ready = c->dinv_ready = false;
     c->structured = false;
     c->epencil = false;
+    c->mr_fold_checked = false;
+    dfree(c->d_small);
+    dfree(c->d_hbpart);
+    c->hb_nblk = 0;
 }
 
 // ---- profiling helpers ---------------------------------------------------------------------------
@@ -257,6 +261,15 @@ void build_layout(cdfem_ctx *c, const std::vector<int32_t> &perm)
 }
 
 bool use_brick(const cdfem_ctx *c) { return c->structured && brick_supported(c->dim, c->p) && brick_fits(c); }
+
+// the high-order brick CG (3D p = 3, 4, one rank, affine box with constant coefficients: the Kronecker
+// tile core on 2^3-element blocks, brick_kernels.hip k_hobrick_cg, then the brick update)
+bool use_hobrick_cg(const cdfem_ctx *c)
+{
+    return c->ho_brick != 0 && c->structured && c->qlay == 1 && c->hb_nblk > 0 && tile_kron(c) && tile_den_ok(c) &&
+           !multi_rank(c) && !c->fa_ready && brick_fits(c);
+}
+bool use_brick_cg(const cdfem_ctx *c) { return use_brick(c) || use_hobrick_cg(c); }
 
 const double *ones_vector(cdfem_ctx *c)
 {
@@ -380,6 +393,31 @@ const double *solver_dinv(cdfem_ctx *c)
     return c->d_dinv_p;
 }
 
+// cg_mr_fold all-reduces partial vectors, so every rank must take it and hold as many partials as the
+// others: the apply's (one per brick) and the update's (cg_den_fold_grid).  Decided once per partition
+// by every rank of a multi-rank solve from the all-reduced eligibility flags and the sums of the counts
+// and of their squares (equal on every rank, so every rank takes the same branch): the fold runs iff
+// every rank is eligible and the counts' variance is zero.
+// The result is kept until a local input changes (the options, the partition): ranks change their
+// options together, so they re-check together.
+bool mr_fold_agreed(cdfem_ctx *c)
+{
+    const double ok = cg_mr_fold(c) ? 1.0 : 0.0, nb = brick_count(c), ng = cg_den_fold_grid(c);
+    const double key = ok + 2.0 * (nb + 1e6 * ng);
+    if (c->mr_fold_checked && c->mr_fold_key == key) return c->mr_fold_agree;
+    c->mr_fold_key = key;
+    double h[5] = {ok, nb, nb * nb, ng, ng * ng};
+    if (!c->d_small) c->d_small = dalloc<double>(8);
+    HIPCHK(hipMemcpyAsync(c->d_small, h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+    comm_allreduce(c, c->d_small, 5);
+    HIPCHK(hipMemcpyAsync(h, c->d_small, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const double n = c->nranks;
+    c->mr_fold_agree = h[0] == n && h[2] * n == h[1] * h[1] && h[4] * n == h[3] * h[3];
+    c->mr_fold_checked = true;
+    return c->mr_fold_agree;
+}
+
 // brick-path CG (MFEM CGSolver arithmetic): per iteration k_brick_cg (direction + apply + den
 // partials) -> den finalizer -> k_cg_update_faces (q assembly + x, r update + betanom partials) ->
 // betanom finalizer.  The search direction alternates between two buffers.
@@ -388,6 +426,12 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
 {
     double *x = c->d_w[2], *r = c->d_w[3], *q = c->d_w[4];
     if (!c->d_dalt) c->d_dalt = dalloc<double>(c->nl);
+    const int nbrick = brick_count(c);
+    if (!c->d_face) {  // (p = 3, 4: the blocks' patch buffer, first use)
+        const int S = brick_patch_side(c);
+        c->d_face = dalloc<double>((size_t)nbrick * S * S * S);
+    }
+    if (c->p >= 3 && !c->d_hbpart) c->d_hbpart = dalloc<double>(nbrick);
     double *dprev = c->d_w[5], *dcur = c->d_dalt;
     const double *dinv;
     if (p.pc == CDFEM_PC_JACOBI) {
@@ -424,7 +468,10 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     double *const dbuf0 = dcur, *const dbuf1 = dprev;  // apply j writes d_j into dbuf[(j - 1) & 1]
     // betanom fold (cg_beta_fold): apply j > 0 takes the betanom step of update j - 1 (nupd updates so
     // far); the loop always ends with an apply, so every update's step runs
-    const bool bfold = !mr && cg_beta_fold_ok(c);
+    // several ranks (cg_mr_fold): the den and betanom partial vectors are all-reduced and both folds
+    // run as on one rank; the per-iteration kernels are then the one-rank pair plus the plane pack
+    const bool mrfold = mr && mr_fold_agreed(c);
+    const bool bfold = mr ? mrfold : cg_beta_fold_ok(c);
     int nupd = 0;
     int napply = 0;
     auto apply = [&] {
@@ -435,13 +482,17 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             HIPCHK(hipStreamWaitEvent(c->stream2, c->ov_ev[0], 0));
             // boundary layers on the side stream, interior layers queued on the main stream
             // before the (possibly host-blocking) exchange is issued
-            HIPCHK(launch_brick_cg2_split(c, r, dinv, dprev, dcur, q, c->stream2, xf));
+            HIPCHK(launch_brick_cg2_split(c, r, dinv, dprev, dcur, q, c->stream2, xf, bfold ? nupd : -1));
             HIPCHK(launch_pack_qplanes(c, q, c->stream2));
             comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], c->Lx * c->Ly, c->stream2);
             HIPCHK(hipEventRecord(c->ov_ev[1], c->stream2));
             HIPCHK(hipStreamWaitEvent(c->stream, c->ov_ev[1], 0));
-            HIPCHK(launch_fin_sum(c, c->nblk, 0));
-            comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
+            if (mrfold) {
+                comm_allreduce(c, c->d_part, nbrick);  // the den partials: the update sums them
+            } else {
+                HIPCHK(launch_fin_sum(c, nbrick, 0));
+                comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
+            }
             return;
         }
         prof_mark(c, CDFEM_K_APPLY, true);
@@ -452,10 +503,16 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             // neighbours' partial sums of q on the shared planes (added by the update kernel)
             HIPCHK(launch_pack_qplanes(c, q));
             comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], c->Lx * c->Ly);
-            HIPCHK(launch_fin_sum(c, c->nblk, 0));
-            comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
-        } else if (!c->cg_den_fold) {
-            HIPCHK(launch_den_fin(c, c->nblk));  // (cg_den_fold: the update kernel takes the den step)
+            if (mrfold) {
+                comm_allreduce(c, c->d_part, nbrick);
+            } else {
+                HIPCHK(launch_fin_sum(c, nbrick, 0));
+                comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
+            }
+        } else if (c->p >= 3) {
+            HIPCHK(launch_den_from_partials(c, c->d_hbpart, nbrick));  // (one partial per 8-element block)
+        } else if (!cg_den_fold_on(c)) {
+            HIPCHK(launch_den_fin(c, nbrick));  // (cg_den_fold: the update kernel takes the den step)
         }
         prof_mark(c, CDFEM_K_E2L, false);
     };
@@ -466,8 +523,10 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             prof_mark(c, CDFEM_K_UPDATE, true);
             HIPCHK(launch_cg_update_faces(c, x, r, q, dcur, dinv,
                                           mr && c->zlo_shared ? c->d_if[1] : nullptr,
-                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr, xfold));
-            if (mr) {
+                                          mr && c->zhi_shared ? c->d_if[3] : nullptr, mr && !mrfold, xfold));
+            if (mrfold) {
+                comm_allreduce(c, c->d_part + c->nblk, cg_den_fold_grid(c));  // the next apply sums them
+            } else if (mr) {
                 comm_allreduce(c, red + 1, 1);
                 HIPCHK(launch_update_step(c));
             }
@@ -885,6 +944,11 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
             // (k_e2l_box); element-major qdata and map are kept
             c->structured = true;
             c->epencil = c->nl < ((int64_t)1 << 32);
+            c->hb_nbx = (nx + kHoBrickEdge - 1) / kHoBrickEdge;
+            c->hb_nby = (ny + kHoBrickEdge - 1) / kHoBrickEdge;
+            c->hb_nbz = (nz + kHoBrickEdge - 1) / kHoBrickEdge;
+            c->hb_nblk = c->hb_nbx * c->hb_nby * c->hb_nbz;
+            dfree(c->d_face);  // the high-order brick CG's patch buffer: allocated by its first solve
             return CDFEM_OK;
         }
         c->nbx = (nx + kBrick - 1) / kBrick;
@@ -926,6 +990,7 @@ int cdfem_set_slab(cdfem_ctx *c, int zlo_shared, int zhi_shared)
         c->zhi_shared = zhi_shared != 0;
         const int64_t n = c->Lx * c->Ly;
         c->part_mode = 1;
+        c->mr_fold_checked = false;
         c->skip_lo = c->zlo_shared ? n : 0;  // the lower plane is owned by the rank below
         for (auto &b : c->d_if) {
             dfree(b);
@@ -1597,7 +1662,7 @@ int cdfem_solve(cdfem_ctx *c, const cdfem_solver_params *p, const double *B, dou
             c->perm_space = true;
         }
         if (p->method == CDFEM_CG) {
-            if (use_brick(c))
+            if (use_brick_cg(c))
                 solve_cg_brick(c, *p, dBs, dXs, *res);
             else
                 solve_cg(c, *p, dBs, dXs, *res);
@@ -1685,6 +1750,15 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "brick_byte_limit") {
             if (value < 1) throw ArgError("brick_byte_limit must be 1..2^31-1");
             c->brick_limit = value;
+        } else if (k == "cg_mr_fold") {
+            if (value != 0 && value != 1) throw ArgError("cg_mr_fold must be 0 or 1");
+            c->cg_mr_fold = value;
+        } else if (k == "ho_brick_mfma") {
+            if (value != 0 && value != 1) throw ArgError("ho_brick_mfma must be 0 or 1");
+            c->ho_brick_mfma = value;
+        } else if (k == "ho_brick") {
+            if (value != 0 && value != 1) throw ArgError("ho_brick must be 0 or 1");
+            c->ho_brick = value;
         } else if (k == "mr_overlap") {
             if (value < 0 || value > 1) throw ArgError("mr_overlap must be 0 or 1");
             c->mr_overlap = value;
@@ -1697,6 +1771,7 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "cg_den_fold") {
             if (value != 0 && (value < 64 || value > 16384)) throw ArgError("cg_den_fold must be 0 or 64..16384");
             c->cg_den_fold = value;
+            c->mr_fold_checked = false;
         } else if (k == "brick_upd_pb") {
             if (value != 0 && value != 1) throw ArgError("brick_upd_pb must be 0 or 1");
             c->brick_upd_pb = value;
@@ -1857,6 +1932,16 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
             return CDFEM_OK;
         }
         const double nq = nq_of(c, c->rule_op);
+        if (use_hobrick_cg(c) && (k == CDFEM_K_APPLY || k == CDFEM_K_UPDATE)) {
+            // the high-order brick CG: factors + gathered r, M^-1, d + ess flags + d (writer) + patch
+            // outputs (+ x read and written under the x-fold); update: r, M^-1, ess, r write + patches
+            const double S = brick_patch_side(c);
+            const double patches = 8.0 * S * S * S * (double)brick_count(c);
+            const bool xf = c->cg_xfold != 0;
+            *bytes = k == CDFEM_K_APPLY ? 8.0 * c->ncomp * ne + 33.0 * nl + patches + (xf ? 16.0 * nl : 0.0)
+                                        : (xf ? 25.0 : 49.0) * nl + patches;
+            return CDFEM_OK;
+        }
         if (use_brick(c)) {
             // CG-mode brick kernels (what the Krylov loop launches); see DESIGN.md section 4
             const int64_t s1 = (int64_t)kBrick * c->p;

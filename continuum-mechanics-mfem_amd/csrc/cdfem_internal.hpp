@@ -150,6 +150,12 @@ struct cdfem_ctx {
     bool epencil = false;               // qlay 1 on a structured box: pencil E-vector layout (ho_eidx)
     int sx = 0, sy = 0, sz = 0;         // elements per axis of the local box
     int nbx = 0, nby = 0, nbz = 0;      // bricks per axis
+    // 3D p = 3, 4 on a structured box: blocks of kHoBrickEdge^3 elements for the high-order brick CG
+    // (brick_kernels.hip k_hobrick_cg; set_option "ho_brick")
+    int hb_nbx = 0, hb_nby = 0, hb_nbz = 0, hb_nblk = 0;
+    int ho_brick = 0;                   // set_option "ho_brick": high-order CG through k_hobrick_cg + the brick update
+    double *d_hbpart = nullptr;         // k_hobrick_cg's den partials (one per block; two-stage sum)
+    int ho_brick_mfma = 0;              // set_option "ho_brick_mfma": its x stage on v_mfma_f64_16x16x4_f64 (kinds 7)
     int64_t Lx = 0, Ly = 0, Lz = 0;     // dof lattice per axis
     double *d_face = nullptr;           // [nblk][F] brick-face partial sums
     double *d_ones = nullptr;           // all-ones vector (unpreconditioned brick CG)
@@ -225,6 +231,10 @@ struct cdfem_ctx {
     hipEvent_t ov_ev[2] = {};           // fork / join of the side stream
     int brick_mult_pb = 1;              // set_option "brick_mult_pb": structured Mult through the patch buffer
     int cg_beta_fold = 1;               // set_option "cg_beta_fold": brick CG betanom step in the next apply
+    int cg_mr_fold = 1;                 // set_option "cg_mr_fold": both folds on several ranks (partials all-reduced)
+    bool mr_fold_checked = false, mr_fold_agree = false;  // every rank holds as many partials (checked once)
+    double mr_fold_key = 0.0;           //   for these local inputs (eligibility, counts)
+    double *d_small = nullptr;          // a few doubles of device scratch (mr_fold_agreed's all-reduce)
     int cg_den_fold = 1024;             // set_option "cg_den_fold": brick CG den step in the update (N workgroups; 0 off)
     int brick_upd_pb = 1;               // set_option "brick_upd_pb": predicated-load face sums in the brick CG update
     int ho_dfold = 1;                   // set_option "ho_dfold": CG direction folded into the Kronecker tile apply
@@ -334,7 +344,15 @@ bool apply_supported(int dim, int p);
 
 // ---- structured brick kernels (brick_kernels.hip) --------------------------------------------
 constexpr int kBrick = 4;               // elements per brick edge (4^3 = 64 = one wavefront)
+constexpr int kHoBrickEdge = 2;         // p = 3, 4: elements per block edge of the high-order brick CG
 bool brick_supported(int dim, int p);
+int brick_count(const cdfem_ctx *c);        // bricks (p <= 2) or high-order blocks (p = 3, 4)
+int brick_patch_side(const cdfem_ctx *c);   // S: 4p + 1 (p <= 2), 2p + 1 (p = 3, 4)
+bool cg_den_fold_on(const cdfem_ctx *c);
+bool cg_mr_fold(const cdfem_ctx *c);
+constexpr int kMrFoldMaxParts = 8192;   // cg_mr_fold: apply partials every update workgroup re-sums
+// the Kronecker tile's x-stage table (ho_kernels.hip), built for the context's p and rule
+hipError_t ho_ktab(cdfem_ctx *c, const double **out);
 // every buffer the brick kernels reach through a 32-bit buffer resource is below c->brick_limit bytes
 bool brick_fits(const cdfem_ctx *c);
 // y = A x (constrained: ess in -> 0, y[ess] = x[ess]); fused E->L through LDS + face partials
@@ -404,7 +422,7 @@ hipError_t launch_cg_init_nofin(cdfem_ctx *c, const double *B, double *x, double
 // pack the local partial sums of q on the shared interface planes into d_if[0] / d_if[2]
 hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q, hipStream_t s = nullptr);
 hipError_t launch_brick_cg2_split(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
-                                  double *d_new, double *q, hipStream_t s, double *x = nullptr);
+                                  double *d_new, double *q, hipStream_t s, double *x = nullptr, int bfkk = -1);
 
 // ---- bandwidth probes (stream_kernels.hip): mode 0 read 16 B/lane, 1 read 8 B/lane, 2 copy 16 B
 // full assembly on simplices (fa_kernels.hip)

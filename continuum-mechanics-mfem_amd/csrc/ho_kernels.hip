@@ -52,36 +52,7 @@ struct TileGeo {
 // that owns it (the highest element index along each axis).  That is exactly (d, q) with q the
 // constrained L-vector, so the E->L sum no longer has to precede the den step and can be fused
 // into the CG update (k_e2l_box<UPD>).
-typedef double v4d_t __attribute__((ext_vector_type(4)));
-
-// One block-wide GEMM on the matrix cores: out(row, col) = sum_k a(row, k) b(k, col) for
-// row < ROWS (the block's elements stacked), k < 4 KS, col < 16, as v_mfma_f64_16x16x4_f64 tiles of
-// 16 rows; the four waves of the block take row tiles round-robin.  a() and b() return 0 outside
-// the operator; o(row, col, v) stores (and drops padding columns).  Lane maps (MI355X f64 MFMA):
-// A[l & 15][k = l >> 4], B[k = l >> 4][l & 15], D[(l >> 4) + 4 r][l & 15].
-template <int ROWS, int KS, typename FA, typename FB, typename FO>
-__device__ __forceinline__ void block_mfma(const FA &a, const FB &b, const FO &o)
-{
-    constexpr int NTL = (ROWS + 15) / 16;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, kq = lane >> 4, col = lane & 15;
-    double bop[KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) bop[ks] = b(ks * 4 + kq, col);
-    for (int tt = wv; tt < NTL; tt += 4) {
-        const int rho = tt * 16 + col;
-        v4d_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const double av = rho < ROWS ? a(rho, ks * 4 + kq) : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bop[ks], acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = tt * 16 + kq + 4 * r;
-            if (row < ROWS) o(row, col, acc[r]);
-        }
-    }
-}
+// (v4d_t and block_mfma: pa_core.hpp)
 
 // The tile apply's LDS stages as block GEMMs (MF bit k = stage on the matrix cores):
 //   bit 0  stage x    [BX | GX](e dz dy, qx)      = X(e dz dy, dx) . [B | G]^T(dx, qx)
@@ -601,6 +572,46 @@ k_apply3d_ktile(const int32_t *__restrict__ map, const double *__restrict__ x, c
     }
 }
 
+// the x-stage rows of the Kronecker tile kernels (k_apply3d_ktile, brick_kernels.hip k_hobrick_cg):
+// canonical entries of make_tab's orbit averages, as tM / tK / tCacc read them, [M | K | C | Ct][i][j]
+template <int D1, int Q1>
+static hipError_t ktab_build(cdfem_ctx *c, const Tab<D1, Q1> &T)
+{
+    const int key = c->p * 64 + c->rule_op.q1;
+    if (c->ktab_key == key) return hipSuccess;
+    // (a rebuild follows a new setup: let any copy still reading h_ktab finish first)
+    const hipError_t es = hipStreamSynchronize(c->stream);
+    if (es != hipSuccess) return es;
+    if (!c->d_ktab) {
+        const hipError_t e = hipMalloc(&c->d_ktab, sizeof(c->h_ktab));
+        if (e != hipSuccess) return e;
+    }
+    for (int i = 0; i < D1; ++i)
+        for (int j = 0; j < D1; ++j) {
+            const int m = sym_can(D1, i, j), ca = anti_can(D1, i, j), sa = anti_sign(D1, i, j);
+            const int cb = anti_can(D1, j, i), sb = anti_sign(D1, j, i);
+            c->h_ktab[(0 * D1 + i) * D1 + j] = T.M1[m / D1][m % D1];
+            c->h_ktab[(1 * D1 + i) * D1 + j] = T.K1[m / D1][m % D1];
+            c->h_ktab[(2 * D1 + i) * D1 + j] = sa == 0 ? 0.0 : sa * T.C1[ca / D1][ca % D1];
+            c->h_ktab[(3 * D1 + i) * D1 + j] = sb == 0 ? 0.0 : sb * T.C1[cb / D1][cb % D1];
+        }
+    const hipError_t e = hipMemcpyAsync(c->d_ktab, c->h_ktab, sizeof(double) * 4 * D1 * D1, hipMemcpyHostToDevice,
+                                        c->stream);
+    if (e != hipSuccess) return e;
+    c->ktab_key = key;
+    return hipSuccess;
+}
+
+hipError_t ho_ktab(cdfem_ctx *c, const double **out)
+{
+    const int q1 = c->rule_op.q1;
+    hipError_t e = hipErrorInvalidValue;
+    if (c->p == 3 && q1 == 5) e = ktab_build<4, 5>(c, make_tab<4, 5>(c->rule_op));
+    if (c->p == 4 && q1 == 6) e = ktab_build<5, 6>(c, make_tab<5, 6>(c->rule_op));
+    *out = c->d_ktab;
+    return e;
+}
+
 template <int D1, int Q1, unsigned K>
 static hipError_t ktile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool con, const KrylovState *st,
                               double *den_part, const double *dold = nullptr, double *dnew = nullptr)
@@ -616,29 +627,9 @@ static hipError_t ktile_kinds(cdfem_ctx *c, const double *x, double *Ye, bool co
     geo.ess = c->d_ess;
     const double *qa = c->d_qaff;
     double *const np = nullptr;
-    // the x-stage rows (canonical entries of make_tab's orbit averages, as tM / tK / tCacc read them)
-    const int key = c->p * 64 + c->rule_op.q1;
-    if (c->ktab_key != key) {
-        // (a rebuild follows a new setup: let any copy still reading h_ktab finish first)
-        const hipError_t es = hipStreamSynchronize(c->stream);
-        if (es != hipSuccess) return es;
-        if (!c->d_ktab) {
-            const hipError_t e = hipMalloc(&c->d_ktab, sizeof(c->h_ktab));
-            if (e != hipSuccess) return e;
-        }
-        for (int i = 0; i < D1; ++i)
-            for (int j = 0; j < D1; ++j) {
-                const int m = sym_can(D1, i, j), ca = anti_can(D1, i, j), sa = anti_sign(D1, i, j);
-                const int cb = anti_can(D1, j, i), sb = anti_sign(D1, j, i);
-                c->h_ktab[(0 * D1 + i) * D1 + j] = T.M1[m / D1][m % D1];
-                c->h_ktab[(1 * D1 + i) * D1 + j] = T.K1[m / D1][m % D1];
-                c->h_ktab[(2 * D1 + i) * D1 + j] = sa == 0 ? 0.0 : sa * T.C1[ca / D1][ca % D1];
-                c->h_ktab[(3 * D1 + i) * D1 + j] = sb == 0 ? 0.0 : sb * T.C1[cb / D1][cb % D1];
-            }
-        const hipError_t e = hipMemcpyAsync(c->d_ktab, c->h_ktab, sizeof(double) * 4 * D1 * D1,
-                                            hipMemcpyHostToDevice, c->stream);
+    {
+        const hipError_t e = ktab_build<D1, Q1>(c, T);
         if (e != hipSuccess) return e;
-        c->ktab_key = key;
     }
     const double *kt = c->d_ktab;
     if (kt == nullptr) return hipErrorInvalidValue;

@@ -499,6 +499,37 @@ __device__ __forceinline__ void elem_apply3d_af(const XL &xl, const double *__re
     else elem_apply3d<D1, Q1, K, XL, Q1, AF == 1>(xl, q0, lane, T, Y);
 }
 
+typedef double v4d_t __attribute__((ext_vector_type(4)));
+
+// One block-wide GEMM on the matrix cores: out(row, col) = sum_k a(row, k) b(k, col) for
+// row < ROWS (the block's elements stacked), k < 4 KS, col < 16, as v_mfma_f64_16x16x4_f64 tiles of
+// 16 rows; the four waves of the block take row tiles round-robin.  a() and b() return 0 outside
+// the operator; o(row, col, v) stores (and drops padding columns).  Lane maps (MI355X f64 MFMA):
+// A[l & 15][k = l >> 4], B[k = l >> 4][l & 15], D[(l >> 4) + 4 r][l & 15].
+template <int ROWS, int KS, typename FA, typename FB, typename FO>
+__device__ __forceinline__ void block_mfma(const FA &a, const FB &b, const FO &o)
+{
+    constexpr int NTL = (ROWS + 15) / 16;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, kq = lane >> 4, col = lane & 15;
+    double bop[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) bop[ks] = b(ks * 4 + kq, col);
+    for (int tt = wv; tt < NTL; tt += 4) {
+        const int rho = tt * 16 + col;
+        v4d_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const double av = rho < ROWS ? a(rho, ks * 4 + kq) : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bop[ks], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = tt * 16 + kq + 4 * r;
+            if (row < ROWS) o(row, col, acc[r]);
+        }
+    }
+}
+
 // exact unsigned division by a run-time divisor: n / d == (n * m) >> k for n < 2^31
 struct FastDiv {
     uint64_t m;

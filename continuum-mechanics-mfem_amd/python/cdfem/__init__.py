@@ -638,6 +638,28 @@ class Context:
         self._chk(self.L.cdfem_comm_init_host(self.h, rank, world, self._cb[0], self._cb[1], None))
         self._chk(self.L.cdfem_comm_set_host_nbr_exchange(self.h, self._cb[2], None))
 
+    def comm_init_host(self, rank, world, allreduce, exchange):
+        """Host-callback communicator from two Python functions (numpy views of the staging buffers):
+        allreduce(a) sums the 1-D array a over the ranks in place; exchange(send_lo, recv_lo, send_hi,
+        recv_hi) swaps interface planes with the ranks below / above (None where there is no neighbour).
+        Used to run several ranks as threads of one process (tools/mr_kernel_list.py)."""
+        def ar(buf, n, _user):
+            try:
+                allreduce(np.ctypeslib.as_array(buf, shape=(n,)))
+                return 0
+            except Exception:  # errors must not unwind through C
+                return 1
+
+        def ex(send_lo, recv_lo, send_hi, recv_hi, n, _user):
+            try:
+                v = [np.ctypeslib.as_array(q, (n,)) if bool(q) else None for q in (send_lo, recv_lo, send_hi, recv_hi)]
+                exchange(*v)
+                return 0
+            except Exception:
+                return 1
+        self._cb = (ALLREDUCE_FN(ar), EXCHANGE_FN(ex))  # keep alive
+        self._chk(self.L.cdfem_comm_init_host(self.h, int(rank), int(world), self._cb[0], self._cb[1], None))
+
     def set_slab(self, zlo_shared, zhi_shared):
         self._chk(self.L.cdfem_set_slab(self.h, int(bool(zlo_shared)), int(bool(zhi_shared))))
 

@@ -252,6 +252,25 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *              fixed order; the one-block den finalizer is not launched (iterates agree with the
  *              finalizer path, 0, to rounding; C2: 62.4 against 64.6 us per iteration,
  *              profiles/r04/ab_c2_den_fold.json).
+ * "cg_mr_fold": 1 (default) — several ranks (slab partition, p <= 2, both folds on): the ranks
+ *              all-reduce the apply's den partials and the update's betanom partials as vectors, so the
+ *              update and the next apply take MFEM's den and betanom steps as on one rank (no sum or
+ *              step kernels between them); taken only when every rank holds as many partials (checked
+ *              once, collectively); 0 = per-rank sums, 8-byte all-reduces and step kernels.
+ * "ho_brick": 0 (default) — 1: the CG solve on a structured affine box at 3D p = 3, 4 (one rank,
+ *              Kronecker form) runs on blocks of 2^3 elements (k_hobrick_cg: the tile core, the
+ *              block's E->L in LDS, the patch buffer) and the brick update, instead of the tile apply's
+ *              E-vector and the flat E->L update.  Iterates agree to rounding; off by default: slower at C3
+ *              (4515 against 4259 us per iteration, profiles/r05/ab_c3_ho_brick.json).
+ * "ho_brick_mfma": 0 (default) — with ho_brick on the full operator (kinds 7): the x stage of the
+ *              block's eight elements as GEMMs on v_mfma_f64_16x16x4_f64 (rows = element rows, k = the
+ *              five input points padded to eight, columns = M, K, C, C^T per output point), staged to
+ *              the tile threads through LDS; the y and z stages stay on the VALU.  Same operator to
+ *              rounding; the north star's MFMA contraction, A/B'd in DESIGN.md 4.2.
+ * "brick_byte_limit": 2^31 (default) — the structured brick kernels address their vectors and patch
+ *              buffer with 32-bit buffer offsets (out-of-range marker 2^31), so a box whose 8 N_L or
+ *              8 S^3 bricks reach the limit runs the generic element kernels instead; lower values
+ *              force that fallback (tests).
  * "brick_upd_pb": 1 (default) — the brick CG update (k_cg_update_faces) reads each dof's 1-8 patch
  *              entries as eight predicated buffer loads (absent ones out of range) instead of
  *              branching on the face planes (0); bitwise the same sums.

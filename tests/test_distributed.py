@@ -242,6 +242,64 @@ def test_gpu_overlapped_exchange_bitwise(tmp_path, world):
         np.testing.assert_array_equal(x[0], x[2])
 
 
+def _gpu_mr_fold_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    import cdfem
+    dist = _init(rank, world, port)
+    n, per = 8, 12                       # 3 brick layers per rank: the overlapped form runs too
+    m = cdfem.box_mesh(3, (n, n, per * world), P, z_range=(rank * per, (rank + 1) * per))
+    ctx = cdfem.Context(0)
+    ctx.upload_mesh(m).set_structured(n, n, per)
+    ctx.comm_init_torch()
+    ctx.set_slab(rank > 0, rank < world - 1)
+    b = np.random.default_rng(400 + rank).uniform(-1, 1, m.nl)
+    res = {}
+    for kinds in (7, 5):
+        ctx.pa_setup(kinds=kinds, kappa=KAPPA, alpha=1.0, conv=CONV, mass=S)
+        _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+        for ov in (0, 1):
+            ctx.set_option("mr_overlap", ov)
+            for fold in (1, 0):
+                ctx.set_option("cg_mr_fold", fold)
+                X, info = ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=7)
+                res[f"fixed_k{kinds}_ov{ov}_f{fold}"] = (X, info["iterations"], info["converged"])
+                if kinds == 5:
+                    X, info = ctx.solve(B, method="cg", pc="jacobi", rel_tol=1e-9, max_iter=2000, check_every=5)
+                    res[f"conv_k{kinds}_ov{ov}_f{fold}"] = (X, info["iterations"], info["converged"])
+    np.savez(os.path.join(out_dir, f"mrf{rank}.npz"), **{k: v[0] for k, v in res.items()},
+             **{k + "_its": np.array([v[1], v[2]]) for k, v in res.items()})
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_mr_fold_matches_step_kernels(tmp_path, world):
+    """cg_mr_fold (default on several ranks): the ranks all-reduce the apply's den partials and the
+    update's betanom partials as vectors and both scalar steps run inside the kernels, as on one rank
+    (the per-iteration kernels are the one-rank pair plus the plane pack: tools/mr_kernel_list.py).
+    Against the finalizer path (sum kernel, 8-byte all-reduce, step kernel): the scalars are summed in
+    another order, so 40 fixed iterates agree to 1e-12 and a converging SPD solve stops on the same
+    iteration; one-launch and overlapped applies, end ranks and (world 3) a middle rank."""
+    mp.start_processes(_gpu_mr_fold_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    for r in range(world):
+        d = np.load(tmp_path / f"mrf{r}.npz")
+        for kinds in (7, 5):
+            for ov in (0, 1):
+                for what in ("fixed", "conv") if kinds == 5 else ("fixed",):
+                    a, b_ = d[f"{what}_k{kinds}_ov{ov}_f1"], d[f"{what}_k{kinds}_ov{ov}_f0"]
+                    ia, ib = d[f"{what}_k{kinds}_ov{ov}_f1_its"], d[f"{what}_k{kinds}_ov{ov}_f0_its"]
+                    assert ia[0] == ib[0] and ia[1] == ib[1], (r, kinds, ov, what)
+                    if what == "fixed":
+                        assert ia[0] == 40
+                    assert np.linalg.norm(a - b_) <= 1e-12 * np.linalg.norm(b_), (r, kinds, ov, what)
+            # the overlapped fold equals the one-launch fold bitwise (same kernels, same sums)
+            np.testing.assert_array_equal(d[f"fixed_k{kinds}_ov1_f1"], d[f"fixed_k{kinds}_ov0_f1"])
+
+
 # ---------------------------------------------------------------------------------------------
 # GMRES(m) + left Jacobi (PETSc KSPGMRES semantics, Input/petsc.opts:2-6) on the slab partition,
 # full convection-diffusion-reaction operator (nonsymmetric).  The distributed restatement below

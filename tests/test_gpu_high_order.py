@@ -353,8 +353,9 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
             gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
             _, B = gpu_ctx.form_linear_system(u, b)
             xg, ig = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=50, check_every=7)
+            nb = gpu_ctx.kernel_bytes(cdfem.K_APPLY)  # (the tile apply's; the block CG, ho_brick, reports its own)
             out[aff] = dict(y=gpu_ctx.mult(x), yc=gpu_ctx.mult(x, constrained=True), dg=gpu_ctx.diagonal(),
-                            bytes=gpu_ctx.kernel_bytes(cdfem.K_APPLY), x=xg, it=ig["iterations"])
+                            bytes=nb, x=xg, it=ig["iterations"])
     finally:
         gpu_ctx.set_option("pa_affine", 2)
     yo = A.mult(x)
@@ -369,3 +370,104 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
             assert np.linalg.norm(out[aff]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
 
 
+
+
+@pytest.mark.parametrize("shape,p,kinds", [((4, 4, 4), 4, 7), ((5, 3, 6), 4, 5), ((3, 4, 5), 3, 7), ((4, 5, 3), 3, 3),
+                                           ((2, 2, 2), 4, 6), ((1, 3, 2), 4, 7)])
+def test_ho_brick_cg_parity(gpu_ctx, shape, p, kinds):
+    """ho_brick (off by default: slower at C3): the high-order CG on an affine structured box through k_hobrick_cg (the
+    Kronecker tile core on 2^3-element blocks, the block's E->L in LDS, the patch buffer) and the brick
+    update, instead of the tile apply's E-vector and the flat E->L update.  Boxes with partial blocks
+    in every direction and non-zero essential values: 40 fixed Jacobi-CG iterates against the oracle
+    (1e-11) and the tile path (1e-12); a converging SPD solve stops on the tile path's iteration with
+    its solution (1e-10); bitwise repeatable; the byte count shows the block path ran."""
+    om = O.BoxMesh(3, shape, p)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(kinds))
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    rng = np.random.default_rng(23)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
+    out, conv, nbytes = {}, {}, {}
+    try:
+        for hb in (1, 0):
+            gpu_ctx.set_option("ho_brick", hb)
+            gpu_ctx.upload_mesh(gm).set_structured(*shape)
+            gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            nbytes[hb] = gpu_ctx.kernel_bytes(cdfem.K_UPDATE)
+            _, B = gpu_ctx.form_linear_system(u, b)
+            out[hb] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=7)
+            if hb:
+                again = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40)
+                np.testing.assert_array_equal(again[0], out[hb][0])
+            if kinds == 5:
+                conv[hb] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=1e-10, max_iter=2000, check_every=9)
+    finally:
+        gpu_ctx.set_option("ho_brick", 0)
+    assert nbytes[1] != nbytes[0]
+    for hb, (xg, ig) in out.items():
+        assert ig["iterations"] == 40
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), hb
+    assert np.linalg.norm(out[1][0] - out[0][0]) <= 1e-12 * np.linalg.norm(out[0][0])
+    if conv:
+        assert conv[1][1]["converged"] and conv[1][1]["iterations"] == conv[0][1]["iterations"]
+        assert np.linalg.norm(conv[1][0] - conv[0][0]) <= 1e-10 * np.linalg.norm(conv[0][0])
+
+
+def test_ho_brick_c3_full_size_residual(gpu_ctx):
+    """C3 itself (128^3 p = 4, 135 M DoFs) through the block CG: 20 Jacobi-CG iterations on the full
+    operator, then the recomputed constrained residual equals the recursive one and the iterates
+    equal the tile path's (the E->L sums differ in order only: 1e-12)."""
+    n, p = 128, 4
+    gm = cdfem.box_mesh(3, n, p, with_coords=False)
+    b = np.random.default_rng(20261015).uniform(-1, 1, gm.nl)
+    out = {}
+    try:
+        for hb in (1, 0):
+            gpu_ctx.set_option("ho_brick", hb)
+            gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+            gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            _, B = gpu_ctx.form_linear_system(np.zeros(gm.nl), b)
+            out[hb] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=20)
+    finally:
+        gpu_ctx.set_option("ho_brick", 0)
+    assert out[1][1]["iterations"] == out[0][1]["iterations"] == 20
+    assert np.linalg.norm(out[1][0] - out[0][0]) <= 1e-12 * np.linalg.norm(out[0][0])
+    assert abs(out[1][1]["final_norm"] - out[0][1]["final_norm"]) <= 1e-10 * out[0][1]["initial_norm"]
+
+
+@pytest.mark.parametrize("shape,p", [((4, 4, 4), 4), ((3, 5, 4), 3), ((5, 3, 3), 4)])
+def test_ho_brick_mfma_parity(gpu_ctx, shape, p):
+    """ho_brick_mfma: the block CG's x stage as block GEMMs on v_mfma_f64_16x16x4_f64 (the north star's
+    MFMA contraction), the full operator (kinds 7) with non-zero essential values: 40 fixed Jacobi-CG
+    iterates against the oracle (1e-11) and against the VALU x stage (1e-12), bitwise repeatable."""
+    om = O.BoxMesh(3, shape, p)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(7))
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    rng = np.random.default_rng(29)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
+    out = {}
+    try:
+        gpu_ctx.set_option("ho_brick", 1)
+        for mf in (1, 0):
+            gpu_ctx.set_option("ho_brick_mfma", mf)
+            gpu_ctx.upload_mesh(gm).set_structured(*shape)
+            gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            _, B = gpu_ctx.form_linear_system(u, b)
+            out[mf] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40)
+            if mf:
+                again = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40)
+                np.testing.assert_array_equal(again[0], out[mf][0])
+    finally:
+        gpu_ctx.set_option("ho_brick_mfma", 0)
+        gpu_ctx.set_option("ho_brick", 0)
+    for mf, (xg, ig) in out.items():
+        assert ig["iterations"] == 40
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), mf
+    assert np.linalg.norm(out[1][0] - out[0][0]) <= 1e-12 * np.linalg.norm(out[0][0])

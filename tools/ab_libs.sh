@@ -10,13 +10,14 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 CMD=${1:?command}
 PAIRS=${2:-2}
+VARIANTS=${VARIANTS:-"a b"}   # abtmp/<v>.so for each v, interleaved; the last one is left installed
 LIB=continuum-mechanics-mfem_amd/lib/libcdfem.so
 mkdir -p gpurun_out
 for k in $(seq 1 "$PAIRS"); do
-  for v in a b; do
+  for v in $VARIANTS; do
     cp "abtmp/$v.so" "$LIB" || exit 1
     timeout -k 10 300 $CMD > "gpurun_out/ab_${v}_$k.log" 2>&1 || exit $?
-    echo "$v $k: $(grep -hE '"(iter_us|spmv_us|orth_us)"' "gpurun_out/ab_${v}_$k.log" | tr -d ' \n')"
+    echo "$v $k: $(grep -hE '"(iter_us|it_us|apply_us|upd_us|spmv_us|orth_us)"' "gpurun_out/ab_${v}_$k.log" | tr -d ' \n')"
   done
 done
-cp abtmp/b.so "$LIB"
+cp "abtmp/${VARIANTS##* }.so" "$LIB"
