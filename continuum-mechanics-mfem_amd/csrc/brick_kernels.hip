@@ -118,6 +118,17 @@ __device__ __forceinline__ size_t patch_idx(const BrickGeom &g, int bx, int by, 
     return ((((size_t)bz * S + pz) * g.nby + by) * S + py) * ((size_t)g.nbx * S) + (size_t)bx * S + px;
 }
 
+// f(std::integral_constant<int, k>) for k = B .. E - 1, unrolled at compile time (array indices
+// stay compile-time, so the arrays stay in registers)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F &&f)
+{
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 // v unchanged, but opaque to the optimiser: index arithmetic that depends on it cannot be hoisted
 // above this point (LLVM otherwise computes a later phase's per-position indices at kernel entry
 // and spills them across the element apply)
@@ -592,12 +603,10 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     constexpr int NPL = 16;  // BF: partials per lane (nupart <= 64 NPL)
     double pv[NPL];
     if constexpr (BF) {
-        if (kk > 0) {
+        if (kk > 0) {  // (buffer loads: past nupart they read 0, no branch per load)
+            const auto bu = brsrc(upart, 8u * (uint32_t)nupart);
 #pragma unroll
-            for (int i = 0; i < NPL; ++i) {
-                const int j = (int)threadIdx.x + 64 * i;
-                pv[i] = j < nupart ? upart[j] : 0.0;
-            }
+            for (int i = 0; i < NPL; ++i) pv[i] = bload(bu, 8u * ((uint32_t)threadIdx.x + 64u * i));
         }
     }
     // x-fold (XF, set_option "cg_xfold"): the previous iteration's x += alpha d_old, for the dofs
@@ -640,8 +649,12 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     constexpr uint32_t wdx = 64 % S, wdy = (64 / S) % S, wdz = 64 / (S * S);
     const uint32_t dgid = wdx + wdy * uLx + wdz * uLxy, cxd = uLx - S, cyd = uLxy - S * uLx;
     LatWalk<S> pw0(t, (uint32_t)gx0 + uLx * (uint32_t)gy0 + uLxy * (uint32_t)gz0, uLx, uLxy);
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
+    // W >= 3 waves per SIMD: the patch is gathered and formed in two halves, so only half of its
+    // loads are in registers at once (round 5: the gather is not the register peak, the Kronecker
+    // core is; at 168 registers the kernel still spills 22, so the default stays at 2 waves)
+    constexpr int NG = W >= 3 ? 2 : 1, GK = (NI + NG - 1) / NG;
+    auto gather = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
         const unsigned i = t + 64 * k;
         const int px = pw0.x, py = pw0.y, pz = pw0.z;
         const uint32_t gid = pw0.gid;
@@ -657,12 +670,30 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         woffv[k] = writer ? off : kOOB;
         dbits |= (uint32_t)(writer && !(zlo_shared && gz == 0)) << k;
         if constexpr (XF) xv[k] = bload(bxf, woffv[k]);
-    }
+    };
+    auto form = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const unsigned i = t + 64 * k;
+        if (k == NI - 1 && i >= S3) return;
+        const double dn = mv[k] * rv[k] + beta * ov[k];  // 0 outside the lattice
+        const bool e = ev[k] != 0;
+        bstore(bd, woffv[k], dn);
+        if constexpr (XF) bstore(bxf, woffv[k], xv[k] + alpha_prev * ov[k]);
+        // (A_c d)_i = d_i on ess dofs
+        den += (e && ((dbits >> k) & 1u)) ? dn * dn : 0.0;
+        s_in[i] = e ? 0.0 : dn;
+        s_out[i] = 0.0;
+        if constexpr (EP) {  // (unconditional: a predicated LDS store compiles to a branch per position)
+            ebits |= (uint32_t)e << k;
+            s_d[i] = ((dbits >> k) & 1u) ? dn : 0.0;
+        }
+    };
+    static_for<0, GK>(gather);
     if constexpr (BF) {
         if (kk > 0) {
             double v = 0.0;
 #pragma unroll
-            for (int i = 0; i < NPL; ++i) v += pv[i];
+            for (int q = 0; q < NPL; ++q) v += pv[q];
             const double B = wave_sum(v);
             // cg_update_logic's decision (cg_stop_kind), taken identically by every workgroup at the
             // host's update count kk; workgroup 0 records it at the same kk
@@ -677,22 +708,10 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
             beta = B / st->nom;
         }
     }
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const unsigned i = t + 64 * k;
-        if (k == NI - 1 && i >= S3) break;
-        const double dn = mv[k] * rv[k] + beta * ov[k];  // 0 outside the lattice
-        const bool e = ev[k] != 0;
-        bstore(bd, woffv[k], dn);
-        if constexpr (XF) bstore(bxf, woffv[k], xv[k] + alpha_prev * ov[k]);
-        // (A_c d)_i = d_i on ess dofs
-        den += (e && ((dbits >> k) & 1u)) ? dn * dn : 0.0;
-        s_in[i] = e ? 0.0 : dn;
-        s_out[i] = 0.0;
-        if constexpr (EP) {  // (unconditional: a predicated LDS store compiles to a branch per position)
-            ebits |= (uint32_t)e << k;
-            s_d[i] = ((dbits >> k) & 1u) ? dn : 0.0;
-        }
+    static_for<0, GK>(form);
+    if constexpr (NG == 2) {
+        static_for<GK, NI>(gather);
+        static_for<GK, NI>(form);
     }
     __syncthreads();
 
@@ -755,7 +774,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
     constexpr int s1 = S - 1;
     __shared__ double sh[kRedThreads / 64 + 1];
     if (st->done) return;
-    double alpha;
+    double alpha = 0.0;
     if constexpr (DS) {
         // (16 loads per thread in flight at once: the apply's 4096 partials in one round trip)
         const double den = sum_partials_all<16>(apart, napart, sh);
@@ -781,7 +800,10 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
     if constexpr (EP) {
         // the apply's essential-row patch entries (EP in k_brick_cg): q is the sum of the row's 1-8
         // entries everywhere (with the neighbour's plane sums on a slab), so the loop reads r, M^-1 and
-        // the patch only, every load independent of the others (no essential flag, no d)
+        // the patch only, every load independent of the others (no essential flag, no d).  Measured and
+        // not kept (profiles/r05/ab_c2_update_pipe.json): the loop software-pipelined with the den sum
+        // under the first loads (59.2-59.4 against 59.05 us per iteration) and two dofs per pass (62.5
+        // against 59.8)
         static_assert(PB, "EP reads the patch buffer with the predicated loads");
         const auto bp = brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S));
         for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += gridDim.x * blockDim.x) {
@@ -880,7 +902,7 @@ constexpr int kHoBrick = kHoBrickEdge;  // elements per block edge (high order)
 // north star's "MFMA for the per-element B^T D B contraction at high order", A/B'd against the VALU
 // x stage.
 template <int D1, int Q1, unsigned K, bool XF, bool MF = false>
-__global__ void __launch_bounds__(((kHoBrick * kHoBrick * kHoBrick * D1 * D1 + 63) / 64) * 64, 2)
+__global__ void __launch_bounds__(((kHoBrick * kHoBrick * kHoBrick * D1 * D1 + 63) / 64) * 64, 4)
 k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, const double *__restrict__ d_old,
              double *__restrict__ d_new, double *__restrict__ face, const double *__restrict__ qaff,
              const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g, int nex, int ney, int nez,
@@ -893,7 +915,10 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
     constexpr int NT = ((NEB * DD + 63) / 64) * 64, NI = (S3 + NT - 1) / NT;
     __shared__ double s_in[S3];
     __shared__ double sP[NEB][4][ND];  // [element][grp][jz][iy][ix]
-    __shared__ double sE[NEB][ND];     // element outputs Y [dz][dy][dx]
+    // element outputs Y [dz][dy][dx], in place of group 0 of the element's y-stage output: thread (a, bb)
+    // reads all its groups' (jz, bb, a) entries before it writes its Y at (dz, bb, a), and no other
+    // thread reads or writes those (8 KB less LDS: four blocks per CU)
+    auto sE = [&](int e8, int idx) -> double & { return sP[e8][0][idx]; };
     __shared__ double shd[NT / 64];
     if (st->done) return;
     const double beta = st->beta;
@@ -979,11 +1004,14 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
             return k < D1 ? s_in[ob + jz * S2 + jy * S + k] : 0.0;
         };
         auto bcol = [&](int k, int col) { return (k < D1 && col < NCOL) ? ktab[col * D1 + k] : 0.0; };
-        block_mfma<NR, (D1 + 3) / 4>(arow, bcol, [&](int row, int col, double v) { xs[row * NCOL + col] = v; });
-        block_mfma<NR, (D1 + 3) / 4>(arow, [&](int k, int col) { return bcol(k, 16 + col); },
-                                     [&](int row, int col, double v) {
-                                         if (16 + col < NCOL) xs[row * NCOL + 16 + col] = v;
-                                     });
+        auto o16 = [&](int row, int col, double v) { xs[row * NCOL + col] = v; };
+        auto b16 = [&](int k, int col) { return bcol(k, 16 + col); };
+        auto o4 = [&](int row, int col, double v) {
+            if (16 + col < NCOL) xs[row * NCOL + 16 + col] = v;
+        };
+        block_mfma<NR, (D1 + 3) / 4, decltype(arow), decltype(bcol), decltype(o16), NT / 64>(arow, bcol, o16);
+        if constexpr (NCOL > 16)  // (p = 4: C^T's last 4 columns; p = 3 fits one 16-column GEMM)
+            block_mfma<NR, (D1 + 3) / 4, decltype(arow), decltype(b16), decltype(o4), NT / 64>(arow, b16, o4);
         __syncthreads();
         if (tile) {
 #pragma unroll
@@ -1046,7 +1074,7 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
         for (int dz = 0; dz < D1; ++dz) {
             const double y = valid ? Yz[dz] : 0.0;
             den += s_in[o0 + dz * S2 + bb * S + a] * y;
-            sE[le][(dz * D1 + bb) * D1 + a] = y;
+            sE(le, (dz * D1 + bb) * D1 + a) = y;
         }
     }
     __syncthreads();
@@ -1074,7 +1102,7 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
                 const int cx = c & 1, cy = (c >> 1) & 1, cz = c >> 2;
                 const bool ok = (cx ? hx1 : hx0) && (cy ? hy1 : hy0) && (cz ? hz1 : hz0);
                 const int lx = cx ? x1 : x0, ly = cy ? y1 : y0, lz = cz ? z1 : z0;
-                const double t = sE[cx + 2 * cy + 4 * cz][ok ? (lz * D1 + ly) * D1 + lx : 0];
+                const double t = sE(cx + 2 * cy + 4 * cz, ok ? (lz * D1 + ly) * D1 + lx : 0);
                 sum += ok ? t : 0.0;
             }
             bstore(bp, 8u * (base + (uint32_t)pw.z * A + (uint32_t)pw.y * R + (uint32_t)pw.x), sum);
@@ -1106,14 +1134,15 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
     const double *qd = c->d_qaff ? c->d_qaff : c->d_qd;
     const double *upart = c->d_part + c->nblk;  // the den-fold update's partials
+    double *const dpart = c->den_out ? c->den_out : c->d_part;  // the apply's den partials
 #define CDFEM_BCG5(AFF_, W_, XF_, BF_, FU_)                                                                 \
     if (whole)                                                                                               \
         CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_>), grid, block, 0, r, dinv, d_old, d_new, q, \
-                     c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x, upart, run.nupart, \
+                     c->d_face, qd, c->d_ess, T, g, c->zlo_shared, dpart, c->d_state, x, upart, run.nupart,     \
                      run.kk);                                                                                \
     else                                                                                                     \
         hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_>), grid, block, 0, run.s, r, dinv,     \
-                           d_old, d_new, q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, c->d_part, c->d_state, x, \
+                           d_old, d_new, q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, dpart, c->d_state, x, \
                            upart, run.nupart, run.kk)
 #define CDFEM_BCG4(AFF_, W_, XF_, BF_)                                                                      \
     if (full) { CDFEM_BCG5(AFF_, W_, XF_, BF_, true); } else { CDFEM_BCG5(AFF_, W_, XF_, BF_, false); }
@@ -1228,7 +1257,8 @@ int cg_den_fold_grid(const cdfem_ctx *c)
 // update's <= 1024)
 static bool cg_folds_fit(const cdfem_ctx *c)
 {
-    return c->cg_den_fold != 0 && c->cg_beta_fold != 0 && c->p <= 2 && pa_af(c) == 2 && cg_den_fold_grid(c) <= 1024;
+    return c->cg_den_fold != 0 && c->cg_beta_fold != 0 && c->p <= 2 && pa_af(c) == 2 && cg_den_fold_grid(c) <= 1024 &&
+           brick_count(c) <= kDenFoldMaxParts;
 }
 
 // several ranks (set_option "cg_mr_fold"): the ranks all-reduce the apply's den partials and the
@@ -1249,7 +1279,7 @@ bool cg_beta_fold_ok(const cdfem_ctx *c)
 // 64-element brick; the high-order blocks leave too many partials and keep the finalizer)
 bool cg_den_fold_on(const cdfem_ctx *c)
 {
-    return c->cg_den_fold != 0 && c->p <= 2 && (!multi_rank(c) || cg_mr_fold(c));
+    return c->cg_den_fold != 0 && c->p <= 2 && brick_count(c) <= kDenFoldMaxParts && (!multi_rank(c) || cg_mr_fold(c));
 }
 
 // the first and last brick layers (the shared planes' partial sums) on stream s, the interior

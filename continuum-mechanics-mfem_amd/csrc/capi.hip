@@ -431,7 +431,15 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
         const int S = brick_patch_side(c);
         c->d_face = dalloc<double>((size_t)nbrick * S * S * S);
     }
-    if (c->p >= 3 && !c->d_hbpart) c->d_hbpart = dalloc<double>(nbrick);
+    // the apply's den partials in two stages (a block per 1/256 of them, then one block) when the one
+    // block finalizer would sum too many: the p = 3, 4 blocks, and one rank past the den fold's bound
+    const bool two_stage = c->p >= 3 || (!multi_rank(c) && nbrick > kDenFoldMaxParts);
+    if (two_stage && !c->d_hbpart) c->d_hbpart = dalloc<double>(nbrick);
+    c->den_out = two_stage && c->p <= 2 ? c->d_hbpart : nullptr;
+    struct DenOutReset {
+        cdfem_ctx *c;
+        ~DenOutReset() { c->den_out = nullptr; }
+    } den_out_reset{c};
     double *dprev = c->d_w[5], *dcur = c->d_dalt;
     const double *dinv;
     if (p.pc == CDFEM_PC_JACOBI) {
@@ -509,8 +517,8 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
                 HIPCHK(launch_fin_sum(c, nbrick, 0));
                 comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
             }
-        } else if (c->p >= 3) {
-            HIPCHK(launch_den_from_partials(c, c->d_hbpart, nbrick));  // (one partial per 8-element block)
+        } else if (two_stage) {
+            HIPCHK(launch_den_from_partials(c, c->d_hbpart, nbrick));  // (one partial per brick / block)
         } else if (!cg_den_fold_on(c)) {
             HIPCHK(launch_den_fin(c, nbrick));  // (cg_den_fold: the update kernel takes the den step)
         }

@@ -154,7 +154,9 @@ struct cdfem_ctx {
     // (brick_kernels.hip k_hobrick_cg; set_option "ho_brick")
     int hb_nbx = 0, hb_nby = 0, hb_nbz = 0, hb_nblk = 0;
     int ho_brick = 0;                   // set_option "ho_brick": high-order CG through k_hobrick_cg + the brick update
-    double *d_hbpart = nullptr;         // k_hobrick_cg's den partials (one per block; two-stage sum)
+    double *d_hbpart = nullptr;         // den partials summed in two stages: k_hobrick_cg's, and k_brick_cg's past
+                                        // kDenFoldMaxParts bricks on one rank (one per brick)
+    double *den_out = nullptr;          // k_brick_cg writes its den partials here instead of d_part (set by the solve)
     int ho_brick_mfma = 0;              // set_option "ho_brick_mfma": its x stage on v_mfma_f64_16x16x4_f64 (kinds 7)
     int64_t Lx = 0, Ly = 0, Lz = 0;     // dof lattice per axis
     double *d_face = nullptr;           // [nblk][F] brick-face partial sums
@@ -351,6 +353,8 @@ int brick_patch_side(const cdfem_ctx *c);   // S: 4p + 1 (p <= 2), 2p + 1 (p = 3
 bool cg_den_fold_on(const cdfem_ctx *c);
 bool cg_mr_fold(const cdfem_ctx *c);
 constexpr int kMrFoldMaxParts = 8192;   // cg_mr_fold: apply partials every update workgroup re-sums
+constexpr int kDenFoldMaxParts = 16384; // cg_den_fold: beyond (C5's 256^3 on one GPU: 262,144 bricks) the
+                                        // den finalizer (the update workgroups' redundant sums grow with it)
 // the Kronecker tile's x-stage table (ho_kernels.hip), built for the context's p and rule
 hipError_t ho_ktab(cdfem_ctx *c, const double **out);
 // every buffer the brick kernels reach through a 32-bit buffer resource is below c->brick_limit bytes

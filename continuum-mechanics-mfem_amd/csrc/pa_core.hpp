@@ -503,10 +503,10 @@ typedef double v4d_t __attribute__((ext_vector_type(4)));
 
 // One block-wide GEMM on the matrix cores: out(row, col) = sum_k a(row, k) b(k, col) for
 // row < ROWS (the block's elements stacked), k < 4 KS, col < 16, as v_mfma_f64_16x16x4_f64 tiles of
-// 16 rows; the four waves of the block take row tiles round-robin.  a() and b() return 0 outside
+// 16 rows; the NW waves of the block (4 by default) take row tiles round-robin.  a() and b() return 0 outside
 // the operator; o(row, col, v) stores (and drops padding columns).  Lane maps (MI355X f64 MFMA):
 // A[l & 15][k = l >> 4], B[k = l >> 4][l & 15], D[(l >> 4) + 4 r][l & 15].
-template <int ROWS, int KS, typename FA, typename FB, typename FO>
+template <int ROWS, int KS, typename FA, typename FB, typename FO, int NW = 4>
 __device__ __forceinline__ void block_mfma(const FA &a, const FB &b, const FO &o)
 {
     constexpr int NTL = (ROWS + 15) / 16;
@@ -514,7 +514,7 @@ __device__ __forceinline__ void block_mfma(const FA &a, const FB &b, const FO &o
     double bop[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) bop[ks] = b(ks * 4 + kq, col);
-    for (int tt = wv; tt < NTL; tt += 4) {
+    for (int tt = wv; tt < NTL; tt += NW) {  // (NW: the block's waves)
         const int rho = tt * 16 + col;
         v4d_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll

@@ -127,3 +127,27 @@ def test_c4_full_size_parity(gpu_ctx):
     xg, ig = gpu_ctx.solve(B, method="gmres", pc="jacobi", restart=30, rel_tol=0.0, abs_tol=0.0, max_iter=60)
     assert io["iterations"] == ig["iterations"] == 60
     assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
+
+
+def test_c5_one_gpu_folds_bounded(gpu_ctx):
+    """BASELINE configs[4]'s 256^3 p = 2 mesh on one GPU (262,144 bricks): past kDenFoldMaxParts
+    apply partials the den step goes back to the one-block finalizer, and with it the betanom step (the
+    two folds are taken together).  20 fixed Jacobi-CG iterates on the full operator equal the
+    finalizer path's (cg_den_fold 0) to rounding and give the same residual norm."""
+    n, p = 256, 2
+    gm = cdfem.box_mesh(3, n, p, with_coords=False)
+    b = np.random.default_rng(20261015).uniform(-1, 1, gm.nl)
+    out = {}
+    try:
+        for fold in (1024, 0):
+            gpu_ctx.set_option("cg_den_fold", fold)
+            gpu_ctx.upload_mesh(gm).set_structured(n, n, n)
+            gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            _, B = gpu_ctx.form_linear_system(np.zeros(gm.nl), b)
+            out[fold] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=20)
+    finally:
+        gpu_ctx.set_option("cg_den_fold", 1024)
+    (x1, i1), (x0, i0) = out[1024], out[0]
+    assert i1["iterations"] == i0["iterations"] == 20
+    assert np.linalg.norm(x1 - x0) <= 1e-12 * np.linalg.norm(x0)
+    assert abs(i1["final_norm"] - i0["final_norm"]) <= 1e-10 * i0["initial_norm"]
