@@ -86,6 +86,20 @@ def parse():
     return a
 
 
+def kernel_label(name, affine):
+    """The roofline kernel (cdfem_kernel_name: rocprof's name first) with what it does."""
+    what = {
+        "k_brick_cg": "brick patch gather + fused CG direction + D/C/M PA apply" +
+                      (", Kronecker form of the affine factors, x += alpha d folded in" if affine else "") +
+                      " + in-LDS E->L + d.Ad",
+        "k_hobrick_cg": "2^3-element blocks: patch gather + CG direction, D1 x D1 thread tile per element in the "
+                        "Kronecker form, in-LDS E->L, x += alpha d folded in",
+        "k_apply3d_ktile": "D1 x D1 thread tile per element, Kronecker form of the affine factors, CG direction folded in",
+        "k_apply3d_tile": "Q1 x Q1 thread tile per element, z planes in registers",
+        "k_apply3d": "fused L->E gather + D/C/M PA apply"}
+    return f"{name} ({what.get(name, 'PA apply')})"
+
+
 def kinds_label(kinds):
     """Integrator set of a kinds bit mask: 1 Diffusion, 2 Convection, 4 Mass (e.g. 7 -> D+C+M)."""
     return "+".join(n for b, n in ((1, "D"), (2, "C"), (4, "M")) if kinds & b)
@@ -645,14 +659,7 @@ def main():
             else:
                 roof = {"bound": "hbm", **hbm_view}
             roof.update({
-                    "kernel": (("k_brick_cg (brick patch gather + fused CG direction + D/C/M PA apply" +
-                                (", Kronecker form of the affine factors, x += alpha d folded in" if affine else "") +
-                                " + in-LDS E->L + d.Ad)") if args.path == "brick"
-                               else ("k_apply3d_ktile (D1 x D1 thread tile per element, Kronecker form of the affine "
-                                     "factors, CG direction folded in)" if affine else
-                                     "k_apply3d_tile (Q1 x Q1 thread tile per element, z planes in registers)")
-                               if args.order >= 3
-                               else "k_apply3d (fused L->E gather + D/C/M PA apply)"),
+                    "kernel": kernel_label(ctx.kernel_name(cdfem.K_APPLY), affine),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
                     "launches": cnt,
                     # what binds the kernel per its SQ counters (issue / memory / LDS), beside the closer roofline

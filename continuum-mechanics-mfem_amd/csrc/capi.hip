@@ -1864,15 +1864,19 @@ int cdfem_profile_read(cdfem_ctx *c, int k, double *total_ms, int64_t *count)
 }
 
 // name of the HIP kernel that kernel id runs as in the current configuration (rocprof's kernel
-// name without its template arguments); the assembled-operator apply only (the PA applies are named
-// by the bench from their path)
+// name without its template arguments): the apply of a CG solve (the roofline kernel of the bench)
 int cdfem_kernel_name(cdfem_ctx *c, int k, char *buf, size_t n)
 {
     return guarded(c, [&] {
         require_pa(c);
         if (!buf || n == 0) throw ArgError("buffer is null");
-        if (k != CDFEM_K_APPLY || !c->fa_ready) throw UnsupportedError("kernel names: the assembled-operator apply only");
-        std::snprintf(buf, n, "%s", c->lds_rows > 0 ? "k_sell_spmv_lds" : "k_sell_spmv");
+        if (k != CDFEM_K_APPLY) throw UnsupportedError("kernel names: the operator apply only");
+        const char *name = c->fa_ready ? (c->lds_rows > 0 ? "k_sell_spmv_lds" : "k_sell_spmv")
+                           : use_brick(c) ? "k_brick_cg"
+                           : use_hobrick_cg(c) ? "k_hobrick_cg"
+                           : c->qlay == 1 ? (tile_kron(c) ? "k_apply3d_ktile" : "k_apply3d_tile")
+                                          : "k_apply3d";
+        std::snprintf(buf, n, "%s", name);
         return CDFEM_OK;
     });
 }

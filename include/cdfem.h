@@ -257,11 +257,11 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *              update and the next apply take MFEM's den and betanom steps as on one rank (no sum or
  *              step kernels between them); taken only when every rank holds as many partials (checked
  *              once, collectively); 0 = per-rank sums, 8-byte all-reduces and step kernels.
- * "ho_brick": 0 (default) — 1: the CG solve on a structured affine box at 3D p = 3, 4 (one rank,
- *              Kronecker form) runs on blocks of 2^3 elements (k_hobrick_cg: the tile core, the
- *              block's E->L in LDS, the patch buffer) and the brick update, instead of the tile apply's
- *              E-vector and the flat E->L update.  Iterates agree to rounding; off by default: slower at C3
- *              (4515 against 4259 us per iteration, profiles/r05/ab_c3_ho_brick.json).
+ * "ho_brick": 1 (default) — the CG solve on a structured affine box at 3D p = 3, 4 (one rank,
+ *              Kronecker form) runs on blocks of 2^3 elements (k_hobrick_cg: the tile core, the block's
+ *              E->L in LDS, the 9^3 patch buffer of the p = 2 brick) and the brick update, instead of the
+ *              tile apply's E-vector and the flat E->L update (0).  Iterates agree to rounding; C3:
+ *              4114 against 4287 us per iteration (profiles/r05/ab_c3_ho_brick_occ4.json).
  * "ho_brick_mfma": 0 (default) — with ho_brick on the full operator (kinds 7): the x stage of the
  *              block's eight elements as GEMMs on v_mfma_f64_16x16x4_f64 (rows = element rows, k = the
  *              five input points padded to eight, columns = M, K, C, C^T per output point), staged to
@@ -357,7 +357,9 @@ int cdfem_kernel_bytes(cdfem_ctx *ctx, int kernel, double *bytes);
  * Kronecker-form element apply under pa_affine 2                                 */
 int cdfem_kernel_flops(cdfem_ctx *ctx, int kernel, double *flops);
 /* the HIP kernel name (without template arguments) kernel id runs as in the current configuration,
- * as rocprof reports it: the assembled-operator apply (CDFEM_K_APPLY after cdfem_fa_setup) only   */
+ * as rocprof reports it: the operator apply of a CG solve (CDFEM_K_APPLY) only — the SpMV after
+ * cdfem_fa_setup, else the partial-assembly apply of the path the context takes (brick CG, the
+ * high-order block CG, the tile applies, the element-block apply)                                  */
 int cdfem_kernel_name(cdfem_ctx *ctx, int kernel, char *buf, size_t n);
 
 /* ---- multi-GPU (element-partitioned z-slabs, one context per GPU / rank) ----------------------

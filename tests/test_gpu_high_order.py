@@ -180,6 +180,7 @@ def test_ho_dfold_matches_direction_pass(gpu_ctx, shape, p, kinds):
     xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
     out, conv = {}, {}
     try:
+        gpu_ctx.set_option("ho_brick", 0)  # the tile path's fused CG (the block CG has its own tests)
         for df in (1, 0):
             gpu_ctx.set_option("ho_dfold", df)
             gpu_ctx.upload_mesh(gm).set_structured(*shape)
@@ -189,6 +190,7 @@ def test_ho_dfold_matches_direction_pass(gpu_ctx, shape, p, kinds):
             conv[df] = gpu_ctx.solve(B, method="cg", rel_tol=1e-6, abs_tol=0.0, max_iter=400, check_every=16)
     finally:
         gpu_ctx.set_option("ho_dfold", 1)
+        gpu_ctx.set_option("ho_brick", 1)
     for df, (xg, ig) in out.items():
         assert ig["iterations"] == 40
         assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), df
@@ -353,7 +355,9 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
             gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
             _, B = gpu_ctx.form_linear_system(u, b)
             xg, ig = gpu_ctx.solve(B, method="cg", rel_tol=0.0, abs_tol=0.0, max_iter=50, check_every=7)
-            nb = gpu_ctx.kernel_bytes(cdfem.K_APPLY)  # (the tile apply's; the block CG, ho_brick, reports its own)
+            gpu_ctx.set_option("ho_brick", 0)  # the tile apply's bytes (the block CG reports its own)
+            nb = gpu_ctx.kernel_bytes(cdfem.K_APPLY)
+            gpu_ctx.set_option("ho_brick", 1)
             out[aff] = dict(y=gpu_ctx.mult(x), yc=gpu_ctx.mult(x, constrained=True), dg=gpu_ctx.diagonal(),
                             bytes=nb, x=xg, it=ig["iterations"])
     finally:
@@ -375,7 +379,7 @@ def test_ho_affine_factors(gpu_ctx, n, p, structured, kinds):
 @pytest.mark.parametrize("shape,p,kinds", [((4, 4, 4), 4, 7), ((5, 3, 6), 4, 5), ((3, 4, 5), 3, 7), ((4, 5, 3), 3, 3),
                                            ((2, 2, 2), 4, 6), ((1, 3, 2), 4, 7)])
 def test_ho_brick_cg_parity(gpu_ctx, shape, p, kinds):
-    """ho_brick (off by default: slower at C3): the high-order CG on an affine structured box through k_hobrick_cg (the
+    """ho_brick (default): the high-order CG on an affine structured box through k_hobrick_cg (the
     Kronecker tile core on 2^3-element blocks, the block's E->L in LDS, the patch buffer) and the brick
     update, instead of the tile apply's E-vector and the flat E->L update.  Boxes with partial blocks
     in every direction and non-zero essential values: 40 fixed Jacobi-CG iterates against the oracle
@@ -405,7 +409,7 @@ def test_ho_brick_cg_parity(gpu_ctx, shape, p, kinds):
             if kinds == 5:
                 conv[hb] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=1e-10, max_iter=2000, check_every=9)
     finally:
-        gpu_ctx.set_option("ho_brick", 0)
+        gpu_ctx.set_option("ho_brick", 1)
     assert nbytes[1] != nbytes[0]
     for hb, (xg, ig) in out.items():
         assert ig["iterations"] == 40
@@ -432,7 +436,7 @@ def test_ho_brick_c3_full_size_residual(gpu_ctx):
             _, B = gpu_ctx.form_linear_system(np.zeros(gm.nl), b)
             out[hb] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=20)
     finally:
-        gpu_ctx.set_option("ho_brick", 0)
+        gpu_ctx.set_option("ho_brick", 1)
     assert out[1][1]["iterations"] == out[0][1]["iterations"] == 20
     assert np.linalg.norm(out[1][0] - out[0][0]) <= 1e-12 * np.linalg.norm(out[0][0])
     assert abs(out[1][1]["final_norm"] - out[0][1]["final_norm"]) <= 1e-10 * out[0][1]["initial_norm"]
@@ -466,7 +470,7 @@ def test_ho_brick_mfma_parity(gpu_ctx, shape, p):
                 np.testing.assert_array_equal(again[0], out[mf][0])
     finally:
         gpu_ctx.set_option("ho_brick_mfma", 0)
-        gpu_ctx.set_option("ho_brick", 0)
+        gpu_ctx.set_option("ho_brick", 1)
     for mf, (xg, ig) in out.items():
         assert ig["iterations"] == 40
         assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), mf
