@@ -77,7 +77,11 @@ def parse():
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N>1 data-path communicator: rccl (production, one GPU per rank) or host "
                          "(gloo callbacks; rehearses the N>1 flow with several ranks on one GPU)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=INT",
+                    help="cdfem_set_option before the mesh upload (repeatable; A/B runs, e.g. ho_brick=0). "
+                         "The options in effect are echoed in config.options")
     a = ap.parse_args()
+    a.set = dict((k, int(v)) for k, v in (kv.split("=") for kv in a.set))
     c3 = a.config == "c3"
     a.n = a.n or (128 if c3 else 256 if a.config in ("c5", "c5w") else 64)
     a.order = a.order or (4 if c3 else 2)
@@ -411,6 +415,8 @@ def main_c4(args):
         mesh = cdfem.Mesh(mesh.dim, mesh.order, mesh.verts, g[mesh.dofmap], mesh.nl, np.sort(g[mesh.ess]),
                           None, simplex=True)
     ctx = cdfem.Context(0)
+    for k, v in args.set.items():
+        ctx.set_option(k, v)
     ctx.upload_mesh(mesh)
     t0 = time.perf_counter()
     ctx.fa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=(1.0, -2.0, 0.5), mass=1.0)
@@ -517,6 +523,8 @@ def main():
     mesh = cdfem.box_mesh(3, (n, n, nz), p, z_range=(rank * nzr, (rank + 1) * nzr), with_coords=False)
     ndev = cdfem.device_count()
     ctx = cdfem.Context(local % ndev)  # one rank per GPU on a node; ranks share a GPU only in rehearsals
+    for k, v in args.set.items():
+        ctx.set_option(k, v)
     ctx.upload_mesh(mesh)
     if args.path == "brick" or p >= 3:
         ctx.set_structured(n, n, nzr)  # p >= 3: structured E->L (no position arrays)
@@ -744,6 +752,8 @@ def main():
     per_point = None
     if world == 1 and affine and args.per_point_steps > 0 and args.config in ("c2", "c3"):
         c2 = cdfem.Context(local % ndev)
+        for k, v in args.set.items():
+            c2.set_option(k, v)
         c2.set_option("pa_affine", 0)
         c2.upload_mesh(mesh)
         if args.path == "brick" or p >= 3:
@@ -803,7 +813,10 @@ def main():
                                          "(CG on the symmetric kK+sM, SURVEY 8d)") if args.kinds & 2 else
                                         "fixed-iteration Jacobi-CG on a symmetric operator",
                        "dofs": total_dofs, "elements": n * n * nz, "cg_iters_per_step": args.cg_iters,
-                       "parallelism": f"slab{world}" if world > 1 else "single", "path": args.path,
+                       "parallelism": f"slab{world}" if world > 1 else "single",
+                       "path": {"k_brick_cg": "brick", "k_hobrick_cg": "ho_brick"}.get(
+                           ctx.kernel_name(cdfem.K_APPLY), args.path),
+                       **({"options": args.set} if args.set else {}),
                        "qdata": ("affine: 10 factors per element applied in their Kronecker form (pa_affine 2, 1D rule "
                                  "matrices per axis); the operator equals the per-point form to rounding (1e-13 "
                                  "relative, tests/test_gpu_affine.py)" if affine
