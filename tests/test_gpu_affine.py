@@ -161,3 +161,30 @@ def test_affine_tolerance_is_element_relative(gpu_ctx):
     v2 = om.verts.copy()
     v2[13, 7, :] += 1e-9 * 0.01  # vertex (1,1,1) of one element, 1e-9 of its edge
     assert apply_bytes(v2) >= stream
+
+
+@pytest.mark.parametrize("p", [1, 2])
+def test_graded_box_brick_cg(gpu_ctx, p):
+    """A box graded along x and y (every element a box, the sizes differ: affine, each element its own
+    factors) through the brick CG in the Kronecker form: the apply reads the factors, not the stream,
+    and 30 Jacobi-CG iterates match the oracle to 1e-11."""
+    shape = (8, 6, 5)
+    om = O.BoxMesh(3, shape, p)
+    v = om.verts.copy()
+    v[..., 0] = v[..., 0] ** 1.5
+    v[..., 1] = 0.5 * (v[..., 1] + v[..., 1] ** 2)
+    om.verts = np.ascontiguousarray(v)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3)
+    rng = np.random.default_rng(11)
+    b = rng.uniform(-1, 1, om.nl)
+    u = np.zeros(om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(*shape)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    assert gpu_ctx.kernel_bytes(cdfem.K_APPLY) < 8.0 * 10 * (p + 2) ** 3 * om.ne
+    _, B = gpu_ctx.form_linear_system(u, b)
+    assert _relmax(B, Bo) <= TOL
+    xg, ig = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    assert ig["iterations"] == 30
+    assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
