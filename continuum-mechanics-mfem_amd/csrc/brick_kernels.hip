@@ -23,6 +23,12 @@
 #include "pa_core.hpp"
 #include "reduce.hpp"
 
+// LDS of the brick CG apply (k_brick_cg): 0 = three linear S^3 patches (in, out, essential d), 1 = the
+// essential d in registers, 2 = that plus the padded patch pitch
+#ifndef CDFEM_BRICK_LDS
+#define CDFEM_BRICK_LDS 1
+#endif
+
 namespace cdfem {
 
 struct BrickGeom {
@@ -172,10 +178,10 @@ __host__ __device__ constexpr int e2l_member(int cls, int r)
 }
 
 // s_out[o0 + patch offset of local dof] += Y for the 64 elements of a brick, deterministic order
-template <int D1, int S>
+// (patch strides SY per row, S2 per plane in LDS: S, S^2 unpadded)
+template <int D1, int S, int SY = S, int S2 = S * S>
 __device__ __forceinline__ void brick_e2l(double *s_out, int o0, const double (&Y)[D1][D1][D1])
 {
-    constexpr int S2 = S * S;
     if constexpr (D1 == 3) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
@@ -184,7 +190,7 @@ __device__ __forceinline__ void brick_e2l(double *s_out, int o0, const double (&
                 const int l = e2l_member(cls, r);
                 if (l < 0) continue;
                 const int dz = l / 9, dy = (l / 3) % 3, dx = l % 3;
-                s_out[o0 + dz * S2 + dy * S + dx] += Y[dz][dy][dx];
+                s_out[o0 + dz * S2 + dy * SY + dx] += Y[dz][dy][dx];
             }
             __syncthreads();
         }
@@ -196,7 +202,7 @@ __device__ __forceinline__ void brick_e2l(double *s_out, int o0, const double (&
             for (int dy = 0; dy < D1; ++dy)
 #pragma unroll
                 for (int dx = 0; dx < D1; ++dx) {
-                    s_out[o0 + dz * S2 + dy * S + dx] += Y[dz][dy][dx];
+                    s_out[o0 + dz * S2 + dy * SY + dx] += Y[dz][dy][dx];
                     __syncthreads();
                 }
     }
@@ -591,13 +597,21 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     constexpr int S2 = S * S, S3 = S * S * S;
     constexpr int NC = QLayout<K, 3>::nc;
     constexpr int NQ = Q1 * Q1 * Q1;
-    __shared__ double s_in[S3];
-    __shared__ double s_out[S3];
+    // LDS patch layout (CDFEM_BRICK_LDS 2, p = 2): rows padded to SY = 12 and planes to SZ = 112 doubles,
+    // so the 32 element origins of a ds_read_b64 half-wave (2 ex + 2 SY ey + 2 SZ ez) fall on 16
+    // distinct bank pairs (2-way, the floor for even origins) instead of up to 4-way at SY = 9, SZ = 81
+    constexpr bool PAD = CDFEM_BRICK_LDS == 2 && P == 2;
+    constexpr int SY = PAD ? 12 : S, SZ = PAD ? 112 : S2, PS = (S - 1) * SZ + (S - 1) * SY + S;
+    __shared__ double s_in[PS];
+    __shared__ double s_out[PS];
     // EP (the Kronecker form, AF 2): the essential rows' patch entries carry (A_c d)_i = d_i, the
     // writer brick's d (0 where the den ownership bit is off: non-writers, and the slab plane the rank
-    // below owns), so the update's sum of a row's entries is its q with no essential flag or d read
+    // below owns), so the update's sum of a row's entries is its q with no essential flag or d read.
+    // CDFEM_BRICK_LDS 0 keeps those d in a third LDS patch; >= 1 in registers (each position is formed
+    // and stored by the same thread: 12 doubles live through the core, the LDS round trip gone)
     constexpr bool EP = AF == 2;
-    __shared__ double s_d[EP ? S3 : 1];
+    constexpr bool EPL = EP && CDFEM_BRICK_LDS == 0;
+    __shared__ double s_d[EPL ? S3 : 1];
     if (st->done) return;
     double beta = st->beta;
     constexpr int NPL = 16;  // BF: partials per lane (nupart <= 64 NPL)
@@ -643,6 +657,8 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     uint32_t woffv[NI];
     uint32_t dbits = 0, ebits = 0;
     uint8_t ev[NI];
+    uint32_t liv[PAD ? NI : 1];     // PAD: the position's LDS index
+    double dev[EP && !EPL ? NI : 1];  // EP in registers: the essential entries' d
     // FULL (every brick of the box has its whole patch inside the lattice: the element counts are
     // multiples of 4): no lattice bound per position
     const uint32_t uLx = (uint32_t)Lx, uLxy = (uint32_t)Lxy;
@@ -658,6 +674,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         const unsigned i = t + 64 * k;
         const int px = pw0.x, py = pw0.y, pz = pw0.z;
         const uint32_t gid = pw0.gid;
+        if constexpr (PAD) liv[k] = (uint32_t)px + SY * (uint32_t)py + SZ * (uint32_t)pz;
         pw0.next(dgid, cxd, cyd);
         const int gz = gz0 + pz;
         const bool in = i < S3 && (FULL || (gx0 + px < g.Lx && gy0 + py < g.Ly && gz < g.Lz));
@@ -681,11 +698,13 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         if constexpr (XF) bstore(bxf, woffv[k], xv[k] + alpha_prev * ov[k]);
         // (A_c d)_i = d_i on ess dofs
         den += (e && ((dbits >> k) & 1u)) ? dn * dn : 0.0;
-        s_in[i] = e ? 0.0 : dn;
-        s_out[i] = 0.0;
+        const unsigned li = PAD ? liv[PAD ? k : 0] : i;
+        s_in[li] = e ? 0.0 : dn;
+        s_out[li] = 0.0;
         if constexpr (EP) {  // (unconditional: a predicated LDS store compiles to a branch per position)
             ebits |= (uint32_t)e << k;
-            s_d[i] = ((dbits >> k) & 1u) ? dn : 0.0;
+            if constexpr (EPL) s_d[i] = ((dbits >> k) & 1u) ? dn : 0.0;
+            else dev[EPL ? 0 : k] = ((dbits >> k) & 1u) ? dn : 0.0;
         }
     };
     static_for<0, GK>(gather);
@@ -716,8 +735,8 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     __syncthreads();
 
     const int ex = t & 3, ey = (t >> 2) & 3, ez = t >> 4;
-    const int o0 = P * ez * S2 + P * ey * S + P * ex;
-    auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * S2 + dy * S + dx]; };
+    const int o0 = P * ez * SZ + P * ey * SY + P * ex;
+    auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * SZ + dy * SY + dx]; };
     double Y[D1][D1][D1];
     elem_apply3d_af<D1, Q1, K, AF>(xl, q0, t, T, Y);
 
@@ -727,8 +746,8 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
 #pragma unroll
         for (int dy = 0; dy < D1; ++dy)
 #pragma unroll
-            for (int dx = 0; dx < D1; ++dx) den += s_in[o0 + dz * S2 + dy * S + dx] * Y[dz][dy][dx];
-    brick_e2l<D1, S>(s_out, o0, Y);
+            for (int dx = 0; dx < D1; ++dx) den += s_in[o0 + dz * SZ + dy * SY + dx] * Y[dz][dy][dx];
+    brick_e2l<D1, S, SY, SZ>(s_out, o0, Y);
 
     // the brick's whole patch output (interior rows complete, face rows partial) -> the patch buffer
     // (patch_idx, here in 32-bit arithmetic with the brick's part uniform: index = base + pz A + py R
@@ -743,8 +762,9 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         for (int k = 0; k < NI; ++k) {
             const unsigned i = to + 64 * k;
             if (k == NI - 1 && i >= S3) break;
-            double v = s_out[i];
-            if constexpr (EP) v = ((ebits >> k) & 1u) ? s_d[i] : v;
+            double v = s_out[PAD ? (uint32_t)pw.x + SY * (uint32_t)pw.y + SZ * (uint32_t)pw.z : i];
+            if constexpr (EPL) v = ((ebits >> k) & 1u) ? s_d[i] : v;
+            else if constexpr (EP) v = ((ebits >> k) & 1u) ? dev[EPL ? 0 : k] : v;
             bstore(bp, 8u * (base + (uint32_t)pw.z * A + (uint32_t)pw.y * R + (uint32_t)pw.x), v);
             pw.next();
         }
