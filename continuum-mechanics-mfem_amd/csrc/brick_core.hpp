@@ -1,0 +1,80 @@
+// brick_core.hpp — the structured-box lattice geometry, raw buffer access and the patch-buffer row
+// sum, shared by the brick kernels (brick_kernels.hip) and the GMRES passes that read the structured
+// Mult's patch buffer directly (gmres.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "pa_core.hpp"
+
+namespace cdfem {
+
+struct BrickGeom {
+    int nbx, nby, nbz;  // bricks per axis
+    int Lx, Ly, Lz;     // dof lattice per axis
+    int xcd;            // 1: XCD-contiguous brick order (default; set_option "brick_xcd")
+    int bz0, bzs;       // k_brick_cg: the launch covers brick layers bz0, bz0 + bzs, ... (all: 0, 1)
+};
+
+// Raw buffer access (MI355X buffer resources): a 32-bit byte offset from a scalar base instead of a
+// 64-bit address per lane, and an offset past num_records (kOOB) reads 0 and drops a store, so the
+// brick kernels' out-of-lattice positions and predicated stores need neither branches nor clamps.
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+constexpr uint32_t kOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, double v)
+{
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, off, 0, 0);
+}
+
+// The 1-8 patch-buffer entries of lattice dof (gx, gy, gz) summed in a fixed order (lower brick first
+// per face axis, z outermost): eight buffer loads at fixed offsets from its own brick's entry P (the
+// lower brick's face entry along x / y / z sits at P - 1 / P - R / P - A in the pencil layout of
+// patch_idx), the absent ones at kOOB (read as 0).
+template <int S>
+__device__ __forceinline__ double patch_sum8(__amdgpu_buffer_rsrc_t bp, const BrickGeom &g, int gx, int gy, int gz)
+{
+    constexpr int s1 = S - 1;
+    const int qx = min(gx / s1, g.nbx - 1), qy = min(gy / s1, g.nby - 1), qz = min(gz / s1, g.nbz - 1);
+    const int px = gx - qx * s1, py = gy - qy * s1, pz = gz - qz * s1;
+    const bool fx = px == 0 && qx > 0, fy = py == 0 && qy > 0, fz = pz == 0 && qz > 0;
+    const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
+    const uint32_t P = (((uint32_t)qz * S + pz) * g.nby + qy) * S * R + (uint32_t)py * R + (uint32_t)qx * S + px;
+    double t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int sz = (k >> 2) & 1 ? 0 : 1, sy = (k >> 1) & 1 ? 0 : 1, sx = k & 1 ? 0 : 1;
+        const bool ok = (!sx || fx) && (!sy || fy) && (!sz || fz);
+        const uint32_t o = P - (uint32_t)sx - (uint32_t)sy * R - (uint32_t)sz * A;
+        t[k] = bload(bp, ok ? 8u * o : kOOB);
+    }
+    double q = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q += t[k];
+    return q;
+}
+
+// GMRES on the structured Mult (set_option "gm_pb"): A_c V_j is each row's 1-8 patch entries of the
+// patch-buffer Mult (k_brick3d<..., PBO>), V_j itself on the essential rows; pass 1 forms it there
+// (k_gm_pass1<..., S>), so the E->L kernel's y write and pass 1's re-read of it go away
+struct GmPatchSrc {
+    const double *pb;    // the patch buffer
+    const uint8_t *ess;  // essential flags
+    const double *x;     // the Mult's input V_j
+    BrickGeom g;
+    FastDiv fdx, fdxy;   // lattice row / plane
+    int S;               // patch side (4p + 1)
+};
+// the patch-buffer Mult is in use (brick_mult_pb, Kronecker form, offsets within 32 bits)
+bool brick_mult_pb_on(const cdfem_ctx *c);
+GmPatchSrc gm_patch_src(const cdfem_ctx *c, const double *x);
+
+}  // namespace cdfem

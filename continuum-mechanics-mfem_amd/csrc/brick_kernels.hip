@@ -20,6 +20,7 @@
 #include <type_traits>
 
 #include "cdfem_internal.hpp"
+#include "brick_core.hpp"
 #include "pa_core.hpp"
 #include "reduce.hpp"
 
@@ -30,13 +31,6 @@
 #endif
 
 namespace cdfem {
-
-struct BrickGeom {
-    int nbx, nby, nbz;  // bricks per axis
-    int Lx, Ly, Lz;     // dof lattice per axis
-    int xcd;            // 1: XCD-contiguous brick order (default; set_option "brick_xcd")
-    int bz0, bzs;       // k_brick_cg: the launch covers brick layers bz0, bz0 + bzs, ... (all: 0, 1)
-};
 
 // workgroup b runs on XCD b % 8; with xcd = 1 each XCD takes a contiguous range of bricks, so a
 // brick's neighbours (which re-read its patch faces) are mostly on the same L2.  Measured in
@@ -144,24 +138,6 @@ __device__ __forceinline__ int opaque(int v)
     return v;
 }
 
-// Raw buffer access (MI355X buffer resources): a 32-bit byte offset from a scalar base instead of a
-// 64-bit address per lane, and an offset past num_records (kOOB) reads 0 and drops a store, so the
-// brick kernels' out-of-lattice positions and predicated stores need neither branches nor clamps.
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-constexpr uint32_t kOOB = 0x80000000u;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t bytes)
-{
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, uint32_t off)
-{
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-}
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, double v)
-{
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, off, 0, 0);
-}
-
 // In-LDS E->L schedule.  At P = 2 an element's local dof d lands on patch position 2e + d per axis,
 // so two (element, local dof) pairs meet on one position only if their local dofs agree mod 2: the
 // 27 local dofs split into 8 parity classes (dx & 1, dy & 1, dz & 1) of 8, 4, 4, 2, 4, 2, 2, 1 dofs
@@ -206,33 +182,6 @@ __device__ __forceinline__ void brick_e2l(double *s_out, int o0, const double (&
                     __syncthreads();
                 }
     }
-}
-
-// The 1-8 patch-buffer entries of lattice dof (gx, gy, gz) summed in a fixed order (lower brick first
-// per face axis, z outermost): eight buffer loads at fixed offsets from its own brick's entry P (the
-// lower brick's face entry along x / y / z sits at P - 1 / P - R / P - A in the pencil layout of
-// patch_idx), the absent ones at kOOB (read as 0).
-template <int S>
-__device__ __forceinline__ double patch_sum8(__amdgpu_buffer_rsrc_t bp, const BrickGeom &g, int gx, int gy, int gz)
-{
-    constexpr int s1 = S - 1;
-    const int qx = min(gx / s1, g.nbx - 1), qy = min(gy / s1, g.nby - 1), qz = min(gz / s1, g.nbz - 1);
-    const int px = gx - qx * s1, py = gy - qy * s1, pz = gz - qz * s1;
-    const bool fx = px == 0 && qx > 0, fy = py == 0 && qy > 0, fz = pz == 0 && qz > 0;
-    const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
-    const uint32_t P = (((uint32_t)qz * S + pz) * g.nby + qy) * S * R + (uint32_t)py * R + (uint32_t)qx * S + px;
-    double t[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int sz = (k >> 2) & 1 ? 0 : 1, sy = (k >> 1) & 1 ? 0 : 1, sx = k & 1 ? 0 : 1;
-        const bool ok = (!sx || fx) && (!sy || fy) && (!sz || fz);
-        const uint32_t o = P - (uint32_t)sx - (uint32_t)sy * R - (uint32_t)sz * A;
-        t[k] = bload(bp, ok ? 8u * o : kOOB);
-    }
-    double q = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) q += t[k];
-    return q;
 }
 
 // MODE 0: y = A x;  MODE 1: y = A_c x (ConstrainedOperator).  (The CG loop runs k_brick_cg.)
@@ -473,6 +422,15 @@ static BrickGeom geom_of(const cdfem_ctx *c)
 int brick_count(const cdfem_ctx *c) { return c->p >= 3 ? c->hb_nblk : c->nblk; }
 int brick_patch_side(const cdfem_ctx *c) { return c->p >= 3 ? kHoBrickEdge * c->p + 1 : kBrick * c->p + 1; }
 
+// patch-buffer Mult (Kronecker form, byte offsets within 32 bits)
+bool brick_mult_pb_on(const cdfem_ctx *c) { return c->brick_mult_pb != 0 && pa_af(c) == 2 && brick_fits(c); }
+
+GmPatchSrc gm_patch_src(const cdfem_ctx *c, const double *x)
+{
+    return GmPatchSrc{c->d_face, c->d_ess, x, geom_of(c), make_fastdiv((uint32_t)c->Lx),
+                      make_fastdiv((uint32_t)(c->Lx * c->Ly)), kBrick * c->p + 1};
+}
+
 static dim3 faces_grid(const cdfem_ctx *c)
 {
     const int64_t plane = c->Lx * c->Ly;
@@ -487,8 +445,7 @@ static hipError_t brick_launch(cdfem_ctx *c, const double *x, const double *dinv
 {
     constexpr int S = kBrick * (D1 - 1) + 1;
     const BrickGeom g = geom_of(c);
-    // patch-buffer Mult (Kronecker form, byte offsets within 32 bits)
-    const bool mpb = c->brick_mult_pb != 0 && pa_af(c) == 2 && brick_fits(c);
+    const bool mpb = brick_mult_pb_on(c);
     if (which & 1) {
         const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
 #define CDFEM_B3(AF_, QD_)                                                                                    \

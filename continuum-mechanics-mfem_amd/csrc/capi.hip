@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "cdfem_internal.hpp"
+#include "brick_core.hpp"
 
 using namespace cdfem;
 
@@ -707,6 +708,8 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
         HIPCHK(hipEventSynchronize(c->gm_ev[slot]));
         return poll[slot];
     };
+    // one rank on the structured patch-buffer Mult: pass 1 forms A_c v_j from the patch buffer itself
+    const bool gpb = c->gm_pb != 0 && !ilu && !multi_rank(c) && use_brick(c) && brick_mult_pb_on(c);
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemsetAsync(x, 0, n * sizeof(double), c->stream));
@@ -727,7 +730,20 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
         post(0);
         if (wait(0).done) break;
         for (int j = 0; j < m; ++j) {
-            op_apply_global(c, V + (int64_t)j * ldv, w, true);
+            const double *Vj = V + (int64_t)j * ldv;
+            if (gpb) {  // the structured Mult's patch buffer, summed per row by pass 1 (gm_pb)
+                prof_mark(c, CDFEM_K_APPLY, true);
+                HIPCHK(launch_brick_mult(c, Vj, w, true, 1));
+                prof_mark(c, CDFEM_K_APPLY, false);
+                const GmPatchSrc src = gm_patch_src(c, Vj);
+                prof_mark(c, CDFEM_K_ORTH, true);
+                HIPCHK(launch_gm_orth(c, w, dinv, V, ldv, part, st, m, &poll[j & 1], &src));
+                prof_mark(c, CDFEM_K_ORTH, false);
+                post(j & 1);
+                if (j > 0 && wait((j - 1) & 1).cycle_done) break;
+                continue;
+            }
+            op_apply_global(c, Vj, w, true);
             if (ilu) HIPCHK(ilu_apply(c));  // w <- (LU)^{-1} A v_j, in ilu.z
             prof_mark(c, CDFEM_K_ORTH, true);
             HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, ldv, part, st, m, &poll[j & 1]));
@@ -1800,6 +1816,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 8)
                 throw ArgError("sell_order must be 0..8 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton, 8 Morton LDS windows / auto)");
             c->sell_mode = value;
+        } else if (k == "gm_pb") {
+            if (value < 0 || value > 1) throw ArgError("gm_pb must be 0 or 1");
+            c->gm_pb = value;
         } else if (k == "pa_affine") {  // read by cdfem_pa_setup
             if (value < 0 || value > 2) throw ArgError("pa_affine must be 0, 1 or 2");
             c->pa_affine = value;

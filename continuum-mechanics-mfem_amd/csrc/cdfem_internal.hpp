@@ -165,6 +165,7 @@ struct cdfem_ctx {
     int nface = 0;                      // F
     int gm_ept = 0;                     // set_option "gm_ept": GMRES orthogonalisation entries per thread (0: auto, orth_ept)
     int gm_ept_auto = 4;                // the automatic choice for vectors of gm_ept_n entries
+    int gm_pb = 1;                      // set_option "gm_pb": GMRES pass 1 reads the structured Mult's patch buffer
     int64_t gm_ept_n = -1;
     int brick_xcd = 1;                  // k_brick_cg brick order: 0 dispatch, 1 XCD-contiguous (default)
     // the brick kernels address r, M^-1, d, x, ess and the patch buffer through buffer resources with
@@ -507,8 +508,10 @@ hipError_t launch_gm_init(cdfem_ctx *c, GmresState *st, int m, int max_it);
 // poll: pinned host slot the step's last scalar kernel writes the state head into (solve_gmres)
 hipError_t launch_gm_residual(cdfem_ctx *c, const double *b, const double *Ax, const double *dinv, double *v0,
                               double *part, GmresState *st, bool first, double rtol, double atol, GmresState *poll);
+// ps (gm_pb): pass 1 reads the structured Mult's patch buffer for A_c V_j instead of w (brick_core.hpp)
+struct GmPatchSrc;
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m, GmresState *poll);
+                          GmresState *st, int m, GmresState *poll, const GmPatchSrc *ps = nullptr);
 hipError_t launch_gm_update(cdfem_ctx *c, double *x, const double *V, int64_t ldv, GmresState *st, GmresState *poll);
 hipError_t launch_stream(cdfem_ctx *c, int mode, const double *a, double *b, int64_t n);
 // ILU(0) (ilu_kernels.hip): factor + capture once per operator; apply: ilu.z = (LU)^{-1} d_w[4]

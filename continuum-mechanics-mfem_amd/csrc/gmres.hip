@@ -21,6 +21,7 @@
 
 #include <algorithm>
 
+#include "brick_core.hpp"
 #include "cdfem_internal.hpp"
 #include "reduce.hpp"
 
@@ -112,14 +113,17 @@ k_gm_start(const double *__restrict__ part, int nb, GmresState *__restrict__ st,
 
 // ---- pass 1: w = s_j M^{-1} A V_j (in place over the apply output), partial (w, V_i), i <= j ----
 // The projections are formed BAT at a time: BAT * kGmEPT loads per lane in flight, all
-// unconditional (indices clamped to j; the clamped duplicates of V_j are cache hits whose sums are
+// unconditional (past V_0 the indices repeat V_0: cache hits whose sums are
 // dropped).  Each wave parks its wave sums in LDS, so the whole step needs ONE barrier before the
 // block sums.  Measured at C4 (orthogonalisation per step): one barrier per batch of 8, 93.9 us;
 // one barrier in all, batches of 8 / 4 / 2 / 1: 85.7 / 83.2 / 82.6 / 82.1 us.
-template <int BAT, int EPT>
+// S > 0 (gm_pb, GmPatchSrc): A_c V_j from the structured Mult's patch buffer (patch_sum8, S = 4p + 1)
+// instead of w; w is still written (pass 2 reads it)
+template <int BAT, int EPT, int S = 0>
 __global__ void __launch_bounds__(kRedThreads)
 k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double *__restrict__ V, int64_t n,
-           int64_t ldv, int64_t skip_lo, double *__restrict__ part, int nb, const GmresState *__restrict__ st)
+           int64_t ldv, int64_t skip_lo, double *__restrict__ part, int nb, const GmresState *__restrict__ st,
+           const GmPatchSrc ps)
 {
     __shared__ double sh[kGmMaxRestart + 1][kRedThreads / 64];
     if (st->cycle_done) return;
@@ -133,18 +137,34 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
         const int64_t k = base + (int64_t)e * kRedThreads;
         double v = 0.0;
         if (k < n) {
-            v = sj * w[k];
+            double y;
+            if constexpr (S == 0) {
+                y = w[k];
+            } else {  // (n < 2^28 on the brick path: brick_fits)
+                const uint32_t gid = (uint32_t)k, plane = (uint32_t)(ps.g.Lx * ps.g.Ly);
+                const uint32_t gz = fdiv(gid, ps.fdxy), rem = gid - gz * plane, gy = fdiv(rem, ps.fdx);
+                const uint32_t gx = rem - gy * (uint32_t)ps.g.Lx;
+                const auto bp = brsrc(ps.pb, 8u * (uint32_t)ps.g.nbx * ps.g.nby * ps.g.nbz * (S * S * S));
+                y = patch_sum8<S>(bp, ps.g, (int)gx, (int)gy, (int)gz);
+                if (ps.ess[k]) y = ps.x[k];  // A_c: the identity row
+            }
+            v = sj * y;
             if (dinv) v *= dinv[k];
             w[k] = v;
         }
         wv[e] = k >= skip_lo ? v : 0.0;  // projections: owned entries only
     }
+    // the basis is read from V_j DOWN to V_0 (each projection is its own sum, so the order of the
+    // vectors changes nothing): V_0, V_1, ... are then the most recently read lines when pass 2 reads
+    // them again in ascending order, so the first ~256 MB of pass 2's basis come from the MALL
+    // (Infinity Cache) instead of HBM; with both passes ascending every pass-2 read missed (an LRU
+    // scan of more than the cache)
 #pragma unroll 1
-    for (int i0 = 0; i0 <= j; i0 += BAT) {
+    for (int r0 = 0; r0 <= j; r0 += BAT) {
         double vv[BAT][EPT];
 #pragma unroll
         for (int b = 0; b < BAT; ++b) {
-            const double *vi = V + (int64_t)(i0 + b <= j ? i0 + b : j) * ldv;
+            const double *vi = V + (int64_t)(r0 + b <= j ? j - (r0 + b) : 0) * ldv;
 #pragma unroll
             for (int e = 0; e < EPT; ++e) {
                 const int64_t k = base + (int64_t)e * kRedThreads;
@@ -157,7 +177,7 @@ k_gm_pass1(double *__restrict__ w, const double *__restrict__ dinv, const double
 #pragma unroll
             for (int e = 0; e < EPT; ++e) a += wv[e] * vv[b][e];
             const double t = wave_sum(a);
-            if (lane == 0 && i0 + b <= j) sh[i0 + b][wv_id] = t;
+            if (lane == 0 && r0 + b <= j) sh[j - (r0 + b)][wv_id] = t;
         }
     }
     __syncthreads();
@@ -480,7 +500,7 @@ static int orth_ept(cdfem_ctx *c)
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gm_pass1<kGmBatch, 4>, kRedThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gm_pass1<kGmBatch, 4, 0>, kRedThreads, 0);
     const int64_t cap = (int64_t)std::max(cus, 1) * std::max(per, 1);
     int ept = 8;
     for (int e : {4, 5, 6, 8})
@@ -495,13 +515,19 @@ static int orth_ept(cdfem_ctx *c)
 
 template <int EPT>
 static void orth_passes(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                        GmresState *st, int m, GmresState *poll)
+                        GmresState *st, int m, GmresState *poll, const GmPatchSrc *ps)
 {
     const int nb = (int)((c->nl + (int64_t)kRedThreads * EPT - 1) / ((int64_t)kRedThreads * EPT));
     const int64_t n = c->nl;
     const bool mr = multi_rank(c);
-    hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, ldv,
-                       owned_from(c), part, nb, st);
+    const GmPatchSrc src = ps ? *ps : GmPatchSrc{};
+#define CDFEM_P1(S_)                                                                                      \
+    hipLaunchKernelGGL((k_gm_pass1<kGmBatch, EPT, S_>), dim3(nb), dim3(kRedThreads), 0, c->stream, w, dinv, V, n, \
+                       ldv, owned_from(c), part, nb, st, src)
+    if (ps && ps->S == 9) CDFEM_P1(9);
+    else if (ps && ps->S == 5) CDFEM_P1(5);
+    else CDFEM_P1(0);
+#undef CDFEM_P1
     hipLaunchKernelGGL(k_gm_dots_fin_mb, dim3(m + 1), dim3(kRedThreads), 0, c->stream, part, nb, st, mr ? 1 : 0);
     if (mr) {
         comm_allreduce(c, red_of(st), m + 1);
@@ -518,13 +544,14 @@ static void orth_passes(cdfem_ctx *c, double *w, const double *dinv, double *V, 
 }
 
 hipError_t launch_gm_orth(cdfem_ctx *c, double *w, const double *dinv, double *V, int64_t ldv, double *part,
-                          GmresState *st, int m, GmresState *poll)
+                          GmresState *st, int m, GmresState *poll, const GmPatchSrc *ps)
 {
+    if (ps && ps->S != 5 && ps->S != 9) return hipErrorInvalidValue;
     switch (orth_ept(c)) {
-    case 5: orth_passes<5>(c, w, dinv, V, ldv, part, st, m, poll); break;
-    case 6: orth_passes<6>(c, w, dinv, V, ldv, part, st, m, poll); break;
-    case 8: orth_passes<8>(c, w, dinv, V, ldv, part, st, m, poll); break;
-    default: orth_passes<4>(c, w, dinv, V, ldv, part, st, m, poll); break;
+    case 5: orth_passes<5>(c, w, dinv, V, ldv, part, st, m, poll, ps); break;
+    case 6: orth_passes<6>(c, w, dinv, V, ldv, part, st, m, poll, ps); break;
+    case 8: orth_passes<8>(c, w, dinv, V, ldv, part, st, m, poll, ps); break;
+    default: orth_passes<4>(c, w, dinv, V, ldv, part, st, m, poll, ps); break;
     }
     return hipGetLastError();
 }

@@ -331,6 +331,10 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "spmv_xcd": 1 (default) — contiguous slice range per XCD for the windowed SpMV layout.
  * "gm_ept": 0 (default, auto) — entries per thread of the GMRES orthogonalisation passes (4, 5, 6
  *           or 8); auto takes the smallest whose grid is resident in one round (same results).
+ * "gm_pb": 1 (default) — GMRES on the structured patch-buffer Mult (one rank, Jacobi or no
+ *          preconditioner): the first orthogonalisation pass sums each row's patch entries itself, so
+ *          the Mult's row-sum kernel and its output vector's write and re-read go away (same sums in
+ *          the same order: bitwise the same iterates); 0 = the Mult's own row sums.
  * Variants measured slower and removed in round 3 (their records stay under profiles/r02_ab_*):
  * brick element cores 1-10 and the four-waves-per-brick kernel, x-fold / paired x updates, the
  * folded high-order direction, the derived mass weight, per-XCD SpMV sort, SpMV stream offsets and

@@ -150,3 +150,27 @@ def test_gmres_tight_solution_parity_fa_tets(gpu_ctx):
                            max_iter=5000)
     assert io["converged"] and ig["converged"], (io, ig)
     assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
+
+
+@pytest.mark.parametrize("n,p,kinds", [(8, 2, 7), (6, 2, 5), (7, 1, 7), (9, 2, 3)])
+def test_gmres_patch_buffer_pass_bitwise(gpu_ctx, n, p, kinds):
+    """gm_pb: on the structured patch-buffer Mult, the first orthogonalisation pass sums each row's
+    patch entries itself (essential rows: the basis vector) instead of reading the Mult's row-sum
+    kernel output.  Same sums in the same order: 35 GMRES(10) iterates (three restarts, so the
+    cycle-start Mult through the row-sum kernel is exercised too) bitwise equal to gm_pb 0, and
+    1e-11 of the oracle; partial bricks (n not a multiple of 4) included."""
+    om, Ac, Bo, B = _system(gpu_ctx, 3, n, p, 0.1, kinds=kinds, structured=True)
+    xo, _ = O.gmres(Ac, Bo, dinv=1.0 / Ac.diag(), restart=10, rtol=0.0, atol=0.0, max_it=35)
+    out = {}
+    try:
+        for pb in (0, 1):
+            gpu_ctx.set_option("gm_pb", pb)
+            out[pb] = gpu_ctx.solve(B, method="gmres", pc="jacobi", restart=10, rel_tol=0.0, abs_tol=0.0,
+                                    max_iter=35)
+    finally:
+        gpu_ctx.set_option("gm_pb", 1)
+    (x0, i0), (x1, i1) = out[0], out[1]
+    assert i0["iterations"] == i1["iterations"] == 35
+    np.testing.assert_array_equal(x1, x0)
+    assert i1["final_norm"] == i0["final_norm"]
+    assert np.linalg.norm(x1 - xo) <= 1e-11 * np.linalg.norm(xo)
