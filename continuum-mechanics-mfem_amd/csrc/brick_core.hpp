@@ -8,6 +8,10 @@
 
 #include "pa_core.hpp"
 
+#ifndef CDFEM_PS8_SKIP
+#define CDFEM_PS8_SKIP 1
+#endif
+
 namespace cdfem {
 
 struct BrickGeom {
@@ -48,13 +52,24 @@ __device__ __forceinline__ double patch_sum8(__amdgpu_buffer_rsrc_t bp, const Br
     const bool fx = px == 0 && qx > 0, fy = py == 0 && qy > 0, fz = pz == 0 && qz > 0;
     const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
     const uint32_t P = (((uint32_t)qz * S + pz) * g.nby + qy) * S * R + (uint32_t)py * R + (uint32_t)qx * S + px;
+    // (CDFEM_PS8_SKIP: a wave none of whose dofs sits on a y or z brick face issues no load for those
+    // neighbours: the 64 consecutive dofs of a wave share one or two lattice rows, so most waves load
+    // 2 entries, not 8.  An out-of-range buffer load moves no memory but still returns 64 lanes of
+    // data; the skipped terms are the zeros they would have read, so the sum is unchanged)
+    bool ax = true, ay = true, az = true;
+    if constexpr (CDFEM_PS8_SKIP) {
+        ax = __builtin_amdgcn_ballot_w64(fx) != 0;
+        ay = __builtin_amdgcn_ballot_w64(fy) != 0;
+        az = __builtin_amdgcn_ballot_w64(fz) != 0;
+    }
     double t[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int sz = (k >> 2) & 1 ? 0 : 1, sy = (k >> 1) & 1 ? 0 : 1, sx = k & 1 ? 0 : 1;
         const bool ok = (!sx || fx) && (!sy || fy) && (!sz || fz);
         const uint32_t o = P - (uint32_t)sx - (uint32_t)sy * R - (uint32_t)sz * A;
-        t[k] = bload(bp, ok ? 8u * o : kOOB);
+        t[k] = 0.0;
+        if ((!sx || ax) && (!sy || ay) && (!sz || az)) t[k] = bload(bp, ok ? 8u * o : kOOB);
     }
     double q = 0.0;
 #pragma unroll
