@@ -19,6 +19,7 @@ struct BrickGeom {
     int Lx, Ly, Lz;     // dof lattice per axis
     int xcd;            // 1: XCD-contiguous brick order (default; set_option "brick_xcd")
     int bz0, bzs;       // k_brick_cg: the launch covers brick layers bz0, bz0 + bzs, ... (all: 0, 1)
+    const uint8_t *bess;  // per brick: 1 if a dof of its patch is essential (nullptr: assume so)
 };
 
 // Raw buffer access (MI355X buffer resources): a 32-bit byte offset from a scalar base instead of a

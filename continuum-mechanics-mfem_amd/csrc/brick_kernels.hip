@@ -415,8 +415,8 @@ bool brick_fits(const cdfem_ctx *c)
 // the brick lattice of the context: 4^3-element bricks at p <= 2, 2^3-element blocks at p = 3, 4 (ho_brick)
 static BrickGeom geom_of(const cdfem_ctx *c)
 {
-    if (c->p >= 3) return BrickGeom{c->hb_nbx, c->hb_nby, c->hb_nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1};
-    return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1};
+    if (c->p >= 3) return BrickGeom{c->hb_nbx, c->hb_nby, c->hb_nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1, c->d_bess};
+    return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1, c->d_bess};
 }
 
 int brick_count(const cdfem_ctx *c) { return c->p >= 3 ? c->hb_nblk : c->nblk; }
@@ -606,6 +606,9 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const uint32_t nl = (uint32_t)Lxy * (uint32_t)g.Lz;
     const auto br = brsrc(r, 8u * nl), bm = brsrc(dinv, 8u * nl), bo = brsrc(d_old, 8u * nl);
     const auto be = brsrc(ess, nl), bd = brsrc(d_new, 8u * nl), bxf = brsrc(x, XF ? 8u * nl : 0u);
+    // (the essential flags are loaded in every brick: skipping them where g.bess says the patch has
+    // none, as k_hobrick_cg does, splits the gather's back-to-back loads and cost 2 us per launch,
+    // profiles/r05/ab_bess/)
     // per position: the writer's byte offset (kOOB where this brick does not write the dof) and one
     // bit of dbits for "writer, and its d^2 counts in den" (not on a slab plane the rank below owns),
     // formed once here: the second pass then needs neither the patch walk nor the lane masks (which
@@ -910,6 +913,10 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
     const uint32_t nl = (uint32_t)Lxy * (uint32_t)g.Lz;
     const auto br = brsrc(r, 8u * nl), bm = brsrc(dinv, 8u * nl), bo = brsrc(d_old, 8u * nl);
     const auto be = brsrc(ess, nl), bd = brsrc(d_new, 8u * nl), bxf = brsrc(x, XF ? 8u * nl : 0u);
+    // blocks with no essential dof in their patch (g.bess, formed at cdfem_mesh_set_structured: all but
+    // the boundary layer) load no essential flags (a wave-uniform branch; C3 apply 2,948 -> 2,786 us,
+    // profiles/r05/ab_bess/)
+    const bool bhas = g.bess == nullptr || g.bess[b] != 0;
     // this thread's element tile and x-stage rows (ix = a), loaded with the patch
     const int le = tid / DD, tt = tid - le * DD, a = tt % D1, bb = tt / D1;
     const int lex = le & 1, ley = (le >> 1) & 1, lez = le >> 2;
@@ -945,7 +952,8 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
             rv[k] = bload(br, offv[k]);
             mv[k] = bload(bm, offv[k]);
             ov[k] = bload(bo, offv[k]);
-            ev[k] = __builtin_amdgcn_raw_buffer_load_b8(be, in ? gid : kOOB, 0, 0);
+            ev[k] = 0;
+            if (bhas) ev[k] = __builtin_amdgcn_raw_buffer_load_b8(be, in ? gid : kOOB, 0, 0);
             const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
             if constexpr (XF) xv[k] = bload(bxf, writer ? offv[k] : kOOB);
         }

@@ -171,7 +171,30 @@ void free_mesh(cdfem_ctx *c)
     c->mr_fold_checked = false;
     dfree(c->d_small);
     dfree(c->d_hbpart);
+    dfree(c->d_bess);
     c->hb_nblk = 0;
+}
+
+// per brick (edge E elements, nb* bricks per axis): 1 if a lattice dof of its patch (E p + 1 per axis,
+// clipped to the lattice) is essential; the brick CG kernels skip the essential-flag loads elsewhere
+static void upload_brick_ess(cdfem_ctx *c, int E, int nbx, int nby, int nbz)
+{
+    const int64_t s1 = (int64_t)E * c->p, Lx = c->Lx, Ly = c->Ly, Lz = c->Lz;
+    std::vector<uint8_t> has((size_t)nbx * nby * nbz, 0);
+    for (int bz = 0; bz < nbz; ++bz)
+        for (int by = 0; by < nby; ++by)
+            for (int bx = 0; bx < nbx; ++bx) {
+                uint8_t h = 0;
+                for (int64_t z = bz * s1; z <= std::min(bz * s1 + s1, Lz - 1) && !h; ++z)
+                    for (int64_t y = by * s1; y <= std::min(by * s1 + s1, Ly - 1) && !h; ++y) {
+                        const uint8_t *row = c->h_ess.data() + (size_t)(z * Ly + y) * Lx;
+                        for (int64_t x = bx * s1; x <= std::min(bx * s1 + s1, Lx - 1); ++x) h |= row[x];
+                    }
+                has[((size_t)bz * nby + by) * nbx + bx] = h;
+            }
+    dfree(c->d_bess);
+    c->d_bess = dalloc<uint8_t>(has.size());
+    HIPCHK(hipMemcpy(c->d_bess, has.data(), has.size(), hipMemcpyHostToDevice));
 }
 
 // ---- profiling helpers ---------------------------------------------------------------------------
@@ -972,6 +995,7 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
             c->hb_nby = (ny + kHoBrickEdge - 1) / kHoBrickEdge;
             c->hb_nbz = (nz + kHoBrickEdge - 1) / kHoBrickEdge;
             c->hb_nblk = c->hb_nbx * c->hb_nby * c->hb_nbz;
+            upload_brick_ess(c, kHoBrickEdge, c->hb_nbx, c->hb_nby, c->hb_nbz);
             dfree(c->d_face);  // the high-order brick CG's patch buffer: allocated by its first solve
             return CDFEM_OK;
         }
@@ -979,6 +1003,7 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
         c->nby = (ny + kBrick - 1) / kBrick;
         c->nbz = (nz + kBrick - 1) / kBrick;
         c->nblk = c->nbx * c->nby * c->nbz;
+        upload_brick_ess(c, kBrick, c->nbx, c->nby, c->nbz);
         // brick permutation: block = brick (lexicographic), lane = ex + 4 (ey + 4 ez)
         std::vector<int32_t> perm((size_t)c->nblk * kLanes, -1);
         for (int b = 0; b < c->nblk; ++b) {

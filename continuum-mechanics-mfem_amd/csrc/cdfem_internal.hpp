@@ -153,6 +153,7 @@ struct cdfem_ctx {
     // 3D p = 3, 4 on a structured box: blocks of kHoBrickEdge^3 elements for the high-order brick CG
     // (brick_kernels.hip k_hobrick_cg; set_option "ho_brick")
     int hb_nbx = 0, hb_nby = 0, hb_nbz = 0, hb_nblk = 0;
+    uint8_t *d_bess = nullptr;          // per brick (block): 1 if a dof of its patch is essential
     int ho_brick = 1;                   // set_option "ho_brick": high-order CG through k_hobrick_cg + the brick update
     double *d_hbpart = nullptr;         // den partials summed in two stages: k_hobrick_cg's, and k_brick_cg's past
                                         // kDenFoldMaxParts bricks on one rank (one per brick)
