@@ -409,7 +409,10 @@ int brick_patch_side(const cdfem_ctx *c);
 bool brick_fits(const cdfem_ctx *c)
 {
     const double S = brick_patch_side(c), lim = (double)c->brick_limit;
-    return 8.0 * (double)c->nl < lim && 8.0 * (double)brick_count(c) * S * S * S < lim;
+    // a slab partition decides on the largest rank's sizes (cdfem_set_slab), the same on every rank
+    const double nl = (double)std::max<int64_t>(c->nl, c->part_mode == 1 ? c->slab_nl_max : 0);
+    const double nb = (double)std::max<int64_t>(brick_count(c), c->part_mode == 1 ? c->slab_nb_max : 0);
+    return 8.0 * nl < lim && 8.0 * nb * S * S * S < lim;
 }
 
 // the brick lattice of the context: 4^3-element bricks at p <= 2, 2^3-element blocks at p = 3, 4 (ho_brick)

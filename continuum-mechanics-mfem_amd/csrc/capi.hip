@@ -168,7 +168,8 @@ void free_mesh(cdfem_ctx *c)
     c->mesh_ready = c->pa_ready = c->dinv_ready = false;
     c->structured = false;
     c->epencil = false;
-    c->mr_fold_checked = false;
+    c->slab_nl_max = 0;
+    c->slab_nb_max = 0;
     dfree(c->d_small);
     dfree(c->d_hbpart);
     dfree(c->d_bess);
@@ -418,18 +419,15 @@ const double *solver_dinv(cdfem_ctx *c)
 }
 
 // cg_mr_fold all-reduces partial vectors, so every rank must take it and hold as many partials as the
-// others: the apply's (one per brick) and the update's (cg_den_fold_grid).  Decided once per partition
-// by every rank of a multi-rank solve from the all-reduced eligibility flags and the sums of the counts
-// and of their squares (equal on every rank, so every rank takes the same branch): the fold runs iff
-// every rank is eligible and the counts' variance is zero.
-// The result is kept until a local input changes (the options, the partition): ranks change their
-// options together, so they re-check together.
+// others: the apply's (one per brick) and the update's (cg_den_fold_grid).  Decided by every rank of a
+// multi-rank solve from the all-reduced eligibility flags and the sums of the counts and of their
+// squares (equal on every rank, so every rank takes the same branch): the fold runs iff every rank is
+// eligible and the counts' variance is zero.  The 5-double all-reduce runs on EVERY multi-rank brick CG
+// entry, whatever the rank's local state (a cached decision let one rank skip the
+// collective after an option change that left its own key unchanged while another rank's key moved).
 bool mr_fold_agreed(cdfem_ctx *c)
 {
     const double ok = cg_mr_fold(c) ? 1.0 : 0.0, nb = brick_count(c), ng = cg_den_fold_grid(c);
-    const double key = ok + 2.0 * (nb + 1e6 * ng);
-    if (c->mr_fold_checked && c->mr_fold_key == key) return c->mr_fold_agree;
-    c->mr_fold_key = key;
     double h[5] = {ok, nb, nb * nb, ng, ng * ng};
     if (!c->d_small) c->d_small = dalloc<double>(8);
     HIPCHK(hipMemcpyAsync(c->d_small, h, sizeof(h), hipMemcpyHostToDevice, c->stream));
@@ -437,9 +435,7 @@ bool mr_fold_agreed(cdfem_ctx *c)
     HIPCHK(hipMemcpyAsync(h, c->d_small, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     const double n = c->nranks;
-    c->mr_fold_agree = h[0] == n && h[2] * n == h[1] * h[1] && h[4] * n == h[3] * h[3];
-    c->mr_fold_checked = true;
-    return c->mr_fold_agree;
+    return h[0] == n && h[2] * n == h[1] * h[1] && h[4] * n == h[3] * h[3];
 }
 
 // brick-path CG (MFEM CGSolver arithmetic): per iteration k_brick_cg (direction + apply + den
@@ -1039,7 +1035,27 @@ int cdfem_set_slab(cdfem_ctx *c, int zlo_shared, int zhi_shared)
         c->zhi_shared = zhi_shared != 0;
         const int64_t n = c->Lx * c->Ly;
         c->part_mode = 1;
-        c->mr_fold_checked = false;
+        c->slab_nl_max = c->nl;
+        c->slab_nb_max = brick_count(c);
+        if (multi_rank(c)) {  // (collective: every rank declares its slab) each rank's counts in its own slots
+            const int R = c->nranks;
+            std::vector<double> h((size_t)2 * R, 0.0);
+            h[2 * c->rank] = (double)c->nl;
+            h[2 * c->rank + 1] = (double)brick_count(c);
+            double *d = dalloc<double>(h.size());
+            struct Free {
+                double *p;
+                ~Free() { (void)hipFree(p); }
+            } fr{d};
+            HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->stream));
+            comm_allreduce(c, d, 2 * R);
+            HIPCHK(hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            for (int k = 0; k < R; ++k) {
+                c->slab_nl_max = std::max<int64_t>(c->slab_nl_max, (int64_t)h[2 * k]);
+                c->slab_nb_max = std::max<int64_t>(c->slab_nb_max, (int64_t)h[2 * k + 1]);
+            }
+        }
         c->skip_lo = c->zlo_shared ? n : 0;  // the lower plane is owned by the rank below
         for (auto &b : c->d_if) {
             dfree(b);
@@ -1797,8 +1813,8 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 1) throw ArgError("brick_xcd must be 0 or 1");
             c->brick_xcd = value;
         } else if (k == "brick_byte_limit") {
-            if (value < 1) throw ArgError("brick_byte_limit must be 1..2^31-1");
-            c->brick_limit = value;
+            if (value < 0) throw ArgError("brick_byte_limit must be 0 (the default 2^31) or 1..2^31-1");
+            c->brick_limit = value == 0 ? (int64_t)1 << 31 : value;
         } else if (k == "cg_mr_fold") {
             if (value != 0 && value != 1) throw ArgError("cg_mr_fold must be 0 or 1");
             c->cg_mr_fold = value;
@@ -1820,7 +1836,6 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "cg_den_fold") {
             if (value != 0 && (value < 64 || value > 16384)) throw ArgError("cg_den_fold must be 0 or 64..16384");
             c->cg_den_fold = value;
-            c->mr_fold_checked = false;
         } else if (k == "brick_upd_pb") {
             if (value != 0 && value != 1) throw ArgError("brick_upd_pb must be 0 or 1");
             c->brick_upd_pb = value;

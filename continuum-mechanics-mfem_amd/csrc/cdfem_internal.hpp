@@ -174,6 +174,10 @@ struct cdfem_ctx {
     // 2^31 bytes (8 N_L and 8 S^3 nblk); larger boxes take the generic 64-bit-indexed element kernels.
     // set_option "brick_byte_limit" lowers the bound (tests force the fallback on small boxes).
     int64_t brick_limit = (int64_t)1 << 31;
+    // slab partition: the largest L-vector and brick count over all ranks (all-reduced by cdfem_set_slab),
+    // so brick_fits takes the same decision on every rank (slabs of different sizes near the
+    // bound would otherwise send ranks down CG paths with different collective sequences)
+    int64_t slab_nl_max = 0, slab_nb_max = 0;
     int ncu = 0;                        // compute units of the device
     int zlo_shared = 0;                 // local gz=0 plane owned by the rank below (slabs)
     int zhi_shared = 0;                 // local gz=Lz-1 plane shared with the rank above
@@ -236,8 +240,6 @@ struct cdfem_ctx {
     int brick_mult_pb = 1;              // set_option "brick_mult_pb": structured Mult through the patch buffer
     int cg_beta_fold = 1;               // set_option "cg_beta_fold": brick CG betanom step in the next apply
     int cg_mr_fold = 1;                 // set_option "cg_mr_fold": both folds on several ranks (partials all-reduced)
-    bool mr_fold_checked = false, mr_fold_agree = false;  // every rank holds as many partials (checked once)
-    double mr_fold_key = 0.0;           //   for these local inputs (eligibility, counts)
     double *d_small = nullptr;          // a few doubles of device scratch (mr_fold_agreed's all-reduce)
     int cg_den_fold = 1024;             // set_option "cg_den_fold": brick CG den step in the update (N workgroups; 0 off)
     int brick_upd_pb = 1;               // set_option "brick_upd_pb": predicated-load face sums in the brick CG update

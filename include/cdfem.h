@@ -270,7 +270,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  * "brick_byte_limit": 2^31 (default) — the structured brick kernels address their vectors and patch
  *              buffer with 32-bit buffer offsets (out-of-range marker 2^31), so a box whose 8 N_L or
  *              8 S^3 bricks reach the limit runs the generic element kernels instead; lower values
- *              force that fallback (tests).
+ *              force that fallback (tests); 0 restores the default.  On a slab partition the
+ *              decision is taken on the largest rank's sizes (all-reduced by cdfem_set_slab), so
+ *              every rank runs the same CG path.
  * "brick_upd_pb": 1 (default) — the brick CG update (k_cg_update_faces) reads each dof's 1-8 patch
  *              entries as eight predicated buffer loads (absent ones out of range) instead of
  *              branching on the face planes (0); bitwise the same sums.

@@ -1862,6 +1862,81 @@ ORC_API void orc_pa_mult(orc_pa *pa, const int *ess_marker, const double *x, dou
     pa->ess = NULL;
 }
 
+/* diag_e[i] += sum_q F[q] wx[qx][ix] wy[qy][iy] wz[qz][iz] (i = ix + D (iy + D iz)): one separable term
+ * of an element diagonal, contracted x, then y, then z (the shape of MFEM's PA*AssembleDiagonal kernels) */
+static void pa_diag_term(int D, int Q, const double *F, const double *wx, const double *wy, const double *wz,
+                         double *diag)
+{
+    double tx[8][8][8], ty[8][8][8];  /* [qz][qy][ix], [qz][iy][ix] */
+    for (int qz = 0; qz < Q; qz++)
+        for (int qy = 0; qy < Q; qy++)
+            for (int ix = 0; ix < D; ix++) {
+                double a = 0.0;
+                for (int qx = 0; qx < Q; qx++) a += wx[qx * D + ix] * F[qx + Q * (qy + Q * qz)];
+                tx[qz][qy][ix] = a;
+            }
+    for (int qz = 0; qz < Q; qz++)
+        for (int iy = 0; iy < D; iy++)
+            for (int ix = 0; ix < D; ix++) {
+                double a = 0.0;
+                for (int qy = 0; qy < Q; qy++) a += wy[qy * D + iy] * tx[qz][qy][ix];
+                ty[qz][iy][ix] = a;
+            }
+    for (int iz = 0; iz < D; iz++)
+        for (int iy = 0; iy < D; iy++)
+            for (int ix = 0; ix < D; ix++) {
+                double a = 0.0;
+                for (int qz = 0; qz < Q; qz++) a += wz[qz * D + iz] * ty[qz][iy][ix];
+                diag[ix + D * (iy + D * iz)] += a;
+            }
+}
+
+/*
+ * [MFEM-ext] BilinearForm::AssembleDiagonal at AssemblyLevel::PARTIAL: every integrator's
+ * AssembleDiagonalPA on the element (PADiffusionDiagonal3D: sum_q of the symmetric point matrix against
+ * the products of the 1D value / derivative tables, off-diagonal components twice; the convection and
+ * mass diagonals the same way with their point data), then ElementRestriction::MultTranspose (the E->L
+ * sum over every element holding the dof).  Unconstrained: the Jacobi smoother of FormLinearSystem sets
+ * the essential entries to 1 itself.  The diagonal the GPU's OperatorJacobiSmoother (d_dinv) inverts.
+ */
+ORC_API void orc_pa_diag(orc_pa *pa, double *y)
+{
+    const int D = pa->d1, Q = pa->nq, nd = pa->nd, q3 = pa->q3, ne = pa->ne;
+    double BB[64], BG[64], GG[64];
+    for (int k = 0; k < Q * D; k++) {
+        BB[k] = pa->B[k] * pa->B[k];
+        BG[k] = pa->B[k] * pa->G[k];
+        GG[k] = pa->G[k] * pa->G[k];
+    }
+    #pragma omp parallel for schedule(static)
+    for (int e = 0; e < ne; e++) {
+        double *de = pa->ye + (size_t)e * nd, F[512];
+        for (int i = 0; i < nd; i++) de[i] = 0.0;
+        if (pa->use_diff) {
+            const double *Dq = pa->qd_d + (size_t)e * 6 * q3;
+            /* components d00 d01 d02 d11 d12 d22: (x, y, z) weight tables and the symmetric factor */
+            const double *W[6][3] = {{GG, BB, BB}, {BG, BG, BB}, {BG, BB, BG}, {BB, GG, BB}, {BB, BG, BG}, {BB, BB, GG}};
+            const double f[6] = {1.0, 2.0, 2.0, 1.0, 2.0, 1.0};
+            for (int k = 0; k < 6; k++) {
+                for (int q = 0; q < q3; q++) F[q] = f[k] * Dq[k * q3 + q];
+                pa_diag_term(D, Q, F, W[k][0], W[k][1], W[k][2], de);
+            }
+        }
+        if (pa->use_conv) {
+            const double *Cq = pa->qd_c + (size_t)e * 3 * q3;
+            const double *W[3][3] = {{BG, BB, BB}, {BB, BG, BB}, {BB, BB, BG}};
+            for (int k = 0; k < 3; k++) pa_diag_term(D, Q, Cq + (size_t)k * q3, W[k][0], W[k][1], W[k][2], de);
+        }
+        if (pa->use_mass) pa_diag_term(D, Q, pa->qd_m + (size_t)e * q3, BB, BB, BB, de);
+    }
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < pa->nl; i++) {
+        double acc = 0.0;
+        for (int64_t k = pa->off[i]; k < pa->off[i + 1]; k++) acc += pa->ye[pa->idx[k]];
+        y[i] = acc;
+    }
+}
+
 static void pa_con_op(const void *op, const double *x, double *y) { pa_apply((const orc_pa *)op, x, y, 1); }
 
 /* CGSolver on the ConstrainedOperator of the PA form (dinv: Jacobi, ess entries 1) */

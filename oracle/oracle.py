@@ -75,6 +75,7 @@ def lib():
                                    C.c_int]
         L.orc_pa_free.argtypes = [C.c_void_p]
         L.orc_pa_mult.argtypes = [C.c_void_p, ip, dp, dp]
+        L.orc_pa_diag.argtypes = [C.c_void_p, dp]
         L.orc_pa_cg.argtypes = [C.c_void_p, ip, dp, dp, dp, C.c_double, C.c_double, C.c_int, ip, dp]
         L.orc_stream_triad.argtypes = [C.c_int64, C.c_int]
         L.orc_stream_triad.restype = C.c_double
@@ -363,6 +364,22 @@ class PA:
         y = np.empty(self.nl)
         lib().orc_pa_mult(self.h, _i(self.bdr) if constrained else None, _d(x), _d(y))
         return y
+
+    def diag(self):
+        """AssembleDiagonal at the PA level (orc_pa_diag: per-integrator sum-factorised element
+        diagonals, then the E->L sum); unconstrained, as the FA CSR's diagonal."""
+        y = np.empty(self.nl)
+        lib().orc_pa_diag(self.h, _d(y))
+        return y
+
+    def form_linear_system(self, X, b):
+        """FormLinearSystem on the PA operator (ConstrainedOperator::EliminateRHS, DIAG_ONE): B = b - A X_e
+        with X_e = X on the essential dofs and 0 elsewhere, then B_ess = X_ess."""
+        ess = self.bdr != 0
+        xe = np.where(ess, X, 0.0)
+        B = np.asarray(b, dtype=np.float64) - self.mult(xe)
+        B[ess] = X[ess]
+        return B
 
     def cg(self, b, dinv=None, rel_tol=1e-12, abs_tol=0.0, max_iter=500):
         """CGSolver on the constrained operator (b: FormLinearSystem's B, dinv: 1 / diag with ess 1)."""

@@ -607,3 +607,60 @@ def test_gpu_c5_per_rank_slabs(tmp_path, world):
         np.testing.assert_array_equal(xr[r + 1][:plane], xr[r][-plane:])
     xg = np.concatenate([xr[0]] + [x[plane:] for x in xr[1:]])
     assert np.linalg.norm(xg - xs) <= 1e-12 * np.linalg.norm(xs)
+
+
+# ---------------------------------------------------------------------------------------------
+# the multi-rank fold decision is a collective taken on every solve.  Uneven slabs where
+# one rank holds more bricks than kMrFoldMaxParts (8,192: that rank is not eligible for the fold, the
+# other is), with cg_mr_fold toggled on every rank between solves: each solve must enter the same
+# collectives on both ranks (no hang, no mixed sums) and equal the one-context solve.
+UN_N, UN_PER, UN_ITERS = 128, (40, 8), 15
+
+
+def _gpu_uneven_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    import cdfem
+    dist = _init(rank, world, port)
+    z0 = sum(UN_PER[:rank])
+    m = cdfem.box_mesh(3, (UN_N, UN_N, sum(UN_PER)), P, z_range=(z0, z0 + UN_PER[rank]), with_coords=False)
+    ctx = cdfem.Context(0)
+    ctx.upload_mesh(m).set_structured(UN_N, UN_N, UN_PER[rank])
+    ctx.comm_init_torch()
+    ctx.set_slab(rank > 0, rank < world - 1)
+    ctx.pa_setup(kinds=7, kappa=KAPPA, alpha=1.0, conv=CONV, mass=S)
+    b = np.random.default_rng(900 + rank).uniform(-1, 1, m.nl)
+    np.save(os.path.join(out_dir, f"b{rank}.npy"), b)
+    _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+    xs = []
+    for opt, val in (("cg_mr_fold", 1), ("cg_mr_fold", 0), ("cg_mr_fold", 1), ("cg_beta_fold", 0), ("cg_beta_fold", 1)):
+        ctx.set_option(opt, val)
+        X, info = ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=UN_ITERS,
+                            check_every=5)
+        assert info["iterations"] == UN_ITERS
+        xs.append(X)
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), np.stack(xs))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_uneven_slabs_fold_toggle(tmp_path):
+    import cdfem
+    world = 2
+    mp.start_processes(_gpu_uneven_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    plane = (P * UN_N + 1) ** 2
+    bfull = _gathered_rhs(tmp_path, plane, world)
+    m = cdfem.box_mesh(3, (UN_N, UN_N, sum(UN_PER)), P, with_coords=False)
+    with cdfem.Context(0) as ctx:
+        ctx.upload_mesh(m).set_structured(UN_N, UN_N, sum(UN_PER))
+        ctx.pa_setup(kinds=7, kappa=KAPPA, alpha=1.0, conv=CONV, mass=S)
+        _, B = ctx.form_linear_system(np.zeros(m.nl), bfull)
+        xs, info = ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=UN_ITERS)
+    x0, x1 = np.load(tmp_path / "x0.npy"), np.load(tmp_path / "x1.npy")
+    for k in range(x0.shape[0]):
+        np.testing.assert_array_equal(x1[k][:plane], x0[k][-plane:])
+        xg = np.concatenate([x0[k], x1[k][plane:]])
+        assert np.linalg.norm(xg - xs) <= 1e-12 * np.linalg.norm(xs), k

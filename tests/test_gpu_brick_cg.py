@@ -253,7 +253,7 @@ def test_brick_byte_limit_falls_back_to_generic(gpu_ctx):
             out[lim] = dict(y=gpu_ctx.mult(x), yc=gpu_ctx.mult(x, constrained=True), x=xg, it=ig["iterations"],
                             ndir=ndir)
     finally:
-        gpu_ctx.set_option("brick_byte_limit", 2**31 - 1)
+        gpu_ctx.set_option("brick_byte_limit", 0)  # 0: back to the default bound, 2^31 bytes
         gpu_ctx.profile(False)
     assert out[None]["ndir"] == 0 and out[4096]["ndir"] > 0
     yo = A.mult(x)
@@ -263,4 +263,4 @@ def test_brick_byte_limit_falls_back_to_generic(gpu_ctx):
         assert np.linalg.norm(out[lim]["x"] - xo) <= 1e-11 * np.linalg.norm(xo)
     assert np.abs(out[4096]["yc"] - out[None]["yc"]).max() <= 1e-13 * np.abs(out[None]["yc"]).max()
     with pytest.raises(cdfem.CdfemError):
-        gpu_ctx.set_option("brick_byte_limit", 0)
+        gpu_ctx.set_option("brick_byte_limit", -1)

@@ -17,6 +17,14 @@ C4 (configs[3]): Kuhn 55^3 x 6 tets, P2, 1,367,631 DoFs, GPU-assembled FA CSR (p
 1e-13), Mult / diagonal / FormLinearSystem 1e-13, and 60 GMRES(30) + Jacobi inner steps (two restart
 cycles, the bench's step) with tolerances 0: relative L2 <= 1e-11 against the oracle's PETSc KSPGMRES
 restatement.
+C3 (configs[2]): 128^3 hex, p = 4, 135,005,697 DoFs, kinds 7, through the block CG (k_hobrick_cg: 2^3-element
+blocks, the den partials summed in two stages, 262,144 blocks and a 1.53 GB patch buffer) and C5's mesh
+(configs[4]): 256^3 hex, p = 2, 135,005,697 DoFs on ONE GPU (262,144 bricks: past kDenFoldMaxParts, so the
+den step goes through the two-stage finalizer).  Both against the oracle's host partial assembly (O.PA:
+MFEM's per-integrator point data and sum-factorised element loops, pinned to the FA CSR by
+tests/test_oracle.py): Mult, constrained Mult, diagonal (orc_pa_diag) and FormLinearSystem <= 1e-13, and
+20 fixed Jacobi-CG iterates on the bench's RHS seed <= 1e-11.  The size-dependent code of both paths runs
+only at these sizes.  Host memory of the oracle: ~36 GB of point data at C3, ~86 GB at C5.
 
 The oracle runs on the box's CPU share (OpenMP): assembling either matrix takes seconds
 (bench.py's cpu_baseline assembles both), the CG and GMRES legs a few seconds more.
@@ -151,3 +159,44 @@ def test_c5_one_gpu_folds_bounded(gpu_ctx):
     assert i1["iterations"] == i0["iterations"] == 20
     assert np.linalg.norm(x1 - x0) <= 1e-12 * np.linalg.norm(x0)
     assert abs(i1["final_norm"] - i0["final_norm"]) <= 1e-10 * i0["initial_norm"]
+
+
+def _pa_full_size(gpu_ctx, n, p, kernel):
+    """Full-size parity of the default CG path on an n^3 box of order p against the host PA."""
+    om = O.BoxMesh(3, n, p)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(n, n, n)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    assert gpu_ctx.kernel_name(cdfem.K_APPLY) == kernel
+    pa = O.PA(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=7)
+    om.verts = None  # (the point data is formed; the host copy of the geometry is not needed again)
+    x = np.random.default_rng(20261016).uniform(-1, 1, om.nl)
+    assert _relmax(gpu_ctx.mult(x), pa.mult(x)) <= TOL_MULT
+    assert _relmax(gpu_ctx.mult(x, constrained=True), pa.mult(x, constrained=True)) <= TOL_MULT
+    del x
+    diag = pa.diag()
+    assert _relmax(gpu_ctx.diagonal(), diag) <= TOL_MULT
+    ess = om.bdr != 0
+    dinv = np.where(ess, 1.0, 1.0 / np.where(ess, 1.0, diag))
+    del diag
+    b = np.random.default_rng(20261015).uniform(-1, 1, om.nl)   # bench.py's RHS
+    u = np.zeros(om.nl)
+    Bo = pa.form_linear_system(u, b)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    assert _relmax(B, Bo) <= TOL_MULT
+    del b, B
+    xo, io = pa.cg(Bo, dinv=dinv, rel_tol=0.0, abs_tol=0.0, max_iter=20)
+    xg, ig = gpu_ctx.solve(Bo, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=20)
+    assert io["iterations"] == ig["iterations"] == 20 and not ig["converged"]
+    assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo)
+    assert abs(ig["final_norm"] - io["final_norm"]) <= 1e-9 * io["final_norm"]
+
+
+def test_c3_full_size_oracle_parity(gpu_ctx):
+    """BASELINE configs[2] (128^3, p = 4) on the bench's block CG against the host PA oracle."""
+    _pa_full_size(gpu_ctx, 128, 4, "k_hobrick_cg")
+
+
+def test_c5_one_gpu_full_size_oracle_parity(gpu_ctx):
+    """BASELINE configs[4]'s 256^3 p = 2 mesh on one GPU (262,144 bricks, the two-stage den sum)
+    against the host PA oracle."""
+    _pa_full_size(gpu_ctx, 256, 2, "k_brick_cg")

@@ -427,7 +427,7 @@ def test_ho_brick_c3_full_size_residual(gpu_ctx):
     n, p = 128, 4
     gm = cdfem.box_mesh(3, n, p, with_coords=False)
     b = np.random.default_rng(20261015).uniform(-1, 1, gm.nl)
-    out = {}
+    out, rec = {}, {}
     try:
         for hb in (1, 0):
             gpu_ctx.set_option("ho_brick", hb)
@@ -435,9 +435,18 @@ def test_ho_brick_c3_full_size_residual(gpu_ctx):
             gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
             _, B = gpu_ctx.form_linear_system(np.zeros(gm.nl), b)
             out[hb] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=20)
+            # the true constrained residual r = B - A_c x in the solver's norm sqrt(r . M^-1 r)
+            dg = gpu_ctx.diagonal()
+            ess = np.zeros(gm.nl, dtype=bool)
+            ess[gm.ess] = True
+            r = B - gpu_ctx.mult(out[hb][0], constrained=True)
+            rec[hb] = np.sqrt(np.dot(r, np.where(ess, r, r / np.where(ess, 1.0, dg))))
+            del dg, r, ess
     finally:
         gpu_ctx.set_option("ho_brick", 1)
     assert out[1][1]["iterations"] == out[0][1]["iterations"] == 20
+    for hb in (1, 0):  # the recursive residual of the CG recursion equals the recomputed one
+        assert abs(rec[hb] - out[hb][1]["final_norm"]) <= 1e-9 * out[hb][1]["initial_norm"], hb
     assert np.linalg.norm(out[1][0] - out[0][0]) <= 1e-12 * np.linalg.norm(out[0][0])
     assert abs(out[1][1]["final_norm"] - out[0][1]["final_norm"]) <= 1e-10 * out[0][1]["initial_norm"]
 

@@ -195,6 +195,26 @@ def test_oracle_pa_matches_fa(shape, p, pert, kinds):
     assert np.linalg.norm(x2 - x1) <= 1e-12 * np.linalg.norm(x1)
 
 
+@pytest.mark.parametrize("shape,p,pert,kinds", [((3, 4, 2), 2, 0.2, 7), ((2, 3, 2), 4, 0.15, 7), ((3, 2, 2), 3, 0.1, 5),
+                                                 ((2, 2, 3), 1, 0.2, 2), ((3, 3, 3), 2, 0.0, 4)])
+def test_oracle_pa_diag_and_fls_match_fa(shape, p, pert, kinds):
+    """orc_pa_diag (MFEM's AssembleDiagonal at the PA level: per-integrator sum-factorised element
+    diagonals, E->L sum) is the assembled CSR's diagonal, and the PA FormLinearSystem (B = b - A X_e,
+    B_ess = X_ess) the CSR elimination's B, both to 1e-13 on perturbed (non-affine) meshes.  These pin
+    the host PA that checks the full-size C3 / C5 runs (tests/test_gpu_full_size.py)."""
+    om = O.BoxMesh(3, shape, p, perturb=pert)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=(1.0, -2.0, 0.5), kinds=kinds)
+    pa = O.PA(om, kappa=0.1, alpha=1.0, s=1.0, c=(1.0, -2.0, 0.5), kinds=kinds)
+    do = A.diag()
+    assert np.abs(pa.diag() - do).max() <= 1e-13 * np.abs(do).max()
+    rng = np.random.default_rng(2)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    _, Bo = O.form_linear_system(A, om.bdr, u, b)
+    assert np.abs(pa.form_linear_system(u, b) - Bo).max() <= 1e-13 * np.abs(Bo).max()
+
+
 def test_oracle_cg_indefinite_preconditioner():
     """MFEM CGSolver stops unconverged when (r, M^-1 r) < 0: at iteration 0 (nom0 < 0) or at the
     iteration where betanom turns negative (kK + sM with s = -124: 210 negative Jacobi entries)."""
