@@ -61,6 +61,9 @@ def parse():
                     help="per-launch HBM bytes of the apply kernel from a rocprofv3 --pmc pass")
     ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "sq_counters.json"),
                     help="SQ counter record of the apply kernel (tools/sq_record.py): roofline.limiter")
+    ap.add_argument("--rocprof-json", default=os.path.join(ROOT, "profiles", "rocprof_kernels.json"),
+                    help="rocprofv3 kernel-trace averages of the apply kernel (tools/rocprof_avg.py): "
+                         "roofline.rocprof_avg_us and its source CSV")
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--path", choices=["brick", "generic"], default=None,
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
@@ -453,7 +456,13 @@ def main_c4(args):
         o_ms, o_cnt = ctx.profile_read(cdfem.K_ORTH)
         ctx.profile(False)
         if cnt:
-            per = ms / cnt * 1e-3
+            # every solve ends with an apply that returns at its first check (the update before it set
+            # `done`, or its betanom step stops the solve): a launch with no work.  The roofline
+            # divides the launch's bytes by the FULL launches' average (>= half the median: the
+            # early-return ones take a few us); the all-launch average is kept beside it
+            full = each[each >= 0.5 * np.median(each)] if len(each) else each
+            per_all = ms / cnt * 1e-3
+            per = float(full.mean()) * 1e-3 if len(full) else per_all
             bytes_ = ctx.kernel_bytes(cdfem.K_APPLY)
             traffic = None
             if os.path.exists(args.traffic_json):
@@ -620,6 +629,7 @@ def main():
             step()
         ctx.synchronize()
         ms, cnt = ctx.profile_read(cdfem.K_APPLY)
+        each = ctx.profile_launches(cdfem.K_APPLY)
         # the other kernels: one extra (untimed) step with events around every kernel
         ctx.profile(False)
         ctx.set_option("profile_mask", -1)
@@ -631,7 +641,13 @@ def main():
         d_ms, d_cnt = ctx.profile_read(cdfem.K_DIRECTION)
         ctx.profile(False)
         if cnt:
-            per = ms / cnt * 1e-3
+            # every solve ends with an apply that returns at its first check (the update before it set
+            # `done`, or its betanom step stops the solve): a launch with no work.  The roofline
+            # divides the launch's bytes by the FULL launches' average (>= half the median: the
+            # early-return ones take a few us); the all-launch average is kept beside it
+            full = each[each >= 0.5 * np.median(each)] if len(each) else each
+            per_all = ms / cnt * 1e-3
+            per = float(full.mean()) * 1e-3 if len(full) else per_all
             bytes_ = ctx.kernel_bytes(cdfem.K_APPLY)
             achieved = bytes_ / per / 1e9
             traffic = None
@@ -666,10 +682,26 @@ def main():
                     roof = {"bound": "hbm", **hbm_view, "valu_view": valu_view}
             else:
                 roof = {"bound": "hbm", **hbm_view}
+            rp = None
+            if os.path.exists(args.rocprof_json):
+                try:
+                    rp = json.load(open(args.rocprof_json)).get(key)
+                except Exception:
+                    rp = None
             roof.update({
                     "kernel": kernel_label(ctx.kernel_name(cdfem.K_APPLY), affine),
                     "algorithmic_bytes_per_launch": bytes_, "avg_launch_us": round(per * 1e6, 2),
-                    "launches": cnt,
+                    "avg_launch_us_all": round(per_all * 1e6, 2),
+                    "launches": cnt, "full_launches": int(len(full)),
+                    "avg_note": "avg_launch_us: the full launches (each solve's last apply returns at its first check "
+                                "and is left out: avg_launch_us_all keeps it); achieved/frac use avg_launch_us",
+                    # the same kernel in a rocprofv3 --kernel-trace of the bench (full launches), and the CSV of its
+                    # per-launch durations the figure is recomputed from (tools/rocprof_avg.py)
+                    "rocprof_avg_us": rp.get("avg_us_full") if rp else None,
+                    "rocprof_avg_all_us": rp.get("avg_us_all") if rp else None,
+                    "rocprof_source": rp.get("source") if rp else None,
+                    "rocprof_frac_hbm": (round(bytes_ / (rp["avg_us_full"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+                                         if rp and rp.get("avg_us_full") else None),
                     # what binds the kernel per its SQ counters (issue / memory / LDS), beside the closer roofline
                     "limiter": limiter["limiter"] if limiter else None,
                     "limiter_counters": limiter,

@@ -232,6 +232,7 @@ void prof_collect(cdfem_ctx *c)
             HIPCHK(hipEventElapsedTime(&ms, s.ev[2 * i], s.ev[2 * i + 1]));
             s.total_ms += ms;
             s.count++;
+            s.each.push_back(ms);
         }
         s.used = 0;
     }
@@ -1784,7 +1785,7 @@ int cdfem_stream_bench(cdfem_ctx *c, int mode, size_t bytes, int reps, double *g
 int cdfem_fp64_bench(cdfem_ctx *c, int mode, int reps, double *tflops)
 {
     return guarded(c, [&] {
-        if (!tflops || reps < 1 || mode < 0 || mode > 1) throw ArgError("bad fp64 bench arguments");
+        if (!tflops || reps < 1 || mode < 0 || mode > 4) throw ArgError("bad fp64 bench arguments");
         double *out = dalloc<double>(1), flops = 0.0;
         HIPCHK(launch_fp64_probe(c, mode, out, &flops));  // warm-up
         hipEvent_t e0, e1;
@@ -1907,6 +1908,7 @@ int cdfem_profile_reset(cdfem_ctx *c)
             s.used = 0;
             s.total_ms = 0.0;
             s.count = 0;
+            s.each.clear();
         }
         return CDFEM_OK;
     });
@@ -1918,6 +1920,19 @@ int cdfem_profile_read(cdfem_ctx *c, int k, double *total_ms, int64_t *count)
         if (k < 0 || k >= CDFEM_K_COUNT) throw ArgError("bad kernel id");
         if (total_ms) *total_ms = c->prof[k].total_ms;
         if (count) *count = c->prof[k].count;
+        return CDFEM_OK;
+    });
+}
+
+int cdfem_profile_launches(cdfem_ctx *c, int k, double *ms, int64_t cap, int64_t *count)
+{
+    return guarded(c, [&] {
+        if (k < 0 || k >= CDFEM_K_COUNT) throw ArgError("bad kernel id");
+        const auto &e = c->prof[k].each;
+        const int64_t n = (int64_t)e.size();
+        if (count) *count = n;
+        if (ms)
+            for (int64_t i = 0; i < std::min(cap, n); ++i) ms[i] = e[i];
         return CDFEM_OK;
     });
 }

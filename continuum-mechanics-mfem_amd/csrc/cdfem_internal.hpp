@@ -119,6 +119,7 @@ struct ProfileSlot {
     int used = 0;
     double total_ms = 0.0;
     int64_t count = 0;
+    std::vector<float> each;  // per-launch ms since the last reset (cdfem_profile_launches)
 };
 
 }  // namespace cdfem

@@ -157,6 +157,37 @@ __global__ void __launch_bounds__(256) k_fp64_mfma(double seed, double *out)
     if (s == 12345.678) out[0] = s;
 }
 
+// Mixed probe (the MFMA-vs-VALU question of the brick kernels): every wave interleaves
+// 4 v_mfma_f64_16x16x4_f64 chains with NV independent v_fma_f64 chains per lane in one loop.  If the
+// matrix core and the VALU run concurrently, the rate approaches the sum of the two single-pipe rates;
+// if they share one f64 pipe, it stays at the single rate.
+template <int NV>
+__global__ void __launch_bounds__(256) k_fp64_mixed(double seed, double *out)
+{
+    const double a = seed + (threadIdx.x & 63), b = 1.0 + 1e-9 * seed;
+    v4d_t acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = v4d_t{0.0, 0.0, 0.0, (double)k};
+    double v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = seed + threadIdx.x + k;
+    const double m = 1.0 + 1e-9 * seed, c = 1e-12;
+    for (int i = 0; i < kFp64Iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
+#pragma unroll
+            for (int j = k; j < NV; j += 4) v[j] = fma(v[j], m, c);
+        }
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) s += v[k];
+    if (s == 12345.678) out[0] = s;
+}
+
 hipError_t launch_fp64_probe(cdfem_ctx *c, int mode, double *out, double *flops)
 {
     const dim3 grid(256 * 8), block(256);
@@ -167,6 +198,12 @@ hipError_t launch_fp64_probe(cdfem_ctx *c, int mode, double *out, double *flops)
     } else if (mode == 1) {
         hipLaunchKernelGGL(k_fp64_mfma, grid, block, 0, c->stream, 1.0, out);
         *flops = waves * 4.0 * 2048.0 * kFp64Iters;
+    } else if (mode == 2 || mode == 3 || mode == 4) {  // mixed: 16 / 32 / 64 VALU FMAs per 4 MFMAs
+        const int nv = mode == 2 ? 16 : mode == 3 ? 32 : 64;
+        if (mode == 2) hipLaunchKernelGGL(k_fp64_mixed<16>, grid, block, 0, c->stream, 1.0, out);
+        if (mode == 3) hipLaunchKernelGGL(k_fp64_mixed<32>, grid, block, 0, c->stream, 1.0, out);
+        if (mode == 4) hipLaunchKernelGGL(k_fp64_mixed<64>, grid, block, 0, c->stream, 1.0, out);
+        *flops = waves * (4.0 * 2048.0 + 64.0 * 2.0 * nv) * kFp64Iters;
     } else {
         return hipErrorInvalidValue;
     }

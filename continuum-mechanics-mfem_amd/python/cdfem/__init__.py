@@ -109,6 +109,7 @@ def _declare(L):
         "cdfem_kernel_bytes": (C.c_int, [vp, C.c_int, _dp]),
         "cdfem_kernel_flops": (C.c_int, [vp, C.c_int, _dp]),
         "cdfem_kernel_name": (C.c_int, [vp, C.c_int, C.c_char_p, C.c_size_t]),
+        "cdfem_profile_launches": (C.c_int, [vp, C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
         "cdfem_comm_unique_id": (C.c_int, [C.c_char_p]),
         "cdfem_comm_init_rccl": (C.c_int, [vp, C.c_int, C.c_int, C.c_char_p]),
         "cdfem_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, ALLREDUCE_FN, EXCHANGE_FN, vp]),
@@ -753,6 +754,14 @@ class Context:
         ms, n = C.c_double(), C.c_int64()
         self._chk(self.L.cdfem_profile_read(self.h, kernel, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def profile_launches(self, kernel):
+        """Per-launch milliseconds of kernel id since the last reset (launch order)."""
+        n = C.c_int64()
+        self._chk(self.L.cdfem_profile_launches(self.h, kernel, None, 0, C.byref(n)))
+        out = np.zeros(n.value)
+        self._chk(self.L.cdfem_profile_launches(self.h, kernel, out.ctypes.data, n.value, C.byref(n)))
+        return out
 
     def kernel_name(self, kernel):
         """HIP kernel name of kernel id in the current configuration (assembled-operator apply)."""

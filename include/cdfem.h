@@ -226,7 +226,9 @@ int cdfem_stream_bench(cdfem_ctx *ctx, int mode, size_t bytes, int reps, double 
 
 /* f64 compute-rate probe (diagnostic; backs DESIGN.md's VALU-vs-MFMA choice for the high-order
  * contractions): mode 0 = v_fma_f64 (8 independent chains per lane), 1 = v_mfma_f64_16x16x4_f64
- * (4 independent accumulators per wave); *tflops = achieved f64 TFLOP/s over `reps` launches. */
+ * (4 independent accumulators per wave), 2 / 3 / 4 = both in one loop (4 MFMA chains interleaved
+ * with 16 / 32 / 64 v_fma_f64 per lane: does the matrix core run beside the VALU?);
+ * *tflops = achieved f64 TFLOP/s over `reps` launches. */
 int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
 
 /* ---- tuning knobs (performance only; results identical to rounding) --------------------------
@@ -354,6 +356,9 @@ int cdfem_profile_enable(cdfem_ctx *ctx, int on);
 int cdfem_profile_reset(cdfem_ctx *ctx);
 /* total milliseconds and launch count of kernel id (CDFEM_K_*) since the last reset */
 int cdfem_profile_read(cdfem_ctx *ctx, int kernel, double *total_ms, int64_t *count);
+/* per-launch milliseconds of kernel id since the last reset, in launch order: the first min(cap, count)
+ * into ms, the count into *count (bench.py separates the full launches from the early-return ones) */
+int cdfem_profile_launches(cdfem_ctx *ctx, int kernel, double *ms, int64_t cap, int64_t *count);
 /* algorithmic bytes moved by one launch of kernel id (see DESIGN.md for the per-unit figures); on
  * structured boxes the figure is that of the kernel the CG solve launches (the brick CG kernels, the
  * fused high-order apply with its direction fold)                                                 */
