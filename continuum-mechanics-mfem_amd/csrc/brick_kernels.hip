@@ -550,7 +550,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            double *__restrict__ face, const double *__restrict__ qd, const uint8_t *__restrict__ ess,
            const Tab<D1, Q1> T, const BrickGeom g, int zlo_shared, double *__restrict__ part,
            KrylovState *__restrict__ st, double *__restrict__ x, const double *__restrict__ upart, int nupart,
-           int kk)
+           int kk, double *__restrict__ gsum, uint32_t *__restrict__ gcnt, int grp, int nbrick)
 {
     constexpr int P = D1 - 1;
     constexpr int S = kBrick * P + 1;
@@ -733,7 +733,31 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         }
     }
     den = wave_sum(den);
-    if (t == 0) part[b] = den;
+    if (grp <= 1) {
+        if (t == 0) part[b] = den;
+        return;
+    }
+    // grouped partials (den_grp > 1): the partial goes out write-through (sc1: an agent-scope relaxed
+    // store), the wave waits for it, then counts its arrival on the group's agent-scope counter; the
+    // brick whose add returns the group's last count reads the group's partials with sc1 loads (L2 and
+    // L1 bypassed: correct wherever the group's bricks ran, MI355X_MICROARCH.md inter-workgroup
+    // visibility) and sums them by the fixed wave tree, so the group sum does not depend on the order
+    // of arrival.  The counter is reset for the next launch by the same brick.
+    const int gi = b / grp, g0 = gi * grp, gn = min(grp, nbrick - g0);
+    uint32_t prev = 0;
+    if (t == 0) {
+        __hip_atomic_store(&part[b], den, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        prev = __hip_atomic_fetch_add(&gcnt[gi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    prev = (uint32_t)__shfl((int)prev, 0, 64);
+    if (prev != (uint32_t)(gn - 1)) return;
+    double v = t < gn ? __hip_atomic_load(&part[g0 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    v = wave_sum(v);
+    if (t == 0) {
+        gsum[gi] = v;
+        __hip_atomic_store(&gcnt[gi], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // PB (set_option "brick_upd_pb"): the 1-8 patch entries of every dof as eight unconditional buffer
@@ -1123,15 +1147,16 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const double *qd = c->d_qaff ? c->d_qaff : c->d_qd;
     const double *upart = c->d_part + c->nblk;  // the den-fold update's partials
     double *const dpart = c->den_out ? c->den_out : c->d_part;  // the apply's den partials
+    const int grp = c->den_grp, nbrick = c->nblk;               // (grouped: sums into d_gsum)
 #define CDFEM_BCG5(AFF_, W_, XF_, BF_, FU_)                                                                 \
     if (whole)                                                                                               \
         CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_>), grid, block, 0, r, dinv, d_old, d_new, q, \
                      c->d_face, qd, c->d_ess, T, g, c->zlo_shared, dpart, c->d_state, x, upart, run.nupart,     \
-                     run.kk);                                                                                \
+                     run.kk, c->d_gsum, c->d_gcnt, grp, nbrick);                                             \
     else                                                                                                     \
         hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_>), grid, block, 0, run.s, r, dinv,     \
                            d_old, d_new, q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, dpart, c->d_state, x, \
-                           upart, run.nupart, run.kk)
+                           upart, run.nupart, run.kk, c->d_gsum, c->d_gcnt, grp, nbrick)
 #define CDFEM_BCG4(AFF_, W_, XF_, BF_)                                                                      \
     if (full) { CDFEM_BCG5(AFF_, W_, XF_, BF_, true); } else { CDFEM_BCG5(AFF_, W_, XF_, BF_, false); }
 #define CDFEM_BCG3(AFF_, W_, XF_) CDFEM_BCG5(AFF_, W_, XF_, false, false)
@@ -1246,7 +1271,29 @@ int cg_den_fold_grid(const cdfem_ctx *c)
 static bool cg_folds_fit(const cdfem_ctx *c)
 {
     return c->cg_den_fold != 0 && c->cg_beta_fold != 0 && c->p <= 2 && pa_af(c) == 2 && cg_den_fold_grid(c) <= 1024 &&
-           brick_count(c) <= kDenFoldMaxParts;
+           den_parts(c) <= kDenFoldMaxParts;
+}
+
+// den partial groups (p <= 2, several ranks): none while the bricks fit the fold bound (kMrFoldMaxParts; C2's
+// 4,096 bricks per rank), else the smallest power of two <= 64 leaving <= kDenGroupParts group sums (C5's
+// per-rank slab of 32,768 bricks: 8 -> 4,096), so the multi-rank fold stays on; 1 when even 64 leaves too many.
+// One rank keeps per-brick partials (its 256^3 p = 2 box: the two-stage den sum, 3,491 us of kernels per
+// iteration against 3,503 with groups of 64, profiles/r06/r06c_c5_1gpu*.json); set_option "den_group"
+// forces a size on any box (tests)
+int den_group(const cdfem_ctx *c)
+{
+    const int nb = brick_count(c);
+    if (c->p > 2) return 1;
+    if (c->den_group_opt > 0) return c->den_group_opt;
+    if (!multi_rank(c) || nb <= kMrFoldMaxParts) return 1;
+    for (int g = 2; g <= 64; g *= 2)
+        if ((nb + g - 1) / g <= kDenGroupParts) return g;
+    return 1;
+}
+int den_parts(const cdfem_ctx *c)
+{
+    const int g = den_group(c);
+    return (brick_count(c) + g - 1) / g;
 }
 
 // several ranks (set_option "cg_mr_fold"): the ranks all-reduce the apply's den partials and the
@@ -1255,7 +1302,7 @@ static bool cg_folds_fit(const cdfem_ctx *c)
 // den and betanom steps as on one rank; no sum / step kernels between them
 bool cg_mr_fold(const cdfem_ctx *c)
 {
-    return multi_rank(c) && c->cg_mr_fold != 0 && cg_folds_fit(c) && brick_count(c) <= kMrFoldMaxParts;
+    return multi_rank(c) && c->cg_mr_fold != 0 && cg_folds_fit(c) && den_parts(c) <= kMrFoldMaxParts;
 }
 
 bool cg_beta_fold_ok(const cdfem_ctx *c)
@@ -1267,7 +1314,7 @@ bool cg_beta_fold_ok(const cdfem_ctx *c)
 // 64-element brick; the high-order blocks leave too many partials and keep the finalizer)
 bool cg_den_fold_on(const cdfem_ctx *c)
 {
-    return c->cg_den_fold != 0 && c->p <= 2 && brick_count(c) <= kDenFoldMaxParts && (!multi_rank(c) || cg_mr_fold(c));
+    return c->cg_den_fold != 0 && c->p <= 2 && den_parts(c) <= kDenFoldMaxParts && (!multi_rank(c) || cg_mr_fold(c));
 }
 
 // the first and last brick layers (the shared planes' partial sums) on stream s, the interior
@@ -1300,10 +1347,13 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     const bool ds = !den_step && cg_den_fold_on(c);
     const unsigned ugrid = ds ? (unsigned)cg_den_fold_grid(c) : grid;
     double *const upart = ds ? c->d_part + c->nblk : c->d_part;
+    // the apply's den partials the den fold sums: one per brick, or the group sums (den_grp > 1)
+    const double *const apart = c->den_grp > 1 ? c->d_gsum : c->d_part;
+    const int napart = c->den_grp > 1 ? den_parts(c) : c->nblk;
 #define CDFEM_UPD4(S_, XF_, PB_, DS_, EP_)                                                                 \
     hipLaunchKernelGGL((k_cg_update_faces<S_, XF_, PB_, DS_, EP_>), dim3(ugrid), dim3(kRedThreads), 0, c->stream, x, \
                        r, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, upart, \
-                       c->d_state, (int)den_step, c->d_part, c->nblk)
+                       c->d_state, (int)den_step, apart, napart)
     // the apply's essential-row patch entries (k_brick_cg EP: the Kronecker form at p <= 2)
     const bool ep = pa_af(c) == 2 && c->p <= 2;
 #define CDFEM_UPD3(S_, XF_, PB_, DS_)                                                                      \

@@ -171,6 +171,10 @@ void free_mesh(cdfem_ctx *c)
     c->slab_nl_max = 0;
     c->slab_nb_max = 0;
     dfree(c->d_small);
+    dfree(c->d_gsum);
+    dfree(c->d_gcnt);
+    c->gsum_cap = 0;
+    c->den_grp = 1;
     dfree(c->d_hbpart);
     dfree(c->d_bess);
     c->hb_nblk = 0;
@@ -428,7 +432,7 @@ const double *solver_dinv(cdfem_ctx *c)
 // collective after an option change that left its own key unchanged while another rank's key moved).
 bool mr_fold_agreed(cdfem_ctx *c)
 {
-    const double ok = cg_mr_fold(c) ? 1.0 : 0.0, nb = brick_count(c), ng = cg_den_fold_grid(c);
+    const double ok = cg_mr_fold(c) ? 1.0 : 0.0, nb = den_parts(c), ng = cg_den_fold_grid(c);
     double h[5] = {ok, nb, nb * nb, ng, ng * ng};
     if (!c->d_small) c->d_small = dalloc<double>(8);
     HIPCHK(hipMemcpyAsync(c->d_small, h, sizeof(h), hipMemcpyHostToDevice, c->stream));
@@ -454,12 +458,13 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     }
     // the apply's den partials in two stages (a block per 1/256 of them, then one block) when the one
     // block finalizer would sum too many: the p = 3, 4 blocks, and one rank past the den fold's bound
-    const bool two_stage = c->p >= 3 || (!multi_rank(c) && nbrick > kDenFoldMaxParts);
+    const int ndp = den_parts(c);  // the den partials the folds sum (grouped past the bounds: den_group)
+    const bool two_stage = c->p >= 3 || (!multi_rank(c) && ndp > kDenFoldMaxParts);
     if (two_stage && !c->d_hbpart) c->d_hbpart = dalloc<double>(nbrick);
     c->den_out = two_stage && c->p <= 2 ? c->d_hbpart : nullptr;
     struct DenOutReset {
         cdfem_ctx *c;
-        ~DenOutReset() { c->den_out = nullptr; }
+        ~DenOutReset() { c->den_out = nullptr; c->den_grp = 1; }
     } den_out_reset{c};
     double *dprev = c->d_w[5], *dcur = c->d_dalt;
     const double *dinv;
@@ -501,6 +506,18 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     // run as on one rank; the per-iteration kernels are then the one-rank pair plus the plane pack
     const bool mrfold = mr && mr_fold_agreed(c);
     const bool bfold = mr ? mrfold : cg_beta_fold_ok(c);
+    // grouped den partials: taken when a fold sums them (several ranks: the fold; one rank: the den fold)
+    const int grp = (mr ? mrfold : (!two_stage && cg_den_fold_on(c))) ? den_group(c) : 1;
+    if (grp > 1 && c->gsum_cap < ndp) {
+        dfree(c->d_gsum);
+        dfree(c->d_gcnt);
+        c->d_gsum = dalloc<double>(ndp);
+        c->d_gcnt = dalloc<uint32_t>(ndp);
+        HIPCHK(hipMemsetAsync(c->d_gcnt, 0, (size_t)ndp * sizeof(uint32_t), c->stream));
+        c->gsum_cap = ndp;
+    }
+    c->den_grp = grp;
+    double *const dparts = grp > 1 ? c->d_gsum : c->d_part;  // what the mr fold all-reduces (ndp of them)
     int nupd = 0;
     int napply = 0;
     auto apply = [&] {
@@ -517,7 +534,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             HIPCHK(hipEventRecord(c->ov_ev[1], c->stream2));
             HIPCHK(hipStreamWaitEvent(c->stream, c->ov_ev[1], 0));
             if (mrfold) {
-                comm_allreduce(c, c->d_part, nbrick);  // the den partials: the update sums them
+                comm_allreduce(c, dparts, ndp);  // the den partials: the update sums them
             } else {
                 HIPCHK(launch_fin_sum(c, nbrick, 0));
                 comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
@@ -533,7 +550,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             HIPCHK(launch_pack_qplanes(c, q));
             comm_exchange(c, c->d_if[0], c->d_if[1], c->d_if[2], c->d_if[3], c->Lx * c->Ly);
             if (mrfold) {
-                comm_allreduce(c, c->d_part, nbrick);
+                comm_allreduce(c, dparts, ndp);
             } else {
                 HIPCHK(launch_fin_sum(c, nbrick, 0));
                 comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
@@ -1816,6 +1833,10 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "brick_byte_limit") {
             if (value < 0) throw ArgError("brick_byte_limit must be 0 (the default 2^31) or 1..2^31-1");
             c->brick_limit = value == 0 ? (int64_t)1 << 31 : value;
+        } else if (k == "den_group") {
+            if (value < 0 || value > 64 || (value & (value - 1)) != 0)
+                throw ArgError("den_group must be 0 (automatic) or a power of two up to 64");
+            c->den_group_opt = value;
         } else if (k == "cg_mr_fold") {
             if (value != 0 && value != 1) throw ArgError("cg_mr_fold must be 0 or 1");
             c->cg_mr_fold = value;

@@ -159,6 +159,14 @@ struct cdfem_ctx {
     double *d_hbpart = nullptr;         // den partials summed in two stages: k_hobrick_cg's, and k_brick_cg's past
                                         // kDenFoldMaxParts bricks on one rank (one per brick)
     double *den_out = nullptr;          // k_brick_cg writes its den partials here instead of d_part (set by the solve)
+    // grouped den partials (p <= 2 past the fold bounds: C5's per-rank slab of 32,768 bricks, its 262,144 on one
+    // GPU): the last-arriving brick of each group of den_grp sums the group's partials in a fixed order
+    // (k_brick_cg tail: write-through partial, agent-scope arrival count), so the folds sum <= 4,096 values
+    int den_grp = 1;                    // group size of the running solve (1: one partial per brick)
+    int den_group_opt = 0;              // set_option "den_group": 0 automatic, else this group size (tests)
+    double *d_gsum = nullptr;           // [ceil(nblk / den_grp)] group sums
+    uint32_t *d_gcnt = nullptr;         // [same] arrival counters (0 between launches)
+    int64_t gsum_cap = 0;
     int ho_brick_mfma = 0;              // set_option "ho_brick_mfma": its x stage on v_mfma_f64_16x16x4_f64 (kinds 7)
     int64_t Lx = 0, Ly = 0, Lz = 0;     // dof lattice per axis
     double *d_face = nullptr;           // [nblk][F] brick-face partial sums
@@ -357,6 +365,11 @@ int brick_count(const cdfem_ctx *c);        // bricks (p <= 2) or high-order blo
 int brick_patch_side(const cdfem_ctx *c);   // S: 4p + 1 (p <= 2), 2p + 1 (p = 3, 4)
 bool cg_den_fold_on(const cdfem_ctx *c);
 bool cg_mr_fold(const cdfem_ctx *c);
+// den partial groups of the brick CG apply at p <= 2: 1 when the bricks fit the fold bounds, else the
+// power of two (<= 64) that brings them to <= kDenGroupParts sums; den_parts = the folds' partial count
+constexpr int kDenGroupParts = 4096;
+int den_group(const cdfem_ctx *c);
+int den_parts(const cdfem_ctx *c);
 constexpr int kMrFoldMaxParts = 8192;   // cg_mr_fold: apply partials every update workgroup re-sums
 constexpr int kDenFoldMaxParts = 16384; // cg_den_fold: beyond (C5's 256^3 on one GPU: 262,144 bricks) the
                                         // den finalizer (the update workgroups' redundant sums grow with it)

@@ -269,6 +269,11 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *              five input points padded to eight, columns = M, K, C, C^T per output point), staged to
  *              the tile threads through LDS; the y and z stages stay on the VALU.  Same operator to
  *              rounding; the north star's MFMA contraction, A/B'd in DESIGN.md 4.2.
+ * "den_group": 0 (default) — on several ranks the brick CG apply's den partials (one per 64-element brick)
+ *              are summed in groups by the group's last-arriving brick once there are more than the
+ *              multi-rank fold sums (8,192: C5's per-rank slab of 32,768 bricks -> groups of 8), so the
+ *              fold stays on; one rank keeps per-brick partials (measured: its 256^3 box runs the
+ *              two-stage den sum 0.3 % faster); a power of two up to 64 forces that size (tests).
  * "brick_byte_limit": 2^31 (default) — the structured brick kernels address their vectors and patch
  *              buffer with 32-bit buffer offsets (out-of-range marker 2^31), so a box whose 8 N_L or
  *              8 S^3 bricks reach the limit runs the generic element kernels instead; lower values

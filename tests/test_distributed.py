@@ -242,6 +242,52 @@ def test_gpu_overlapped_exchange_bitwise(tmp_path, world):
         np.testing.assert_array_equal(x[0], x[2])
 
 
+def _gpu_mr_group_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "continuum-mechanics-mfem_amd", "python"))
+    import cdfem
+    dist = _init(rank, world, port)
+    n, per = 16, 12                      # 4 x 4 x 3 = 48 bricks per rank: groups of 8 (6) and of 32 (2, one partial)
+    m = cdfem.box_mesh(3, (n, n, per * world), P, z_range=(rank * per, (rank + 1) * per))
+    ctx = cdfem.Context(0)
+    ctx.upload_mesh(m).set_structured(n, n, per)
+    ctx.comm_init_torch()
+    ctx.set_slab(rank > 0, rank < world - 1)
+    b = np.random.default_rng(450 + rank).uniform(-1, 1, m.nl)
+    ctx.pa_setup(kinds=7, kappa=KAPPA, alpha=1.0, conv=CONV, mass=S)
+    _, B = ctx.form_linear_system(np.zeros(m.nl), b)
+    res = {}
+    for ov in (0, 1):
+        ctx.set_option("mr_overlap", ov)
+        for grp in (0, 8, 32):
+            ctx.set_option("den_group", grp)
+            X, info = ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30, check_every=7)
+            assert info["iterations"] == 30
+            res[f"ov{ov}_g{grp}"] = X
+    ctx.set_option("den_group", 0)
+    np.savez(os.path.join(out_dir, f"mrg{rank}.npz"), **res)
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_mr_fold_grouped_partials(tmp_path, world):
+    """The multi-rank fold with grouped den partials (den_group; automatic on C5's 32,768-brick per-rank
+    slab): each group's last-arriving brick sums the group, and the ranks all-reduce the group sums.
+    Against the per-brick partials: 30 fixed iterates within 1e-12, one-launch and overlapped applies
+    bitwise equal (the group sums do not depend on which launch or order the bricks arrive in)."""
+    mp.start_processes(_gpu_mr_group_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    for r in range(world):
+        d = np.load(tmp_path / f"mrg{r}.npz")
+        for grp in (8, 32):
+            np.testing.assert_array_equal(d[f"ov1_g{grp}"], d[f"ov0_g{grp}"])
+            a, b_ = d[f"ov0_g{grp}"], d["ov0_g0"]
+            assert np.linalg.norm(a - b_) <= 1e-12 * np.linalg.norm(b_), (r, grp)
+
+
 def _gpu_mr_fold_worker(rank, world, port, out_dir):
     import sys
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))

@@ -107,6 +107,46 @@ def test_den_fold_matches_den_finalizer(gpu_ctx, shape, p, kinds, fold):
         assert np.linalg.norm(conv[fold][0] - conv[0][0]) <= 1e-10 * np.linalg.norm(conv[0][0])
 
 
+@pytest.mark.parametrize("shape,p,kinds,grp", [((12, 16, 8), 2, 7, 8), ((12, 16, 8), 2, 5, 16), ((9, 6, 7), 2, 7, 4),
+                                                ((10, 8, 13), 1, 7, 64)])
+def test_den_group_matches_ungrouped(gpu_ctx, shape, p, kinds, grp):
+    """den_group G (automatic past the fold bounds: C5's per-rank slab, its 256^3 on one GPU; forced here on
+    small boxes): each group of G bricks' den partials is summed by the group's last-arriving brick (a
+    write-through partial, an agent-scope arrival count, sc1 loads of the group) and the folds sum the
+    group sums.  Groups of 8 / 16 / 4 / 64 over 24 / 24 / 24 / 48 bricks (a partial last group in three
+    of them): 30 fixed iterates within 1e-12 of the ungrouped fold and 1e-11 of the oracle, bitwise
+    repeatable (the group sum does not depend on the order the bricks arrive in)."""
+    om = O.BoxMesh(3, shape, p)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3,
+                      kinds=(O.DIFFUSION if kinds & 1 else 0) | (O.CONVECTION if kinds & 2 else 0) |
+                      (O.MASS if kinds & 4 else 0))
+    rng = np.random.default_rng(37)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(*shape)
+    gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    out = {}
+    try:
+        for g in (grp, 0):
+            gpu_ctx.set_option("den_group", g)
+            out[g] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30, check_every=7)
+        gpu_ctx.set_option("den_group", grp)
+        again = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=30)
+    finally:
+        gpu_ctx.set_option("den_group", 0)
+    np.testing.assert_array_equal(again[0], out[grp][0])
+    for g, (xg, ig) in out.items():
+        assert ig["iterations"] == 30
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), g
+    assert np.linalg.norm(out[grp][0] - out[0][0]) <= 1e-12 * np.linalg.norm(out[0][0])
+    with pytest.raises(cdfem.CdfemError):
+        gpu_ctx.set_option("den_group", 3)
+
+
 @pytest.mark.parametrize("shape,p,kinds", [((8, 8, 8), 2, 7), ((9, 6, 7), 2, 5), ((6, 5, 7), 1, 7), ((5, 9, 10), 2, 3)])
 def test_brick_mult_patch_buffer_bitwise(gpu_ctx, shape, p, kinds):
     """brick_mult_pb: the structured Mult through the patch buffer (k_brick3d<..., PBO> +
