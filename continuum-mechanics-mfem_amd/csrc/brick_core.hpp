@@ -43,16 +43,17 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, d
 // The 1-8 patch-buffer entries of lattice dof (gx, gy, gz) summed in a fixed order (lower brick first
 // per face axis, z outermost): eight buffer loads at fixed offsets from its own brick's entry P (the
 // lower brick's face entry along x / y / z sits at P - 1 / P - R / P - A in the pencil layout of
-// patch_idx), the absent ones at kOOB (read as 0).
-template <int S>
+// patch_idx), the absent ones at kOOB (read as 0).  Patches are S x S x SZ (SZ > S: the z-elongated
+// high-order blocks, set_option "ho_block_z").
+template <int S, int SZ = S>
 __device__ __forceinline__ double patch_sum8(__amdgpu_buffer_rsrc_t bp, const BrickGeom &g, int gx, int gy, int gz)
 {
-    constexpr int s1 = S - 1;
-    const int qx = min(gx / s1, g.nbx - 1), qy = min(gy / s1, g.nby - 1), qz = min(gz / s1, g.nbz - 1);
-    const int px = gx - qx * s1, py = gy - qy * s1, pz = gz - qz * s1;
+    constexpr int s1 = S - 1, sz1 = SZ - 1;
+    const int qx = min(gx / s1, g.nbx - 1), qy = min(gy / s1, g.nby - 1), qz = min(gz / sz1, g.nbz - 1);
+    const int px = gx - qx * s1, py = gy - qy * s1, pz = gz - qz * sz1;
     const bool fx = px == 0 && qx > 0, fy = py == 0 && qy > 0, fz = pz == 0 && qz > 0;
     const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
-    const uint32_t P = (((uint32_t)qz * S + pz) * g.nby + qy) * S * R + (uint32_t)py * R + (uint32_t)qx * S + px;
+    const uint32_t P = (((uint32_t)qz * SZ + pz) * g.nby + qy) * S * R + (uint32_t)py * R + (uint32_t)qx * S + px;
     // (CDFEM_PS8_SKIP: a wave none of whose dofs sits on a y or z brick face issues no load for those
     // neighbours: the 64 consecutive dofs of a wave share one or two lattice rows, so most waves load
     // 2 entries, not 8.  An out-of-range buffer load moves no memory but still returns 64 lanes of

@@ -112,10 +112,10 @@ constexpr int face_count() { return 2 * S * S + (S - 2) * (4 * S - 4); }
 // The CG apply's patch-output buffer, x rows of the brick lattice contiguous ([bz][pz][by][py][bx][px]):
 // a brick writes 81 runs of S, and the update kernel's wave over a lattice x row reads one contiguous
 // run (each dof's 1-8 entries: its own brick's, plus the neighbours' on brick faces)
-template <int S>
+template <int S, int SZ = S>
 __device__ __forceinline__ size_t patch_idx(const BrickGeom &g, int bx, int by, int bz, int px, int py, int pz)
 {
-    return ((((size_t)bz * S + pz) * g.nby + by) * S + py) * ((size_t)g.nbx * S) + (size_t)bx * S + px;
+    return ((((size_t)bz * SZ + pz) * g.nby + by) * S + py) * ((size_t)g.nbx * S) + (size_t)bx * S + px;
 }
 
 // f(std::integral_constant<int, k>) for k = B .. E - 1, unrolled at compile time (array indices
@@ -408,11 +408,11 @@ int brick_patch_side(const cdfem_ctx *c);
 // dropped store would land inside the buffer
 bool brick_fits(const cdfem_ctx *c)
 {
-    const double S = brick_patch_side(c), lim = (double)c->brick_limit;
+    const double S = brick_patch_side(c), SZ = brick_patch_side_z(c), lim = (double)c->brick_limit;
     // a slab partition decides on the largest rank's sizes (cdfem_set_slab), the same on every rank
     const double nl = (double)std::max<int64_t>(c->nl, c->part_mode == 1 ? c->slab_nl_max : 0);
     const double nb = (double)std::max<int64_t>(brick_count(c), c->part_mode == 1 ? c->slab_nb_max : 0);
-    return 8.0 * nl < lim && 8.0 * nb * S * S * S < lim;
+    return 8.0 * nl < lim && 8.0 * nb * S * S * SZ < lim;
 }
 
 // the brick lattice of the context: 4^3-element bricks at p <= 2, 2^3-element blocks at p = 3, 4 (ho_brick)
@@ -424,6 +424,7 @@ static BrickGeom geom_of(const cdfem_ctx *c)
 
 int brick_count(const cdfem_ctx *c) { return c->p >= 3 ? c->hb_nblk : c->nblk; }
 int brick_patch_side(const cdfem_ctx *c) { return c->p >= 3 ? kHoBrickEdge * c->p + 1 : kBrick * c->p + 1; }
+int brick_patch_side_z(const cdfem_ctx *c) { return c->p >= 3 ? c->hb_ez * c->p + 1 : kBrick * c->p + 1; }
 
 // patch-buffer Mult (Kronecker form, byte offsets within 32 bits)
 bool brick_mult_pb_on(const cdfem_ctx *c) { return c->brick_mult_pb != 0 && pa_af(c) == 2 && brick_fits(c); }
@@ -768,7 +769,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
 // napart) in one fixed order and takes MFEM's den step itself (workgroup 0 records it), so the
 // one-block den finalizer and its launch go away; the grid is a few hundred to a few thousand
 // workgroups (grid-stride loop) to keep the redundant sums small, and its partials go to part.
-template <int S, bool XF, bool PB = false, bool DS = false, bool EP = false>
+template <int S, bool XF, bool PB = false, bool DS = false, bool EP = false, int SZ = S>
 __global__ void __launch_bounds__(kRedThreads)
 k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ d,
                   const double *__restrict__ dinv, const double *__restrict__ pb,
@@ -778,7 +779,8 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
                   double *__restrict__ part, KrylovState *__restrict__ st, int den_step,
                   const double *__restrict__ apart, int napart)
 {
-    constexpr int s1 = S - 1;
+    constexpr int s1 = S - 1, sz1 = SZ - 1;
+    constexpr uint32_t PV = (uint32_t)S * S * SZ;  // patch entries per brick / block
     __shared__ double sh[kRedThreads / 64 + 1];
     if (st->done) return;
     double alpha = 0.0;
@@ -812,7 +814,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
         // under the first loads (59.2-59.4 against 59.05 us per iteration) and two dofs per pass (62.5
         // against 59.8)
         static_assert(PB, "EP reads the patch buffer with the predicated loads");
-        const auto bp = brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S));
+        const auto bp = brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * PV);
         for (int gid = blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += gridDim.x * blockDim.x) {
             const int gz = (int)fdiv((uint32_t)gid, fdxy);
             const int rem = gid - gz * plane;
@@ -820,7 +822,7 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
             const int gx = rem - gy * g.Lx;
             const double rold = r[gid], mi = dinv[gid];
             const double xi = XF ? 0.0 : x[gid], di = XF ? 0.0 : d[gid];
-            double qi = patch_sum8<S>(bp, g, gx, gy, gz);
+            double qi = patch_sum8<S, SZ>(bp, g, gx, gy, gz);
             if (remote_lo && gz == 0) qi += remote_lo[rem];
             if (remote_hi && gz == g.Lz - 1) qi += remote_hi[rem];
             if constexpr (!XF) __builtin_nontemporal_store(xi + alpha * di, &x[gid]);
@@ -842,10 +844,10 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
             const double rold = r[gid], mi = dinv[gid];
             double qi;
             if constexpr (PB) {
-                qi = patch_sum8<S>(brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * (S * S * S)), g, gx, gy, gz);
-            } else if (gx % s1 == 0 || gy % s1 == 0 || gz % s1 == 0) {
+                qi = patch_sum8<S, SZ>(brsrc(pb, 8u * (uint32_t)g.nbx * g.nby * g.nbz * PV), g, gx, gy, gz);
+            } else if (gx % s1 == 0 || gy % s1 == 0 || gz % sz1 == 0) {
                 int bxs[2], pxs[2], nxc = 0, bys[2], pys[2], nyc = 0, bzs[2], pzs[2], nzc = 0;
-                const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
+                const int qx = gx / s1, qy = gy / s1, qz = gz / sz1;
                 if (gx - qx * s1 == 0) {
                     if (qx - 1 >= 0) { bxs[nxc] = qx - 1; pxs[nxc] = s1; ++nxc; }
                     if (qx < g.nbx) { bxs[nxc] = qx; pxs[nxc] = 0; ++nxc; }
@@ -854,19 +856,19 @@ k_cg_update_faces(double *__restrict__ x, double *__restrict__ r, const double *
                     if (qy - 1 >= 0) { bys[nyc] = qy - 1; pys[nyc] = s1; ++nyc; }
                     if (qy < g.nby) { bys[nyc] = qy; pys[nyc] = 0; ++nyc; }
                 } else { bys[0] = qy; pys[0] = gy - qy * s1; nyc = 1; }
-                if (gz - qz * s1 == 0) {
-                    if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = s1; ++nzc; }
+                if (gz - qz * sz1 == 0) {
+                    if (qz - 1 >= 0) { bzs[nzc] = qz - 1; pzs[nzc] = sz1; ++nzc; }
                     if (qz < g.nbz) { bzs[nzc] = qz; pzs[nzc] = 0; ++nzc; }
-                } else { bzs[0] = qz; pzs[0] = gz - qz * s1; nzc = 1; }
+                } else { bzs[0] = qz; pzs[0] = gz - qz * sz1; nzc = 1; }
                 qi = 0.0;
                 for (int kz = 0; kz < nzc; ++kz)
                     for (int ky = 0; ky < nyc; ++ky)
                         for (int kx = 0; kx < nxc; ++kx) {
-                            qi += pb[patch_idx<S>(g, bxs[kx], bys[ky], bzs[kz], pxs[kx], pys[ky], pzs[kz])];
+                            qi += pb[patch_idx<S, SZ>(g, bxs[kx], bys[ky], bzs[kz], pxs[kx], pys[ky], pzs[kz])];
                         }
             } else {  // inside one brick's patch
-                const int qx = gx / s1, qy = gy / s1, qz = gz / s1;
-                qi = pb[patch_idx<S>(g, qx, qy, qz, gx - qx * s1, gy - qy * s1, gz - qz * s1)];
+                const int qx = gx / s1, qy = gy / s1, qz = gz / sz1;
+                qi = pb[patch_idx<S, SZ>(g, qx, qy, qz, gx - qx * s1, gy - qy * s1, gz - qz * sz1)];
             }
             // interface planes: add the neighbour rank's partial sums
             if (remote_lo && gz == 0) qi += remote_lo[rem];
@@ -908,8 +910,11 @@ constexpr int kHoBrick = kHoBrickEdge;  // elements per block edge (high order)
 // threads, which form the element combinations and the y / z stages on the VALU as before.  The
 // north star's "MFMA for the per-element B^T D B contraction at high order", A/B'd against the VALU
 // x stage.
-template <int D1, int Q1, unsigned K, bool XF, bool MF = false>
-__global__ void __launch_bounds__(((kHoBrick * kHoBrick * kHoBrick * D1 * D1 + 63) / 64) * 64, 4)
+// EZ (set_option "ho_block_z"): elements per block along z, 2 (2^3 blocks: 8 tiles = 200 of 256 threads busy
+// at p = 4, 1.42 patch entries per dof) or 4 (2 x 2 x 4 blocks: 16 tiles = 400 of 448, 1.34 entries per dof;
+// an S x S x SZ patch, SZ = 4p + 1)
+template <int D1, int Q1, unsigned K, bool XF, bool MF = false, int EZ = kHoBrick>
+__global__ void __launch_bounds__(((kHoBrick * kHoBrick * EZ * D1 * D1 + 63) / 64) * 64, 4)
 k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, const double *__restrict__ d_old,
              double *__restrict__ d_new, double *__restrict__ face, const double *__restrict__ qaff,
              const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g, int nex, int ney, int nez,
@@ -917,8 +922,8 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
              const double *__restrict__ ktab)
 {
     using L = QLayout<K, 3>;
-    constexpr int P = D1 - 1, EB = kHoBrick, S = EB * P + 1, S2 = S * S, S3 = S * S * S;
-    constexpr int DD = D1 * D1, ND = DD * D1, NEB = EB * EB * EB, NC = L::nc;
+    constexpr int P = D1 - 1, EB = kHoBrick, S = EB * P + 1, SZ = EZ * P + 1, S2 = S * S, S3 = S * S * SZ;
+    constexpr int DD = D1 * D1, ND = DD * D1, NEB = EB * EB * EZ, NC = L::nc;
     constexpr int NT = ((NEB * DD + 63) / 64) * 64, NI = (S3 + NT - 1) / NT;
     __shared__ double s_in[S3];
     __shared__ double sP[NEB][4][ND];  // [element][grp][jz][iy][ix]
@@ -934,7 +939,7 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
     const int b = brick_id(g);
     const int nxy = g.nbx * g.nby;
     const int bz = b / nxy, by = (b - bz * nxy) / g.nbx, bx = b - bz * nxy - by * g.nbx;
-    const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (S - 1) * bz;
+    const int gx0 = (S - 1) * bx, gy0 = (S - 1) * by, gz0 = (SZ - 1) * bz;
     const bool lastx = bx == g.nbx - 1, lasty = by == g.nby - 1, lastz = bz == g.nbz - 1;
     const int Lx = g.Lx, Lxy = g.Lx * g.Ly;
     const uint32_t nl = (uint32_t)Lxy * (uint32_t)g.Lz;
@@ -947,7 +952,7 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
     // this thread's element tile and x-stage rows (ix = a), loaded with the patch
     const int le = tid / DD, tt = tid - le * DD, a = tt % D1, bb = tt / D1;
     const int lex = le & 1, ley = (le >> 1) & 1, lez = le >> 2;
-    const int ex = EB * bx + lex, ey = EB * by + ley, ez = EB * bz + lez;
+    const int ex = EB * bx + lex, ey = EB * by + ley, ez = EZ * bz + lez;
     const bool tile = le < NEB, valid = tile && ex < nex && ey < ney && ez < nez;
     const int64_t ec = valid ? (int64_t)ex + (int64_t)nex * (ey + (int64_t)ney * ez) : 0;
     double Mr[D1], Kr[D1], Cr[D1], Ctr[D1], gf[NC];
@@ -981,7 +986,7 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
             ov[k] = bload(bo, offv[k]);
             ev[k] = 0;
             if (bhas) ev[k] = __builtin_amdgcn_raw_buffer_load_b8(be, in ? gid : kOOB, 0, 0);
-            const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
+            const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < SZ - 1 || lastz);
             if constexpr (XF) xv[k] = bload(bxf, writer ? offv[k] : kOOB);
         }
         PatchWalk<S, NT> pw1(tid);
@@ -994,7 +999,7 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
             const bool in = offv[k] != kOOB;
             const double dn = mv[k] * rv[k] + beta * ov[k];  // 0 outside the lattice
             const bool e = ev[k] != 0;
-            const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < S - 1 || lastz);
+            const bool writer = in && (px < S - 1 || lastx) && (py < S - 1 || lasty) && (pz < SZ - 1 || lastz);
             const uint32_t woff = writer ? offv[k] : kOOB;
             bstore(bd, woff, dn);
             if constexpr (XF) bstore(bxf, woff, xv[k] + alpha_prev * ov[k]);
@@ -1007,6 +1012,7 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
     const int o0 = P * lez * S2 + P * ley * S + P * lex;
     double xq[MF ? 4 : 1][MF ? D1 : 1];  // MF: this thread's (M, K, C, C^T) X rows, from the GEMM
     if constexpr (MF) {
+        static_assert(EZ == kHoBrick, "the MFMA x stage is built for 2^3 blocks");
         constexpr int NR = NEB * DD, NCOL = 4 * D1;
         static_assert(NR * NCOL <= NEB * 4 * ND, "the x-stage output aliases the y-stage groups");
         double *xs = &sP[0][0][0];
@@ -1094,7 +1100,7 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
     //    (lower element first per axis, z outermost) -> the patch buffer
     {
         const uint32_t R = (uint32_t)g.nbx * S, A = (uint32_t)g.nby * S * R;
-        const uint32_t base = (uint32_t)bz * S * A + (uint32_t)by * S * R + (uint32_t)bx * S;
+        const uint32_t base = (uint32_t)bz * SZ * A + (uint32_t)by * S * R + (uint32_t)bx * S;
         const auto bp = brsrc(face, 8u * (uint32_t)g.nbx * g.nby * g.nbz * S3);
         const unsigned to = (unsigned)opaque(tid);
         PatchWalk<S, NT> pw(to);
@@ -1103,18 +1109,27 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
             const unsigned i = to + NT * k;
             if (i >= S3) break;
             const int px = pw.x, py = pw.y, pz = pw.z;
-            // per axis: element 0 holds positions 0..P, element 1 positions P..2P (local P + 0..P)
-            const int x0 = px < P ? px : P, y0 = py < P ? py : P, z0 = pz < P ? pz : P;
-            const bool hx1 = px >= P, hy1 = py >= P, hz1 = pz >= P;
-            const bool hx0 = px <= P, hy0 = py <= P, hz0 = pz <= P;
-            const int x1 = px - P, y1 = py - P, z1 = pz - P;
+            // per axis: element 0 holds positions 0..P, element 1 positions P..2P (local P + 0..P); along z
+            // the pair of candidate elements is (kz - 1, kz) around position pz = kz P + lz (lower first)
+            const int x0 = px < P ? px : P, y0 = py < P ? py : P;
+            const bool hx1 = px >= P, hy1 = py >= P;
+            const bool hx0 = px <= P, hy0 = py <= P;
+            const int x1 = px - P, y1 = py - P;
+            int kz = pz / P;
+            kz = kz < EZ ? kz : EZ - 1;
+            const int zl = pz - kz * P;  // 0..P: local z in element kz
+            const bool zlow = zl == 0 && kz > 0;  // also the top face of element kz - 1
             double sum = 0.0;
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 const int cx = c & 1, cy = (c >> 1) & 1, cz = c >> 2;
-                const bool ok = (cx ? hx1 : hx0) && (cy ? hy1 : hy0) && (cz ? hz1 : hz0);
-                const int lx = cx ? x1 : x0, ly = cy ? y1 : y0, lz = cz ? z1 : z0;
-                const double t = sE(cx + 2 * cy + 4 * cz, ok ? (lz * D1 + ly) * D1 + lx : 0);
+                // cz = 0: the lower z element (kz - 1 at local P when zlow, else kz), cz = 1: element kz
+                // when zlow (at local 0); the same order as the 2^3 form's (lower element first)
+                const bool okz = cz ? zlow : true;
+                const int ez8 = cz ? kz : (zlow ? kz - 1 : kz), lz = cz ? 0 : (zlow ? P : zl);
+                const bool ok = (cx ? hx1 : hx0) && (cy ? hy1 : hy0) && okz;
+                const int lx = cx ? x1 : x0, ly = cy ? y1 : y0;
+                const double t = sE(cx + 2 * cy + 4 * ez8, ok ? (lz * D1 + ly) * D1 + lx : 0);
                 sum += ok ? t : 0.0;
             }
             bstore(bp, 8u * (base + (uint32_t)pw.z * A + (uint32_t)pw.y * R + (uint32_t)pw.x), sum);
@@ -1181,11 +1196,15 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     return hipGetLastError();
 }
 
-template <int D1, int Q1, unsigned K>
+template <int D1, int Q1, unsigned K, int EZ = kHoBrick>
 static hipError_t hobrick_launch(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old, double *d_new,
                                  double *x)
 {
-    constexpr int NT = ((kHoBrick * kHoBrick * kHoBrick * D1 * D1 + 63) / 64) * 64;
+    if constexpr (EZ == kHoBrick) {
+        if (c->hb_ez == 4) return hobrick_launch<D1, Q1, K, 4>(c, r, dinv, d_old, d_new, x);
+    }
+    if (c->hb_ez != EZ) return hipErrorInvalidValue;
+    constexpr int NT = ((kHoBrick * kHoBrick * EZ * D1 * D1 + 63) / 64) * 64;
     const Tab<D1, Q1> T = make_tab<D1, Q1>(c->rule_op);
     const double *kt = nullptr;
     if (c->d_hbpart == nullptr) return hipErrorInvalidValue;
@@ -1194,9 +1213,9 @@ static hipError_t hobrick_launch(cdfem_ctx *c, const double *r, const double *di
     const BrickGeom g = geom_of(c);
     const dim3 grid((unsigned)c->hb_nblk), block(NT);
 #define CDFEM_HB(XF_, MF_)                                                                                     \
-    CDFEM_LAUNCH(c, (k_hobrick_cg<D1, Q1, K, XF_, MF_>), grid, block, 0, r, dinv, d_old, d_new, c->d_face, c->d_qaff, \
+    CDFEM_LAUNCH(c, (k_hobrick_cg<D1, Q1, K, XF_, MF_, EZ>), grid, block, 0, r, dinv, d_old, d_new, c->d_face, c->d_qaff, \
                  c->d_ess, T, g, c->sx, c->sy, c->sz, c->d_hbpart, c->d_state, x, kt)
-    if constexpr (K == 7) {  // the MFMA x stage is built for the full operator only (ho_brick_mfma)
+    if constexpr (K == 7 && EZ == kHoBrick) {  // the MFMA x stage: the full operator on 2^3 blocks (ho_brick_mfma)
         if (c->ho_brick_mfma) {
             if (x) { CDFEM_HB(true, true); } else { CDFEM_HB(false, true); }
             return hipGetLastError();
@@ -1351,7 +1370,7 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     const double *const apart = c->den_grp > 1 ? c->d_gsum : c->d_part;
     const int napart = c->den_grp > 1 ? den_parts(c) : c->nblk;
 #define CDFEM_UPD4(S_, XF_, PB_, DS_, EP_)                                                                 \
-    hipLaunchKernelGGL((k_cg_update_faces<S_, XF_, PB_, DS_, EP_>), dim3(ugrid), dim3(kRedThreads), 0, c->stream, x, \
+    hipLaunchKernelGGL((k_cg_update_faces<S_, XF_, PB_, DS_, EP_, SZ_>), dim3(ugrid), dim3(kRedThreads), 0, c->stream, x, \
                        r, d, dinv, c->d_face, c->d_ess, g, fdx, fdxy, c->zlo_shared, remote_lo, remote_hi, upart, \
                        c->d_state, (int)den_step, apart, napart)
     // the apply's essential-row patch entries (k_brick_cg EP: the Kronecker form at p <= 2)
@@ -1368,11 +1387,21 @@ hipError_t launch_cg_update_faces(cdfem_ctx *c, double *x, double *r, const doub
     } else {                                                                                                \
         if (pb) { CDFEM_UPD2(S_, false, true); } else { CDFEM_UPD2(S_, false, false); }                     \
     }
+    // (SZ_: the patch's z side, in scope of CDFEM_UPD4; p = 3, 4 with ho_block_z 4: 2 x 2 x 4 blocks)
     if (c->p == 1) {
+        constexpr int SZ_ = kBrick * 1 + 1;
         CDFEM_UPD(kBrick * 1 + 1);
-    } else if (c->p == 2 || c->p == 4) {  // (p = 4: 2^3-element blocks, the same 9^3 patch)
+    } else if (c->p == 2 || (c->p == 4 && c->hb_ez == 2)) {  // (p = 4: 2^3-element blocks, the same 9^3 patch)
+        constexpr int SZ_ = kBrick * 2 + 1;
         CDFEM_UPD(kBrick * 2 + 1);
-    } else if (c->p == 3) {
+    } else if (c->p == 4 && c->hb_ez == 4) {
+        constexpr int SZ_ = 4 * 4 + 1;
+        CDFEM_UPD(kHoBrickEdge * 4 + 1);
+    } else if (c->p == 3 && c->hb_ez == 2) {
+        constexpr int SZ_ = kHoBrickEdge * 3 + 1;
+        CDFEM_UPD(kHoBrickEdge * 3 + 1);
+    } else if (c->p == 3 && c->hb_ez == 4) {
+        constexpr int SZ_ = 4 * 3 + 1;
         CDFEM_UPD(kHoBrickEdge * 3 + 1);
     } else {
         return hipErrorInvalidValue;

@@ -180,17 +180,18 @@ void free_mesh(cdfem_ctx *c)
     c->hb_nblk = 0;
 }
 
-// per brick (edge E elements, nb* bricks per axis): 1 if a lattice dof of its patch (E p + 1 per axis,
-// clipped to the lattice) is essential; the brick CG kernels skip the essential-flag loads elsewhere
-static void upload_brick_ess(cdfem_ctx *c, int E, int nbx, int nby, int nbz)
+// per brick (edge E elements in x and y, EZ in z; nb* bricks per axis): 1 if a lattice dof of its patch
+// (E p + 1 per axis, EZ p + 1 along z, clipped to the lattice) is essential; the brick CG kernels skip the
+// essential-flag loads elsewhere
+static void upload_brick_ess(cdfem_ctx *c, int E, int EZ, int nbx, int nby, int nbz)
 {
-    const int64_t s1 = (int64_t)E * c->p, Lx = c->Lx, Ly = c->Ly, Lz = c->Lz;
+    const int64_t s1 = (int64_t)E * c->p, sz1 = (int64_t)EZ * c->p, Lx = c->Lx, Ly = c->Ly, Lz = c->Lz;
     std::vector<uint8_t> has((size_t)nbx * nby * nbz, 0);
     for (int bz = 0; bz < nbz; ++bz)
         for (int by = 0; by < nby; ++by)
             for (int bx = 0; bx < nbx; ++bx) {
                 uint8_t h = 0;
-                for (int64_t z = bz * s1; z <= std::min(bz * s1 + s1, Lz - 1) && !h; ++z)
+                for (int64_t z = bz * sz1; z <= std::min(bz * sz1 + sz1, Lz - 1) && !h; ++z)
                     for (int64_t y = by * s1; y <= std::min(by * s1 + s1, Ly - 1) && !h; ++y) {
                         const uint8_t *row = c->h_ess.data() + (size_t)(z * Ly + y) * Lx;
                         for (int64_t x = bx * s1; x <= std::min(bx * s1 + s1, Lx - 1); ++x) h |= row[x];
@@ -453,8 +454,8 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     if (!c->d_dalt) c->d_dalt = dalloc<double>(c->nl);
     const int nbrick = brick_count(c);
     if (!c->d_face) {  // (p = 3, 4: the blocks' patch buffer, first use)
-        const int S = brick_patch_side(c);
-        c->d_face = dalloc<double>((size_t)nbrick * S * S * S);
+        const int S = brick_patch_side(c), SZ = brick_patch_side_z(c);
+        c->d_face = dalloc<double>((size_t)nbrick * S * S * SZ);
     }
     // the apply's den partials in two stages (a block per 1/256 of them, then one block) when the one
     // block finalizer would sum too many: the p = 3, 4 blocks, and one rank past the den fold's bound
@@ -1005,11 +1006,12 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
             // (k_e2l_box); element-major qdata and map are kept
             c->structured = true;
             c->epencil = c->nl < ((int64_t)1 << 32);
+            c->hb_ez = c->ho_block_z;
             c->hb_nbx = (nx + kHoBrickEdge - 1) / kHoBrickEdge;
             c->hb_nby = (ny + kHoBrickEdge - 1) / kHoBrickEdge;
-            c->hb_nbz = (nz + kHoBrickEdge - 1) / kHoBrickEdge;
+            c->hb_nbz = (nz + c->hb_ez - 1) / c->hb_ez;
             c->hb_nblk = c->hb_nbx * c->hb_nby * c->hb_nbz;
-            upload_brick_ess(c, kHoBrickEdge, c->hb_nbx, c->hb_nby, c->hb_nbz);
+            upload_brick_ess(c, kHoBrickEdge, c->hb_ez, c->hb_nbx, c->hb_nby, c->hb_nbz);
             dfree(c->d_face);  // the high-order brick CG's patch buffer: allocated by its first solve
             return CDFEM_OK;
         }
@@ -1017,7 +1019,7 @@ int cdfem_mesh_set_structured(cdfem_ctx *c, int nx, int ny, int nz)
         c->nby = (ny + kBrick - 1) / kBrick;
         c->nbz = (nz + kBrick - 1) / kBrick;
         c->nblk = c->nbx * c->nby * c->nbz;
-        upload_brick_ess(c, kBrick, c->nbx, c->nby, c->nbz);
+        upload_brick_ess(c, kBrick, kBrick, c->nbx, c->nby, c->nbz);
         // brick permutation: block = brick (lexicographic), lane = ex + 4 (ey + 4 ez)
         std::vector<int32_t> perm((size_t)c->nblk * kLanes, -1);
         for (int b = 0; b < c->nblk; ++b) {
@@ -1843,6 +1845,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "ho_brick_mfma") {
             if (value != 0 && value != 1) throw ArgError("ho_brick_mfma must be 0 or 1");
             c->ho_brick_mfma = value;
+        } else if (k == "ho_block_z") {  // read by cdfem_mesh_set_structured
+            if (value != 2 && value != 4) throw ArgError("ho_block_z must be 2 or 4");
+            c->ho_block_z = value;
         } else if (k == "ho_brick") {
             if (value != 0 && value != 1) throw ArgError("ho_brick must be 0 or 1");
             c->ho_brick = value;
@@ -2042,8 +2047,8 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
         if (use_hobrick_cg(c) && (k == CDFEM_K_APPLY || k == CDFEM_K_UPDATE)) {
             // the high-order brick CG: factors + gathered r, M^-1, d + ess flags + d (writer) + patch
             // outputs (+ x read and written under the x-fold); update: r, M^-1, ess, r write + patches
-            const double S = brick_patch_side(c);
-            const double patches = 8.0 * S * S * S * (double)brick_count(c);
+            const double S = brick_patch_side(c), SZ = brick_patch_side_z(c);
+            const double patches = 8.0 * S * S * SZ * (double)brick_count(c);
             const bool xf = c->cg_xfold != 0;
             *bytes = k == CDFEM_K_APPLY ? 8.0 * c->ncomp * ne + 33.0 * nl + patches + (xf ? 16.0 * nl : 0.0)
                                         : (xf ? 25.0 : 49.0) * nl + patches;

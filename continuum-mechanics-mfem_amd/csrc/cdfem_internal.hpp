@@ -154,6 +154,9 @@ struct cdfem_ctx {
     // 3D p = 3, 4 on a structured box: blocks of kHoBrickEdge^3 elements for the high-order brick CG
     // (brick_kernels.hip k_hobrick_cg; set_option "ho_brick")
     int hb_nbx = 0, hb_nby = 0, hb_nbz = 0, hb_nblk = 0;
+    int ho_block_z = 2;                 // set_option "ho_block_z": elements per block along z (2 or 4), read by
+                                        // cdfem_mesh_set_structured; 4 = 2 x 2 x 4 blocks
+    int hb_ez = 2;                      //   the block depth of the current structured box
     uint8_t *d_bess = nullptr;          // per brick (block): 1 if a dof of its patch is essential
     int ho_brick = 1;                   // set_option "ho_brick": high-order CG through k_hobrick_cg + the brick update
     double *d_hbpart = nullptr;         // den partials summed in two stages: k_hobrick_cg's, and k_brick_cg's past
@@ -363,6 +366,7 @@ constexpr int kHoBrickEdge = 2;         // p = 3, 4: elements per block edge of 
 bool brick_supported(int dim, int p);
 int brick_count(const cdfem_ctx *c);        // bricks (p <= 2) or high-order blocks (p = 3, 4)
 int brick_patch_side(const cdfem_ctx *c);   // S: 4p + 1 (p <= 2), 2p + 1 (p = 3, 4)
+int brick_patch_side_z(const cdfem_ctx *c); // the patch's z side: S, or hb_ez p + 1 (p = 3, 4)
 bool cg_den_fold_on(const cdfem_ctx *c);
 bool cg_mr_fold(const cdfem_ctx *c);
 // den partial groups of the brick CG apply at p <= 2: 1 when the bricks fit the fold bounds, else the

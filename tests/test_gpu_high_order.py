@@ -420,6 +420,50 @@ def test_ho_brick_cg_parity(gpu_ctx, shape, p, kinds):
         assert np.linalg.norm(conv[1][0] - conv[0][0]) <= 1e-10 * np.linalg.norm(conv[0][0])
 
 
+@pytest.mark.parametrize("shape,p,kinds", [((4, 4, 8), 4, 7), ((3, 5, 6), 4, 5), ((5, 3, 7), 3, 7), ((2, 3, 3), 4, 3),
+                                           ((4, 2, 9), 3, 5)])
+def test_ho_block_z4_parity(gpu_ctx, shape, p, kinds):
+    """ho_block_z 4: the high-order brick CG on 2 x 2 x 4-element blocks (16 element tiles per block, an
+    S x S x (4p + 1) patch; k_cg_update_faces with the patch's z side).  Boxes with partial blocks in z
+    (6, 7, 3, 9 element layers) and in x / y, non-zero essential values: 40 fixed Jacobi-CG iterates
+    against the oracle (1e-11) and against the 2^3 blocks (1e-12), bitwise repeatable; on the SPD operator
+    a converging solve stops on the 2^3 blocks' iteration."""
+    om = O.BoxMesh(3, shape, p)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3, kinds=_kinds_o(kinds))
+    gm = cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)
+    rng = np.random.default_rng(41)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
+    out, conv = {}, {}
+    try:
+        for bz in (4, 2):
+            gpu_ctx.set_option("ho_block_z", bz)
+            gpu_ctx.upload_mesh(gm).set_structured(*shape)
+            gpu_ctx.pa_setup(kinds=kinds, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+            assert gpu_ctx.kernel_name(cdfem.K_APPLY) == "k_hobrick_cg"
+            _, B = gpu_ctx.form_linear_system(u, b)
+            out[bz] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=7)
+            if bz == 4:
+                again = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40)
+                np.testing.assert_array_equal(again[0], out[bz][0])
+            if kinds == 5:
+                conv[bz] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=1e-10, max_iter=2000, check_every=9)
+    finally:
+        gpu_ctx.set_option("ho_block_z", 2)
+    for bz, (xg, ig) in out.items():
+        assert ig["iterations"] == 40
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), bz
+    assert np.linalg.norm(out[4][0] - out[2][0]) <= 1e-12 * np.linalg.norm(out[2][0])
+    if conv:
+        assert conv[4][1]["converged"] and conv[4][1]["iterations"] == conv[2][1]["iterations"]
+        assert np.linalg.norm(conv[4][0] - conv[2][0]) <= 1e-10 * np.linalg.norm(conv[2][0])
+    with pytest.raises(cdfem.CdfemError):
+        gpu_ctx.set_option("ho_block_z", 3)
+
+
 def test_ho_brick_c3_full_size_residual(gpu_ctx):
     """C3 itself (128^3 p = 4, 135 M DoFs) through the block CG: 20 Jacobi-CG iterations on the full
     operator, then the recomputed constrained residual equals the recursive one and the iterates
