@@ -544,7 +544,14 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // with its patch gather, sums them in one fixed order, takes MFEM's decision (workgroup 0 records it,
 // cg_update_logic; kk = updates so far, from the host) and forms beta itself, so the one-block update
 // finalizer is not launched.
-template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false, bool BF = false, bool FULL = false>
+// MX (set_option "brick_mfma", kinds 7, the Kronecker form): the x stage of the brick's
+// 64 elements on the matrix cores.  Per input plane jz and row jy, four v_mfma_f64_16x16x4_f64 (16 elements
+// each): A = the 1D matrices stacked as rows (q, ix) = 4 q + ix (M, K, C, C^T; 12 of 16 rows), k = jx (3 of
+// 4), B = the 16 elements' input rows from the LDS patch (column = element).  Lane (ix, element) then holds
+// that element's four x-applied values for column ix and stores them to LDS, where each element's thread
+// reads them back for the combinations and the y / z stages (kron_core otherwise).  A/B in DESIGN.md 4.1.
+template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false, bool BF = false, bool FULL = false,
+          bool MX = false>
 __global__ void __launch_bounds__(64, W)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
@@ -573,6 +580,8 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     constexpr bool EP = AF == 2;
     constexpr bool EPL = EP && CDFEM_BRICK_LDS == 0;
     __shared__ double s_d[EPL ? S3 : 1];
+    static_assert(!MX || (AF == 2 && D1 == 3), "the MFMA x stage is built for the p = 2 Kronecker form");
+    __shared__ double s_x[MX ? 3 * 3 * 4 * 64 : 1];  // MX: [jy][ix][q][element] of one input plane
     if (st->done) return;
     double beta = st->beta;
     constexpr int NPL = 16;  // BF: partials per lane (nupart <= 64 NPL)
@@ -702,7 +711,66 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const int o0 = P * ez * SZ + P * ey * SY + P * ex;
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * SZ + dy * SY + dx]; };
     double Y[D1][D1][D1];
-    elem_apply3d_af<D1, Q1, K, AF>(xl, q0, t, T, Y);
+    if constexpr (MX) {
+        double gk[NC];
+        kron_load_g<K>(q0, t, gk);
+        // A operand: lane (row = l & 15 = 4 q + ix, k = l >> 4 = jx) -> F_q[ix][jx] (0 in the padding)
+        const int row = t & 15, kq = t >> 4, qa = row >> 2, ia = row & 3;
+        double av = 0.0;
+        static_for<0, D1>([&](auto ic) {
+            static_for<0, D1>([&](auto jc) {
+                constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
+                const double fm = tM(T, i, j), fk = tK(T, i, j), fc = tCacc(T, i, j, 1.0, 0.0),
+                             fct = tCacc(T, j, i, 1.0, 0.0);
+                if (ia == i && kq == j) av = qa == 0 ? fm : qa == 1 ? fk : qa == 2 ? fc : fct;
+            });
+        });
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+            for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < D1; ++dx) Y[dz][dy][dx] = 0.0;
+#pragma unroll
+        for (int jz = 0; jz < D1; ++jz) {
+#pragma unroll
+            for (int jy = 0; jy < D1; ++jy)
+#pragma unroll
+                for (int tl = 0; tl < 4; ++tl) {
+                    const int eb = 16 * tl + row;  // B column = element of tile tl
+                    const int ob = P * (eb >> 4) * SZ + P * ((eb >> 2) & 3) * SY + P * (eb & 3);
+                    const double bv = kq < D1 ? s_in[ob + jz * SZ + jy * SY + kq] : 0.0;
+                    const v4d_t acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, v4d_t{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+                    if (kq < D1) {  // lane (ix = kq, element eb): its (M, K, C, C^T) X row values
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) s_x[((jy * 3 + kq) * 4 + q) * 64 + eb] = acc[q];
+                    }
+                }
+            __syncthreads();
+#pragma unroll
+            for (int ix = 0; ix < D1; ++ix) {
+                double v[D1][5];
+#pragma unroll
+                for (int jy = 0; jy < D1; ++jy) {
+                    const double *xr = &s_x[((jy * 3 + ix) * 4) * 64 + t];
+                    kron_xcombine<K>(gk, xr[0], xr[64], xr[128], xr[192], v[jy]);
+                }
+                auto col = [&](int q, int jy) { return v[jy][q]; };
+#pragma unroll
+                for (int iy = 0; iy < D1; ++iy) {
+                    double Yz[D1];
+#pragma unroll
+                    for (int iz = 0; iz < D1; ++iz) Yz[iz] = Y[iz][iy][ix];
+                    kron_yz<D1, Q1, K>(T, gk, col, iy, jz, Yz);
+#pragma unroll
+                    for (int iz = 0; iz < D1; ++iz) Y[iz][iy][ix] = Yz[iz];
+                }
+            }
+            __syncthreads();
+        }
+    } else {
+        elem_apply3d_af<D1, Q1, K, AF>(xl, q0, t, T, Y);
+    }
 
     // element-wise den contribution d0_e . (A_e d0_e) and deterministic in-LDS E->L
 #pragma unroll
@@ -1163,15 +1231,24 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     const double *upart = c->d_part + c->nblk;  // the den-fold update's partials
     double *const dpart = c->den_out ? c->den_out : c->d_part;  // the apply's den partials
     const int grp = c->den_grp, nbrick = c->nblk;               // (grouped: sums into d_gsum)
-#define CDFEM_BCG5(AFF_, W_, XF_, BF_, FU_)                                                                 \
+#define CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, MX_)                                                            \
     if (whole)                                                                                               \
-        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_>), grid, block, 0, r, dinv, d_old, d_new, q, \
+        CDFEM_LAUNCH(c, (k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_, MX_>), grid, block, 0, r, dinv, d_old, d_new, q, \
                      c->d_face, qd, c->d_ess, T, g, c->zlo_shared, dpart, c->d_state, x, upart, run.nupart,     \
                      run.kk, c->d_gsum, c->d_gcnt, grp, nbrick);                                             \
     else                                                                                                     \
-        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_>), grid, block, 0, run.s, r, dinv,     \
+        hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_, MX_>), grid, block, 0, run.s, r, dinv, \
                            d_old, d_new, q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, dpart, c->d_state, x, \
                            upart, run.nupart, run.kk, c->d_gsum, c->d_gcnt, grp, nbrick)
+    // (brick_mfma: the MFMA x stage, built for the Kronecker form of the full operator at p = 2)
+    constexpr bool kMX = K == 7 && D1 == 3;
+    const bool mx = kMX && c->brick_mfma != 0;
+#define CDFEM_BCG5(AFF_, W_, XF_, BF_, FU_)                                                                 \
+    if constexpr (kMX && AFF_ == 2) {                                                                        \
+        if (mx) { CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, kMX); } else { CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, false); } \
+    } else {                                                                                                 \
+        CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, false);                                                          \
+    }
 #define CDFEM_BCG4(AFF_, W_, XF_, BF_)                                                                      \
     if (full) { CDFEM_BCG5(AFF_, W_, XF_, BF_, true); } else { CDFEM_BCG5(AFF_, W_, XF_, BF_, false); }
 #define CDFEM_BCG3(AFF_, W_, XF_) CDFEM_BCG5(AFF_, W_, XF_, false, false)
@@ -1193,6 +1270,7 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
 #undef CDFEM_BCG3
 #undef CDFEM_BCG4
 #undef CDFEM_BCG5
+#undef CDFEM_BCG6
     return hipGetLastError();
 }
 

@@ -1845,6 +1845,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "ho_brick_mfma") {
             if (value != 0 && value != 1) throw ArgError("ho_brick_mfma must be 0 or 1");
             c->ho_brick_mfma = value;
+        } else if (k == "brick_mfma") {
+            if (value != 0 && value != 1) throw ArgError("brick_mfma must be 0 or 1");
+            c->brick_mfma = value;
         } else if (k == "ho_block_z") {  // read by cdfem_mesh_set_structured
             if (value != 2 && value != 4) throw ArgError("ho_block_z must be 2 or 4");
             c->ho_block_z = value;

@@ -259,6 +259,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *              update and the next apply take MFEM's den and betanom steps as on one rank (no sum or
  *              step kernels between them); taken only when every rank holds as many partials (checked
  *              once, collectively); 0 = per-rank sums, 8-byte all-reduces and step kernels.
+ * "brick_mfma": 0 (default) or 1 — the p = 2 brick CG apply's x stage (kinds 7, Kronecker form) on
+ *              v_mfma_f64_16x16x4_f64: 16 elements per GEMM, outputs staged through LDS to the element
+ *              threads.  Parity-green, measured slower.
  * "ho_block_z": 2 (default) or 4 — elements per block along z of the high-order brick CG (read by
  *              cdfem_mesh_set_structured): 2 x 2 x 2 blocks (8 element tiles, 200 of 256 threads busy at
  *              p = 4) or 2 x 2 x 4 (16 tiles, 400 of 448; 1.34 patch entries per dof against 1.42).

@@ -107,6 +107,40 @@ def test_den_fold_matches_den_finalizer(gpu_ctx, shape, p, kinds, fold):
         assert np.linalg.norm(conv[fold][0] - conv[0][0]) <= 1e-10 * np.linalg.norm(conv[0][0])
 
 
+@pytest.mark.parametrize("shape,pert", [((8, 8, 8), 0.0), ((9, 6, 7), 0.0), ((5, 9, 10), 0.0)])
+def test_brick_mfma_x_stage_parity(gpu_ctx, shape, pert):
+    """brick_mfma: k_brick_cg's x stage (p = 2, kinds 7, Kronecker form) on v_mfma_f64_16x16x4_f64, 16
+    elements per GEMM, the outputs staged through LDS to the element threads.  Partial bricks, non-zero
+    essential values: 40 fixed Jacobi-CG iterates against the oracle (1e-11) and against the VALU x stage
+    (1e-12; the matrix core sums each length-3 row in its own order), bitwise repeatable."""
+    p = 2
+    om = O.BoxMesh(3, shape, p, perturb=pert)
+    A = O.fa_assemble(om, kappa=0.1, alpha=1.0, s=1.0, c=C3)
+    rng = np.random.default_rng(43)
+    u = np.zeros(om.nl)
+    u[om.ess] = rng.uniform(-1, 1, len(om.ess))
+    b = rng.uniform(-1, 1, om.nl)
+    Ac, Bo = O.form_linear_system(A, om.bdr, u, b)
+    xo, _ = O.cg(Ac, Bo, dinv=1.0 / Ac.diag(), rel_tol=0.0, abs_tol=0.0, max_iter=40)
+    gpu_ctx.upload_mesh(cdfem.Mesh(3, p, om.verts, om.dofmap, om.nl, om.ess)).set_structured(*shape)
+    gpu_ctx.pa_setup(kinds=7, kappa=0.1, alpha=1.0, conv=C3, mass=1.0)
+    _, B = gpu_ctx.form_linear_system(u, b)
+    out = {}
+    try:
+        for mx in (1, 0):
+            gpu_ctx.set_option("brick_mfma", mx)
+            out[mx] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=7)
+        gpu_ctx.set_option("brick_mfma", 1)
+        again = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40)
+    finally:
+        gpu_ctx.set_option("brick_mfma", 0)
+    np.testing.assert_array_equal(again[0], out[1][0])
+    for mx, (xg, ig) in out.items():
+        assert ig["iterations"] == 40
+        assert np.linalg.norm(xg - xo) <= 1e-11 * np.linalg.norm(xo), mx
+    assert np.linalg.norm(out[1][0] - out[0][0]) <= 1e-12 * np.linalg.norm(out[0][0])
+
+
 @pytest.mark.parametrize("shape,p,kinds,grp", [((12, 16, 8), 2, 7, 8), ((12, 16, 8), 2, 5, 16), ((9, 6, 7), 2, 7, 4),
                                                 ((10, 8, 13), 1, 7, 64)])
 def test_den_group_matches_ungrouped(gpu_ctx, shape, p, kinds, grp):
