@@ -456,13 +456,7 @@ def main_c4(args):
         o_ms, o_cnt = ctx.profile_read(cdfem.K_ORTH)
         ctx.profile(False)
         if cnt:
-            # every solve ends with an apply that returns at its first check (the update before it set
-            # `done`, or its betanom step stops the solve): a launch with no work.  The roofline
-            # divides the launch's bytes by the FULL launches' average (>= half the median: the
-            # early-return ones take a few us); the all-launch average is kept beside it
-            full = each[each >= 0.5 * np.median(each)] if len(each) else each
-            per_all = ms / cnt * 1e-3
-            per = float(full.mean()) * 1e-3 if len(full) else per_all
+            per = ms / cnt * 1e-3
             bytes_ = ctx.kernel_bytes(cdfem.K_APPLY)
             traffic = None
             if os.path.exists(args.traffic_json):
