@@ -20,7 +20,24 @@ struct BrickGeom {
     int xcd;            // 1: XCD-contiguous brick order (default; set_option "brick_xcd")
     int bz0, bzs;       // k_brick_cg: the launch covers brick layers bz0, bz0 + bzs, ... (all: 0, 1)
     const uint8_t *bess;  // per brick: 1 if a dof of its patch is essential (nullptr: assume so)
+    // first-round stagger of the brick CG apply (k_brick_cg; set_option "brick_stagger"):
+    // stag bits 0-3 a shift s, bits 4-8 a count n; stag_round = the workgroups resident at once (2 per SIMD)
+    int stag = 0, stag_round = 0;
 };
+
+// The first round of a brick kernel's workgroups starts together, so every wave gathers its patch at
+// once (one HBM burst) and then every wave computes (one VALU crush).  Workgroups b < stag_round with bit
+// s of b set (s = log2 CUs: half of every CU's waves) sleep n x 2,048 cycles first, so half the first
+// round gathers while the other half computes.  Launches of at least two rounds only.  C2 (4,096 bricks
+// on 256 CUs, n = 4): k_brick_cg 39.0 -> 37.4 us (profiles/r06/ab_c2_stagger/); the GMRES leg's Mult
+// (k_brick3d, whose gather is one vector) ran 35.0 -> 35.8 us with it and is left alone.
+__device__ __forceinline__ void brick_stagger(const BrickGeom &g)
+{
+    if (g.stag == 0 || gridDim.x < 2u * (unsigned)g.stag_round) return;
+    const unsigned wb = blockIdx.x;
+    if (wb < (unsigned)g.stag_round && ((wb >> (g.stag & 15)) & 1u))
+        for (int i = 0; i < ((g.stag >> 4) & 31); ++i) __builtin_amdgcn_s_sleep(32);
+}
 
 // Raw buffer access (MI355X buffer resources): a 32-bit byte offset from a scalar base instead of a
 // 64-bit address per lane, and an offset past num_records (kOOB) reads 0 and drops a store, so the

@@ -419,7 +419,15 @@ bool brick_fits(const cdfem_ctx *c)
 static BrickGeom geom_of(const cdfem_ctx *c)
 {
     if (c->p >= 3) return BrickGeom{c->hb_nbx, c->hb_nby, c->hb_nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1, c->d_bess};
-    return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1, c->d_bess};
+    // brick_stagger: -1 automatic (shift log2 CUs when the CU count is a power of two, n = 4), 0 off
+    int stag = c->brick_stagger;
+    if (stag < 0) {
+        int sh = 0;
+        while ((1 << sh) < c->ncu) ++sh;
+        stag = (c->ncu > 0 && (1 << sh) == c->ncu) ? (sh | (4 << 4)) : 0;
+    }
+    return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1, c->d_bess,
+                     stag, 8 * c->ncu};
 }
 
 int brick_count(const cdfem_ctx *c) { return c->p >= 3 ? c->hb_nblk : c->nblk; }
@@ -583,6 +591,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     static_assert(!MX || (AF == 2 && D1 == 3), "the MFMA x stage is built for the p = 2 Kronecker form");
     __shared__ double s_x[MX ? 3 * 3 * 4 * 64 : 1];  // MX: [jy][ix][q][element] of one input plane
     if (st->done) return;
+    brick_stagger(g);
     double beta = st->beta;
     constexpr int NPL = 16;  // BF: partials per lane (nupart <= 64 NPL)
     double pv[NPL];

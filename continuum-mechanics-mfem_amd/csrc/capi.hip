@@ -1845,6 +1845,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "ho_brick_mfma") {
             if (value != 0 && value != 1) throw ArgError("ho_brick_mfma must be 0 or 1");
             c->ho_brick_mfma = value;
+        } else if (k == "brick_stagger") {
+            if (value < -1 || value > 511) throw ArgError("brick_stagger must be -1 (automatic), 0 (off) or 1..511");
+            c->brick_stagger = value;
         } else if (k == "brick_mfma") {
             if (value != 0 && value != 1) throw ArgError("brick_mfma must be 0 or 1");
             c->brick_mfma = value;

@@ -171,6 +171,7 @@ struct cdfem_ctx {
     uint32_t *d_gcnt = nullptr;         // [same] arrival counters (0 between launches)
     int64_t gsum_cap = 0;
     int ho_brick_mfma = 0;              // set_option "ho_brick_mfma": its x stage on v_mfma_f64_16x16x4_f64 (kinds 7)
+    int brick_stagger = -1;             // set_option "brick_stagger": BrickGeom::stag (-1 automatic, 0 off)
     int brick_mfma = 0;                 // set_option "brick_mfma": k_brick_cg's x stage on the matrix cores (p = 2, kinds 7)
     int64_t Lx = 0, Ly = 0, Lz = 0;     // dof lattice per axis
     double *d_face = nullptr;           // [nblk][F] brick-face partial sums

@@ -259,6 +259,11 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *              update and the next apply take MFEM's den and betanom steps as on one rank (no sum or
  *              step kernels between them); taken only when every rank holds as many partials (checked
  *              once, collectively); 0 = per-rank sums, 8-byte all-reduces and step kernels.
+ * "brick_stagger": -1 (default, automatic: s = log2 CUs, n = 4), 0 off, or bits 0-3 a shift s and bits
+ *              4-8 a count n: the first round of the brick CG apply (k_brick_cg workgroups b < 8 x CUs,
+ *              launches of >= 2 rounds) with bit s of b set sleeps n x 2,048 cycles at entry, so half the
+ *              round gathers its patches while the other half computes (C2: 39.0 -> 37.4 us per apply,
+ *              DESIGN.md 4.1).
  * "brick_mfma": 0 (default) or 1 — the p = 2 brick CG apply's x stage (kinds 7, Kronecker form) on
  *              v_mfma_f64_16x16x4_f64: 16 elements per GEMM, outputs staged through LDS to the element
  *              threads.  Parity-green, measured slower.
