@@ -996,7 +996,7 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
              double *__restrict__ d_new, double *__restrict__ face, const double *__restrict__ qaff,
              const uint8_t *__restrict__ ess, const Tab<D1, Q1> T, const BrickGeom g, int nex, int ney, int nez,
              double *__restrict__ part, const KrylovState *__restrict__ st, double *__restrict__ x,
-             const double *__restrict__ ktab)
+             const double *__restrict__ ktab, int zlo_shared)
 {
     using L = QLayout<K, 3>;
     constexpr int P = D1 - 1, EB = kHoBrick, S = EB * P + 1, SZ = EZ * P + 1, S2 = S * S, S3 = S * S * SZ;
@@ -1080,7 +1080,8 @@ k_hobrick_cg(const double *__restrict__ r, const double *__restrict__ dinv, cons
             const uint32_t woff = writer ? offv[k] : kOOB;
             bstore(bd, woff, dn);
             if constexpr (XF) bstore(bxf, woff, xv[k] + alpha_prev * ov[k]);
-            den += (writer && e) ? dn * dn : 0.0;  // (A_c d)_i = d_i on ess dofs
+            // (A_c d)_i = d_i on ess dofs; on a slab the lower plane's are the rank below's
+            den += (writer && e && !(zlo_shared && gz0 + pz == 0)) ? dn * dn : 0.0;
             s_in[i] = e ? 0.0 : dn;
         }
     }
@@ -1301,7 +1302,7 @@ static hipError_t hobrick_launch(cdfem_ctx *c, const double *r, const double *di
     const dim3 grid((unsigned)c->hb_nblk), block(NT);
 #define CDFEM_HB(XF_, MF_)                                                                                     \
     CDFEM_LAUNCH(c, (k_hobrick_cg<D1, Q1, K, XF_, MF_, EZ>), grid, block, 0, r, dinv, d_old, d_new, c->d_face, c->d_qaff, \
-                 c->d_ess, T, g, c->sx, c->sy, c->sz, c->d_hbpart, c->d_state, x, kt)
+                 c->d_ess, T, g, c->sx, c->sy, c->sz, c->d_hbpart, c->d_state, x, kt, c->zlo_shared)
     if constexpr (K == 7 && EZ == kHoBrick) {  // the MFMA x stage: the full operator on 2^3 blocks (ho_brick_mfma)
         if (c->ho_brick_mfma) {
             if (x) { CDFEM_HB(true, true); } else { CDFEM_HB(false, true); }
@@ -1557,11 +1558,16 @@ hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q, hipStream_t s)
     const int n = (int)(c->Lx * c->Ly);
     const dim3 grid((n + 255) / 256), block(256);
     if (!s) s = c->stream;
+    // (p = 3, 4: the 2^3-element blocks' cubic patches, S = 2p + 1; p = 4 shares S = 9 with p = 2)
+    if (c->p >= 3 && c->hb_ez != kHoBrickEdge) return hipErrorInvalidValue;
     if (c->p == 1)
         hipLaunchKernelGGL(k_pack_qplanes<kBrick * 1 + 1>, grid, block, 0, s, q, c->d_face, g,
                            c->zlo_shared, c->zhi_shared, c->d_if[0], c->d_if[2], c->d_state);
-    else if (c->p == 2)
+    else if (c->p == 2 || c->p == 4)
         hipLaunchKernelGGL(k_pack_qplanes<kBrick * 2 + 1>, grid, block, 0, s, q, c->d_face, g,
+                           c->zlo_shared, c->zhi_shared, c->d_if[0], c->d_if[2], c->d_state);
+    else if (c->p == 3)
+        hipLaunchKernelGGL(k_pack_qplanes<kHoBrickEdge * 3 + 1>, grid, block, 0, s, q, c->d_face, g,
                            c->zlo_shared, c->zhi_shared, c->d_if[0], c->d_if[2], c->d_state);
     else
         return hipErrorInvalidValue;

@@ -293,12 +293,13 @@ void build_layout(cdfem_ctx *c, const std::vector<int32_t> &perm)
 
 bool use_brick(const cdfem_ctx *c) { return c->structured && brick_supported(c->dim, c->p) && brick_fits(c); }
 
-// the high-order brick CG (3D p = 3, 4, one rank, affine box with constant coefficients: the Kronecker
-// tile core on 2^3-element blocks, brick_kernels.hip k_hobrick_cg, then the brick update)
+// the high-order brick CG (3D p = 3, 4, affine box with constant coefficients: the Kronecker tile core on
+// 2^3-element blocks, brick_kernels.hip k_hobrick_cg, then the brick update); on several ranks a z-slab
+// of 2^3 blocks (round 6: the plane pack and exchange of the p = 2 brick CG, rank-local den sums)
 bool use_hobrick_cg(const cdfem_ctx *c)
 {
     return c->ho_brick != 0 && c->structured && c->qlay == 1 && c->hb_nblk > 0 && tile_kron(c) && tile_den_ok(c) &&
-           !multi_rank(c) && !c->fa_ready && brick_fits(c);
+           (!multi_rank(c) || (c->part_mode == 1 && c->hb_ez == kHoBrickEdge)) && !c->fa_ready && brick_fits(c);
 }
 bool use_brick_cg(const cdfem_ctx *c) { return use_brick(c) || use_hobrick_cg(c); }
 
@@ -491,7 +492,7 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
     // only, so those layers run first on a side stream, whose pack + exchange then overlap the
     // interior layers on the main stream.  Same kernels, same sums: bitwise equal
     // to the one-launch form.  Profiling keeps the one-launch form (one timed apply kernel).
-    const bool overlap = mr && c->mr_overlap && !c->profile && c->nbz >= 3;
+    const bool overlap = mr && c->mr_overlap && !c->profile && c->p <= 2 && c->nbz >= 3;
     if (overlap && !c->stream2) {
         HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
         for (auto &e : c->ov_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -553,7 +554,8 @@ void solve_cg_brick(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB
             if (mrfold) {
                 comm_allreduce(c, dparts, ndp);
             } else {
-                HIPCHK(launch_fin_sum(c, nbrick, 0));
+                if (c->p >= 3) HIPCHK(launch_den_local_from_partials(c, c->d_hbpart, nbrick));  // (one per block)
+                else HIPCHK(launch_fin_sum(c, nbrick, 0));
                 comm_allreduce(c, red + 0, 1);  // den step: folded into the update kernel
             }
         } else if (two_stage) {

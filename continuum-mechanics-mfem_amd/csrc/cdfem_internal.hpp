@@ -522,6 +522,7 @@ hipError_t launch_apply_den_dfold(cdfem_ctx *c, const double *z, const double *d
                                   const KrylovState *st, double *part);
 bool e2l_box_ok(const cdfem_ctx *c);
 hipError_t launch_den_from_partials(cdfem_ctx *c, const double *in, int64_t n);
+hipError_t launch_den_local_from_partials(cdfem_ctx *c, const double *in, int64_t n);
 hipError_t launch_e2l_cg_update(cdfem_ctx *c, const double *Ye, const double *d, double *x, double *r, double *z,
                                 const double *dinv);
 

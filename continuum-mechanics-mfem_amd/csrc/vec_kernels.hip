@@ -518,6 +518,16 @@ k_part_reduce(const double *__restrict__ in, int64_t n, double *__restrict__ par
 
 constexpr int kDenStage = 256;
 
+// several ranks: the same first stage, then the rank-local sum into the state's den slot (all-reduced next)
+hipError_t launch_den_local_from_partials(cdfem_ctx *c, const double *in, int64_t n)
+{
+    hipLaunchKernelGGL(k_part_reduce, dim3(kDenStage), dim3(kRedThreads), 0, c->stream, in, n, c->d_part,
+                       (const KrylovState *)c->d_state);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_fin_sum(c, kDenStage, 0);
+}
+
 hipError_t launch_den_from_partials(cdfem_ctx *c, const double *in, int64_t n)
 {
     hipLaunchKernelGGL(k_part_reduce, dim3(kDenStage), dim3(kRedThreads), 0, c->stream, in, n, c->d_part,
