@@ -750,6 +750,24 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     };
     // one rank on the structured patch-buffer Mult: pass 1 forms A_c v_j from the patch buffer itself
     const bool gpb = c->gm_pb != 0 && !ilu && !multi_rank(c) && use_brick(c) && brick_mult_pb_on(c);
+    // gm_poll k (default 4): an event and a host check every k inner steps (and at a cycle's last step)
+    // instead of every step: each event costs the GPU ~5 us before the next Mult (rocprofv3 trace gaps,
+    // profiles/r06/ab_gmres_poll/; C2 step 181.3-182.8 -> 178.1-178.2 us at k = 4).  Every step's last scalar kernel still posts the state head into poll[j & 1]; the host reads the
+    // slot of its last check's step, whose state may already be newer (cycle_done only turns on within a
+    // cycle).  Steps queued past the end of a cycle exit at entry (their Mult does not check and runs once
+    // more at most k - 1 times per converged cycle).
+    const int pk = std::max(1, c->gm_poll);
+    int nposts = 0, last_posted = -1;
+    auto step_end = [&](int j, bool cycle_last) -> bool {  // true: the cycle is done, leave the step loop
+        if (!cycle_last && (j + 1) % pk != 0) return false;
+        post(nposts & 1);
+        const int prev = last_posted;
+        last_posted = j;
+        ++nposts;
+        if (nposts < 2 || prev < 0) return false;
+        HIPCHK(hipEventSynchronize(c->gm_ev[(nposts - 2) & 1]));  // the previous check's event
+        return poll[prev & 1].cycle_done != 0;                      // its step's poll slot (or newer)
+    };
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemsetAsync(x, 0, n * sizeof(double), c->stream));
@@ -779,8 +797,7 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
                 prof_mark(c, CDFEM_K_ORTH, true);
                 HIPCHK(launch_gm_orth(c, w, dinv, V, ldv, part, st, m, &poll[j & 1], &src));
                 prof_mark(c, CDFEM_K_ORTH, false);
-                post(j & 1);
-                if (j > 0 && wait((j - 1) & 1).cycle_done) break;
+                if (step_end(j, j == m - 1)) break;
                 continue;
             }
             op_apply_global(c, Vj, w, true);
@@ -788,9 +805,10 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
             prof_mark(c, CDFEM_K_ORTH, true);
             HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, ldv, part, st, m, &poll[j & 1]));
             prof_mark(c, CDFEM_K_ORTH, false);
-            post(j & 1);
-            if (j > 0 && wait((j - 1) & 1).cycle_done) break;
+            if (step_end(j, j == m - 1)) break;
         }
+        nposts = 0;
+        last_posted = -1;
         prof_mark(c, CDFEM_K_UPDATE, true);
         HIPCHK(launch_gm_update(c, x, V, ldv, st, &poll[0]));
         prof_mark(c, CDFEM_K_UPDATE, false);
@@ -1891,6 +1909,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
             if (value < 0 || value > 8)
                 throw ArgError("sell_order must be 0..8 (0 natural, 1 natural + windows, 2 RCM + windows, 3 auto, 4 RCM, 5 geometric, 6 Morton + windows, 7 Morton, 8 Morton LDS windows / auto)");
             c->sell_mode = value;
+        } else if (k == "gm_poll") {
+            if (value < 1 || value > 64) throw ArgError("gm_poll must be 1..64");
+            c->gm_poll = value;
         } else if (k == "gm_pb") {
             if (value < 0 || value > 1) throw ArgError("gm_pb must be 0 or 1");
             c->gm_pb = value;

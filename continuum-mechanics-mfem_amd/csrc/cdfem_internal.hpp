@@ -181,6 +181,7 @@ struct cdfem_ctx {
     int gm_ept = 0;                     // set_option "gm_ept": GMRES orthogonalisation entries per thread (0: auto, orth_ept)
     int gm_ept_auto = 4;                // the automatic choice for vectors of gm_ept_n entries
     int gm_pb = 1;                      // set_option "gm_pb": GMRES pass 1 reads the structured Mult's patch buffer
+    int gm_poll = 4;                    // set_option "gm_poll": the host polls the GMRES state every k inner steps
     int64_t gm_ept_n = -1;
     int brick_xcd = 1;                  // k_brick_cg brick order: 0 dispatch, 1 XCD-contiguous (default)
     // the brick kernels address r, M^-1, d, x, ess and the patch buffer through buffer resources with

@@ -259,6 +259,9 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *              update and the next apply take MFEM's den and betanom steps as on one rank (no sum or
  *              step kernels between them); taken only when every rank holds as many partials (checked
  *              once, collectively); 0 = per-rank sums, 8-byte all-reduces and step kernels.
+ * "gm_poll": 4 (default) — the GMRES host loop records an event and checks the device state every k
+ *              inner steps (and at every cycle's last step) instead of after every step (1: every step).
+ *              Steps queued past a converged step exit at entry; their Mult runs (at most k - 1 per solve).
  * "brick_stagger": -1 (default, automatic: s = log2 CUs, n = 4), 0 off, or bits 0-3 a shift s and bits
  *              4-8 a count n: the first round of the brick CG apply (k_brick_cg workgroups b < 8 x CUs,
  *              launches of >= 2 rounds) with bit s of b set sleeps n x 2,048 cycles at entry, so half the

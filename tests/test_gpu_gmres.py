@@ -174,3 +174,36 @@ def test_gmres_patch_buffer_pass_bitwise(gpu_ctx, n, p, kinds):
     np.testing.assert_array_equal(x1, x0)
     assert i1["final_norm"] == i0["final_norm"]
     assert np.linalg.norm(x1 - xo) <= 1e-11 * np.linalg.norm(xo)
+
+
+@pytest.mark.parametrize("structured,restart", [(True, 30), (True, 7), (False, 10)])
+def test_gmres_poll_interval_bitwise(gpu_ctx, structured, restart):
+    """gm_poll k (default 4): the host records an event and checks the device state every k inner steps
+    instead of after every step.  Steps it queued past the converged step exit at their first check (their
+    Mult runs and writes scratch only), so the solution, the iteration count and the final residual are
+    bitwise those of checking every step, for converging solves (the stop inside a poll interval) and
+    for fixed step counts across restarts; on the structured patch-buffer path and the generic one."""
+    om, Ac, Bo, B = _system(gpu_ctx, 3, 6, 2, 0.0 if structured else 0.1, structured=structured, seed=19)
+    xo, io = O.gmres(Ac, Bo, dinv=1.0 / Ac.diag(), restart=restart, rtol=1e-10, atol=1e-12, max_it=500)
+    out = {}
+    try:
+        for k in (1, 4, 7):
+            gpu_ctx.set_option("gm_poll", k)
+            out[k] = (gpu_ctx.solve(B, method="gmres", pc="jacobi", restart=restart, rel_tol=1e-10, abs_tol=1e-12,
+                                    max_iter=500),
+                      gpu_ctx.solve(B, method="gmres", pc="jacobi", restart=restart, rel_tol=0.0, abs_tol=0.0,
+                                    max_iter=2 * restart + 3))
+    finally:
+        gpu_ctx.set_option("gm_poll", 4)
+    (x1, i1), (f1, j1) = out[1]
+    assert i1["converged"] and abs(i1["iterations"] - io["iterations"]) <= 1
+    assert np.linalg.norm(x1 - xo) <= 1e-8 * np.linalg.norm(xo)
+    assert j1["iterations"] == 2 * restart + 3
+    for k in (4, 7):
+        (xk, ik), (fk, jk) = out[k]
+        np.testing.assert_array_equal(xk, x1)
+        assert ik["iterations"] == i1["iterations"] and ik["converged"] and ik["final_norm"] == i1["final_norm"]
+        np.testing.assert_array_equal(fk, f1)
+        assert jk["iterations"] == j1["iterations"]
+    with pytest.raises(cdfem.CdfemError):
+        gpu_ctx.set_option("gm_poll", 0)
