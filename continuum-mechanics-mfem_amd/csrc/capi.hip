@@ -724,7 +724,9 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     }
     if (!c->d_gmst) {
         HIPCHK(hipMalloc(&c->d_gmst, sizeof(GmresState)));
-        HIPCHK(hipHostMalloc(&c->h_gmpoll, 2 * sizeof(GmresState), hipHostMallocDefault));
+        // poll slots: 0 for the cycle start / end, 1 + j for inner step j (each step its own slot, so a
+        // host check reads exactly the state of the step it waited for: ranks decide alike)
+        HIPCHK(hipHostMalloc(&c->h_gmpoll, (kGmMaxRestart + 1) * sizeof(GmresState), hipHostMallocDefault));
         for (auto &e : c->gm_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     const double *dinv = nullptr;
@@ -752,10 +754,12 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
     const bool gpb = c->gm_pb != 0 && !ilu && !multi_rank(c) && use_brick(c) && brick_mult_pb_on(c);
     // gm_poll k (default 4): an event and a host check every k inner steps (and at a cycle's last step)
     // instead of every step: each event costs the GPU ~5 us before the next Mult (rocprofv3 trace gaps,
-    // profiles/r06/ab_gmres_poll/; C2 step 181.3-182.8 -> 178.1-178.2 us at k = 4).  Every step's last scalar kernel still posts the state head into poll[j & 1]; the host reads the
-    // slot of its last check's step, whose state may already be newer (cycle_done only turns on within a
-    // cycle).  Steps queued past the end of a cycle exit at entry (their Mult does not check and runs once
-    // more at most k - 1 times per converged cycle).
+    // profiles/r06/ab_gmres_poll/; C2 step 181.3-182.8 -> 178.1-178.2 us at k = 4).  Every step's last
+    // scalar kernel posts the state head into its own slot poll[1 + j]; a check waits for the previous
+    // check's event and reads exactly that step's slot, never a later step's (on several ranks every rank
+    // must leave the loop at the same step: their collectives pair up).  Steps queued past the end of a
+    // cycle exit at entry (their Mult does not check, and runs at most k - 1 times per converged cycle).
+
     const int pk = std::max(1, c->gm_poll);
     int nposts = 0, last_posted = -1;
     auto step_end = [&](int j, bool cycle_last) -> bool {  // true: the cycle is done, leave the step loop
@@ -766,7 +770,7 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
         ++nposts;
         if (nposts < 2 || prev < 0) return false;
         HIPCHK(hipEventSynchronize(c->gm_ev[(nposts - 2) & 1]));  // the previous check's event
-        return poll[prev & 1].cycle_done != 0;                      // its step's poll slot (or newer)
+        return poll[1 + prev].cycle_done != 0;                      // exactly its step's state
     };
     HIPCHK(hipStreamSynchronize(c->stream));
     const auto t0 = std::chrono::steady_clock::now();
@@ -795,7 +799,7 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
                 prof_mark(c, CDFEM_K_APPLY, false);
                 const GmPatchSrc src = gm_patch_src(c, Vj);
                 prof_mark(c, CDFEM_K_ORTH, true);
-                HIPCHK(launch_gm_orth(c, w, dinv, V, ldv, part, st, m, &poll[j & 1], &src));
+                HIPCHK(launch_gm_orth(c, w, dinv, V, ldv, part, st, m, &poll[1 + j], &src));
                 prof_mark(c, CDFEM_K_ORTH, false);
                 if (step_end(j, j == m - 1)) break;
                 continue;
@@ -803,7 +807,7 @@ void solve_gmres(cdfem_ctx *c, const cdfem_solver_params &p, const double *dB, d
             op_apply_global(c, Vj, w, true);
             if (ilu) HIPCHK(ilu_apply(c));  // w <- (LU)^{-1} A v_j, in ilu.z
             prof_mark(c, CDFEM_K_ORTH, true);
-            HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, ldv, part, st, m, &poll[j & 1]));
+            HIPCHK(launch_gm_orth(c, ilu ? c->ilu.z : w, dinv, V, ldv, part, st, m, &poll[1 + j]));
             prof_mark(c, CDFEM_K_ORTH, false);
             if (step_end(j, j == m - 1)) break;
         }
