@@ -722,12 +722,16 @@ def main():
                                     max_iter=args.gmres_iters, restart=30)
         gstep()
         ctx.synchronize()
-        ctx.set_option("profile_mask", -1)
-        ctx.profile(True)
         t0 = time.perf_counter()
         ginfo = gstep()
         ctx.synchronize()
         gdt = time.perf_counter() - t0
+        # breakdown from a profiled pass of the same solve, after the timed one: the events bracketing the
+        # apply and the CGS passes cost the GPU ~10 us each per step (profiles/r06/ab_gmres_events)
+        ctx.set_option("profile_mask", (1 << cdfem.K_APPLY) | (1 << cdfem.K_ORTH))
+        ctx.profile(True)
+        gstep()
+        ctx.synchronize()
         o_ms, o_cnt = ctx.profile_read(cdfem.K_ORTH)
         a_ms, a_cnt = ctx.profile_read(cdfem.K_APPLY)
         ctx.profile(False)
