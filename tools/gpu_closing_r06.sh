@@ -3,7 +3,11 @@
 # (one GPU), each from the committed tree.
 set -u
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/${TAG:-closing}; mkdir -p $O
-timeout -k 10 700 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread \
+# heartbeat: the suite's longest tests (the full-size oracle checks) print nothing for a minute or two
+( while true; do date +%T >> $O/heartbeat; sleep 50; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+timeout -k 10 700 python -u -m pytest tests -m gpu -v --maxfail=10 --timeout 300 --timeout-method thread \
     -p no:cacheprovider --durations=15 > $O/suite.log 2>&1 || { echo "suite rc=$?"; grep -E "^(FAILED|ERROR)|passed|failed" $O/suite.log | head -20; exit 1; }
 tail -2 $O/suite.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; tail $O/smoke.log; exit 1; }
