@@ -569,6 +569,14 @@ def main():
     nq = (p + 2) ** 3
     ncomp = (6 if args.kinds & 1 else 0) + (3 if args.kinds & 2 else 0) + (1 if args.kinds & 4 else 0)
     affine = ctx.kernel_bytes(cdfem.K_APPLY) < 8.0 * ncomp * nq * mesh.ne
+    # pa_uniform (default): on this uniformly refined box every element has the same factors, and the
+    # brick CG applies the one 27 x 27 element matrix on the matrix cores; the byte count (no factor
+    # stream) tells whether the context took that form
+    uni_opt = int(args.set.get("pa_uniform", 1))
+    uni_bytes = ctx.kernel_bytes(cdfem.K_APPLY)
+    ctx.set_option("pa_uniform", 0)
+    uniform = uni_opt != 0 and ctx.kernel_bytes(cdfem.K_APPLY) != uni_bytes
+    ctx.set_option("pa_uniform", uni_opt)
 
     # synthetic RHS resident in HBM: B = FormLinearSystem(u_bc = 0, b ~ U[-1,1))
     rng = np.random.default_rng(20261015 + rank)
@@ -705,6 +713,21 @@ def main():
                         "e2l": round(e_ms / max(e_cnt, 1) * 1e3, 2),
                         "cg_update": round(u_ms / max(u_cnt, 1) * 1e3, 2),
                         "cg_direction": round(d_ms / max(d_cnt, 1) * 1e3, 2)}})
+
+    # informational: the same steps with the Kronecker form of the per-element factors (pa_uniform 0,
+    # the form any affine box takes), when the uniform element matrix ran above
+    kron = None
+    if world == 1 and uniform:
+        ctx.set_option("pa_uniform", 0)
+        step()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        kits = sum(step()["iterations"] for _ in range(args.steps))
+        ctx.synchronize()
+        kdt = time.perf_counter() - t0
+        ctx.set_option("pa_uniform", uni_opt)
+        kron = {"value": mesh.nl * kits / kdt, "unit": "DoF-iter/s", "ms_per_step": kdt / args.steps * 1e3,
+                "qdata": "the Kronecker form of the per-element factors on the VALU (pa_uniform 0)"}
 
     # host-boundary (PCIe-inclusive) rate: one solve with B and X in host memory (not `value`)
     host_rate = None
@@ -847,7 +870,12 @@ def main():
                        "path": {"k_brick_cg": "brick", "k_hobrick_cg": "ho_brick"}.get(
                            ctx.kernel_name(cdfem.K_APPLY), args.path),
                        **({"options": args.set} if args.set else {}),
-                       "qdata": ("affine: 10 factors per element applied in their Kronecker form (pa_affine 2, 1D rule "
+                       "qdata": ("uniform box: every element's factors equal, so the apply runs the one 27 x 27 "
+                                 "element matrix as a GEMM on the matrix cores (pa_uniform 1, 56 "
+                                 "v_mfma_f64_16x16x4_f64 per 64 elements); the operator equals the Kronecker and "
+                                 "per-point forms to rounding (tests/test_gpu_uniform.py); the Kronecker form's "
+                                 "rate is the 'kronecker_form' line" if uniform else
+                                 "affine: 10 factors per element applied in their Kronecker form (pa_affine 2, 1D rule "
                                  "matrices per axis); the operator equals the per-point form to rounding (1e-13 "
                                  "relative, tests/test_gpu_affine.py)" if affine
                                  else "per-point stream (MFEM's PA layout)"),
@@ -858,6 +886,8 @@ def main():
                        **({"comm_host_timing": comm_timing} if comm_timing else {})},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if kron is not None:
+            out["kronecker_form"] = kron
         if gm is not None:
             out["gmres"] = gm
         if spd is not None:

@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
+#include <vector>
+#include <algorithm>
+#include <cmath>
 
 #include "cdfem_internal.hpp"
 #include "brick_core.hpp"
@@ -558,8 +561,18 @@ hipError_t launch_brick_mult(cdfem_ctx *c, const double *x, double *y, bool cons
 // 4), B = the 16 elements' input rows from the LDS patch (column = element).  Lane (ix, element) then holds
 // that element's four x-applied values for column ix and stores them to LDS, where each element's thread
 // reads them back for the combinations and the y / z stages (kron_core otherwise).  A/B in DESIGN.md 4.1.
+// MX 2 (pa_uniform, a uniformly refined box: every element has the same factors, so the same 27 x 27
+// matrix A_e, formed once by setup_uniform_elem): the brick's 64 element applies as one GEMM on the
+// matrix cores, Y (27 x 64) = A_e (27 x 27) X (27 x 64), 2 x 4 tiles of 16 x 16 over 7 k-steps of 4 = 56
+// v_mfma_f64_16x16x4_f64 per brick (729 useful MACs per element against ~1,560 f64 FMAs of the Kronecker
+// form on the VALU).  qd is then A_e in operand order: [mt][ks][lane] = A_e[16 mt + (lane & 15)][4 ks +
+// (lane >> 4)] (0 past 27), 14 doubles per lane held for the whole kernel.  B (lane: input node 4 ks +
+// (lane >> 4) of element 16 nt + (lane & 15)) comes straight from the LDS patch; accumulator i of a lane is
+// row 16 mt + 4 i + (lane >> 4) of element 16 nt + (lane & 15).  The den terms are taken in
+// the accumulator layout, then the accumulators go through LDS (over the two patches) to the
+// thread-per-element layout of brick_e2l.
 template <int D1, int Q1, unsigned K, int AF, int W = 1, bool XF = false, bool BF = false, bool FULL = false,
-          bool MX = false>
+          int MX = 0>
 __global__ void __launch_bounds__(64, W)
 k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
            const double *__restrict__ d_old, double *__restrict__ d_new, double *__restrict__ q,
@@ -578,8 +591,16 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     // distinct bank pairs (2-way, the floor for even origins) instead of up to 4-way at SY = 9, SZ = 81
     constexpr bool PAD = CDFEM_BRICK_LDS == 2 && P == 2;
     constexpr int SY = PAD ? 12 : S, SZ = PAD ? 112 : S2, PS = (S - 1) * SZ + (S - 1) * SY + S;
-    __shared__ double s_in[PS];
-    __shared__ double s_out[PS];
+    constexpr bool UM = MX == 2;
+    constexpr int NDE = D1 * D1 * D1;
+    // UM: the accumulators' trip to the thread-per-element layout reuses both patches ([node][element],
+    // 13.8 KB against the patches' 11.7).  Measured (profiles/r06/ab_c2_uniform_mfma/): two trips of half
+    // the brick each (11.7 KB) at 2 waves per SIMD 1.5 % slower per CG iteration; at 3 waves (168
+    // registers, 31 spilled) 20 % slower
+    constexpr int UMB = UM ? (2 * PS > NDE * 64 ? 2 * PS : NDE * 64) : PS;
+    __shared__ double s_in[UMB];
+    __shared__ double s_out_own[UM ? 1 : PS];
+    double *const s_out = UM ? s_in + PS : s_out_own;
     // EP (the Kronecker form, AF 2): the essential rows' patch entries carry (A_c d)_i = d_i, the
     // writer brick's d (0 where the den ownership bit is off: non-writers, and the slab plane the rank
     // below owns), so the update's sum of a row's entries is its q with no essential flag or d read.
@@ -588,8 +609,8 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     constexpr bool EP = AF == 2;
     constexpr bool EPL = EP && CDFEM_BRICK_LDS == 0;
     __shared__ double s_d[EPL ? S3 : 1];
-    static_assert(!MX || (AF == 2 && D1 == 3), "the MFMA x stage is built for the p = 2 Kronecker form");
-    __shared__ double s_x[MX ? 3 * 3 * 4 * 64 : 1];  // MX: [jy][ix][q][element] of one input plane
+    static_assert(!MX || (AF == 2 && D1 == 3), "the MFMA stages are built for the p = 2 Kronecker form");
+    __shared__ double s_x[MX == 1 ? 3 * 3 * 4 * 64 : 1];  // MX 1: [jy][ix][q][element] of one input plane
     if (st->done) return;
     brick_stagger(g);
     double beta = st->beta;
@@ -682,7 +703,7 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         den += (e && ((dbits >> k) & 1u)) ? dn * dn : 0.0;
         const unsigned li = PAD ? liv[PAD ? k : 0] : i;
         s_in[li] = e ? 0.0 : dn;
-        s_out[li] = 0.0;
+        if constexpr (!UM) s_out[li] = 0.0;  // (UM: after the accumulators' trip through LDS)
         if constexpr (EP) {  // (unconditional: a predicated LDS store compiles to a branch per position)
             ebits |= (uint32_t)e << k;
             if constexpr (EPL) s_d[i] = ((dbits >> k) & 1u) ? dn : 0.0;
@@ -720,7 +741,74 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
     const int o0 = P * ez * SZ + P * ey * SY + P * ex;
     auto xl = [&](int dz, int dy, int dx) { return s_in[o0 + dz * SZ + dy * SY + dx]; };
     double Y[D1][D1][D1];
-    if constexpr (MX) {
+    if constexpr (UM) {
+        const int n16 = t & 15, kg = t >> 4;
+        double av[2][7];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int ks = 0; ks < 7; ++ks) av[mt][ks] = qd[(mt * 7 + ks) * 64 + t];
+        // element 16 nt + n16 of the brick: (ex, ey, ez) = (n16 & 3, n16 >> 2, nt)
+        const int ob0 = P * (n16 >> 2) * SY + P * (n16 & 3);
+        auto node_off = [&](int j) { return (j / 9) * SZ + ((j / 3) % 3) * SY + j % 3; };
+        v4d_t acc[2][4];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = v4d_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < 7; ++ks) {
+            const int j = 4 * ks + kg;  // this lane's input node (27 = the k padding: B = 0)
+            const int jo = node_off(j < NDE ? j : 0);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const double bv = j < NDE ? s_in[P * nt * SZ + ob0 + jo] : 0.0;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mt][ks], bv, acc[mt][nt], 0, 0, 0);
+            }
+        }
+        // den: sum over (node m, element n) of X[m][n] Y[m][n], in the accumulator layout (lane: acc[i]
+        // = row 16 mt + 4 i + kg of element 16 nt + n16; the layout the MX 1 stage relies on too)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = 16 * mt + 4 * i + kg;
+                const int mo = node_off(m < NDE ? m : 0);
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt)
+                    den += m < NDE ? s_in[P * nt * SZ + ob0 + mo] * acc[mt][nt][i] : 0.0;
+            }
+        __syncthreads();
+        double *const yb = s_in;  // [node][element] over both patches
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = 16 * mt + 4 * i + kg;
+                if (mt == 0 || m < NDE) {
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) yb[m * 64 + 16 * nt + n16] = acc[mt][nt][i];
+                }
+            }
+        __syncthreads();
+#pragma unroll
+        for (int dz = 0; dz < D1; ++dz)
+#pragma unroll
+            for (int dy = 0; dy < D1; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < D1; ++dx) Y[dz][dy][dx] = yb[((dz * D1 + dy) * D1 + dx) * 64 + t];
+        __syncthreads();
+        // the output patch, zeroed now that the accumulators have left it
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const unsigned i = t + 64 * k;
+            if (k == NI - 1 && i >= S3) break;
+            s_out[PAD ? liv[PAD ? k : 0] : i] = 0.0;
+        }
+        __syncthreads();
+    } else if constexpr (MX == 1) {
         double gk[NC];
         kron_load_g<K>(q0, t, gk);
         // A operand: lane (row = l & 15 = 4 q + ix, k = l >> 4 = jx) -> F_q[ix][jx] (0 in the padding)
@@ -781,13 +869,15 @@ k_brick_cg(const double *__restrict__ r, const double *__restrict__ dinv,
         elem_apply3d_af<D1, Q1, K, AF>(xl, q0, t, T, Y);
     }
 
-    // element-wise den contribution d0_e . (A_e d0_e) and deterministic in-LDS E->L
+    // element-wise den contribution d0_e . (A_e d0_e) (UM: taken above) and deterministic in-LDS E->L
+    if constexpr (!UM) {
 #pragma unroll
-    for (int dz = 0; dz < D1; ++dz)
+        for (int dz = 0; dz < D1; ++dz)
 #pragma unroll
-        for (int dy = 0; dy < D1; ++dy)
+            for (int dy = 0; dy < D1; ++dy)
 #pragma unroll
-            for (int dx = 0; dx < D1; ++dx) den += s_in[o0 + dz * SZ + dy * SY + dx] * Y[dz][dy][dx];
+                for (int dx = 0; dx < D1; ++dx) den += s_in[o0 + dz * SZ + dy * SY + dx] * Y[dz][dy][dx];
+    }
     brick_e2l<D1, S, SY, SZ>(s_out, o0, Y);
 
     // the brick's whole patch output (interior rows complete, face rows partial) -> the patch buffer
@@ -1237,7 +1327,7 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
     g.bzs = run.bzs;
     const dim3 grid((unsigned)(c->nbx * c->nby * run.nlay)), block(64);
     const bool whole = run.nlay == c->nbz && run.s == c->stream;
-    const double *qd = c->d_qaff ? c->d_qaff : c->d_qd;
+    const double *qd = c->d_qaff ? c->d_qaff : c->d_qd;  // (pa_uniform: the element matrix, below)
     const double *upart = c->d_part + c->nblk;  // the den-fold update's partials
     double *const dpart = c->den_out ? c->den_out : c->d_part;  // the apply's den partials
     const int grp = c->den_grp, nbrick = c->nblk;               // (grouped: sums into d_gsum)
@@ -1250,14 +1340,21 @@ static hipError_t brick_cg2_launch(cdfem_ctx *c, const double *r, const double *
         hipLaunchKernelGGL((k_brick_cg<D1, Q1, K, AFF_, W_, XF_, BF_, FU_, MX_>), grid, block, 0, run.s, r, dinv, \
                            d_old, d_new, q, c->d_face, qd, c->d_ess, T, g, c->zlo_shared, dpart, c->d_state, x, \
                            upart, run.nupart, run.kk, c->d_gsum, c->d_gcnt, grp, nbrick)
-    // (brick_mfma: the MFMA x stage, built for the Kronecker form of the full operator at p = 2)
+    // (brick_mfma: the MFMA x stage, built for the Kronecker form of the full operator at p = 2;
+    // pa_uniform: the common element matrix on the matrix cores, p = 2, instantiated for the full
+    // operator and the symmetric kK + sM of the bench (kinds 7, 5); other kinds keep the Kronecker form)
     constexpr bool kMX = K == 7 && D1 == 3;
+    constexpr bool kUM = (K == 7 || K == 5) && D1 == 3;
     const bool mx = kMX && c->brick_mfma != 0;
+    const bool um = kUM && uniform_elem(c);
+    if (um) qd = c->d_uelem;
 #define CDFEM_BCG5(AFF_, W_, XF_, BF_, FU_)                                                                 \
-    if constexpr (kMX && AFF_ == 2) {                                                                        \
-        if (mx) { CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, kMX); } else { CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, false); } \
+    if constexpr (kUM && AFF_ == 2) {                                                                        \
+        if (um) { CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, 2); }                                                  \
+        else if (mx) { CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, (kMX ? 1 : 0)); }                                 \
+        else { CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, 0); }                                                     \
     } else {                                                                                                 \
-        CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, false);                                                          \
+        CDFEM_BCG6(AFF_, W_, XF_, BF_, FU_, 0);                                                              \
     }
 #define CDFEM_BCG4(AFF_, W_, XF_, BF_)                                                                      \
     if (full) { CDFEM_BCG5(AFF_, W_, XF_, BF_, true); } else { CDFEM_BCG5(AFF_, W_, XF_, BF_, false); }
@@ -1572,6 +1669,104 @@ hipError_t launch_pack_qplanes(cdfem_ctx *c, const double *q, hipStream_t s)
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
+}
+
+// ---- pa_uniform: the common element matrix of a uniformly refined box (k_brick_cg<..., MX 2>) ------
+// Every element slot's factors against slot 0's (brick 0, lane 0: element (0, 0, 0)); any component
+// further than tol flags the box as not uniform (plain vector stores of the same value).
+__global__ void __launch_bounds__(256)
+k_uniform_check(const double *__restrict__ gaff, const int32_t *__restrict__ perm, int nslots, int nc, int ne,
+                double tol, int *__restrict__ bad)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nslots) return;
+    const int e = perm[s];
+    if (e < 0 || e >= ne) return;
+    const size_t b = (size_t)(s / kLanes), lane = (size_t)(s % kLanes);
+    bool diff = false;
+    for (int k = 0; k < nc; ++k) diff |= fabs(gaff[(b * nc + k) * kLanes + lane] - gaff[(size_t)k * kLanes]) > tol;
+    if (diff) *bad = 1;
+}
+
+// column j of the element matrix = the Kronecker core (what k_brick_cg<..., AF 2> applies) on the unit
+// vector e_j with element 0's factors: thread j writes A[i][j], row-major N x N
+template <int D1, int Q1, unsigned K>
+__global__ void __launch_bounds__(64)
+k_uniform_elem(const double *__restrict__ gaff, const Tab<D1, Q1> T, double *__restrict__ A)
+{
+    constexpr int N = D1 * D1 * D1;
+    const int j = threadIdx.x;
+    if (j >= N) return;
+    double g[QLayout<K, 3>::nc];
+    kron_load_g<K>(gaff, 0, g);
+    auto xl = [&](int z, int y, int x) { return (z * D1 + y) * D1 + x == j ? 1.0 : 0.0; };
+    double Y[D1][D1][D1];
+    kron_core<D1, Q1, K>(xl, g, T, Y);
+    for (int i = 0; i < N; ++i) A[i * N + j] = Y[i / (D1 * D1)][(i / D1) % D1][i % D1];
+}
+
+hipError_t setup_uniform_elem(cdfem_ctx *c)
+{
+    if (c->d_uelem) {
+        const hipError_t e = hipFree(c->d_uelem);
+        c->d_uelem = nullptr;
+        if (e != hipSuccess) return e;
+    }
+    if (!c->pa_uniform || !c->structured || c->qlay != 0 || c->dim != 3 || pa_af(c) != 2 || c->p != 2 ||
+        c->rule_op.q1 != 4 || c->ncomp < 1 || (c->kinds != 7 && c->kinds != 5))
+        return hipSuccess;
+    const int nc = c->ncomp;
+    std::vector<double> g0(nc);
+    hipError_t e = hipMemcpy2D(g0.data(), sizeof(double), c->d_qaff, kLanes * sizeof(double), sizeof(double), nc,
+                               hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    double gmax = 0.0;
+    for (double v : g0) gmax = std::max(gmax, std::fabs(v));
+    // one scratch allocation: the flag, then the N x N matrix
+    constexpr int N = 27;
+    void *scratch = nullptr;
+    if ((e = hipMalloc(&scratch, sizeof(double) * (N * N + 1))) != hipSuccess) return e;
+    int *bad = static_cast<int *>(scratch);
+    double *A = static_cast<double *>(scratch) + 1;
+    int hbad = 0;
+    const int nslots = c->nblk * kLanes;
+    e = hipMemsetAsync(bad, 0, sizeof(int), c->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_uniform_check, dim3((nslots + 255) / 256), dim3(256), 0, c->stream, c->d_qaff, c->d_perm,
+                           nslots, nc, (int)c->ne, 1e-14 * gmax, bad);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    std::vector<double> h(N * N), op(2 * 7 * 64, 0.0);
+    if (e == hipSuccess && !hbad) {
+        const Tab<3, 4> T = make_tab<3, 4>(c->rule_op);
+        if (c->kinds == 7) hipLaunchKernelGGL((k_uniform_elem<3, 4, 7>), dim3(1), dim3(64), 0, c->stream, c->d_qaff, T, A);
+        else hipLaunchKernelGGL((k_uniform_elem<3, 4, 5>), dim3(1), dim3(64), 0, c->stream, c->d_qaff, T, A);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(h.data(), A, sizeof(double) * N * N, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    const hipError_t ef = hipFree(scratch);
+    if (e != hipSuccess) return e;
+    if (ef != hipSuccess) return ef;
+    if (hbad) return hipSuccess;  // not uniform: the Kronecker form
+    // the A operands of v_mfma_f64_16x16x4_f64 in lane order: [mt][ks][lane] = A[16 mt + (lane & 15)][4 ks + (lane >> 4)]
+    for (int mt = 0; mt < 2; ++mt)
+        for (int ks = 0; ks < 7; ++ks)
+            for (int l = 0; l < 64; ++l) {
+                const int i = 16 * mt + (l & 15), j = 4 * ks + (l >> 4);
+                op[(mt * 7 + ks) * 64 + l] = (i < N && j < N) ? h[i * N + j] : 0.0;
+            }
+    void *d = nullptr;
+    if ((e = hipMalloc(&d, sizeof(double) * op.size())) != hipSuccess) return e;
+    e = hipMemcpy(d, op.data(), sizeof(double) * op.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return e;
+    }
+    c->d_uelem = static_cast<double *>(d);
+    return hipSuccess;
 }
 
 }  // namespace cdfem

@@ -137,6 +137,7 @@ void free_mesh(cdfem_ctx *c)
     dfree(c->d_cpos); dfree(c->d_vals); dfree(c->d_vals_c); dfree(c->d_Ee);
     dfree(c->d_sptr); dfree(c->d_srows); dfree(c->d_scols); dfree(c->d_smap); dfree(c->d_sdel); dfree(c->d_svals);
     dfree(c->d_swide);
+    dfree(c->d_uelem);
     c->d_sdel = nullptr;
     c->d_swide = nullptr;
     c->sell_nnz_wide = 0;
@@ -1408,6 +1409,7 @@ static int pa_setup_form(cdfem_ctx *c, const cdfem_form_coeffs *f)
         HIPCHK(launch_setup_qdata(c, dk, dkm, f->kappa, f->alpha, f->conv, dc, dm, f->mass));
         HIPCHK(hipStreamSynchronize(c->stream));
         dfree(dk); dfree(dkm); dfree(dc); dfree(dm);
+        HIPCHK(setup_uniform_elem(c));  // pa_uniform: the common element matrix of a uniform box
         c->pa_ready = true;
         c->fa_ready = false;
         c->dinv_ready = false;
@@ -1872,6 +1874,9 @@ int cdfem_set_option(cdfem_ctx *c, const char *key, int value)
         } else if (k == "brick_stagger") {
             if (value < -1 || value > 511) throw ArgError("brick_stagger must be -1 (automatic), 0 (off) or 1..511");
             c->brick_stagger = value;
+        } else if (k == "pa_uniform") {  // the matrix is formed by cdfem_pa_setup; 0 leaves it unused
+            if (value != 0 && value != 1) throw ArgError("pa_uniform must be 0 or 1");
+            c->pa_uniform = value;
         } else if (k == "brick_mfma") {
             if (value != 0 && value != 1) throw ArgError("brick_mfma must be 0 or 1");
             c->brick_mfma = value;
@@ -2027,6 +2032,12 @@ int cdfem_kernel_flops(cdfem_ctx *c, int k, double *flops)
         // Fields: value, plus the three reference derivatives when diffusion or convection is on.
         const int D = c->d1, Q = c->rule_op.q1;
         const bool kD = c->kinds & CDFEM_DIFFUSION, kC = c->kinds & CDFEM_CONVECTION, kM = c->kinds & CDFEM_MASS;
+        if (c->qlay == 0 && uniform_elem(c) && use_brick(c)) {
+            // the common element matrix (k_brick_cg<..., MX 2>): nd^2 MACs per element (the MFMA tiles'
+            // zero padding, 56 x 1024 MACs per 64 elements against 64 x 729, is not counted)
+            *flops = 2.0 * (double)c->nd * c->nd * (double)c->ne;
+            return CDFEM_OK;
+        }
         if ((c->qlay == 0 && pa_af(c) == 2) || (c->qlay == 1 && tile_kron(c))) {
             // Kronecker form (pa_core.hpp elem_apply3d_kron; the tile kernel k_apply3d_ktile runs the
             // same stages across threads), per input z plane: a length-n linear combination counts
@@ -2105,8 +2116,9 @@ int cdfem_kernel_bytes(cdfem_ctx *c, int k, double *bytes)
             case CDFEM_K_APPLY:   // qdata (or per-element affine factors) + gathered r, M^-1, d + ess
                                   // flags + d (each dof by its one writer brick) + patch outputs
                                   // (+ x read and written by its writer brick under the x-fold)
-                *bytes = 8.0 * c->ncomp * (c->d_qaff ? 1.0 : nq) * ne + 24.0 * nl + 1.0 * nl + 8.0 * nl + patches +
-                         (xf ? 16.0 * nl : 0.0);
+                // (pa_uniform: one element matrix, 14 x 64 operand doubles, instead of the factor stream)
+                *bytes = (uniform_elem(c) ? 8.0 * 14 * 64 : 8.0 * c->ncomp * (c->d_qaff ? 1.0 : nq) * ne) + 24.0 * nl +
+                         1.0 * nl + 8.0 * nl + patches + (xf ? 16.0 * nl : 0.0);
                 return CDFEM_OK;
             case CDFEM_K_E2L:     // the Mult's row sums: the patch buffer + ess flags + y (brick_mult_pb,
                                   // Kronecker form), or face partials + x, ess, y of the face dofs

@@ -173,6 +173,11 @@ struct cdfem_ctx {
     int ho_brick_mfma = 0;              // set_option "ho_brick_mfma": its x stage on v_mfma_f64_16x16x4_f64 (kinds 7)
     int brick_stagger = -1;             // set_option "brick_stagger": BrickGeom::stag (-1 automatic, 0 off)
     int brick_mfma = 0;                 // set_option "brick_mfma": k_brick_cg's x stage on the matrix cores (p = 2, kinds 7)
+    int pa_uniform = 1;                 // set_option "pa_uniform": when every element's factors equal the first
+                                        // element's (a uniformly refined box, what MFEM's MakeCartesian3D
+                                        // gives), the p = 2 brick CG applies that element's 27 x 27 matrix on
+                                        // the matrix cores (k_brick_cg<..., MX 2>); 0 keeps the Kronecker form
+    double *d_uelem = nullptr;          // pa_uniform: the common element matrix in MFMA A-operand order
     int64_t Lx = 0, Ly = 0, Lz = 0;     // dof lattice per axis
     double *d_face = nullptr;           // [nblk][F] brick-face partial sums
     double *d_ones = nullptr;           // all-ones vector (unpreconditioned brick CG)
@@ -349,6 +354,9 @@ inline bool tile_kron(const cdfem_ctx *c) { return c->d_qaff != nullptr && c->ho
 // the element core of the 3D p <= 2 applies (pa_core.hpp elem_apply3d_af): 0 per-point stream,
 // 1 point data from the affine factors, 2 Kronecker form of the factors
 inline int pa_af(const cdfem_ctx *c) { return c->d_qaff == nullptr ? 0 : (c->pa_affine == 2 ? 2 : 1); }
+// the brick CG applies the common element matrix of a uniform box (pa_uniform: formed at the PA setup;
+// set_option "pa_uniform" 0 switches back to the Kronecker form without a new setup)
+inline bool uniform_elem(const cdfem_ctx *c) { return c->d_uelem != nullptr && c->pa_uniform != 0 && pa_af(c) == 2; }
 
 // ---- kernel launchers (pa_kernels.hip) -------------------------------------------------------
 hipError_t launch_setup_qdata(cdfem_ctx *c, const double *d_kappa_q, const double *d_kmat_q, double kappa, double alpha,
@@ -412,6 +420,10 @@ hipError_t launch_zero(cdfem_ctx *c, double *y);
 hipError_t launch_den_fin(cdfem_ctx *c, int nparts);
 hipError_t launch_update_fin(cdfem_ctx *c, int nparts, int64_t off = 0);
 // brick CG v2 (brick_kernels.hip): d_new = M^{-1} r + beta d_old, q/face partials, den partials
+// pa_uniform: after the PA setup of a structured p = 2 box in the Kronecker form (kinds 7 or 5), checks
+// that every element's factors equal the first element's (within 1e-14 of the largest) and, if so, forms
+// that element's 27 x 27 matrix (column j = the Kronecker core on e_j) in d_uelem (freed otherwise)
+hipError_t setup_uniform_elem(cdfem_ctx *c);
 hipError_t launch_brick_cg2(cdfem_ctx *c, const double *r, const double *dinv, const double *d_old,
                             double *d_new, double *q, double *x = nullptr, int bfkk = -1);
 int cg_den_fold_grid(const cdfem_ctx *c);

@@ -267,6 +267,13 @@ int cdfem_fp64_bench(cdfem_ctx *ctx, int mode, int reps, double *tflops);
  *              launches of >= 2 rounds) with bit s of b set sleeps n x 2,048 cycles at entry, so half the
  *              round gathers its patches while the other half computes (C2: 39.0 -> 37.4 us per apply,
  *              DESIGN.md 4.1).
+ * "pa_uniform": 1 (default) — under pa_affine 2 on a structured p = 2 box (kinds 7 or 5), cdfem_pa_setup
+ *              checks whether every element's factors equal the first element's (each within 1e-14 of the
+ *              largest factor: a uniformly refined box, what MFEM's MakeCartesian3D gives) and, if so,
+ *              forms that element's 27 x 27 matrix once (column j = the Kronecker apply of e_j); the brick
+ *              CG apply then runs it as a GEMM on the matrix cores (56 v_mfma_f64_16x16x4_f64 per 64
+ *              elements; the same operator to rounding).  0 = the Kronecker form (takes effect without a
+ *              new setup; 1 needs one).  The GMRES Mult and the other applies keep the Kronecker form.
  * "brick_mfma": 0 (default) or 1 — the p = 2 brick CG apply's x stage (kinds 7, Kronecker form) on
  *              v_mfma_f64_16x16x4_f64: 16 elements per GEMM, outputs staged through LDS to the element
  *              threads.  Parity-green, measured slower.

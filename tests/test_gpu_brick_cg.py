@@ -127,6 +127,7 @@ def test_brick_mfma_x_stage_parity(gpu_ctx, shape, pert):
     _, B = gpu_ctx.form_linear_system(u, b)
     out = {}
     try:
+        gpu_ctx.set_option("pa_uniform", 0)  # (a uniform box: the x stage belongs to the Kronecker form)
         for mx in (1, 0):
             gpu_ctx.set_option("brick_mfma", mx)
             out[mx] = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40, check_every=7)
@@ -134,6 +135,7 @@ def test_brick_mfma_x_stage_parity(gpu_ctx, shape, pert):
         again = gpu_ctx.solve(B, method="cg", pc="jacobi", rel_tol=0.0, abs_tol=0.0, max_iter=40)
     finally:
         gpu_ctx.set_option("brick_mfma", 0)
+        gpu_ctx.set_option("pa_uniform", 1)
     np.testing.assert_array_equal(again[0], out[1][0])
     for mx, (xg, ig) in out.items():
         assert ig["iterations"] == 40
