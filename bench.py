@@ -65,6 +65,8 @@ def parse():
                     help="rocprofv3 kernel-trace averages of the apply kernel (tools/rocprof_avg.py): "
                          "roofline.rocprof_avg_us and its source CSV")
     ap.add_argument("--no-profile-events", action="store_true")
+    ap.add_argument("--no-kron-form", action="store_true",
+                    help="skip the informational Kronecker-form leg (profiles: its k_brick_cg launches share the name)")
     ap.add_argument("--path", choices=["brick", "generic"], default=None,
                     help="brick: structured fast path (fused E->L, fused CG direction); generic: any mesh")
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c4s", "c4u", "c5", "c5w"], default="c2",
@@ -717,7 +719,7 @@ def main():
     # informational: the same steps with the Kronecker form of the per-element factors (pa_uniform 0,
     # the form any affine box takes), when the uniform element matrix ran above
     kron = None
-    if world == 1 and uniform:
+    if world == 1 and uniform and not args.no_kron_form:
         ctx.set_option("pa_uniform", 0)
         step()
         ctx.synchronize()

@@ -6,7 +6,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 OUT=$1; shift
 mkdir -p $OUT
-ARGS="--steps 1 --warmup 0 --cg-iters 20 --gmres-iters 0 --spd-steps 0 --per-point-steps 0 --no-profile-events --no-cpu-baseline $*"
+ARGS="--steps 1 --warmup 0 --cg-iters 20 --gmres-iters 0 --spd-steps 0 --per-point-steps 0 --no-profile-events --no-cpu-baseline --no-kron-form $*"
 timeout -k 10 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 i=0
 for G in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" \

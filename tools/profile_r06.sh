@@ -20,7 +20,7 @@ case $CFG in
 esac
 timeout -k 10 600 python -u bench.py --config $CFG --steps 5 --warmup 1 "$@" > $OUT/bench.json 2> $OUT/bench.err || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/stats -o run --output-format csv -- python3 bench.py \
-    --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-profile-events --spd-steps 0 --per-point-steps 0 \
+    --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-profile-events --no-kron-form --spd-steps 0 --per-point-steps 0 \
     --gmres-iters 0 "$@" > $OUT/stats.log 2>&1 || exit $?
 python3 tools/rocprof_avg.py --trace $OUT/stats --kernel $KERN --key $KEY --csv $OUT/${KERN}_launches.csv \
     --json $OUT/rocprof_kernels.json > $OUT/rocprof_avg.json || exit $?

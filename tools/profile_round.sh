@@ -20,9 +20,9 @@ case $CFG in
   c5) SHORT="--cg-iters 10 --gmres-iters 0 --spd-steps 0";;
 esac
 timeout -k 10 900 python bench.py --config $CFG --steps 5 --warmup 1 > $OUT/bench.json 2> $OUT/bench.err || exit $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/stats -o run --output-format csv -- python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-profile-events --spd-steps 0 --per-point-steps 0 --gmres-iters 0 > $OUT/stats.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/stats -o run --output-format csv -- python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-profile-events --no-kron-form --spd-steps 0 --per-point-steps 0 --gmres-iters 0 > $OUT/stats.log 2>&1 || exit $?
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace -T -d $OUT/pmc_$C -o run --output-format csv -- python3 bench.py --config $CFG --steps 1 --warmup 0 $SHORT --no-cpu-baseline --no-profile-events --per-point-steps 0 > $OUT/pmc_$C.log 2>&1 || exit $?
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace -T -d $OUT/pmc_$C -o run --output-format csv -- python3 bench.py --config $CFG --steps 1 --warmup 0 $SHORT --no-cpu-baseline --no-profile-events --no-kron-form --per-point-steps 0 > $OUT/pmc_$C.log 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace -T -d $OUT/calib_$C -o run --output-format csv -- python3 tools/calib.py > $OUT/calib_$C.log 2>&1 || exit $?
 done
 exit 0
