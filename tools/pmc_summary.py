@@ -86,7 +86,9 @@ def main():
         n = int(wl.split("x")[0])
         order = int(wl.split("p=")[1].split(",")[0])
         kinds = int(wl.split("kinds=")[1].split(")")[0])
-        key = f"n{n}_p{order}_k{kinds}" + ("_aff" if cfg.get("qdata", "").startswith("affine") else "")
+        # (bench.py's roofline key: "_aff" for the factor forms, the uniform element matrix included)
+        qd = cfg.get("qdata", "")
+        key = f"n{n}_p{order}_k{kinds}" + ("_aff" if qd.startswith("affine") or qd.startswith("uniform") else "")
     tj[key] = {"hbm_bytes_per_launch": apply["hbm_bytes_per_launch"], "round": tag,
                                      "kernel": kname, "source": f"profiles/{tag}_pmc.json"}
     json.dump(tj, open(p, "w"), indent=1)
