@@ -422,12 +422,15 @@ bool brick_fits(const cdfem_ctx *c)
 static BrickGeom geom_of(const cdfem_ctx *c)
 {
     if (c->p >= 3) return BrickGeom{c->hb_nbx, c->hb_nby, c->hb_nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1, c->d_bess};
-    // brick_stagger: -1 automatic (shift log2 CUs when the CU count is a power of two, n = 4), 0 off
+    // brick_stagger: -1 automatic (shift log2 CUs when the CU count is a power of two; n = 4 sleeps, 2 for
+    // the matrix-core apply of a uniform box, whose compute phase is shorter: profiles/r06/ab_c2_stagger_um/),
+    // 0 off
     int stag = c->brick_stagger;
     if (stag < 0) {
         int sh = 0;
         while ((1 << sh) < c->ncu) ++sh;
-        stag = (c->ncu > 0 && (1 << sh) == c->ncu) ? (sh | (4 << 4)) : 0;
+        const int n = (uniform_elem(c) && c->p == 2) ? 2 : 4;
+        stag = (c->ncu > 0 && (1 << sh) == c->ncu) ? (sh | (n << 4)) : 0;
     }
     return BrickGeom{c->nbx, c->nby, c->nbz, (int)c->Lx, (int)c->Ly, (int)c->Lz, c->brick_xcd, 0, 1, c->d_bess,
                      stag, 8 * c->ncu};
